@@ -1,0 +1,81 @@
+/*
+ * mt_types.h -- binary wire format shared by the C-ABI boundary (include/mt_replay.h),
+ * the HIP kernels and the CPU oracle.
+ *
+ * One sequenced merge-tree message (ISequencedDocumentMessage carrying an
+ * IMergeTreeInsert/Remove/Annotate op; PD/protocol.ts:132-172, MT/ops.ts:63-110) is encoded
+ * as one 32-byte mt_op_rec.  A GROUP op (MT/ops.ts:104-107) becomes one record per member
+ * with MT_F_GROUP_MORE set on all but the last (members share seq/refSeq/client and the
+ * seq/msn update happens once, after the last member: MT/client.ts:768-819).  A non-"op"
+ * message only advances seq/msn (MT/client.ts:805,818) and is encoded as MT_OP_NOOP.
+ *
+ * Text payloads are UTF-16 code units (JS string semantics, MT/textSegment.ts:45,105) in a
+ * separate arena.  Property sets are interned to 32-bit key/value ids by the host; values
+ * carry MT_VAL_FALSY_BIT when the JS value is falsy (needed by the `rewrite` rule
+ * `!newProps[key]`, MT/segmentPropertiesManager.ts:72).
+ */
+#ifndef MT_TYPES_H
+#define MT_TYPES_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mt_op_kind {
+    MT_OP_INSERT = 0,     /* MergeTreeDeltaType.INSERT   MT/ops.ts:30 */
+    MT_OP_REMOVE = 1,     /* MergeTreeDeltaType.REMOVE   MT/ops.ts:31 */
+    MT_OP_ANNOTATE = 2,   /* MergeTreeDeltaType.ANNOTATE MT/ops.ts:32 */
+    MT_OP_NOOP = 3        /* non-"op" message: seq/msn update only */
+};
+
+enum mt_op_flags {
+    MT_F_GROUP_MORE = 1,  /* another member of the same GROUP message follows */
+    MT_F_MARKER = 2       /* insert of a Marker (length 1); payload = refType */
+};
+
+#define MT_NO_PROPS 0xFFFFFFFFu      /* props field: no property set */
+#define MT_VAL_NULL 0xFFFFFFFFu      /* value id of JSON null (delete) */
+#define MT_VAL_FALSY_BIT 0x80000000u /* value id flag: JS value is falsy */
+#define MT_COMBINE_NONE 0u
+#define MT_COMBINE_REWRITE 1u        /* ICombiningOp { name: "rewrite" } */
+#define MT_COMBINE_OTHER 2u          /* any other combining op: rejected */
+
+typedef struct mt_op_rec {
+    int32_t seq;        /* sequenceNumber */
+    int32_t ref_seq;    /* referenceSequenceNumber */
+    int32_t min_seq;    /* minimumSequenceNumber */
+    int32_t pos1;       /* op.pos1 */
+    int32_t pos2;       /* remove/annotate: op.pos2; insert: payload length (UTF-16 units) */
+    uint32_t payload;   /* insert: offset into the text arena (UTF-16 units);
+                           marker insert: refType */
+    uint32_t props;     /* offset (u32 words) of a props-op record in the props arena, or
+                           MT_NO_PROPS.  record = [count | combine<<16, (key, value) x count] */
+    uint16_t client;    /* short client id of the writer (first-seen order, observer = 0) */
+    uint8_t kind;       /* enum mt_op_kind */
+    uint8_t flags;      /* enum mt_op_flags */
+} mt_op_rec;
+
+/* Per-document verification checksum: all-gathered across ranks. */
+typedef struct mt_checksum {
+    uint32_t length;     /* observer length, MergeTree.length MT/mergeTree.ts:1617 */
+    uint32_t n_segments; /* live leaf segments (diagnostic, tree-shape dependent) */
+    uint64_t text_hash;  /* FNV-1a 64 over the UTF-16LE text (getText, MT/textSegment.ts:154) */
+    uint64_t props_hash; /* FNV-1a 64 over the observer-visible property runs */
+    uint64_t delta_hash; /* FNV-1a 64 over every mergeTreeDeltaCallback record */
+} mt_checksum;
+
+/* Per-document status codes (mt_doc_status). */
+enum mt_doc_status {
+    MT_DOC_OK = 0,
+    MT_DOC_INSERT_FAILED = 1,   /* "MergeTree insert failed" MT/mergeTree.ts:2243-2249 */
+    MT_DOC_SEQ_ORDER = 2,       /* assert currentSeq < seq     MT/client.ts:462-463 */
+    MT_DOC_MINSEQ_ORDER = 3,    /* assert minSeq <= msn        MT/client.ts:464-465 */
+    MT_DOC_CAPACITY = 4,        /* a per-document capacity was exceeded */
+    MT_DOC_UNSUPPORTED = 5      /* combining op other than rewrite */
+};
+
+#ifdef __cplusplus
+}
+#endif
+#endif

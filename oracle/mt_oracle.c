@@ -1,0 +1,1155 @@
+/*
+ * TEST INFRASTRUCTURE ONLY -- CPU restatement of the reference merge-tree observer replay.
+ *
+ * This is the checker for the HIP path, not part of the product: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.  It deliberately keeps
+ * the reference's *pointer B-tree* structure (blocks of <= MaxNodesInBlock-1 children,
+ * recursive walks, binary-heap zamboni) so that it is an independent restatement of the
+ * algorithm the GPU path re-derives as flat scans.  Every function cites the reference
+ * (paths relative to /root/reference/packages/dds/merge-tree/src/, "MT/").
+ *
+ * Parity pin: oracle/ref_harness.mjs runs the reference itself (transpiled by
+ * oracle/build_ref.py) and tests/golden/ holds its outputs; tests/test_oracle.py checks
+ * this file against them.
+ *
+ * Scope: the observer replica of SURVEY.md Appendix A -- every message is remote, no local
+ * ops, all branch ids 0, no local references, no tracking groups.
+ */
+#include "mt_oracle.h"
+
+#include <limits.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MAXN 8                 /* MaxNodesInBlock               MT/mergeTree.ts:333 */
+#define TEXT_GRANULARITY 256   /* MergeTree.TextSegmentGranularity MT/mergeTree.ts:1093 */
+#define ZAMBONI_MAX 2          /* MergeTree.zamboniSegmentsMaxCount MT/mergeTree.ts:1095 */
+#define RSEQ_NONE INT32_MIN    /* removedSeq === undefined */
+#define OBSERVER 0             /* collabWindow.clientId of the observer */
+#define UNASSIGNED (-1)        /* UnassignedSequenceNumber       MT/constants.ts:12 */
+#define SCOUR_UNDEF (-1)       /* needsScour === undefined */
+
+typedef struct Props {
+    int n, cap;
+    uint32_t *key, *val;
+} Props;
+
+struct Block;
+typedef struct Node {
+    int leaf;
+    struct Block *parent;
+    int index;
+} Node;
+
+typedef struct Seg {
+    Node n;
+    int32_t len, seq, client, rseq, rclient;
+    int novl, ovlcap;
+    int32_t *ovl;          /* removedClientOverlap, push order */
+    int32_t marker;        /* -1: TextSegment, else Marker refType */
+    uint16_t *text;
+    int tcap;
+    Props *props;          /* NULL == properties undefined */
+} Seg;
+
+typedef struct Block {
+    Node n;
+    int count;
+    Node *ch[MAXN + 1];
+    int needs_scour;       /* -1 undefined, 0 false, 1 true */
+} Block;
+
+typedef struct HeapEnt {
+    int32_t max_seq;
+    Seg *seg;
+} HeapEnt;
+
+typedef struct Vec {
+    void **p;
+    int n, cap;
+} Vec;
+
+typedef struct IVec {
+    int32_t *p;
+    int64_t n, cap;
+} IVec;
+
+struct orc_doc {
+    Block *root;
+    int32_t min_seq, current_seq;
+    int32_t status;
+    HeapEnt *heap;         /* 1-based like Collections.Heap MT/collections.ts:212-265 */
+    int heap_n, heap_cap;
+    Vec allocs;
+    int record;
+    IVec dlog;             /* optional flattened delta records */
+    uint64_t delta_hash;
+};
+
+/* ------------------------------------------------------------------ utilities */
+static void vec_push(Vec *v, void *x) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 64;
+        v->p = (void **)realloc(v->p, sizeof(void *) * v->cap);
+    }
+    v->p[v->n++] = x;
+}
+static void ivec_push(IVec *v, int32_t x) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 256;
+        v->p = (int32_t *)realloc(v->p, sizeof(int32_t) * v->cap);
+    }
+    v->p[v->n++] = x;
+}
+static void *dalloc(orc_doc *d, size_t sz) {
+    void *p = calloc(1, sz);
+    vec_push(&d->allocs, p);
+    return p;
+}
+
+#define FNV_OFF 1469598103934665603ULL
+#define FNV_PRIME 1099511628211ULL
+static inline uint64_t fnv_u32(uint64_t h, uint32_t x) {
+    for (int i = 0; i < 4; i++) {
+        h ^= (x >> (8 * i)) & 0xFF;
+        h *= FNV_PRIME;
+    }
+    return h;
+}
+
+/* ------------------------------------------------------------------ properties */
+static Props *props_new(orc_doc *d) {
+    Props *p = (Props *)dalloc(d, sizeof(Props));
+    return p;
+}
+static int props_find(const Props *p, uint32_t key) {
+    for (int i = 0; i < p->n; i++)
+        if (p->key[i] == key) return i;
+    return -1;
+}
+static void props_set(orc_doc *d, Props *p, uint32_t key, uint32_t val) {
+    int i = props_find(p, key);
+    if (i >= 0) {
+        p->val[i] = val;
+        return;
+    }
+    if (p->n == p->cap) {
+        int nc = p->cap ? p->cap * 2 : 4;
+        uint32_t *k = (uint32_t *)dalloc(d, sizeof(uint32_t) * nc);
+        uint32_t *v = (uint32_t *)dalloc(d, sizeof(uint32_t) * nc);
+        if (p->n) {
+            memcpy(k, p->key, sizeof(uint32_t) * p->n);
+            memcpy(v, p->val, sizeof(uint32_t) * p->n);
+        }
+        p->key = k;
+        p->val = v;
+        p->cap = nc;
+    }
+    p->key[p->n] = key;
+    p->val[p->n] = val;
+    p->n++;
+}
+static void props_del(Props *p, uint32_t key) {  /* `delete obj[key]` keeps order of rest */
+    int i = props_find(p, key);
+    if (i < 0) return;
+    for (int j = i + 1; j < p->n; j++) {
+        p->key[j - 1] = p->key[j];
+        p->val[j - 1] = p->val[j];
+    }
+    p->n--;
+}
+static Props *props_clone(orc_doc *d, const Props *src) {
+    if (!src) return NULL;
+    Props *p = props_new(d);
+    for (int i = 0; i < src->n; i++) props_set(d, p, src->key[i], src->val[i]);
+    return p;
+}
+/* Properties.matchProperties MT/properties.ts:61-92 (value ids are canonical, so deep
+   equality of values == id equality). */
+static int match_props(const Props *a, const Props *b) {
+    if (a) {
+        if (!b) return 0;
+        for (int i = 0; i < a->n; i++) {
+            int j = props_find(b, a->key[i]);
+            if (j < 0 || b->val[j] != a->val[i]) return 0;
+        }
+        for (int j = 0; j < b->n; j++)
+            if (props_find(a, b->key[j]) < 0) return 0;
+        return 1;
+    }
+    return b ? 0 : 1;
+}
+
+/* ------------------------------------------------------------------ tree nodes */
+static Block *make_block(orc_doc *d, int count) {   /* MergeTree.makeBlock :1148-1157 */
+    Block *b = (Block *)dalloc(d, sizeof(Block));
+    b->n.leaf = 0;
+    b->count = count;
+    b->needs_scour = SCOUR_UNDEF;
+    return b;
+}
+static Seg *make_text_seg(orc_doc *d, const uint16_t *text, int32_t len) {
+    Seg *s = (Seg *)dalloc(d, sizeof(Seg));
+    s->n.leaf = 1;
+    s->len = len;
+    s->seq = 0;               /* UniversalSequenceNumber  MT/mergeTree.ts:433 */
+    s->client = -1;           /* LocalClientId            MT/mergeTree.ts:432 */
+    s->rseq = RSEQ_NONE;
+    s->marker = -1;
+    s->tcap = len > 0 ? len : 1;
+    s->text = (uint16_t *)malloc(sizeof(uint16_t) * s->tcap);
+    vec_push(&d->allocs, s->text);
+    if (len) memcpy(s->text, text, sizeof(uint16_t) * len);
+    return s;
+}
+static void assign_child(Block *b, Node *child, int index) {  /* assignChild :374-381 */
+    child->parent = b;
+    child->index = index;
+    b->ch[index] = child;
+}
+static int ovl_has(const Seg *s, int32_t c) {
+    for (int i = 0; i < s->novl; i++)
+        if (s->ovl[i] == c) return 1;
+    return 0;
+}
+static void ovl_push(orc_doc *d, Seg *s, int32_t c) {   /* addOverlappingClient :2577-2585 */
+    if (s->novl == s->ovlcap) {
+        int nc = s->ovlcap ? s->ovlcap * 2 : 4;
+        int32_t *p = (int32_t *)dalloc(d, sizeof(int32_t) * nc);
+        if (s->novl) memcpy(p, s->ovl, sizeof(int32_t) * s->novl);
+        s->ovl = p;
+        s->ovlcap = nc;
+    }
+    s->ovl[s->novl++] = c;
+}
+
+/* localNetLength :1195-1206 */
+static inline int32_t local_net_length(const Seg *s) {
+    return s->rseq != RSEQ_NONE ? 0 : s->len;
+}
+
+/* nodeLength :1692-1732.  Interior nodes: the reference reads PartialSequenceLengths
+   (MT/partialLengths.ts:432-486) whose contract is the sum of the leaves' lengths. */
+static int32_t node_len(const Node *n, int32_t ref_seq, int32_t client) {
+    if (!n->leaf) {
+        const Block *b = (const Block *)n;
+        int32_t sum = 0;
+        for (int i = 0; i < b->count; i++) sum += node_len(b->ch[i], ref_seq, client);
+        return sum;
+    }
+    const Seg *s = (const Seg *)n;
+    if (client == OBSERVER) return local_net_length(s);
+    if (s->client == client || (s->seq != UNASSIGNED && s->seq <= ref_seq)) {
+        if (s->rseq != RSEQ_NONE) {
+            if (s->rclient == client || ovl_has(s, client) ||
+                (s->rseq != UNASSIGNED && s->rseq <= ref_seq))
+                return 0;
+            return s->len;
+        }
+        return s->len;
+    }
+    return 0;
+}
+
+/* getPosition :1619-1636 (always in the observer's view here) */
+static int32_t get_position(const Node *node) {
+    int32_t total = 0;
+    const Block *parent = node->parent;
+    const Node *prev = node;
+    while (parent) {
+        for (int i = 0; i < parent->count; i++) {
+            const Node *c = parent->ch[i];
+            if (c == prev) break;
+            total += node_len(c, 0, OBSERVER);
+        }
+        prev = &parent->n;
+        parent = parent->n.parent;
+    }
+    return total;
+}
+
+/* ------------------------------------------------------------------ zamboni heap */
+static void heap_swap(HeapEnt *a, HeapEnt *b) {
+    HeapEnt t = *a;
+    *a = *b;
+    *b = t;
+}
+static void heap_add(orc_doc *d, Seg *s, int32_t max_seq) {   /* Heap.add/fixup */
+    if (d->heap_n + 2 > d->heap_cap) {
+        d->heap_cap = d->heap_cap ? d->heap_cap * 2 : 64;
+        d->heap = (HeapEnt *)realloc(d->heap, sizeof(HeapEnt) * d->heap_cap);
+    }
+    int k = ++d->heap_n;
+    d->heap[k].max_seq = max_seq;
+    d->heap[k].seg = s;
+    while (k > 1 && d->heap[k >> 1].max_seq - d->heap[k].max_seq > 0) {
+        heap_swap(&d->heap[k >> 1], &d->heap[k]);
+        k >>= 1;
+    }
+}
+static HeapEnt heap_get(orc_doc *d) {   /* Heap.get/fixdown MT/collections.ts:227-262 */
+    HeapEnt x = d->heap[1];
+    d->heap[1] = d->heap[d->heap_n];
+    d->heap_n--;
+    int k = 1;
+    while ((k << 1) <= d->heap_n) {
+        int j = k << 1;
+        if (j < d->heap_n && d->heap[j].max_seq - d->heap[j + 1].max_seq > 0) j++;
+        if (d->heap[k].max_seq - d->heap[j].max_seq <= 0) break;
+        heap_swap(&d->heap[k], &d->heap[j]);
+        k = j;
+    }
+    return x;
+}
+
+/* addToLRUSet :1306-1316 */
+static void add_to_lru(orc_doc *d, Seg *s, int32_t seq) {
+    if (s->n.parent->needs_scour != 1 && seq > d->current_seq) {
+        s->n.parent->needs_scour = 1;
+        heap_add(d, s, seq);
+    }
+}
+
+/* TextSegment.canAppend MT/textSegment.ts:63-68 (Marker.canAppend is false :827-829) */
+static int can_append(const Seg *prev, const Seg *s) {
+    if (prev->marker >= 0) return 0;
+    if (prev->len > 0 && prev->text[prev->len - 1] == '\n') return 0;
+    if (s->marker >= 0) return 0;
+    return prev->len <= TEXT_GRANULARITY || s->len <= TEXT_GRANULARITY;
+}
+/* TextSegment.append :74-85 */
+static void seg_append(orc_doc *d, Seg *prev, const Seg *s) {
+    if (prev->len + s->len > prev->tcap) {
+        int nc = (prev->len + s->len) * 2;
+        uint16_t *t = (uint16_t *)dalloc(d, sizeof(uint16_t) * nc);
+        memcpy(t, prev->text, sizeof(uint16_t) * prev->len);
+        prev->text = t;
+        prev->tcap = nc;
+    }
+    memcpy(prev->text + prev->len, s->text, sizeof(uint16_t) * s->len);
+    prev->len += s->len;
+}
+
+/* scourNode :1322-1398 */
+static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
+    Seg *prev = NULL;
+    for (int k = 0; k < node->count; k++) {
+        Node *child = node->ch[k];
+        if (child->leaf) {
+            Seg *s = (Seg *)child;
+            if (s->rseq != RSEQ_NONE) {
+                if (s->rseq > d->min_seq) {
+                    hold[(*nhold)++] = child;
+                } else {
+                    s->n.parent = NULL;            /* unlink */
+                }
+                prev = NULL;
+            } else if (s->seq <= d->min_seq) {
+                int ok = prev && can_append(prev, s) && match_props(prev->props, s->props) &&
+                         local_net_length(s) > 0;
+                if (ok) {
+                    seg_append(d, prev, s);
+                    s->n.parent = NULL;
+                } else {
+                    hold[(*nhold)++] = child;
+                    prev = local_net_length(s) > 0 ? s : NULL;
+                }
+            } else {
+                hold[(*nhold)++] = child;
+                prev = NULL;
+            }
+        } else {
+            hold[(*nhold)++] = child;
+            prev = NULL;
+        }
+    }
+}
+
+/* pack :1401-1453 */
+static void pack(orc_doc *d, Block *block) {
+    Block *parent = block->n.parent;
+    Node *hold[MAXN * MAXN + 8];
+    int nhold = 0;
+    for (int ci = 0; ci < parent->count; ci++) {
+        Block *cb = (Block *)parent->ch[ci];
+        scour_node(d, cb, hold, &nhold);
+        cb->n.parent = NULL;
+    }
+    int total = nhold;
+    int half = MAXN / 2;
+    int child_count = total / half;
+    if (child_count > MAXN - 1) child_count = MAXN - 1;
+    if (child_count < 1) child_count = 1;
+    int base = total / child_count;
+    int extra = total % child_count;
+    int read = 0;
+    for (int ni = 0; ni < child_count; ni++) {
+        int cnt = base;
+        if (extra > 0) {
+            cnt++;
+            extra--;
+        }
+        Block *pb = make_block(d, cnt);
+        for (int j = 0; j < cnt; j++) assign_child(pb, hold[read++], j);
+        pb->n.parent = parent;
+        assign_child(parent, &pb->n, ni);
+    }
+    parent->count = child_count;
+    if (parent->count < MAXN / 2 && parent->n.parent) pack(d, parent);
+}
+
+/* zamboniSegments :1455-1511 */
+static void zamboni(orc_doc *d) {
+    for (int i = 0; i < ZAMBONI_MAX; i++) {
+        if (d->heap_n == 0 || d->heap[1].max_seq > d->min_seq) break;
+        HeapEnt e = heap_get(d);
+        Block *block = e.seg->n.parent;
+        if (block && block->needs_scour != 0) {
+            Node *hold[MAXN + 1];
+            int nhold = 0;
+            scour_node(d, block, hold, &nhold);
+            block->needs_scour = 0;
+            if (nhold < block->count) {
+                block->count = nhold;
+                for (int j = 0; j < nhold; j++) assign_child(block, hold[j], j);
+                if (block->count < MAXN / 2 && block->n.parent) pack(d, block);
+            }
+        }
+    }
+}
+
+/* split :2509-2522 */
+static Block *split_block(orc_doc *d, Block *node) {
+    int half = MAXN / 2;
+    Block *nb = make_block(d, half);
+    node->count = half;
+    for (int i = 0; i < half; i++) {
+        assign_child(nb, node->ch[half + i], i);
+        node->ch[half + i] = NULL;
+    }
+    return nb;
+}
+/* updateRoot :1909-1920 */
+static void update_root(orc_doc *d, Block *split_node) {
+    if (split_node) {
+        Block *nr = make_block(d, 2);
+        assign_child(nr, &d->root->n, 0);
+        assign_child(nr, &split_node->n, 1);
+        nr->n.parent = NULL;
+        d->root = nr;
+    }
+}
+
+/* BaseSegment.splitAt :523-567 + TextSegment.createSplitSegmentAt MT/textSegment.ts:103-111
+   + SegmentPropertiesManager.copyTo MT/segmentPropertiesManager.ts:113-128 */
+static Seg *split_at(orc_doc *d, Seg *s, int32_t pos) {
+    if (!(pos > 0) || s->marker >= 0) return NULL;
+    Seg *r = make_text_seg(d, s->text + pos, s->len - pos);
+    s->len = pos;
+    r->props = props_clone(d, s->props);
+    r->n.parent = s->n.parent;
+    r->rclient = s->rclient;
+    r->rseq = s->rseq;
+    r->seq = s->seq;
+    r->client = s->client;
+    for (int i = 0; i < s->novl; i++) ovl_push(d, r, s->ovl[i]);
+    return r;
+}
+
+/* breakTie :2281-2310 (remote client: never the collab window's own client) */
+static int break_tie(int32_t pos, const Node *node, int32_t ref_seq, int32_t client) {
+    if (node->leaf) {
+        if (pos == 0) {
+            const Seg *s = (const Seg *)node;
+            if (s->rseq != RSEQ_NONE && s->rseq != 0 && s->rseq <= ref_seq && s->rseq != UNASSIGNED)
+                return 0;
+            if (client == OBSERVER) return 1;
+            if (s->seq != UNASSIGNED) return 1;
+        }
+        return 0;
+    }
+    return 1;
+}
+
+enum { WALK_SPLIT = 0, WALK_INSERT = 1 };
+
+/* insertingWalk :2378-2507 with leaf = splitLeafSegment (:2258-2272) or onLeaf
+   (:2213-2223).  continuePredicate never fires for remote-only replay (no unacked local
+   segments, :2176-2194). */
+static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_seq,
+                             int32_t client, int mode, Seg *cand) {
+    int ci;
+    Node *new_node = NULL;
+    for (ci = 0; ci < block->count; ci++) {
+        Node *child = block->ch[ci];
+        int32_t len = node_len(child, ref_seq, client);
+        if (pos < len || (pos == len && break_tie(pos, child, ref_seq, client))) {
+            if (!child->leaf) {
+                Block *sn = inserting_walk(d, (Block *)child, pos, ref_seq, client, mode, cand);
+                if (!sn) return NULL;
+                new_node = &sn->n;
+                ci++;
+            } else {
+                Seg *s = (Seg *)child;
+                if (mode == WALK_INSERT) {
+                    assign_child(block, &cand->n, ci);
+                    new_node = &s->n;
+                    ci++;
+                } else {
+                    Seg *next = split_at(d, s, pos);
+                    if (!next) return NULL;
+                    new_node = &next->n;
+                    ci++;
+                }
+            }
+            break;
+        } else {
+            pos -= len;
+        }
+    }
+    if (!new_node && pos == 0 && mode == WALK_INSERT) new_node = &cand->n;
+    if (new_node) {
+        for (int i = block->count; i > ci; i--) {
+            block->ch[i] = block->ch[i - 1];
+            block->ch[i]->index = i;
+        }
+        assign_child(block, new_node, ci);
+        block->count++;
+        if (block->count < MAXN) return NULL;
+        return split_block(d, block);
+    }
+    return NULL;
+}
+
+/* ensureIntervalBoundary :2274-2278 */
+static void ensure_boundary(orc_doc *d, int32_t pos, int32_t ref_seq, int32_t client) {
+    Block *sn = inserting_walk(d, d->root, pos, ref_seq, client, WALK_SPLIT, NULL);
+    update_root(d, sn);
+}
+
+/* ------------------------------------------------------------------ delta callbacks */
+typedef struct DeltaSeg {
+    Seg *seg;
+    int npd;
+    uint32_t *pd;   /* (key, old) pairs */
+} DeltaSeg;
+
+static void emit_deltas(orc_doc *d, int32_t seq, int kind, DeltaSeg *ds, int n) {
+    uint64_t h = d->delta_hash;
+    h = fnv_u32(h, (uint32_t)seq);
+    h = fnv_u32(h, (uint32_t)kind);
+    h = fnv_u32(h, (uint32_t)n);
+    if (d->record) {
+        ivec_push(&d->dlog, seq);
+        ivec_push(&d->dlog, kind);
+        ivec_push(&d->dlog, n);
+    }
+    for (int i = 0; i < n; i++) {
+        Seg *s = ds[i].seg;
+        int32_t pos = s->n.parent ? get_position(&s->n) : -1;
+        h = fnv_u32(h, (uint32_t)pos);
+        h = fnv_u32(h, (uint32_t)s->len);
+        if (d->record) {
+            ivec_push(&d->dlog, pos);
+            ivec_push(&d->dlog, s->len);
+        }
+        if (kind == MT_OP_ANNOTATE) {
+            h = fnv_u32(h, (uint32_t)ds[i].npd);
+            if (d->record) ivec_push(&d->dlog, ds[i].npd);
+            for (int j = 0; j < ds[i].npd; j++) {
+                h = fnv_u32(h, ds[i].pd[2 * j]);
+                h = fnv_u32(h, ds[i].pd[2 * j + 1]);
+                if (d->record) {
+                    ivec_push(&d->dlog, (int32_t)ds[i].pd[2 * j]);
+                    ivec_push(&d->dlog, (int32_t)ds[i].pd[2 * j + 1]);
+                }
+            }
+        }
+    }
+    d->delta_hash = h;
+}
+
+/* ------------------------------------------------------------------ nodeMap */
+typedef struct MapCtx {
+    int kind;
+    int32_t seq, client;
+    const uint32_t *props_rec;
+    DeltaSeg *ds;
+    int nds, cap;
+    orc_doc *d;
+} MapCtx;
+
+static void ds_push(MapCtx *m, Seg *s, int npd, uint32_t *pd) {
+    if (m->nds == m->cap) {
+        m->cap = m->cap ? m->cap * 2 : 16;
+        m->ds = (DeltaSeg *)realloc(m->ds, sizeof(DeltaSeg) * m->cap);
+    }
+    m->ds[m->nds].seg = s;
+    m->ds[m->nds].npd = npd;
+    m->ds[m->nds].pd = pd;
+    m->nds++;
+}
+
+/* SegmentPropertiesManager.addProperties MT/segmentPropertiesManager.ts:35-111 for a
+   sequenced remote op (seq != Unassigned, collaborating, no pending local keys). */
+static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, uint32_t **pd_out) {
+    uint32_t count = rec[0] & 0xFFFF, combine = rec[0] >> 16;
+    if (!s->props) s->props = props_new(d);
+    Props *p = s->props;
+    /* deltas: ordered map key -> previous value (insertion order, overwrite in place) */
+    uint32_t *pd = (uint32_t *)dalloc(d, sizeof(uint32_t) * 2 * (p->n + count + 1));
+    int npd = 0;
+#define PD_SET(k, v)                                   \
+    do {                                               \
+        int f_ = -1;                                   \
+        for (int q_ = 0; q_ < npd; q_++)               \
+            if (pd[2 * q_] == (k)) f_ = q_;            \
+        if (f_ < 0) {                                  \
+            pd[2 * npd] = (k);                         \
+            pd[2 * npd + 1] = (v);                     \
+            npd++;                                     \
+        } else                                         \
+            pd[2 * f_ + 1] = (v);                      \
+    } while (0)
+    if (combine == MT_COMBINE_REWRITE) {
+        /* delete all keys not (truthily) present in newProps  :66-79 */
+        for (int i = 0; i < p->n;) {
+            uint32_t key = p->key[i];
+            int truthy = 0;
+            for (uint32_t j = 0; j < count; j++) {
+                if (rec[1 + 2 * j] == key) {
+                    uint32_t v = rec[2 + 2 * j];
+                    truthy = (v != MT_VAL_NULL) && !(v & MT_VAL_FALSY_BIT);
+                }
+            }
+            if (!truthy) {
+                PD_SET(key, p->val[i]);
+                props_del(p, key);
+            } else {
+                i++;
+            }
+        }
+    }
+    for (uint32_t j = 0; j < count; j++) {
+        uint32_t key = rec[1 + 2 * j], val = rec[2 + 2 * j];
+        int i = props_find(p, key);
+        PD_SET(key, i >= 0 ? p->val[i] : MT_VAL_NULL);
+        if (val == MT_VAL_NULL)
+            props_del(p, key);
+        else
+            props_set(d, p, key, val);
+    }
+#undef PD_SET
+    *pd_out = pd;
+    return npd;
+}
+
+/* markRemoved / annotateSegment leaf actions :2647-2693, :2607-2620 */
+static void map_leaf(MapCtx *m, Seg *s) {
+    orc_doc *d = m->d;
+    if (m->kind == MT_OP_REMOVE) {
+        if (s->rseq != RSEQ_NONE) {
+            ovl_push(d, s, m->client);
+        } else {
+            s->rclient = m->client;
+            s->rseq = m->seq;
+            ds_push(m, s, 0, NULL);
+        }
+        add_to_lru(d, s, m->seq);
+    } else {
+        uint32_t *pd;
+        int npd = add_properties(d, s, m->props_rec, &pd);
+        ds_push(m, s, npd, pd);
+        add_to_lru(d, s, m->seq);
+    }
+}
+
+/* nodeMap :2936-2998 */
+static void node_map(MapCtx *m, Block *node, int32_t ref_seq, int32_t client, int32_t start,
+                     int32_t end) {
+    for (int ci = 0; ci < node->count; ci++) {
+        Node *child = node->ch[ci];
+        int32_t len = node_len(child, ref_seq, client);
+        if (end > 0 && len > 0 && start < len) {
+            if (!child->leaf)
+                node_map(m, (Block *)child, ref_seq, client, start, end);
+            else
+                map_leaf(m, (Seg *)child);
+        }
+        start -= len;
+        end -= len;
+    }
+}
+
+/* ------------------------------------------------------------------ op application */
+static Seg *segment_from_op(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
+                            const uint32_t *props_arena) {
+    Seg *s;
+    if (op->flags & MT_F_MARKER) {           /* Marker.make  MT/mergeTree.ts:676-688 */
+        s = make_text_seg(d, NULL, 0);
+        s->marker = (int32_t)op->payload;
+        s->len = 1;
+    } else {                                 /* TextSegment.make MT/textSegment.ts:23-29 */
+        s = make_text_seg(d, text_arena + op->payload, op->pos2);
+    }
+    if (op->props != MT_NO_PROPS) {
+        /* addProperties(props) without op/seq: keys with null dropped, {} kept (Q5) */
+        const uint32_t *rec = props_arena + op->props;
+        uint32_t count = rec[0] & 0xFFFF;
+        s->props = props_new(d);
+        for (uint32_t j = 0; j < count; j++)
+            if (rec[2 + 2 * j] != MT_VAL_NULL) props_set(d, s->props, rec[1 + 2 * j], rec[2 + 2 * j]);
+    }
+    return s;
+}
+
+/* updateSeqNumbers / updateMinSeq / setMinSeq  MT/client.ts:821-828, 991-1004;
+   MT/mergeTree.ts:1751-1769 */
+static int update_seq_numbers(orc_doc *d, int32_t msn, int32_t seq) {
+    if (!(d->current_seq <= seq)) return MT_DOC_SEQ_ORDER;
+    d->current_seq = seq;
+    if (!(msn <= seq)) return MT_DOC_MINSEQ_ORDER;
+    if (!(d->min_seq <= msn)) return MT_DOC_MINSEQ_ORDER;
+    if (msn > d->min_seq) {
+        d->min_seq = msn;
+        zamboni(d);
+    }
+    return MT_DOC_OK;
+}
+
+int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
+                  const uint32_t *props_arena) {
+    if (d->status) return d->status;
+    int32_t r = op->ref_seq, c = op->client, seq = op->seq;
+    if (op->kind == MT_OP_INSERT) {
+        /* Client.applyInsertOp MT/client.ts:394-442 -> MergeTree.insertSegments :2001-2031 */
+        Seg *s = segment_from_op(d, op, text_arena, props_arena);
+        ensure_boundary(d, op->pos1, r, c);
+        if (s->len > 0) {                   /* blockInsert :2227-2256 */
+            s->seq = seq;
+            s->client = c;
+            Block *sn = inserting_walk(d, d->root, op->pos1, r, c, WALK_INSERT, s);
+            if (s->n.parent == NULL) {
+                d->status = MT_DOC_INSERT_FAILED;
+                return d->status;
+            }
+            update_root(d, sn);
+            if (seq > d->min_seq) add_to_lru(d, s, seq);   /* saveIfLocal :2197-2212 */
+        }
+        DeltaSeg ds = {s, 0, NULL};
+        emit_deltas(d, seq, MT_OP_INSERT, &ds, 1);
+        zamboni(d);
+    } else if (op->kind == MT_OP_REMOVE || op->kind == MT_OP_ANNOTATE) {
+        /* markRangeRemoved :2640-2752 / annotateRange :2598-2638 */
+        if (op->kind == MT_OP_ANNOTATE && op->props != MT_NO_PROPS &&
+            (props_arena[op->props] >> 16) == MT_COMBINE_OTHER) {
+            d->status = MT_DOC_UNSUPPORTED;
+            return d->status;
+        }
+        ensure_boundary(d, op->pos1, r, c);
+        ensure_boundary(d, op->pos2, r, c);
+        MapCtx m;
+        memset(&m, 0, sizeof(m));
+        m.kind = op->kind;
+        m.seq = seq;
+        m.client = c;
+        m.d = d;
+        m.props_rec = op->props != MT_NO_PROPS ? props_arena + op->props : NULL;
+        static const uint32_t empty_rec[1] = {0};
+        if (!m.props_rec) m.props_rec = empty_rec;
+        node_map(&m, d->root, r, c, op->pos1, op->pos2);
+        emit_deltas(d, seq, op->kind, m.ds, m.nds);
+        free(m.ds);
+        zamboni(d);
+    }
+    if (op->kind != MT_OP_NOOP) {
+        /* completeAndLogOp asserts MT/client.ts:451-479 */
+        if (!(d->current_seq < seq)) return d->status = MT_DOC_SEQ_ORDER;
+        if (!(d->min_seq <= op->min_seq)) return d->status = MT_DOC_MINSEQ_ORDER;
+    }
+    if (!(op->flags & MT_F_GROUP_MORE)) {
+        int st = update_seq_numbers(d, op->min_seq, seq);
+        if (st) d->status = st;
+    }
+    return d->status;
+}
+
+/* ------------------------------------------------------------------ lifecycle / output */
+orc_doc *orc_new(const uint16_t *seed_text, int32_t seed_len) {
+    orc_doc *d = (orc_doc *)calloc(1, sizeof(orc_doc));
+    d->root = make_block(d, 0);             /* initialNode :1159-1163 */
+    d->delta_hash = FNV_OFF;
+    if (seed_len > 0) {
+        /* insertSegmentLocal before collaboration: seq 0, client LocalClientId (-1) */
+        Seg *s = make_text_seg(d, seed_text, seed_len);
+        assign_child(d->root, &s->n, 0);
+        d->root->count = 1;
+    }
+    return d;
+}
+void orc_free(orc_doc *d) {
+    if (!d) return;
+    for (int i = 0; i < d->allocs.n; i++) free(d->allocs.p[i]);
+    free(d->allocs.p);
+    free(d->heap);
+    free(d->dlog.p);
+    free(d);
+}
+int32_t orc_status(const orc_doc *d) { return d->status; }
+void orc_set_record_deltas(orc_doc *d, int32_t on) { d->record = on; }
+int32_t orc_view_length(orc_doc *d, int32_t ref_seq, int32_t client) {
+    return node_len(&d->root->n, ref_seq, client);
+}
+int32_t orc_length(orc_doc *d) { return node_len(&d->root->n, 0, OBSERVER); }
+
+typedef void (*seg_fn)(Seg *, void *);
+static void walk_segs(Node *n, seg_fn fn, void *arg) {   /* walkAllSegments :3002-3016 */
+    if (n->leaf) {
+        fn((Seg *)n, arg);
+        return;
+    }
+    Block *b = (Block *)n;
+    for (int i = 0; i < b->count; i++) walk_segs(b->ch[i], fn, arg);
+}
+
+typedef struct TextAcc {
+    uint16_t *out;
+    int32_t cap, n;
+} TextAcc;
+static void text_fn(Seg *s, void *arg) {   /* gatherText MT/textSegment.ts:188-275 */
+    TextAcc *a = (TextAcc *)arg;
+    if (s->rseq != RSEQ_NONE || s->marker >= 0) return;
+    for (int i = 0; i < s->len; i++) {
+        if (a->n < a->cap) a->out[a->n] = s->text[i];
+        a->n++;
+    }
+}
+int32_t orc_text(orc_doc *d, uint16_t *out, int32_t cap) {
+    TextAcc a = {out, cap, 0};
+    walk_segs(&d->root->n, text_fn, &a);
+    return a.n;
+}
+
+typedef struct SegAcc {
+    int32_t *out;
+    int32_t cap, n;
+} SegAcc;
+static void seg_fn_dump(Seg *s, void *arg) {
+    SegAcc *a = (SegAcc *)arg;
+    if (a->n < a->cap) {
+        int32_t *r = a->out + 8 * a->n;
+        r[0] = s->len;
+        r[1] = s->seq;
+        r[2] = s->client;
+        r[3] = s->rseq;
+        r[4] = s->rseq == RSEQ_NONE ? INT32_MIN : s->rclient;
+        r[5] = s->novl;
+        r[6] = s->marker;
+        r[7] = s->props ? 1 : 0;
+    }
+    a->n++;
+}
+int32_t orc_segments(orc_doc *d, int32_t *out, int32_t cap_rows) {
+    SegAcc a = {out, cap_rows, 0};
+    walk_segs(&d->root->n, seg_fn_dump, &a);
+    return a.n;
+}
+typedef struct PropAcc {
+    int32_t want, idx;
+    Seg *hit;
+} PropAcc;
+static void prop_fn(Seg *s, void *arg) {
+    PropAcc *a = (PropAcc *)arg;
+    if (a->idx++ == a->want) a->hit = s;
+}
+int32_t orc_segment_props(orc_doc *d, int32_t seg_index, uint32_t *out, int32_t cap_pairs) {
+    PropAcc a = {seg_index, 0, NULL};
+    walk_segs(&d->root->n, prop_fn, &a);
+    if (!a.hit || !a.hit->props) return -1;
+    for (int i = 0; i < a.hit->props->n && i < cap_pairs; i++) {
+        out[2 * i] = a.hit->props->key[i];
+        out[2 * i + 1] = a.hit->props->val[i];
+    }
+    return a.hit->props->n;
+}
+
+static void leaves_rec(Block *b, int32_t *out, int32_t cap, int32_t *n) {
+    if (b->count == 0 || b->ch[0]->leaf) {
+        if (*n < cap) out[*n] = b->count;
+        (*n)++;
+        return;
+    }
+    for (int i = 0; i < b->count; i++) leaves_rec((Block *)b->ch[i], out, cap, n);
+}
+int32_t orc_leaves(orc_doc *d, int32_t *out, int32_t cap) {
+    int32_t n = 0;
+    leaves_rec(d->root, out, cap, &n);
+    return n;
+}
+
+typedef struct SumAcc {
+    uint64_t th, ph;
+    uint32_t len, nseg;
+    Seg *run;          /* current props run representative */
+    int32_t run_len;
+    int have;
+} SumAcc;
+static int same_ordered(const Props *a, const Props *b) {
+    if (!a || !b) return a == b;
+    if (a->n != b->n) return 0;
+    for (int i = 0; i < a->n; i++)
+        if (a->key[i] != b->key[i] || a->val[i] != b->val[i]) return 0;
+    return 1;
+}
+static uint64_t fold_run(uint64_t h, const Props *p, int32_t len) {
+    h = fnv_u32(h, (uint32_t)len);
+    h = fnv_u32(h, p ? 1u : 0u);
+    if (p) {
+        h = fnv_u32(h, (uint32_t)p->n);
+        for (int i = 0; i < p->n; i++) {
+            h = fnv_u32(h, p->key[i]);
+            h = fnv_u32(h, p->val[i]);
+        }
+    }
+    return h;
+}
+static void sum_fn(Seg *s, void *arg) {
+    SumAcc *a = (SumAcc *)arg;
+    a->nseg++;
+    if (s->rseq != RSEQ_NONE) return;
+    a->len += s->len;
+    if (s->marker < 0) {
+        for (int i = 0; i < s->len; i++) {
+            a->th ^= s->text[i] & 0xFF;
+            a->th *= FNV_PRIME;
+            a->th ^= s->text[i] >> 8;
+            a->th *= FNV_PRIME;
+        }
+    }
+    if (a->have && same_ordered(a->run->props, s->props)) {
+        a->run_len += s->len;
+    } else {
+        if (a->have) a->ph = fold_run(a->ph, a->run->props, a->run_len);
+        a->run = s;
+        a->run_len = s->len;
+        a->have = 1;
+    }
+}
+void orc_checksum(orc_doc *d, mt_checksum *out) {
+    SumAcc a;
+    memset(&a, 0, sizeof(a));
+    a.th = FNV_OFF;
+    a.ph = FNV_OFF;
+    walk_segs(&d->root->n, sum_fn, &a);
+    if (a.have) a.ph = fold_run(a.ph, a.run->props, a.run_len);
+    out->length = a.len;
+    out->n_segments = a.nseg;
+    out->text_hash = a.th;
+    out->props_hash = a.ph;
+    out->delta_hash = d->delta_hash;
+}
+int32_t orc_deltas(orc_doc *d, int32_t *out, int32_t cap) {
+    for (int64_t i = 0; i < d->dlog.n && i < cap; i++) out[i] = d->dlog.p[i];
+    return (int32_t)d->dlog.n;
+}
+
+/* ------------------------------------------------------------------ generator */
+typedef struct Rng {
+    uint32_t s[4];
+} Rng;
+static uint32_t splitmix32(uint32_t *x) {
+    *x += 0x9E3779B9u;
+    uint32_t z = *x;
+    z = (z ^ (z >> 16)) * 0x85EBCA6Bu;
+    z = (z ^ (z >> 13)) * 0xC2B2AE35u;
+    return z ^ (z >> 16);
+}
+static void rng_init(Rng *r, uint32_t seed, int32_t doc) {
+    uint32_t x = seed ^ ((uint32_t)(doc + 1) * 0x9E3779B9u);
+    for (int i = 0; i < 4; i++) r->s[i] = splitmix32(&x);
+}
+static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+static uint32_t rng_next(Rng *r) {   /* xoshiro128** */
+    uint32_t *s = r->s;
+    uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
+    uint32_t t = s[1] << 9;
+    s[2] ^= s[0];
+    s[3] ^= s[1];
+    s[1] ^= s[2];
+    s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = rotl32(s[3], 11);
+    return result;
+}
+static inline uint32_t rng_uniform(Rng *r, uint32_t n) {
+    return (uint32_t)(((uint64_t)rng_next(r) * n) >> 32);
+}
+static int gen_text(Rng *r, uint16_t *out, int n, uint64_t p_nl) {
+    for (int i = 0; i < n; i++) {
+        uint32_t v = rng_next(r);
+        out[i] = ((uint64_t)v < p_nl) ? (uint16_t)'\n' : (uint16_t)(97 + rng_uniform(r, 26));
+    }
+    return n;
+}
+/* writes [count, (key, val)*] ; returns words used */
+static int gen_props(Rng *r, const orc_gen_cfg *cfg, uint32_t *out) {
+    uint32_t nk = 1 + rng_uniform(r, (uint32_t)cfg->max_keys_per_op);
+    uint32_t count = 0;
+    for (uint32_t j = 0; j < nk; j++) {
+        uint32_t key = rng_uniform(r, (uint32_t)cfg->n_keys);
+        int is_null = (uint64_t)rng_next(r) < cfg->p_null;
+        uint32_t val = rng_uniform(r, (uint32_t)cfg->n_values);
+        int dup = 0;
+        for (uint32_t q = 0; q < count; q++)
+            if (out[1 + 2 * q] == key) dup = 1;
+        if (dup) continue;
+        out[1 + 2 * count] = key;
+        out[2 + 2 * count] = is_null ? MT_VAL_NULL : (val | (val == 0 ? MT_VAL_FALSY_BIT : 0));
+        count++;
+    }
+    out[0] = count;
+    return 1 + 2 * (int)count;
+}
+
+int32_t orc_generate(const orc_gen_cfg *cfg_in, int32_t doc, mt_op_rec *ops, int32_t ops_cap,
+                     uint16_t *text, int32_t text_cap, int32_t *text_used, uint32_t *props,
+                     int32_t props_cap, int32_t *props_used, uint16_t *seed_out,
+                     int32_t *seed_len_out, orc_doc **keep) {
+    const orc_gen_cfg *cfg = cfg_in;
+    Rng rng;
+    rng_init(&rng, cfg->seed, doc);
+    gen_text(&rng, seed_out, cfg->seed_len, 0);
+    *seed_len_out = cfg->seed_len;
+    orc_doc *d = orc_new(seed_out, cfg->seed_len);
+    int W = cfg->writers;
+    int32_t *last_ref = (int32_t *)calloc(W + 1, sizeof(int32_t));
+    int32_t *short_id = (int32_t *)calloc(W + 1, sizeof(int32_t));
+    int32_t next_short = 1;
+    int32_t tu = 0, pu = 0, n = 0;
+    uint64_t p_ins = cfg->p_insert, p_ir = cfg->p_insert_remove;
+    for (int32_t t = 1; t <= cfg->ops; t++) {
+        int k = 1 + (int)rng_uniform(&rng, (uint32_t)W);
+        int32_t lo = last_ref[k] > t - 1 - cfg->lag ? last_ref[k] : t - 1 - cfg->lag;
+        if (lo < 0) lo = 0;
+        int32_t r = lo + (int32_t)rng_uniform(&rng, (uint32_t)(t - 1 - lo + 1));
+        last_ref[k] = r;
+        int32_t msn = INT32_MAX;
+        for (int j = 1; j <= W; j++)
+            if (last_ref[j] < msn) msn = last_ref[j];
+        if (!short_id[k]) short_id[k] = next_short++;
+        int32_t c = short_id[k];
+        int32_t len = orc_view_length(d, r, c);
+        uint32_t u = rng_next(&rng);
+        if (n >= ops_cap) goto fail;
+        mt_op_rec *op = &ops[n];
+        memset(op, 0, sizeof(*op));
+        op->seq = t;
+        op->ref_seq = r;
+        op->min_seq = msn;
+        op->client = (uint16_t)c;
+        op->props = MT_NO_PROPS;
+        if (len == 0 || (uint64_t)u < p_ins) {
+            int32_t pos = (int32_t)rng_uniform(&rng, (uint32_t)(len + 1));
+            int32_t tl = 1 + (int32_t)rng_uniform(&rng, (uint32_t)cfg->text_max);
+            if (tu + tl > text_cap) goto fail;
+            gen_text(&rng, text + tu, tl, cfg->p_newline);
+            op->kind = MT_OP_INSERT;
+            op->pos1 = pos;
+            op->pos2 = tl;
+            op->payload = (uint32_t)tu;
+            tu += tl;
+            if (cfg->p_insert_props > 0 && (uint64_t)rng_next(&rng) < cfg->p_insert_props) {
+                if (pu + 1 + 2 * cfg->max_keys_per_op > props_cap) goto fail;
+                op->props = (uint32_t)pu;
+                pu += gen_props(&rng, cfg, props + pu);
+            }
+        } else {
+            int32_t p1 = (int32_t)rng_uniform(&rng, (uint32_t)len);
+            int32_t m = 1;
+            while (m < 64 && (uint64_t)rng_next(&rng) < cfg->p_len_continue) m++;
+            int32_t p2 = p1 + m < len ? p1 + m : len;
+            op->pos1 = p1;
+            op->pos2 = p2;
+            if ((uint64_t)u < p_ir) {
+                op->kind = MT_OP_REMOVE;
+            } else {
+                if (pu + 1 + 2 * cfg->max_keys_per_op > props_cap) goto fail;
+                op->kind = MT_OP_ANNOTATE;
+                op->props = (uint32_t)pu;
+                pu += gen_props(&rng, cfg, props + pu);
+            }
+        }
+        if (orc_apply(d, op, text, props) != MT_DOC_OK) goto fail;
+        n++;
+    }
+    free(last_ref);
+    free(short_id);
+    *text_used = tu;
+    *props_used = pu;
+    if (keep)
+        *keep = d;
+    else
+        orc_free(d);
+    return n;
+fail:
+    free(last_ref);
+    free(short_id);
+    orc_free(d);
+    if (keep) *keep = NULL;
+    return -1;
+}
+
+/* ------------------------------------------------------------------ batch replay */
+typedef struct BatchArg {
+    int32_t d0, d1;
+    const int64_t *doc_op_off;
+    const mt_op_rec *ops;
+    const uint16_t *text;
+    const uint32_t *props;
+    const int64_t *seed_off;
+    const uint16_t *seed;
+    mt_checksum *sum;
+    int32_t *status;
+} BatchArg;
+
+static void *batch_worker(void *p) {
+    BatchArg *a = (BatchArg *)p;
+    for (int32_t doc = a->d0; doc < a->d1; doc++) {
+        orc_doc *d = orc_new(a->seed + a->seed_off[doc], (int32_t)(a->seed_off[doc + 1] - a->seed_off[doc]));
+        for (int64_t i = a->doc_op_off[doc]; i < a->doc_op_off[doc + 1]; i++)
+            if (orc_apply(d, &a->ops[i], a->text, a->props)) break;
+        orc_checksum(d, &a->sum[doc]);
+        a->status[doc] = d->status;
+        orc_free(d);
+    }
+    return NULL;
+}
+
+int32_t orc_replay_batch(int32_t n_docs, const int64_t *doc_op_off, const mt_op_rec *ops,
+                         const uint16_t *text_arena, const uint32_t *props_arena,
+                         const int64_t *seed_off, const uint16_t *seed_arena,
+                         mt_checksum *out_sum, int32_t *out_status, int32_t threads) {
+    if (threads < 1) threads = 1;
+    if (threads > n_docs) threads = n_docs > 0 ? n_docs : 1;
+    pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
+    BatchArg *args = (BatchArg *)calloc(threads, sizeof(BatchArg));
+    for (int t = 0; t < threads; t++) {
+        BatchArg *a = &args[t];
+        a->d0 = (int32_t)((int64_t)n_docs * t / threads);
+        a->d1 = (int32_t)((int64_t)n_docs * (t + 1) / threads);
+        a->doc_op_off = doc_op_off;
+        a->ops = ops;
+        a->text = text_arena;
+        a->props = props_arena;
+        a->seed_off = seed_off;
+        a->seed = seed_arena;
+        a->sum = out_sum;
+        a->status = out_status;
+        pthread_create(&th[t], NULL, batch_worker, a);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(args);
+    return 0;
+}

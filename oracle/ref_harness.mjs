@@ -1,0 +1,340 @@
+// TEST INFRASTRUCTURE ONLY: drives the *transpiled reference* (oracle/_ref, built by
+// oracle/build_ref.py from /root/reference) as the observer replica of SURVEY.md App. A:
+//   observer = new Client(segmentFromSpec, logger)            MT/client.ts:75-84
+//   seed text inserted before collaboration (seq 0, client -1) MT/client.ts:202, 394-442
+//   observer.startOrUpdateCollaboration("observer")            MT/client.ts:1053-1073
+//   observer.applyMsg(msg) for every sequenced message         MT/client.ts:797-819
+// and records what the product must reproduce bit-exactly: final text, length, property
+// runs, every mergeTreeDeltaCallback (op kind, observer position, length, propertyDeltas),
+// plus the leaf segment table / B-tree shape for debugging.
+//
+// Modes:
+//   gen   : synthesise op streams with the shared generator (DESIGN.md "Synthetic op
+//           streams"); the writer's view length comes from the reference itself
+//           (MergeTree.getLength(refSeq, clientId), MT/mergeTree.ts:1610).
+//   replay: replay op logs given as JSON.
+// Usage:
+//   node oracle/ref_harness.mjs gen  <config.json> <doc_begin> <doc_end> <out.json>
+//   node oracle/ref_harness.mjs replay <logs.json> <out.json>
+import fs from "fs";
+import * as MT from "./_ref/mt/index.mjs";
+
+const { Client, TextSegment, Marker } = MT;
+
+function segmentFromSpec(spec) {           // SEQ/sequenceFactory.ts:31-37
+    const t = TextSegment.fromJSONObject(spec);
+    if (t) { return t; }
+    const m = Marker.fromJSONObject(spec);
+    if (m) { return m; }
+    throw new Error("bad spec");
+}
+const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+
+// ---------------------------------------------------------------- shared generator PRNG
+// xoshiro128** seeded through splitmix32 (identical in oracle/mt_oracle.c and the HIP
+// generator kernel).
+function splitmix32(state) {
+    state.x = (state.x + 0x9E3779B9) | 0;
+    let z = state.x;
+    z = Math.imul(z ^ (z >>> 16), 0x85EBCA6B);
+    z = Math.imul(z ^ (z >>> 13), 0xC2B2AE35);
+    return (z ^ (z >>> 16)) >>> 0;
+}
+class Rng {
+    constructor(seed, doc) {
+        const st = { x: (seed ^ Math.imul(doc + 1, 0x9E3779B9)) | 0 };
+        this.s = [splitmix32(st), splitmix32(st), splitmix32(st), splitmix32(st)];
+    }
+    next() {
+        const s = this.s;
+        const rotl = (x, k) => ((x << k) | (x >>> (32 - k))) >>> 0;
+        const result = Math.imul(rotl(Math.imul(s[1], 5) >>> 0, 7), 9) >>> 0;
+        const t = (s[1] << 9) >>> 0;
+        s[2] = (s[2] ^ s[0]) >>> 0;
+        s[3] = (s[3] ^ s[1]) >>> 0;
+        s[1] = (s[1] ^ s[2]) >>> 0;
+        s[0] = (s[0] ^ s[3]) >>> 0;
+        s[2] = (s[2] ^ t) >>> 0;
+        s[3] = rotl(s[3], 11);
+        return result;
+    }
+    uniform(n) { return Math.floor(this.next() * n / 4294967296); }
+}
+const frac = (p) => Math.floor(p * 4294967296);
+
+function genText(rng, n, pNl) {
+    let s = "";
+    for (let i = 0; i < n; i++) {
+        const v = rng.next();
+        s += (v < pNl) ? "\n" : String.fromCharCode(97 + rng.uniform(26));
+    }
+    return s;
+}
+function genProps(rng, cfg) {
+    const nk = 1 + rng.uniform(cfg.max_keys_per_op);
+    const props = {};
+    const seen = new Set();
+    for (let j = 0; j < nk; j++) {
+        const key = rng.uniform(cfg.n_keys);
+        const isNull = rng.next() < frac(cfg.p_null);
+        const val = rng.uniform(cfg.n_values);
+        if (seen.has(key)) { continue; }
+        seen.add(key);
+        props[`k${key}`] = isNull ? null : val;
+    }
+    return props;
+}
+
+// ---------------------------------------------------------------- observer replica
+function makeObserver(seedText) {
+    const c = new Client(segmentFromSpec, logger);
+    if (seedText.length > 0) {
+        c.insertSegmentLocal(0, TextSegment.make(seedText));
+    }
+    c.startOrUpdateCollaboration("observer");
+    const deltas = [];
+    c.mergeTreeDeltaCallback = (opArgs, dargs) => {
+        const mt = c.mergeTree;
+        const cw = mt.getCollabWindow();
+        const rec = [opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1,
+            dargs.operation, dargs.deltaSegments.length];
+        const segs = [];
+        for (const d of dargs.deltaSegments) {
+            const seg = d.segment;
+            const pos = seg.parent ? mt.getPosition(seg, cw.currentSeq, cw.clientId) : -1;
+            segs.push(d.propertyDeltas !== undefined ? [pos, seg.cachedLength, d.propertyDeltas]
+                : [pos, seg.cachedLength]);
+        }
+        rec.push(segs);
+        deltas.push(rec);
+    };
+    return { c, deltas };
+}
+
+function makeMsg(k, seq, ref, msn, cseq, contents) {
+    return {
+        clientId: `client-${k}`, sequenceNumber: seq, referenceSequenceNumber: ref,
+        minimumSequenceNumber: msn, clientSequenceNumber: cseq, type: "op", contents,
+        timestamp: 0, term: 1, traces: [],
+    };
+}
+
+function collectOutputs(c, deltas) {
+    const mt = c.mergeTree;
+    const cw = mt.getCollabWindow();
+    const text = c.createTextHelper().getText(cw.currentSeq, cw.clientId);
+    const segs = [];
+    const runs = [];
+    const leaves = [];
+    const shape = (block) => {
+        const out = [];
+        for (let i = 0; i < block.childCount; i++) {
+            const ch = block.children[i];
+            if (ch.isLeaf()) {
+                out.push(null);
+            } else {
+                out.push(shape(ch));
+            }
+        }
+        return out;
+    };
+    mt.walkAllSegments(mt.root, (seg) => {
+        const rec = {
+            len: seg.cachedLength, seq: seg.seq, cli: seg.clientId,
+            rseq: seg.removedSeq === undefined ? null : seg.removedSeq,
+            rcli: seg.removedClientId === undefined ? null : seg.removedClientId,
+            ovl: seg.removedClientOverlap ? [...seg.removedClientOverlap] : [],
+            marker: Marker.is(seg) ? seg.refType : null,
+            props: seg.properties === undefined ? null : seg.properties,
+        };
+        segs.push(rec);
+        if (seg.removedSeq === undefined) {
+            const p = seg.properties === undefined ? null : JSON.stringify(seg.properties);
+            if (runs.length && runs[runs.length - 1][1] === p) {
+                runs[runs.length - 1][0] += seg.cachedLength;
+            } else {
+                runs.push([seg.cachedLength, p]);
+            }
+        }
+        return true;
+    });
+    // leaf-block partition: childCount of every block whose children are segments
+    const walk = (block) => {
+        if (block.childCount === 0 || block.children[0].isLeaf()) {
+            leaves.push(block.childCount);
+            return;
+        }
+        for (let i = 0; i < block.childCount; i++) { walk(block.children[i]); }
+    };
+    walk(mt.root);
+    return {
+        text, length: c.getLength(), currentSeq: cw.currentSeq, minSeq: cw.minSeq,
+        runs: runs.map(([l, p]) => [l, p === null ? null : JSON.parse(p)]),
+        segs, leaves, tree: shape(mt.root), deltas,
+    };
+}
+
+function genDoc(cfg, doc) {
+    const rng = new Rng(cfg.seed >>> 0, doc);
+    const seedText = genText(rng, cfg.seed_len, 0);
+    const { c, deltas } = makeObserver(seedText);
+    const W = cfg.writers;
+    const lastRef = new Array(W + 1).fill(0);
+    const cseq = new Array(W + 1).fill(0);
+    const msgs = [];
+    const t0 = process.hrtime.bigint();
+    for (let t = 1; t <= cfg.ops; t++) {
+        const k = 1 + rng.uniform(W);
+        let lo = Math.max(lastRef[k], t - 1 - cfg.lag);
+        if (lo < 0) { lo = 0; }
+        const r = lo + rng.uniform(t - 1 - lo + 1);
+        lastRef[k] = r;
+        let msn = Infinity;
+        for (let j = 1; j <= W; j++) { msn = Math.min(msn, lastRef[j]); }
+        const shortId = c.getOrAddShortClientId(`client-${k}`);
+        const len = c.mergeTree.getLength(r, shortId);
+        const u = rng.next();
+        let op;
+        if (len === 0 || u < frac(cfg.p_insert)) {
+            const pos = rng.uniform(len + 1);
+            const tl = 1 + rng.uniform(cfg.text_max);
+            const text = genText(rng, tl, frac(cfg.p_newline));
+            let seg = text;
+            if (cfg.p_insert_props > 0 && rng.next() < frac(cfg.p_insert_props)) {
+                seg = { text, props: genProps(rng, cfg) };
+            }
+            op = { pos1: pos, seg, type: 0 };
+        } else {
+            const p1 = rng.uniform(len);
+            let n = 1;
+            while (n < 64 && rng.next() < frac(cfg.p_len_continue)) { n++; }
+            const p2 = Math.min(p1 + n, len);
+            if (u < frac(cfg.p_insert + cfg.p_remove)) {
+                op = { pos1: p1, pos2: p2, type: 1 };
+            } else {
+                op = { pos1: p1, pos2: p2, props: genProps(rng, cfg), type: 2 };
+            }
+        }
+        const msg = makeMsg(k, t, r, msn, ++cseq[k], op);
+        msgs.push([k, t, r, msn, op]);
+        c.applyMsg(JSON.parse(JSON.stringify(msg)));
+    }
+    const ns = Number(process.hrtime.bigint() - t0);
+    const out = collectOutputs(c, deltas);
+    return { doc, seed_text: seedText, msgs, out, ref_ns: ns };
+}
+
+// Edge-case streams (fixtures only; replayed by the oracle and the HIP path, never
+// re-generated by them): markers, rewrite annotates, GROUP messages, noop messages, empty
+// inserts, ranges past the view end, and non-numeric / falsy property values.
+const EXT_VALUES = [0, 1, "", "x", false, true, { a: 1, b: [1, 2] }, { b: [1, 2], a: 1 }, [0], "0", 2.5, null];
+function genPropsExt(rng, cfg) {
+    const nk = 1 + rng.uniform(cfg.max_keys_per_op);
+    const props = {};
+    for (let j = 0; j < nk; j++) {
+        const key = `k${rng.uniform(cfg.n_keys)}`;
+        const v = EXT_VALUES[rng.uniform(EXT_VALUES.length)];
+        if (key in props) { continue; }
+        props[key] = v;
+    }
+    return props;
+}
+function genOpExt(rng, cfg, len) {
+    const u = rng.next();
+    if (len === 0 || u < frac(cfg.p_insert)) {
+        const pos = rng.uniform(len + 1);
+        if (rng.next() < frac(cfg.p_marker)) {
+            const seg = { marker: { refType: 1 + rng.uniform(2) } };
+            if (rng.next() < frac(0.5)) { seg.props = genPropsExt(rng, cfg); }
+            return { pos1: pos, seg, type: 0 };
+        }
+        const empty = rng.next() < frac(cfg.p_empty);
+        const text = empty ? "" : genText(rng, 1 + rng.uniform(cfg.text_max), frac(cfg.p_newline));
+        let seg = text;
+        if (rng.next() < frac(cfg.p_insert_props)) { seg = { text, props: genPropsExt(rng, cfg) }; }
+        return { pos1: pos, seg, type: 0 };
+    }
+    const p1 = rng.uniform(len);
+    let n = 1;
+    while (n < 300 && rng.next() < frac(cfg.p_len_continue)) { n++; }
+    let p2 = Math.min(p1 + n, len);
+    if (rng.next() < frac(cfg.p_oob)) { p2 = len + 1 + rng.uniform(5); }
+    if (u < frac(cfg.p_insert + cfg.p_remove)) { return { pos1: p1, pos2: p2, type: 1 }; }
+    const op = { pos1: p1, pos2: p2, props: genPropsExt(rng, cfg), type: 2 };
+    if (rng.next() < frac(cfg.p_rewrite)) { op.combiningOp = { name: "rewrite" }; }
+    return op;
+}
+function genDocExt(cfg, doc) {
+    const rng = new Rng(cfg.seed >>> 0, doc);
+    const seedText = genText(rng, cfg.seed_len, frac(cfg.p_newline));
+    const { c, deltas } = makeObserver(seedText);
+    const W = cfg.writers;
+    const lastRef = new Array(W + 1).fill(0);
+    const cseq = new Array(W + 1).fill(0);
+    const msgs = [];
+    for (let t = 1; t <= cfg.ops; t++) {
+        const k = 1 + rng.uniform(W);
+        let lo = Math.max(lastRef[k], t - 1 - cfg.lag);
+        if (lo < 0) { lo = 0; }
+        const r = lo + rng.uniform(t - 1 - lo + 1);
+        lastRef[k] = r;
+        let msn = Infinity;
+        for (let j = 1; j <= W; j++) { msn = Math.min(msn, lastRef[j]); }
+        const shortId = c.getOrAddShortClientId(`client-${k}`);
+        let len = c.mergeTree.getLength(r, shortId);
+        let contents;
+        let type = "op";
+        const g = rng.next();
+        if (g < frac(cfg.p_noop)) {
+            type = "noop";
+            contents = null;
+        } else if (g < frac(cfg.p_noop + cfg.p_group)) {
+            const members = [];
+            const m = 2 + rng.uniform(2);
+            let removed = 0;
+            for (let j = 0; j < m; j++) {
+                const op = genOpExt(rng, cfg, Math.max(0, len - removed));
+                if (op.type === 1) { removed += Math.max(0, Math.min(op.pos2, len) - op.pos1); }
+                if (op.type === 0 && typeof op.seg === "string") { len += op.seg.length; }
+                members.push(op);
+            }
+            contents = { type: 3, ops: members };
+        } else {
+            contents = genOpExt(rng, cfg, len);
+        }
+        const msg = makeMsg(k, t, r, msn, ++cseq[k], contents);
+        msg.type = type;
+        msgs.push([k, t, r, msn, contents, type]);
+        c.applyMsg(JSON.parse(JSON.stringify(msg)));
+    }
+    const out = collectOutputs(c, deltas);
+    return { doc, seed_text: seedText, msgs, out, ref_ns: 0 };
+}
+
+function replayDoc(log) {
+    const { c, deltas } = makeObserver(log.seed_text);
+    const cseq = {};
+    for (const [k, t, r, msn, op, type] of log.msgs) {
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        c.applyMsg(msg);
+    }
+    return collectOutputs(c, deltas);
+}
+
+const [mode, ...rest] = process.argv.slice(2);
+if (mode === "gen") {
+    const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+    const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
+    const docs = [];
+    for (let d = d0; d < d1; d++) { docs.push(cfg.ext ? genDocExt(cfg, d) : genDoc(cfg, d)); }
+    fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
+} else if (mode === "replay") {
+    const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+    const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
+    fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
+} else {
+    console.error("usage: ref_harness.mjs gen|replay ...");
+    process.exit(2);
+}

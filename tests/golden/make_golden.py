@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Regenerates the golden fixtures in tests/golden/ from the reference itself.
+
+Runs only in the build container (needs /root/reference and node): builds the transpiled
+reference with oracle/build_ref.py, then drives it with oracle/ref_harness.mjs.  Each
+fixture holds, per document, the input op log (compact messages) and the reference's
+outputs (text, length, property runs, leaf-block partition, segment table, every delta
+callback).  The fixtures are data, not reference source.
+
+    python3 tests/golden/make_golden.py
+"""
+import gzip
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+FIXTURES = {
+    # name: (base config from bench/configs.json or inline, overrides, docs)
+    "ref_c2": ("c2", {"ops": 2000}, 4),
+    "ref_c3": ("c3", {"ops": 2500}, 4),
+    "ref_c4": ("c4", {"ops": 3000}, 3),
+    "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),
+    "ref_ext": (None, {"ext": True, "seed": 77, "ops": 700, "writers": 5, "lag": 40, "seed_len": 40,
+                       "p_insert": 0.5, "p_remove": 0.3, "text_max": 12, "p_newline": 0.08,
+                       "p_len_continue": 0.8, "p_insert_props": 0.3, "n_keys": 5,
+                       "max_keys_per_op": 3, "p_marker": 0.1, "p_rewrite": 0.3, "p_group": 0.1,
+                       "p_noop": 0.05, "p_empty": 0.05, "p_oob": 0.05}, 8),
+    "ref_ext_long": (None, {"ext": True, "seed": 91, "ops": 1500, "writers": 12, "lag": 300,
+                            "seed_len": 600, "p_insert": 0.45, "p_remove": 0.35, "text_max": 300,
+                            "p_newline": 0.002, "p_len_continue": 0.97, "p_insert_props": 0.2,
+                            "n_keys": 4, "max_keys_per_op": 2, "p_marker": 0.02, "p_rewrite": 0.2,
+                            "p_group": 0.05, "p_noop": 0.02, "p_empty": 0.01, "p_oob": 0.02}, 3),
+}
+
+
+def main():
+    subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
+    configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
+    for name, (base, over, ndocs) in FIXTURES.items():
+        cfg = dict(configs[base]) if base else {}
+        cfg.update(over)
+        with tempfile.TemporaryDirectory() as td:
+            cp = os.path.join(td, "cfg.json")
+            op = os.path.join(td, "out.json")
+            json.dump(cfg, open(cp, "w"))
+            subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "gen", cp,
+                                   "0", str(ndocs), op])
+            data = json.load(open(op))
+        for d in data["docs"]:
+            d["out"].pop("tree", None)
+            d.pop("ref_ns", None)
+        with gzip.open(os.path.join(HERE, name + ".json.gz"), "wt") as fh:
+            json.dump(data, fh, separators=(",", ":"))
+        print(name, ndocs, "docs")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+"""Helpers turning reference-generated golden fixtures (tests/golden/*.json.gz, made by
+tests/golden/make_golden.py from the reference itself) into wire-format inputs and
+id-space expected outputs, and comparing implementation outputs against them."""
+import gzip
+import json
+import os
+
+import numpy as np
+
+from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+INT_MIN = -2 ** 31
+ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long"]
+
+
+def load(name):
+    with gzip.open(os.path.join(GOLDEN, name + ".json.gz"), "rt") as fh:
+        return json.load(fh)
+
+
+def interner_for(fixture):
+    return Interner(synthetic=not fixture["config"].get("ext", False))
+
+
+def encode_docs(fixture, interner, docs=None):
+    b = Batch(interner)
+    for d in (fixture["docs"] if docs is None else docs):
+        b.add_doc(d["seed_text"], compact_msgs_to_dicts(d["msgs"]))
+    return b.arrays()
+
+
+def _sid(v):
+    """value id as int32 (the oracle reports signed ints)."""
+    return v - 2 ** 32 if v >= 2 ** 31 else v
+
+
+def expected(doc, interner):
+    out = doc["out"]
+    segs = []
+    seg_props = []
+    for r in out["segs"]:
+        segs.append([r["len"], r["seq"], r["cli"], INT_MIN if r["rseq"] is None else r["rseq"],
+                     INT_MIN if r["rcli"] is None else r["rcli"], len(r["ovl"]),
+                     -1 if r["marker"] is None else r["marker"], 0 if r["props"] is None else 1])
+        seg_props.append(None if r["props"] is None else
+                         [(interner.key(k), interner.val(v)) for k, v in r["props"].items()])
+    flat = []
+    for seq, kind, n, dsegs in out["deltas"]:
+        flat += [seq, kind, n]
+        for s in dsegs:
+            flat += [s[0], s[1]]
+            if kind == 2:
+                pd = s[2]
+                flat.append(len(pd))
+                for k, v in pd.items():
+                    flat += [interner.key(k), _sid(interner.val(v))]
+    return dict(text=out["text"], length=out["length"], leaves=out["leaves"], segs=segs,
+                seg_props=seg_props, deltas=flat)
+
+
+def compare_oracle(o, exp):
+    errs = []
+    if o["status"]:
+        errs.append(f"status {o['status']}")
+    if o["text"] != exp["text"]:
+        errs.append("text")
+    if o["length"] != exp["length"]:
+        errs.append(f"length {o['length']} != {exp['length']}")
+    if o["leaves"] != exp["leaves"]:
+        errs.append("leaves")
+    if o["segs"].tolist() != exp["segs"]:
+        errs.append("segs")
+    if o["seg_props"] != exp["seg_props"]:
+        errs.append("seg_props")
+    if o["deltas"] != exp["deltas"]:
+        errs.append("deltas")
+    return errs

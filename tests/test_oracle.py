@@ -1,0 +1,44 @@
+"""Pins the CPU restatement oracle (oracle/mt_oracle.c) to the reference itself: every
+golden fixture under tests/golden/ was produced by the reference's own MergeTree/Client
+(transpiled by oracle/build_ref.py, driven by oracle/ref_harness.mjs)."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+
+@pytest.mark.parametrize("name", gu.ALL_FIXTURES)
+def test_oracle_matches_reference(oracle_lib, name):
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    for doc in fx["docs"]:
+        a = gu.encode_docs(fx, interner, [doc])
+        od = oracle_lib.OracleDoc.new(a["seed"][: a["seed_off"][1]])
+        od.apply_all(a["ops"], a["text"], a["props"])
+        errs = gu.compare_oracle(od.outputs(), gu.expected(doc, interner))
+        assert not errs, f"{name} doc {doc['doc']}: {errs}"
+
+
+@pytest.mark.parametrize("name", ["ref_small", "ref_c2", "ref_c3", "ref_c4"])
+def test_oracle_generator_reproduces_reference_streams(oracle_lib, name):
+    """The generator (shared spec) draws identical op streams whether the view
+    lengths come from the reference or from the oracle."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    for doc in fx["docs"]:
+        a = gu.encode_docs(fx, interner, [doc])
+        g = oracle_lib.generate(fx["config"], doc["doc"])
+        assert np.array_equal(g["ops"], a["ops"]), f"doc {doc['doc']} ops differ"
+        assert np.array_equal(g["text"][: len(a["text"])], a["text"])
+        assert np.array_equal(g["seed"], a["seed"][: a["seed_off"][1]])
+
+
+def test_batch_replay_checksums_consistent(oracle_lib):
+    fx = gu.load("ref_c3")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    s1, st1 = oracle_lib.replay_batch(a, threads=1)
+    s4, st4 = oracle_lib.replay_batch(a, threads=4)
+    assert (st1 == 0).all() and np.array_equal(s1, s4)
+    for i, doc in enumerate(fx["docs"]):
+        assert s1[i]["length"] == doc["out"]["length"]
