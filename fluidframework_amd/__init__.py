@@ -1,0 +1,216 @@
+"""fluidframework_amd -- MI355X replay / catch-up backend for Fluid Framework's merge-tree.
+
+The hot path (Client.applyMsg over thousands of independent SharedString documents) runs in
+hand-written HIP kernels (csrc/) behind the C ABI in include/mt_replay.h.  This Python
+module is host plumbing mirroring the reference `Client` surface for tests and the bench;
+the Node/N-API facade in js/ is the reference-language binding."""
+import ctypes
+
+import numpy as np
+
+from . import _native
+from .wire import CHECKSUM_DTYPE, OP_DTYPE, Batch, Interner  # noqa: F401
+
+__all__ = ["MergeTreeBatch", "DeviceBatch", "Batch", "Interner"]
+
+
+class MergeTreeBatch:
+    """N observer replicas (one per document) resident on one GPU.
+
+    Mirrors, per document, `new Client(...)` + `startOrUpdateCollaboration` (MT/client.ts:
+    75-84, 1053-1073), `applyMsg` (:797-819), `getLength` (:1051), `getText` via
+    MergeTreeTextHelper (MT/textSegment.ts:154-172) and `getPropertiesAtPosition` (:1011-1025).
+    """
+
+    def __init__(self, n_docs, device=0, seg_capacity=0, block_capacity=0, heap_capacity=0,
+                 text_capacity=0, props_capacity=0, delta_log_capacity=0):
+        self.lib = _native.load()
+        opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
+                                text_capacity, props_capacity, delta_log_capacity)
+        self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
+        if not self.h:
+            raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")
+        self.n_docs = n_docs
+
+    def close(self):
+        if self.h:
+            self.lib.mt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.mt_last_error(self.h).decode()}")
+
+    # -------------------------------------------------------------- input
+    def load_initial_text(self, seed_off, seed):
+        seed_off = np.ascontiguousarray(seed_off, dtype=np.int64)
+        seed = np.ascontiguousarray(seed, dtype=np.uint16)
+        self._check(self.lib.mt_load_initial_text(self.h, _native.ptr(seed_off), _native.ptr(seed)),
+                    "mt_load_initial_text")
+
+    def apply_arrays(self, a):
+        ops = np.ascontiguousarray(a["ops"], dtype=OP_DTYPE)
+        off = np.ascontiguousarray(a["doc_off"], dtype=np.int64)
+        text = np.ascontiguousarray(a["text"], dtype=np.uint16)
+        props = np.ascontiguousarray(a["props"], dtype=np.uint32)
+        self._check(self.lib.mt_apply_ops(self.h, _native.ptr(off), _native.ptr(ops), len(ops),
+                                          _native.ptr(text), len(text), _native.ptr(props), len(props)),
+                    "mt_apply_ops")
+
+    def upload(self, a):
+        return DeviceBatch(self, a)
+
+    def generate(self, cfg, doc_base=0, trace=None):
+        c = _native.gen_cfg(cfg)
+        b = self.lib.mt_generate(self.h, ctypes.byref(c), doc_base, _native.ptr(trace))
+        if not b:
+            raise RuntimeError(f"mt_generate failed: {self.lib.mt_last_error(self.h).decode()}")
+        return DeviceBatch(self, None, handle=b)
+
+    def generated_seeds(self, cfg, doc_base=0):
+        c = _native.gen_cfg(cfg)
+        off = np.zeros(self.n_docs + 1, dtype=np.int64)
+        self._check(self.lib.mt_generated_seeds(self.h, ctypes.byref(c), doc_base, _native.ptr(off), None),
+                    "mt_generated_seeds")
+        seed = np.zeros(max(int(off[-1]), 1), dtype=np.uint16)
+        self._check(self.lib.mt_generated_seeds(self.h, ctypes.byref(c), doc_base, _native.ptr(off),
+                                                _native.ptr(seed)), "mt_generated_seeds")
+        return off, seed
+
+    def sync(self):
+        self._check(self.lib.mt_sync(self.h), "mt_sync")
+
+    def last_kernel_ms(self):
+        return float(self.lib.mt_last_kernel_ms(self.h))
+
+    # -------------------------------------------------------------- read-out
+    def status(self):
+        out = np.zeros(self.n_docs, dtype=np.int32)
+        self._check(self.lib.mt_get_status(self.h, _native.ptr(out)), "mt_get_status")
+        return out
+
+    def get_length(self, doc):
+        out = ctypes.c_uint32()
+        self._check(self.lib.mt_get_length(self.h, doc, ctypes.byref(out)), "mt_get_length")
+        return out.value
+
+    def get_text(self, doc):
+        n = ctypes.c_uint32()
+        self._check(self.lib.mt_get_text(self.h, doc, None, 0, ctypes.byref(n)), "mt_get_text")
+        buf = np.zeros(max(n.value, 1), dtype=np.uint16)
+        self._check(self.lib.mt_get_text(self.h, doc, _native.ptr(buf), n.value, ctypes.byref(n)),
+                    "mt_get_text")
+        return buf[: n.value].tobytes().decode("utf-16-le", errors="surrogatepass")
+
+    def get_segments(self, doc):
+        nr, nl = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.mt_get_segments(self.h, doc, None, 0, ctypes.byref(nr), None, 0,
+                                             ctypes.byref(nl)), "mt_get_segments")
+        rows = np.zeros((max(nr.value, 1), 8), dtype=np.int32)
+        leaves = np.zeros(max(nl.value, 1), dtype=np.int32)
+        self._check(self.lib.mt_get_segments(self.h, doc, _native.ptr(rows), nr.value, ctypes.byref(nr),
+                                             _native.ptr(leaves), nl.value, ctypes.byref(nl)),
+                    "mt_get_segments")
+        return rows[: nr.value], leaves[: nl.value].tolist()
+
+    def get_segment_props(self, doc, i):
+        pairs = np.zeros(64, dtype=np.uint32)
+        n = ctypes.c_int32()
+        self._check(self.lib.mt_get_segment_props(self.h, doc, i, _native.ptr(pairs), 32, ctypes.byref(n)),
+                    "mt_get_segment_props")
+        if n.value < 0:
+            return None
+        return [(int(pairs[2 * j]), int(pairs[2 * j + 1])) for j in range(n.value)]
+
+    def get_prop_runs(self, doc):
+        nr, nw = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.mt_get_prop_runs(self.h, doc, None, 0, ctypes.byref(nr), None, 0,
+                                              ctypes.byref(nw)), "mt_get_prop_runs")
+        runs = np.zeros((max(nr.value, 1), 3), dtype=np.uint32)
+        recs = np.zeros(max(nw.value, 1), dtype=np.uint32)
+        self._check(self.lib.mt_get_prop_runs(self.h, doc, _native.ptr(runs), nr.value, ctypes.byref(nr),
+                                              _native.ptr(recs), nw.value, ctypes.byref(nw)),
+                    "mt_get_prop_runs")
+        out = []
+        for s, l, r in runs[: nr.value].tolist():
+            if r == 0xFFFFFFFF:
+                out.append((s, l, None))
+            else:
+                n = int(recs[r])
+                out.append((s, l, [(int(recs[r + 1 + 2 * j]), int(recs[r + 2 + 2 * j])) for j in range(n)]))
+        return out
+
+    def get_properties_at_position(self, doc, pos):
+        for s, l, p in self.get_prop_runs(doc):
+            if s <= pos < s + l:
+                return p
+        return None
+
+    def get_delta_log(self, doc):
+        n = ctypes.c_uint32()
+        self._check(self.lib.mt_get_delta_log(self.h, doc, None, 0, ctypes.byref(n)), "mt_get_delta_log")
+        buf = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._check(self.lib.mt_get_delta_log(self.h, doc, _native.ptr(buf), n.value, ctypes.byref(n)),
+                    "mt_get_delta_log")
+        return buf[: n.value].tolist()
+
+    def checksums(self):
+        out = np.zeros(self.n_docs, dtype=CHECKSUM_DTYPE)
+        self._check(self.lib.mt_checksums(self.h, _native.ptr(out)), "mt_checksums")
+        return out
+
+    def checksums_device(self, device_ptr):
+        self._check(self.lib.mt_checksums_device(self.h, ctypes.c_void_p(device_ptr)), "mt_checksums_device")
+
+
+class DeviceBatch:
+    """A batch of encoded messages resident in HBM (mt_batch)."""
+
+    def __init__(self, owner, a, handle=None):
+        self.owner = owner
+        lib = owner.lib
+        if handle is None:
+            ops = np.ascontiguousarray(a["ops"], dtype=OP_DTYPE)
+            off = np.ascontiguousarray(a["doc_off"], dtype=np.int64)
+            text = np.ascontiguousarray(a["text"], dtype=np.uint16)
+            props = np.ascontiguousarray(a["props"], dtype=np.uint32)
+            handle = lib.mt_batch_upload(owner.h, _native.ptr(off), _native.ptr(ops), len(ops),
+                                         _native.ptr(text), len(text), _native.ptr(props), len(props))
+            if not handle:
+                raise RuntimeError(f"mt_batch_upload failed: {lib.mt_last_error(owner.h).decode()}")
+        self.b = handle
+        self.n_ops = int(lib.mt_batch_num_ops(self.b))
+
+    def apply_async(self):
+        self.owner._check(self.owner.lib.mt_batch_apply_async(self.owner.h, self.b), "mt_batch_apply_async")
+
+    def download(self):
+        lib = self.owner.lib
+        n, t, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib.mt_batch_sizes(self.b, ctypes.byref(n), ctypes.byref(t), ctypes.byref(p))
+        off = np.zeros(self.owner.n_docs + 1, dtype=np.int64)
+        ops = np.zeros(n.value, dtype=OP_DTYPE)
+        text = np.zeros(max(t.value, 1), dtype=np.uint16)
+        props = np.zeros(max(p.value, 1), dtype=np.uint32)
+        rc = lib.mt_batch_download(self.b, _native.ptr(off), _native.ptr(ops), _native.ptr(text),
+                                   _native.ptr(props))
+        if rc:
+            raise RuntimeError("mt_batch_download failed")
+        return dict(doc_off=off, ops=ops, text=text, props=props)
+
+    def free(self):
+        if self.b:
+            self.owner.lib.mt_batch_free(self.b)
+            self.b = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

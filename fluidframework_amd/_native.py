@@ -1,0 +1,90 @@
+"""ctypes binding of the C-ABI in include/mt_replay.h (libmtreplay.so).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is visible,
+the calls raise."""
+import ctypes
+import os
+
+import numpy as np
+
+from .wire import CHECKSUM_DTYPE, OP_DTYPE
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmtreplay.so")
+
+
+class MtOptions(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("seg_capacity", ctypes.c_int32),
+                ("block_capacity", ctypes.c_int32), ("heap_capacity", ctypes.c_int32),
+                ("text_capacity", ctypes.c_int32), ("props_capacity", ctypes.c_int32),
+                ("delta_log_capacity", ctypes.c_int32)]
+
+
+class MtGenCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint32), ("ops", ctypes.c_int32), ("writers", ctypes.c_int32),
+                ("lag", ctypes.c_int32), ("seed_len", ctypes.c_int32), ("text_max", ctypes.c_int32),
+                ("n_keys", ctypes.c_int32), ("n_values", ctypes.c_int32),
+                ("max_keys_per_op", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("p_insert", ctypes.c_uint64), ("p_insert_remove", ctypes.c_uint64),
+                ("p_newline", ctypes.c_uint64), ("p_len_continue", ctypes.c_uint64),
+                ("p_insert_props", ctypes.c_uint64), ("p_null", ctypes.c_uint64)]
+
+
+# (name, restype, argtypes) for every symbol of include/mt_replay.h
+_P, _I, _U32, _U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+SIGNATURES = [
+    ("mt_create", _P, [_U32, _P]),
+    ("mt_destroy", None, [_P]),
+    ("mt_last_error", ctypes.c_char_p, [_P]),
+    ("mt_num_docs", _U32, [_P]),
+    ("mt_load_initial_text", _I, [_P, _P, _P]),
+    ("mt_apply_ops", _I, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),
+    ("mt_batch_upload", _P, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),
+    ("mt_batch_apply_async", _I, [_P, _P]),
+    ("mt_batch_num_ops", _U64, [_P]),
+    ("mt_batch_free", None, [_P]),
+    ("mt_sync", _I, [_P]),
+    ("mt_last_kernel_ms", ctypes.c_float, [_P]),
+    ("mt_generate", _P, [_P, _P, _U32, _P]),
+    ("mt_generated_seeds", _I, [_P, _P, _U32, _P, _P]),
+    ("mt_batch_sizes", _I, [_P, _P, _P, _P]),
+    ("mt_batch_download", _I, [_P, _P, _P, _P, _P]),
+    ("mt_get_status", _I, [_P, _P]),
+    ("mt_get_length", _I, [_P, _U32, _P]),
+    ("mt_get_text", _I, [_P, _U32, _P, _U32, _P]),
+    ("mt_get_prop_runs", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
+    ("mt_get_segments", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
+    ("mt_get_segment_props", _I, [_P, _U32, _U32, _P, _U32, _P]),
+    ("mt_get_delta_log", _I, [_P, _U32, _P, _U32, _P]),
+    ("mt_checksums", _I, [_P, _P]),
+    ("mt_checksums_device", _I, [_P, _P]),
+]
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP replay library missing: {LIB_PATH} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def gen_cfg(cfg):
+    from .wire import gen_thresholds
+    return MtGenCfg(seed=cfg["seed"], ops=cfg["ops"], writers=cfg["writers"], lag=cfg["lag"],
+                    seed_len=cfg["seed_len"], text_max=cfg["text_max"], n_keys=cfg["n_keys"],
+                    n_values=cfg["n_values"], max_keys_per_op=cfg["max_keys_per_op"],
+                    **gen_thresholds(cfg))

@@ -1,0 +1,137 @@
+// mt_device.h -- device-side data layout and wave primitives of the MI355X merge-tree
+// replay engine.  One wavefront (64 lanes, one workgroup) owns one document for the whole
+// launch and applies that document's ops in sequence order.
+//
+// Per-document state in HBM (struct-of-arrays, document-major, fixed per-doc strides):
+//   segA[S]  int4  {cachedLength, seq, removedSeq (INT_MIN = undefined), client|rclient<<16}
+//   segO[S]  u64   removedClientOverlap as a bit mask over short client ids 1..64
+//   segB[S]  uint4 {text offset (marker: refType), props record handle, uid|MARKER, 0}
+//            -- all in *document order*: the flat order of the reference's leaves
+//   cnt[LV][B] u8  child counts of every B-tree level in order (level 0 = leaf blocks);
+//            the reference's tree (MT/mergeTree.ts:333 MaxNodesInBlock=8) is exactly
+//            determined by these counts because every leaf sits at the same depth
+//   flg[B]   i8    leaf-block needsScour tri-state (-1 undefined, 0 false, 1 true)
+//   heap[H]  int2  zamboni LRU heap {maxSeq, uid} (1-based, MT/collections.ts:212-265)
+//   text[2][T] u16 UTF-16 arena, two halves for compaction
+//   props[2][P][PREC] u32 property-set records {n, (key, value) x KMAX}
+// During a launch the B-tree counts and flags are staged in LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mt_types.h"
+
+#define MT_WAVE 64
+#define MT_LV 8                 // max B-tree levels (7^8 leaves >> any capacity)
+#define MT_MAXN 8               // MaxNodesInBlock           MT/mergeTree.ts:333
+#define MT_HALF 4               // MaxNodesInBlock / 2       MT/mergeTree.ts:2510
+#define MT_GRAN 256             // TextSegmentGranularity    MT/mergeTree.ts:1093
+#define MT_ZAMBONI 2            // zamboniSegmentsMaxCount   MT/mergeTree.ts:1095
+#define MT_KMAX 8               // max keys in one segment's property set
+#define MT_PREC (1 + 2 * MT_KMAX)
+#define MT_RSEQ_NONE ((int32_t)0x80000000)
+#define MT_MARKER_BIT 0x80000000u
+#define MT_SCOUR_UNDEF ((int8_t)-1)
+
+typedef unsigned long long u64;
+
+struct DocHdr {               // 128 bytes per document
+    int32_t n_seg, depth, heap_n, cur_seq;
+    int32_t min_seq, text_top, text_half, props_top;
+    int32_t props_half, next_uid, status, dlog_n;
+    int32_t n_blk[MT_LV];
+    u64 delta_hash;
+    int32_t n_ops, pad0;
+    int32_t pad[8];
+};
+static_assert(sizeof(DocHdr) == 128, "DocHdr size");
+
+struct DevState {
+    DocHdr *hdr;
+    int4 *segA;
+    u64 *segO;
+    uint4 *segB;
+    uint8_t *cnt;
+    int8_t *flg;
+    int2 *heap;
+    uint16_t *text;
+    uint32_t *props;
+    int32_t *dlog;
+    int32_t S, B, H, T, P, DL;
+    int32_t n_docs;
+};
+
+// ------------------------------------------------------------------ wave primitives
+__device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+
+__device__ __forceinline__ int wave_scan_incl(int v) {
+    const int L = lane();
+#pragma unroll
+    for (int o = 1; o < MT_WAVE; o <<= 1) {
+        int t = __shfl_up(v, o, MT_WAVE);
+        if (L >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, MT_WAVE);
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, MT_WAVE));
+    return v;
+}
+__device__ __forceinline__ int bcast(int v, int l) { return __shfl(v, l, MT_WAVE); }
+__device__ __forceinline__ u64 bcast64(u64 v, int l) {
+    uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, MT_WAVE);
+    uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, MT_WAVE);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 ballot(bool p) { return (u64)__ballot(p); }
+__device__ __forceinline__ int first_lane(u64 m) { return __ffsll((long long)m) - 1; }
+
+// ------------------------------------------------------------------ hashing
+#define MT_FNV_OFF 1469598103934665603ULL
+#define MT_FNV_PRIME 1099511628211ULL
+__device__ __forceinline__ u64 fnv_u32(u64 h, uint32_t x) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        h ^= (x >> (8 * i)) & 0xFF;
+        h *= MT_FNV_PRIME;
+    }
+    return h;
+}
+__device__ __forceinline__ u64 fnv_u64(u64 h, u64 x) {
+    h = fnv_u32(h, (uint32_t)x);
+    return fnv_u32(h, (uint32_t)(x >> 32));
+}
+
+// ------------------------------------------------------------------ segment fields
+__device__ __forceinline__ int seg_cli(int4 a) { return (int)(short)(a.w & 0xFFFF); }
+__device__ __forceinline__ int seg_rcli(int4 a) { return (int)(short)((uint32_t)a.w >> 16); }
+__device__ __forceinline__ int pack_cli(int cli, int rcli) {
+    return (int)(((uint32_t)(uint16_t)cli) | (((uint32_t)(uint16_t)rcli) << 16));
+}
+__device__ __forceinline__ bool ovl_has(u64 o, int c) {
+    return c >= 1 && c <= 64 && ((o >> (c - 1)) & 1ull);
+}
+
+// nodeLength for a leaf in a remote view (c, r)   MT/mergeTree.ts:1692-1732
+__device__ __forceinline__ int view_len(int4 a, u64 o, int r, int c) {
+    const int len = a.x, seq = a.y, rseq = a.z;
+    const bool ins = (seg_cli(a) == c) || (seq != -1 && seq <= r);
+    if (!ins) return 0;
+    if (rseq != MT_RSEQ_NONE) {
+        if (seg_rcli(a) == c || ovl_has(o, c) || (rseq != -1 && rseq <= r)) return 0;
+    }
+    return len;
+}
+// localNetLength (observer view)   MT/mergeTree.ts:1195-1206
+__device__ __forceinline__ int obs_len(int4 a) { return a.z == MT_RSEQ_NONE ? a.x : 0; }
+// breakTie for a leaf at pos == len == 0, remote client   MT/mergeTree.ts:2281-2306
+__device__ __forceinline__ bool tie(int4 a, int r) {
+    const int rs = a.z;
+    return !(rs != MT_RSEQ_NONE && rs != 0 && rs <= r && rs != -1) && a.y != -1;
+}

@@ -1,0 +1,132 @@
+/*
+ * mt_replay.h -- C-ABI drop-in boundary of the MI355X merge-tree replay backend.
+ *
+ * The reference has no FFI: its boundary is the TypeScript class `Client`
+ * (packages/dds/merge-tree/src/client.ts:43), constructed once per SharedString by
+ * SharedSegmentSequence (packages/dds/sequence/src/sequence.ts:131-134) and fed one
+ * sequenced message at a time through Client.applyMsg (client.ts:797-819).  This library
+ * replaces N such observer Clients with one handle that owns N documents resident in HBM
+ * and applies whole batches of sequenced messages per document in HIP kernels.  The
+ * binding a maintainer adds on the reference side is the N-API addon in
+ * fluidframework_amd/js/ (INTEGRATION.md shows it); ctypes (Python) binds the same symbols.
+ *
+ * Conventions: every function returns 0 on success or a negative MT_E_* code; the text of
+ * the last error is available from mt_last_error().  Per-document failures (the
+ * reference's throws / asserts, enum mt_doc_status in mt_types.h) do not fail the call:
+ * the document is marked and skipped by later batches, other documents continue.
+ * A handle is single-writer; calls are synchronous unless named *_async.
+ */
+#ifndef MT_REPLAY_H
+#define MT_REPLAY_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MT_E_INVALID (-1)    /* bad argument */
+#define MT_E_HIP (-2)        /* HIP runtime error */
+#define MT_E_NOMEM (-3)      /* device allocation failed */
+#define MT_E_NODEVICE (-4)   /* no HIP device visible: the product has no CPU fallback */
+
+typedef struct mt_handle mt_handle;
+typedef struct mt_batch mt_batch;
+
+/* Per-document capacities (0 = default).  Exceeding one marks that document
+   MT_DOC_CAPACITY; the host may re-run it with larger capacities. */
+typedef struct mt_options {
+    int32_t device;          /* HIP device ordinal (one process per GPU) */
+    int32_t seg_capacity;    /* leaf segments per document          (default 2048) */
+    int32_t block_capacity;  /* blocks per tree level per document  (default seg/2) */
+    int32_t heap_capacity;   /* zamboni LRU heap entries            (default 2*seg) */
+    int32_t text_capacity;   /* UTF-16 units per document text arena half (default 32768) */
+    int32_t props_capacity;  /* property-set records per document   (default seg) */
+    int32_t delta_log_capacity; /* int32 words of per-document delta log; 0 = hash only */
+} mt_options;
+
+/* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the
+   probabilities are thresholds floor(p * 2^32) compared against a u32 draw. */
+typedef struct mt_gen_cfg {
+    uint32_t seed;
+    int32_t ops, writers, lag, seed_len, text_max, n_keys, n_values, max_keys_per_op;
+    int32_t _pad;
+    uint64_t p_insert, p_insert_remove, p_newline, p_len_continue, p_insert_props, p_null;
+} mt_gen_cfg;
+
+/* Creates n_docs observer replicas (`new Client(...)` + startOrUpdateCollaboration,
+   client.ts:75-84, 1053-1073) on opt->device. */
+mt_handle *mt_create(uint32_t n_docs, const mt_options *opt);
+void mt_destroy(mt_handle *h);
+const char *mt_last_error(const mt_handle *h);
+uint32_t mt_num_docs(const mt_handle *h);
+
+/* Initial document contents, inserted before collaboration starts (seq 0, client
+   LocalClientId -- Client.insertSegmentLocal client.ts:202-215).  seed_off[n_docs+1]
+   indexes seed_text (UTF-16).  Resets every document. */
+int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *seed_text);
+
+/* Client.applyMsg for every message of a batch (client.ts:797-819).  Records are grouped
+   per document in sequence order: doc_op_off[n_docs+1] indexes ops.  Host buffers; the
+   call uploads, applies and synchronises. */
+int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, uint64_t n_ops,
+                 const uint16_t *text, uint64_t text_len, const uint32_t *props,
+                 uint64_t props_len);
+
+/* Device-resident batches (bench / pipelined path). */
+mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops,
+                          uint64_t n_ops, const uint16_t *text, uint64_t text_len,
+                          const uint32_t *props, uint64_t props_len);
+int mt_batch_apply_async(mt_handle *h, const mt_batch *b);   /* enqueue on the handle's stream */
+uint64_t mt_batch_num_ops(const mt_batch *b);
+void mt_batch_free(mt_batch *b);
+int mt_sync(mt_handle *h);
+/* Device time of the most recent replay kernel (HIP events on the handle's stream). */
+float mt_last_kernel_ms(const mt_handle *h);
+
+/* Generates ops_per_doc synthetic messages per document on the device, applying them as
+   it goes (the generator reads each writer's view length from the live replica), and
+   returns them as a device-resident batch.  Documents end in the generated final state;
+   call mt_load_initial_text again to replay the batch from scratch. */
+mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
+                      int32_t *view_len_trace /* nullable host [n_docs*ops*4] diagnostic:
+                                                 per op {view length, n_seg, refSeq,
+                                                 client} */);
+/* Initial seed texts as the generator draws them (seed_off[n_docs+1], seed_text). */
+int mt_generated_seeds(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
+                       int64_t *seed_off, uint16_t *seed_text);
+/* Copies a batch back to the host (arrays sized by mt_batch_sizes). */
+int mt_batch_sizes(const mt_batch *b, uint64_t *n_ops, uint64_t *text_len, uint64_t *props_len);
+int mt_batch_download(const mt_batch *b, int64_t *doc_op_off, mt_op_rec *ops, uint16_t *text,
+                      uint32_t *props);
+
+/* ---- read-out (MergeTree.length client.ts:1051; getText textSegment.ts:154-172;
+        getPropertiesAtPosition client.ts:1011-1025) ---- */
+int mt_get_status(mt_handle *h, int32_t *out_status);                 /* [n_docs] */
+int mt_get_length(mt_handle *h, uint32_t doc, uint32_t *out);
+int mt_get_text(mt_handle *h, uint32_t doc, uint16_t *out, uint32_t cap, uint32_t *out_len);
+/* Observer-visible property runs: rows of (start, length, props_record_index) plus the
+   records [count, (key, value)*].  Returns counts through the out pointers. */
+int mt_get_prop_runs(mt_handle *h, uint32_t doc, uint32_t *runs, uint32_t cap_runs,
+                     uint32_t *n_runs, uint32_t *records, uint32_t cap_words,
+                     uint32_t *n_words);
+/* Diagnostic: segment rows of 8 int32 (len, seq, client, rseq, rclient, n_overlap,
+   marker refType or -1, has_props) in document order, and the leaf-block partition. */
+int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows,
+                    uint32_t *n_rows, int32_t *leaves, uint32_t cap_leaves, uint32_t *n_leaves);
+int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_t *pairs,
+                         uint32_t cap_pairs, int32_t *n_pairs);
+/* Delta log (only with delta_log_capacity > 0), oracle layout. */
+int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uint32_t *n);
+
+/* Per-document checksums (mt_types.h), to host memory or straight into device memory
+   on the handle's device (e.g. a torch tensor's data_ptr() before an RCCL all-gather). */
+int mt_checksums(mt_handle *h, mt_checksum *out);
+int mt_checksums_device(mt_handle *h, void *device_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

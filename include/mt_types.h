@@ -60,9 +60,10 @@ typedef struct mt_op_rec {
 typedef struct mt_checksum {
     uint32_t length;     /* observer length, MergeTree.length MT/mergeTree.ts:1617 */
     uint32_t n_segments; /* live leaf segments (diagnostic, tree-shape dependent) */
-    uint64_t text_hash;  /* FNV-1a 64 over the UTF-16LE text (getText, MT/textSegment.ts:154) */
+    uint64_t text_hash;  /* chunked FNV-1a 64 of the getText() string (MT/textSegment.ts:154) */
     uint64_t props_hash; /* FNV-1a 64 over the observer-visible property runs */
     uint64_t delta_hash; /* FNV-1a 64 over every mergeTreeDeltaCallback record */
+    /* exact definitions: DESIGN.md "Checksums"; restated in oracle/mt_oracle.c */
 } mt_checksum;
 
 /* Per-document status codes (mt_doc_status). */
@@ -72,7 +73,8 @@ enum mt_doc_status {
     MT_DOC_SEQ_ORDER = 2,       /* assert currentSeq < seq     MT/client.ts:462-463 */
     MT_DOC_MINSEQ_ORDER = 3,    /* assert minSeq <= msn        MT/client.ts:464-465 */
     MT_DOC_CAPACITY = 4,        /* a per-document capacity was exceeded */
-    MT_DOC_UNSUPPORTED = 5      /* combining op other than rewrite */
+    MT_DOC_UNSUPPORTED = 5,     /* combining op other than rewrite */
+    MT_DOC_INTERNAL = 6         /* engine invariant violated (bug) */
 };
 
 #ifdef __cplusplus

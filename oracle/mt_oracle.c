@@ -535,11 +535,19 @@ typedef struct DeltaSeg {
     uint32_t *pd;   /* (key, old) pairs */
 } DeltaSeg;
 
+static inline uint64_t fnv_u64(uint64_t h, uint64_t x) {
+    h = fnv_u32(h, (uint32_t)x);
+    return fnv_u32(h, (uint32_t)(x >> 32));
+}
+
+/* Delta hash (DESIGN.md "Checksums"), streamable so the GPU can fold lane-parallel:
+     seg_hash = FNV(pos, len [, (key, old)*, npd])            per delta segment
+     cb       = FNV(seq, kind) <- seg_hash_0 .. seg_hash_{n-1} <- n   per callback
+     H        = fnv_u64(H, cb)                                  per document */
 static void emit_deltas(orc_doc *d, int32_t seq, int kind, DeltaSeg *ds, int n) {
-    uint64_t h = d->delta_hash;
-    h = fnv_u32(h, (uint32_t)seq);
-    h = fnv_u32(h, (uint32_t)kind);
-    h = fnv_u32(h, (uint32_t)n);
+    uint64_t cb = FNV_OFF;
+    cb = fnv_u32(cb, (uint32_t)seq);
+    cb = fnv_u32(cb, (uint32_t)kind);
     if (d->record) {
         ivec_push(&d->dlog, seq);
         ivec_push(&d->dlog, kind);
@@ -548,26 +556,29 @@ static void emit_deltas(orc_doc *d, int32_t seq, int kind, DeltaSeg *ds, int n) 
     for (int i = 0; i < n; i++) {
         Seg *s = ds[i].seg;
         int32_t pos = s->n.parent ? get_position(&s->n) : -1;
-        h = fnv_u32(h, (uint32_t)pos);
-        h = fnv_u32(h, (uint32_t)s->len);
+        uint64_t sh = FNV_OFF;
+        sh = fnv_u32(sh, (uint32_t)pos);
+        sh = fnv_u32(sh, (uint32_t)s->len);
         if (d->record) {
             ivec_push(&d->dlog, pos);
             ivec_push(&d->dlog, s->len);
         }
         if (kind == MT_OP_ANNOTATE) {
-            h = fnv_u32(h, (uint32_t)ds[i].npd);
             if (d->record) ivec_push(&d->dlog, ds[i].npd);
             for (int j = 0; j < ds[i].npd; j++) {
-                h = fnv_u32(h, ds[i].pd[2 * j]);
-                h = fnv_u32(h, ds[i].pd[2 * j + 1]);
+                sh = fnv_u32(sh, ds[i].pd[2 * j]);
+                sh = fnv_u32(sh, ds[i].pd[2 * j + 1]);
                 if (d->record) {
                     ivec_push(&d->dlog, (int32_t)ds[i].pd[2 * j]);
                     ivec_push(&d->dlog, (int32_t)ds[i].pd[2 * j + 1]);
                 }
             }
+            sh = fnv_u32(sh, (uint32_t)ds[i].npd);
         }
+        cb = fnv_u64(cb, sh);
     }
-    d->delta_hash = h;
+    cb = fnv_u32(cb, (uint32_t)n);
+    d->delta_hash = fnv_u64(d->delta_hash, cb);
 }
 
 /* ------------------------------------------------------------------ nodeMap */
@@ -889,7 +900,7 @@ int32_t orc_leaves(orc_doc *d, int32_t *out, int32_t cap) {
 }
 
 typedef struct SumAcc {
-    uint64_t th, ph;
+    uint64_t ph;
     uint32_t len, nseg;
     Seg *run;          /* current props run representative */
     int32_t run_len;
@@ -902,6 +913,8 @@ static int same_ordered(const Props *a, const Props *b) {
         if (a->key[i] != b->key[i] || a->val[i] != b->val[i]) return 0;
     return 1;
 }
+/* props hash: FNV over maximal runs of observer-visible segments with identical
+   (ordered) property sets: (len, has, n, (key, val)*) per run. */
 static uint64_t fold_run(uint64_t h, const Props *p, int32_t len) {
     h = fnv_u32(h, (uint32_t)len);
     h = fnv_u32(h, p ? 1u : 0u);
@@ -919,14 +932,6 @@ static void sum_fn(Seg *s, void *arg) {
     a->nseg++;
     if (s->rseq != RSEQ_NONE) return;
     a->len += s->len;
-    if (s->marker < 0) {
-        for (int i = 0; i < s->len; i++) {
-            a->th ^= s->text[i] & 0xFF;
-            a->th *= FNV_PRIME;
-            a->th ^= s->text[i] >> 8;
-            a->th *= FNV_PRIME;
-        }
-    }
     if (a->have && same_ordered(a->run->props, s->props)) {
         a->run_len += s->len;
     } else {
@@ -936,18 +941,37 @@ static void sum_fn(Seg *s, void *arg) {
         a->have = 1;
     }
 }
+/* text hash: H = FNV(n) folded with h_k = FNV-1a over the UTF-16LE bytes of characters
+   [64k, 64k+64) of the getText() string (markers contribute nothing). */
+uint64_t orc_text_hash(const uint16_t *t, int32_t n) {
+    uint64_t h = fnv_u32(FNV_OFF, (uint32_t)n);
+    for (int32_t k = 0; k < n; k += 64) {
+        uint64_t hk = FNV_OFF;
+        for (int32_t i = k; i < n && i < k + 64; i++) {
+            hk ^= t[i] & 0xFF;
+            hk *= FNV_PRIME;
+            hk ^= t[i] >> 8;
+            hk *= FNV_PRIME;
+        }
+        h = fnv_u64(h, hk);
+    }
+    return h;
+}
 void orc_checksum(orc_doc *d, mt_checksum *out) {
     SumAcc a;
     memset(&a, 0, sizeof(a));
-    a.th = FNV_OFF;
     a.ph = FNV_OFF;
     walk_segs(&d->root->n, sum_fn, &a);
     if (a.have) a.ph = fold_run(a.ph, a.run->props, a.run_len);
+    int32_t n = orc_text(d, NULL, 0);
+    uint16_t *t = (uint16_t *)malloc(sizeof(uint16_t) * (n > 0 ? n : 1));
+    orc_text(d, t, n);
     out->length = a.len;
     out->n_segments = a.nseg;
-    out->text_hash = a.th;
+    out->text_hash = orc_text_hash(t, n);
     out->props_hash = a.ph;
     out->delta_hash = d->delta_hash;
+    free(t);
 }
 int32_t orc_deltas(orc_doc *d, int32_t *out, int32_t cap) {
     for (int64_t i = 0; i < d->dlog.n && i < cap; i++) out[i] = d->dlog.p[i];
@@ -955,6 +979,8 @@ int32_t orc_deltas(orc_doc *d, int32_t *out, int32_t cap) {
 }
 
 /* ------------------------------------------------------------------ generator */
+static __thread int32_t *g_trace = NULL;
+void orc_set_gen_trace(int32_t *trace) { g_trace = trace; }
 typedef struct Rng {
     uint32_t s[4];
 } Rng;
@@ -1040,6 +1066,7 @@ int32_t orc_generate(const orc_gen_cfg *cfg_in, int32_t doc, mt_op_rec *ops, int
         if (!short_id[k]) short_id[k] = next_short++;
         int32_t c = short_id[k];
         int32_t len = orc_view_length(d, r, c);
+        if (g_trace) g_trace[t - 1] = len;
         uint32_t u = rng_next(&rng);
         if (n >= ops_cap) goto fail;
         mt_op_rec *op = &ops[n];

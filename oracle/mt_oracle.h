@@ -40,6 +40,7 @@ int32_t orc_leaves(orc_doc *d, int32_t *out, int32_t cap);
    segment has no property object; writes (key, value) pairs */
 int32_t orc_segment_props(orc_doc *d, int32_t seg_index, uint32_t *out, int32_t cap_pairs);
 void orc_checksum(orc_doc *d, mt_checksum *out);
+uint64_t orc_text_hash(const uint16_t *t, int32_t n);
 /* delta log: flattened records  [seq, kind, nsegs, (pos, len, ndeltas, (key, oldval)*)*]* */
 int32_t orc_deltas(orc_doc *d, int32_t *out, int32_t cap);
 void orc_set_record_deltas(orc_doc *d, int32_t on);
@@ -50,6 +51,8 @@ int32_t orc_generate(const orc_gen_cfg *cfg, int32_t doc, mt_op_rec *ops, int32_
                      uint16_t *text, int32_t text_cap, int32_t *text_used,
                      uint32_t *props, int32_t props_cap, int32_t *props_used,
                      uint16_t *seed_out, int32_t *seed_len_out, orc_doc **keep);
+
+void orc_set_gen_trace(int32_t *trace);   /* per-op writer view lengths (diagnostic) */
 
 /* Replay a CSR batch of documents on `threads` host threads; fills checksum/status. */
 int32_t orc_replay_batch(int32_t n_docs, const int64_t *doc_op_off, const mt_op_rec *ops,

@@ -1,0 +1,106 @@
+"""HIP path vs the reference (golden fixtures made by the reference itself) and vs the CPU
+oracle, through the C ABI.  Bit-exact on every output: text, length, leaf-block partition,
+segment table, property sets, every delta-callback record, checksums."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_batch(n_docs, **kw):
+    from fluidframework_amd import MergeTreeBatch
+    kw.setdefault("delta_log_capacity", 1 << 18)
+    kw.setdefault("seg_capacity", 4096)
+    kw.setdefault("text_capacity", 1 << 17)
+    return MergeTreeBatch(n_docs, **kw)
+
+
+def _gpu_outputs(mt, doc):
+    rows, leaves = mt.get_segments(doc)
+    return dict(text=mt.get_text(doc), length=mt.get_length(doc), leaves=leaves, segs=rows,
+                seg_props=[mt.get_segment_props(doc, i) for i in range(len(rows))],
+                deltas=mt.get_delta_log(doc), status=int(mt.status()[doc]))
+
+
+@pytest.mark.parametrize("name", gu.ALL_FIXTURES)
+def test_gpu_matches_reference(name):
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]))
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, f"{name}: {bad[:4]}"
+
+
+@pytest.mark.parametrize("name", ["ref_c3", "ref_ext", "ref_ext_long"])
+def test_gpu_checksums_match_oracle(oracle_lib, name):
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]))
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    sums = mt.checksums()
+    osums, ost = oracle_lib.replay_batch(a, threads=2)
+    assert (ost == 0).all()
+    for f in ("length", "text_hash", "props_hash", "delta_hash", "n_segments"):
+        assert np.array_equal(sums[f], osums[f]), f
+
+
+def test_gpu_split_batches_equal_single_batch(oracle_lib):
+    """Applying a document's messages in several calls equals one call (state persists)."""
+    fx = gu.load("ref_c2")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt1 = _gpu_batch(len(fx["docs"]))
+    mt1.load_initial_text(a["seed_off"], a["seed"])
+    mt1.apply_arrays(a)
+    mt2 = _gpu_batch(len(fx["docs"]))
+    mt2.load_initial_text(a["seed_off"], a["seed"])
+    off = a["doc_off"]
+    for lo_frac, hi_frac in ((0.0, 0.3), (0.3, 0.31), (0.31, 1.0)):
+        sel, noff = [], [0]
+        for d in range(len(off) - 1):
+            n = off[d + 1] - off[d]
+            lo, hi = off[d] + int(n * lo_frac), off[d] + int(n * hi_frac)
+            sel.append(np.arange(lo, hi))
+            noff.append(noff[-1] + hi - lo)
+        idx = np.concatenate(sel)
+        mt2.apply_arrays(dict(a, ops=a["ops"][idx], doc_off=np.asarray(noff, dtype=np.int64)))
+    s1, s2 = mt1.checksums(), mt2.checksums()
+    assert np.array_equal(s1, s2)
+
+
+@pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6)])
+def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs):
+    import json
+    import os
+    cfg = json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))[cfgname]
+    cfg = dict(cfg, ops=ops)
+    mt = _gpu_batch(docs)
+    b = mt.generate(cfg)
+    got = b.download()
+    gsums = mt.checksums()
+    for d in range(docs):
+        g = oracle_lib.generate(cfg, d, keep=True)
+        lo, hi = got["doc_off"][d], got["doc_off"][d + 1]
+        ops_d = got["ops"][lo:hi].copy()
+        assert np.array_equal(ops_d[["seq", "ref_seq", "min_seq", "pos1", "pos2", "client", "kind"]],
+                              g["ops"][["seq", "ref_seq", "min_seq", "pos1", "pos2", "client", "kind"]]), d
+        osum = g["doc"].outputs()["checksum"]
+        for f in ("length", "text_hash", "props_hash", "delta_hash"):
+            assert gsums[d][f] == osum[f], (d, f)
+    # replaying the generated batch from the seeds reproduces the same final state
+    seed_off, seed = mt.generated_seeds(cfg)
+    mt.load_initial_text(seed_off, seed)
+    b.apply_async()
+    mt.sync()
+    assert np.array_equal(mt.checksums(), gsums)
