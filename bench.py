@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: sequenced merge-tree ops applied per second on MI355X (BASELINE.json metric).
+
+One *step* = replaying one batch of synthetic sequenced messages through the observer
+replicas of every document on the GPU (Client.applyMsg semantics, bit-exact with the
+reference), starting from the documents' initial contents.  At N=1 the workload is
+BASELINE.json configs[1] (C2): 10k documents x 2k ops, 4 writers, refSeq lag <= 32,
+insert 0.6 / remove 0.4.  With N ranks every rank replays its own 10k-document shard
+(weak scaling; documents are independent, so there is no data-path collective); the only
+collective is an RCCL all-gather of per-document checksums after the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--docs D] [--ops O]
+
+Inputs are generated on the GPU (untimed) and stay resident in HBM; the timed region is
+reset + replay kernels only.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s
+SEG_BYTES = 40             # segA 16 + segO 8 + segB 16
+OP_BYTES = 32              # mt_op_rec
+PROFILE_PMC = os.path.join(REPO, "profiles", "pmc_summary.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: config)")
+    ap.add_argument("--ops", type=int, default=0, help="ops per document (default: config)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample-docs", type=int, default=0, help="0 = all docs of rank 0")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def capacities(cfg):
+    """Per-document capacities sized for the workload (DESIGN.md 'HBM layout')."""
+    if cfg["writers"] > 8 or cfg["lag"] > 64:
+        return dict(seg_capacity=8192, text_capacity=1 << 16, heap_capacity=8192, props_capacity=8192 + 256)
+    if cfg["ops"] > 4000:
+        return dict(seg_capacity=1024, text_capacity=1 << 15, heap_capacity=2048, props_capacity=1024 + 128)
+    return dict(seg_capacity=512, text_capacity=1 << 14, heap_capacity=1024, props_capacity=512 + 128)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from fluidframework_amd import MergeTreeBatch
+    configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
+    cfg = dict(configs[args.config])
+    docs = args.docs or (cfg["docs"] if args.config == "c2" else min(cfg["docs"], 16384))
+    if args.ops:
+        cfg["ops"] = args.ops
+    doc_base = rank * docs
+
+    mt = MergeTreeBatch(docs, device=local_rank, **capacities(cfg))
+    t_gen = time.time()
+    batch = mt.generate(cfg, doc_base)              # untimed: inputs resident in HBM
+    gen_sums = mt.checksums()
+    t_gen = time.time() - t_gen
+    seed_off, seed = mt.generated_seeds(cfg, doc_base)
+    mt.load_initial_text(seed_off, seed)
+    n_ops = batch.n_ops
+
+    def step():
+        mt.reset()
+        batch.apply_async()
+
+    for _ in range(args.warmup):
+        step()
+        mt.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    kernel_ms = []
+    barrier()
+    mt.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        mt.sync()                     # per-step sync to read this step's kernel events
+        kernel_ms.append(mt.last_kernel_ms())
+    mt.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    status = mt.status()
+    sums = mt.checksums()
+    replay_consistent = bool(np.array_equal(sums, gen_sums)) and int((status != 0).sum()) == 0
+
+    # the only collective: all-gather of per-document checksums over RCCL/xGMI
+    digest = None
+    if dist is not None:
+        import torch
+        local = torch.empty(docs * 32, dtype=torch.uint8, device="cuda")
+        mt.checksums_device(local.data_ptr())
+        gathered = torch.empty(world * docs * 32, dtype=torch.uint8, device="cuda")
+        dist.all_gather_into_tensor(gathered, local)
+        g = gathered.cpu().numpy().view(np.uint64)
+        digest = int(np.bitwise_xor.reduce(g))
+        ok = torch.tensor([1 if replay_consistent else 0], device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        replay_consistent = bool(ok.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    total_ops = n_ops * world
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = total_ops * args.steps / elapsed
+
+    # roofline: algorithmic bytes per launch (DESIGN.md "Roofline accounting")
+    host = batch.download()
+    ins = host["ops"]["kind"] == 0
+    payload_chars = int(host["ops"]["pos2"][ins].sum())
+    final_bytes = int(sums["n_segments"].astype(np.int64).sum()) * SEG_BYTES + 2 * int(sums["length"].astype(np.int64).sum())
+    alg_bytes = n_ops * OP_BYTES + 2 * payload_chars + final_bytes
+    k_ms = float(np.mean(kernel_ms))
+    achieved = alg_bytes / (k_ms / 1000.0)
+    traffic = None
+    if os.path.exists(PROFILE_PMC):
+        try:
+            pm = json.load(open(PROFILE_PMC))
+            if pm.get("config") == args.config and pm.get("docs") == docs and pm.get("ops") == cfg["ops"]:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    parity = None
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import pyoracle                            # the checker, timed as the CPU baseline
+        n_sample = args.cpu_sample_docs or docs
+        off = host["doc_off"]
+        sel_end = int(off[n_sample])
+        arrays = dict(ops=host["ops"][:sel_end], doc_off=off[: n_sample + 1], text=host["text"],
+                      props=host["props"], seed_off=seed_off[: n_sample + 1], seed=seed)
+        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        t_c = time.perf_counter()
+        osums, ost = pyoracle.replay_batch(arrays, threads=threads)
+        t_c = time.perf_counter() - t_c
+        cpu = dict(value=round(sel_end / t_c, 1), unit="ops/s", cores=threads, kind="port",
+                   sample=f"oracle/mt_oracle.c replay of rank-0 docs [0,{n_sample}) of the same "
+                          f"{args.config} batch ({sel_end} ops) on {threads} host threads, {t_c:.2f} s")
+        parity = dict(docs_checked=n_sample,
+                      mismatches=int((osums != sums[:n_sample]).sum() + (ost != 0).sum()))
+
+    out = {
+        "metric": "sequenced merge-tree ops applied/sec (node) at 100k docs; bit-exact text+props",
+        "value": round(value, 1),
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.config}: {docs} docs/GPU x {cfg['ops']} sequenced ops, {cfg['writers']} writers, "
+                        f"refSeq lag <= {cfg['lag']}, insert {cfg['p_insert']} / remove {cfg['p_remove']}"
+                        f"{' / annotate ' + str(round(1 - cfg['p_insert'] - cfg['p_remove'], 3)) if cfg['p_insert'] + cfg['p_remove'] < 1 else ''}",
+            "docs_total": docs * world, "ops_per_doc": cfg["ops"], "ops_per_step": total_ops,
+            "parallelism": f"doc-shard x{world}",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic,
+            "kernel": "k_replay", "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
+        },
+        "cpu_baseline": cpu,
+        "parity": {"replay_equals_generation": replay_consistent, "oracle_sample": parity,
+                   "checksum_allgather_digest": digest},
+        "gen_s": round(t_gen, 2),
+    }
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -54,6 +54,10 @@ class MergeTreeBatch:
         self._check(self.lib.mt_load_initial_text(self.h, _native.ptr(seed_off), _native.ptr(seed)),
                     "mt_load_initial_text")
 
+    def reset(self):
+        """Asynchronously re-initialise every document from the loaded initial contents."""
+        self._check(self.lib.mt_reset(self.h), "mt_reset")
+
     def apply_arrays(self, a):
         ops = np.ascontiguousarray(a["ops"], dtype=OP_DTYPE)
         off = np.ascontiguousarray(a["doc_off"], dtype=np.int64)

@@ -344,8 +344,11 @@ struct mt_handle {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
+    bool timed = false;      // ev0/ev1 bracket a launch not yet read by mt_sync
     std::string err;
     mt_checksum *d_sums = nullptr;
+    int64_t *d_seed_off = nullptr;   // initial contents kept on device for mt_reset
+    uint16_t *d_seed = nullptr;
 };
 struct mt_batch {
     int device = 0;
@@ -426,7 +429,8 @@ void mt_destroy(mt_handle *h) {
     if (!h) return;
     hipSetDevice(h->device);
     DevState &st = h->st;
-    void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums};
+    void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
+                  h->d_seed_off, h->d_seed};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -441,21 +445,30 @@ uint32_t mt_num_docs(const mt_handle *h) { return h ? h->n_docs : 0; }
 int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *seed_text) {
     if (!h) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    int64_t *d_off = nullptr;
-    uint16_t *d_seed = nullptr;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->d_seed_off) hipFree(h->d_seed_off);
+    if (h->d_seed) hipFree(h->d_seed);
+    h->d_seed_off = nullptr;
+    h->d_seed = nullptr;
     if (seed_off) {
         const size_t n = seed_off[h->n_docs];
-        HIPCHK(h, hipMalloc(&d_off, (h->n_docs + 1) * sizeof(int64_t)));
-        HIPCHK(h, hipMalloc(&d_seed, std::max<size_t>(n, 1) * sizeof(uint16_t)));
-        HIPCHK(h, hipMemcpyAsync(d_off, seed_off, (h->n_docs + 1) * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-        if (n) HIPCHK(h, hipMemcpyAsync(d_seed, seed_text, n * sizeof(uint16_t), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMalloc(&h->d_seed_off, (h->n_docs + 1) * sizeof(int64_t)));
+        HIPCHK(h, hipMalloc(&h->d_seed, std::max<size_t>(n, 1) * sizeof(uint16_t)));
+        HIPCHK(h, hipMemcpy(h->d_seed_off, seed_off, (h->n_docs + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+        if (n) HIPCHK(h, hipMemcpy(h->d_seed, seed_text, n * sizeof(uint16_t), hipMemcpyHostToDevice));
     }
-    if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
-    hipLaunchKernelGGL(k_init, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, d_off, d_seed);
-    HIPCHK(h, hipGetLastError());
+    int rc = mt_reset(h);
+    if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    if (d_off) hipFree(d_off);
-    if (d_seed) hipFree(d_seed);
+    return 0;
+}
+
+int mt_reset(mt_handle *h) {
+    if (!h) return MT_E_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
+    hipLaunchKernelGGL(k_init, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, h->d_seed_off, h->d_seed);
+    HIPCHK(h, hipGetLastError());
     return 0;
 }
 
@@ -496,6 +509,7 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
                        b->ops, b->off, b->text, b->props);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    h->timed = true;
     return 0;
 }
 
@@ -515,8 +529,12 @@ int mt_sync(mt_handle *h) {
     if (!h) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
+    if (h->timed) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
+        (void)hipGetLastError();   // never leave a sticky error for the next launch check
+        h->timed = false;
+    }
     return 0;
 }
 

@@ -67,6 +67,9 @@ uint32_t mt_num_docs(const mt_handle *h);
    LocalClientId -- Client.insertSegmentLocal client.ts:202-215).  seed_off[n_docs+1]
    indexes seed_text (UTF-16).  Resets every document. */
 int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *seed_text);
+/* Re-initialises every document from the contents last given to mt_load_initial_text
+   (kept in HBM); asynchronous on the handle's stream. */
+int mt_reset(mt_handle *h);
 
 /* Client.applyMsg for every message of a batch (client.ts:797-819).  Records are grouped
    per document in sequence order: doc_op_off[n_docs+1] indexes ops.  Host buffers; the
