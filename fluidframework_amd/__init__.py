@@ -23,10 +23,11 @@ class MergeTreeBatch:
     """
 
     def __init__(self, n_docs, device=0, seg_capacity=0, block_capacity=0, heap_capacity=0,
-                 text_capacity=0, props_capacity=0, delta_log_capacity=0):
+                 text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
-                                text_capacity, props_capacity, delta_log_capacity)
+                                text_capacity, props_capacity, delta_log_capacity,
+                                lds_seg_capacity)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")

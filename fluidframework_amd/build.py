@@ -10,7 +10,7 @@ DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", 
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mt_replay.h", "mt_types.h")]
 OUT = os.path.join(HERE, "libmtreplay.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-result",
+FLAGS = os.environ.get("MT_EXTRA_FLAGS", "").split() + ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-result",
          "-Wno-unused-value"]
 
 

@@ -32,8 +32,13 @@
 #define MT_RSEQ_NONE ((int32_t)0x80000000)
 #define MT_MARKER_BIT 0x80000000u
 #define MT_SCOUR_UNDEF ((int8_t)-1)
+#define MT_DOC_RETRY 100        // internal: document outgrew the LDS tier, replay it in HBM
 
 typedef unsigned long long u64;
+// clang ext-vector types (not HIP_vector_type): usable through LDS / global pointers
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 struct DocHdr {               // 128 bytes per document
     int32_t n_seg, depth, heap_n, cur_seq;
@@ -48,15 +53,16 @@ static_assert(sizeof(DocHdr) == 128, "DocHdr size");
 
 struct DevState {
     DocHdr *hdr;
-    int4 *segA;
+    v4i *segA;
     u64 *segO;
-    uint4 *segB;
+    v4u *segB;
     uint8_t *cnt;
     int8_t *flg;
-    int2 *heap;
+    v2i *heap;
     uint16_t *text;
     uint32_t *props;
     int32_t *dlog;
+    int32_t *retry;           // per document: replay this batch in the HBM tier
     int32_t S, B, H, T, P, DL;
     int32_t n_docs;
 };
@@ -109,29 +115,30 @@ __device__ __forceinline__ u64 fnv_u64(u64 h, u64 x) {
 }
 
 // ------------------------------------------------------------------ segment fields
-__device__ __forceinline__ int seg_cli(int4 a) { return (int)(short)(a.w & 0xFFFF); }
-__device__ __forceinline__ int seg_rcli(int4 a) { return (int)(short)((uint32_t)a.w >> 16); }
+__device__ __forceinline__ int seg_cli(v4i a) { return (int)(short)(a.w & 0xFFFF); }
+__device__ __forceinline__ int seg_rcli(v4i a) { return (int)(short)((uint32_t)a.w >> 16); }
 __device__ __forceinline__ int pack_cli(int cli, int rcli) {
     return (int)(((uint32_t)(uint16_t)cli) | (((uint32_t)(uint16_t)rcli) << 16));
 }
 __device__ __forceinline__ bool ovl_has(u64 o, int c) {
-    return c >= 1 && c <= 64 && ((o >> (c - 1)) & 1ull);
+    const uint32_t sh = (uint32_t)(c - 1) & 63u;
+    const uint32_t w = sh < 32 ? (uint32_t)o : (uint32_t)(o >> 32);
+    return (c >= 1) & (c <= 64) & (((w >> (sh & 31u)) & 1u) != 0);
 }
 
 // nodeLength for a leaf in a remote view (c, r)   MT/mergeTree.ts:1692-1732
-__device__ __forceinline__ int view_len(int4 a, u64 o, int r, int c) {
+// (branch-free: every term is evaluated, no shift depends on an unchecked c)
+__device__ __forceinline__ int view_len(v4i a, u64 o, int r, int c) {
     const int len = a.x, seq = a.y, rseq = a.z;
-    const bool ins = (seg_cli(a) == c) || (seq != -1 && seq <= r);
-    if (!ins) return 0;
-    if (rseq != MT_RSEQ_NONE) {
-        if (seg_rcli(a) == c || ovl_has(o, c) || (rseq != -1 && rseq <= r)) return 0;
-    }
-    return len;
+    const int cli = seg_cli(a), rcli = seg_rcli(a);
+    const bool ins = (cli == c) | ((seq != -1) & (seq <= r));
+    const bool gone = (rseq != MT_RSEQ_NONE) & ((rcli == c) | ovl_has(o, c) | ((rseq != -1) & (rseq <= r)));
+    return (ins & !gone) ? len : 0;
 }
 // localNetLength (observer view)   MT/mergeTree.ts:1195-1206
-__device__ __forceinline__ int obs_len(int4 a) { return a.z == MT_RSEQ_NONE ? a.x : 0; }
+__device__ __forceinline__ int obs_len(v4i a) { return a.z == MT_RSEQ_NONE ? a.x : 0; }
 // breakTie for a leaf at pos == len == 0, remote client   MT/mergeTree.ts:2281-2306
-__device__ __forceinline__ bool tie(int4 a, int r) {
+__device__ __forceinline__ bool tie(v4i a, int r) {
     const int rs = a.z;
-    return !(rs != MT_RSEQ_NONE && rs != 0 && rs <= r && rs != -1) && a.y != -1;
+    return !((rs != MT_RSEQ_NONE) & (rs != 0) & (rs <= r) & (rs != -1)) & (a.y != -1);
 }

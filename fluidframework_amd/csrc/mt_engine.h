@@ -1,77 +1,139 @@
 // mt_engine.h -- the per-document replay engine executed by one wavefront.
 //
 // Every function here is called by all 64 lanes with wave-uniform arguments; scalar
-// document state lives in the (uniform) Doc struct, the segment table in HBM, and the
-// B-tree counts in LDS.  The semantics follow the reference observer replica
-//  -- see oracle/mt_oracle.c for the function-by-function
-// restatement this engine is tested against.  Reference paths below are relative to
+// document state lives in the (uniform) Doc struct, the B-tree counts in LDS, and the
+// segment table + zamboni heap in the storage tier the engine is instantiated for:
+//
+//   TierLds  the whole segment table and heap are staged into LDS for the launch (the
+//            common case: C2 documents hold <= ~100 live segments).  A document that
+//            outgrows the LDS capacities is *not* written back: it is flagged for retry
+//            and the same batch is replayed for it by the TierGlb instantiation.
+//   TierGlb  the segment table and heap stay in HBM (fallback for large documents).
+//
+// Text and property records always live in HBM.  The semantics follow the reference
+// observer replica; oracle/mt_oracle.c is the function-by-function
+// CPU restatement this engine is tested against.  Reference paths below are relative to
 // /root/reference/packages/dds/merge-tree/src/ ("MT/").
 #pragma once
 #include "mt_device.h"
 
-#define WSYNC() __syncthreads()
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+struct TierLds {
+    static constexpr bool kLds = true;
+    typedef LDS_AS v4i *A_t;
+    typedef LDS_AS u64 *O_t;
+    typedef LDS_AS v4u *B_t;
+    typedef LDS_AS v2i *H_t;
+};
+struct TierGlb {
+    static constexpr bool kLds = false;
+    typedef GLB_AS v4i *A_t;
+    typedef GLB_AS u64 *O_t;
+    typedef GLB_AS v4u *B_t;
+    typedef GLB_AS v2i *H_t;
+};
+
+// Cross-lane ordering inside one wavefront.  LDS instructions of a wave execute in order,
+// so the LDS tier only needs the compiler not to reorder; global memory written by one
+// lane and read by another waits for the stores to complete.
+__device__ __forceinline__ void gsync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <class T> __device__ __forceinline__ void wsync() {
+    if constexpr (T::kLds)
+        asm volatile("" ::: "memory");
+    else
+        gsync();
+}
+
+// segB.w flags
+#define SEGF_NL_KNOWN 1u   // SEGF_NL is valid
+#define SEGF_NL 2u         // the segment's text ends with '\n' (TextSegment.canAppend :63-68)
 
 __device__ static const uint32_t kEmptyPropsRec = 0u;
 
-struct Doc {
-    DocHdr *hp;
-    int4 *A;
-    u64 *O;
-    uint4 *Bv;
-    uint8_t *gcnt;
-    int8_t *gflg;
-    int2 *heap;
-    uint16_t *text;
-    uint32_t *props;
-    int32_t *dlog;
+template <class T> struct DocT {
+    DocHdr *hp;   // generic: POD struct copies
+    typename T::A_t A;
+    typename T::O_t O;
+    typename T::B_t Bv;
+    typename T::H_t heap;
+    GLB_AS uint16_t *text;
+    GLB_AS uint32_t *props;
+    GLB_AS int32_t *dlog;
     int32_t S_cap, B_cap, H_cap, T_cap, P_cap, DL_cap;
     // LDS
-    uint8_t *cnt;      // [MT_LV][B_cap]
-    int8_t *flg;       // [B_cap]
-    uint16_t *ends;    // [B_cap] scratch: level-0 block end indices
-    int32_t *scr;      // small scratch (scour plans)
+    LDS_AS uint8_t *cnt;    // [MT_LV][B_cap]
+    LDS_AS int8_t *flg;     // [B_cap]
+    LDS_AS uint16_t *ends;  // [B_cap] scratch: level-0 block end indices
+    LDS_AS int32_t *scr;    // [64] scratch (scour plans)
+    LDS_AS int32_t *nb;     // [MT_LV] blocks per level
     // scalars (uniform)
     int n, depth, heap_n, cur_seq, min_seq, text_top, text_half, props_top, props_half, next_uid,
-        status, dlog_n;
-    int nb[MT_LV];
+        status, dlog_n, text_gcs, props_gcs;
     u64 dhash;
 };
 
-__device__ __forceinline__ void fail(Doc &d, int code) {
+#define TD template <class T> __device__ __forceinline__
+
+// Per-launch LDS layout of one document (host and device agree on it).
+struct LdsLayout {
+    uint32_t offA, offO, offB, offH, offCnt, offFlg, offEnds, offScr, offNb, offGen, total;
+};
+static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, int B, int H, int gen_words) {
+    LdsLayout L;
+    uint32_t o = 0;
+    if (seg_in_lds) {
+        L.offA = o; o += 16u * S;
+        L.offB = o; o += 16u * S;
+        L.offO = o; o += 8u * S;
+        L.offH = o; o += 8u * (H + 1);
+    } else {
+        L.offA = L.offB = L.offO = L.offH = 0;
+    }
+    L.offScr = o; o += 64u * 4;
+    L.offNb = o; o += MT_LV * 4;
+    L.offGen = o; o += 4u * gen_words;
+    L.offEnds = o; o += 2u * B;
+    L.offCnt = o; o += (uint32_t)MT_LV * B;
+    L.offFlg = o; o += (uint32_t)B;
+    L.total = (o + 15u) & ~15u;
+    return L;
+}
+
+TD void fail(DocT<T> &d, int code) {
     if (d.status == 0) d.status = code;
 }
-__device__ __forceinline__ uint8_t *lvl(Doc &d, int l) { return d.cnt + l * d.B_cap; }
-__device__ __forceinline__ uint16_t *text_base(Doc &d, int half) {
-    return d.text + (size_t)half * d.T_cap;
-}
-__device__ __forceinline__ uint32_t *prec(Doc &d, int half, uint32_t h) {
+// Out of a capacity: the LDS tier hands the document to the HBM tier, which reports it.
+TD void fail_cap(DocT<T> &d) { fail(d, T::kLds ? MT_DOC_RETRY : MT_DOC_CAPACITY); }
+
+TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) { return d.cnt + l * d.B_cap; }
+TD GLB_AS uint16_t *text_base(DocT<T> &d, int half) { return d.text + (size_t)half * d.T_cap; }
+TD GLB_AS uint32_t *prec(DocT<T> &d, int half, uint32_t h) {
     return d.props + ((size_t)half * d.P_cap + h) * MT_PREC;
 }
 
 // ------------------------------------------------------------------ load / store
-__device__ void load_doc(Doc &d, const DevState &st, int doc, uint8_t *smem) {
+// Binds the document's HBM state; for TierLds stages the segment table and heap into LDS.
+// Returns false (status MT_DOC_RETRY) when the document does not fit the LDS capacities.
+TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, const LdsLayout &L,
+                 int S_l, int B_l, int H_l) {
     const size_t S = st.S, B = st.B;
     d.hp = st.hdr + doc;
-    d.A = st.segA + doc * S;
-    d.O = st.segO + doc * S;
-    d.Bv = st.segB + doc * S;
-    d.gcnt = st.cnt + doc * (size_t)MT_LV * B;
-    d.gflg = st.flg + doc * B;
-    d.heap = st.heap + doc * (size_t)(st.H + 1);
-    d.text = st.text + doc * (size_t)2 * st.T;
-    d.props = st.props + doc * (size_t)2 * st.P * MT_PREC;
-    d.dlog = st.DL ? st.dlog + doc * (size_t)st.DL : nullptr;
-    d.S_cap = st.S;
-    d.B_cap = st.B;
-    d.H_cap = st.H;
+    d.text = (GLB_AS uint16_t *)(st.text + doc * (size_t)2 * st.T);
+    d.props = (GLB_AS uint32_t *)(st.props + doc * (size_t)2 * st.P * MT_PREC);
+    d.dlog = st.DL ? (GLB_AS int32_t *)(st.dlog + doc * (size_t)st.DL) : nullptr;
     d.T_cap = st.T;
     d.P_cap = st.P;
     d.DL_cap = st.DL;
-    d.cnt = smem;
-    d.flg = (int8_t *)(smem + MT_LV * st.B);
-    d.ends = (uint16_t *)(smem + (MT_LV + 1) * st.B);
-    d.scr = (int32_t *)(smem + (MT_LV + 3) * st.B);
-    DocHdr h = *d.hp;
+    d.scr = (LDS_AS int32_t *)(smem + L.offScr);
+    d.nb = (LDS_AS int32_t *)(smem + L.offNb);
+    d.ends = (LDS_AS uint16_t *)(smem + L.offEnds);
+    d.cnt = smem + L.offCnt;
+    d.flg = (LDS_AS int8_t *)(smem + L.offFlg);
+    GLB_AS const uint8_t *gcnt = (GLB_AS const uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
+    GLB_AS const int8_t *gflg = (GLB_AS const int8_t *)(st.flg + doc * B);
+    const DocHdr h = *d.hp;
     d.n = h.n_seg;
     d.depth = h.depth;
     d.heap_n = h.heap_n;
@@ -84,20 +146,78 @@ __device__ void load_doc(Doc &d, const DevState &st, int doc, uint8_t *smem) {
     d.next_uid = h.next_uid;
     d.status = h.status;
     d.dlog_n = h.dlog_n;
-    for (int l = 0; l < MT_LV; l++) d.nb[l] = h.n_blk[l];
     d.dhash = h.delta_hash;
-    for (int l = 0; l < d.depth; l++)
-        for (int b = lane(); b < d.nb[l]; b += MT_WAVE) lvl(d, l)[b] = d.gcnt[l * B + b];
-    for (int b = lane(); b < d.nb[0]; b += MT_WAVE) d.flg[b] = d.gflg[b];
-    WSYNC();
+    d.text_gcs = 0;
+    d.props_gcs = 0;
+    if (d.status) return true;   // failed earlier: the caller leaves it untouched
+    int maxnb = 0;
+#pragma unroll
+    for (int l = 0; l < MT_LV; l++) maxnb = max(maxnb, h.n_blk[l]);
+    if (T::kLds) {
+        d.S_cap = S_l;
+        d.B_cap = B_l;
+        d.H_cap = H_l;
+        if (d.n > S_l || maxnb > B_l || d.heap_n > H_l) {
+            d.status = MT_DOC_RETRY;
+            return false;
+        }
+        d.A = (typename T::A_t)(smem + L.offA);
+        d.Bv = (typename T::B_t)(smem + L.offB);
+        d.O = (typename T::O_t)(smem + L.offO);
+        d.heap = (typename T::H_t)(smem + L.offH);
+        GLB_AS const v4i *gA = (GLB_AS const v4i *)(st.segA + doc * S);
+        GLB_AS const v4u *gB = (GLB_AS const v4u *)(st.segB + doc * S);
+        GLB_AS const u64 *gO = (GLB_AS const u64 *)(st.segO + doc * S);
+        GLB_AS const v2i *gH = (GLB_AS const v2i *)(st.heap + doc * (size_t)(st.H + 1));
+        for (int i = lane(); i < d.n; i += MT_WAVE) {
+            d.A[i] = gA[i];
+            d.Bv[i] = gB[i];
+            d.O[i] = gO[i];
+        }
+        for (int i = 1 + lane(); i <= d.heap_n; i += MT_WAVE) d.heap[i] = gH[i];
+    } else {
+        d.S_cap = st.S;
+        d.B_cap = st.B;
+        d.H_cap = st.H;
+        d.A = (typename T::A_t)(st.segA + doc * S);
+        d.Bv = (typename T::B_t)(st.segB + doc * S);
+        d.O = (typename T::O_t)(st.segO + doc * S);
+        d.heap = (typename T::H_t)(st.heap + doc * (size_t)(st.H + 1));
+    }
+    if (lane() < MT_LV) d.nb[lane()] = d.hp->n_blk[lane()];
+    wsync<T>();
+    for (int l = 0; l < d.depth; l++) {
+        const int nbl = d.nb[l];
+        for (int b = lane(); b < nbl; b += MT_WAVE) lvl(d, l)[b] = gcnt[l * B + b];
+    }
+    for (int b = lane(); b < h.n_blk[0]; b += MT_WAVE) d.flg[b] = gflg[b];
+    wsync<T>();
+    return true;
 }
 
-__device__ void store_doc(Doc &d) {
-    WSYNC();
-    const int B = d.B_cap;
+TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
+    wsync<T>();
+    const size_t S = st.S, B = st.B;
+    GLB_AS uint8_t *gcnt = (GLB_AS uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
+    GLB_AS int8_t *gflg = (GLB_AS int8_t *)(st.flg + doc * B);
+    if (T::kLds) {
+        GLB_AS v4i *gA = (GLB_AS v4i *)(st.segA + doc * S);
+        GLB_AS v4u *gB = (GLB_AS v4u *)(st.segB + doc * S);
+        GLB_AS u64 *gO = (GLB_AS u64 *)(st.segO + doc * S);
+        GLB_AS v2i *gH = (GLB_AS v2i *)(st.heap + doc * (size_t)(st.H + 1));
+        for (int i = lane(); i < d.n; i += MT_WAVE) {
+            gA[i] = d.A[i];
+            gB[i] = d.Bv[i];
+            gO[i] = d.O[i];
+        }
+        for (int i = 1 + lane(); i <= d.heap_n; i += MT_WAVE) gH[i] = d.heap[i];
+    }
     for (int l = 0; l < d.depth; l++)
-        for (int b = lane(); b < d.nb[l]; b += MT_WAVE) d.gcnt[l * B + b] = lvl(d, l)[b];
-    for (int b = lane(); b < d.nb[0]; b += MT_WAVE) d.gflg[b] = d.flg[b];
+        for (int b = lane(); b < d.nb[l]; b += MT_WAVE) gcnt[l * B + b] = lvl(d, l)[b];
+    for (int b = lane(); b < d.nb[0]; b += MT_WAVE) gflg[b] = d.flg[b];
+    int nbl[MT_LV];
+#pragma unroll
+    for (int l = 0; l < MT_LV; l++) nbl[l] = d.nb[l];
     if (lane() == 0) {
         DocHdr h;
         h.n_seg = d.n;
@@ -112,10 +232,12 @@ __device__ void store_doc(Doc &d) {
         h.next_uid = d.next_uid;
         h.status = d.status;
         h.dlog_n = d.dlog_n;
-        for (int l = 0; l < MT_LV; l++) h.n_blk[l] = d.nb[l];
+#pragma unroll
+        for (int l = 0; l < MT_LV; l++) h.n_blk[l] = nbl[l];
         h.delta_hash = d.dhash;
         h.n_ops = d.hp->n_ops;
         h.pad0 = 0;
+#pragma unroll
         for (int i = 0; i < 8; i++) h.pad[i] = 0;
         *d.hp = h;
     }
@@ -123,41 +245,67 @@ __device__ void store_doc(Doc &d) {
 
 // ------------------------------------------------------------------ segment table moves
 // [from, n) -> [from + k, n + k)
-__device__ void seg_move_right(Doc &d, int from, int k) {
+TD void seg_move_right(DocT<T> &d, int from, int k) {
     for (int hi = d.n; hi > from; hi -= MT_WAVE) {
         const int lo = max(from, hi - MT_WAVE);
         const int i = lo + lane();
+        v4i a;
+        u64 o;
+        v4u b;
         if (i < hi) {
-            int4 a = d.A[i];
-            u64 o = d.O[i];
-            uint4 b = d.Bv[i];
+            a = d.A[i];
+            o = d.O[i];
+            b = d.Bv[i];
+        }
+        wsync<T>();
+        if (i < hi) {
             d.A[i + k] = a;
             d.O[i + k] = o;
             d.Bv[i + k] = b;
         }
+        wsync<T>();
     }
-    WSYNC();
 }
 // [from, n) -> [from - k, n - k)
-__device__ void seg_move_left(Doc &d, int from, int k) {
+TD void seg_move_left(DocT<T> &d, int from, int k) {
     for (int lo = from; lo < d.n; lo += MT_WAVE) {
         const int i = lo + lane();
+        v4i a;
+        u64 o;
+        v4u b;
         if (i < d.n) {
-            int4 a = d.A[i];
-            u64 o = d.O[i];
-            uint4 b = d.Bv[i];
+            a = d.A[i];
+            o = d.O[i];
+            b = d.Bv[i];
+        }
+        wsync<T>();
+        if (i < d.n) {
             d.A[i - k] = a;
             d.O[i - k] = o;
             d.Bv[i - k] = b;
         }
+        wsync<T>();
     }
-    WSYNC();
+}
+
+// Loads a segment's {A, O} for a scan lane.  The load is unconditional (inactive lanes read
+// slot 0) and pinned in registers: a 64-bit LDS/global load that the compiler sinks into a
+// divergent branch was observed to return wrong masks on gfx950 / ROCm 7.2.
+TD void load_ao(DocT<T> &d, int i, bool v, v4i &a, u64 &o) {
+    const int ic = v ? i : 0;
+    a = d.A[ic];
+    o = d.O[ic];
+    asm volatile("" : "+v"(a), "+v"(o));
+    if (!v) {
+        a = v4i{0, 0, MT_RSEQ_NONE, 0};
+        o = 0ull;
+    }
 }
 
 // ------------------------------------------------------------------ B-tree counts (LDS)
 // First block b of level l whose end (prefix of counts) is > x (strict) or >= x.
-__device__ int blk_find(Doc &d, int l, int x, bool strict, int &start) {
-    const uint8_t *c = lvl(d, l);
+TD int blk_find(DocT<T> &d, int l, int x, bool strict, int &start) {
+    const LDS_AS uint8_t *c = lvl(d, l);
     const int nb = d.nb[l];
     int carry = 0;
     for (int base = 0; base < nb; base += MT_WAVE) {
@@ -177,8 +325,8 @@ __device__ int blk_find(Doc &d, int l, int x, bool strict, int &start) {
     return -1;
 }
 // sum of counts of blocks [0, b) at level l
-__device__ int blk_prefix(Doc &d, int l, int b) {
-    const uint8_t *c = lvl(d, l);
+TD int blk_prefix(DocT<T> &d, int l, int b) {
+    const LDS_AS uint8_t *c = lvl(d, l);
     int s = 0;
     for (int base = 0; base < b; base += MT_WAVE) {
         const int i = base + lane();
@@ -187,8 +335,8 @@ __device__ int blk_prefix(Doc &d, int l, int b) {
     return s;
 }
 // shift entries [from, nb) of level l by delta (right if > 0), flags too at level 0
-__device__ void blk_shift(Doc &d, int l, int from, int delta) {
-    uint8_t *c = lvl(d, l);
+TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
+    LDS_AS uint8_t *c = lvl(d, l);
     const int nb = d.nb[l];
     if (delta > 0) {
         for (int hi = nb; hi > from; hi -= MT_WAVE) {
@@ -200,12 +348,12 @@ __device__ void blk_shift(Doc &d, int l, int from, int delta) {
                 v = c[i];
                 if (l == 0) f = d.flg[i];
             }
-            __syncthreads();
+            wsync<T>();
             if (i < hi) {
                 c[i + delta] = v;
                 if (l == 0) d.flg[i + delta] = f;
             }
-            __syncthreads();
+            wsync<T>();
         }
     } else if (delta < 0) {
         for (int lo = from; lo < nb; lo += MT_WAVE) {
@@ -216,24 +364,26 @@ __device__ void blk_shift(Doc &d, int l, int from, int delta) {
                 v = c[i];
                 if (l == 0) f = d.flg[i];
             }
-            __syncthreads();
+            wsync<T>();
             if (i < nb) {
                 c[i + delta] = v;
                 if (l == 0) d.flg[i + delta] = f;
             }
-            __syncthreads();
+            wsync<T>();
         }
     }
-    d.nb[l] += delta;
+    wsync<T>();
+    if (lane() == 0) d.nb[l] = nb + delta;
+    wsync<T>();
 }
 
 // A block at level l reached MaxNodesInBlock: split 4|4 and propagate (insertingWalk
 // :2479-2503, split :2509-2522, updateRoot :1909-1920).  New blocks have needsScour
 // undefined; the original keeps its flag.
-__device__ void blk_split_up(Doc &d, int l, int b) {
+TD void blk_split_up(DocT<T> &d, int l, int b) {
     while (true) {
         if (d.nb[l] + 1 > d.B_cap) {
-            fail(d, MT_DOC_CAPACITY);
+            fail_cap(d);
             return;
         }
         const bool has_parent = l + 1 < d.depth;
@@ -251,23 +401,25 @@ __device__ void blk_split_up(Doc &d, int l, int b) {
             lvl(d, l)[b + 1] = MT_HALF;
             if (l == 0) d.flg[b + 1] = MT_SCOUR_UNDEF;
         }
-        WSYNC();
+        wsync<T>();
         if (!has_parent) {
             const int nl = d.depth;
             if (nl >= MT_LV) {
-                fail(d, MT_DOC_CAPACITY);
+                fail_cap(d);
                 return;
             }
             d.depth++;
-            d.nb[nl] = 1;
-            if (lane() == 0) lvl(d, nl)[0] = 2;
-            WSYNC();
+            if (lane() == 0) {
+                d.nb[nl] = 1;
+                lvl(d, nl)[0] = 2;
+            }
+            wsync<T>();
             return;
         }
         const int pc = lvl(d, l + 1)[P] + 1;
-        WSYNC();
+        wsync<T>();
         if (lane() == 0) lvl(d, l + 1)[P] = (uint8_t)pc;
-        WSYNC();
+        wsync<T>();
         if (pc < MT_MAXN) return;
         l = l + 1;
         b = P;
@@ -276,36 +428,37 @@ __device__ void blk_split_up(Doc &d, int l, int b) {
 
 // Replace entries [b0, b0 + nold) of level l with k entries sized base (+1 for the first
 // `extra`), as pack :1414-1446 does; new level-0 blocks have needsScour undefined.
-__device__ void blk_replace(Doc &d, int l, int b0, int nold, int k, int base, int extra) {
+TD void blk_replace(DocT<T> &d, int l, int b0, int nold, int k, int base, int extra) {
     if (d.nb[l] + (k - nold) > d.B_cap) {
-        fail(d, MT_DOC_CAPACITY);
+        fail_cap(d);
         return;
     }
     blk_shift(d, l, b0 + nold, k - nold);
-    uint8_t *c = lvl(d, l);
+    LDS_AS uint8_t *c = lvl(d, l);
     for (int j = lane(); j < k; j += MT_WAVE) {
         c[b0 + j] = (uint8_t)(base + (j < extra ? 1 : 0));
         if (l == 0) d.flg[b0 + j] = MT_SCOUR_UNDEF;
     }
-    WSYNC();
+    wsync<T>();
 }
 
 // level-0 end indices into LDS (for per-lane block lookups)
-__device__ void compute_ends(Doc &d) {
-    const uint8_t *c = lvl(d, 0);
+TD void compute_ends(DocT<T> &d) {
+    const LDS_AS uint8_t *c = lvl(d, 0);
+    const int nb = d.nb[0];
     int carry = 0;
-    for (int base = 0; base < d.nb[0]; base += MT_WAVE) {
+    for (int base = 0; base < nb; base += MT_WAVE) {
         const int b = base + lane();
-        const int v = b < d.nb[0] ? c[b] : 0;
+        const int v = b < nb ? c[b] : 0;
         const int inc = wave_scan_incl(v);
-        if (b < d.nb[0]) d.ends[b] = (uint16_t)(carry + inc);
+        if (b < nb) d.ends[b] = (uint16_t)(carry + inc);
         carry += bcast(inc, MT_WAVE - 1);
     }
-    WSYNC();
+    wsync<T>();
 }
 // first block with end > i (binary search over d.ends; per-lane)
-__device__ __forceinline__ int block_of(Doc &d, int i) {
-    int lo = 0, hi = d.nb[0] - 1;
+TD int block_of(DocT<T> &d, int i, int nb) {
+    int lo = 0, hi = nb - 1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (d.ends[mid] > i)
@@ -318,54 +471,60 @@ __device__ __forceinline__ int block_of(Doc &d, int i) {
 
 // ------------------------------------------------------------------ zamboni heap
 // Collections.Heap add/get (MT/collections.ts:212-265); touched by lane 0 only.
-__device__ void heap_add(Doc &d, int max_seq, int uid) {
+TD void heap_add(DocT<T> &d, int max_seq, int uid) {
     if (d.heap_n + 1 > d.H_cap) {
-        fail(d, MT_DOC_CAPACITY);
+        fail_cap(d);
         return;
     }
     d.heap_n++;
     if (lane() == 0) {
-        int2 *h = d.heap;
+        typename T::H_t h = d.heap;
         int k = d.heap_n;
-        h[k] = make_int2(max_seq, uid);
-        while (k > 1 && h[k >> 1].x - h[k].x > 0) {
-            int2 t = h[k >> 1];
-            h[k >> 1] = h[k];
-            h[k] = t;
+        const v2i e = v2i{max_seq, uid};
+        while (k > 1) {
+            const v2i p = h[k >> 1];
+            if (!(p.x - e.x > 0)) break;
+            h[k] = p;
             k >>= 1;
         }
+        h[k] = e;
     }
 }
-__device__ int2 heap_top(Doc &d) {
+TD v2i heap_top(DocT<T> &d) {
     int x = 0, y = 0;
     if (lane() == 0) {
-        int2 t = d.heap[1];
+        const v2i t = d.heap[1];
         x = t.x;
         y = t.y;
     }
-    return make_int2(bcast(x, 0), bcast(y, 0));
+    return v2i{bcast(x, 0), bcast(y, 0)};
 }
-__device__ void heap_pop(Doc &d) {
+TD void heap_pop(DocT<T> &d) {
     if (lane() == 0) {
-        int2 *h = d.heap;
-        int n = d.heap_n;
-        h[1] = h[n];
-        n--;
+        typename T::H_t h = d.heap;
+        const int n = d.heap_n - 1;
+        const v2i e = h[d.heap_n];
         int k = 1;
         while ((k << 1) <= n) {
             int j = k << 1;
-            if (j < n && h[j].x - h[j + 1].x > 0) j++;
-            if (h[k].x - h[j].x <= 0) break;
-            int2 t = h[k];
-            h[k] = h[j];
-            h[j] = t;
+            v2i cj = h[j];
+            if (j < n) {
+                const v2i cj1 = h[j + 1];
+                if (cj.x - cj1.x > 0) {
+                    j++;
+                    cj = cj1;
+                }
+            }
+            if (e.x - cj.x <= 0) break;
+            h[k] = cj;
             k = j;
         }
+        h[k] = e;
     }
     d.heap_n--;
 }
 
-__device__ int find_uid(Doc &d, uint32_t uid) {
+TD int find_uid(DocT<T> &d, uint32_t uid) {
     for (int base = 0; base < d.n; base += MT_WAVE) {
         const int i = base + lane();
         const u64 m = ballot(i < d.n && (d.Bv[i].z & ~MT_MARKER_BIT) == uid);
@@ -375,29 +534,36 @@ __device__ int find_uid(Doc &d, uint32_t uid) {
 }
 
 // sum of observer lengths over [0, x)  (getPosition :1619-1636 in the observer view)
-__device__ int obs_prefix(Doc &d, int x) {
+TD int obs_prefix(DocT<T> &d, int x) {
     int s = 0;
     for (int base = 0; base < x; base += MT_WAVE) {
         const int i = base + lane();
-        s += wave_sum(i < x ? obs_len(d.A[i]) : 0);
+        s += i < x ? obs_len(d.A[i]) : 0;
     }
-    return s;
+    return wave_sum(s);
 }
 
 // ------------------------------------------------------------------ text arena
-__device__ void wave_copy16(uint16_t *dst, const uint16_t *src, int n) {
+// dst/src in the same arena half; callers gsync() before reading text written this launch
+TD void copy_text(GLB_AS uint16_t *dst, const GLB_AS uint16_t *src, int n) {
     for (int j = lane(); j < n; j += MT_WAVE) dst[j] = src[j];
 }
 // Compact all live text (non-removed TextSegments) into the other half, document order.
-__device__ void text_gc(Doc &d) {
-    WSYNC();
+TD void text_gc(DocT<T> &d) {
+    if (T::kLds && d.text_gcs > 0) {   // a second flip would overwrite the saved half
+        fail_cap(d);
+        return;
+    }
+    d.text_gcs++;
+    gsync();
     const int dh = 1 - d.text_half;
-    uint16_t *dst = text_base(d, dh), *src = text_base(d, d.text_half);
+    GLB_AS uint16_t *dst = text_base(d, dh);
+    const GLB_AS uint16_t *src = text_base(d, d.text_half);
     int carry = 0;
     for (int base = 0; base < d.n; base += MT_WAVE) {
         const int i = base + lane();
-        int4 a = make_int4(0, 0, 0, 0);
-        uint4 b = make_uint4(0, 0, 0, 0);
+        v4i a = v4i{0, 0, 0, 0};
+        v4u b = v4u{0, 0, 0, 0};
         if (i < d.n) {
             a = d.A[i];
             b = d.Bv[i];
@@ -411,26 +577,33 @@ __device__ void text_gc(Doc &d) {
             const int j = first_lane(m);
             m &= m - 1;
             const int lj = bcast(len, j), oj = bcast(off, j), sj = bcast((int)b.x, j);
-            wave_copy16(dst + oj, src + sj, lj);
+            copy_text<T>(dst + oj, src + sj, lj);
         }
+        wsync<T>();
         if (live) d.Bv[i].x = (uint32_t)off;
         carry += bcast(inc, MT_WAVE - 1);
     }
     d.text_half = dh;
     d.text_top = carry;
-    WSYNC();
+    wsync<T>();
 }
-__device__ bool text_ensure(Doc &d, int need) {
+TD bool text_ensure(DocT<T> &d, int need) {
     if (d.text_top + need <= d.T_cap) return true;
     text_gc(d);
+    if (d.status) return false;
     if (d.text_top + need <= d.T_cap) return true;
-    fail(d, MT_DOC_CAPACITY);
+    fail_cap(d);
     return false;
 }
 
 // ------------------------------------------------------------------ property records
-__device__ void props_gc(Doc &d) {
-    WSYNC();
+TD void props_gc(DocT<T> &d) {
+    if (T::kLds && d.props_gcs > 0) {
+        fail_cap(d);
+        return;
+    }
+    d.props_gcs++;
+    gsync();
     const int dh = 1 - d.props_half;
     int carry = 1;
     for (int base = 0; base < d.n; base += MT_WAVE) {
@@ -440,31 +613,34 @@ __device__ void props_gc(Doc &d) {
         const int inc = wave_scan_incl(has);
         const uint32_t nh = (uint32_t)(carry + inc - has);
         if (has) {
-            const uint32_t *s = prec(d, d.props_half, h);
-            uint32_t *t = prec(d, dh, nh);
+            const GLB_AS uint32_t *s = prec(d, d.props_half, h);
+            GLB_AS uint32_t *t = prec(d, dh, nh);
             const uint32_t n = s[0];
             t[0] = n;
             for (uint32_t k = 0; k < 2 * n; k++) t[1 + k] = s[1 + k];
-            d.Bv[i].y = nh;
         }
+        wsync<T>();
+        if (has) d.Bv[i].y = nh;
         carry += bcast(inc, MT_WAVE - 1);
     }
     d.props_half = dh;
     d.props_top = carry;
-    WSYNC();
+    gsync();
+    wsync<T>();
 }
-__device__ bool props_ensure(Doc &d, int need) {
+TD bool props_ensure(DocT<T> &d, int need) {
     if (d.props_top + need <= d.P_cap) return true;
     props_gc(d);
+    if (d.status) return false;
     if (d.props_top + need <= d.P_cap) return true;
-    fail(d, MT_DOC_CAPACITY);
+    fail_cap(d);
     return false;
 }
 // Properties.matchProperties MT/properties.ts:61-92 over interned ids
-__device__ bool match_props(Doc &d, uint32_t ha, uint32_t hb) {
+TD bool match_props(DocT<T> &d, uint32_t ha, uint32_t hb) {
     if (ha == 0 || hb == 0) return ha == hb;
     if (ha == hb) return true;
-    const uint32_t *a = prec(d, d.props_half, ha), *b = prec(d, d.props_half, hb);
+    const GLB_AS uint32_t *a = prec(d, d.props_half, ha), *b = prec(d, d.props_half, hb);
     const uint32_t na = a[0], nbb = b[0];
     if (na != nbb) return false;
     for (uint32_t i = 0; i < na; i++) {
@@ -482,7 +658,7 @@ struct Cb {
     int n;
     int log_hdr;  // dlog index of the record header, -1 if not logging
 };
-__device__ Cb cb_begin(Doc &d, int seq, int kind) {
+TD Cb cb_begin(DocT<T> &d, int seq, int kind) {
     Cb cb;
     cb.h = fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)seq), (uint32_t)kind);
     cb.n = 0;
@@ -497,12 +673,12 @@ __device__ Cb cb_begin(Doc &d, int seq, int kind) {
     }
     return cb;
 }
-__device__ void cb_end(Doc &d, Cb &cb) {
+TD void cb_end(DocT<T> &d, Cb &cb) {
     cb.h = fnv_u32(cb.h, (uint32_t)cb.n);
     d.dhash = fnv_u64(d.dhash, cb.h);
     if (cb.log_hdr >= 0 && lane() == 0) d.dlog[cb.log_hdr + 2] = cb.n;
 }
-__device__ void cb_log(Doc &d, int32_t v) {
+TD void cb_log(DocT<T> &d, int32_t v) {
     if (d.dlog && d.dlog_n + 1 <= d.DL_cap) {
         if (lane() == 0) d.dlog[d.dlog_n] = v;
         d.dlog_n++;
@@ -512,9 +688,10 @@ __device__ void cb_log(Doc &d, int32_t v) {
 // ------------------------------------------------------------------ splitting
 // BaseSegment.splitAt :523-567 (right half inserted right after the left half in the same
 // leaf block, which may then split).  Property records are immutable, so both halves share.
-__device__ void split_seg(Doc &d, int i, int q) {
+// The left half's last character is unknown until a scour needs it.
+TD void split_seg(DocT<T> &d, int i, int q) {
     if (d.n + 1 > d.S_cap) {
-        fail(d, MT_DOC_CAPACITY);
+        fail_cap(d);
         return;
     }
     int bstart;
@@ -525,15 +702,17 @@ __device__ void split_seg(Doc &d, int i, int q) {
     }
     seg_move_right(d, i + 1, 1);
     if (lane() == 0) {
-        int4 a = d.A[i];
-        uint4 bb = d.Bv[i];
-        int4 r = a;
+        v4i a = d.A[i];
+        v4u bb = d.Bv[i];
+        v4i r = a;
         r.x = a.x - q;
         a.x = q;
-        uint4 rb = bb;
+        v4u rb = bb;
         rb.x = bb.x + (uint32_t)q;
         rb.z = (uint32_t)d.next_uid | (bb.z & MT_MARKER_BIT);
+        bb.w &= ~(SEGF_NL_KNOWN | SEGF_NL);
         d.A[i] = a;
+        d.Bv[i] = bb;
         d.A[i + 1] = r;
         d.O[i + 1] = d.O[i];
         d.Bv[i + 1] = rb;
@@ -541,24 +720,31 @@ __device__ void split_seg(Doc &d, int i, int q) {
     d.next_uid++;
     d.n++;
     const int c = lvl(d, 0)[b] + 1;
-    WSYNC();
+    wsync<T>();
     if (lane() == 0) lvl(d, 0)[b] = (uint8_t)c;
-    WSYNC();
+    wsync<T>();
     if (c == MT_MAXN) blk_split_up(d, 0, b);
 }
 
 // ensureIntervalBoundary :2274-2278 -- split the leaf strictly containing view position p
-__device__ void boundary(Doc &d, int p, int r, int c) {
+TD void boundary(DocT<T> &d, int p, int r, int c) {
     int carry = 0;
     for (int base = 0; base < d.n; base += MT_WAVE) {
         const int i = base + lane();
         const bool v = i < d.n;
-        int4 a = v ? d.A[i] : make_int4(0, 0, MT_RSEQ_NONE, 0);
-        const u64 o = v ? d.O[i] : 0ull;
+        v4i a;
+        u64 o;
+        load_ao(d, i, v, a, o);
         const int vl = v ? view_len(a, o, r, c) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin = carry + inc;
         const u64 m = ballot(v && pex < p && p < pin);
+#ifdef MT_DEBUG_BOUNDARY
+        if (d.dlog) {
+            cb_log(d, 0x7777); cb_log(d, p); cb_log(d, r); cb_log(d, c); cb_log(d, base);
+            for (int q = 0; q < 16; q++) { cb_log(d, bcast(vl, q)); cb_log(d, bcast(a.z, q)); cb_log(d, bcast(a.w, q)); cb_log(d, (int)bcast64(o, q)); }
+        }
+#endif
         if (m) {
             const int l = first_lane(m);
             split_seg(d, base + l, p - bcast(pex, l));
@@ -569,13 +755,13 @@ __device__ void boundary(Doc &d, int p, int r, int c) {
     }
 }
 
-// addToLRUSet :1306-1316 for the segment at index i in leaf block b
-__device__ void add_to_lru_block(Doc &d, int b, uint32_t uid, int seq) {
+// addToLRUSet :1306-1316 for a segment in leaf block b
+TD void add_to_lru_block(DocT<T> &d, int b, uint32_t uid, int seq) {
     const int f = d.flg[b];
-    WSYNC();
     if (f != 1 && seq > d.cur_seq) {
+        wsync<T>();
         if (lane() == 0) d.flg[b] = 1;
-        WSYNC();
+        wsync<T>();
         heap_add(d, seq, (int)uid);
     }
 }
@@ -590,43 +776,67 @@ __device__ __forceinline__ bool can_append(int plen, bool pmarker, bool p_nl, in
 }
 
 // scourNode :1322-1398 over leaf block [s, e); compacts the table.  Returns survivors.
-__device__ int scour_block(Doc &d, int s, int e) {
-    // plan (lane 0): scr[k] = -2 keep, -1 unlink, >=0 append into that local index
-    int *plan = d.scr;
-    int *glen = d.scr + 16;  // merged length per keeper
+TD int scour_block(DocT<T> &d, int s, int e) {
     const int cntb = e - s;
+    // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
+    {
+        const int k = lane();
+        bool need = false;
+        v4i a;
+        v4u b;
+        if (k < cntb) {
+            a = d.A[s + k];
+            b = d.Bv[s + k];
+            need = a.z == MT_RSEQ_NONE && a.y <= d.min_seq && !(b.z & MT_MARKER_BIT) && a.x > 0 &&
+                   !(b.w & SEGF_NL_KNOWN);
+        }
+        if (ballot(need)) {
+            gsync();
+            if (need) {
+                const uint16_t ch = text_base(d, d.text_half)[b.x + a.x - 1];
+                d.Bv[s + k].w = (b.w & ~SEGF_NL) | SEGF_NL_KNOWN | (ch == '\n' ? SEGF_NL : 0u);
+            }
+            wsync<T>();
+        }
+    }
+    // plan (lane 0): scr[k] = -2 keep, -1 unlink, >=0 append into that local index
+    LDS_AS int *plan = d.scr;
+    LDS_AS int *glen = d.scr + 16;  // merged length per keeper
+    LDS_AS int *gw = d.scr + 32;    // merged flags per keeper
     int need = 0;
     if (lane() == 0) {
-        const uint16_t *tb = text_base(d, d.text_half);
         int prev = -1;
         int plen = 0;
         bool pmark = false, pnl = false;
         uint32_t pprops = 0;
         int pend = 0;  // arena end of prev's current contiguous text (-1 if not contiguous)
         for (int k = 0; k < cntb; k++) {
-            const int4 a = d.A[s + k];
-            const uint4 b = d.Bv[s + k];
+            const v4i a = d.A[s + k];
+            const v4u b = d.Bv[s + k];
             const bool mk = (b.z & MT_MARKER_BIT) != 0;
             glen[k] = a.x;
+            gw[k] = (int)b.w;
             if (a.z != MT_RSEQ_NONE) {
                 plan[k] = (a.z > d.min_seq) ? -2 : -1;
                 prev = -1;
             } else if (a.y <= d.min_seq) {
                 const bool ok = prev >= 0 && can_append(plen, pmark, pnl, a.x, mk) &&
                                 match_props(d, pprops, b.y) && a.x > 0;
+                const bool nl = (b.w & SEGF_NL) != 0;
                 if (ok) {
                     plan[k] = prev;
-                    if (pend != (int)b.x) need += 1;  // needs a copy (flag)
+                    if (pend != (int)b.x) need += 1;
                     pend = pend == (int)b.x ? (int)b.x + a.x : -1;
                     plen += a.x;
                     glen[prev] = plen;
-                    pnl = tb[b.x + a.x - 1] == '\n';
+                    gw[prev] = (int)b.w;
+                    pnl = nl;
                 } else {
                     plan[k] = -2;
                     prev = k;
                     plen = a.x;
                     pmark = mk;
-                    pnl = !mk && a.x > 0 && tb[b.x + a.x - 1] == '\n';
+                    pnl = !mk && a.x > 0 && nl;
                     pprops = b.y;
                     pend = (int)b.x + a.x;
                 }
@@ -636,63 +846,65 @@ __device__ int scour_block(Doc &d, int s, int e) {
             }
         }
     }
-    WSYNC();
+    wsync<T>();
     need = bcast(need, 0);
     if (need) {
-        // total bytes of groups that are not contiguous
+        // total length of the groups (upper bound of what gets copied)
         int tot = 0;
         for (int k = 0; k < cntb; k++)
             if (plan[k] == -2) tot += glen[k];
         if (!text_ensure(d, tot)) return cntb;
+        gsync();
     }
     // execute text merges group by group (uniform loops; cntb <= 8)
     for (int k = 0; k < cntb; k++) {
         if (plan[k] != -2 || glen[k] == d.A[s + k].x) continue;
         // keeper k with appended followers
-        uint4 bk = d.Bv[s + k];
-        int4 ak = d.A[s + k];
+        const v4u bk = d.Bv[s + k];
+        const v4i ak = d.A[s + k];
         bool contig = true;
         int endp = (int)bk.x + ak.x;
         for (int j = k + 1; j < cntb && plan[j] == k; j++) {
-            const uint4 bj = d.Bv[s + j];
+            const v4u bj = d.Bv[s + j];
             if ((int)bj.x != endp) contig = false;
             endp += d.A[s + j].x;
         }
-        uint16_t *tb = text_base(d, d.text_half);
+        GLB_AS uint16_t *tb = text_base(d, d.text_half);
         uint32_t newoff = bk.x;
         if (!contig) {
             int dst;
             if ((int)bk.x + ak.x == d.text_top) {
-                dst = d.text_top + 0;
-                newoff = bk.x;
                 dst = d.text_top;
             } else {
                 newoff = (uint32_t)d.text_top;
-                wave_copy16(tb + d.text_top, tb + bk.x, ak.x);
+                copy_text<T>(tb + d.text_top, tb + bk.x, ak.x);
                 dst = d.text_top + ak.x;
             }
             for (int j = k + 1; j < cntb && plan[j] == k; j++) {
-                const uint4 bj = d.Bv[s + j];
+                const v4u bj = d.Bv[s + j];
                 const int lj = d.A[s + j].x;
-                wave_copy16(tb + dst, tb + bj.x, lj);
+                copy_text<T>(tb + dst, tb + bj.x, lj);
                 dst += lj;
             }
             d.text_top = dst;
         }
-        WSYNC();
+        wsync<T>();
         if (lane() == 0) {
             d.A[s + k].x = glen[k];
-            d.Bv[s + k].x = newoff;
+            v4u nb = bk;
+            nb.x = newoff;
+            nb.w = (uint32_t)gw[k];
+            d.Bv[s + k] = nb;
         }
-        WSYNC();
+        wsync<T>();
     }
     // compaction: survivors to the front of the block, tail moved left
     int keep = 0;
     for (int k = 0; k < cntb; k++) keep += plan[k] == -2 ? 1 : 0;
     if (keep < cntb) {
-        int4 a;
+        v4i a;
         u64 o;
-        uint4 b;
+        v4u b;
         int dst = -1;
         if (lane() < cntb && plan[lane()] == -2) {
             a = d.A[s + lane()];
@@ -702,13 +914,13 @@ __device__ int scour_block(Doc &d, int s, int e) {
             for (int k = 0; k < lane(); k++) r += plan[k] == -2 ? 1 : 0;
             dst = s + r;
         }
-        WSYNC();
+        wsync<T>();
         if (dst >= 0) {
             d.A[dst] = a;
             d.O[dst] = o;
             d.Bv[dst] = b;
         }
-        WSYNC();
+        wsync<T>();
         const int from = e, k = cntb - keep;
         seg_move_left(d, from, k);
         d.n -= k;
@@ -717,7 +929,7 @@ __device__ int scour_block(Doc &d, int s, int e) {
 }
 
 // pack :1401-1453 starting from the underflowing block b of level l
-__device__ void pack(Doc &d, int l, int b) {
+TD void pack(DocT<T> &d, int l, int b) {
     while (true) {
         int c0;
         const int P = blk_find(d, l + 1, b, true, c0);
@@ -733,9 +945,9 @@ __device__ void pack(Doc &d, int l, int b) {
                 const int old = lvl(d, 0)[cb];
                 const int kept = scour_block(d, pos, pos + old);
                 if (d.status) return;
-                WSYNC();
+                wsync<T>();
                 if (lane() == 0) lvl(d, 0)[cb] = (uint8_t)kept;
-                WSYNC();
+                wsync<T>();
                 pos += kept;
                 total += kept;
             }
@@ -747,8 +959,9 @@ __device__ void pack(Doc &d, int l, int b) {
         if (k < 1) k = 1;
         const int base = total / k, extra = total % k;
         blk_replace(d, l, c0, nch, k, base, extra);
+        if (d.status) return;
         if (lane() == 0) lvl(d, l + 1)[P] = (uint8_t)k;
-        WSYNC();
+        wsync<T>();
         if (k < MT_HALF && l + 2 < d.depth) {
             l = l + 1;
             b = P;
@@ -759,12 +972,13 @@ __device__ void pack(Doc &d, int l, int b) {
 }
 
 // zamboniSegments :1455-1511
-__device__ void zamboni(Doc &d) {
+TD void zamboni(DocT<T> &d) {
     for (int it = 0; it < MT_ZAMBONI && d.status == 0; it++) {
         if (d.heap_n == 0) break;
-        const int2 top = heap_top(d);
+        const v2i top = heap_top(d);
         if (top.x > d.min_seq) break;
         heap_pop(d);
+        wsync<T>();
         const int i = find_uid(d, (uint32_t)top.y);
         if (i < 0) continue;
         int bstart;
@@ -775,23 +989,37 @@ __device__ void zamboni(Doc &d) {
         }
         const int f = d.flg[b];
         const int old = lvl(d, 0)[b];
-        WSYNC();
         if (f == 0) continue;
         const int kept = scour_block(d, bstart, bstart + old);
         if (d.status) return;
-        WSYNC();
+        wsync<T>();
         if (lane() == 0) {
             d.flg[b] = 0;
             lvl(d, 0)[b] = (uint8_t)kept;
         }
-        WSYNC();
+        wsync<T>();
         if (kept < old && kept < MT_HALF && d.depth > 1) pack(d, 0, b);
     }
 }
 
 // ------------------------------------------------------------------ ops
+// One sequenced message as the engine consumes it: the record plus (prefetched) the first
+// 8 UTF-16 units of an insert's payload and whether the payload ends with '\n'.
+struct OpIn {
+    mt_op_rec op;
+    u64 pay_lo, pay_hi;   // units 0..3 / 4..7 when pay_ok
+    bool pay_ok;
+    bool nl;
+};
+
+__device__ __forceinline__ uint16_t pay_unit(const OpIn &in, int j) {
+    const u64 w = j < 4 ? (in.pay_lo >> (16 * j)) : (in.pay_hi >> (16 * (j - 4)));
+    return (uint16_t)(w & 0xFFFF);
+}
+
 // Client.applyInsertOp MT/client.ts:394-442 -> MergeTree.insertSegments :2001-2031
-__device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, const uint32_t *pin) {
+TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    const mt_op_rec &op = in.op;
     const int r = op.ref_seq, c = op.client, seq = op.seq, p = op.pos1;
     const bool marker = (op.flags & MT_F_MARKER) != 0;
     const int slen = marker ? 1 : op.pos2;
@@ -800,8 +1028,9 @@ __device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, cons
     for (int base = 0; base < d.n; base += MT_WAVE) {
         const int i = base + lane();
         const bool v = i < d.n;
-        const int4 a = v ? d.A[i] : make_int4(0, 0, MT_RSEQ_NONE, 0);
-        const u64 o = v ? d.O[i] : 0ull;
+        v4i a;
+        u64 o;
+        load_ao(d, i, v, a, o);
         const int vl = v ? view_len(a, o, r, c) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin_ = carry + inc;
@@ -844,7 +1073,7 @@ __device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, cons
         return;
     }
     if (d.n + 1 > d.S_cap) {
-        fail(d, MT_DOC_CAPACITY);
+        fail_cap(d);
         return;
     }
     if (!marker && !text_ensure(d, slen)) return;
@@ -853,26 +1082,24 @@ __device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, cons
         if (!props_ensure(d, 1)) return;
         ph = (uint32_t)d.props_top;
         d.props_top++;
-        const uint32_t *rec = pin + op.props;
+        const GLB_AS uint32_t *rec = pin + op.props;
         const uint32_t cntk = rec[0] & 0xFFFF;
-        if (lane() == 0) {
-            uint32_t *t = prec(d, d.props_half, ph);
-            uint32_t n = 0;
-            for (uint32_t j = 0; j < cntk; j++) {
-                if (rec[2 + 2 * j] == MT_VAL_NULL) continue;  // null dropped (Q5)
-                if (n < MT_KMAX) {
-                    t[1 + 2 * n] = rec[1 + 2 * j];
-                    t[2 + 2 * n] = rec[2 + 2 * j];
-                }
-                n++;
-            }
-            t[0] = n;
-        }
         int cn = 0;
         for (uint32_t j = 0; j < cntk; j++) cn += rec[2 + 2 * j] != MT_VAL_NULL;
         if (cn > MT_KMAX) {
             fail(d, MT_DOC_CAPACITY);
             return;
+        }
+        if (lane() == 0) {
+            GLB_AS uint32_t *t = prec(d, d.props_half, ph);
+            uint32_t n = 0;
+            for (uint32_t j = 0; j < cntk; j++) {
+                if (rec[2 + 2 * j] == MT_VAL_NULL) continue;  // null dropped (Q5)
+                t[1 + 2 * n] = rec[1 + 2 * j];
+                t[2 + 2 * n] = rec[2 + 2 * j];
+                n++;
+            }
+            t[0] = n;
         }
     }
     int bstart;
@@ -883,27 +1110,33 @@ __device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, cons
     }
     const int bend = bstart + lvl(d, 0)[B];
     const int x = (js >= 0 && js < bend) ? js : bend;
-    uint32_t toff;
+    uint32_t toff, segw = 0;
     if (marker) {
         toff = op.payload;
     } else {
         toff = (uint32_t)d.text_top;
-        wave_copy16(text_base(d, d.text_half) + d.text_top, tin + op.payload, slen);
+        GLB_AS uint16_t *dst = text_base(d, d.text_half) + d.text_top;
+        if (in.pay_ok) {
+            if (lane() < slen) dst[lane()] = pay_unit(in, lane());
+        } else {
+            copy_text<T>(dst, tin + op.payload, slen);
+        }
         d.text_top += slen;
+        segw = SEGF_NL_KNOWN | (in.nl ? SEGF_NL : 0u);
     }
     seg_move_right(d, x, 1);
     const uint32_t uid = (uint32_t)d.next_uid;
     if (lane() == 0) {
-        d.A[x] = make_int4(slen, seq, MT_RSEQ_NONE, pack_cli(c, 0));
+        d.A[x] = v4i{slen, seq, MT_RSEQ_NONE, pack_cli(c, 0)};
         d.O[x] = 0ull;
-        d.Bv[x] = make_uint4(toff, ph, uid | (marker ? MT_MARKER_BIT : 0u), 0u);
+        d.Bv[x] = v4u{toff, ph, uid | (marker ? MT_MARKER_BIT : 0u), segw};
     }
     d.next_uid++;
     d.n++;
     const int nc = lvl(d, 0)[B] + 1;
-    WSYNC();
+    wsync<T>();
     if (lane() == 0) lvl(d, 0)[B] = (uint8_t)nc;
-    WSYNC();
+    wsync<T>();
     int lb = B;
     if (nc == MT_MAXN) {
         blk_split_up(d, 0, B);
@@ -911,6 +1144,7 @@ __device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, cons
         if (x - bstart >= MT_HALF) lb = B + 1;
     }
     if (seq > d.min_seq) add_to_lru_block(d, lb, uid, seq);  // saveIfLocal :2197-2212
+    if (d.status) return;
     // delta callback: position of the new segment in the observer view
     const int pos = obs_prefix(d, x);
     cb.n = 1;
@@ -923,12 +1157,12 @@ __device__ void op_insert(Doc &d, const mt_op_rec &op, const uint16_t *tin, cons
 
 // SegmentPropertiesManager.addProperties MT/segmentPropertiesManager.ts:35-111 applied by
 // one lane to its segment: writes the new record nh, returns the seg hash contribution of
-// the propertyDeltas (and logs them when `log` is set).  Returns false on key overflow.
-__device__ bool annotate_record(Doc &d, uint32_t oh, uint32_t nh, const uint32_t *rec,
-                                u64 &sh, int32_t *logp, int &nlog) {
+// the propertyDeltas (and logs them when `logp` is set).  Returns false on key overflow.
+TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint32_t *rec, u64 &sh,
+                        GLB_AS int32_t *logp, int &nlog) {
     const uint32_t cntk = rec[0] & 0xFFFF, comb = rec[0] >> 16;
-    const uint32_t *o = oh ? prec(d, d.props_half, oh) : nullptr;
-    uint32_t *t = prec(d, d.props_half, nh);
+    const GLB_AS uint32_t *o = oh ? prec(d, d.props_half, oh) : nullptr;
+    GLB_AS uint32_t *t = prec(d, d.props_half, nh);
     const uint32_t on = o ? o[0] : 0;
     uint32_t n = 0;
     int npd = 0;
@@ -1002,29 +1236,33 @@ __device__ bool annotate_record(Doc &d, uint32_t oh, uint32_t nh, const uint32_t
 // markRangeRemoved :2640-2752 / annotateRange :2598-2638.  After the two boundary splits
 // the visited leaves are exactly those with view length > 0 inside [p1, p2) (nodeMap
 // :2936-2998 is tree-shape independent), processed in document order.
-__device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
+TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
     const int r = op.ref_seq, c = op.client, seq = op.seq, p1 = op.pos1, p2 = op.pos2;
     const bool rem = op.kind == MT_OP_REMOVE;
-    const uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
+    const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
     if (rec && (rec[0] >> 16) == MT_COMBINE_OTHER) {
         fail(d, MT_DOC_UNSUPPORTED);
         return;
     }
+    if (!rec) rec = (const GLB_AS uint32_t *)&kEmptyPropsRec;
     boundary(d, p1, r, c);
     if (d.status) return;
     boundary(d, p2, r, c);
     if (d.status) return;
     compute_ends(d);
+    if (!rem) gsync();   // property records written earlier in this launch are read below
     Cb cb = cb_begin(d, seq, op.kind);
     int carry = 0, ocarry = 0, last_b = -1;
     const int L = lane();
+    const int nblk = d.nb[0];
     for (int base = 0; base < d.n; base += MT_WAVE) {
         if (!rem && !props_ensure(d, MT_WAVE)) return;
         const int i = base + L;
         const bool v = i < d.n;
-        int4 a = v ? d.A[i] : make_int4(0, 0, MT_RSEQ_NONE, 0);
-        const u64 o = v ? d.O[i] : 0ull;
-        const uint4 bv = v ? d.Bv[i] : make_uint4(0, 0, 0, 0);
+        v4i a;
+        u64 o;
+        load_ao(d, i, v, a, o);
+        const v4u bv = d.Bv[v ? i : 0];
         const int vl = v ? view_len(a, o, r, c) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin_ = carry + inc;
@@ -1054,7 +1292,7 @@ __device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
         u64 sh = fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)opos), (uint32_t)a.x);
         if (!rem && sel) {
             int unused = 0;
-            if (!annotate_record(d, bv.y, nh, rec ? rec : &kEmptyPropsRec, sh, nullptr, unused)) bad = true;
+            if (!annotate_record(d, bv.y, nh, rec, sh, (GLB_AS int32_t *)nullptr, unused)) bad = true;
             d.Bv[i].y = nh;
         }
         if (ballot(bad)) {
@@ -1062,7 +1300,7 @@ __device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
             return;
         }
         if (!rem) d.props_top += __popcll(sel_m);
-        WSYNC();
+        wsync<T>();
         // fold the callback records in document order
         u64 em = ballot(entry);
         while (em) {
@@ -1076,13 +1314,13 @@ __device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
                 if (!rem) {
                     // re-derive this segment's propertyDeltas into the log (debug only)
                     const uint32_t ohj = (uint32_t)bcast((int)bv.y, j), nhj = (uint32_t)bcast((int)nh, j);
-                    (void)ohj;
                     int nl = 0;
                     u64 dummy = 0;
                     const int at = d.dlog_n + 1;
+                    gsync();
                     if (L == 0 && at + 4 * MT_KMAX + 2 <= d.DL_cap) {
                         // old record is untouched (new record went to a fresh handle)
-                        annotate_record(d, ohj, nhj, rec ? rec : &kEmptyPropsRec, dummy, d.dlog + at, nl);
+                        annotate_record(d, ohj, nhj, rec, dummy, d.dlog + at, nl);
                         d.dlog[at - 1] = nl / 2;
                     }
                     nl = bcast(nl, 0);
@@ -1091,7 +1329,7 @@ __device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
             }
         }
         // addToLRUSet for every visited segment, first one per leaf block (:2680-2689)
-        const int b = sel ? block_of(d, i) : -1;
+        const int b = sel ? block_of(d, i, nblk) : -1;
         const u64 below = sel_m & ((1ull << L) - 1ull);
         const int prevl = below ? 63 - __clzll((long long)below) : -1;
         const int pb = __shfl(b, prevl < 0 ? 0 : prevl, MT_WAVE);
@@ -1102,6 +1340,7 @@ __device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
             fm &= fm - 1;
             add_to_lru_block(d, bcast(b, j), (uint32_t)bcast((int)(bv.z & ~MT_MARKER_BIT), j), seq);
         }
+        if (d.status) return;
         if (sel_m) last_b = bcast(b, 63 - __clzll((long long)sel_m));
         carry += bcast(inc, MT_WAVE - 1);
         ocarry += bcast(oinc, MT_WAVE - 1);
@@ -1113,7 +1352,7 @@ __device__ void op_range(Doc &d, const mt_op_rec &op, const uint32_t *pin) {
 
 // updateSeqNumbers / updateMinSeq / setMinSeq  MT/client.ts:821-828, 991-1004,
 // MT/mergeTree.ts:1751-1769
-__device__ void update_seq(Doc &d, int msn, int seq) {
+TD void update_seq(DocT<T> &d, int msn, int seq) {
     if (!(d.cur_seq <= seq)) {
         fail(d, MT_DOC_SEQ_ORDER);
         return;
@@ -1130,9 +1369,10 @@ __device__ void update_seq(Doc &d, int msn, int seq) {
 }
 
 // Client.applyMsg MT/client.ts:797-819 for one encoded record
-__device__ void apply_op(Doc &d, const mt_op_rec &op, const uint16_t *tin, const uint32_t *pin) {
+TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    const mt_op_rec &op = in.op;
     if (op.kind == MT_OP_INSERT) {
-        op_insert(d, op, tin, pin);
+        op_insert(d, in, tin, pin);
     } else if (op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE) {
         op_range(d, op, pin);
     }

@@ -15,6 +15,28 @@
 // Initial document contents (Client.insertSegmentLocal before collaboration: seq 0,
 // client LocalClientId -1; MT/client.ts:202-215) and collaboration start
 // (MT/mergeTree.ts:1287-1304): one leaf block under the root.
+__device__ static void init_doc_hdr(const DevState &st, int doc, int len) {
+    DocHdr h;
+    memset(&h, 0, sizeof(h));
+    h.depth = 1;
+    h.n_blk[0] = 1;
+    h.text_top = len;
+    h.props_top = 1;
+    h.next_uid = 1;
+    h.delta_hash = MT_FNV_OFF;
+    h.status = len > st.T ? MT_DOC_CAPACITY : 0;
+    const size_t S = st.S;
+    if (len > 0) {
+        h.n_seg = 1;
+        st.segA[doc * S] = v4i{len, 0, MT_RSEQ_NONE, pack_cli(-1, 0)};
+        st.segO[doc * S] = 0ull;
+        st.segB[doc * S] = v4u{0u, 0u, 0u, 0u};
+    }
+    st.cnt[(size_t)doc * MT_LV * st.B] = len > 0 ? 1 : 0;
+    st.flg[(size_t)doc * st.B] = MT_SCOUR_UNDEF;
+    st.hdr[doc] = h;
+}
+
 __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *seed_off,
                                                   const uint16_t *seed) {
     const int doc = blockIdx.x;
@@ -24,43 +46,96 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
     uint16_t *text = st.text + (size_t)doc * 2 * st.T;
     for (int j = lane(); j < len && j < st.T; j += MT_WAVE) text[j] = seed[s0 + j];
     if (lane() == 0) {
-        DocHdr h;
-        memset(&h, 0, sizeof(h));
-        h.depth = 1;
-        h.n_blk[0] = 1;
-        h.text_top = len;
-        h.props_top = 1;
-        h.next_uid = 1;
-        h.delta_hash = MT_FNV_OFF;
-        h.status = len > st.T ? MT_DOC_CAPACITY : 0;
-        const size_t S = st.S;
-        if (len > 0) {
-            h.n_seg = 1;
-            st.segA[doc * S] = make_int4(len, 0, MT_RSEQ_NONE, pack_cli(-1, 0));
-            st.segO[doc * S] = 0ull;
-            st.segB[doc * S] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        st.cnt[(size_t)doc * MT_LV * st.B] = len > 0 ? 1 : 0;
-        st.flg[(size_t)doc * st.B] = MT_SCOUR_UNDEF;
-        st.hdr[doc] = h;
+        init_doc_hdr(st, doc, len);
+        st.retry[doc] = 0;
     }
 }
 
-// Client.applyMsg for every record of this document (one wavefront per document).
+// Per-launch LDS capacities of the tier (the HBM tier keeps only the B-tree counts in LDS).
+struct TierCaps {
+    int S, B, H;
+};
+
+// Client.applyMsg for every record of this document (one wavefront per document).  The
+// records are prefetched 64 at a time (lane l holds record k+l plus up to 8 payload units)
+// and broadcast with readlane, so no op waits on HBM latency.
+template <class T>
 __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec *ops,
                                                     const int64_t *off, const uint16_t *tin,
-                                                    const uint32_t *pin) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+                                                    const uint32_t *pin, TierCaps caps) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
-    Doc d;
-    load_doc(d, st, doc, smem);
-    const int64_t k0 = off[doc], k1 = off[doc + 1];
-    for (int64_t k = k0; k < k1 && d.status == 0; k++) {
-        const mt_op_rec op = ops[k];
-        apply_op(d, op, tin, pin);
+    if (!T::kLds && !st.retry[doc]) return;
+    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 0);
+    DocT<T> d;
+    if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
+        if (lane() == 0) st.retry[doc] = 1;
+        return;
     }
-    store_doc(d);
+    if (d.status) {
+        if (!T::kLds && lane() == 0) st.retry[doc] = 0;
+        return;
+    }
+    const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
+    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
+    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
+    const int64_t k0 = off[doc], k1 = off[doc + 1];
+    for (int64_t kb = k0; kb < k1 && d.status == 0; kb += MT_WAVE) {
+        const int64_t k = kb + lane();
+        v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        int nl = 0, pok = 0;
+        if (k < k1) {
+            r0 = o4[2 * k];
+            r1 = o4[2 * k + 1];
+            const int kind = (r1.w >> 16) & 0xFF, flags = ((uint32_t)r1.w >> 24) & 0xFF;
+            const int len = r1.x;
+            if (kind == MT_OP_INSERT && !(flags & MT_F_MARKER) && len > 0) {
+                const GLB_AS uint16_t *src = gt + (uint32_t)r1.y;
+                nl = src[len - 1] == '\n';
+                if (len <= 8) {
+                    pok = 1;
+                    uint32_t u[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) u[j] = j < len ? src[j] : 0u;
+                    w0 = u[0] | (u[1] << 16);
+                    w1 = u[2] | (u[3] << 16);
+                    w2 = u[4] | (u[5] << 16);
+                    w3 = u[6] | (u[7] << 16);
+                }
+            }
+        }
+        const int cnt = (int)min((int64_t)MT_WAVE, k1 - kb);
+        for (int j = 0; j < cnt && d.status == 0; j++) {
+            OpIn in;
+            in.op.seq = __builtin_amdgcn_readlane(r0.x, j);
+            in.op.ref_seq = __builtin_amdgcn_readlane(r0.y, j);
+            in.op.min_seq = __builtin_amdgcn_readlane(r0.z, j);
+            in.op.pos1 = __builtin_amdgcn_readlane(r0.w, j);
+            in.op.pos2 = __builtin_amdgcn_readlane(r1.x, j);
+            in.op.payload = (uint32_t)__builtin_amdgcn_readlane(r1.y, j);
+            in.op.props = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
+            const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane(r1.w, j);
+            in.op.client = (uint16_t)(cw & 0xFFFF);
+            in.op.kind = (uint8_t)((cw >> 16) & 0xFF);
+            in.op.flags = (uint8_t)(cw >> 24);
+            in.pay_lo = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w0, j) |
+                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w1, j) << 32);
+            in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
+                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
+            in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
+            in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
+            apply_op(d, in, gt, gp);
+        }
+    }
+    if (T::kLds && d.status == MT_DOC_RETRY) {
+        if (lane() == 0) st.retry[doc] = 1;
+        return;
+    }
+    if (!T::kLds && lane() == 0) st.retry[doc] = 0;
+    store_doc(d, st, doc);
 }
 
 // ---------------------------------------------------------------- synthetic generator
@@ -93,7 +168,7 @@ __host__ __device__ static inline uint32_t rng_next(Rng &r) {   // xoshiro128**
 __host__ __device__ static inline uint32_t rng_uniform(Rng &r, uint32_t n) {
     return (uint32_t)(((uint64_t)rng_next(r) * n) >> 32);
 }
-__device__ static uint32_t gen_props(Rng &r, const mt_gen_cfg &cfg, uint32_t *out) {
+__device__ static __forceinline__ uint32_t gen_props(Rng &r, const mt_gen_cfg &cfg, uint32_t *out) {
     const uint32_t nk = 1 + rng_uniform(r, (uint32_t)cfg.max_keys_per_op);
     uint32_t count = 0;
     for (uint32_t j = 0; j < nk; j++) {
@@ -101,6 +176,7 @@ __device__ static uint32_t gen_props(Rng &r, const mt_gen_cfg &cfg, uint32_t *ou
         const bool is_null = (uint64_t)rng_next(r) < cfg.p_null;
         const uint32_t val = rng_uniform(r, (uint32_t)cfg.n_values);
         bool dup = false;
+        gsync();
         for (uint32_t q = 0; q < count; q++)
             if (out[1 + 2 * q] == key) dup = true;   // lane 0 wrote these
         if (dup) continue;
@@ -108,27 +184,30 @@ __device__ static uint32_t gen_props(Rng &r, const mt_gen_cfg &cfg, uint32_t *ou
             out[1 + 2 * count] = key;
             out[2 + 2 * count] = is_null ? MT_VAL_NULL : (val | (val == 0 ? MT_VAL_FALSY_BIT : 0u));
         }
-        __syncthreads();
         count++;
     }
     if (lane() == 0) out[0] = count;
-    __syncthreads();
+    gsync();
     return 1 + 2 * count;
 }
 
 // Generates and applies cfg.ops messages per document (DESIGN.md "Synthetic op streams");
 // the view length each writer draws positions from is read off the live replica.
+template <class T>
 __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cfg, uint32_t doc_base,
                                                       mt_op_rec *ops_out, uint16_t *text_out,
                                                       uint32_t *props_out, int64_t tstride,
                                                       int64_t pstride, int32_t *fail_out,
-                                                      int32_t *dbg_len) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+                                                      int32_t *dbg_len, TierCaps caps) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
+    if (!T::kLds && !st.retry[doc]) return;
     const int W = cfg.writers;
-    int32_t *last_ref = (int32_t *)(smem + (MT_LV + 3) * st.B + 64 * 4);
-    int32_t *short_id = last_ref + (W + 1);
+    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 2 * (W + 1));
+    LDS_AS int32_t *last_ref = (LDS_AS int32_t *)(smem + L.offGen);
+    LDS_AS int32_t *short_id = last_ref + (W + 1);
     Rng rng;
     rng_init(rng, cfg.seed, (int)(doc_base + doc));
     // seed text (drawn exactly like the oracle / reference harness)
@@ -138,60 +217,47 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
         const uint16_t ch = (uint16_t)(97 + rng_uniform(rng, 26));
         if (lane() == 0) arena[i] = ch;
     }
-    if (lane() == 0) {
-        DocHdr h;
-        memset(&h, 0, sizeof(h));
-        h.depth = 1;
-        h.n_blk[0] = 1;
-        h.text_top = cfg.seed_len;
-        h.props_top = 1;
-        h.next_uid = 1;
-        h.delta_hash = MT_FNV_OFF;
-        const size_t S = st.S;
-        if (cfg.seed_len > 0) {
-            h.n_seg = 1;
-            st.segA[doc * S] = make_int4(cfg.seed_len, 0, MT_RSEQ_NONE, pack_cli(-1, 0));
-            st.segO[doc * S] = 0ull;
-            st.segB[doc * S] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        st.cnt[(size_t)doc * MT_LV * st.B] = cfg.seed_len > 0 ? 1 : 0;
-        st.flg[(size_t)doc * st.B] = MT_SCOUR_UNDEF;
-        st.hdr[doc] = h;
-    }
+    if (lane() == 0) init_doc_hdr(st, doc, cfg.seed_len);
     for (int j = lane(); j <= W; j += MT_WAVE) {
         last_ref[j] = 0;
         short_id[j] = 0;
     }
-    __syncthreads();
-    Doc d;
-    load_doc(d, st, doc, smem);
+    gsync();
+    DocT<T> d;
+    if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
+        if (lane() == 0) st.retry[doc] = 1;
+        return;
+    }
     int next_short = 1;
     int64_t tu = 0, pu = 0;
     const int64_t tb = (int64_t)doc * tstride, pb = (int64_t)doc * pstride;
-    for (int t = 1; t <= cfg.ops; t++) {
+    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)text_out;
+    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)props_out;
+    for (int t = 1; t <= cfg.ops && d.status == 0; t++) {
         const int k = 1 + (int)rng_uniform(rng, (uint32_t)W);
         int lo = max(last_ref[k], t - 1 - cfg.lag);
         if (lo < 0) lo = 0;
         const int r = lo + (int)rng_uniform(rng, (uint32_t)(t - 1 - lo + 1));
-        __syncthreads();
+        wsync<T>();
         if (lane() == 0) last_ref[k] = r;
-        __syncthreads();
+        wsync<T>();
         int msn = 0x7fffffff;
-        for (int j = 1; j <= W; j++) msn = min(msn, last_ref[j]);
+        for (int j = 1 + lane(); j <= W; j += MT_WAVE) msn = min(msn, last_ref[j]);
+        msn = -wave_max(-msn);
         int c = short_id[k];
         if (!c) {
             c = next_short++;
-            __syncthreads();
+            wsync<T>();
             if (lane() == 0) short_id[k] = c;
-            __syncthreads();
+            wsync<T>();
         }
         int vsum = 0;
         for (int base = 0; base < d.n; base += MT_WAVE) {
             const int i = base + lane();
-            if (i < d.n) {
-                const int4 a = d.A[i];
-                vsum += view_len(a, d.O[i], r, c);
-            }
+            v4i a;
+            u64 o;
+            load_ao(d, i, i < d.n, a, o);
+            vsum += i < d.n ? view_len(a, o, r, c) : 0;
         }
         const int len = wave_sum(vsum);
         if (dbg_len && lane() == 0) {
@@ -202,7 +268,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
             q[3] = c;
         }
         const uint32_t u = rng_next(rng);
-        mt_op_rec op;
+        OpIn in;
+        mt_op_rec &op = in.op;
         op.seq = t;
         op.ref_seq = r;
         op.min_seq = msn;
@@ -210,18 +277,28 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
         op.flags = 0;
         op.props = MT_NO_PROPS;
         op.payload = 0;
+        in.pay_ok = true;
+        in.nl = false;
+        u64 plo = 0, phi = 0;
         if (len == 0 || (uint64_t)u < cfg.p_insert) {
             op.kind = MT_OP_INSERT;
             op.pos1 = (int)rng_uniform(rng, (uint32_t)(len + 1));
             const int tl = 1 + (int)rng_uniform(rng, (uint32_t)cfg.text_max);
             op.pos2 = tl;
             op.payload = (uint32_t)(tb + tu);
+            uint16_t ch = 0;
             for (int j = 0; j < tl; j++) {
                 const uint32_t v = rng_next(rng);
-                uint16_t ch = (uint16_t)'\n';
+                ch = (uint16_t)'\n';
                 if ((uint64_t)v >= cfg.p_newline) ch = (uint16_t)(97 + rng_uniform(rng, 26));
                 if (lane() == 0) text_out[tb + tu + j] = ch;
+                if (j < 4)
+                    plo |= (u64)ch << (16 * j);
+                else if (j < 8)
+                    phi |= (u64)ch << (16 * (j - 4));
             }
+            in.nl = ch == '\n';
+            in.pay_ok = tl <= 8;
             tu += tl;
             if (cfg.p_insert_props > 0 && (uint64_t)rng_next(rng) < cfg.p_insert_props) {
                 op.props = (uint32_t)(pb + pu);
@@ -241,32 +318,41 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
                 pu += gen_props(rng, cfg, props_out + pb + pu);
             }
         }
+        in.pay_lo = plo;
+        in.pay_hi = phi;
         if (lane() == 0) ops_out[(int64_t)doc * cfg.ops + (t - 1)] = op;
-        __syncthreads();
-        apply_op(d, op, text_out, props_out);
-        if (d.status) {
-            if (lane() == 0) fail_out[doc] = d.status;
-            break;
-        }
+        gsync();
+        apply_op(d, in, gt, gp);
     }
-    store_doc(d);
+    if (T::kLds && d.status == MT_DOC_RETRY) {
+        if (lane() == 0) st.retry[doc] = 1;
+        return;
+    }
+    if (lane() == 0) {
+        if (d.status) fail_out[doc] = d.status;
+        if (!T::kLds) st.retry[doc] = 0;
+    }
+    store_doc(d, st, doc);
 }
 
 // ---------------------------------------------------------------- checksums
-__device__ static bool same_ordered(Doc &d, uint32_t ha, uint32_t hb) {
+struct SumCtx {
+    const uint32_t *props;
+};
+__device__ static bool same_ordered(const uint32_t *pr, uint32_t ha, uint32_t hb) {
     if (ha == 0 || hb == 0) return ha == hb;
     if (ha == hb) return true;
-    const uint32_t *a = prec(d, d.props_half, ha), *b = prec(d, d.props_half, hb);
+    const uint32_t *a = pr + (size_t)ha * MT_PREC, *b = pr + (size_t)hb * MT_PREC;
     if (a[0] != b[0]) return false;
     for (uint32_t i = 0; i < 2 * a[0]; i++)
         if (a[1 + i] != b[1 + i]) return false;
     return true;
 }
-__device__ static u64 fold_run(Doc &d, u64 h, uint32_t ph, int len) {
+__device__ static u64 fold_run(const uint32_t *pr, u64 h, uint32_t ph, int len) {
     h = fnv_u32(h, (uint32_t)len);
     h = fnv_u32(h, ph ? 1u : 0u);
     if (ph) {
-        const uint32_t *p = prec(d, d.props_half, ph);
+        const uint32_t *p = pr + (size_t)ph * MT_PREC;
         h = fnv_u32(h, p[0]);
         for (uint32_t i = 0; i < 2 * p[0]; i++) h = fnv_u32(h, p[1 + i]);
     }
@@ -274,32 +360,35 @@ __device__ static u64 fold_run(Doc &d, u64 h, uint32_t ph, int len) {
 }
 // mt_checksum per document (definitions: DESIGN.md "Checksums", oracle/mt_oracle.c).
 __global__ void __launch_bounds__(MT_WAVE) k_checksum(DevState st, mt_checksum *out) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
-    Doc d;
-    load_doc(d, st, doc, smem);
+    const DocHdr h = st.hdr[doc];
+    const size_t S = st.S;
+    const v4i *A = st.segA + doc * S;
+    const v4u *Bv = st.segB + doc * S;
+    const uint16_t *tb = st.text + ((size_t)doc * 2 + h.text_half) * st.T;
+    const uint32_t *pr = st.props + ((size_t)doc * 2 + h.props_half) * st.P * MT_PREC;
+    const int n = h.n_seg;
     int len = 0, ntext = 0;
-    for (int base = 0; base < d.n; base += MT_WAVE) {
+    for (int base = 0; base < n; base += MT_WAVE) {
         const int i = base + lane();
         int l = 0, t = 0;
-        if (i < d.n) {
-            const int4 a = d.A[i];
+        if (i < n) {
+            const v4i a = A[i];
             l = obs_len(a);
-            t = (d.Bv[i].z & MT_MARKER_BIT) ? 0 : l;
+            t = (Bv[i].z & MT_MARKER_BIT) ? 0 : l;
         }
         len += wave_sum(l);
         ntext += wave_sum(t);
     }
     if (lane() == 0) {
-        const uint16_t *tb = text_base(d, d.text_half);
         u64 th = fnv_u32(MT_FNV_OFF, (uint32_t)ntext), hk = MT_FNV_OFF, ph = MT_FNV_OFF;
         int g = 0, run_len = 0;
         bool have = false;
         uint32_t run_p = 0;
-        for (int i = 0; i < d.n; i++) {
-            const int4 a = d.A[i];
-            const uint4 b = d.Bv[i];
+        for (int i = 0; i < n; i++) {
+            const v4i a = A[i];
+            const v4u b = Bv[i];
             if (a.z != MT_RSEQ_NONE) continue;
             if (!(b.z & MT_MARKER_BIT)) {
                 for (int j = 0; j < a.x; j++) {
@@ -315,23 +404,23 @@ __global__ void __launch_bounds__(MT_WAVE) k_checksum(DevState st, mt_checksum *
                     }
                 }
             }
-            if (have && same_ordered(d, run_p, b.y)) {
+            if (have && same_ordered(pr, run_p, b.y)) {
                 run_len += a.x;
             } else {
-                if (have) ph = fold_run(d, ph, run_p, run_len);
+                if (have) ph = fold_run(pr, ph, run_p, run_len);
                 run_p = b.y;
                 run_len = a.x;
                 have = true;
             }
         }
         if (g & 63) th = fnv_u64(th, hk);
-        if (have) ph = fold_run(d, ph, run_p, run_len);
+        if (have) ph = fold_run(pr, ph, run_p, run_len);
         mt_checksum cs;
         cs.length = (uint32_t)len;
-        cs.n_segments = (uint32_t)d.n;
+        cs.n_segments = (uint32_t)n;
         cs.text_hash = th;
         cs.props_hash = ph;
-        cs.delta_hash = d.dhash;
+        cs.delta_hash = h.delta_hash;
         out[doc] = cs;
     }
 }
@@ -349,6 +438,7 @@ struct mt_handle {
     mt_checksum *d_sums = nullptr;
     int64_t *d_seed_off = nullptr;   // initial contents kept on device for mt_reset
     uint16_t *d_seed = nullptr;
+    TierCaps lds{0, 0, 0};           // LDS-tier capacities (S == 0: tier disabled)
 };
 struct mt_batch {
     int device = 0;
@@ -369,8 +459,9 @@ struct mt_batch {
         }                                                                          \
     } while (0)
 
-static size_t lds_bytes(const DevState &st, int extra_ints) {
-    return (size_t)(MT_LV + 3) * st.B + 64 * 4 + (size_t)extra_ints * 4;
+static TierCaps glb_caps(const mt_handle *h) { return TierCaps{0, h->st.B, 0}; }
+static size_t tier_lds_bytes(bool seg_in_lds, const TierCaps &c, int gen_words) {
+    return lds_layout(seg_in_lds, c.S, c.B, c.H, gen_words).total;
 }
 
 extern "C" {
@@ -396,6 +487,14 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.T = o.text_capacity > 0 ? o.text_capacity : 32768;
     st.P = o.props_capacity > 0 ? o.props_capacity : st.S + 2 * MT_WAVE;
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
+    if (o.lds_seg_capacity >= 0) {
+        int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 128;
+        S_l = std::min(S_l, st.S);
+        h->lds.S = S_l;
+        h->lds.B = std::min(st.B, std::max(64, (S_l / 2 + 15) / 16 * 16));
+        h->lds.H = std::min(st.H, S_l);
+        if (tier_lds_bytes(true, h->lds, 0) > 60 * 1024) h->lds = TierCaps{0, 0, 0};
+    }
     const size_t N = n_docs;
     bool ok = true;
     auto alloc = [&](void **p, size_t bytes) {
@@ -413,6 +512,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.props, N * 2 * (size_t)st.P * MT_PREC * sizeof(uint32_t));
     if (st.DL) alloc((void **)&st.dlog, N * (size_t)st.DL * sizeof(int32_t));
     alloc((void **)&h->d_sums, N * sizeof(mt_checksum));
+    alloc((void **)&st.retry, N * sizeof(int32_t));
     if (!ok || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         mt_destroy(h);
@@ -430,7 +530,7 @@ void mt_destroy(mt_handle *h) {
     hipSetDevice(h->device);
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
-                  h->d_seed_off, h->d_seed};
+                  h->d_seed_off, h->d_seed, st.retry};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -505,8 +605,17 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     if (!h || !b || b->n_docs != h->n_docs) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    hipLaunchKernelGGL(k_replay, dim3(h->n_docs), dim3(MT_WAVE), lds_bytes(h->st, 0), h->stream, h->st,
-                       b->ops, b->off, b->text, b->props);
+    if (h->lds.S > 0) {
+        // LDS tier for every document; the ones that outgrow it are flagged and replayed
+        // from HBM by the second launch (whose other workgroups exit at once)
+        hipLaunchKernelGGL(k_replay<TierLds>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
+        HIPCHK(h, hipGetLastError());
+    } else {
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream));
+    }
+    hipLaunchKernelGGL(k_replay<TierGlb>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+                       h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -581,11 +690,21 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
              hipMemset(d_fail, 0, N * 4) == hipSuccess;
     }
     if (ok) {
-        const size_t lds = lds_bytes(h->st, 2 * (cfg->writers + 1));
-        hipLaunchKernelGGL(k_generate, dim3(h->n_docs), dim3(MT_WAVE), lds, h->stream, h->st, *cfg,
-                           doc_index_base, b->ops, b->text, b->props, tstride, pstride, d_fail,
-                           d_trace);
-        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+        const int gw = 2 * (cfg->writers + 1);
+        if (h->lds.S > 0) {
+            hipLaunchKernelGGL(k_generate<TierLds>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, gw),
+                               h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
+                               pstride, d_fail, d_trace, h->lds);
+            ok = hipGetLastError() == hipSuccess;
+        } else {
+            ok = hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream) == hipSuccess;
+        }
+        if (ok) {
+            hipLaunchKernelGGL(k_generate<TierGlb>, dim3(h->n_docs), dim3(MT_WAVE),
+                               tier_lds_bytes(false, glb_caps(h), gw), h->stream, h->st, *cfg, doc_index_base,
+                               b->ops, b->text, b->props, tstride, pstride, d_fail, d_trace, glb_caps(h));
+            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+        }
     }
     if (ok) {
         std::vector<int32_t> f(N);
@@ -845,7 +964,7 @@ int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uin
 int mt_checksums_device(mt_handle *h, void *device_out) {
     if (!h || !device_out) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    hipLaunchKernelGGL(k_checksum, dim3(h->n_docs), dim3(MT_WAVE), lds_bytes(h->st, 0), h->stream, h->st,
+    hipLaunchKernelGGL(k_checksum, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st,
                        (mt_checksum *)device_out);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(h->stream));

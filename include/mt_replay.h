@@ -45,6 +45,9 @@ typedef struct mt_options {
     int32_t text_capacity;   /* UTF-16 units per document text arena half (default 32768) */
     int32_t props_capacity;  /* property-set records per document   (default seg) */
     int32_t delta_log_capacity; /* int32 words of per-document delta log; 0 = hash only */
+    int32_t lds_seg_capacity;   /* segments a document may hold while staged in LDS
+                                   (default 128; -1 = always replay from HBM).  A document
+                                   that outgrows it is replayed from HBM transparently. */
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

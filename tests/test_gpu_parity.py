@@ -24,12 +24,15 @@ def _gpu_outputs(mt, doc):
                 deltas=mt.get_delta_log(doc), status=int(mt.status()[doc]))
 
 
+# lds_seg_capacity: 0 = default LDS tier (large documents retried from HBM), -1 = HBM tier
+# only, 16 = tiny LDS tier (most documents overflow mid-batch and are replayed from HBM)
+@pytest.mark.parametrize("lds", [0, -1, 16])
 @pytest.mark.parametrize("name", gu.ALL_FIXTURES)
-def test_gpu_matches_reference(name):
+def test_gpu_matches_reference(name, lds):
     fx = gu.load(name)
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
-    mt = _gpu_batch(len(fx["docs"]))
+    mt = _gpu_batch(len(fx["docs"]), lds_seg_capacity=lds)
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     bad = []
@@ -79,13 +82,14 @@ def test_gpu_split_batches_equal_single_batch(oracle_lib):
     assert np.array_equal(s1, s2)
 
 
+@pytest.mark.parametrize("lds", [0, -1])
 @pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6)])
-def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs):
+def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, lds):
     import json
     import os
     cfg = json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))[cfgname]
     cfg = dict(cfg, ops=ops)
-    mt = _gpu_batch(docs)
+    mt = _gpu_batch(docs, lds_seg_capacity=lds)
     b = mt.generate(cfg)
     got = b.download()
     gsums = mt.checksums()
