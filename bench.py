@@ -51,7 +51,7 @@ def capacities(cfg):
         return dict(seg_capacity=8192, text_capacity=1 << 16, heap_capacity=8192, props_capacity=8192 + 256)
     if cfg["ops"] > 4000:
         return dict(seg_capacity=1024, text_capacity=1 << 15, heap_capacity=2048, props_capacity=1024 + 128)
-    return dict(seg_capacity=512, text_capacity=1 << 14, heap_capacity=1024, props_capacity=512 + 128)
+    return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
 
 def main():
@@ -112,6 +112,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    hbm_docs = mt.last_hbm_docs()
     status = mt.status()
     sums = mt.checksums()
     replay_consistent = bool(np.array_equal(sums, gen_sums)) and int((status != 0).sum()) == 0
@@ -200,6 +201,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
             "kernel": "k_replay", "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
+            "docs_replayed_from_hbm": hbm_docs,
         },
         "cpu_baseline": cpu,
         "parity": {"replay_equals_generation": replay_consistent, "oracle_sample": parity,

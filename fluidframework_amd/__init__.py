@@ -91,6 +91,13 @@ class MergeTreeBatch:
     def sync(self):
         self._check(self.lib.mt_sync(self.h), "mt_sync")
 
+    def last_hbm_docs(self):
+        """Documents of the last batch replayed from HBM (outgrew the LDS tier)."""
+        out = np.zeros(8, dtype=np.uint32)
+        self._check(self.lib.mt_last_hbm_docs(self.h, _native.ptr(out)), "mt_last_hbm_docs")
+        return dict(total=int(out[0]), spilled=int(out[1]), segments=int(out[2]), blocks=int(out[3]), heap=int(out[4]),
+                    text=int(out[5]), props=int(out[6]), at_load=int(out[7]))
+
     def last_kernel_ms(self):
         return float(self.lib.mt_last_kernel_ms(self.h))
 
@@ -156,6 +163,16 @@ class MergeTreeBatch:
             if s <= pos < s + l:
                 return p
         return None
+
+    def debug_raw(self, doc):
+        """Raw segment records (n x 8 u32: segA, segB) and the 32-word document header."""
+        n = ctypes.c_uint32()
+        hdr = np.zeros(32, dtype=np.int32)
+        self._check(self.lib.mt_debug_raw(self.h, doc, None, 0, ctypes.byref(n), _native.ptr(hdr)), "mt_debug_raw")
+        rows = np.zeros((max(n.value, 1), 8), dtype=np.uint32)
+        self._check(self.lib.mt_debug_raw(self.h, doc, _native.ptr(rows), n.value, ctypes.byref(n), None),
+                    "mt_debug_raw")
+        return rows[:n.value], hdr
 
     def get_delta_log(self, doc):
         n = ctypes.c_uint32()

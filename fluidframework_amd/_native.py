@@ -46,6 +46,7 @@ SIGNATURES = [
     ("mt_batch_free", None, [_P]),
     ("mt_sync", _I, [_P]),
     ("mt_last_kernel_ms", ctypes.c_float, [_P]),
+    ("mt_last_hbm_docs", _I, [_P, _P]),
     ("mt_generate", _P, [_P, _P, _U32, _P]),
     ("mt_generated_seeds", _I, [_P, _P, _U32, _P, _P]),
     ("mt_batch_sizes", _I, [_P, _P, _P, _P]),
@@ -57,6 +58,7 @@ SIGNATURES = [
     ("mt_get_segments", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
     ("mt_get_segment_props", _I, [_P, _U32, _U32, _P, _U32, _P]),
     ("mt_get_delta_log", _I, [_P, _U32, _P, _U32, _P]),
+    ("mt_debug_raw", _I, [_P, _U32, _P, _U32, _P, _P]),
     ("mt_checksums", _I, [_P, _P]),
     ("mt_checksums_device", _I, [_P, _P]),
 ]

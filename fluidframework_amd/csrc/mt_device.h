@@ -62,7 +62,9 @@ struct DevState {
     uint16_t *text;
     uint32_t *props;
     int32_t *dlog;
-    int32_t *retry;           // per document: replay this batch in the HBM tier
+    int32_t *retry;           // per document: replay (the rest of) this batch in the HBM tier
+    int64_t *resume;          // per document: first op the HBM tier replays
+    uint32_t *stats;          // [0]: documents replayed in the HBM tier by the last launch
     int32_t S, B, H, T, P, DL;
     int32_t n_docs;
 };

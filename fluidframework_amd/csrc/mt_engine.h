@@ -49,6 +49,8 @@ template <class T> __device__ __forceinline__ void wsync() {
 // segB.w flags
 #define SEGF_NL_KNOWN 1u   // SEGF_NL is valid
 #define SEGF_NL 2u         // the segment's text ends with '\n' (TextSegment.canAppend :63-68)
+#define SEGF_SLACK_SHIFT 16 // bits 16..31: arena units reserved after the text for appends
+__device__ __forceinline__ int text_slack(int len) { return min((len >> 1) + 8, 4096); }
 
 __device__ static const uint32_t kEmptyPropsRec = 0u;
 
@@ -70,7 +72,7 @@ template <class T> struct DocT {
     LDS_AS int32_t *nb;     // [MT_LV] blocks per level
     // scalars (uniform)
     int n, depth, heap_n, cur_seq, min_seq, text_top, text_half, props_top, props_half, next_uid,
-        status, dlog_n, text_gcs, props_gcs;
+        status, dlog_n, text_gcs, props_gcs, cap_cause;
     u64 dhash;
 };
 
@@ -105,7 +107,11 @@ TD void fail(DocT<T> &d, int code) {
     if (d.status == 0) d.status = code;
 }
 // Out of a capacity: the LDS tier hands the document to the HBM tier, which reports it.
-TD void fail_cap(DocT<T> &d) { fail(d, T::kLds ? MT_DOC_RETRY : MT_DOC_CAPACITY); }
+// cause (diagnostic): 1 segments, 2 blocks, 3 heap, 4 text, 5 property records
+TD void fail_cap(DocT<T> &d, int cause) {
+    if (d.status == 0) d.cap_cause = cause;
+    fail(d, T::kLds ? MT_DOC_RETRY : MT_DOC_CAPACITY);
+}
 
 TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) { return d.cnt + l * d.B_cap; }
 TD GLB_AS uint16_t *text_base(DocT<T> &d, int half) { return d.text + (size_t)half * d.T_cap; }
@@ -149,6 +155,7 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.dhash = h.delta_hash;
     d.text_gcs = 0;
     d.props_gcs = 0;
+    d.cap_cause = 0;
     if (d.status) return true;   // failed earlier: the caller leaves it untouched
     int maxnb = 0;
 #pragma unroll
@@ -159,6 +166,7 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
         d.H_cap = H_l;
         if (d.n > S_l || maxnb > B_l || d.heap_n > H_l) {
             d.status = MT_DOC_RETRY;
+            d.cap_cause = 6;
             return false;
         }
         d.A = (typename T::A_t)(smem + L.offA);
@@ -383,7 +391,7 @@ TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
 TD void blk_split_up(DocT<T> &d, int l, int b) {
     while (true) {
         if (d.nb[l] + 1 > d.B_cap) {
-            fail_cap(d);
+            fail_cap(d, 2);
             return;
         }
         const bool has_parent = l + 1 < d.depth;
@@ -405,7 +413,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
         if (!has_parent) {
             const int nl = d.depth;
             if (nl >= MT_LV) {
-                fail_cap(d);
+                fail_cap(d, 2);
                 return;
             }
             d.depth++;
@@ -430,7 +438,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
 // `extra`), as pack :1414-1446 does; new level-0 blocks have needsScour undefined.
 TD void blk_replace(DocT<T> &d, int l, int b0, int nold, int k, int base, int extra) {
     if (d.nb[l] + (k - nold) > d.B_cap) {
-        fail_cap(d);
+        fail_cap(d, 2);
         return;
     }
     blk_shift(d, l, b0 + nold, k - nold);
@@ -473,7 +481,7 @@ TD int block_of(DocT<T> &d, int i, int nb) {
 // Collections.Heap add/get (MT/collections.ts:212-265); touched by lane 0 only.
 TD void heap_add(DocT<T> &d, int max_seq, int uid) {
     if (d.heap_n + 1 > d.H_cap) {
-        fail_cap(d);
+        fail_cap(d, 3);
         return;
     }
     d.heap_n++;
@@ -550,10 +558,6 @@ TD void copy_text(GLB_AS uint16_t *dst, const GLB_AS uint16_t *src, int n) {
 }
 // Compact all live text (non-removed TextSegments) into the other half, document order.
 TD void text_gc(DocT<T> &d) {
-    if (T::kLds && d.text_gcs > 0) {   // a second flip would overwrite the saved half
-        fail_cap(d);
-        return;
-    }
     d.text_gcs++;
     gsync();
     const int dh = 1 - d.text_half;
@@ -580,7 +584,12 @@ TD void text_gc(DocT<T> &d) {
             copy_text<T>(dst + oj, src + sj, lj);
         }
         wsync<T>();
-        if (live) d.Bv[i].x = (uint32_t)off;
+        if (live) {
+            v4u nb = b;
+            nb.x = (uint32_t)off;
+            nb.w &= 0xFFFFu;   // compaction drops the append slack
+            d.Bv[i] = nb;
+        }
         carry += bcast(inc, MT_WAVE - 1);
     }
     d.text_half = dh;
@@ -592,16 +601,12 @@ TD bool text_ensure(DocT<T> &d, int need) {
     text_gc(d);
     if (d.status) return false;
     if (d.text_top + need <= d.T_cap) return true;
-    fail_cap(d);
+    fail_cap(d, 4);
     return false;
 }
 
 // ------------------------------------------------------------------ property records
 TD void props_gc(DocT<T> &d) {
-    if (T::kLds && d.props_gcs > 0) {
-        fail_cap(d);
-        return;
-    }
     d.props_gcs++;
     gsync();
     const int dh = 1 - d.props_half;
@@ -633,7 +638,7 @@ TD bool props_ensure(DocT<T> &d, int need) {
     props_gc(d);
     if (d.status) return false;
     if (d.props_top + need <= d.P_cap) return true;
-    fail_cap(d);
+    fail_cap(d, 5);
     return false;
 }
 // Properties.matchProperties MT/properties.ts:61-92 over interned ids
@@ -691,7 +696,7 @@ TD void cb_log(DocT<T> &d, int32_t v) {
 // The left half's last character is unknown until a scour needs it.
 TD void split_seg(DocT<T> &d, int i, int q) {
     if (d.n + 1 > d.S_cap) {
-        fail_cap(d);
+        fail_cap(d, 1);
         return;
     }
     int bstart;
@@ -710,7 +715,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
         v4u rb = bb;
         rb.x = bb.x + (uint32_t)q;
         rb.z = (uint32_t)d.next_uid | (bb.z & MT_MARKER_BIT);
-        bb.w &= ~(SEGF_NL_KNOWN | SEGF_NL);
+        bb.w &= ~(SEGF_NL_KNOWN | SEGF_NL | (0xFFFFu << SEGF_SLACK_SHIFT));
         d.A[i] = a;
         d.Bv[i] = bb;
         d.A[i + 1] = r;
@@ -802,7 +807,6 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     // plan (lane 0): scr[k] = -2 keep, -1 unlink, >=0 append into that local index
     LDS_AS int *plan = d.scr;
     LDS_AS int *glen = d.scr + 16;  // merged length per keeper
-    LDS_AS int *gw = d.scr + 32;    // merged flags per keeper
     int need = 0;
     if (lane() == 0) {
         int prev = -1;
@@ -815,7 +819,6 @@ TD int scour_block(DocT<T> &d, int s, int e) {
             const v4u b = d.Bv[s + k];
             const bool mk = (b.z & MT_MARKER_BIT) != 0;
             glen[k] = a.x;
-            gw[k] = (int)b.w;
             if (a.z != MT_RSEQ_NONE) {
                 plan[k] = (a.z > d.min_seq) ? -2 : -1;
                 prev = -1;
@@ -829,7 +832,6 @@ TD int scour_block(DocT<T> &d, int s, int e) {
                     pend = pend == (int)b.x ? (int)b.x + a.x : -1;
                     plen += a.x;
                     glen[prev] = plen;
-                    gw[prev] = (int)b.w;
                     pnl = nl;
                 } else {
                     plan[k] = -2;
@@ -849,51 +851,85 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     wsync<T>();
     need = bcast(need, 0);
     if (need) {
-        // total length of the groups (upper bound of what gets copied)
+        // upper bound of what the merges below allocate (group text + slack)
         int tot = 0;
         for (int k = 0; k < cntb; k++)
-            if (plan[k] == -2) tot += glen[k];
+            if (plan[k] == -2) tot += glen[k] + text_slack(glen[k]);
         if (!text_ensure(d, tot)) return cntb;
         gsync();
     }
-    // execute text merges group by group (uniform loops; cntb <= 8)
+    // execute text merges group by group (uniform loops; cntb <= 8).  A keeper copied to
+    // the arena top reserves slack after its text so that later appends land in place
+    // (TextSegment.append :70-85 is a string concatenation; this keeps it amortised O(1)).
+    LDS_AS int *psrc = d.scr + 48;   // gather pieces of one group: source offset, length
+    LDS_AS int *plen = d.scr + 56;
     for (int k = 0; k < cntb; k++) {
         if (plan[k] != -2 || glen[k] == d.A[s + k].x) continue;
-        // keeper k with appended followers
         const v4u bk = d.Bv[s + k];
         const v4i ak = d.A[s + k];
+        const uint32_t kslack = bk.w >> SEGF_SLACK_SHIFT;
         bool contig = true;
-        int endp = (int)bk.x + ak.x;
+        int endp = (int)bk.x + ak.x, add = 0;
+        uint32_t lastw = 0;   // the last appended segment's flags (read after any text_gc)
         for (int j = k + 1; j < cntb && plan[j] == k; j++) {
             const v4u bj = d.Bv[s + j];
+            const int lj = d.A[s + j].x;
             if ((int)bj.x != endp) contig = false;
-            endp += d.A[s + j].x;
+            endp += lj;
+            add += lj;
+            lastw = bj.w;
         }
-        GLB_AS uint16_t *tb = text_base(d, d.text_half);
-        uint32_t newoff = bk.x;
+        uint32_t newoff = bk.x, newslack = lastw >> SEGF_SLACK_SHIFT;
         if (!contig) {
-            int dst;
-            if ((int)bk.x + ak.x == d.text_top) {
+            int dst, np = 0, ntot = 0;
+            if ((uint32_t)add <= kslack) {                       // append into the slack
+                dst = (int)bk.x + ak.x;
+                newslack = kslack - (uint32_t)add;
+            } else if ((int)bk.x + ak.x == d.text_top) {        // keeper ends at the top
                 dst = d.text_top;
-            } else {
+                newslack = (uint32_t)text_slack(glen[k]);
+                d.text_top += add + (int)newslack;
+            } else {                                            // move keeper + appends
                 newoff = (uint32_t)d.text_top;
-                copy_text<T>(tb + d.text_top, tb + bk.x, ak.x);
-                dst = d.text_top + ak.x;
+                dst = d.text_top;
+                newslack = (uint32_t)text_slack(glen[k]);
+                d.text_top += glen[k] + (int)newslack;
+                if (lane() == 0) {
+                    psrc[0] = (int)bk.x;
+                    plen[0] = ak.x;
+                }
+                np = 1;
+                ntot = ak.x;
             }
             for (int j = k + 1; j < cntb && plan[j] == k; j++) {
-                const v4u bj = d.Bv[s + j];
-                const int lj = d.A[s + j].x;
-                copy_text<T>(tb + dst, tb + bj.x, lj);
-                dst += lj;
+                if (lane() == 0) {
+                    psrc[np] = (int)d.Bv[s + j].x;
+                    plen[np] = d.A[s + j].x;
+                }
+                ntot += d.A[s + j].x;
+                np++;
             }
-            d.text_top = dst;
+            wsync<T>();
+            GLB_AS uint16_t *tb = text_base(d, d.text_half);
+            for (int base = 0; base < ntot; base += MT_WAVE) {   // one gather per 64 units
+                const int t = base + lane();
+                int src = -1, pre = 0;
+                for (int q = 0; q < np; q++) {
+                    const int lq = plen[q];
+                    if (src < 0 && t < pre + lq) src = psrc[q] + (t - pre);
+                    pre += lq;
+                }
+                uint16_t ch = 0;
+                if (t < ntot) ch = tb[src];
+                if (t < ntot) tb[dst + t] = ch;
+            }
         }
         wsync<T>();
         if (lane() == 0) {
             d.A[s + k].x = glen[k];
             v4u nb = bk;
             nb.x = newoff;
-            nb.w = (uint32_t)gw[k];
+            nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | (newslack << SEGF_SLACK_SHIFT);
             d.Bv[s + k] = nb;
         }
         wsync<T>();
@@ -1003,6 +1039,24 @@ TD void zamboni(DocT<T> &d) {
 }
 
 // ------------------------------------------------------------------ ops
+// LDS tier: is there room for one more message of this kind without overflowing the LDS
+// capacities mid-message?  Bounds: an op adds <= 3 segments (2 boundary splits + 1
+// insert), each of which may split one block per level; every pack (<= 2 zamboni scours
+// per call, <= 2 calls per message) can grow a level by <= 6 blocks; an insert adds <= 1
+// heap entry, a range op <= one per leaf block.  A message that fails this check is handed
+// to the HBM tier *before* it is applied (the LDS state is spilled first), so the LDS tier
+// never has to roll back.
+TD bool lds_room(DocT<T> &d, const mt_op_rec &op) {
+    if (d.n + 3 > d.S_cap) return false;
+    if (d.depth + 2 > MT_LV) return false;
+    const int nb0 = d.nb[0];
+    int need_heap = op.kind == MT_OP_INSERT ? 1 : nb0 + 3;
+    if (d.heap_n + need_heap > d.H_cap) return false;
+    bool ok = true;
+    for (int l = 0; l < d.depth; l++) ok = ok && d.nb[l] + 3 + 24 <= d.B_cap;
+    return ok;
+}
+
 // One sequenced message as the engine consumes it: the record plus (prefetched) the first
 // 8 UTF-16 units of an insert's payload and whether the payload ends with '\n'.
 struct OpIn {
@@ -1073,7 +1127,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         return;
     }
     if (d.n + 1 > d.S_cap) {
-        fail_cap(d);
+        fail_cap(d, 1);
         return;
     }
     if (!marker && !text_ensure(d, slen)) return;

@@ -54,11 +54,17 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
 // Per-launch LDS capacities of the tier (the HBM tier keeps only the B-tree counts in LDS).
 struct TierCaps {
     int S, B, H;
+    int resume;   // TierGlb: start from resume[doc] (documents handed over by the LDS tier)
 };
 
 // Client.applyMsg for every record of this document (one wavefront per document).  The
 // records are prefetched 64 at a time (lane l holds record k+l plus up to 8 payload units)
 // and broadcast with readlane, so no op waits on HBM latency.
+//
+// TierLds: the document is staged in LDS; before each message lds_room() checks that the
+// LDS capacities cannot overflow while applying it.  If they could, the LDS state is
+// spilled to HBM and the document continues from that message in the TierGlb launch
+// (retry[doc] = 1, resume[doc] = message index).
 template <class T>
 __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec *ops,
                                                     const int64_t *off, const uint16_t *tin,
@@ -68,10 +74,17 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     if (!T::kLds && !st.retry[doc]) return;
+    if (!T::kLds && lane() == 0) atomicAdd(st.stats, 1u);
     const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 0);
+    const int64_t k1 = off[doc + 1];
+    const int64_t k0 = (T::kLds || !caps.resume) ? off[doc] : st.resume[doc];
     DocT<T> d;
     if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
-        if (lane() == 0) st.retry[doc] = 1;
+        if (lane() == 0) {
+            st.retry[doc] = 1;
+            st.resume[doc] = k0;
+            atomicAdd(st.stats + 1 + d.cap_cause, 1u);
+        }
         return;
     }
     if (d.status) {
@@ -81,8 +94,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
     const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
-    const int64_t k0 = off[doc], k1 = off[doc + 1];
-    for (int64_t kb = k0; kb < k1 && d.status == 0; kb += MT_WAVE) {
+    int64_t spill_at = -1;
+    for (int64_t kb = k0; kb < k1 && d.status == 0 && spill_at < 0; kb += MT_WAVE) {
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
         uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
@@ -121,6 +134,10 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
             in.op.client = (uint16_t)(cw & 0xFFFF);
             in.op.kind = (uint8_t)((cw >> 16) & 0xFF);
             in.op.flags = (uint8_t)(cw >> 24);
+            if (T::kLds && !lds_room(d, in.op)) {
+                spill_at = kb + j;
+                break;
+            }
             in.pay_lo = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w0, j) |
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w1, j) << 32);
             in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
@@ -131,8 +148,16 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
         }
     }
     if (T::kLds && d.status == MT_DOC_RETRY) {
-        if (lane() == 0) st.retry[doc] = 1;
-        return;
+        // an LDS capacity overflowed mid-message despite lds_room(): not resumable
+        d.status = MT_DOC_CAPACITY;
+        if (lane() == 0) atomicAdd(st.stats + 1 + d.cap_cause, 1u);
+    }
+    if (T::kLds && spill_at >= 0) {
+        if (lane() == 0) {
+            st.retry[doc] = 1;
+            st.resume[doc] = spill_at;
+            atomicAdd(st.stats + 1, 1u);
+        }
     }
     if (!T::kLds && lane() == 0) st.retry[doc] = 0;
     store_doc(d, st, doc);
@@ -438,7 +463,7 @@ struct mt_handle {
     mt_checksum *d_sums = nullptr;
     int64_t *d_seed_off = nullptr;   // initial contents kept on device for mt_reset
     uint16_t *d_seed = nullptr;
-    TierCaps lds{0, 0, 0};           // LDS-tier capacities (S == 0: tier disabled)
+    TierCaps lds{0, 0, 0, 0};        // LDS-tier capacities (S == 0: tier disabled)
 };
 struct mt_batch {
     int device = 0;
@@ -459,7 +484,7 @@ struct mt_batch {
         }                                                                          \
     } while (0)
 
-static TierCaps glb_caps(const mt_handle *h) { return TierCaps{0, h->st.B, 0}; }
+static TierCaps glb_caps(const mt_handle *h) { return TierCaps{0, h->st.B, 0, h->lds.S > 0 ? 1 : 0}; }
 static size_t tier_lds_bytes(bool seg_in_lds, const TierCaps &c, int gen_words) {
     return lds_layout(seg_in_lds, c.S, c.B, c.H, gen_words).total;
 }
@@ -493,7 +518,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         h->lds.S = S_l;
         h->lds.B = std::min(st.B, std::max(64, (S_l / 2 + 15) / 16 * 16));
         h->lds.H = std::min(st.H, S_l);
-        if (tier_lds_bytes(true, h->lds, 0) > 60 * 1024) h->lds = TierCaps{0, 0, 0};
+        if (tier_lds_bytes(true, h->lds, 0) > 60 * 1024) h->lds = TierCaps{0, 0, 0, 0};
     }
     const size_t N = n_docs;
     bool ok = true;
@@ -513,6 +538,8 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     if (st.DL) alloc((void **)&st.dlog, N * (size_t)st.DL * sizeof(int32_t));
     alloc((void **)&h->d_sums, N * sizeof(mt_checksum));
     alloc((void **)&st.retry, N * sizeof(int32_t));
+    alloc((void **)&st.resume, N * sizeof(int64_t));
+    alloc((void **)&st.stats, 16 * sizeof(uint32_t));
     if (!ok || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         mt_destroy(h);
@@ -530,7 +557,7 @@ void mt_destroy(mt_handle *h) {
     hipSetDevice(h->device);
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
-                  h->d_seed_off, h->d_seed, st.retry};
+                  h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -604,6 +631,7 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
 int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     if (!h || !b || b->n_docs != h->n_docs) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     if (h->lds.S > 0) {
         // LDS tier for every document; the ones that outgrow it are flagged and replayed
@@ -648,6 +676,14 @@ int mt_sync(mt_handle *h) {
 }
 
 float mt_last_kernel_ms(const mt_handle *h) { return h ? h->last_ms : 0.f; }
+
+int mt_last_hbm_docs(mt_handle *h, uint32_t *out) {
+    if (!h || !out) return MT_E_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(out, h->st.stats, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return 0;
+}
 
 int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, uint64_t n_ops,
                  const uint16_t *text, uint64_t text_len, const uint32_t *props,
@@ -922,6 +958,22 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
     const int nb0 = hd.hdr.n_blk[0];
     for (int b = 0; b < nb0 && leaves && (uint32_t)b < cap_leaves; b++) leaves[b] = hd.cnt[b];
     if (n_leaves) *n_leaves = (uint32_t)nb0;
+    return 0;
+}
+
+// Debug: raw segment records (segA, segB as 8 u32 per segment) and header words.
+int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, uint32_t *n_rows,
+                 int32_t *hdr_words) {
+    HostDoc hd;
+    int rc = fetch_doc(h, doc, hd, false, false);
+    if (rc) return rc;
+    const int n = hd.hdr.n_seg;
+    for (int i = 0; i < n && rows && (uint32_t)i < cap_rows; i++) {
+        memcpy(rows + 8 * i, &hd.A[i], 16);
+        memcpy(rows + 8 * i + 4, &hd.B[i], 16);
+    }
+    if (n_rows) *n_rows = (uint32_t)n;
+    if (hdr_words) memcpy(hdr_words, &hd.hdr, sizeof(DocHdr));
     return 0;
 }
 

@@ -91,6 +91,10 @@ void mt_batch_free(mt_batch *b);
 int mt_sync(mt_handle *h);
 /* Device time of the most recent replay kernel (HIP events on the handle's stream). */
 float mt_last_kernel_ms(const mt_handle *h);
+/* Documents of the most recent batch that outgrew the LDS tier and were replayed from HBM:
+   out[8] = {total, spilled before a message, segments, blocks, heap, text, property
+   records, at load} (the causes count LDS capacities hit inside a message). */
+int mt_last_hbm_docs(mt_handle *h, uint32_t *out);
 
 /* Generates ops_per_doc synthetic messages per document on the device, applying them as
    it goes (the generator reads each writer's view length from the live replica), and
@@ -124,6 +128,9 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
                     uint32_t *n_rows, int32_t *leaves, uint32_t cap_leaves, uint32_t *n_leaves);
 int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_t *pairs,
                          uint32_t cap_pairs, int32_t *n_pairs);
+/* Debug: raw segment records (8 u32 per segment: segA then segB) and the 32-word header. */
+int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, uint32_t *n_rows,
+                 int32_t *hdr_words);
 /* Delta log (only with delta_log_capacity > 0), oracle layout. */
 int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uint32_t *n);
 
