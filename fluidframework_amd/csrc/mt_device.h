@@ -72,29 +72,32 @@ struct DevState {
 // ------------------------------------------------------------------ wave primitives
 __device__ __forceinline__ int lane() { return (int)threadIdx.x; }
 
+// Inclusive prefix sum over the wavefront with DPP row shifts + row broadcasts (6 VALU
+// ops, no LDS traffic).  Lanes that have no source read the identity (bound_ctrl off,
+// old = 0).
 __device__ __forceinline__ int wave_scan_incl(int v) {
-    const int L = lane();
-#pragma unroll
-    for (int o = 1; o < MT_WAVE; o <<= 1) {
-        int t = __shfl_up(v, o, MT_WAVE);
-        if (L >= o) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
     return v;
 }
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, MT_WAVE);
-    return v;
-}
+// Wave-uniform results come back through readlane/readfirstlane so that the compiler keeps
+// them in SGPRs and branches on them uniformly.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_scan_incl(v), 63); }
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, MT_WAVE));
-    return v;
+    return uni(v);
 }
-__device__ __forceinline__ int bcast(int v, int l) { return __shfl(v, l, MT_WAVE); }
+// value of lane l (l wave-uniform)
+__device__ __forceinline__ int bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ u64 bcast64(u64 v, int l) {
-    uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, MT_WAVE);
-    uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, MT_WAVE);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
     return ((u64)hi << 32) | lo;
 }
 __device__ __forceinline__ u64 ballot(bool p) { return (u64)__ballot(p); }

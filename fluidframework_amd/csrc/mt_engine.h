@@ -78,6 +78,24 @@ template <class T> struct DocT {
 
 #define TD template <class T> __device__ __forceinline__
 
+#ifdef MT_PROF
+__device__ unsigned long long g_prof[32];
+#define PROF_WRAP_BEGIN const unsigned long long _t0 = __builtin_amdgcn_s_memtime();
+#define PROF_WRAP_END(k) if (lane() == 0) { atomicAdd(&g_prof[k], __builtin_amdgcn_s_memtime() - _t0); atomicAdd(&g_prof[16 + k], 1ull); }
+#endif
+
+// Makes the document's uniform state opaque to the optimiser at the top of every message:
+// nothing derived from it is hoisted across messages (hoisted loop invariants of the fully
+// inlined engine were spilling hundreds of SGPRs).
+TD void opaque(DocT<T> &d) {
+    asm volatile("" : "+s"(d.n), "+s"(d.depth), "+s"(d.heap_n), "+s"(d.cur_seq), "+s"(d.min_seq),
+                 "+s"(d.text_top), "+s"(d.text_half), "+s"(d.props_top), "+s"(d.props_half));
+    asm volatile("" : "+s"(d.next_uid), "+s"(d.status), "+s"(d.dlog_n), "+s"(d.dhash), "+s"(d.text),
+                 "+s"(d.props), "+s"(d.dlog), "+s"(d.hp));
+    asm volatile("" : "+s"(d.S_cap), "+s"(d.B_cap), "+s"(d.H_cap), "+s"(d.T_cap), "+s"(d.P_cap),
+                 "+s"(d.DL_cap));
+}
+
 // Per-launch LDS layout of one document (host and device agree on it).
 struct LdsLayout {
     uint32_t offA, offO, offB, offH, offCnt, offFlg, offEnds, offScr, offNb, offGen, total;
@@ -114,6 +132,14 @@ TD void fail_cap(DocT<T> &d, int cause) {
 }
 
 TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) { return d.cnt + l * d.B_cap; }
+// wave-uniform reads of LDS state (kept in SGPRs)
+TD int nbr(DocT<T> &d, int l) { return uni(d.nb[l]); }
+TD int cntr(DocT<T> &d, int l, int b) { return uni(lvl(d, l)[b]); }
+TD int flgr(DocT<T> &d, int b) { return uni(d.flg[b]); }
+__device__ __forceinline__ v4i uni4(v4i a) { return v4i{uni(a.x), uni(a.y), uni(a.z), uni(a.w)}; }
+__device__ __forceinline__ v4u uni4(v4u a) {
+    return v4u{(uint32_t)uni((int)a.x), (uint32_t)uni((int)a.y), (uint32_t)uni((int)a.z), (uint32_t)uni((int)a.w)};
+}
 TD GLB_AS uint16_t *text_base(DocT<T> &d, int half) { return d.text + (size_t)half * d.T_cap; }
 TD GLB_AS uint32_t *prec(DocT<T> &d, int half, uint32_t h) {
     return d.props + ((size_t)half * d.P_cap + h) * MT_PREC;
@@ -195,7 +221,7 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     if (lane() < MT_LV) d.nb[lane()] = d.hp->n_blk[lane()];
     wsync<T>();
     for (int l = 0; l < d.depth; l++) {
-        const int nbl = d.nb[l];
+        const int nbl = nbr(d, l);
         for (int b = lane(); b < nbl; b += MT_WAVE) lvl(d, l)[b] = gcnt[l * B + b];
     }
     for (int b = lane(); b < h.n_blk[0]; b += MT_WAVE) d.flg[b] = gflg[b];
@@ -221,11 +247,11 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
         for (int i = 1 + lane(); i <= d.heap_n; i += MT_WAVE) gH[i] = d.heap[i];
     }
     for (int l = 0; l < d.depth; l++)
-        for (int b = lane(); b < d.nb[l]; b += MT_WAVE) gcnt[l * B + b] = lvl(d, l)[b];
-    for (int b = lane(); b < d.nb[0]; b += MT_WAVE) gflg[b] = d.flg[b];
+        for (int b = lane(); b < nbr(d, l); b += MT_WAVE) gcnt[l * B + b] = lvl(d, l)[b];
+    for (int b = lane(); b < nbr(d, 0); b += MT_WAVE) gflg[b] = d.flg[b];
     int nbl[MT_LV];
 #pragma unroll
-    for (int l = 0; l < MT_LV; l++) nbl[l] = d.nb[l];
+    for (int l = 0; l < MT_LV; l++) nbl[l] = nbr(d, l);
     if (lane() == 0) {
         DocHdr h;
         h.n_seg = d.n;
@@ -314,7 +340,7 @@ TD void load_ao(DocT<T> &d, int i, bool v, v4i &a, u64 &o) {
 // First block b of level l whose end (prefix of counts) is > x (strict) or >= x.
 TD int blk_find(DocT<T> &d, int l, int x, bool strict, int &start) {
     const LDS_AS uint8_t *c = lvl(d, l);
-    const int nb = d.nb[l];
+    const int nb = nbr(d, l);
     int carry = 0;
     for (int base = 0; base < nb; base += MT_WAVE) {
         const int b = base + lane();
@@ -345,7 +371,7 @@ TD int blk_prefix(DocT<T> &d, int l, int b) {
 // shift entries [from, nb) of level l by delta (right if > 0), flags too at level 0
 TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
     LDS_AS uint8_t *c = lvl(d, l);
-    const int nb = d.nb[l];
+    const int nb = nbr(d, l);
     if (delta > 0) {
         for (int hi = nb; hi > from; hi -= MT_WAVE) {
             const int lo = max(from, hi - MT_WAVE);
@@ -390,7 +416,7 @@ TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
 // undefined; the original keeps its flag.
 TD void blk_split_up(DocT<T> &d, int l, int b) {
     while (true) {
-        if (d.nb[l] + 1 > d.B_cap) {
+        if (nbr(d, l) + 1 > d.B_cap) {
             fail_cap(d, 2);
             return;
         }
@@ -424,7 +450,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
             wsync<T>();
             return;
         }
-        const int pc = lvl(d, l + 1)[P] + 1;
+        const int pc = cntr(d, l + 1, P) + 1;
         wsync<T>();
         if (lane() == 0) lvl(d, l + 1)[P] = (uint8_t)pc;
         wsync<T>();
@@ -437,7 +463,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
 // Replace entries [b0, b0 + nold) of level l with k entries sized base (+1 for the first
 // `extra`), as pack :1414-1446 does; new level-0 blocks have needsScour undefined.
 TD void blk_replace(DocT<T> &d, int l, int b0, int nold, int k, int base, int extra) {
-    if (d.nb[l] + (k - nold) > d.B_cap) {
+    if (nbr(d, l) + (k - nold) > d.B_cap) {
         fail_cap(d, 2);
         return;
     }
@@ -453,7 +479,7 @@ TD void blk_replace(DocT<T> &d, int l, int b0, int nold, int k, int base, int ex
 // level-0 end indices into LDS (for per-lane block lookups)
 TD void compute_ends(DocT<T> &d) {
     const LDS_AS uint8_t *c = lvl(d, 0);
-    const int nb = d.nb[0];
+    const int nb = nbr(d, 0);
     int carry = 0;
     for (int base = 0; base < nb; base += MT_WAVE) {
         const int b = base + lane();
@@ -542,7 +568,18 @@ TD int find_uid(DocT<T> &d, uint32_t uid) {
 }
 
 // sum of observer lengths over [0, x)  (getPosition :1619-1636 in the observer view)
+#ifdef MT_PROF
+TD int obs_prefix_impl(DocT<T> &d, int x);
 TD int obs_prefix(DocT<T> &d, int x) {
+    PROF_WRAP_BEGIN
+    auto _r = obs_prefix_impl(d, x);
+    PROF_WRAP_END(8)
+    return _r;
+}
+TD int obs_prefix_impl(DocT<T> &d, int x) {
+#else
+TD int obs_prefix(DocT<T> &d, int x) {
+#endif
     int s = 0;
     for (int base = 0; base < x; base += MT_WAVE) {
         const int i = base + lane();
@@ -557,7 +594,18 @@ TD void copy_text(GLB_AS uint16_t *dst, const GLB_AS uint16_t *src, int n) {
     for (int j = lane(); j < n; j += MT_WAVE) dst[j] = src[j];
 }
 // Compact all live text (non-removed TextSegments) into the other half, document order.
+#ifdef MT_PROF
+TD void text_gc_impl(DocT<T> &d);
 TD void text_gc(DocT<T> &d) {
+    PROF_WRAP_BEGIN
+    text_gc_impl(d);
+    PROF_WRAP_END(5)
+    
+}
+TD void text_gc_impl(DocT<T> &d) {
+#else
+TD void text_gc(DocT<T> &d) {
+#endif
     d.text_gcs++;
     gsync();
     const int dh = 1 - d.text_half;
@@ -694,7 +742,18 @@ TD void cb_log(DocT<T> &d, int32_t v) {
 // BaseSegment.splitAt :523-567 (right half inserted right after the left half in the same
 // leaf block, which may then split).  Property records are immutable, so both halves share.
 // The left half's last character is unknown until a scour needs it.
+#ifdef MT_PROF
+TD void split_seg_impl(DocT<T> &d, int i, int q);
 TD void split_seg(DocT<T> &d, int i, int q) {
+    PROF_WRAP_BEGIN
+    split_seg_impl(d, i, q);
+    PROF_WRAP_END(0)
+    
+}
+TD void split_seg_impl(DocT<T> &d, int i, int q) {
+#else
+TD void split_seg(DocT<T> &d, int i, int q) {
+#endif
     if (d.n + 1 > d.S_cap) {
         fail_cap(d, 1);
         return;
@@ -724,7 +783,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
     }
     d.next_uid++;
     d.n++;
-    const int c = lvl(d, 0)[b] + 1;
+    const int c = cntr(d, 0, b) + 1;
     wsync<T>();
     if (lane() == 0) lvl(d, 0)[b] = (uint8_t)c;
     wsync<T>();
@@ -732,7 +791,18 @@ TD void split_seg(DocT<T> &d, int i, int q) {
 }
 
 // ensureIntervalBoundary :2274-2278 -- split the leaf strictly containing view position p
+#ifdef MT_PROF
+TD void boundary_impl(DocT<T> &d, int p, int r, int c);
 TD void boundary(DocT<T> &d, int p, int r, int c) {
+    PROF_WRAP_BEGIN
+    boundary_impl(d, p, r, c);
+    PROF_WRAP_END(1)
+    
+}
+TD void boundary_impl(DocT<T> &d, int p, int r, int c) {
+#else
+TD void boundary(DocT<T> &d, int p, int r, int c) {
+#endif
     int carry = 0;
     for (int base = 0; base < d.n; base += MT_WAVE) {
         const int i = base + lane();
@@ -762,7 +832,7 @@ TD void boundary(DocT<T> &d, int p, int r, int c) {
 
 // addToLRUSet :1306-1316 for a segment in leaf block b
 TD void add_to_lru_block(DocT<T> &d, int b, uint32_t uid, int seq) {
-    const int f = d.flg[b];
+    const int f = flgr(d, b);
     if (f != 1 && seq > d.cur_seq) {
         wsync<T>();
         if (lane() == 0) d.flg[b] = 1;
@@ -781,191 +851,212 @@ __device__ __forceinline__ bool can_append(int plen, bool pmarker, bool p_nl, in
 }
 
 // scourNode :1322-1398 over leaf block [s, e); compacts the table.  Returns survivors.
+#ifdef MT_PROF
+TD int scour_block_impl(DocT<T> &d, int s, int e);
 TD int scour_block(DocT<T> &d, int s, int e) {
-    const int cntb = e - s;
+    PROF_WRAP_BEGIN
+    auto _r = scour_block_impl(d, s, e);
+    PROF_WRAP_END(2)
+    return _r;
+}
+TD int scour_block_impl(DocT<T> &d, int s, int e) {
+#else
+TD int scour_block(DocT<T> &d, int s, int e) {
+#endif
+    const int cntb = e - s;   // <= MaxNodesInBlock
+    const int k = lane();
+    const bool in = k < cntb;
+    v4i a = d.A[in ? s + k : s];
+    v4u b = d.Bv[in ? s + k : s];
+    const bool removed = a.z != MT_RSEQ_NONE;
+    const bool marker = (b.z & MT_MARKER_BIT) != 0;
+    const bool settled = in && !removed && a.y <= d.min_seq;   // merge candidate
     // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
-    {
-        const int k = lane();
-        bool need = false;
-        v4i a;
-        v4u b;
-        if (k < cntb) {
-            a = d.A[s + k];
-            b = d.Bv[s + k];
-            need = a.z == MT_RSEQ_NONE && a.y <= d.min_seq && !(b.z & MT_MARKER_BIT) && a.x > 0 &&
-                   !(b.w & SEGF_NL_KNOWN);
+    const bool need_nl = settled && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
+    if (ballot(need_nl)) {
+        gsync();
+        if (need_nl) {
+            const uint16_t ch = text_base(d, d.text_half)[b.x + a.x - 1];
+            b.w = (b.w & ~SEGF_NL) | SEGF_NL_KNOWN | (ch == '\n' ? SEGF_NL : 0u);
+            d.Bv[s + k].w = b.w;
         }
-        if (ballot(need)) {
-            gsync();
-            if (need) {
-                const uint16_t ch = text_base(d, d.text_half)[b.x + a.x - 1];
-                d.Bv[s + k].w = (b.w & ~SEGF_NL) | SEGF_NL_KNOWN | (ch == '\n' ? SEGF_NL : 0u);
-            }
-            wsync<T>();
-        }
+        wsync<T>();
     }
-    // plan (lane 0): scr[k] = -2 keep, -1 unlink, >=0 append into that local index
-    LDS_AS int *plan = d.scr;
-    LDS_AS int *glen = d.scr + 16;  // merged length per keeper
-    int need = 0;
-    if (lane() == 0) {
-        int prev = -1;
-        int plen = 0;
-        bool pmark = false, pnl = false;
-        uint32_t pprops = 0;
-        int pend = 0;  // arena end of prev's current contiguous text (-1 if not contiguous)
-        for (int k = 0; k < cntb; k++) {
-            const v4i a = d.A[s + k];
-            const v4u b = d.Bv[s + k];
-            const bool mk = (b.z & MT_MARKER_BIT) != 0;
-            glen[k] = a.x;
-            if (a.z != MT_RSEQ_NONE) {
-                plan[k] = (a.z > d.min_seq) ? -2 : -1;
-                prev = -1;
-            } else if (a.y <= d.min_seq) {
-                const bool ok = prev >= 0 && can_append(plen, pmark, pnl, a.x, mk) &&
-                                match_props(d, pprops, b.y) && a.x > 0;
-                const bool nl = (b.w & SEGF_NL) != 0;
-                if (ok) {
-                    plan[k] = prev;
-                    if (pend != (int)b.x) need += 1;
-                    pend = pend == (int)b.x ? (int)b.x + a.x : -1;
-                    plen += a.x;
-                    glen[prev] = plen;
-                    pnl = nl;
-                } else {
-                    plan[k] = -2;
-                    prev = k;
-                    plen = a.x;
-                    pmark = mk;
-                    pnl = !mk && a.x > 0 && nl;
-                    pprops = b.y;
-                    pend = (int)b.x + a.x;
-                }
+    const u64 m_unlink = ballot(in && removed && a.z <= d.min_seq);
+    const u64 m_settled = ballot(settled);
+    const u64 m_mark = ballot(in && marker);
+    const u64 m_nl = ballot(in && (b.w & SEGF_NL) != 0);
+    // plan (scalar): owner of each entry, 4 bits per entry: its own index = survivor,
+    // another index = appended to that keeper, 0xF = unlinked
+    uint32_t owners = 0;
+    int prev = -1, plen = 0;
+    bool pmark = false, pnl = false;
+    uint32_t pprops = 0;
+    for (int j = 0; j < cntb; j++) {
+        uint32_t own = (uint32_t)j;
+        if ((m_unlink >> j) & 1ull) {
+            own = 0xF;
+            prev = -1;
+        } else if (!((m_settled >> j) & 1ull)) {
+            prev = -1;
+        } else {
+            const int lj = bcast(a.x, j);
+            const bool mk = (m_mark >> j) & 1ull, nl = (m_nl >> j) & 1ull;
+            const uint32_t pj = (uint32_t)bcast((int)b.y, j);
+            const bool ok = prev >= 0 && lj > 0 && can_append(plen, pmark, pnl, lj, mk) &&
+                            match_props(d, pprops, pj);
+            if (ok) {
+                own = (uint32_t)prev;
+                plen += lj;
+                pnl = nl;
             } else {
-                plan[k] = -2;
-                prev = -1;
+                prev = j;
+                plen = lj;
+                pmark = mk;
+                pnl = !mk && lj > 0 && nl;
+                pprops = pj;
             }
         }
+        owners |= own << (4 * j);
     }
-    wsync<T>();
-    need = bcast(need, 0);
-    if (need) {
-        // upper bound of what the merges below allocate (group text + slack)
+    const uint32_t myown = in ? (owners >> (4 * k)) & 0xFu : 0xFu;
+    const u64 m_keep = ballot(in && myown == (uint32_t)k);
+    const u64 m_app = ballot(in && myown != 0xFu && myown != (uint32_t)k);
+    if (m_app) {
+        // group length per keeper (lanes that are keepers sum their members)
+        int glen = 0;
+        if (in && myown == (uint32_t)k) {
+            for (int j = 0; j < cntb; j++) glen += ((owners >> (4 * j)) & 0xFu) == (uint32_t)k ? bcast(a.x, j) : 0;
+        }
+        // keepers with appended members
+        u64 m_grp = 0;
+        for (int j = 0; j < cntb; j++)
+            if ((m_app >> j) & 1ull) m_grp |= 1ull << ((owners >> (4 * j)) & 0xFu);
+        // upper bound of what the merges allocate (group text + slack)
         int tot = 0;
-        for (int k = 0; k < cntb; k++)
-            if (plan[k] == -2) tot += glen[k] + text_slack(glen[k]);
+        for (u64 g = m_grp; g; g &= g - 1) {
+            const int gl = bcast(glen, first_lane(g));
+            tot += gl + text_slack(gl);
+        }
         if (!text_ensure(d, tot)) return cntb;
         gsync();
-    }
-    // execute text merges group by group (uniform loops; cntb <= 8).  A keeper copied to
-    // the arena top reserves slack after its text so that later appends land in place
-    // (TextSegment.append :70-85 is a string concatenation; this keeps it amortised O(1)).
-    LDS_AS int *psrc = d.scr + 48;   // gather pieces of one group: source offset, length
-    LDS_AS int *plen = d.scr + 56;
-    for (int k = 0; k < cntb; k++) {
-        if (plan[k] != -2 || glen[k] == d.A[s + k].x) continue;
-        const v4u bk = d.Bv[s + k];
-        const v4i ak = d.A[s + k];
-        const uint32_t kslack = bk.w >> SEGF_SLACK_SHIFT;
-        bool contig = true;
-        int endp = (int)bk.x + ak.x, add = 0;
-        uint32_t lastw = 0;   // the last appended segment's flags (read after any text_gc)
-        for (int j = k + 1; j < cntb && plan[j] == k; j++) {
-            const v4u bj = d.Bv[s + j];
-            const int lj = d.A[s + j].x;
-            if ((int)bj.x != endp) contig = false;
-            endp += lj;
-            add += lj;
-            lastw = bj.w;
-        }
-        uint32_t newoff = bk.x, newslack = lastw >> SEGF_SLACK_SHIFT;
-        if (!contig) {
-            int dst, np = 0, ntot = 0;
-            if ((uint32_t)add <= kslack) {                       // append into the slack
-                dst = (int)bk.x + ak.x;
-                newslack = kslack - (uint32_t)add;
-            } else if ((int)bk.x + ak.x == d.text_top) {        // keeper ends at the top
-                dst = d.text_top;
-                newslack = (uint32_t)text_slack(glen[k]);
-                d.text_top += add + (int)newslack;
-            } else {                                            // move keeper + appends
-                newoff = (uint32_t)d.text_top;
-                dst = d.text_top;
-                newslack = (uint32_t)text_slack(glen[k]);
-                d.text_top += glen[k] + (int)newslack;
-                if (lane() == 0) {
-                    psrc[0] = (int)bk.x;
-                    plen[0] = ak.x;
-                }
-                np = 1;
-                ntot = ak.x;
+        // execute text merges group by group.  A keeper copied to the arena top reserves
+        // slack after its text so that later appends land in place (TextSegment.append
+        // :70-85 is a string concatenation; this keeps it amortised O(1)).
+        LDS_AS int *psrc = d.scr + 48;   // gather pieces of one group: source offset, length
+        LDS_AS int *plen_ = d.scr + 56;
+        for (u64 g = m_grp; g; g &= g - 1) {
+            const int kk = first_lane(g);
+            const int gk = bcast(glen, kk);
+            const v4u bk = uni4(d.Bv[s + kk]);   // fresh: text_ensure may have compacted
+            const int ak = uni(d.A[s + kk].x);
+            const uint32_t kslack = bk.w >> SEGF_SLACK_SHIFT;
+            bool contig = true;
+            int endp = (int)bk.x + ak, add = 0;
+            uint32_t lastw = 0;
+            for (int j = kk + 1; j < cntb && ((owners >> (4 * j)) & 0xFu) == (uint32_t)kk; j++) {
+                const v4u bj = uni4(d.Bv[s + j]);
+                const int lj = bcast(a.x, j);
+                if ((int)bj.x != endp) contig = false;
+                endp += lj;
+                add += lj;
+                lastw = bj.w;
             }
-            for (int j = k + 1; j < cntb && plan[j] == k; j++) {
-                if (lane() == 0) {
-                    psrc[np] = (int)d.Bv[s + j].x;
-                    plen[np] = d.A[s + j].x;
+            uint32_t newoff = bk.x, newslack = lastw >> SEGF_SLACK_SHIFT;
+            if (!contig) {
+                int dst, np = 0, ntot = 0;
+                if ((uint32_t)add <= kslack) {                       // append into the slack
+                    dst = (int)bk.x + ak;
+                    newslack = kslack - (uint32_t)add;
+                } else if ((int)bk.x + ak == d.text_top) {          // keeper ends at the top
+                    dst = d.text_top;
+                    newslack = (uint32_t)text_slack(gk);
+                    d.text_top += add + (int)newslack;
+                } else {                                            // move keeper + appends
+                    newoff = (uint32_t)d.text_top;
+                    dst = d.text_top;
+                    newslack = (uint32_t)text_slack(gk);
+                    d.text_top += gk + (int)newslack;
+                    if (lane() == 0) {
+                        psrc[0] = (int)bk.x;
+                        plen_[0] = ak;
+                    }
+                    np = 1;
+                    ntot = ak;
                 }
-                ntot += d.A[s + j].x;
-                np++;
+                for (int j = kk + 1; j < cntb && ((owners >> (4 * j)) & 0xFu) == (uint32_t)kk; j++) {
+                    const int lj = bcast(a.x, j);
+                    if (lane() == 0) {
+                        psrc[np] = (int)d.Bv[s + j].x;
+                        plen_[np] = lj;
+                    }
+                    ntot += lj;
+                    np++;
+                }
+                wsync<T>();
+                GLB_AS uint16_t *tb = text_base(d, d.text_half);
+                for (int base = 0; base < ntot; base += MT_WAVE) {   // one gather per 64 units
+                    const int t = base + lane();
+                    int src = -1, pre = 0;
+                    for (int q = 0; q < np; q++) {
+                        const int lq = plen_[q];
+                        if (src < 0 && t < pre + lq) src = psrc[q] + (t - pre);
+                        pre += lq;
+                    }
+                    uint16_t ch = 0;
+                    if (t < ntot) ch = tb[src];
+                    if (t < ntot) tb[dst + t] = ch;
+                }
+            }
+            if (lane() == 0) {
+                d.A[s + kk].x = gk;
+                v4u nb = bk;
+                nb.x = newoff;
+                nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | (newslack << SEGF_SLACK_SHIFT);
+                d.Bv[s + kk] = nb;
             }
             wsync<T>();
-            GLB_AS uint16_t *tb = text_base(d, d.text_half);
-            for (int base = 0; base < ntot; base += MT_WAVE) {   // one gather per 64 units
-                const int t = base + lane();
-                int src = -1, pre = 0;
-                for (int q = 0; q < np; q++) {
-                    const int lq = plen[q];
-                    if (src < 0 && t < pre + lq) src = psrc[q] + (t - pre);
-                    pre += lq;
-                }
-                uint16_t ch = 0;
-                if (t < ntot) ch = tb[src];
-                if (t < ntot) tb[dst + t] = ch;
-            }
         }
-        wsync<T>();
-        if (lane() == 0) {
-            d.A[s + k].x = glen[k];
-            v4u nb = bk;
-            nb.x = newoff;
-            nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | (newslack << SEGF_SLACK_SHIFT);
-            d.Bv[s + k] = nb;
-        }
-        wsync<T>();
     }
-    // compaction: survivors to the front of the block, tail moved left
-    int keep = 0;
-    for (int k = 0; k < cntb; k++) keep += plan[k] == -2 ? 1 : 0;
+    const int keep = __popcll(m_keep);
     if (keep < cntb) {
-        v4i a;
-        u64 o;
-        v4u b;
-        int dst = -1;
-        if (lane() < cntb && plan[lane()] == -2) {
-            a = d.A[s + lane()];
-            o = d.O[s + lane()];
-            b = d.Bv[s + lane()];
-            int r = 0;
-            for (int k = 0; k < lane(); k++) r += plan[k] == -2 ? 1 : 0;
-            dst = s + r;
+        // compaction: survivors to the front of the block, tail moved left
+        const bool surv = (m_keep >> k) & 1ull;
+        v4i sa;
+        u64 so;
+        v4u sb;
+        if (surv) {
+            sa = d.A[s + k];
+            so = d.O[s + k];
+            sb = d.Bv[s + k];
+        }
+        const int dst = s + __popcll(m_keep & ((1ull << k) - 1ull));
+        wsync<T>();
+        if (surv) {
+            d.A[dst] = sa;
+            d.O[dst] = so;
+            d.Bv[dst] = sb;
         }
         wsync<T>();
-        if (dst >= 0) {
-            d.A[dst] = a;
-            d.O[dst] = o;
-            d.Bv[dst] = b;
-        }
-        wsync<T>();
-        const int from = e, k = cntb - keep;
-        seg_move_left(d, from, k);
-        d.n -= k;
+        seg_move_left(d, e, cntb - keep);
+        d.n -= cntb - keep;
     }
     return keep;
 }
 
 // pack :1401-1453 starting from the underflowing block b of level l
+#ifdef MT_PROF
+TD void pack_impl(DocT<T> &d, int l, int b);
 TD void pack(DocT<T> &d, int l, int b) {
+    PROF_WRAP_BEGIN
+    pack_impl(d, l, b);
+    PROF_WRAP_END(3)
+    
+}
+TD void pack_impl(DocT<T> &d, int l, int b) {
+#else
+TD void pack(DocT<T> &d, int l, int b) {
+#endif
     while (true) {
         int c0;
         const int P = blk_find(d, l + 1, b, true, c0);
@@ -973,12 +1064,12 @@ TD void pack(DocT<T> &d, int l, int b) {
             fail(d, MT_DOC_INTERNAL);
             return;
         }
-        const int nch = lvl(d, l + 1)[P];
+        const int nch = cntr(d, l + 1, P);
         int total = 0;
         if (l == 0) {
             int pos = blk_prefix(d, 0, c0);
             for (int cb = c0; cb < c0 + nch; cb++) {
-                const int old = lvl(d, 0)[cb];
+                const int old = cntr(d, 0, cb);
                 const int kept = scour_block(d, pos, pos + old);
                 if (d.status) return;
                 wsync<T>();
@@ -988,7 +1079,7 @@ TD void pack(DocT<T> &d, int l, int b) {
                 total += kept;
             }
         } else {
-            for (int cb = c0; cb < c0 + nch; cb++) total += lvl(d, l)[cb];
+            for (int cb = c0; cb < c0 + nch; cb++) total += cntr(d, l, cb);
         }
         int k = total / MT_HALF;
         if (k > MT_MAXN - 1) k = MT_MAXN - 1;
@@ -1008,7 +1099,18 @@ TD void pack(DocT<T> &d, int l, int b) {
 }
 
 // zamboniSegments :1455-1511
+#ifdef MT_PROF
+TD void zamboni_impl(DocT<T> &d);
 TD void zamboni(DocT<T> &d) {
+    PROF_WRAP_BEGIN
+    zamboni_impl(d);
+    PROF_WRAP_END(4)
+    
+}
+TD void zamboni_impl(DocT<T> &d) {
+#else
+TD void zamboni(DocT<T> &d) {
+#endif
     for (int it = 0; it < MT_ZAMBONI && d.status == 0; it++) {
         if (d.heap_n == 0) break;
         const v2i top = heap_top(d);
@@ -1023,8 +1125,8 @@ TD void zamboni(DocT<T> &d) {
             fail(d, MT_DOC_INTERNAL);
             return;
         }
-        const int f = d.flg[b];
-        const int old = lvl(d, 0)[b];
+        const int f = flgr(d, b);
+        const int old = cntr(d, 0, b);
         if (f == 0) continue;
         const int kept = scour_block(d, bstart, bstart + old);
         if (d.status) return;
@@ -1049,11 +1151,11 @@ TD void zamboni(DocT<T> &d) {
 TD bool lds_room(DocT<T> &d, const mt_op_rec &op) {
     if (d.n + 3 > d.S_cap) return false;
     if (d.depth + 2 > MT_LV) return false;
-    const int nb0 = d.nb[0];
+    const int nb0 = nbr(d, 0);
     int need_heap = op.kind == MT_OP_INSERT ? 1 : nb0 + 3;
     if (d.heap_n + need_heap > d.H_cap) return false;
     bool ok = true;
-    for (int l = 0; l < d.depth; l++) ok = ok && d.nb[l] + 3 + 24 <= d.B_cap;
+    for (int l = 0; l < d.depth; l++) ok = ok && nbr(d, l) + 3 + 24 <= d.B_cap;
     return ok;
 }
 
@@ -1072,7 +1174,18 @@ __device__ __forceinline__ uint16_t pay_unit(const OpIn &in, int j) {
 }
 
 // Client.applyInsertOp MT/client.ts:394-442 -> MergeTree.insertSegments :2001-2031
+#ifdef MT_PROF
+TD void op_insert_impl(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin);
 TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    PROF_WRAP_BEGIN
+    op_insert_impl(d, in, tin, pin);
+    PROF_WRAP_END(6)
+    
+}
+TD void op_insert_impl(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+#else
+TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+#endif
     const mt_op_rec &op = in.op;
     const int r = op.ref_seq, c = op.client, seq = op.seq, p = op.pos1;
     const bool marker = (op.flags & MT_F_MARKER) != 0;
@@ -1162,7 +1275,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         fail(d, MT_DOC_INTERNAL);
         return;
     }
-    const int bend = bstart + lvl(d, 0)[B];
+    const int bend = bstart + cntr(d, 0, B);
     const int x = (js >= 0 && js < bend) ? js : bend;
     uint32_t toff, segw = 0;
     if (marker) {
@@ -1187,7 +1300,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     }
     d.next_uid++;
     d.n++;
-    const int nc = lvl(d, 0)[B] + 1;
+    const int nc = cntr(d, 0, B) + 1;
     wsync<T>();
     if (lane() == 0) lvl(d, 0)[B] = (uint8_t)nc;
     wsync<T>();
@@ -1290,7 +1403,18 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
 // markRangeRemoved :2640-2752 / annotateRange :2598-2638.  After the two boundary splits
 // the visited leaves are exactly those with view length > 0 inside [p1, p2) (nodeMap
 // :2936-2998 is tree-shape independent), processed in document order.
+#ifdef MT_PROF
+TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin);
 TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+    PROF_WRAP_BEGIN
+    op_range_impl(d, op, pin);
+    PROF_WRAP_END(7)
+    
+}
+TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+#else
+TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+#endif
     const int r = op.ref_seq, c = op.client, seq = op.seq, p1 = op.pos1, p2 = op.pos2;
     const bool rem = op.kind == MT_OP_REMOVE;
     const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
@@ -1308,7 +1432,7 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
     Cb cb = cb_begin(d, seq, op.kind);
     int carry = 0, ocarry = 0, last_b = -1;
     const int L = lane();
-    const int nblk = d.nb[0];
+    const int nblk = nbr(d, 0);
     for (int base = 0; base < d.n; base += MT_WAVE) {
         if (!rem && !props_ensure(d, MT_WAVE)) return;
         const int i = base + L;

@@ -144,6 +144,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
             in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
+
             apply_op(d, in, gt, gp);
         }
     }
@@ -1011,6 +1012,24 @@ int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uin
     if (out && cnt) HIPCHK(h, hipMemcpy(out, h->st.dlog + (size_t)doc * h->st.DL, cnt * 4, hipMemcpyDeviceToHost));
     if (n) *n = (uint32_t)hdr.dlog_n;
     return 0;
+}
+
+// Debug: section timers of an MT_PROF build (s_memtime ticks and call counts, 16 + 16).
+int mt_debug_prof(mt_handle *h, uint64_t *out, int reset) {
+#ifdef MT_PROF
+    if (!h) return MT_E_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipDeviceSynchronize());
+    if (out) HIPCHK(h, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), 32 * sizeof(uint64_t)));
+    if (reset) {
+        uint64_t z[32] = {0};
+        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+    }
+    return 0;
+#else
+    (void)h; (void)out; (void)reset;
+    return MT_E_INVALID;
+#endif
 }
 
 int mt_checksums_device(mt_handle *h, void *device_out) {

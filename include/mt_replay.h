@@ -131,6 +131,8 @@ int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_
 /* Debug: raw segment records (8 u32 per segment: segA then segB) and the 32-word header. */
 int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, uint32_t *n_rows,
                  int32_t *hdr_words);
+/* Debug: section timers of a build with -DMT_PROF (MT_E_INVALID otherwise). */
+int mt_debug_prof(mt_handle *h, uint64_t *out /* [32] */, int reset);
 /* Delta log (only with delta_log_capacity > 0), oracle layout. */
 int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uint32_t *n);
 
