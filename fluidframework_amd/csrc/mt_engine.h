@@ -20,15 +20,19 @@
 #define LDS_AS __attribute__((address_space(3)))
 #define GLB_AS __attribute__((address_space(1)))
 
-struct TierLds {
+// kLog: the delta log (a debug/verification feature) is compiled in only when a handle asks
+// for one, so the replay fast path does not carry its registers.
+template <bool kLogT> struct TierLdsT {
     static constexpr bool kLds = true;
+    static constexpr bool kLog = kLogT;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS u64 *O_t;
     typedef LDS_AS v4u *B_t;
     typedef LDS_AS v2i *H_t;
 };
-struct TierGlb {
+template <bool kLogT> struct TierGlbT {
     static constexpr bool kLds = false;
+    static constexpr bool kLog = kLogT;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
     typedef GLB_AS v4u *B_t;
@@ -39,6 +43,17 @@ struct TierGlb {
 // so the LDS tier only needs the compiler not to reorder; global memory written by one
 // lane and read by another waits for the stores to complete.
 __device__ __forceinline__ void gsync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Before a lane reads global data (text, property records) that another lane of the same
+// wavefront stored earlier.  A wavefront's vector-memory instructions reach the L1/L2 in
+// issue order, so a later load observes an earlier store to the same address: only the
+// compiler must not reorder.  (-DMT_STRICT_GSYNC waits for the stores instead.)
+__device__ __forceinline__ void gsync_rd() {
+#ifdef MT_STRICT_GSYNC
+    gsync();
+#else
+    asm volatile("" ::: "memory");
+#endif
+}
 template <class T> __device__ __forceinline__ void wsync() {
     if constexpr (T::kLds)
         asm volatile("" ::: "memory");
@@ -74,31 +89,57 @@ template <class T> struct DocT {
     int n, depth, heap_n, cur_seq, min_seq, text_top, text_half, props_top, props_half, next_uid,
         status, dlog_n, text_gcs, props_gcs, cap_cause;
     u64 dhash;
+#ifdef MT_PROF
+    LDS_AS u64 *prof;       // [32] section timers
+#endif
 };
 
 #define TD template <class T> __device__ __forceinline__
 
 #ifdef MT_PROF
 __device__ unsigned long long g_prof[32];
+// per-wave accumulators live in LDS (no global atomics inside the timed sections: they
+// would be waited for by the engine's s_waitcnt vmcnt(0))
 #define PROF_WRAP_BEGIN const unsigned long long _t0 = __builtin_amdgcn_s_memtime();
-#define PROF_WRAP_END(k) if (lane() == 0) { atomicAdd(&g_prof[k], __builtin_amdgcn_s_memtime() - _t0); atomicAdd(&g_prof[16 + k], 1ull); }
+#define PROF_WRAP_END(k)                                                              \
+    if (lane() == 0) {                                                                \
+        d.prof[k] += __builtin_amdgcn_s_memtime() - _t0;                              \
+        d.prof[16 + k] += 1ull;                                                       \
+    }
 #endif
 
 // Makes the document's uniform state opaque to the optimiser at the top of every message:
 // nothing derived from it is hoisted across messages (hoisted loop invariants of the fully
 // inlined engine were spilling hundreds of SGPRs).
+template <class P> __device__ __forceinline__ void opq_ptr(P &p) {
+    if constexpr (sizeof(P) == 8) {
+        uint64_t v = (uint64_t)p;
+        uint32_t lo = (uint32_t)uni((int)(uint32_t)v), hi = (uint32_t)uni((int)(uint32_t)(v >> 32));
+        asm volatile("" : "+s"(lo), "+s"(hi));
+        p = (P)(((uint64_t)hi << 32) | lo);
+    } else {
+        uint32_t v = (uint32_t)(uintptr_t)p;
+        v = (uint32_t)uni((int)v);
+        asm volatile("" : "+s"(v));
+        p = (P)(uintptr_t)v;
+    }
+}
+__device__ __forceinline__ void opq(int &x) {
+    x = uni(x);
+    asm volatile("" : "+s"(x));
+}
 TD void opaque(DocT<T> &d) {
-    asm volatile("" : "+s"(d.n), "+s"(d.depth), "+s"(d.heap_n), "+s"(d.cur_seq), "+s"(d.min_seq),
-                 "+s"(d.text_top), "+s"(d.text_half), "+s"(d.props_top), "+s"(d.props_half));
-    asm volatile("" : "+s"(d.next_uid), "+s"(d.status), "+s"(d.dlog_n), "+s"(d.dhash), "+s"(d.text),
-                 "+s"(d.props), "+s"(d.dlog), "+s"(d.hp));
-    asm volatile("" : "+s"(d.S_cap), "+s"(d.B_cap), "+s"(d.H_cap), "+s"(d.T_cap), "+s"(d.P_cap),
-                 "+s"(d.DL_cap));
+    opq(d.n); opq(d.depth); opq(d.heap_n); opq(d.cur_seq); opq(d.min_seq); opq(d.text_top);
+    opq(d.text_half); opq(d.props_top); opq(d.props_half); opq(d.next_uid); opq(d.status);
+    opq(d.dlog_n); opq(d.S_cap); opq(d.B_cap); opq(d.H_cap); opq(d.T_cap); opq(d.P_cap); opq(d.DL_cap);
+    opq_ptr(d.text); opq_ptr(d.props); opq_ptr(d.dlog); opq_ptr(d.hp);
+    opq_ptr(d.cnt); opq_ptr(d.flg); opq_ptr(d.ends); opq_ptr(d.scr); opq_ptr(d.nb);
+    opq_ptr(d.A); opq_ptr(d.O); opq_ptr(d.Bv); opq_ptr(d.heap);
 }
 
 // Per-launch LDS layout of one document (host and device agree on it).
 struct LdsLayout {
-    uint32_t offA, offO, offB, offH, offCnt, offFlg, offEnds, offScr, offNb, offGen, total;
+    uint32_t offA, offO, offB, offH, offCnt, offFlg, offEnds, offScr, offNb, offGen, offProf, total;
 };
 static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, int B, int H, int gen_words) {
     LdsLayout L;
@@ -117,6 +158,12 @@ static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, i
     L.offEnds = o; o += 2u * B;
     L.offCnt = o; o += (uint32_t)MT_LV * B;
     L.offFlg = o; o += (uint32_t)B;
+#ifdef MT_PROF
+    o = (o + 7u) & ~7u;
+    L.offProf = o; o += 32u * 8;
+#else
+    L.offProf = 0;
+#endif
     L.total = (o + 15u) & ~15u;
     return L;
 }
@@ -163,6 +210,10 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.ends = (LDS_AS uint16_t *)(smem + L.offEnds);
     d.cnt = smem + L.offCnt;
     d.flg = (LDS_AS int8_t *)(smem + L.offFlg);
+#ifdef MT_PROF
+    d.prof = (LDS_AS u64 *)(smem + L.offProf);
+    if (lane() < 32) d.prof[lane()] = 0;
+#endif
     GLB_AS const uint8_t *gcnt = (GLB_AS const uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
     GLB_AS const int8_t *gflg = (GLB_AS const int8_t *)(st.flg + doc * B);
     const DocHdr h = *d.hp;
@@ -607,7 +658,7 @@ TD void text_gc_impl(DocT<T> &d) {
 TD void text_gc(DocT<T> &d) {
 #endif
     d.text_gcs++;
-    gsync();
+    gsync_rd();
     const int dh = 1 - d.text_half;
     GLB_AS uint16_t *dst = text_base(d, dh);
     const GLB_AS uint16_t *src = text_base(d, d.text_half);
@@ -656,7 +707,7 @@ TD bool text_ensure(DocT<T> &d, int need) {
 // ------------------------------------------------------------------ property records
 TD void props_gc(DocT<T> &d) {
     d.props_gcs++;
-    gsync();
+    gsync_rd();
     const int dh = 1 - d.props_half;
     int carry = 1;
     for (int base = 0; base < d.n; base += MT_WAVE) {
@@ -678,7 +729,7 @@ TD void props_gc(DocT<T> &d) {
     }
     d.props_half = dh;
     d.props_top = carry;
-    gsync();
+    gsync_rd();
     wsync<T>();
 }
 TD bool props_ensure(DocT<T> &d, int need) {
@@ -716,7 +767,7 @@ TD Cb cb_begin(DocT<T> &d, int seq, int kind) {
     cb.h = fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)seq), (uint32_t)kind);
     cb.n = 0;
     cb.log_hdr = -1;
-    if (d.dlog && d.dlog_n + 3 <= d.DL_cap) {
+    if (T::kLog && d.dlog && d.dlog_n + 3 <= d.DL_cap) {
         cb.log_hdr = d.dlog_n;
         if (lane() == 0) {
             d.dlog[d.dlog_n] = seq;
@@ -729,10 +780,10 @@ TD Cb cb_begin(DocT<T> &d, int seq, int kind) {
 TD void cb_end(DocT<T> &d, Cb &cb) {
     cb.h = fnv_u32(cb.h, (uint32_t)cb.n);
     d.dhash = fnv_u64(d.dhash, cb.h);
-    if (cb.log_hdr >= 0 && lane() == 0) d.dlog[cb.log_hdr + 2] = cb.n;
+    if (T::kLog && cb.log_hdr >= 0 && lane() == 0) d.dlog[cb.log_hdr + 2] = cb.n;
 }
 TD void cb_log(DocT<T> &d, int32_t v) {
-    if (d.dlog && d.dlog_n + 1 <= d.DL_cap) {
+    if (T::kLog && d.dlog && d.dlog_n + 1 <= d.DL_cap) {
         if (lane() == 0) d.dlog[d.dlog_n] = v;
         d.dlog_n++;
     }
@@ -815,7 +866,7 @@ TD void boundary(DocT<T> &d, int p, int r, int c) {
         const int pex = carry + inc - vl, pin = carry + inc;
         const u64 m = ballot(v && pex < p && p < pin);
 #ifdef MT_DEBUG_BOUNDARY
-        if (d.dlog) {
+        if (T::kLog && d.dlog) {
             cb_log(d, 0x7777); cb_log(d, p); cb_log(d, r); cb_log(d, c); cb_log(d, base);
             for (int q = 0; q < 16; q++) { cb_log(d, bcast(vl, q)); cb_log(d, bcast(a.z, q)); cb_log(d, bcast(a.w, q)); cb_log(d, (int)bcast64(o, q)); }
         }
@@ -874,7 +925,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
     const bool need_nl = settled && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
     if (ballot(need_nl)) {
-        gsync();
+        gsync_rd();
         if (need_nl) {
             const uint16_t ch = text_base(d, d.text_half)[b.x + a.x - 1];
             b.w = (b.w & ~SEGF_NL) | SEGF_NL_KNOWN | (ch == '\n' ? SEGF_NL : 0u);
@@ -939,7 +990,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
             tot += gl + text_slack(gl);
         }
         if (!text_ensure(d, tot)) return cntb;
-        gsync();
+        gsync_rd();
         // execute text merges group by group.  A keeper copied to the arena top reserves
         // slack after its text so that later appends land in place (TextSegment.append
         // :70-85 is a string concatenation; this keeps it amortised O(1)).
@@ -1044,6 +1095,194 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     return keep;
 }
 
+// scourNode :1322-1398 applied, in order, to the consecutive leaf blocks [b0, b0 + nbk)
+// whose segments start at index s -- one block for zamboniSegments, every child of the
+// parent for pack.  Lane-parallel: entry j is appended to the run before it iff both are
+// settled (seq <= minSeq, not removed), j is not the first of its block, neither is a
+// Marker, j-1 does not end with '\n' and their property sets match (matchProperties is an
+// equivalence, so comparing with j-1 equals comparing with the run's keeper).  The only
+// order-dependent rule -- canAppend's 256-unit granularity (MT/textSegment.ts:63-68) --
+// can only refuse an entry longer than 256 units: such ranges take the serial per-block
+// plan.  Updates the level-0 counts of the blocks; returns the survivors.
+TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
+    int tot = 0;
+    for (int q = 0; q < nbk; q++) tot += cntr(d, 0, b0 + q);
+    const int k = lane();
+    bool serial = tot > MT_WAVE;
+    const bool in = k < tot;
+    v4i a = d.A[in ? s + k : s];
+    v4u b = d.Bv[in ? s + k : s];
+    int start = 0;   // first index of this lane's block (relative)
+    {
+        int st = 0;
+        for (int q = 0; q < nbk; q++) {
+            if (k >= st) start = st;
+            st += cntr(d, 0, b0 + q);
+        }
+    }
+    const bool removed = a.z != MT_RSEQ_NONE;
+    const bool marker = (b.z & MT_MARKER_BIT) != 0;
+    const bool cand = in && !removed && a.y <= d.min_seq;
+    if (!serial) {
+        // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
+        const bool need_nl = cand && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
+        if (ballot(need_nl)) {
+            gsync_rd();
+            if (need_nl) {
+                const uint16_t ch = text_base(d, d.text_half)[b.x + a.x - 1];
+                b.w = (b.w & ~SEGF_NL) | SEGF_NL_KNOWN | (ch == '\n' ? SEGF_NL : 0u);
+                d.Bv[s + k].w = b.w;
+            }
+            wsync<T>();
+        }
+    }
+    const u64 m_cand = ballot(cand);
+    const u64 m_mark = ballot(in && marker);
+    const u64 m_nl = ballot(in && (b.w & SEGF_NL) != 0);
+    const uint32_t pprops = (uint32_t)__shfl_up((int)b.y, 1, MT_WAVE);
+    const bool pc = k > 0 && ((m_cand >> (k - 1)) & 1ull);
+    const bool pm = k > 0 && ((m_mark >> (k - 1)) & 1ull);
+    const bool pn = k > 0 && ((m_nl >> (k - 1)) & 1ull);
+    bool join = cand && pc && k != start && !marker && !pm && !pn && a.x > 0;
+    if (join && pprops != b.y) join = match_props(d, pprops, b.y);
+    const u64 m_join = ballot(join);
+    if (!serial && ballot(join && a.x > MT_GRAN)) serial = true;
+    if (serial) {   // rare: per-block serial plan (scour_block)
+        int pos = s, kept_all = 0;
+        for (int q = 0; q < nbk; q++) {
+            const int old = cntr(d, 0, b0 + q);
+            const int kept = scour_block(d, pos, pos + old);
+            if (d.status) return kept_all;
+            wsync<T>();
+            if (lane() == 0) lvl(d, 0)[b0 + q] = (uint8_t)kept;
+            wsync<T>();
+            pos += kept;
+            kept_all += kept;
+        }
+        return kept_all;
+    }
+    const bool unlink = in && removed && a.z <= d.min_seq;
+    const bool surv = in && !unlink && !join;
+    const u64 m_surv = ballot(surv);
+    const u64 above = (k < 63) ? (m_join >> (k + 1)) : 0ull;
+    const u64 m_grp = ballot(surv && (above & 1ull));
+    if (m_grp) {
+        // group length of each keeper: inclusive lengths up to the group's last member
+        const int L = wave_scan_incl(in ? a.x : 0);
+        const int gend = k + __ffsll((long long)~above) - 1;   // last member (above has a 0)
+        const int Lend = __shfl(L, gend < MT_WAVE ? gend : MT_WAVE - 1, MT_WAVE);
+        const int glen = Lend - L + (in ? a.x : 0);
+        int totc = 0;
+        for (u64 g = m_grp; g; g &= g - 1) {
+            const int gl = bcast(glen, first_lane(g));
+            totc += gl + text_slack(gl);
+        }
+        if (!text_ensure(d, totc)) return tot;
+        gsync_rd();
+        // text merges group by group.  A keeper copied to the arena top reserves slack after
+        // its text so that later appends land in place (TextSegment.append :70-85 is a
+        // string concatenation; this keeps it amortised O(1)).
+        for (u64 g = m_grp; g; g &= g - 1) {
+            const int kk = first_lane(g);
+            const int gk = bcast(glen, kk);
+            const int ge = bcast(gend, kk);
+            const v4u bk = uni4(d.Bv[s + kk]);   // fresh: text_ensure may have compacted
+            const int ak = uni(d.A[s + kk].x);
+            const uint32_t kslack = bk.w >> SEGF_SLACK_SHIFT;
+            // members kk+1..ge: contiguity of their text after the keeper's
+            const bool mem = k > kk && k <= ge;
+            const v4u bm = d.Bv[mem ? s + k : s];   // fresh offsets after a possible gc
+            const int Lm = L - (in ? a.x : 0);        // exclusive prefix of lengths
+            const int Lk = bcast(L, kk) - ak;         // keeper's exclusive prefix
+            const int rel = Lm - Lk;                  // member's offset inside the merged text
+            const bool contig_lane = !mem || (int)bm.x == (int)bk.x + rel;
+            const bool contig = !ballot(!contig_lane);
+            const int add = gk - ak;
+            const uint32_t lastw = (uint32_t)bcast((int)bm.w, ge);
+            uint32_t newoff = bk.x, newslack = lastw >> SEGF_SLACK_SHIFT;
+            if (!contig) {
+                int dst;
+                bool move_keeper = false;
+                if ((uint32_t)add <= kslack) {                       // append into the slack
+                    dst = (int)bk.x + ak;
+                    newslack = kslack - (uint32_t)add;
+                } else if ((int)bk.x + ak == d.text_top) {          // keeper ends at the top
+                    dst = d.text_top;
+                    newslack = (uint32_t)text_slack(gk);
+                    d.text_top += add + (int)newslack;
+                } else {                                            // move keeper + appends
+                    newoff = (uint32_t)d.text_top;
+                    dst = d.text_top + ak;
+                    move_keeper = true;
+                    newslack = (uint32_t)text_slack(gk);
+                    d.text_top += gk + (int)newslack;
+                }
+                GLB_AS uint16_t *tb = text_base(d, d.text_half);
+                // gather: unit t of the merged text (t < gk); units < ak come from the keeper
+                const int t0 = move_keeper ? 0 : ak;
+                for (int base = t0; base < gk; base += MT_WAVE) {
+                    const int t = base + lane();
+                    int src = 0;
+                    if (t < ak) {
+                        src = (int)bk.x + t;
+                    } else {
+                        // member whose exclusive prefix (relative) is <= t: scan members
+                        for (int j = kk + 1; j <= ge; j++) {
+                            const int rj = bcast(Lm, j) - Lk;
+                            if (t >= rj) src = bcast((int)bm.x, j) + (t - rj);
+                        }
+                    }
+                    uint16_t ch = 0;
+                    if (t < gk) ch = tb[src];
+                    if (t < gk) tb[(move_keeper ? (int)newoff : dst - ak) + t] = ch;
+                }
+            }
+            if (lane() == 0) {
+                d.A[s + kk].x = gk;
+                v4u nb = bk;
+                nb.x = newoff;
+                nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | (newslack << SEGF_SLACK_SHIFT);
+                d.Bv[s + kk] = nb;
+            }
+            wsync<T>();
+        }
+    }
+    const int keep = __popcll(m_surv);
+    if (keep < tot) {
+        // compaction: survivors to the front, tail moved left
+        v4i sa;
+        u64 so;
+        v4u sb;
+        if (surv) {
+            sa = d.A[s + k];
+            so = d.O[s + k];
+            sb = d.Bv[s + k];
+        }
+        const int dst = s + __popcll(m_surv & ((1ull << k) - 1ull));
+        wsync<T>();
+        if (surv) {
+            d.A[dst] = sa;
+            d.O[dst] = so;
+            d.Bv[dst] = sb;
+        }
+        wsync<T>();
+        seg_move_left(d, s + tot, tot - keep);
+        d.n -= tot - keep;
+    }
+    // survivors per block
+    {
+        int st = 0;
+        for (int q = 0; q < nbk; q++) {
+            const int c = cntr(d, 0, b0 + q);
+            const u64 bm = c ? (((c >= 64) ? ~0ull : ((1ull << c) - 1ull)) << st) : 0ull;
+            if (lane() == 0) lvl(d, 0)[b0 + q] = (uint8_t)__popcll(m_surv & bm);
+            st += c;
+        }
+        wsync<T>();
+    }
+    return keep;
+}
+
 // pack :1401-1453 starting from the underflowing block b of level l
 #ifdef MT_PROF
 TD void pack_impl(DocT<T> &d, int l, int b);
@@ -1067,17 +1306,8 @@ TD void pack(DocT<T> &d, int l, int b) {
         const int nch = cntr(d, l + 1, P);
         int total = 0;
         if (l == 0) {
-            int pos = blk_prefix(d, 0, c0);
-            for (int cb = c0; cb < c0 + nch; cb++) {
-                const int old = cntr(d, 0, cb);
-                const int kept = scour_block(d, pos, pos + old);
-                if (d.status) return;
-                wsync<T>();
-                if (lane() == 0) lvl(d, 0)[cb] = (uint8_t)kept;
-                wsync<T>();
-                pos += kept;
-                total += kept;
-            }
+            total = scour_range(d, blk_prefix(d, 0, c0), c0, nch);
+            if (d.status) return;
         } else {
             for (int cb = c0; cb < c0 + nch; cb++) total += cntr(d, l, cb);
         }
@@ -1128,13 +1358,10 @@ TD void zamboni(DocT<T> &d) {
         const int f = flgr(d, b);
         const int old = cntr(d, 0, b);
         if (f == 0) continue;
-        const int kept = scour_block(d, bstart, bstart + old);
+        const int kept = scour_range(d, bstart, b, 1);
         if (d.status) return;
         wsync<T>();
-        if (lane() == 0) {
-            d.flg[b] = 0;
-            lvl(d, 0)[b] = (uint8_t)kept;
-        }
+        if (lane() == 0) d.flg[b] = 0;
         wsync<T>();
         if (kept < old && kept < MT_HALF && d.depth > 1) pack(d, 0, b);
     }
@@ -1232,7 +1459,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         cb_log(d, 0);
         cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)-1), 0u));
         cb_end(d, cb);
-        zamboni(d);
+        // zamboni runs in apply_op (single inlined site)
         return;
     }
     if (ip < 0) {
@@ -1319,7 +1546,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     cb_log(d, slen);
     cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)pos), (uint32_t)slen));
     cb_end(d, cb);
-    zamboni(d);
+    // zamboni runs in apply_op (single inlined site)
 }
 
 // SegmentPropertiesManager.addProperties MT/segmentPropertiesManager.ts:35-111 applied by
@@ -1428,7 +1655,7 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
     boundary(d, p2, r, c);
     if (d.status) return;
     compute_ends(d);
-    if (!rem) gsync();   // property records written earlier in this launch are read below
+    if (!rem) gsync_rd();   // property records written earlier in this launch are read below
     Cb cb = cb_begin(d, seq, op.kind);
     int carry = 0, ocarry = 0, last_b = -1;
     const int L = lane();
@@ -1486,7 +1713,7 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
             em &= em - 1;
             cb.h = fnv_u64(cb.h, bcast64(sh, j));
             cb.n++;
-            if (d.dlog) {
+            if (T::kLog && d.dlog) {
                 cb_log(d, bcast(opos, j));
                 cb_log(d, bcast(a.x, j));
                 if (!rem) {
@@ -1495,7 +1722,7 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
                     int nl = 0;
                     u64 dummy = 0;
                     const int at = d.dlog_n + 1;
-                    gsync();
+                    gsync_rd();
                     if (L == 0 && at + 4 * MT_KMAX + 2 <= d.DL_cap) {
                         // old record is untouched (new record went to a fresh handle)
                         annotate_record(d, ohj, nhj, rec, dummy, d.dlog + at, nl);
@@ -1525,45 +1752,56 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
         if (ballot(v && pex >= p2)) break;
     }
     cb_end(d, cb);
-    zamboni(d);
+    // zamboni runs in apply_op (single inlined site)
 }
 
-// updateSeqNumbers / updateMinSeq / setMinSeq  MT/client.ts:821-828, 991-1004,
-// MT/mergeTree.ts:1751-1769
-TD void update_seq(DocT<T> &d, int msn, int seq) {
-    if (!(d.cur_seq <= seq)) {
-        fail(d, MT_DOC_SEQ_ORDER);
-        return;
-    }
-    d.cur_seq = seq;
-    if (!(msn <= seq) || !(d.min_seq <= msn)) {
-        fail(d, MT_DOC_MINSEQ_ORDER);
-        return;
-    }
-    if (msn > d.min_seq) {
-        d.min_seq = msn;
-        zamboni(d);
-    }
-}
-
-// Client.applyMsg MT/client.ts:797-819 for one encoded record
+// Client.applyMsg MT/client.ts:797-819 for one encoded record: the op (insertSegments /
+// markRangeRemoved / annotateRange each end with zamboniSegments), completeAndLogOp's
+// asserts (:451-479), then updateSeqNumbers -> setMinSeq (:821-828, 991-1004,
+// MT/mergeTree.ts:1751-1769) whose zamboni runs when minSeq advances.  Both zamboni passes
+// share one call site so the (large) zamboni/scour/pack code is inlined once.
 TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     const mt_op_rec &op = in.op;
+    const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
     if (op.kind == MT_OP_INSERT) {
         op_insert(d, in, tin, pin);
-    } else if (op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE) {
+    } else if (is_op) {
         op_range(d, op, pin);
     }
     if (d.status) return;
-    if (op.kind != MT_OP_NOOP) {   // completeAndLogOp asserts MT/client.ts:451-479
-        if (!(d.cur_seq < op.seq)) {
-            fail(d, MT_DOC_SEQ_ORDER);
-            return;
+    bool z = is_op;
+    for (int pass = 0; pass < 2; pass++) {
+        if (z) {
+            zamboni(d);
+            if (d.status) return;
         }
-        if (!(d.min_seq <= op.min_seq)) {
-            fail(d, MT_DOC_MINSEQ_ORDER);
-            return;
+        if (pass == 1) break;
+        if (op.kind != MT_OP_NOOP) {
+            if (!(d.cur_seq < op.seq)) {
+                fail(d, MT_DOC_SEQ_ORDER);
+                return;
+            }
+            if (!(d.min_seq <= op.min_seq)) {
+                fail(d, MT_DOC_MINSEQ_ORDER);
+                return;
+            }
         }
+        z = false;
+        if (!(op.flags & MT_F_GROUP_MORE)) {
+            if (!(d.cur_seq <= op.seq)) {
+                fail(d, MT_DOC_SEQ_ORDER);
+                return;
+            }
+            d.cur_seq = op.seq;
+            if (!(op.min_seq <= op.seq) || !(d.min_seq <= op.min_seq)) {
+                fail(d, MT_DOC_MINSEQ_ORDER);
+                return;
+            }
+            if (op.min_seq > d.min_seq) {
+                d.min_seq = op.min_seq;
+                z = true;
+            }
+        }
+        if (!z) break;
     }
-    if (!(op.flags & MT_F_GROUP_MORE)) update_seq(d, op.min_seq, op.seq);
 }

@@ -144,6 +144,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
             in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
+            opaque(d);
 
             apply_op(d, in, gt, gp);
         }
@@ -161,6 +162,9 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec
         }
     }
     if (!T::kLds && lane() == 0) st.retry[doc] = 0;
+#ifdef MT_PROF
+    if (lane() < 32) atomicAdd(&g_prof[lane()], d.prof[lane()]);
+#endif
     store_doc(d, st, doc);
 }
 
@@ -514,11 +518,11 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.P = o.props_capacity > 0 ? o.props_capacity : st.S + 2 * MT_WAVE;
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
     if (o.lds_seg_capacity >= 0) {
-        int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 128;
+        int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 192;
         S_l = std::min(S_l, st.S);
         h->lds.S = S_l;
-        h->lds.B = std::min(st.B, std::max(64, (S_l / 2 + 15) / 16 * 16));
-        h->lds.H = std::min(st.H, S_l);
+        h->lds.B = std::min(st.B, std::max(64, (S_l / 2 + 32 + 15) / 16 * 16));
+        h->lds.H = std::min(st.H, S_l + 64);
         if (tier_lds_bytes(true, h->lds, 0) > 60 * 1024) h->lds = TierCaps{0, 0, 0, 0};
     }
     const size_t N = n_docs;
@@ -637,14 +641,22 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     if (h->lds.S > 0) {
         // LDS tier for every document; the ones that outgrow it are flagged and replayed
         // from HBM by the second launch (whose other workgroups exit at once)
-        hipLaunchKernelGGL(k_replay<TierLds>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
-                           h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
+        if (h->st.DL)
+            hipLaunchKernelGGL(k_replay<TierLdsT<true>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+                               h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
+        else
+            hipLaunchKernelGGL(k_replay<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+                               h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
         HIPCHK(h, hipGetLastError());
     } else {
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream));
     }
-    hipLaunchKernelGGL(k_replay<TierGlb>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
-                       h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
+    if (h->st.DL)
+        hipLaunchKernelGGL(k_replay<TierGlbT<true>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
+    else
+        hipLaunchKernelGGL(k_replay<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -729,7 +741,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
     if (ok) {
         const int gw = 2 * (cfg->writers + 1);
         if (h->lds.S > 0) {
-            hipLaunchKernelGGL(k_generate<TierLds>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, gw),
+            hipLaunchKernelGGL(k_generate<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, gw),
                                h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
                                pstride, d_fail, d_trace, h->lds);
             ok = hipGetLastError() == hipSuccess;
@@ -737,7 +749,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
             ok = hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream) == hipSuccess;
         }
         if (ok) {
-            hipLaunchKernelGGL(k_generate<TierGlb>, dim3(h->n_docs), dim3(MT_WAVE),
+            hipLaunchKernelGGL(k_generate<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(false, glb_caps(h), gw), h->stream, h->st, *cfg, doc_index_base,
                                b->ops, b->text, b->props, tstride, pstride, d_fail, d_trace, glb_caps(h));
             ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;

@@ -46,7 +46,7 @@ typedef struct mt_options {
     int32_t props_capacity;  /* property-set records per document   (default seg) */
     int32_t delta_log_capacity; /* int32 words of per-document delta log; 0 = hash only */
     int32_t lds_seg_capacity;   /* segments a document may hold while staged in LDS
-                                   (default 128; -1 = always replay from HBM).  A document
+                                   (default 192; -1 = always replay from HBM).  A document
                                    that outgrows it is replayed from HBM transparently. */
 } mt_options;
 
