@@ -32,6 +32,22 @@ def build(force=False, verbose=False):
     return OUT
 
 
+def build_node_addon(verbose=False):
+    """The N-API addon for the Node facade (fluidframework_amd/js); skipped without Node headers."""
+    js = os.path.join(HERE, "js")
+    out = os.path.join(js, "mtreplay.node")
+    if not os.path.exists("/usr/include/node/node_api.h"):
+        return None
+    deps = [os.path.join(js, "binding.cc"), OUT]
+    if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    if verbose:
+        print("sh", os.path.join(js, "build.sh"))
+    subprocess.check_call(["sh", os.path.join(js, "build.sh")])
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    build_node_addon(verbose=True)
     print(OUT)

@@ -1,0 +1,321 @@
+// binding.cc -- thin N-API addon over the C ABI of include/mt_replay.h (libmtreplay.so).
+//
+// The reference's host language is TypeScript on Node; its merge-tree boundary is the
+// class Client (packages/dds/merge-tree/src/client.ts:43) fed by
+// SharedSegmentSequence.processMergeTreeMsg -> client.applyMsg
+// (packages/dds/sequence/src/sequence.ts:579-600).  This addon exposes the batched
+// replacement to JS; js/index.js builds the Client-shaped facade on top of it and
+// js/encode.js turns ISequencedDocumentMessage objects into the binary wire format.
+//
+// Ownership: JS owns the message buffers (typed arrays); mt_apply_ops copies them to the
+// device.  The handle (device state) is owned by a JS external whose finalizer calls
+// mt_destroy.  Errors: negative MT_E_* codes become thrown JS Errors carrying
+// mt_last_error(); per-document failures are reported through status().
+//
+// Build (node-gyp is not available offline): fluidframework_amd/js/build.sh.
+#include <node_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mt_replay.h"
+
+namespace {
+
+#define NAPI_CALL(env, call)                                                \
+    do {                                                                    \
+        if ((call) != napi_ok) {                                            \
+            napi_throw_error((env), nullptr, "N-API call failed: " #call); \
+            return nullptr;                                                 \
+        }                                                                   \
+    } while (0)
+
+struct Handle {
+    mt_handle *h = nullptr;
+};
+
+void finalize_handle(napi_env, void *data, void *) {
+    auto *hd = static_cast<Handle *>(data);
+    if (hd->h) mt_destroy(hd->h);
+    delete hd;
+}
+
+napi_value throw_rc(napi_env env, const Handle *hd, int rc, const char *what) {
+    std::string msg = std::string(what) + " failed (" + std::to_string(rc) + "): " +
+                      (hd && hd->h ? mt_last_error(hd->h) : "");
+    napi_throw_error(env, nullptr, msg.c_str());
+    return nullptr;
+}
+
+bool get_args(napi_env env, napi_callback_info info, size_t n, napi_value *argv) {
+    size_t argc = n;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok || argc < n) {
+        napi_throw_type_error(env, nullptr, "wrong number of arguments");
+        return false;
+    }
+    return true;
+}
+
+Handle *get_handle(napi_env env, napi_value v) {
+    void *p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p || !static_cast<Handle *>(p)->h) {
+        napi_throw_type_error(env, nullptr, "invalid or destroyed handle");
+        return nullptr;
+    }
+    return static_cast<Handle *>(p);
+}
+
+// data pointer + element count of any TypedArray
+bool typed(napi_env env, napi_value v, void **data, size_t *len) {
+    napi_typedarray_type t;
+    napi_value ab;
+    size_t off;
+    if (napi_get_typedarray_info(env, v, &t, len, data, &ab, &off) != napi_ok) {
+        napi_throw_type_error(env, nullptr, "expected a TypedArray");
+        return false;
+    }
+    return true;
+}
+
+int32_t get_i32(napi_env env, napi_value v) {
+    int32_t x = 0;
+    napi_get_value_int32(env, v, &x);
+    return x;
+}
+
+napi_value make_u32(napi_env env, uint32_t x) {
+    napi_value r;
+    napi_create_uint32(env, x, &r);
+    return r;
+}
+
+// create(nDocs, {device, segCapacity, ...}) -> external handle  (mt_create)
+napi_value Create(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    uint32_t n = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[0], &n));
+    mt_options o;
+    memset(&o, 0, sizeof(o));
+    const char *names[] = {"device", "segCapacity", "blockCapacity", "heapCapacity", "textCapacity",
+                           "propsCapacity", "deltaLogCapacity", "ldsSegCapacity"};
+    int32_t *fields[] = {&o.device, &o.seg_capacity, &o.block_capacity, &o.heap_capacity, &o.text_capacity,
+                         &o.props_capacity, &o.delta_log_capacity, &o.lds_seg_capacity};
+    for (int i = 0; i < 8; i++) {
+        bool has = false;
+        napi_has_named_property(env, argv[1], names[i], &has);
+        if (has) {
+            napi_value v;
+            napi_get_named_property(env, argv[1], names[i], &v);
+            *fields[i] = get_i32(env, v);
+        }
+    }
+    auto *hd = new Handle();
+    hd->h = mt_create(n, &o);
+    if (!hd->h) {
+        delete hd;
+        napi_throw_error(env, nullptr,
+                         "mt_create failed: no HIP device visible or out of device memory "
+                         "(the replay backend has no CPU fallback)");
+        return nullptr;
+    }
+    napi_value ext;
+    NAPI_CALL(env, napi_create_external(env, hd, finalize_handle, nullptr, &ext));
+    return ext;
+}
+
+napi_value Destroy(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    void *p = nullptr;
+    NAPI_CALL(env, napi_get_value_external(env, argv[0], &p));
+    auto *hd = static_cast<Handle *>(p);
+    if (hd && hd->h) {
+        mt_destroy(hd->h);
+        hd->h = nullptr;
+    }
+    return nullptr;
+}
+
+// loadInitialText(h, seedOff: BigInt64Array, seed: Uint16Array)
+napi_value LoadInitialText(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *off, *txt;
+    size_t noff, ntxt;
+    if (!typed(env, argv[1], &off, &noff) || !typed(env, argv[2], &txt, &ntxt)) return nullptr;
+    if (noff != mt_num_docs(hd->h) + 1) {
+        napi_throw_range_error(env, nullptr, "seedOff must hold nDocs + 1 offsets");
+        return nullptr;
+    }
+    const int rc = mt_load_initial_text(hd->h, (const int64_t *)off, (const uint16_t *)txt);
+    if (rc) return throw_rc(env, hd, rc, "mt_load_initial_text");
+    return nullptr;
+}
+
+// applyOps(h, docOff: BigInt64Array, ops: Uint8Array (32-byte records), text: Uint16Array,
+//          props: Uint32Array) -- Client.applyMsg for every message (mt_apply_ops)
+napi_value ApplyOps(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *off, *ops, *txt, *props;
+    size_t noff, nops, ntxt, nprops;
+    if (!typed(env, argv[1], &off, &noff) || !typed(env, argv[2], &ops, &nops) ||
+        !typed(env, argv[3], &txt, &ntxt) || !typed(env, argv[4], &props, &nprops))
+        return nullptr;
+    if (noff != mt_num_docs(hd->h) + 1 || nops % sizeof(mt_op_rec) != 0) {
+        napi_throw_range_error(env, nullptr, "docOff must hold nDocs + 1 offsets; ops whole 32-byte records");
+        return nullptr;
+    }
+    const int rc = mt_apply_ops(hd->h, (const int64_t *)off, (const mt_op_rec *)ops, nops / sizeof(mt_op_rec),
+                                (const uint16_t *)txt, ntxt, (const uint32_t *)props, nprops);
+    if (rc) return throw_rc(env, hd, rc, "mt_apply_ops");
+    return nullptr;
+}
+
+// status(h) -> Int32Array[nDocs]   (enum mt_doc_status)
+napi_value Status(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const uint32_t n = mt_num_docs(hd->h);
+    void *data;
+    napi_value ab, arr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 4, &data, &ab));
+    const int rc = mt_get_status(hd->h, (int32_t *)data);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_status");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab, 0, &arr));
+    return arr;
+}
+
+// getLength(h, doc) -> number   (Client.getLength, client.ts:1051)
+napi_value GetLength(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    uint32_t len = 0;
+    const int rc = mt_get_length(hd->h, (uint32_t)get_i32(env, argv[1]), &len);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_length");
+    return make_u32(env, len);
+}
+
+// getText(h, doc) -> string   (MergeTreeTextHelper.getText, textSegment.ts:154-172)
+napi_value GetText(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const uint32_t doc = (uint32_t)get_i32(env, argv[1]);
+    uint32_t n = 0;
+    int rc = mt_get_text(hd->h, doc, nullptr, 0, &n);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_text");
+    std::vector<uint16_t> buf(n ? n : 1);
+    rc = mt_get_text(hd->h, doc, buf.data(), n, &n);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_text");
+    napi_value s;
+    NAPI_CALL(env, napi_create_string_utf16(env, (const char16_t *)buf.data(), n, &s));
+    return s;
+}
+
+// getPropRuns(h, doc) -> {runs: Uint32Array (start, length, record) x n, records: Uint32Array}
+napi_value GetPropRuns(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const uint32_t doc = (uint32_t)get_i32(env, argv[1]);
+    uint32_t nr = 0, nw = 0;
+    int rc = mt_get_prop_runs(hd->h, doc, nullptr, 0, &nr, nullptr, 0, &nw);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_prop_runs");
+    void *rd, *wd;
+    napi_value rab, wab, ra, wa, obj;
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)3 * nr * 4, &rd, &rab));
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)nw * 4, &wd, &wab));
+    rc = mt_get_prop_runs(hd->h, doc, (uint32_t *)rd, nr, &nr, (uint32_t *)wd, nw, &nw);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_prop_runs");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, (size_t)3 * nr, rab, 0, &ra));
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, nw, wab, 0, &wa));
+    NAPI_CALL(env, napi_create_object(env, &obj));
+    NAPI_CALL(env, napi_set_named_property(env, obj, "runs", ra));
+    NAPI_CALL(env, napi_set_named_property(env, obj, "records", wa));
+    return obj;
+}
+
+// getDeltaLog(h, doc) -> Int32Array (only with deltaLogCapacity > 0; oracle layout)
+napi_value GetDeltaLog(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const uint32_t doc = (uint32_t)get_i32(env, argv[1]);
+    uint32_t n = 0;
+    int rc = mt_get_delta_log(hd->h, doc, nullptr, 0, &n);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_delta_log");
+    void *d;
+    napi_value ab, arr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 4, &d, &ab));
+    rc = mt_get_delta_log(hd->h, doc, (int32_t *)d, n, &n);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_delta_log");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab, 0, &arr));
+    return arr;
+}
+
+// checksums(h) -> ArrayBuffer of mt_checksum[nDocs] (32 B each)
+napi_value Checksums(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *d;
+    napi_value ab;
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)mt_num_docs(hd->h) * sizeof(mt_checksum), &d, &ab));
+    const int rc = mt_checksums(hd->h, (mt_checksum *)d);
+    if (rc) return throw_rc(env, hd, rc, "mt_checksums");
+    return ab;
+}
+
+napi_value LastKernelMs(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    napi_value r;
+    NAPI_CALL(env, napi_create_double(env, mt_last_kernel_ms(hd->h), &r));
+    return r;
+}
+
+napi_value NumDocs(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    return make_u32(env, mt_num_docs(hd->h));
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+    struct {
+        const char *name;
+        napi_callback fn;
+    } fns[] = {{"create", Create},         {"destroy", Destroy},           {"loadInitialText", LoadInitialText},
+               {"applyOps", ApplyOps},     {"status", Status},             {"getLength", GetLength},
+               {"getText", GetText},       {"getPropRuns", GetPropRuns},   {"getDeltaLog", GetDeltaLog},
+               {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs}};
+    for (auto &f : fns) {
+        napi_value v;
+        NAPI_CALL(env, napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v));
+        NAPI_CALL(env, napi_set_named_property(env, exports, f.name, v));
+    }
+    return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

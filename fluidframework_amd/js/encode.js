@@ -1,0 +1,226 @@
+"use strict";
+/**
+ * encode.js -- turns ISequencedDocumentMessage objects carrying merge-tree ops
+ * (protocol-definitions/src/protocol.ts:132-172, merge-tree/src/ops.ts:63-110) into the
+ * binary wire format of include/mt_types.h: one 32-byte mt_op_rec per op, a UTF-16 text
+ * arena and a u32 property arena.  Mirrors fluidframework_amd/wire.py (the Python encoder
+ * the tests use) field for field.
+ *
+ * Client ids are interned per document in first-seen order with the observer at 0, like
+ * Client.getOrAddShortClientId (merge-tree/src/client.ts:637-661); only equality of short
+ * ids matters to the replay.  Property keys and values are interned per batch; value ids
+ * carry MT_VAL_FALSY_BIT when the JS value is falsy (the `rewrite` rule tests
+ * `!newProps[key]`, merge-tree/src/segmentPropertiesManager.ts:72).
+ */
+
+const OP_INSERT = 0;
+const OP_REMOVE = 1;
+const OP_ANNOTATE = 2;
+const OP_NOOP = 3;
+const OP_GROUP = 3;          // MergeTreeDeltaType.GROUP in the op JSON (ops.ts:33)
+const F_GROUP_MORE = 1;
+const F_MARKER = 2;
+const NO_PROPS = 0xFFFFFFFF;
+const VAL_NULL = 0xFFFFFFFF;
+const VAL_FALSY_BIT = 0x80000000;
+const COMBINE_NONE = 0;
+const COMBINE_REWRITE = 1;
+const COMBINE_OTHER = 2;
+const OP_BYTES = 32;
+
+/** Canonical JSON (sorted keys): matchProperties compares nested values structurally. */
+function canonical(v) {
+    if (v === null || typeof v !== "object") { return JSON.stringify(v); }
+    if (Array.isArray(v)) { return `[${v.map(canonical).join(",")}]`; }
+    return `{${Object.keys(v).sort().map((k) => `${JSON.stringify(k)}:${canonical(v[k])}`).join(",")}}`;
+}
+
+class Interner {
+    constructor() {
+        this.keys = [];
+        this.keyIds = new Map();
+        this.vals = [];
+        this.valIds = new Map();
+    }
+    key(k) {
+        let i = this.keyIds.get(k);
+        if (i === undefined) {
+            i = this.keys.length;
+            this.keyIds.set(k, i);
+            this.keys.push(k);
+        }
+        return i;
+    }
+    val(v) {
+        if (v === null || v === undefined) { return VAL_NULL; }
+        const c = canonical(v);
+        let i = this.valIds.get(c);
+        if (i === undefined) {
+            i = this.vals.length;
+            this.valIds.set(c, i);
+            this.vals.push(v);
+        }
+        return (i | (v ? 0 : VAL_FALSY_BIT)) >>> 0;
+    }
+    keyName(id) { return this.keys[id]; }
+    value(id) { return id === VAL_NULL ? null : this.vals[(id & ~VAL_FALSY_BIT) >>> 0]; }
+}
+
+/** Growable typed-array builder. */
+class Grow {
+    constructor(Ctor, cap = 1024) {
+        this.Ctor = Ctor;
+        this.a = new Ctor(cap);
+        this.n = 0;
+    }
+    reserve(k) {
+        if (this.n + k <= this.a.length) { return; }
+        let cap = this.a.length * 2;
+        while (cap < this.n + k) { cap *= 2; }
+        const b = new this.Ctor(cap);
+        b.set(this.a.subarray(0, this.n));
+        this.a = b;
+    }
+    push(x) { this.reserve(1); this.a[this.n++] = x; }
+    view() { return this.a.subarray(0, Math.max(this.n, 1)); }
+}
+
+/**
+ * Accumulates the messages of N documents (CSR by document) ready for mt_apply_ops.
+ * Documents are added in handle order; each document's messages in sequence order.
+ */
+class BatchEncoder {
+    constructor(interner = new Interner()) {
+        this.interner = interner;
+        this.ops = new Grow(Uint8Array, 32 * 1024);
+        this.nOps = 0;
+        this.text = new Grow(Uint16Array, 16 * 1024);
+        this.props = new Grow(Uint32Array, 4 * 1024);
+        this.docOff = [0];
+    }
+
+    _text(s) {
+        const off = this.text.n;
+        this.text.reserve(s.length);
+        for (let i = 0; i < s.length; i++) { this.text.a[this.text.n++] = s.charCodeAt(i); }
+        return [off, s.length];
+    }
+
+    _props(p, combine = COMBINE_NONE) {
+        const off = this.props.n;
+        const keys = Object.keys(p);
+        this.props.push((keys.length | (combine << 16)) >>> 0);
+        for (const k of keys) {
+            this.props.push(this.interner.key(k));
+            this.props.push(this.interner.val(p[k]));
+        }
+        return off;
+    }
+
+    _rec(r) {
+        this.ops.reserve(OP_BYTES);
+        const dv = new DataView(this.ops.a.buffer, this.ops.a.byteOffset + this.ops.n, OP_BYTES);
+        dv.setInt32(0, r.seq, true);
+        dv.setInt32(4, r.refSeq, true);
+        dv.setInt32(8, r.minSeq, true);
+        dv.setInt32(12, r.pos1, true);
+        dv.setInt32(16, r.pos2, true);
+        dv.setUint32(20, r.payload >>> 0, true);
+        dv.setUint32(24, r.props >>> 0, true);
+        dv.setUint16(28, r.client, true);
+        dv.setUint8(30, r.kind);
+        dv.setUint8(31, r.flags);
+        this.ops.n += OP_BYTES;
+        this.nOps++;
+    }
+
+    _op(msg, client, op, more) {
+        const r = {
+            seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber, minSeq: msg.minimumSequenceNumber,
+            client, flags: more ? F_GROUP_MORE : 0, props: NO_PROPS, pos1: 0, pos2: 0, payload: 0, kind: OP_NOOP,
+        };
+        if (op.type === OP_INSERT) {
+            const seg = op.seg;
+            r.kind = OP_INSERT;
+            r.pos1 = op.pos1;
+            if (!seg) {
+                // `if (op.seg)` is falsy: applyInsertOp returns without touching the tree
+                // (client.ts:402-426) -> only the seq/msn update
+                r.kind = OP_NOOP;
+            } else if (typeof seg === "string") {
+                [r.payload, r.pos2] = this._text(seg);
+            } else if (seg.text !== undefined) {
+                [r.payload, r.pos2] = this._text(seg.text);
+                if (seg.props !== undefined && seg.props !== null) { r.props = this._props(seg.props); }
+            } else if (seg.marker !== undefined) {
+                r.flags |= F_MARKER;
+                r.payload = seg.marker.refType | 0;
+                r.pos2 = 1;
+                if (seg.props !== undefined && seg.props !== null) { r.props = this._props(seg.props); }
+            } else {
+                throw new Error(`unsupported insert segment ${JSON.stringify(seg)}`);
+            }
+        } else if (op.type === OP_REMOVE || op.type === OP_ANNOTATE) {
+            if (op.relativePos1 !== undefined || op.relativePos2 !== undefined || op.register !== undefined) {
+                throw new Error("relative-position and register ops are not supported by the replay backend");
+            }
+            r.kind = op.type;
+            r.pos1 = op.pos1;
+            r.pos2 = op.pos2;
+            if (op.type === OP_ANNOTATE) {
+                const c = op.combiningOp;
+                const code = !c ? COMBINE_NONE : (c.name === "rewrite" ? COMBINE_REWRITE : COMBINE_OTHER);
+                r.props = this._props(op.props, code);
+            }
+        } else {
+            throw new Error(`unsupported op type ${op.type}`);
+        }
+        this._rec(r);
+    }
+
+    /**
+     * Appends one document's messages.  `clients` is the document's persistent long->short
+     * id map (observer = 0), shared across batches so ids stay stable.
+     */
+    addDoc(msgs, clients) {
+        const short = (id) => {
+            let s = clients.get(id);
+            if (s === undefined) {
+                s = clients.size + 1;
+                clients.set(id, s);
+            }
+            return s;
+        };
+        for (const msg of msgs) {
+            const c = short(msg.clientId);
+            if (msg.type !== undefined && msg.type !== "op") {
+                this._rec({
+                    seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber, minSeq: msg.minimumSequenceNumber,
+                    client: c, kind: OP_NOOP, flags: 0, props: NO_PROPS, pos1: 0, pos2: 0, payload: 0,
+                });
+                continue;
+            }
+            const op = msg.contents;
+            if (op.type === OP_GROUP) {
+                op.ops.forEach((m, i) => this._op(msg, c, m, i + 1 < op.ops.length));
+            } else {
+                this._op(msg, c, op, false);
+            }
+        }
+        this.docOff.push(this.nOps);
+    }
+
+    arrays() {
+        return {
+            docOff: BigInt64Array.from(this.docOff.map(BigInt)),
+            ops: this.ops.a.subarray(0, this.ops.n),
+            text: this.text.view(),
+            props: this.props.view(),
+        };
+    }
+}
+
+module.exports = {
+    BatchEncoder, Interner, canonical,
+    OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_GROUP_MORE, F_MARKER, NO_PROPS, VAL_NULL, VAL_FALSY_BIT,
+};

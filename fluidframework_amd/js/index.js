@@ -1,0 +1,231 @@
+"use strict";
+/**
+ * index.js -- Node facade of the MI355X merge-tree replay backend.
+ *
+ * GpuMergeTreeBatch owns N observer replicas resident on one GPU (one handle of the C ABI,
+ * include/mt_replay.h, through the N-API addon js/binding.cc).  batch.client(doc) returns a
+ * Client-shaped view of one document with the surface SharedSegmentSequence uses on the
+ * reference Client (merge-tree/src/client.ts:43; sequence/src/sequence.ts:131-142,
+ * 473-600): applyMsg, startOrUpdateCollaboration, getLength, getText (as
+ * createTextHelper().getText), getPropertiesAtPosition, getCurrentSeq and the
+ * mergeTreeDeltaCallback property.
+ *
+ * applyMsg only queues the message (the GPU applies whole batches); any read, or an
+ * explicit batch.flush(), applies everything queued for every document in one launch.
+ * Per-document failures are raised from the next call on that document with the
+ * reference's messages and error types (client.ts:462-465, 824-826; mergeTree.ts:2244).
+ * There is no CPU fallback: without the addon or a GPU the constructor throws.
+ */
+const assert = require("assert");
+const path = require("path");
+const { BatchEncoder, Interner, VAL_NULL } = require("./encode");
+
+const native = require(path.join(__dirname, "mtreplay.node"));
+
+const DOC_STATUS = {
+    1: () => new Error("MergeTree insert failed"),
+    2: () => new assert.AssertionError({ message: "Incoming remote op sequence# <= local collabWindow's currentSequence#" }),
+    3: () => new assert.AssertionError({ message: "Incoming remote op minSequence# < local collabWindow's minSequence#" }),
+    4: () => new Error("merge-tree replay: a per-document capacity was exceeded"),
+    5: () => new Error("merge-tree replay: combiningOp other than rewrite is not supported"),
+    6: () => new Error("merge-tree replay: internal error"),
+};
+
+/** JS own-key order: integer-like keys ascending first, then insertion order. */
+function jsKeyOrder(pairs) {
+    const isIndex = (k) => /^(0|[1-9][0-9]*)$/.test(k) && Number(k) < 4294967295;
+    const ints = pairs.filter(([k]) => isIndex(k)).sort((a, b) => Number(a[0]) - Number(b[0]));
+    return ints.concat(pairs.filter(([k]) => !isIndex(k)));
+}
+
+class GpuMergeTreeBatch {
+    /**
+     * @param {number} nDocs  documents (observer replicas) on this GPU
+     * @param {object} options  mt_options: device, segCapacity, textCapacity, deltaLogCapacity, ...
+     */
+    constructor(nDocs, options = {}) {
+        this.h = native.create(nDocs, options);
+        this.nDocs = nDocs;
+        this.interner = new Interner();
+        this.clients = Array.from({ length: nDocs }, () => new Map());
+        this.pending = Array.from({ length: nDocs }, () => []);
+        this.queued = 0;
+        this.failed = new Int32Array(nDocs);
+        this.views = new Map();
+        this.logPos = new Int32Array(nDocs);
+        this.wantsDeltas = !!options.deltaLogCapacity;
+    }
+
+    /** Initial contents of every document (Client.insertSegmentLocal before collaboration). */
+    loadInitialText(texts) {
+        assert(texts.length === this.nDocs);
+        let total = 0;
+        for (const t of texts) { total += t.length; }
+        const seed = new Uint16Array(Math.max(total, 1));
+        const off = new BigInt64Array(this.nDocs + 1);
+        let k = 0;
+        texts.forEach((t, d) => {
+            off[d] = BigInt(k);
+            for (let i = 0; i < t.length; i++) { seed[k++] = t.charCodeAt(i); }
+        });
+        off[this.nDocs] = BigInt(k);
+        native.loadInitialText(this.h, off, seed);
+        this.logPos.fill(0);
+    }
+
+    client(doc) {
+        let v = this.views.get(doc);
+        if (!v) {
+            v = new GpuClient(this, doc);
+            this.views.set(doc, v);
+        }
+        return v;
+    }
+
+    /** Applies every queued message of every document (one mt_apply_ops). */
+    flush() {
+        if (this.queued === 0) { return; }
+        const enc = new BatchEncoder(this.interner);
+        for (let d = 0; d < this.nDocs; d++) {
+            enc.addDoc(this.pending[d], this.clients[d]);
+            this.pending[d] = [];
+        }
+        this.queued = 0;
+        const a = enc.arrays();
+        native.applyOps(this.h, a.docOff, a.ops, a.text, a.props);
+        const st = native.status(this.h);
+        for (let d = 0; d < this.nDocs; d++) {
+            if (st[d] !== 0 && this.failed[d] === 0) { this.failed[d] = st[d]; }
+        }
+        if (this.wantsDeltas) {
+            for (const v of this.views.values()) { v._emitDeltas(); }
+        }
+    }
+
+    status() { this.flush(); return native.status(this.h); }
+
+    /** mt_checksum per document: {length, nSegments, textHash, propsHash, deltaHash}. */
+    checksums() {
+        this.flush();
+        const ab = native.checksums(this.h);
+        const dv = new DataView(ab);
+        const out = [];
+        for (let d = 0; d < this.nDocs; d++) {
+            const o = d * 32;
+            out.push({
+                length: dv.getUint32(o, true), nSegments: dv.getUint32(o + 4, true),
+                textHash: dv.getBigUint64(o + 8, true), propsHash: dv.getBigUint64(o + 16, true),
+                deltaHash: dv.getBigUint64(o + 24, true),
+            });
+        }
+        return out;
+    }
+
+    lastKernelMs() { return native.lastKernelMs(this.h); }
+
+    dispose() { native.destroy(this.h); }
+}
+
+/** Client-shaped view of one document (the observer replica). */
+class GpuClient {
+    constructor(batch, doc) {
+        this.batch = batch;
+        this.doc = doc;
+        this.longClientId = undefined;
+        this.currentSeq = 0;
+        this.mergeTreeDeltaCallback = undefined;
+    }
+
+    _check() {
+        const code = this.batch.failed[this.doc];
+        if (code) { throw DOC_STATUS[code] ? DOC_STATUS[code]() : new Error(`document status ${code}`); }
+    }
+
+    _sync() {
+        this.batch.flush();
+        this._check();
+    }
+
+    /** Client.startOrUpdateCollaboration (client.ts:1053-1073): the observer is short id 0. */
+    startOrUpdateCollaboration(longClientId) {
+        this.longClientId = longClientId;
+    }
+
+    /** Client.applyMsg (client.ts:797-819); applied on the GPU at the next flush. */
+    applyMsg(msg) {
+        this._check();
+        if (msg.clientId === this.longClientId && msg.clientId !== undefined) {
+            throw new Error("merge-tree replay: the observer replica has no local ops to acknowledge");
+        }
+        this.batch.pending[this.doc].push(msg);
+        this.batch.queued++;
+        this.currentSeq = msg.sequenceNumber;
+    }
+
+    getCurrentSeq() { return this.currentSeq; }
+
+    getLength() { this._sync(); return native.getLength(this.batch.h, this.doc); }
+
+    getText() { this._sync(); return native.getText(this.batch.h, this.doc); }
+
+    createTextHelper() { return { getText: () => this.getText() }; }
+
+    /** Client.getPropertiesAtPosition (client.ts:1011-1025). */
+    getPropertiesAtPosition(pos) {
+        this._sync();
+        const { runs, records } = native.getPropRuns(this.batch.h, this.doc);
+        for (let i = 0; i < runs.length; i += 3) {
+            const start = runs[i], len = runs[i + 1], rec = runs[i + 2];
+            if (pos >= start && pos < start + len) {
+                if (rec === 0xFFFFFFFF) { return undefined; }
+                const n = records[rec];
+                const pairs = [];
+                for (let j = 0; j < n; j++) {
+                    pairs.push([this.batch.interner.keyName(records[rec + 1 + 2 * j]),
+                        this.batch.interner.value(records[rec + 2 + 2 * j])]);
+                }
+                const props = {};
+                for (const [k, v] of jsKeyOrder(pairs)) { props[k] = v; }
+                return props;
+            }
+        }
+        return undefined;
+    }
+
+    /**
+     * Replays the device delta log into mergeTreeDeltaCallback(opArgs, deltaArgs) calls
+     * (mergeTreeDeltaCallback.ts:33-41): one per op, deltaSegments carrying the segment's
+     * cachedLength, its observer position at callback time (what SequenceDeltaEvent.ranges
+     * reads through getPosition) and, for annotate, the propertyDeltas.
+     */
+    _emitDeltas() {
+        const cb = this.mergeTreeDeltaCallback;
+        const log = native.getDeltaLog(this.batch.h, this.doc);
+        let i = this.batch.logPos[this.doc];
+        while (i + 3 <= log.length) {
+            const seq = log[i], kind = log[i + 1], n = log[i + 2];
+            i += 3;
+            const deltaSegments = [];
+            for (let s = 0; s < n; s++) {
+                const pos = log[i], len = log[i + 1];
+                i += 2;
+                const delta = { segment: { cachedLength: len }, position: pos };
+                if (kind === 2) {
+                    const npd = log[i++];
+                    const pd = [];
+                    for (let j = 0; j < npd; j++) {
+                        pd.push([this.batch.interner.keyName(log[i]), this.batch.interner.value(log[i + 1] >>> 0)]);
+                        i += 2;
+                    }
+                    delta.propertyDeltas = {};
+                    for (const [k, v] of pd) { delta.propertyDeltas[k] = v === undefined ? null : v; }
+                }
+                if (pos >= 0) { deltaSegments.push(delta); }
+            }
+            if (cb) { cb({ sequencedMessage: { sequenceNumber: seq } }, { operation: kind, deltaSegments }); }
+        }
+        this.batch.logPos[this.doc] = i;
+    }
+}
+
+module.exports = { GpuMergeTreeBatch, GpuClient, native, VAL_NULL };

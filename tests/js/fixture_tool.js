@@ -1,0 +1,54 @@
+"use strict";
+// Test driver for the Node facade (fluidframework_amd/js).  Usage:
+//   node tests/js/fixture_tool.js encode <fixture.json.gz>   -> JSON {ops,text,props,docOff} (hex)
+//   node tests/js/fixture_tool.js replay <fixture.json.gz>   -> JSON per doc {text,length,status,props}
+// The fixtures were produced by the reference itself (tests/golden/make_golden.py).
+const fs = require("fs");
+const zlib = require("zlib");
+const path = require("path");
+const repo = path.join(__dirname, "..", "..");
+const { BatchEncoder, Interner } = require(path.join(repo, "fluidframework_amd", "js", "encode.js"));
+
+function load(file) {
+    return JSON.parse(zlib.gunzipSync(fs.readFileSync(file)).toString("utf8"));
+}
+function msgs(doc) {
+    return doc.msgs.map((rec) => ({
+        clientId: `client-${rec[0]}`, sequenceNumber: rec[1], referenceSequenceNumber: rec[2],
+        minimumSequenceNumber: rec[3], contents: rec[4], type: rec.length > 5 ? rec[5] : "op",
+    }));
+}
+const hex = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("hex");
+
+const [mode, file] = process.argv.slice(2);
+const fx = load(file);
+if (mode === "encode") {
+    const enc = new BatchEncoder(new Interner());
+    for (const d of fx.docs) { enc.addDoc(msgs(d), new Map()); }
+    const a = enc.arrays();
+    process.stdout.write(JSON.stringify({
+        ops: hex(a.ops), text: hex(a.text), props: hex(a.props), docOff: Array.from(a.docOff, Number),
+        keys: enc.interner.keys, vals: enc.interner.vals,
+    }));
+} else if (mode === "replay") {
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const batch = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 4096, textCapacity: 1 << 17 });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const views = fx.docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        for (const m of msgs(d)) { c.applyMsg(m); }
+        return c;
+    });
+    const out = views.map((c, i) => {
+        try {
+            const len = c.getLength();
+            const probe = [];
+            for (let p = 0; p < len; p += Math.max(1, Math.floor(len / 7))) { probe.push([p, c.getPropertiesAtPosition(p) || null]); }
+            return { text: c.getText(), length: len, props: probe };
+        } catch (e) {
+            return { error: e.message, type: e.constructor.name };
+        }
+    });
+    process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }));
+}

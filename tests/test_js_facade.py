@@ -1,0 +1,78 @@
+"""The Node facade (fluidframework_amd/js: N-API addon + encoder + Client-shaped views):
+the addon builds and loads, its encoder produces exactly the Python encoder's wire bytes
+for the reference-generated fixtures, and (GPU) a fixture replayed through
+Client.applyMsg-shaped calls matches the reference's text, length and properties."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JS = os.path.join(REPO, "fluidframework_amd", "js")
+TOOL = os.path.join(REPO, "tests", "js", "fixture_tool.js")
+pytestmark = pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+
+
+def _node(*args, timeout=300):
+    out = subprocess.run(["node", TOOL, *args], capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout)
+
+
+def _addon():
+    from fluidframework_amd import build
+    build.build()
+    if not os.path.exists(os.path.join(JS, "mtreplay.node")):
+        subprocess.check_call(["sh", os.path.join(JS, "build.sh")])
+
+
+def test_addon_loads_and_fails_loudly_without_gpu():
+    _addon()
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run(["node", "-e", "const m=require(process.argv[1]); new m.GpuMergeTreeBatch(2, {});", JS],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "no CPU fallback" in r.stderr
+
+
+@pytest.mark.parametrize("name", ["ref_ext", "ref_ext_long", "ref_small"])
+def test_js_encoder_matches_python_encoder(name):
+    fx = gu.load(name)
+    got = _node("encode", os.path.join(gu.GOLDEN, name + ".json.gz"))
+    interner = gu.Interner()   # real (non-synthetic) interning, as the JS encoder does
+    a = gu.encode_docs(fx, interner)
+    assert got["docOff"] == a["doc_off"].tolist()
+    assert bytes.fromhex(got["ops"]) == a["ops"].tobytes()
+    n_text = len(bytes.fromhex(got["text"])) // 2
+    assert bytes.fromhex(got["text"]) == a["text"][:n_text].tobytes()
+    n_props = len(bytes.fromhex(got["props"])) // 4
+    assert bytes.fromhex(got["props"]) == a["props"][:n_props].tobytes()
+    assert got["keys"] == interner.keys
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_ext", "ref_c3"])
+def test_js_facade_replays_fixture_like_reference(name):
+    _addon()
+    fx = gu.load(name)
+    got = _node("replay", os.path.join(gu.GOLDEN, name + ".json.gz"))
+    for d, g in zip(fx["docs"], got["docs"]):
+        assert "error" not in g, g
+        assert g["text"] == d["out"]["text"]
+        assert g["length"] == d["out"]["length"]
+        # properties at probed positions == the reference's segment properties there
+        runs = []
+        pos = 0
+        for s in d["out"]["segs"]:
+            if s["rseq"] is None:
+                runs.append((pos, s["len"], s["props"]))
+                pos += s["len"]
+        for p, props in g["props"]:
+            exp = next((r[2] for r in runs if r[0] <= p < r[0] + r[1]), None)
+            assert props == exp, (p, props, exp)
