@@ -121,12 +121,10 @@ def main():
     digest = None
     if dist is not None:
         import torch
+        from fluidframework_amd.shard import digest as sum_digest, gather_checksums
         local = torch.empty(docs * 32, dtype=torch.uint8, device="cuda")
         mt.checksums_device(local.data_ptr())
-        gathered = torch.empty(world * docs * 32, dtype=torch.uint8, device="cuda")
-        dist.all_gather_into_tensor(gathered, local)
-        g = gathered.cpu().numpy().view(np.uint64)
-        digest = int(np.bitwise_xor.reduce(g))
+        digest = sum_digest(gather_checksums(local, dist))
         ok = torch.tensor([1 if replay_consistent else 0], device="cuda")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         replay_consistent = bool(ok.item())
