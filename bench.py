@@ -47,10 +47,10 @@ def parse():
 
 def capacities(cfg):
     """Per-document capacities sized for the workload (DESIGN.md 'HBM layout')."""
-    if cfg["writers"] > 8 or cfg["lag"] > 64:
-        return dict(seg_capacity=8192, text_capacity=1 << 16, heap_capacity=8192, props_capacity=8192 + 256)
-    if cfg["ops"] > 4000:
-        return dict(seg_capacity=1024, text_capacity=1 << 15, heap_capacity=2048, props_capacity=1024 + 128)
+    if cfg["writers"] > 8 or cfg["lag"] > 64 or cfg["p_insert_props"] > 0 or cfg["ops"] > 4000:
+        # annotate keeps segments apart (property sets differ): ~0.4 live segments per op
+        segs = max(1024, int(cfg["ops"] * 0.5) + 512)
+        return dict(seg_capacity=segs, text_capacity=1 << 16, heap_capacity=segs, props_capacity=2 * segs + 256)
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
 
@@ -198,7 +198,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "k_replay", "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
+            "kernel": "k_replay<TierLdsT<false>> + k_replay<TierGlbT<false>> (HBM-tier hand-over)",
+            "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
             "docs_replayed_from_hbm": hbm_docs,
         },
         "cpu_baseline": cpu,

@@ -26,11 +26,14 @@ def main():
     stats = {r["Name"]: dict(calls=int(r["Calls"]), avg_ms=float(r["AverageNs"]) / 1e6,
                               pct=float(r["Percentage"]))
              for r in rows(os.path.join(src, "trace", "**", "*kernel_stats.csv"))}
-    counters = {}
+    counters, dispatches = {}, {}
     for r in rows(os.path.join(src, "pmc*", "**", "*counter_collection.csv")):
-        if not r["Kernel_Name"].startswith("void k_replay<TierLds>") and "k_replay<TierLds>" not in r["Kernel_Name"]:
+        if "k_replay<TierLdsT<false>" not in r["Kernel_Name"]:
             continue
         counters[r["Counter_Name"]] = counters.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        dispatches.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
+    # average per dispatch (one dispatch = one replay of the whole batch)
+    counters = {k: v / max(len(dispatches[k]), 1) for k, v in counters.items()}
     per_op = {k: v / ops for k, v in counters.items() if k.startswith("SQ_INSTS") or k.startswith("SQ_WAIT")
               or k in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT",
                        "SQ_LDS_IDX_ACTIVE", "SQ_ACTIVE_INST_VALU")}
@@ -39,7 +42,7 @@ def main():
         hbm = 2 * counters["FETCH_SIZE"] * 1024 + counters["WRITE_SIZE"] * 1024
     out = dict(bench=bench, kernels=stats, lds_tier_counters=counters, lds_tier_per_op=per_op,
                hbm_bytes_per_launch_lds_tier=hbm,
-               note="counters summed over the k_replay<TierLds> dispatch of one step (--steps 1 --warmup 0);"
+               note="counters averaged per k_replay<TierLdsT<false>> dispatch (one replay of the batch);"
                     " FETCH_SIZE doubled per the gfx950 correction; KB = 1024 B")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
