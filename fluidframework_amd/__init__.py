@@ -23,11 +23,13 @@ class MergeTreeBatch:
     """
 
     def __init__(self, n_docs, device=0, seg_capacity=0, block_capacity=0, heap_capacity=0,
-                 text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0):
+                 text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0,
+                 page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
                                 text_capacity, props_capacity, delta_log_capacity,
-                                lds_seg_capacity)
+                                lds_seg_capacity, page_capacity, page_heap_capacity,
+                                unsettled_capacity, uid_capacity)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")
@@ -173,6 +175,10 @@ class MergeTreeBatch:
         self._check(self.lib.mt_debug_raw(self.h, doc, _native.ptr(rows), n.value, ctypes.byref(n), None),
                     "mt_debug_raw")
         return rows[:n.value], hdr
+
+    def is_paged(self, doc):
+        """True when the document lives in the paged layout (DESIGN.md 'Paged documents')."""
+        return bool(self.debug_raw(doc)[1][24])
 
     def get_delta_log(self, doc):
         n = ctypes.c_uint32()

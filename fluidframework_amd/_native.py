@@ -17,7 +17,9 @@ class MtOptions(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("seg_capacity", ctypes.c_int32),
                 ("block_capacity", ctypes.c_int32), ("heap_capacity", ctypes.c_int32),
                 ("text_capacity", ctypes.c_int32), ("props_capacity", ctypes.c_int32),
-                ("delta_log_capacity", ctypes.c_int32), ("lds_seg_capacity", ctypes.c_int32)]
+                ("delta_log_capacity", ctypes.c_int32), ("lds_seg_capacity", ctypes.c_int32),
+                ("page_capacity", ctypes.c_int32), ("page_heap_capacity", ctypes.c_int32),
+                ("unsettled_capacity", ctypes.c_int32), ("uid_capacity", ctypes.c_int32)]
 
 
 class MtGenCfg(ctypes.Structure):

@@ -51,6 +51,21 @@ struct DocHdr {               // 128 bytes per document
 };
 static_assert(sizeof(DocHdr) == 128, "DocHdr size");
 
+// Paged documents (mt_paged.h): a document that outgrows the LDS tier is kept as pages =
+// level-1 nodes of the reference B-tree (<= 7 leaf blocks, <= 64 segment slots each).
+struct PageMeta {             // 24 bytes, indexed by page id
+    uint8_t nseg, nblk, pad0, pad1;
+    uint8_t bcnt[8];          // segments per leaf block
+    int8_t flg[8];            // needsScour per leaf block
+    int32_t obs;              // observer length of the page
+};
+static_assert(sizeof(PageMeta) == 24, "PageMeta size");
+#define MT_PG_SLOTS 64
+// DocHdr.pad[] words used by paged documents
+#define HDR_PAGED 0           // 1: the document lives in the paged layout
+#define HDR_NPAGES 1          // pages in the directory
+#define HDR_UTN 2             // entries of the unsettled-segment table
+
 struct DevState {
     DocHdr *hdr;
     v4i *segA;
@@ -65,6 +80,19 @@ struct DevState {
     int32_t *retry;           // per document: replay (the rest of) this batch in the HBM tier
     int64_t *resume;          // per document: first op the HBM tier replays
     uint32_t *stats;          // [0]: documents replayed in the HBM tier by the last launch
+    // paged layout (PP == 0: disabled)
+    v4i *pgA;                 // [n_docs][PP][64]
+    u64 *pgO;
+    v4u *pgB;
+    PageMeta *pgMeta;         // [n_docs][PP]
+    uint16_t *pgDir;          // [n_docs][PP] page ids in document (level-1) order
+    uint8_t *pgCnt;           // [n_docs][MT_LV][PP] counts of levels >= 1 (level 1 = blocks per page)
+    v2i *pgHeap;              // [n_docs][PH + 1] zamboni heap
+    int32_t *pgUtPage;        // [n_docs][UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
+    v4i *pgUtA;
+    u64 *pgUtO;
+    uint16_t *pgUmap;         // [n_docs][UM] uid -> page
+    int32_t PP, PH, UT, UM;
     int32_t S, B, H, T, P, DL;
     int32_t n_docs;
 };

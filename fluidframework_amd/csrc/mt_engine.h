@@ -89,6 +89,14 @@ template <class T> struct DocT {
     int n, depth, heap_n, cur_seq, min_seq, text_top, text_half, props_top, props_half, next_uid,
         status, dlog_n, text_gcs, props_gcs, cap_cause;
     u64 dhash;
+    // paged documents (mt_paged.h): this DocT is a window onto one page, or the instance
+    // holding the levels >= 1 of the tree (dir != nullptr); all zero for flat documents
+    int paged;              // 1: window onto one page
+    int obs_base;           // observer position of the window's first segment
+    int pend_split;         // the page reached MaxNodesInBlock leaf blocks: split it after the op
+    int pend_second;        // leaf block split while a page split was pending (-1: none)
+    LDS_AS uint16_t *dir;   // upper instance: page ids in level-1 order (moved with level 1)
+    void *pg;               // -> PagedDoc (window instance)
 #ifdef MT_PROF
     LDS_AS u64 *prof;       // [32] section timers
 #endif
@@ -233,7 +241,18 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.text_gcs = 0;
     d.props_gcs = 0;
     d.cap_cause = 0;
+    d.paged = 0;
+    d.obs_base = 0;
+    d.pend_split = 0;
+    d.pend_second = -1;
+    d.dir = nullptr;
+    d.pg = nullptr;
     if (d.status) return true;   // failed earlier: the caller leaves it untouched
+    if (h.pad[HDR_PAGED]) {      // lives in the paged layout: the paged kernel replays it
+        d.status = MT_DOC_RETRY;
+        d.cap_cause = 6;
+        return false;
+    }
     int maxnb = 0;
 #pragma unroll
     for (int l = 0; l < MT_LV; l++) maxnb = max(maxnb, h.n_blk[l]);
@@ -423,6 +442,29 @@ TD int blk_prefix(DocT<T> &d, int l, int b) {
 TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
     LDS_AS uint8_t *c = lvl(d, l);
     const int nb = nbr(d, l);
+    if (d.dir && l == 1 && delta) {   // paged upper instance: page ids move with level 1
+        LDS_AS uint16_t *dr = d.dir;
+        if (delta > 0) {
+            for (int hi = nb; hi > from; hi -= MT_WAVE) {
+                const int lo = max(from, hi - MT_WAVE);
+                const int i = lo + lane();
+                uint16_t v = 0;
+                if (i < hi) v = dr[i];
+                wsync<T>();
+                if (i < hi) dr[i + delta] = v;
+                wsync<T>();
+            }
+        } else {
+            for (int lo = from; lo < nb; lo += MT_WAVE) {
+                const int i = lo + lane();
+                uint16_t v = 0;
+                if (i < nb) v = dr[i];
+                wsync<T>();
+                if (i < nb) dr[i + delta] = v;
+                wsync<T>();
+            }
+        }
+    }
     if (delta > 0) {
         for (int hi = nb; hi > from; hi -= MT_WAVE) {
             const int lo = max(from, hi - MT_WAVE);
@@ -466,7 +508,15 @@ TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
 // :2479-2503, split :2509-2522, updateRoot :1909-1920).  New blocks have needsScour
 // undefined; the original keeps its flag.
 TD void blk_split_up(DocT<T> &d, int l, int b) {
+    // paged window: level 1 is the page itself; its split (a new level-1 node) is done by
+    // the paged driver after the op.  A second leaf split while it is pending is recorded:
+    // it decides which half ends up with 5 blocks (reference order: split page, then leaf).
+    if (d.paged && l == 0 && d.pend_split) d.pend_second = b;
     while (true) {
+        if (d.paged && l == 1) {
+            d.pend_split = 1;
+            return;
+        }
         if (nbr(d, l) + 1 > d.B_cap) {
             fail_cap(d, 2);
             return;
@@ -695,8 +745,11 @@ TD void text_gc(DocT<T> &d) {
     d.text_top = carry;
     wsync<T>();
 }
+TD bool paged_text_ensure(DocT<T> &d, int need);
+TD bool paged_props_ensure(DocT<T> &d, int need);
 TD bool text_ensure(DocT<T> &d, int need) {
     if (d.text_top + need <= d.T_cap) return true;
+    if (d.paged) return paged_text_ensure(d, need);
     text_gc(d);
     if (d.status) return false;
     if (d.text_top + need <= d.T_cap) return true;
@@ -734,6 +787,7 @@ TD void props_gc(DocT<T> &d) {
 }
 TD bool props_ensure(DocT<T> &d, int need) {
     if (d.props_top + need <= d.P_cap) return true;
+    if (d.paged) return paged_props_ensure(d, need);
     props_gc(d);
     if (d.status) return false;
     if (d.props_top + need <= d.P_cap) return true;
@@ -1417,6 +1471,10 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     const int r = op.ref_seq, c = op.client, seq = op.seq, p = op.pos1;
     const bool marker = (op.flags & MT_F_MARKER) != 0;
     const int slen = marker ? 1 : op.pos2;
+    // arena room first (a compaction changes no structure, so doing it before the boundary
+    // split is equivalent; a paged window must not be flushed with a page split pending)
+    if (slen > 0 && !marker && !text_ensure(d, slen)) return;
+    if (slen > 0 && op.props != MT_NO_PROPS && !props_ensure(d, 1)) return;
     // pass: split point, first index with prefix >= p, first tie-able index at prefix == p
     int carry = 0, split_i = -1, split_q = 0, ip = -1, js = -1;
     for (int base = 0; base < d.n; base += MT_WAVE) {
@@ -1470,10 +1528,8 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         fail_cap(d, 1);
         return;
     }
-    if (!marker && !text_ensure(d, slen)) return;
     uint32_t ph = 0;
     if (op.props != MT_NO_PROPS) {
-        if (!props_ensure(d, 1)) return;
         ph = (uint32_t)d.props_top;
         d.props_top++;
         const GLB_AS uint32_t *rec = pin + op.props;
@@ -1540,7 +1596,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     if (seq > d.min_seq) add_to_lru_block(d, lb, uid, seq);  // saveIfLocal :2197-2212
     if (d.status) return;
     // delta callback: position of the new segment in the observer view
-    const int pos = obs_prefix(d, x);
+    const int pos = d.obs_base + obs_prefix(d, x);
     cb.n = 1;
     cb_log(d, pos);
     cb_log(d, slen);
@@ -1627,41 +1683,21 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
     return true;
 }
 
-// markRangeRemoved :2640-2752 / annotateRange :2598-2638.  After the two boundary splits
-// the visited leaves are exactly those with view length > 0 inside [p1, p2) (nodeMap
-// :2936-2998 is tree-shape independent), processed in document order.
-#ifdef MT_PROF
-TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin);
-TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
-    PROF_WRAP_BEGIN
-    op_range_impl(d, op, pin);
-    PROF_WRAP_END(7)
-    
-}
-TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
-#else
-TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
-#endif
+// The marking pass of markRangeRemoved :2640-2752 / annotateRange :2598-2638 over the
+// segments of d (after the boundary splits).  carry / ocarry: view / observer position of
+// d's first segment (advanced past it); the callback record cb accumulates across calls.
+// Returns true when the range ended inside d (or on failure: check d.status).
+TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, int &carry, int &ocarry,
+                   Cb &cb) {
     const int r = op.ref_seq, c = op.client, seq = op.seq, p1 = op.pos1, p2 = op.pos2;
     const bool rem = op.kind == MT_OP_REMOVE;
-    const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
-    if (rec && (rec[0] >> 16) == MT_COMBINE_OTHER) {
-        fail(d, MT_DOC_UNSUPPORTED);
-        return;
-    }
-    if (!rec) rec = (const GLB_AS uint32_t *)&kEmptyPropsRec;
-    boundary(d, p1, r, c);
-    if (d.status) return;
-    boundary(d, p2, r, c);
-    if (d.status) return;
     compute_ends(d);
     if (!rem) gsync_rd();   // property records written earlier in this launch are read below
-    Cb cb = cb_begin(d, seq, op.kind);
-    int carry = 0, ocarry = 0, last_b = -1;
+    int last_b = -1;
     const int L = lane();
     const int nblk = nbr(d, 0);
     for (int base = 0; base < d.n; base += MT_WAVE) {
-        if (!rem && !props_ensure(d, MT_WAVE)) return;
+        if (!rem && !props_ensure(d, MT_WAVE)) return true;
         const int i = base + L;
         const bool v = i < d.n;
         v4i a;
@@ -1702,7 +1738,7 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
         }
         if (ballot(bad)) {
             fail(d, MT_DOC_CAPACITY);
-            return;
+            return true;
         }
         if (!rem) d.props_top += __popcll(sel_m);
         wsync<T>();
@@ -1745,12 +1781,47 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
             fm &= fm - 1;
             add_to_lru_block(d, bcast(b, j), (uint32_t)bcast((int)(bv.z & ~MT_MARKER_BIT), j), seq);
         }
-        if (d.status) return;
+        if (d.status) return true;
         if (sel_m) last_b = bcast(b, 63 - __clzll((long long)sel_m));
         carry += bcast(inc, MT_WAVE - 1);
         ocarry += bcast(oinc, MT_WAVE - 1);
-        if (ballot(v && pex >= p2)) break;
+        if (ballot(v && pex >= p2)) return true;
     }
+    return false;
+}
+
+
+// markRangeRemoved :2640-2752 / annotateRange :2598-2638.  After the two boundary splits
+// the visited leaves are exactly those with view length > 0 inside [p1, p2) (nodeMap
+// :2936-2998 is tree-shape independent), processed in document order.
+#ifdef MT_PROF
+TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin);
+TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+    PROF_WRAP_BEGIN
+    op_range_impl(d, op, pin);
+    PROF_WRAP_END(7)
+    
+}
+TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+#else
+TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+#endif
+    const int r = op.ref_seq, c = op.client, seq = op.seq, p1 = op.pos1, p2 = op.pos2;
+    const bool rem = op.kind == MT_OP_REMOVE;
+    const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
+    if (rec && (rec[0] >> 16) == MT_COMBINE_OTHER) {
+        fail(d, MT_DOC_UNSUPPORTED);
+        return;
+    }
+    if (!rec) rec = (const GLB_AS uint32_t *)&kEmptyPropsRec;
+    boundary(d, p1, r, c);
+    if (d.status) return;
+    boundary(d, p2, r, c);
+    if (d.status) return;
+    Cb cb = cb_begin(d, seq, op.kind);
+    int carry = 0, ocarry = 0;
+    range_mark(d, op, rec, carry, ocarry, cb);
+    if (d.status) return;
     cb_end(d, cb);
     // zamboni runs in apply_op (single inlined site)
 }

@@ -1,0 +1,1024 @@
+// mt_paged.h -- paged layout for documents that outgrow the LDS tier (configs C3/C4:
+// 3.5-4.5 k live segments, annotates keep property sets apart).
+//
+// A page is a level-1 node of the reference B-tree (MT/mergeTree.ts:333 MaxNodesInBlock=8):
+// <= 7 leaf blocks of <= 7 segments, stored in HBM as 64 segment slots in document order
+// plus a PageMeta (leaf-block counts, needsScour flags, observer length).  Levels >= 1 of
+// the tree live in LDS for the launch (level 1 = pages in document order, counted in leaf
+// blocks; `dir` maps level-1 positions to page ids).  An op costs O(pages/64 + unsettled/64)
+// to find its page plus one page of work, instead of the flat engine's O(segments):
+//
+//  * page view lengths for a remote view (c, r): settled segments (seq <= minSeq and not
+//    removed after minSeq) look the same in every view (refSeq >= minSeq), so a page's view
+//    length is its observer length plus the (view - observer) difference of its unsettled
+//    segments, kept in a per-document table (<= 56 entries on C3);
+//  * the page is staged in a "window" DocT and the flat engine's own functions (op_insert,
+//    boundary, range_mark, scour_range, pack at level 0) run on it unchanged; a page that
+//    reaches MaxNodesInBlock leaf blocks is split 4|4 after the op (blk_split_up records it),
+//    a page that underflows is repacked with its siblings (pack at level 1) in HBM;
+//  * the zamboni heap is the flat one (LDS); a uid -> page map in HBM locates its segments.
+#pragma once
+#include "mt_engine.h"
+
+template <class T> struct PagedDoc {
+    DocT<T> w;    // window: one page staged in LDS
+    DocT<T> up;   // levels >= 1 of the tree (level 1 = pages, counted in leaf blocks)
+    LDS_AS PageMeta *meta;    // [PP] by page id
+    LDS_AS int *pvl;          // [PP] by page id: view length of the current view
+    LDS_AS uint16_t *freel;   // [PP] free page ids
+    LDS_AS int *upage;        // [UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
+    LDS_AS v4i *uA;
+    LDS_AS u64 *uO;
+    GLB_AS v4i *gA;           // this document's pages (slot 0 of page 0)
+    GLB_AS u64 *gO;
+    GLB_AS v4u *gB;
+    GLB_AS PageMeta *gmeta;
+    GLB_AS uint16_t *gdir;
+    GLB_AS uint8_t *gcnt;
+    GLB_AS v2i *gheap;
+    GLB_AS int *gupage;
+    GLB_AS v4i *guA;
+    GLB_AS u64 *guO;
+    GLB_AS uint16_t *gumap;
+    int PP, PH, UT, UM;
+    int nfree, ut_n;
+    int cur;                  // page id staged in the window (-1: none)
+};
+
+#define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
+
+struct PagedLayout {
+    uint32_t offWA, offWB, offWO, offWcnt, offWflg, offWends, offWscr, offWnb;
+    uint32_t offUcnt, offUnb, offDir, offMeta, offPvl, offFree, offHeap, offUpage, offUA, offUO, offGen, total;
+};
+static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words) {
+    PagedLayout L;
+    uint32_t o = 0;
+    L.offWA = o; o += 16u * MT_PG_SLOTS;
+    L.offWB = o; o += 16u * MT_PG_SLOTS;
+    L.offWO = o; o += 8u * MT_PG_SLOTS;
+    L.offUA = o; o += 16u * UT;
+    L.offUO = o; o += 8u * UT;
+    L.offHeap = o; o += 8u * (PH + 1);
+    L.offMeta = o; o += 24u * PP;
+    L.offUpage = o; o += 4u * UT;
+    L.offPvl = o; o += 4u * PP;
+    L.offWscr = o; o += 64u * 4;
+    L.offWnb = o; o += MT_LV * 4;
+    L.offUnb = o; o += MT_LV * 4;
+    L.offGen = o; o += 4u * gen_words;
+    L.offDir = o; o += 2u * PP;
+    L.offFree = o; o += 2u * PP;
+    L.offWends = o; o += 2u * PW_B;
+    L.offWcnt = o; o += (uint32_t)MT_LV * PW_B;
+    L.offWflg = o; o += PW_B;
+    L.offUcnt = o; o += (uint32_t)MT_LV * PP;
+    L.total = (o + 15u) & ~15u;
+    return L;
+}
+
+TD PagedDoc<T> &pdoc(DocT<T> &w) { return *(PagedDoc<T> *)w.pg; }
+TD bool unsettled(const v4i a, int min_seq) {
+    return a.y > min_seq || (a.z != MT_RSEQ_NONE && a.z > min_seq);
+}
+// dir position of page id pg (-1 if not in the directory)
+TD int pg_pos(PagedDoc<T> &pd, int pg) {
+    const int np = nbr(pd.up, 1);
+    for (int base = 0; base < np; base += MT_WAVE) {
+        const int q = base + lane();
+        const u64 m = ballot(q < np && pd.up.dir[q] == pg);
+        if (m) return base + first_lane(m);
+    }
+    return -1;
+}
+
+// ------------------------------------------------------------------ window load / store
+TD void pg_win_load(PagedDoc<T> &pd, int pg) {
+    DocT<T> &w = pd.w;
+    const int n = uni(pd.meta[pg].nseg), nb = uni(pd.meta[pg].nblk);
+    const int i = lane();
+    GLB_AS v4i *gA = pd.gA + (size_t)pg * MT_PG_SLOTS;
+    GLB_AS u64 *gO = pd.gO + (size_t)pg * MT_PG_SLOTS;
+    GLB_AS v4u *gB = pd.gB + (size_t)pg * MT_PG_SLOTS;
+    if (i < n) {
+        w.A[i] = gA[i];
+        w.O[i] = gO[i];
+        w.Bv[i] = gB[i];
+    }
+    if (i < PW_B) {
+        lvl(w, 0)[i] = i < nb ? pd.meta[pg].bcnt[i & 7] : 0;
+        w.flg[i] = i < nb ? pd.meta[pg].flg[i & 7] : (int8_t)0;
+    }
+    if (i == 0) {
+        w.nb[0] = nb;
+        w.nb[1] = 1;
+        lvl(w, 1)[0] = (uint8_t)nb;
+    }
+    w.n = n;
+    w.depth = pd.up.depth == 1 ? 1 : 2;
+    w.pend_split = 0;
+    w.pend_second = -1;
+    pd.cur = pg;
+    wsync<T>();
+}
+
+// Removes the table entries of page pg (and every settled entry), then appends the
+// unsettled segments of window slots [lo, hi) under page pg2.
+TD void pg_table_purge(PagedDoc<T> &pd, int pg) {
+    const int ms = pd.w.min_seq;
+    int dst = 0;
+    for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
+        const int e = base + lane();
+        const bool v = e < pd.ut_n;
+        int p = -1;
+        v4i a = v4i{0, 0, MT_RSEQ_NONE, 0};
+        u64 o = 0;
+        if (v) {
+            p = pd.upage[e];
+            a = pd.uA[e];
+            o = pd.uO[e];
+        }
+        const bool keep = v && p != pg && unsettled<T>(a, ms);
+        const u64 km = ballot(keep);
+        const int at = dst + __popcll(km & ((1ull << lane()) - 1ull));
+        wsync<T>();
+        if (keep) {
+            pd.upage[at] = p;
+            pd.uA[at] = a;
+            pd.uO[at] = o;
+        }
+        wsync<T>();
+        dst += __popcll(km);
+    }
+    pd.ut_n = dst;
+}
+TD void pg_table_add(PagedDoc<T> &pd, int lo, int hi, int pg2) {
+    DocT<T> &w = pd.w;
+    const int i = lane() + lo;
+    const bool v = i < hi;
+    v4i a;
+    u64 o;
+    load_ao(w, i, v, a, o);
+    const bool add = v && unsettled<T>(a, w.min_seq);
+    const u64 m = ballot(add);
+    if (pd.ut_n + __popcll(m) > pd.UT) {
+        fail(w, MT_DOC_CAPACITY);
+        return;
+    }
+    const int at = pd.ut_n + __popcll(m & ((1ull << lane()) - 1ull));
+    if (add) {
+        pd.upage[at] = pg2;
+        pd.uA[at] = a;
+        pd.uO[at] = o;
+    }
+    pd.ut_n += __popcll(m);
+    wsync<T>();
+}
+
+// Writes window slots [lo, hi) to page pg (slot 0 = lo) with its meta (blocks [b0, b1) of
+// the window) and the uid -> page map.
+TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1) {
+    DocT<T> &w = pd.w;
+    const int i = lane();
+    GLB_AS v4i *gA = pd.gA + (size_t)pg * MT_PG_SLOTS;
+    GLB_AS u64 *gO = pd.gO + (size_t)pg * MT_PG_SLOTS;
+    GLB_AS v4u *gB = pd.gB + (size_t)pg * MT_PG_SLOTS;
+    int ol = 0;
+    if (lo + i < hi) {
+        const v4i a = w.A[lo + i];
+        const v4u b = w.Bv[lo + i];
+        gA[i] = a;
+        gO[i] = w.O[lo + i];
+        gB[i] = b;
+        const uint32_t uid = b.z & ~MT_MARKER_BIT;
+        if (uid < (uint32_t)pd.UM) pd.gumap[uid] = (uint16_t)pg;
+        ol = obs_len(a);
+    }
+    const int obs = wave_sum(ol);
+    if (i < 8) {
+        pd.meta[pg].bcnt[i] = b0 + i < b1 ? lvl(w, 0)[b0 + i] : 0;
+        pd.meta[pg].flg[i] = b0 + i < b1 ? w.flg[b0 + i] : (int8_t)0;
+    }
+    if (i == 0) {
+        pd.meta[pg].nseg = (uint8_t)(hi - lo);
+        pd.meta[pg].nblk = (uint8_t)(b1 - b0);
+        pd.meta[pg].obs = obs;
+    }
+    wsync<T>();
+}
+
+// Page split: the window's page reached MaxNodesInBlock leaf blocks during the op
+// (insertingWalk :2479-2503 / split :2509-2522 at level 1, updateRoot :1909-1920).  The
+// reference splits 4|4 at once; a second leaf split of the same op then lands in one half.
+TD void pg_split_page(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    const int nbk = nbr(w, 0);
+    const int sp = (nbk == MT_MAXN + 1 && w.pend_second >= 0 && w.pend_second < MT_HALF) ? MT_HALF + 1 : MT_HALF;
+    int s0 = 0;
+    for (int q = 0; q < sp; q++) s0 += cntr(w, 0, q);
+    if (pd.nfree == 0) {
+        fail(w, MT_DOC_CAPACITY);
+        return;
+    }
+    pd.nfree--;
+    const int np = uni(pd.freel[pd.nfree]);
+    const int cur = pd.cur;
+    const int pos = pg_pos(pd, cur);
+    // table: entries of cur are rebuilt for both halves
+    pg_table_purge(pd, cur);
+    pg_table_add(pd, 0, s0, cur);
+    pg_table_add(pd, s0, w.n, np);
+    if (w.status) return;
+    pg_write_page(pd, np, s0, w.n, sp, nbk);
+    // level 1: new node after cur (blk_split_up grows the parents / the root)
+    blk_split_up(up, 1, pos);
+    if (up.status) {
+        fail(w, MT_DOC_CAPACITY);
+        return;
+    }
+    if (lane() == 0) {
+        lvl(up, 1)[pos] = (uint8_t)sp;
+        lvl(up, 1)[pos + 1] = (uint8_t)(nbk - sp);
+        up.dir[pos + 1] = (uint16_t)np;
+    }
+    // the window keeps the first sp blocks
+    w.n = s0;
+    if (lane() == 0) {
+        w.nb[0] = sp;
+        lvl(w, 1)[0] = (uint8_t)sp;
+    }
+    w.pend_split = 0;
+    w.pend_second = -1;
+    wsync<T>();
+}
+
+// Stores the window's page (after any pending page split) and refreshes its table entries.
+TD void pg_win_store(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    if (pd.cur < 0) return;
+    if (w.depth == 2 && up.depth == 1) {   // the root leaf block split: the page is the root now
+        up.depth = 2;
+        if (lane() == 0) up.nb[2] = 0;
+    }
+    if (w.pend_split) {
+        pg_split_page(pd);
+        if (w.status) return;
+    } else {
+        pg_table_purge(pd, pd.cur);
+        pg_table_add(pd, 0, w.n, pd.cur);
+        if (w.status) return;
+    }
+    const int nbk = nbr(w, 0);
+    pg_write_page(pd, pd.cur, 0, w.n, 0, nbk);
+    const int pos = pg_pos(pd, pd.cur);
+    if (lane() == 0) lvl(up, 1)[pos] = (uint8_t)nbk;
+    wsync<T>();
+}
+
+// ------------------------------------------------------------------ page view lengths
+// pvl[page] = view length of every page for (c, r); returns the total.
+TD int pg_views(PagedDoc<T> &pd, int r, int c) {
+    const int np = nbr(pd.up, 1);
+    int tot = 0;
+    for (int base = 0; base < np; base += MT_WAVE) {
+        const int q = base + lane();
+        if (q < np) {
+            const int pg = pd.up.dir[q];
+            pd.pvl[pg] = pd.meta[pg].obs;
+        }
+    }
+    wsync<T>();
+    for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
+        const int e = base + lane();
+        if (e < pd.ut_n) {
+            const v4i a = pd.uA[e];
+            const int dlt = view_len(a, pd.uO[e], r, c) - obs_len(a);
+            if (dlt) atomicAdd((int *)(pd.pvl + pd.upage[e]), dlt);
+        }
+    }
+    wsync<T>();
+    for (int base = 0; base < np; base += MT_WAVE) {
+        const int q = base + lane();
+        tot += q < np ? pd.pvl[pd.up.dir[q]] : 0;
+    }
+    return wave_sum(tot);
+}
+// First level-1 position whose cumulative view end is >= p (strict: > p); start = its
+// view start.  -1 (start = total) if none.
+TD int pg_find(PagedDoc<T> &pd, int p, bool strict, int &start) {
+    const int np = nbr(pd.up, 1);
+    int carry = 0;
+    for (int base = 0; base < np; base += MT_WAVE) {
+        const int q = base + lane();
+        const int v = q < np ? pd.pvl[pd.up.dir[q]] : 0;
+        const int inc = wave_scan_incl(v);
+        const int end = carry + inc;
+        const u64 m = ballot(q < np && (strict ? end > p : end >= p));
+        if (m) {
+            const int fl = first_lane(m);
+            start = bcast(end - v, fl);
+            return base + fl;
+        }
+        carry += bcast(inc, MT_WAVE - 1);
+    }
+    start = carry;
+    return -1;
+}
+TD int pg_obs_start(PagedDoc<T> &pd, int pos) {
+    int s = 0;
+    for (int base = 0; base < pos; base += MT_WAVE) {
+        const int q = base + lane();
+        s += q < pos ? pd.meta[pd.up.dir[q]].obs : 0;
+    }
+    return wave_sum(s);
+}
+TD void pg_load_pos(PagedDoc<T> &pd, int pos) {
+    const int pg = uni(pd.up.dir[pos]);
+    if (pd.cur != pg) {
+        pg_win_store(pd);
+        pg_win_load(pd, pg);
+    }
+    pd.w.obs_base = pg_obs_start(pd, pos);
+}
+
+// ------------------------------------------------------------------ pack at level 1
+// pack :1401-1453 for the underflowing page at level-1 position pos: the leaf blocks of
+// every child of its parent are regrouped into max(1, min(7, n/4)) pages (copied in HBM
+// into fresh pages); then the parent may underflow in turn (counts only above level 1).
+TD void pg_pack1(PagedDoc<T> &pd, int pos) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    pg_win_store(pd);
+    pd.cur = -1;
+    int c0;
+    const int P = blk_find(up, 2, pos, true, c0);
+    if (P < 0) {
+        fail(w, MT_DOC_INTERNAL);
+        return;
+    }
+    const int nch = cntr(up, 2, P);
+    int TB = 0, TS = 0;
+    for (int j = 0; j < nch; j++) {
+        TB += cntr(up, 1, c0 + j);
+        TS += uni(pd.meta[up.dir[c0 + j]].nseg);
+    }
+    int k = TB / MT_HALF;
+    if (k > MT_MAXN - 1) k = MT_MAXN - 1;
+    if (k < 1) k = 1;
+    const int base = TB / k, extra = TB % k;
+    if (pd.nfree < k) {
+        fail(w, MT_DOC_CAPACITY);
+        return;
+    }
+    // per lane: one leaf block of the concatenation (TB <= 49): its old page / index
+    const int bl = lane();
+    int opg = -1, ob = 0, bseg0 = 0;   // old page, block index in it, first segment (concat)
+    {
+        int acc_b = 0, acc_s = 0;
+        for (int j = 0; j < nch; j++) {
+            const int pg = uni(up.dir[c0 + j]);
+            const int nb = uni(pd.meta[pg].nblk);
+            if (bl >= acc_b && bl < acc_b + nb) {
+                opg = pg;
+                ob = bl - acc_b;
+                int s = acc_s;
+                for (int q = 0; q < ob; q++) s += pd.meta[pg].bcnt[q];
+                bseg0 = s;
+            }
+            acc_b += nb;
+            acc_s += uni(pd.meta[pg].nseg);
+        }
+    }
+    const int bcnt = opg >= 0 ? pd.meta[opg].bcnt[ob] : 0;
+    const int8_t bflg = opg >= 0 ? pd.meta[opg].flg[ob] : (int8_t)0;
+    // new page m gets blocks [nb0(m), nb0(m) + base + (m < extra))
+    auto nb0 = [&](int m) { return m * base + min(m, extra); };
+    uint16_t newp[MT_MAXN];
+#pragma unroll
+    for (int m = 0; m < MT_MAXN; m++) newp[m] = 0;
+    for (int m = 0; m < k; m++) {
+        pd.nfree--;
+        newp[m] = (uint16_t)uni(pd.freel[pd.nfree]);
+    }
+    // table entries of the old pages go; the copy pass re-adds the unsettled ones
+    for (int j = 0; j < nch; j++) pg_table_purge(pd, uni(up.dir[c0 + j]));
+    // copy, one new page at a time (<= 7 * 8 segments each)
+    for (int m = 0; m < k; m++) {
+        const int npg = newp[m];
+        const int blo = nb0(m), bhi = nb0(m + 1);
+        const int s_lo = bcast(bseg0, blo);
+        const int s_hi = bhi < TB ? bcast(bseg0, bhi) : TS;
+        const int t = lane();
+        const int g = s_lo + t;
+        int ol = 0;
+        bool add = false;
+        v4i a = v4i{0, 0, MT_RSEQ_NONE, 0};
+        u64 o = 0;
+        if (g < s_hi) {
+            // source: old page j and slot
+            int acc = 0, spg = 0, slot = 0;
+            for (int j = 0; j < nch; j++) {
+                const int pg = uni(up.dir[c0 + j]);
+                const int ns = uni(pd.meta[pg].nseg);
+                if (g >= acc && g < acc + ns) {
+                    spg = pg;
+                    slot = g - acc;
+                }
+                acc += ns;
+            }
+            a = pd.gA[(size_t)spg * MT_PG_SLOTS + slot];
+            o = pd.gO[(size_t)spg * MT_PG_SLOTS + slot];
+            const v4u b = pd.gB[(size_t)spg * MT_PG_SLOTS + slot];
+            pd.gA[(size_t)npg * MT_PG_SLOTS + t] = a;
+            pd.gO[(size_t)npg * MT_PG_SLOTS + t] = o;
+            pd.gB[(size_t)npg * MT_PG_SLOTS + t] = b;
+            const uint32_t uid = b.z & ~MT_MARKER_BIT;
+            if (uid < (uint32_t)pd.UM) pd.gumap[uid] = (uint16_t)npg;
+            ol = obs_len(a);
+            add = unsettled<T>(a, w.min_seq);
+        }
+        const u64 am = ballot(add);
+        if (pd.ut_n + __popcll(am) > pd.UT) {
+            fail(w, MT_DOC_CAPACITY);
+            return;
+        }
+        if (add) {
+            const int at = pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull));
+            pd.upage[at] = npg;
+            pd.uA[at] = a;
+            pd.uO[at] = o;
+        }
+        pd.ut_n += __popcll(am);
+        const int obs = wave_sum(ol);
+        // meta of the new page: blocks blo..bhi of the concatenation
+        const int q = lane() - blo;
+        if (lane() >= blo && lane() < bhi) {
+            pd.meta[npg].bcnt[q] = (uint8_t)bcnt;
+            pd.meta[npg].flg[q] = bflg;
+        } else if (lane() >= 64 - 8) {
+            const int qq = lane() - (64 - 8);
+            if (qq >= bhi - blo) {
+                pd.meta[npg].bcnt[qq] = 0;
+                pd.meta[npg].flg[qq] = 0;
+            }
+        }
+        if (lane() == 0) {
+            pd.meta[npg].nseg = (uint8_t)(s_hi - s_lo);
+            pd.meta[npg].nblk = (uint8_t)(bhi - blo);
+            pd.meta[npg].obs = obs;
+        }
+        wsync<T>();
+    }
+    // free the old pages (their meta marks them empty)
+    for (int j = 0; j < nch; j++) {
+        const int pg = uni(up.dir[c0 + j]);
+        if (lane() == 0) {
+            pd.meta[pg].nseg = 0;
+            pd.meta[pg].nblk = 0;
+            pd.freel[pd.nfree] = (uint16_t)pg;
+        }
+        pd.nfree++;
+        wsync<T>();
+    }
+    // level 1: nch entries -> k entries of base (+1) blocks; then the page ids
+    blk_replace(up, 1, c0, nch, k, base, extra);
+    if (up.status) {
+        fail(w, MT_DOC_CAPACITY);
+        return;
+    }
+    for (int m = 0; m < k; m++)
+        if (lane() == 0) up.dir[c0 + m] = newp[m];
+    if (lane() == 0) lvl(up, 2)[P] = (uint8_t)k;
+    wsync<T>();
+    if (k < MT_HALF && 3 < up.depth) pack(up, 2, P);   // counts only above level 1
+    if (up.status) fail(w, MT_DOC_INTERNAL);
+}
+
+// ------------------------------------------------------------------ zamboni (paged)
+// zamboniSegments :1455-1511 with the heap in LDS and the uid -> page map in HBM.
+TD void pg_zamboni(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    for (int it = 0; it < MT_ZAMBONI && w.status == 0; it++) {
+        if (w.heap_n == 0) break;
+        const v2i top = heap_top(w);
+        if (top.x > w.min_seq) break;
+        heap_pop(w);
+        wsync<T>();
+        const uint32_t uid = (uint32_t)top.y;
+        if (uid >= (uint32_t)pd.UM) continue;
+        const int pg = uni(pd.gumap[uid]);
+        if (pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) continue;
+        if (pd.cur != pg) {
+            pg_win_store(pd);
+            if (w.status) return;
+            pg_win_load(pd, pg);
+        }
+        const int i = find_uid(w, uid);
+        if (i < 0) continue;
+        int bstart;
+        const int b = blk_find(w, 0, i, true, bstart);
+        if (b < 0) {
+            fail(w, MT_DOC_INTERNAL);
+            return;
+        }
+        const int f = flgr(w, b);
+        const int old = cntr(w, 0, b);
+        if (f == 0) continue;
+        const int kept = scour_range(w, bstart, b, 1);
+        if (w.status) return;
+        wsync<T>();
+        if (lane() == 0) w.flg[b] = 0;
+        wsync<T>();
+        if (kept < old && kept < MT_HALF && w.depth > 1) {
+            pack(w, 0, b);   // regroups this page's leaf blocks (stops at the window top)
+            if (w.status) return;
+            if (nbr(w, 0) < MT_HALF && pd.up.depth > 2) {
+                const int pos = pg_pos(pd, pd.cur);
+                pg_pack1(pd, pos);
+                if (w.status) return;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ ops (paged)
+TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    DocT<T> &w = pd.w;
+    const mt_op_rec &op = in.op;
+    const int slen = (op.flags & MT_F_MARKER) ? 1 : op.pos2;
+    pg_views(pd, op.ref_seq, op.client);
+    int start;
+    const int pos = pg_find(pd, op.pos1, false, start);
+    if (pos < 0) {
+        if (slen == 0) {   // boundary only; nothing splits past the end
+            Cb cb = cb_begin(w, op.seq, MT_OP_INSERT);
+            cb.n = 1;
+            cb_log(w, -1);
+            cb_log(w, 0);
+            cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)-1), 0u));
+            cb_end(w, cb);
+            return;
+        }
+        fail(w, MT_DOC_INSERT_FAILED);
+        return;
+    }
+    pg_load_pos(pd, pos);
+    OpIn rel = in;
+    rel.op.pos1 = op.pos1 - start;
+    op_insert(w, rel, tin, pin);
+    if (w.status) return;
+    pg_win_store(pd);
+}
+
+TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
+    pg_views(pd, r, c);
+    int start;
+    const int pos = pg_find(pd, p, true, start);
+    if (pos < 0 || start >= p) return;   // p is at a page boundary or past the end
+    pg_load_pos(pd, pos);
+    boundary(pd.w, p - start, r, c);
+    if (pd.w.status) return;
+    pg_win_store(pd);
+}
+
+TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
+    DocT<T> &w = pd.w;
+    const int r = op.ref_seq, c = op.client, p1 = op.pos1, p2 = op.pos2;
+    const bool rem = op.kind == MT_OP_REMOVE;
+    const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
+    if (rec && (rec[0] >> 16) == MT_COMBINE_OTHER) {
+        fail(w, MT_DOC_UNSUPPORTED);
+        return;
+    }
+    if (!rec) rec = (const GLB_AS uint32_t *)&kEmptyPropsRec;
+    pg_boundary(pd, p1, r, c);
+    if (w.status) return;
+    pg_boundary(pd, p2, r, c);
+    if (w.status) return;
+    Cb cb = cb_begin(w, op.seq, op.kind);
+    pg_views(pd, r, c);
+    int start;
+    int pos = pg_find(pd, p1, true, start);
+    if (pos >= 0) {
+        int carry = start, ocarry = pg_obs_start(pd, pos);
+        const int np = nbr(pd.up, 1);
+        while (pos < np && carry < p2) {
+            pg_load_pos(pd, pos);
+            w.obs_base = ocarry;
+            const bool done = range_mark(w, op, rec, carry, ocarry, cb);
+            if (w.status) return;
+            pg_win_store(pd);
+            if (w.status) return;
+            if (done) break;
+            pos = pg_pos(pd, pd.cur) + 1;   // a page split may have inserted after cur
+        }
+    }
+    cb_end(w, cb);
+}
+
+// Client.applyMsg (MT/client.ts:797-819) for a paged document; mirrors apply_op.
+TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    DocT<T> &w = pd.w;
+    const mt_op_rec &op = in.op;
+    const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
+    if (op.kind == MT_OP_INSERT) {
+        pg_op_insert(pd, in, tin, pin);
+    } else if (is_op) {
+        pg_op_range(pd, op, pin);
+    }
+    if (w.status) return;
+    bool z = is_op;
+    for (int pass = 0; pass < 2; pass++) {
+        if (z) {
+            pg_zamboni(pd);
+            if (w.status) return;
+        }
+        if (pass == 1) break;
+        if (op.kind != MT_OP_NOOP) {
+            if (!(w.cur_seq < op.seq)) {
+                fail(w, MT_DOC_SEQ_ORDER);
+                return;
+            }
+            if (!(w.min_seq <= op.min_seq)) {
+                fail(w, MT_DOC_MINSEQ_ORDER);
+                return;
+            }
+        }
+        z = false;
+        if (!(op.flags & MT_F_GROUP_MORE)) {
+            if (!(w.cur_seq <= op.seq)) {
+                fail(w, MT_DOC_SEQ_ORDER);
+                return;
+            }
+            w.cur_seq = op.seq;
+            if (!(op.min_seq <= op.seq) || !(w.min_seq <= op.min_seq)) {
+                fail(w, MT_DOC_MINSEQ_ORDER);
+                return;
+            }
+            if (op.min_seq > w.min_seq) {
+                w.min_seq = op.min_seq;
+                z = true;
+            }
+        }
+        if (!z) break;
+    }
+}
+
+// ------------------------------------------------------------------ text / props gc (paged)
+// Compacts the live text of every page into the other arena half, page by page.
+TD bool paged_text_ensure(DocT<T> &w, int need) {
+    PagedDoc<T> &pd = pdoc(w);
+    const int keep = pd.cur;
+    pg_win_store(pd);
+    if (w.status) return false;
+    gsync_rd();
+    const int dh = 1 - w.text_half;
+    GLB_AS uint16_t *dst = text_base(w, dh);
+    const GLB_AS uint16_t *src = text_base(w, w.text_half);
+    int carry = 0;
+    const int np = nbr(pd.up, 1);
+    for (int q = 0; q < np; q++) {
+        pg_win_load(pd, uni(pd.up.dir[q]));
+        const int i = lane();
+        const bool v = i < w.n;
+        v4i a = v4i{0, 0, 0, 0};
+        v4u b = v4u{0, 0, 0, 0};
+        if (v) {
+            a = w.A[i];
+            b = w.Bv[i];
+        }
+        const bool live = v && a.z == MT_RSEQ_NONE && !(b.z & MT_MARKER_BIT);
+        const int len = live ? a.x : 0;
+        const int inc = wave_scan_incl(len);
+        const int off = carry + inc - len;
+        u64 m = ballot(live && len > 0);
+        while (m) {
+            const int j = first_lane(m);
+            m &= m - 1;
+            copy_text<T>(dst + bcast(off, j), src + bcast((int)b.x, j), bcast(len, j));
+        }
+        wsync<T>();
+        if (live) {
+            v4u nb = b;
+            nb.x = (uint32_t)off;
+            nb.w &= 0xFFFFu;
+            w.Bv[i] = nb;
+        }
+        carry += bcast(inc, MT_WAVE - 1);
+        wsync<T>();
+        pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0));
+    }
+    w.text_half = dh;
+    w.text_top = carry;
+    pd.cur = -1;
+    if (keep >= 0) pg_win_load(pd, keep);
+    if (w.text_top + need <= w.T_cap) return true;
+    fail(w, MT_DOC_CAPACITY);
+    return false;
+}
+
+TD bool paged_props_ensure(DocT<T> &w, int need) {
+    PagedDoc<T> &pd = pdoc(w);
+    const int keep = pd.cur;
+    pg_win_store(pd);
+    if (w.status) return false;
+    gsync_rd();
+    const int dh = 1 - w.props_half;
+    int carry = 1;
+    const int np = nbr(pd.up, 1);
+    for (int q = 0; q < np; q++) {
+        pg_win_load(pd, uni(pd.up.dir[q]));
+        const int i = lane();
+        const uint32_t h = i < w.n ? w.Bv[i].y : 0;
+        const int has = h != 0;
+        const int inc = wave_scan_incl(has);
+        const uint32_t nh = (uint32_t)(carry + inc - has);
+        if (has) {
+            const GLB_AS uint32_t *s = prec(w, w.props_half, h);
+            GLB_AS uint32_t *t = prec(w, dh, nh);
+            const uint32_t n = s[0];
+            t[0] = n;
+            for (uint32_t k = 0; k < 2 * n; k++) t[1 + k] = s[1 + k];
+        }
+        wsync<T>();
+        if (has) w.Bv[i].y = nh;
+        carry += bcast(inc, MT_WAVE - 1);
+        wsync<T>();
+        pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0));
+    }
+    w.props_half = dh;
+    w.props_top = carry;
+    pd.cur = -1;
+    gsync_rd();
+    if (keep >= 0) pg_win_load(pd, keep);
+    if (w.props_top + need <= w.P_cap) return true;
+    fail(w, MT_DOC_CAPACITY);
+    return false;
+}
+
+// ------------------------------------------------------------------ bind / store / convert
+// Per-document HBM bases of the paged arrays.
+TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
+    const size_t PP = st.PP;
+    pd.gA = (GLB_AS v4i *)(st.pgA + (size_t)doc * PP * MT_PG_SLOTS);
+    pd.gO = (GLB_AS u64 *)(st.pgO + (size_t)doc * PP * MT_PG_SLOTS);
+    pd.gB = (GLB_AS v4u *)(st.pgB + (size_t)doc * PP * MT_PG_SLOTS);
+    pd.gmeta = (GLB_AS PageMeta *)(st.pgMeta + (size_t)doc * PP);
+    pd.gdir = (GLB_AS uint16_t *)(st.pgDir + (size_t)doc * PP);
+    pd.gcnt = (GLB_AS uint8_t *)(st.pgCnt + (size_t)doc * MT_LV * PP);
+    pd.gheap = (GLB_AS v2i *)(st.pgHeap + (size_t)doc * (st.PH + 1));
+    pd.gupage = (GLB_AS int *)(st.pgUtPage + (size_t)doc * st.UT);
+    pd.guA = (GLB_AS v4i *)(st.pgUtA + (size_t)doc * st.UT);
+    pd.guO = (GLB_AS u64 *)(st.pgUtO + (size_t)doc * st.UT);
+    pd.gumap = (GLB_AS uint16_t *)(st.pgUmap + (size_t)doc * st.UM);
+    pd.PP = st.PP;
+    pd.PH = st.PH;
+    pd.UT = st.UT;
+    pd.UM = st.UM;
+}
+
+// Window + upper DocT instances over the LDS layout; scalars from the document header.
+TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *smem, const PagedLayout &L) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    pg_bases(pd, st, doc);
+    w.hp = st.hdr + doc;
+    w.text = (GLB_AS uint16_t *)(st.text + doc * (size_t)2 * st.T);
+    w.props = (GLB_AS uint32_t *)(st.props + doc * (size_t)2 * st.P * MT_PREC);
+    w.dlog = st.DL ? (GLB_AS int32_t *)(st.dlog + doc * (size_t)st.DL) : nullptr;
+    w.T_cap = st.T;
+    w.P_cap = st.P;
+    w.DL_cap = st.DL;
+    w.S_cap = MT_PG_SLOTS;
+    w.B_cap = PW_B;
+    w.H_cap = st.PH;
+    w.A = (typename T::A_t)(smem + L.offWA);
+    w.Bv = (typename T::B_t)(smem + L.offWB);
+    w.O = (typename T::O_t)(smem + L.offWO);
+    w.heap = (typename T::H_t)(smem + L.offHeap);
+    w.cnt = smem + L.offWcnt;
+    w.flg = (LDS_AS int8_t *)(smem + L.offWflg);
+    w.ends = (LDS_AS uint16_t *)(smem + L.offWends);
+    w.scr = (LDS_AS int32_t *)(smem + L.offWscr);
+    w.nb = (LDS_AS int32_t *)(smem + L.offWnb);
+    const DocHdr h = *w.hp;
+    w.n = 0;
+    w.depth = h.depth;
+    w.heap_n = h.heap_n;
+    w.cur_seq = h.cur_seq;
+    w.min_seq = h.min_seq;
+    w.text_top = h.text_top;
+    w.text_half = h.text_half;
+    w.props_top = h.props_top;
+    w.props_half = h.props_half;
+    w.next_uid = h.next_uid;
+    w.status = h.status;
+    w.dlog_n = h.dlog_n;
+    w.dhash = h.delta_hash;
+    w.text_gcs = w.props_gcs = w.cap_cause = 0;
+    w.paged = 1;
+    w.obs_base = 0;
+    w.pend_split = 0;
+    w.pend_second = -1;
+    w.dir = nullptr;
+    w.pg = &pd;
+    up = w;
+    up.paged = 0;
+    up.pg = nullptr;
+    up.cnt = smem + L.offUcnt;
+    up.nb = (LDS_AS int32_t *)(smem + L.offUnb);
+    up.dir = (LDS_AS uint16_t *)(smem + L.offDir);
+    up.B_cap = st.PP;
+    up.status = 0;
+    pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
+    pd.pvl = (LDS_AS int *)(smem + L.offPvl);
+    pd.freel = (LDS_AS uint16_t *)(smem + L.offFree);
+    pd.upage = (LDS_AS int *)(smem + L.offUpage);
+    pd.uA = (LDS_AS v4i *)(smem + L.offUA);
+    pd.uO = (LDS_AS u64 *)(smem + L.offUO);
+    pd.cur = -1;
+}
+
+// Builds the free-page list from the directory (pvl as scratch marks).
+TD void pg_build_free(PagedDoc<T> &pd) {
+    const int np = nbr(pd.up, 1);
+    for (int base = 0; base < pd.PP; base += MT_WAVE)
+        if (base + lane() < pd.PP) pd.pvl[base + lane()] = 0;
+    wsync<T>();
+    for (int base = 0; base < np; base += MT_WAVE)
+        if (base + lane() < np) pd.pvl[pd.up.dir[base + lane()]] = 1;
+    wsync<T>();
+    int nf = 0;
+    for (int base = 0; base < pd.PP; base += MT_WAVE) {
+        const int pg = base + lane();
+        const bool fr = pg < pd.PP && pd.pvl[pg] == 0;
+        const u64 m = ballot(fr);
+        // free pages are popped from the top: keep ascending ids at the top
+        if (fr) pd.freel[nf + __popcll(m & ((1ull << lane()) - 1ull))] = (uint16_t)pg;
+        nf += __popcll(m);
+    }
+    // reverse so that the lowest ids come first
+    for (int i = lane(); i < nf / 2; i += MT_WAVE) {
+        const uint16_t a = pd.freel[i], b = pd.freel[nf - 1 - i];
+        pd.freel[i] = b;
+        pd.freel[nf - 1 - i] = a;
+    }
+    pd.nfree = nf;
+    wsync<T>();
+}
+
+// Loads a paged document's directory, meta, upper counts, heap and table into LDS.
+TD void pg_load(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    const DocHdr h = *w.hp;
+    if (lane() < MT_LV) up.nb[lane()] = w.hp->n_blk[lane()];
+    wsync<T>();
+    const int np = nbr(up, 1);
+    for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = pd.gdir[q];
+    {
+        GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)pd.gmeta;
+        LDS_AS uint32_t *lm = (LDS_AS uint32_t *)pd.meta;
+        for (int i = lane(); i < pd.PP * 6; i += MT_WAVE) lm[i] = gm[i];
+    }
+    for (int l = 1; l < up.depth; l++) {
+        const int nl = nbr(up, l);
+        for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = pd.gcnt[l * pd.PP + b];
+    }
+    for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = pd.gheap[i];
+    pd.ut_n = h.pad[HDR_UTN];
+    for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
+        pd.upage[e] = pd.gupage[e];
+        pd.uA[e] = pd.guA[e];
+        pd.uO[e] = pd.guO[e];
+    }
+    wsync<T>();
+    pg_build_free(pd);
+}
+
+TD void pg_store(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    pg_win_store(pd);
+    wsync<T>();
+    const int np = nbr(up, 1);
+    for (int q = lane(); q < np; q += MT_WAVE) pd.gdir[q] = up.dir[q];
+    {
+        GLB_AS uint32_t *gm = (GLB_AS uint32_t *)pd.gmeta;
+        LDS_AS const uint32_t *lm = (LDS_AS const uint32_t *)pd.meta;
+        for (int i = lane(); i < pd.PP * 6; i += MT_WAVE) gm[i] = lm[i];
+    }
+    for (int l = 1; l < up.depth; l++) {
+        const int nl = nbr(up, l);
+        for (int b = lane(); b < nl; b += MT_WAVE) pd.gcnt[l * pd.PP + b] = lvl(up, l)[b];
+    }
+    for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) pd.gheap[i] = w.heap[i];
+    for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
+        pd.gupage[e] = pd.upage[e];
+        pd.guA[e] = pd.uA[e];
+        pd.guO[e] = pd.uO[e];
+    }
+    int nbl[MT_LV];
+#pragma unroll
+    for (int l = 0; l < MT_LV; l++) nbl[l] = nbr(up, l);
+    int nseg = 0;
+    for (int q = lane(); q < np; q += MT_WAVE) nseg += pd.meta[up.dir[q]].nseg;
+    nseg = wave_sum(nseg);
+    if (lane() == 0) {
+        DocHdr h;
+        memset(&h, 0, sizeof(h));
+        h.n_seg = nseg;
+        h.depth = up.depth;
+        h.heap_n = w.heap_n;
+        h.cur_seq = w.cur_seq;
+        h.min_seq = w.min_seq;
+        h.text_top = w.text_top;
+        h.text_half = w.text_half;
+        h.props_top = w.props_top;
+        h.props_half = w.props_half;
+        h.next_uid = w.next_uid;
+        h.status = w.status;
+        h.dlog_n = w.dlog_n;
+#pragma unroll
+        for (int l = 0; l < MT_LV; l++) h.n_blk[l] = nbl[l];
+        h.delta_hash = w.dhash;
+        h.n_ops = w.hp->n_ops;
+        h.pad[HDR_PAGED] = 1;
+        h.pad[HDR_NPAGES] = np;
+        h.pad[HDR_UTN] = pd.ut_n;
+        *w.hp = h;
+    }
+}
+
+// Converts a flat document (state in the flat HBM arrays: initial contents, or spilled by
+// the LDS tier) into the paged layout: page j = level-1 node j (the whole tree when the
+// root is a leaf block).  Leaves the paged state staged in LDS (pg_store writes it).
+TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    const DocHdr h = *w.hp;
+    const size_t S = st.S, B = st.B;
+    GLB_AS const v4i *fA = (GLB_AS const v4i *)(st.segA + doc * S);
+    GLB_AS const u64 *fO = (GLB_AS const u64 *)(st.segO + doc * S);
+    GLB_AS const v4u *fB = (GLB_AS const v4u *)(st.segB + doc * S);
+    GLB_AS const uint8_t *fc = (GLB_AS const uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
+    GLB_AS const int8_t *ff = (GLB_AS const int8_t *)(st.flg + doc * B);
+    GLB_AS const v2i *fH = (GLB_AS const v2i *)(st.heap + doc * (size_t)(st.H + 1));
+    const int depth = h.depth;
+    const int np = depth == 1 ? 1 : h.n_blk[1];
+    if (np + 8 > pd.PP || h.heap_n > pd.PH) {
+        fail(w, MT_DOC_CAPACITY);
+        return false;
+    }
+    up.depth = depth;
+    if (lane() < MT_LV) up.nb[lane()] = lane() == 0 ? 0 : (lane() == 1 ? np : (lane() < depth ? h.n_blk[lane()] : 0));
+    wsync<T>();
+    for (int l = 2; l < depth; l++) {
+        const int nl = h.n_blk[l];
+        for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = fc[l * B + b];
+    }
+    for (int i = 1 + lane(); i <= h.heap_n; i += MT_WAVE) w.heap[i] = fH[i];
+    for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) {
+        pd.meta[pg].nseg = 0;
+        pd.meta[pg].nblk = 0;
+    }
+    pd.ut_n = 0;
+    wsync<T>();
+    int lb = 0, s = 0;
+    for (int j = 0; j < np; j++) {
+        const int nbk = depth == 1 ? 1 : (int)uni(fc[B + j]);   // level-1 count: leaf blocks
+        int ns = 0;
+        for (int q = 0; q < nbk; q++) ns += depth == 1 ? h.n_seg : (int)uni(fc[lb + q]);
+        if (nbk > MT_MAXN || ns > MT_PG_SLOTS) {
+            fail(w, MT_DOC_INTERNAL);
+            return false;
+        }
+        // stage the page in the window, then write it like any other page
+        const int i = lane();
+        if (i < ns) {
+            w.A[i] = fA[s + i];
+            w.O[i] = fO[s + i];
+            w.Bv[i] = fB[s + i];
+        }
+        if (i < PW_B) {
+            lvl(w, 0)[i] = i < nbk ? (depth == 1 ? (uint8_t)h.n_seg : fc[lb + i]) : 0;
+            w.flg[i] = i < nbk ? ff[lb + i] : (int8_t)0;
+        }
+        if (i == 0) {
+            up.dir[j] = (uint16_t)j;
+            lvl(up, 1)[j] = (uint8_t)nbk;
+        }
+        w.n = ns;
+        wsync<T>();
+        pg_table_add(pd, 0, ns, j);
+        if (w.status) return false;
+        pg_write_page(pd, j, 0, ns, 0, nbk);
+        lb += nbk;
+        s += ns;
+    }
+    pg_build_free(pd);
+    pd.cur = -1;
+    return true;
+}

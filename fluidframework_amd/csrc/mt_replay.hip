@@ -9,7 +9,7 @@
 #include <vector>
 
 #include "../../include/mt_replay.h"
-#include "mt_engine.h"
+#include "mt_paged.h"
 
 // ============================================================================ kernels
 // Initial document contents (Client.insertSegmentLocal before collaboration: seq 0,
@@ -221,8 +221,123 @@ __device__ static __forceinline__ uint32_t gen_props(Rng &r, const mt_gen_cfg &c
     return 1 + 2 * count;
 }
 
-// Generates and applies cfg.ops messages per document (DESIGN.md "Synthetic op streams");
-// the view length each writer draws positions from is read off the live replica.
+// Per-document generator state (DESIGN.md "Synthetic op streams"), shared by the flat and
+// the paged generators.  Every lane draws the same numbers (uniform state).
+struct GenCtx {
+    Rng rng;
+    LDS_AS int32_t *last_ref;
+    LDS_AS int32_t *short_id;
+    int next_short;
+    int64_t tu, pu, tb, pb;
+};
+__device__ static __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
+__device__ static void gen_begin(GenCtx &g, const DevState &st, const mt_gen_cfg &cfg, int gdoc, int doc,
+                                 LDS_AS uint8_t *gen_lds, int64_t tstride, int64_t pstride) {
+    const int W = cfg.writers;
+    g.last_ref = (LDS_AS int32_t *)gen_lds;
+    g.short_id = g.last_ref + (W + 1);
+    rng_init(g.rng, cfg.seed, gdoc);
+    // seed text (drawn exactly like the oracle / reference harness)
+    uint16_t *arena = st.text + (size_t)doc * 2 * st.T;
+    for (int i = 0; i < cfg.seed_len; i++) {
+        (void)rng_next(g.rng);
+        const uint16_t ch = (uint16_t)(97 + rng_uniform(g.rng, 26));
+        if (lane() == 0) arena[i] = ch;
+    }
+    if (lane() == 0) init_doc_hdr(st, doc, cfg.seed_len);
+    for (int j = lane(); j <= W; j += MT_WAVE) {
+        g.last_ref[j] = 0;
+        g.short_id[j] = 0;
+    }
+    gsync();
+    g.next_short = 1;
+    g.tu = g.pu = 0;
+    g.tb = (int64_t)doc * tstride;
+    g.pb = (int64_t)doc * pstride;
+}
+// Writer, reference sequence number and minSeq of message t.
+__device__ static void gen_pick(GenCtx &g, const mt_gen_cfg &cfg, int t, int &r, int &c, int &msn) {
+    const int W = cfg.writers;
+    const int k = 1 + (int)rng_uniform(g.rng, (uint32_t)W);
+    int lo = max(g.last_ref[k], t - 1 - cfg.lag);
+    if (lo < 0) lo = 0;
+    r = lo + (int)rng_uniform(g.rng, (uint32_t)(t - 1 - lo + 1));
+    lds_fence();
+    if (lane() == 0) g.last_ref[k] = r;
+    lds_fence();
+    int m = 0x7fffffff;
+    for (int j = 1 + lane(); j <= W; j += MT_WAVE) m = min(m, g.last_ref[j]);
+    msn = -wave_max(-m);
+    c = g.short_id[k];
+    if (!c) {
+        c = g.next_short++;
+        lds_fence();
+        if (lane() == 0) g.short_id[k] = c;
+        lds_fence();
+    }
+}
+// The op of message t given the writer's view length (drawn like the oracle's generator).
+__device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, int c, int msn, int len,
+                              OpIn &in, mt_op_rec *ops_out, uint16_t *text_out, uint32_t *props_out,
+                              int64_t doc) {
+    const uint32_t u = rng_next(g.rng);
+    mt_op_rec &op = in.op;
+    op.seq = t;
+    op.ref_seq = r;
+    op.min_seq = msn;
+    op.client = (uint16_t)c;
+    op.flags = 0;
+    op.props = MT_NO_PROPS;
+    op.payload = 0;
+    in.pay_ok = true;
+    in.nl = false;
+    u64 plo = 0, phi = 0;
+    if (len == 0 || (uint64_t)u < cfg.p_insert) {
+        op.kind = MT_OP_INSERT;
+        op.pos1 = (int)rng_uniform(g.rng, (uint32_t)(len + 1));
+        const int tl = 1 + (int)rng_uniform(g.rng, (uint32_t)cfg.text_max);
+        op.pos2 = tl;
+        op.payload = (uint32_t)(g.tb + g.tu);
+        uint16_t ch = 0;
+        for (int j = 0; j < tl; j++) {
+            const uint32_t v = rng_next(g.rng);
+            ch = (uint16_t)'\n';
+            if ((uint64_t)v >= cfg.p_newline) ch = (uint16_t)(97 + rng_uniform(g.rng, 26));
+            if (lane() == 0) text_out[g.tb + g.tu + j] = ch;
+            if (j < 4)
+                plo |= (u64)ch << (16 * j);
+            else if (j < 8)
+                phi |= (u64)ch << (16 * (j - 4));
+        }
+        in.nl = ch == '\n';
+        in.pay_ok = tl <= 8;
+        g.tu += tl;
+        if (cfg.p_insert_props > 0 && (uint64_t)rng_next(g.rng) < cfg.p_insert_props) {
+            op.props = (uint32_t)(g.pb + g.pu);
+            g.pu += gen_props(g.rng, cfg, props_out + g.pb + g.pu);
+        }
+    } else {
+        const int p1 = (int)rng_uniform(g.rng, (uint32_t)len);
+        int m = 1;
+        while (m < 64 && (uint64_t)rng_next(g.rng) < cfg.p_len_continue) m++;
+        op.pos1 = p1;
+        op.pos2 = min(p1 + m, len);
+        if ((uint64_t)u < cfg.p_insert_remove) {
+            op.kind = MT_OP_REMOVE;
+        } else {
+            op.kind = MT_OP_ANNOTATE;
+            op.props = (uint32_t)(g.pb + g.pu);
+            g.pu += gen_props(g.rng, cfg, props_out + g.pb + g.pu);
+        }
+    }
+    in.pay_lo = plo;
+    in.pay_hi = phi;
+    if (lane() == 0) ops_out[doc * cfg.ops + (t - 1)] = op;
+    gsync();
+}
+
+// Generates and applies cfg.ops messages per document; the view length each writer draws
+// positions from is read off the live replica.
 template <class T>
 __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cfg, uint32_t doc_base,
                                                       mt_op_rec *ops_out, uint16_t *text_out,
@@ -234,53 +349,19 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     if (!T::kLds && !st.retry[doc]) return;
-    const int W = cfg.writers;
-    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 2 * (W + 1));
-    LDS_AS int32_t *last_ref = (LDS_AS int32_t *)(smem + L.offGen);
-    LDS_AS int32_t *short_id = last_ref + (W + 1);
-    Rng rng;
-    rng_init(rng, cfg.seed, (int)(doc_base + doc));
-    // seed text (drawn exactly like the oracle / reference harness)
-    uint16_t *arena = st.text + (size_t)doc * 2 * st.T;
-    for (int i = 0; i < cfg.seed_len; i++) {
-        (void)rng_next(rng);
-        const uint16_t ch = (uint16_t)(97 + rng_uniform(rng, 26));
-        if (lane() == 0) arena[i] = ch;
-    }
-    if (lane() == 0) init_doc_hdr(st, doc, cfg.seed_len);
-    for (int j = lane(); j <= W; j += MT_WAVE) {
-        last_ref[j] = 0;
-        short_id[j] = 0;
-    }
-    gsync();
+    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 2 * (cfg.writers + 1));
+    GenCtx g;
+    gen_begin(g, st, cfg, (int)(doc_base + doc), doc, smem + L.offGen, tstride, pstride);
     DocT<T> d;
     if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
         if (lane() == 0) st.retry[doc] = 1;
         return;
     }
-    int next_short = 1;
-    int64_t tu = 0, pu = 0;
-    const int64_t tb = (int64_t)doc * tstride, pb = (int64_t)doc * pstride;
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)text_out;
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)props_out;
     for (int t = 1; t <= cfg.ops && d.status == 0; t++) {
-        const int k = 1 + (int)rng_uniform(rng, (uint32_t)W);
-        int lo = max(last_ref[k], t - 1 - cfg.lag);
-        if (lo < 0) lo = 0;
-        const int r = lo + (int)rng_uniform(rng, (uint32_t)(t - 1 - lo + 1));
-        wsync<T>();
-        if (lane() == 0) last_ref[k] = r;
-        wsync<T>();
-        int msn = 0x7fffffff;
-        for (int j = 1 + lane(); j <= W; j += MT_WAVE) msn = min(msn, last_ref[j]);
-        msn = -wave_max(-msn);
-        int c = short_id[k];
-        if (!c) {
-            c = next_short++;
-            wsync<T>();
-            if (lane() == 0) short_id[k] = c;
-            wsync<T>();
-        }
+        int r, c, msn;
+        gen_pick(g, cfg, t, r, c, msn);
         int vsum = 0;
         for (int base = 0; base < d.n; base += MT_WAVE) {
             const int i = base + lane();
@@ -297,61 +378,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
             q[2] = r;
             q[3] = c;
         }
-        const uint32_t u = rng_next(rng);
         OpIn in;
-        mt_op_rec &op = in.op;
-        op.seq = t;
-        op.ref_seq = r;
-        op.min_seq = msn;
-        op.client = (uint16_t)c;
-        op.flags = 0;
-        op.props = MT_NO_PROPS;
-        op.payload = 0;
-        in.pay_ok = true;
-        in.nl = false;
-        u64 plo = 0, phi = 0;
-        if (len == 0 || (uint64_t)u < cfg.p_insert) {
-            op.kind = MT_OP_INSERT;
-            op.pos1 = (int)rng_uniform(rng, (uint32_t)(len + 1));
-            const int tl = 1 + (int)rng_uniform(rng, (uint32_t)cfg.text_max);
-            op.pos2 = tl;
-            op.payload = (uint32_t)(tb + tu);
-            uint16_t ch = 0;
-            for (int j = 0; j < tl; j++) {
-                const uint32_t v = rng_next(rng);
-                ch = (uint16_t)'\n';
-                if ((uint64_t)v >= cfg.p_newline) ch = (uint16_t)(97 + rng_uniform(rng, 26));
-                if (lane() == 0) text_out[tb + tu + j] = ch;
-                if (j < 4)
-                    plo |= (u64)ch << (16 * j);
-                else if (j < 8)
-                    phi |= (u64)ch << (16 * (j - 4));
-            }
-            in.nl = ch == '\n';
-            in.pay_ok = tl <= 8;
-            tu += tl;
-            if (cfg.p_insert_props > 0 && (uint64_t)rng_next(rng) < cfg.p_insert_props) {
-                op.props = (uint32_t)(pb + pu);
-                pu += gen_props(rng, cfg, props_out + pb + pu);
-            }
-        } else {
-            const int p1 = (int)rng_uniform(rng, (uint32_t)len);
-            int m = 1;
-            while (m < 64 && (uint64_t)rng_next(rng) < cfg.p_len_continue) m++;
-            op.pos1 = p1;
-            op.pos2 = min(p1 + m, len);
-            if ((uint64_t)u < cfg.p_insert_remove) {
-                op.kind = MT_OP_REMOVE;
-            } else {
-                op.kind = MT_OP_ANNOTATE;
-                op.props = (uint32_t)(pb + pu);
-                pu += gen_props(rng, cfg, props_out + pb + pu);
-            }
-        }
-        in.pay_lo = plo;
-        in.pay_hi = phi;
-        if (lane() == 0) ops_out[(int64_t)doc * cfg.ops + (t - 1)] = op;
-        gsync();
+        gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
         apply_op(d, in, gt, gp);
     }
     if (T::kLds && d.status == MT_DOC_RETRY) {
@@ -363,6 +391,148 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
         if (!T::kLds) st.retry[doc] = 0;
     }
     store_doc(d, st, doc);
+}
+
+// ---------------------------------------------------------------- paged kernels
+// Replay of the documents flagged by the LDS tier (retry[doc]) in the paged layout: a
+// document seen for the first time is converted from its flat state (initial contents, or
+// what the LDS tier spilled) and stays paged until the next reset.
+template <class T>
+__global__ void __launch_bounds__(MT_WAVE) k_replay_paged(DevState st, const mt_op_rec *ops,
+                                                          const int64_t *off, const uint16_t *tin,
+                                                          const uint32_t *pin, int use_resume) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
+    const int doc = blockIdx.x;
+    if (doc >= st.n_docs) return;
+    if (!st.retry[doc]) return;
+    if (lane() == 0) atomicAdd(st.stats, 1u);
+    const PagedLayout L = paged_layout(st.PP, st.PH, st.UT, 0);
+    const int64_t k1 = off[doc + 1];
+    const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
+    PagedDoc<T> pd;
+    pg_setup(pd, st, doc, smem, L);
+    DocT<T> &w = pd.w;
+    if (w.status) {
+        if (lane() == 0) st.retry[doc] = 0;
+        return;
+    }
+    if (st.hdr[doc].pad[HDR_PAGED]) {
+        pg_load(pd);
+    } else if (!pg_convert(pd, st, doc)) {
+        // stays flat: only the status changes
+        if (lane() == 0) {
+            st.hdr[doc].status = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
+            st.retry[doc] = 0;
+        }
+        return;
+    }
+    const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
+    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
+    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
+    for (int64_t kb = k0; kb < k1 && w.status == 0; kb += MT_WAVE) {
+        const int64_t k = kb + lane();
+        v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        int nl = 0, pok = 0;
+        if (k < k1) {
+            r0 = o4[2 * k];
+            r1 = o4[2 * k + 1];
+            const int kind = (r1.w >> 16) & 0xFF, flags = ((uint32_t)r1.w >> 24) & 0xFF;
+            const int len = r1.x;
+            if (kind == MT_OP_INSERT && !(flags & MT_F_MARKER) && len > 0) {
+                const GLB_AS uint16_t *src = gt + (uint32_t)r1.y;
+                nl = src[len - 1] == '\n';
+                if (len <= 8) {
+                    pok = 1;
+                    uint32_t u[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) u[j] = j < len ? src[j] : 0u;
+                    w0 = u[0] | (u[1] << 16);
+                    w1 = u[2] | (u[3] << 16);
+                    w2 = u[4] | (u[5] << 16);
+                    w3 = u[6] | (u[7] << 16);
+                }
+            }
+        }
+        const int cnt = (int)min((int64_t)MT_WAVE, k1 - kb);
+        for (int j = 0; j < cnt && w.status == 0; j++) {
+            OpIn in;
+            in.op.seq = __builtin_amdgcn_readlane(r0.x, j);
+            in.op.ref_seq = __builtin_amdgcn_readlane(r0.y, j);
+            in.op.min_seq = __builtin_amdgcn_readlane(r0.z, j);
+            in.op.pos1 = __builtin_amdgcn_readlane(r0.w, j);
+            in.op.pos2 = __builtin_amdgcn_readlane(r1.x, j);
+            in.op.payload = (uint32_t)__builtin_amdgcn_readlane(r1.y, j);
+            in.op.props = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
+            const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane(r1.w, j);
+            in.op.client = (uint16_t)(cw & 0xFFFF);
+            in.op.kind = (uint8_t)((cw >> 16) & 0xFF);
+            in.op.flags = (uint8_t)(cw >> 24);
+            in.pay_lo = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w0, j) |
+                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w1, j) << 32);
+            in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
+                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
+            in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
+            in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
+            pg_apply_op(pd, in, gt, gp);
+        }
+    }
+    // a window capacity is a paged-layout capacity: there is no further tier
+    if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
+    pg_store(pd);
+    if (lane() == 0) st.retry[doc] = 0;
+}
+
+// Generator for documents that outgrew the LDS tier: regenerated from the start in the
+// paged layout (the draws are identical, so the op stream is the same).
+template <class T>
+__global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_cfg cfg, uint32_t doc_base,
+                                                            mt_op_rec *ops_out, uint16_t *text_out,
+                                                            uint32_t *props_out, int64_t tstride,
+                                                            int64_t pstride, int32_t *fail_out,
+                                                            int32_t *dbg_len) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
+    const int doc = blockIdx.x;
+    if (doc >= st.n_docs) return;
+    if (!st.retry[doc]) return;
+    const PagedLayout L = paged_layout(st.PP, st.PH, st.UT, 2 * (cfg.writers + 1));
+    GenCtx g;
+    gen_begin(g, st, cfg, (int)(doc_base + doc), doc, smem + L.offGen, tstride, pstride);
+    PagedDoc<T> pd;
+    pg_setup(pd, st, doc, smem, L);
+    DocT<T> &w = pd.w;
+    if (w.status || !pg_convert(pd, st, doc)) {
+        if (lane() == 0) {
+            fail_out[doc] = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
+            st.retry[doc] = 0;
+        }
+        return;
+    }
+    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)text_out;
+    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)props_out;
+    for (int t = 1; t <= cfg.ops && w.status == 0; t++) {
+        int r, c, msn;
+        gen_pick(g, cfg, t, r, c, msn);
+        const int len = pg_views(pd, r, c);
+        if (dbg_len && lane() == 0) {
+            int32_t *q = dbg_len + ((int64_t)doc * cfg.ops + (t - 1)) * 4;
+            q[0] = len;
+            q[1] = -1;
+            q[2] = r;
+            q[3] = c;
+        }
+        OpIn in;
+        gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
+        pg_apply_op(pd, in, gt, gp);
+    }
+    if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
+    if (lane() == 0) {
+        if (w.status) fail_out[doc] = w.status;
+        st.retry[doc] = 0;
+    }
+    pg_store(pd);
 }
 
 // ---------------------------------------------------------------- checksums
@@ -389,65 +559,121 @@ __device__ static u64 fold_run(const uint32_t *pr, u64 h, uint32_t ph, int len) 
     return h;
 }
 // mt_checksum per document (definitions: DESIGN.md "Checksums", oracle/mt_oracle.c).
+// Segment ranges of a document in document order: the flat table, or its pages.
+struct SegRanges {
+    const v4i *A;
+    const v4u *B;
+    int n;
+    bool paged;
+    const uint16_t *dir;
+    const PageMeta *meta;
+    int nr;
+    __device__ int count() const { return nr; }
+    __device__ void get(int r, const v4i *&a, const v4u *&b, int &cnt) const {
+        if (!paged) {
+            a = A;
+            b = B;
+            cnt = n;
+            return;
+        }
+        const int pg = dir[r];
+        a = A + (size_t)pg * MT_PG_SLOTS;
+        b = B + (size_t)pg * MT_PG_SLOTS;
+        cnt = meta[pg].nseg;
+    }
+};
+__device__ static SegRanges seg_ranges(const DevState &st, int doc, const DocHdr &h) {
+    SegRanges R;
+    R.paged = h.pad[HDR_PAGED] != 0;
+    if (R.paged) {
+        const size_t PP = st.PP;
+        R.A = st.pgA + (size_t)doc * PP * MT_PG_SLOTS;
+        R.B = st.pgB + (size_t)doc * PP * MT_PG_SLOTS;
+        R.dir = st.pgDir + (size_t)doc * PP;
+        R.meta = st.pgMeta + (size_t)doc * PP;
+        R.nr = h.pad[HDR_NPAGES];
+        R.n = 0;
+    } else {
+        R.A = st.segA + doc * (size_t)st.S;
+        R.B = st.segB + doc * (size_t)st.S;
+        R.n = h.n_seg;
+        R.nr = 1;
+        R.dir = nullptr;
+        R.meta = nullptr;
+    }
+    return R;
+}
+
+// mt_checksum per document (definitions: DESIGN.md "Checksums", oracle/mt_oracle.c).
 __global__ void __launch_bounds__(MT_WAVE) k_checksum(DevState st, mt_checksum *out) {
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     const DocHdr h = st.hdr[doc];
-    const size_t S = st.S;
-    const v4i *A = st.segA + doc * S;
-    const v4u *Bv = st.segB + doc * S;
+    const SegRanges R = seg_ranges(st, doc, h);
     const uint16_t *tb = st.text + ((size_t)doc * 2 + h.text_half) * st.T;
     const uint32_t *pr = st.props + ((size_t)doc * 2 + h.props_half) * st.P * MT_PREC;
-    const int n = h.n_seg;
-    int len = 0, ntext = 0;
-    for (int base = 0; base < n; base += MT_WAVE) {
-        const int i = base + lane();
-        int l = 0, t = 0;
-        if (i < n) {
-            const v4i a = A[i];
-            l = obs_len(a);
-            t = (Bv[i].z & MT_MARKER_BIT) ? 0 : l;
+    int len = 0, ntext = 0, nseg = 0;
+    for (int r = 0; r < R.count(); r++) {
+        const v4i *A;
+        const v4u *Bv;
+        int n;
+        R.get(r, A, Bv, n);
+        nseg += n;
+        for (int base = 0; base < n; base += MT_WAVE) {
+            const int i = base + lane();
+            int l = 0, t = 0;
+            if (i < n) {
+                const v4i a = A[i];
+                l = obs_len(a);
+                t = (Bv[i].z & MT_MARKER_BIT) ? 0 : l;
+            }
+            len += wave_sum(l);
+            ntext += wave_sum(t);
         }
-        len += wave_sum(l);
-        ntext += wave_sum(t);
     }
     if (lane() == 0) {
         u64 th = fnv_u32(MT_FNV_OFF, (uint32_t)ntext), hk = MT_FNV_OFF, ph = MT_FNV_OFF;
         int g = 0, run_len = 0;
         bool have = false;
         uint32_t run_p = 0;
-        for (int i = 0; i < n; i++) {
-            const v4i a = A[i];
-            const v4u b = Bv[i];
-            if (a.z != MT_RSEQ_NONE) continue;
-            if (!(b.z & MT_MARKER_BIT)) {
-                for (int j = 0; j < a.x; j++) {
-                    const uint16_t ch = tb[b.x + j];
-                    hk ^= ch & 0xFF;
-                    hk *= MT_FNV_PRIME;
-                    hk ^= ch >> 8;
-                    hk *= MT_FNV_PRIME;
-                    g++;
-                    if ((g & 63) == 0) {
-                        th = fnv_u64(th, hk);
-                        hk = MT_FNV_OFF;
+        for (int r = 0; r < R.count(); r++) {
+            const v4i *A;
+            const v4u *Bv;
+            int n;
+            R.get(r, A, Bv, n);
+            for (int i = 0; i < n; i++) {
+                const v4i a = A[i];
+                const v4u b = Bv[i];
+                if (a.z != MT_RSEQ_NONE) continue;
+                if (!(b.z & MT_MARKER_BIT)) {
+                    for (int j = 0; j < a.x; j++) {
+                        const uint16_t ch = tb[b.x + j];
+                        hk ^= ch & 0xFF;
+                        hk *= MT_FNV_PRIME;
+                        hk ^= ch >> 8;
+                        hk *= MT_FNV_PRIME;
+                        g++;
+                        if ((g & 63) == 0) {
+                            th = fnv_u64(th, hk);
+                            hk = MT_FNV_OFF;
+                        }
                     }
                 }
-            }
-            if (have && same_ordered(pr, run_p, b.y)) {
-                run_len += a.x;
-            } else {
-                if (have) ph = fold_run(pr, ph, run_p, run_len);
-                run_p = b.y;
-                run_len = a.x;
-                have = true;
+                if (have && same_ordered(pr, run_p, b.y)) {
+                    run_len += a.x;
+                } else {
+                    if (have) ph = fold_run(pr, ph, run_p, run_len);
+                    run_p = b.y;
+                    run_len = a.x;
+                    have = true;
+                }
             }
         }
         if (g & 63) th = fnv_u64(th, hk);
         if (have) ph = fold_run(pr, ph, run_p, run_len);
         mt_checksum cs;
         cs.length = (uint32_t)len;
-        cs.n_segments = (uint32_t)n;
+        cs.n_segments = (uint32_t)nseg;
         cs.text_hash = th;
         cs.props_hash = ph;
         cs.delta_hash = h.delta_hash;
@@ -525,6 +751,16 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         h->lds.H = std::min(st.H, S_l + 64);
         if (tier_lds_bytes(true, h->lds, 0) > 60 * 1024) h->lds = TierCaps{0, 0, 0, 0};
     }
+    if (o.page_capacity > 0) {
+        st.PP = std::min(o.page_capacity, 65535);
+        st.PH = o.page_heap_capacity > 0 ? o.page_heap_capacity : 1024;
+        st.UT = o.unsettled_capacity > 0 ? o.unsettled_capacity : 256;
+        st.UM = std::min(o.uid_capacity > 0 ? o.uid_capacity : 65536, 1 << 24);
+        if (paged_layout(st.PP, st.PH, st.UT, 2 * 65).total > 64 * 1024) {
+            delete h;
+            return nullptr;
+        }
+    }
     const size_t N = n_docs;
     bool ok = true;
     auto alloc = [&](void **p, size_t bytes) {
@@ -545,6 +781,20 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.retry, N * sizeof(int32_t));
     alloc((void **)&st.resume, N * sizeof(int64_t));
     alloc((void **)&st.stats, 16 * sizeof(uint32_t));
+    if (st.PP > 0) {
+        const size_t slots = N * (size_t)st.PP * MT_PG_SLOTS;
+        alloc((void **)&st.pgA, slots * sizeof(int4));
+        alloc((void **)&st.pgO, slots * sizeof(u64));
+        alloc((void **)&st.pgB, slots * sizeof(uint4));
+        alloc((void **)&st.pgMeta, N * st.PP * sizeof(PageMeta));
+        alloc((void **)&st.pgDir, N * st.PP * sizeof(uint16_t));
+        alloc((void **)&st.pgCnt, N * MT_LV * (size_t)st.PP);
+        alloc((void **)&st.pgHeap, N * (size_t)(st.PH + 1) * sizeof(int2));
+        alloc((void **)&st.pgUtPage, N * (size_t)st.UT * sizeof(int32_t));
+        alloc((void **)&st.pgUtA, N * (size_t)st.UT * sizeof(int4));
+        alloc((void **)&st.pgUtO, N * (size_t)st.UT * sizeof(u64));
+        alloc((void **)&st.pgUmap, N * (size_t)st.UM * sizeof(uint16_t));
+    }
     if (!ok || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         mt_destroy(h);
@@ -562,7 +812,8 @@ void mt_destroy(mt_handle *h) {
     hipSetDevice(h->device);
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
-                  h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume};
+                  h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
+                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -651,7 +902,17 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     } else {
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream));
     }
-    if (h->st.DL)
+    if (h->st.PP > 0) {
+        // documents that outgrew the LDS tier continue in the paged layout
+        const size_t lb = paged_layout(h->st.PP, h->st.PH, h->st.UT, 0).total;
+        const int use_resume = h->lds.S > 0 ? 1 : 0;
+        if (h->st.DL)
+            hipLaunchKernelGGL(k_replay_paged<TierLdsT<true>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                               b->ops, b->off, b->text, b->props, use_resume);
+        else
+            hipLaunchKernelGGL(k_replay_paged<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                               b->ops, b->off, b->text, b->props, use_resume);
+    } else if (h->st.DL)
         hipLaunchKernelGGL(k_replay<TierGlbT<true>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     else
@@ -748,7 +1009,13 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
         } else {
             ok = hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream) == hipSuccess;
         }
-        if (ok) {
+        if (ok && h->st.PP > 0) {
+            const size_t lb = paged_layout(h->st.PP, h->st.PH, h->st.UT, gw).total;
+            hipLaunchKernelGGL(k_generate_paged<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
+                               h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride, pstride, d_fail,
+                               d_trace);
+            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+        } else if (ok) {
             hipLaunchKernelGGL(k_generate<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(false, glb_caps(h), gw), h->stream, h->st, *cfg, doc_index_base,
                                b->ops, b->text, b->props, tstride, pstride, d_fail, d_trace, glb_caps(h));
@@ -830,6 +1097,42 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const DevState &st = h->st;
     HIPCHK(h, hipMemcpy(&hd.hdr, st.hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
+    if (hd.hdr.pad[HDR_PAGED]) {
+        // paged layout: concatenate the pages in directory order; leaf-block counts from
+        // the page metadata
+        const size_t PP = st.PP, slots = PP * MT_PG_SLOTS;
+        const int np = hd.hdr.pad[HDR_NPAGES];
+        std::vector<uint16_t> dir(std::max(np, 1));
+        std::vector<PageMeta> meta(PP);
+        std::vector<int4> pA(slots);
+        std::vector<u64> pO(slots);
+        std::vector<uint4> pB(slots);
+        HIPCHK(h, hipMemcpy(dir.data(), st.pgDir + doc * PP, np * sizeof(uint16_t), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(meta.data(), st.pgMeta + doc * PP, PP * sizeof(PageMeta), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(pA.data(), st.pgA + doc * slots, slots * sizeof(int4), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(pO.data(), st.pgO + doc * slots, slots * sizeof(u64), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(pB.data(), st.pgB + doc * slots, slots * sizeof(uint4), hipMemcpyDeviceToHost));
+        hd.A.clear();
+        hd.O.clear();
+        hd.B.clear();
+        hd.cnt.clear();
+        for (int q = 0; q < np; q++) {
+            const PageMeta &m = meta[dir[q]];
+            const size_t b0 = (size_t)dir[q] * MT_PG_SLOTS;
+            for (int i = 0; i < m.nseg; i++) {
+                hd.A.push_back(pA[b0 + i]);
+                hd.O.push_back(pO[b0 + i]);
+                hd.B.push_back(pB[b0 + i]);
+            }
+            for (int k = 0; k < m.nblk; k++) hd.cnt.push_back(m.bcnt[k]);
+        }
+        hd.hdr.n_seg = (int)hd.A.size();
+        hd.hdr.n_blk[0] = (int)hd.cnt.size();
+        hd.A.resize(std::max<size_t>(hd.A.size(), 1));
+        hd.O.resize(std::max<size_t>(hd.O.size(), 1));
+        hd.B.resize(std::max<size_t>(hd.B.size(), 1));
+        hd.cnt.resize(std::max<size_t>(hd.cnt.size(), 1));
+    } else {
     const int n = hd.hdr.n_seg;
     hd.A.resize(std::max(n, 1));
     hd.O.resize(std::max(n, 1));
@@ -841,6 +1144,7 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
     }
     hd.cnt.resize((size_t)MT_LV * st.B);
     HIPCHK(h, hipMemcpy(hd.cnt.data(), st.cnt + (size_t)doc * MT_LV * st.B, MT_LV * st.B, hipMemcpyDeviceToHost));
+    }
     if (with_text) {
         hd.text.resize(st.T);
         HIPCHK(h, hipMemcpy(hd.text.data(), st.text + ((size_t)doc * 2 + hd.hdr.text_half) * st.T, st.T * 2,

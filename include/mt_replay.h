@@ -48,6 +48,14 @@ typedef struct mt_options {
     int32_t lds_seg_capacity;   /* segments a document may hold while staged in LDS
                                    (default 192; -1 = always replay from HBM).  A document
                                    that outgrows it is replayed from HBM transparently. */
+    int32_t page_capacity;      /* paged layout for documents that outgrow the LDS tier:
+                                   pages (level-1 B-tree nodes, <= 64 segments each) per
+                                   document; 0 = off (such documents replay from the flat
+                                   HBM tier, O(segments) per op) */
+    int32_t page_heap_capacity; /* zamboni heap entries of a paged document (default 1024) */
+    int32_t unsettled_capacity; /* segments of a paged document inserted or removed above
+                                   minSeq (default 256) */
+    int32_t uid_capacity;       /* segment ids of a paged document (default 65536) */
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

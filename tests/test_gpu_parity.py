@@ -24,15 +24,26 @@ def _gpu_outputs(mt, doc):
                 deltas=mt.get_delta_log(doc), status=int(mt.status()[doc]))
 
 
-# lds_seg_capacity: 0 = default LDS tier (large documents retried from HBM), -1 = HBM tier
-# only, 16 = tiny LDS tier (most documents overflow mid-batch and are replayed from HBM)
-@pytest.mark.parametrize("lds", [0, -1, 16])
+# Storage tiers: "lds" = default LDS tier (large documents continue in the flat HBM tier),
+# "hbm" = flat HBM tier only, "tiny" = 16-segment LDS tier (most documents overflow
+# mid-batch), "paged" = every document in the paged layout from the start, "tiny_paged" =
+# documents overflowing a 16-segment LDS tier continue in the paged layout.
+TIERS = {
+    "lds": dict(lds_seg_capacity=0),
+    "hbm": dict(lds_seg_capacity=-1),
+    "tiny": dict(lds_seg_capacity=16),
+    "paged": dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=1024),
+    "tiny_paged": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024),
+}
+
+
+@pytest.mark.parametrize("tier", list(TIERS))
 @pytest.mark.parametrize("name", gu.ALL_FIXTURES)
-def test_gpu_matches_reference(name, lds):
+def test_gpu_matches_reference(name, tier):
     fx = gu.load(name)
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
-    mt = _gpu_batch(len(fx["docs"]), lds_seg_capacity=lds)
+    mt = _gpu_batch(len(fx["docs"]), **TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     bad = []
@@ -41,14 +52,20 @@ def test_gpu_matches_reference(name, lds):
         if errs:
             bad.append((doc["doc"], errs))
     assert not bad, f"{name}: {bad[:4]}"
+    paged = [mt.is_paged(i) for i in range(len(fx["docs"]))]
+    if tier == "paged":
+        assert all(paged)
+    elif "paged" not in tier:
+        assert not any(paged)
 
 
+@pytest.mark.parametrize("tier", ["lds", "paged"])
 @pytest.mark.parametrize("name", ["ref_c3", "ref_ext", "ref_ext_long"])
-def test_gpu_checksums_match_oracle(oracle_lib, name):
+def test_gpu_checksums_match_oracle(oracle_lib, name, tier):
     fx = gu.load(name)
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
-    mt = _gpu_batch(len(fx["docs"]))
+    mt = _gpu_batch(len(fx["docs"]), **TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     sums = mt.checksums()
@@ -58,7 +75,8 @@ def test_gpu_checksums_match_oracle(oracle_lib, name):
         assert np.array_equal(sums[f], osums[f]), f
 
 
-def test_gpu_split_batches_equal_single_batch(oracle_lib):
+@pytest.mark.parametrize("tier", ["lds", "tiny_paged"])
+def test_gpu_split_batches_equal_single_batch(oracle_lib, tier):
     """Applying a document's messages in several calls equals one call (state persists)."""
     fx = gu.load("ref_c2")
     interner = gu.interner_for(fx)
@@ -66,7 +84,7 @@ def test_gpu_split_batches_equal_single_batch(oracle_lib):
     mt1 = _gpu_batch(len(fx["docs"]))
     mt1.load_initial_text(a["seed_off"], a["seed"])
     mt1.apply_arrays(a)
-    mt2 = _gpu_batch(len(fx["docs"]))
+    mt2 = _gpu_batch(len(fx["docs"]), **TIERS[tier])
     mt2.load_initial_text(a["seed_off"], a["seed"])
     off = a["doc_off"]
     for lo_frac, hi_frac in ((0.0, 0.3), (0.3, 0.31), (0.31, 1.0)):
@@ -80,16 +98,20 @@ def test_gpu_split_batches_equal_single_batch(oracle_lib):
         mt2.apply_arrays(dict(a, ops=a["ops"][idx], doc_off=np.asarray(noff, dtype=np.int64)))
     s1, s2 = mt1.checksums(), mt2.checksums()
     assert np.array_equal(s1, s2)
+    if tier == "tiny_paged":
+        assert any(mt2.is_paged(i) for i in range(len(fx["docs"])))
 
 
-@pytest.mark.parametrize("lds", [0, -1])
-@pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6)])
-def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, lds):
+@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged"])
+@pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6), ("c3", 3000, 4)])
+def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     import json
     import os
+    if ops > 1000 and tier in ("hbm", "lds"):
+        pytest.skip("long streams: paged tiers only")
     cfg = json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))[cfgname]
     cfg = dict(cfg, ops=ops)
-    mt = _gpu_batch(docs, lds_seg_capacity=lds)
+    mt = _gpu_batch(docs, **TIERS[tier])
     b = mt.generate(cfg)
     got = b.download()
     gsums = mt.checksums()
