@@ -48,9 +48,18 @@ def parse():
 def capacities(cfg):
     """Per-document capacities sized for the workload (DESIGN.md 'HBM layout')."""
     if cfg["writers"] > 8 or cfg["lag"] > 64 or cfg["p_insert_props"] > 0 or cfg["ops"] > 4000:
-        # annotate keeps segments apart (property sets differ): ~0.4 live segments per op
+        # annotate keeps segments apart (property sets differ): ~0.4 live segments per op.
+        # Documents outgrow the LDS tier early and continue in the paged layout; the flat
+        # HBM arrays only hold what the LDS tier spills.
         segs = max(1024, int(cfg["ops"] * 0.5) + 512)
-        return dict(seg_capacity=segs, text_capacity=1 << 16, heap_capacity=segs, props_capacity=2 * segs + 256)
+        deep = cfg["lag"] > 64
+        return dict(seg_capacity=256, text_capacity=1 << 16, heap_capacity=512, props_capacity=segs + 256,
+                    # high-water marks (mt_last_paged_peaks) at 10k ops: C3 174 pages, 178
+                    # table entries, 153 heap entries; C4 (minSeq ~1k ops behind) far more
+                    page_capacity=max(64, segs // 20 if not deep else segs // 14),
+                    page_heap_capacity=2560 if deep else 512,
+                    unsettled_capacity=2560 if deep else 320,
+                    uid_capacity=min(1 << 16, 3 * cfg["ops"] + 1024))
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
 
@@ -160,7 +169,8 @@ def main():
     if not args.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import pyoracle                            # the checker, timed as the CPU baseline
-        n_sample = args.cpu_sample_docs or docs
+        # bounded sample: about 20M ops of CPU work (all of C2's rank-0 documents)
+        n_sample = args.cpu_sample_docs or min(docs, max(1, 20_000_000 // max(cfg["ops"], 1)))
         off = host["doc_off"]
         sel_end = int(off[n_sample])
         arrays = dict(ops=host["ops"][:sel_end], doc_off=off[: n_sample + 1], text=host["text"],

@@ -100,6 +100,12 @@ class MergeTreeBatch:
         return dict(total=int(out[0]), spilled=int(out[1]), segments=int(out[2]), blocks=int(out[3]), heap=int(out[4]),
                     text=int(out[5]), props=int(out[6]), at_load=int(out[7]))
 
+    def last_paged_peaks(self):
+        """High-water marks of the paged documents of the last batch / generation."""
+        out = np.zeros(4, dtype=np.uint32)
+        self._check(self.lib.mt_last_paged_peaks(self.h, _native.ptr(out)), "mt_last_paged_peaks")
+        return dict(pages=int(out[0]), unsettled=int(out[1]), heap=int(out[2]), segments=int(out[3]))
+
     def last_kernel_ms(self):
         return float(self.lib.mt_last_kernel_ms(self.h))
 

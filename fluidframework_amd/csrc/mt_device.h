@@ -65,6 +65,7 @@ static_assert(sizeof(PageMeta) == 24, "PageMeta size");
 #define HDR_PAGED 0           // 1: the document lives in the paged layout
 #define HDR_NPAGES 1          // pages in the directory
 #define HDR_UTN 2             // entries of the unsettled-segment table
+#define HDR_DIAG 3            // failure diagnostic (source line of an internal error)
 
 struct DevState {
     DocHdr *hdr;

@@ -96,7 +96,6 @@ template <class T> struct DocT {
     int pend_split;         // the page reached MaxNodesInBlock leaf blocks: split it after the op
     int pend_second;        // leaf block split while a page split was pending (-1: none)
     LDS_AS uint16_t *dir;   // upper instance: page ids in level-1 order (moved with level 1)
-    void *pg;               // -> PagedDoc (window instance)
 #ifdef MT_PROF
     LDS_AS u64 *prof;       // [32] section timers
 #endif
@@ -179,6 +178,13 @@ static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, i
 TD void fail(DocT<T> &d, int code) {
     if (d.status == 0) d.status = code;
 }
+// an inconsistent tree: the source line is kept in cap_cause (diagnostic; paged documents
+// store it in their header)
+#define FAIL_INTERNAL(d)                                    \
+    do {                                                    \
+        if ((d).status == 0) (d).cap_cause = 10000 + __LINE__; \
+        fail(d, MT_DOC_INTERNAL);                           \
+    } while (0)
 // Out of a capacity: the LDS tier hands the document to the HBM tier, which reports it.
 // cause (diagnostic): 1 segments, 2 blocks, 3 heap, 4 text, 5 property records
 TD void fail_cap(DocT<T> &d, int cause) {
@@ -246,7 +252,6 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.pend_split = 0;
     d.pend_second = -1;
     d.dir = nullptr;
-    d.pg = nullptr;
     if (d.status) return true;   // failed earlier: the caller leaves it untouched
     if (h.pad[HDR_PAGED]) {      // lives in the paged layout: the paged kernel replays it
         d.status = MT_DOC_RETRY;
@@ -526,7 +531,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
         if (has_parent) {
             P = blk_find(d, l + 1, b, true, pstart);
             if (P < 0) {
-                fail(d, MT_DOC_INTERNAL);
+                FAIL_INTERNAL(d);
                 return;
             }
         }
@@ -866,7 +871,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
     int bstart;
     const int b = blk_find(d, 0, i, true, bstart);
     if (b < 0) {
-        fail(d, MT_DOC_INTERNAL);
+        FAIL_INTERNAL(d);
         return;
     }
     seg_move_right(d, i + 1, 1);
@@ -1354,7 +1359,7 @@ TD void pack(DocT<T> &d, int l, int b) {
         int c0;
         const int P = blk_find(d, l + 1, b, true, c0);
         if (P < 0) {
-            fail(d, MT_DOC_INTERNAL);
+            FAIL_INTERNAL(d);
             return;
         }
         const int nch = cntr(d, l + 1, P);
@@ -1370,6 +1375,34 @@ TD void pack(DocT<T> &d, int l, int b) {
         if (k < 1) k = 1;
         const int base = total / k, extra = total % k;
         blk_replace(d, l, c0, nch, k, base, extra);
+        if (d.status) return;
+        if (lane() == 0) lvl(d, l + 1)[P] = (uint8_t)k;
+        wsync<T>();
+        if (k < MT_HALF && l + 2 < d.depth) {
+            l = l + 1;
+            b = P;
+            continue;
+        }
+        return;
+    }
+}
+
+// pack :1401-1453 above the leaf level only (no scour): the paged upper instance
+TD void pack_counts(DocT<T> &d, int l, int b) {
+    while (true) {
+        int c0;
+        const int P = blk_find(d, l + 1, b, true, c0);
+        if (P < 0) {
+            FAIL_INTERNAL(d);
+            return;
+        }
+        const int nch = cntr(d, l + 1, P);
+        int total = 0;
+        for (int cb = c0; cb < c0 + nch; cb++) total += cntr(d, l, cb);
+        int k = total / MT_HALF;
+        if (k > MT_MAXN - 1) k = MT_MAXN - 1;
+        if (k < 1) k = 1;
+        blk_replace(d, l, c0, nch, k, total / k, total % k);
         if (d.status) return;
         if (lane() == 0) lvl(d, l + 1)[P] = (uint8_t)k;
         wsync<T>();
@@ -1406,7 +1439,7 @@ TD void zamboni(DocT<T> &d) {
         int bstart;
         const int b = blk_find(d, 0, i, true, bstart);
         if (b < 0) {
-            fail(d, MT_DOC_INTERNAL);
+            FAIL_INTERNAL(d);
             return;
         }
         const int f = flgr(d, b);
@@ -1555,7 +1588,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     int bstart;
     const int B = blk_find(d, 0, ip, false, bstart);
     if (B < 0) {
-        fail(d, MT_DOC_INTERNAL);
+        FAIL_INTERNAL(d);
         return;
     }
     const int bend = bstart + cntr(d, 0, B);

@@ -20,8 +20,21 @@
 #pragma once
 #include "mt_engine.h"
 
+// MT_PROF section timers of the paged driver (slots 9..15; the engine uses 0..8)
+#ifdef MT_PROF
+#define PG_T0(k) const unsigned long long _pt##k = __builtin_amdgcn_s_memtime();
+#define PG_T1(k)                                                         \
+    if (lane() == 0) {                                                   \
+        pd.w.prof[k] += __builtin_amdgcn_s_memtime() - _pt##k;           \
+        pd.w.prof[16 + k] += 1ull;                                       \
+    }
+#else
+#define PG_T0(k)
+#define PG_T1(k)
+#endif
+
 template <class T> struct PagedDoc {
-    DocT<T> w;    // window: one page staged in LDS
+    DocT<T> w;    // window: one page staged in LDS (first member: see pdoc)
     DocT<T> up;   // levels >= 1 of the tree (level 1 = pages, counted in leaf blocks)
     LDS_AS PageMeta *meta;    // [PP] by page id
     LDS_AS int *pvl;          // [PP] by page id: view length of the current view
@@ -43,13 +56,16 @@ template <class T> struct PagedDoc {
     int PP, PH, UT, UM;
     int nfree, ut_n;
     int cur;                  // page id staged in the window (-1: none)
+    int cur_pos;              // its level-1 position (-1: not known yet)
+    int dirty;                // the window differs from the page in HBM (slots, uid map, table)
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
 
 struct PagedLayout {
     uint32_t offWA, offWB, offWO, offWcnt, offWflg, offWends, offWscr, offWnb;
-    uint32_t offUcnt, offUnb, offDir, offMeta, offPvl, offFree, offHeap, offUpage, offUA, offUO, offGen, total;
+    uint32_t offUcnt, offUnb, offDir, offMeta, offPvl, offFree, offHeap, offUpage, offUA, offUO, offGen, offProf,
+        total;
 };
 static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words) {
     PagedLayout L;
@@ -73,11 +89,25 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     L.offWcnt = o; o += (uint32_t)MT_LV * PW_B;
     L.offWflg = o; o += PW_B;
     L.offUcnt = o; o += (uint32_t)MT_LV * PP;
+#ifdef MT_PROF
+    o = (o + 7u) & ~7u;
+    L.offProf = o; o += 32u * 8;
+#else
+    L.offProf = 0;
+#endif
     L.total = (o + 15u) & ~15u;
     return L;
 }
 
-TD PagedDoc<T> &pdoc(DocT<T> &w) { return *(PagedDoc<T> *)w.pg; }
+// the window is PagedDoc's first member (standard layout: pointer-interconvertible); no
+// pointer to the PagedDoc is stored, so the whole struct stays in registers
+TD PagedDoc<T> &pdoc(DocT<T> &w) { return *reinterpret_cast<PagedDoc<T> *>(&w); }
+// a paged-layout capacity (cause: 4 text, 5 property records, 7 pages, 8 unsettled table,
+// 9 uid map, 3 heap; kept in the header's HDR_DIAG word)
+TD void pg_fail_cap(DocT<T> &w, int cause) {
+    if (w.status == 0) w.cap_cause = cause;
+    fail(w, MT_DOC_CAPACITY);
+}
 TD bool unsettled(const v4i a, int min_seq) {
     return a.y > min_seq || (a.z != MT_RSEQ_NONE && a.z > min_seq);
 }
@@ -92,8 +122,19 @@ TD int pg_pos(PagedDoc<T> &pd, int pg) {
     return -1;
 }
 
+TD int pg_cur_pos(PagedDoc<T> &pd) {
+    if (pd.cur_pos < 0) pd.cur_pos = pg_pos(pd, pd.cur);
+    return pd.cur_pos;
+}
+
 // ------------------------------------------------------------------ window load / store
+TD void pg_win_load_impl(PagedDoc<T> &pd, int pg);
 TD void pg_win_load(PagedDoc<T> &pd, int pg) {
+    PG_T0(10)
+    pg_win_load_impl(pd, pg);
+    PG_T1(10)
+}
+TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
     DocT<T> &w = pd.w;
     const int n = uni(pd.meta[pg].nseg), nb = uni(pd.meta[pg].nblk);
     const int i = lane();
@@ -119,6 +160,8 @@ TD void pg_win_load(PagedDoc<T> &pd, int pg) {
     w.pend_split = 0;
     w.pend_second = -1;
     pd.cur = pg;
+    pd.cur_pos = -1;
+    pd.dirty = 0;
     wsync<T>();
 }
 
@@ -162,7 +205,7 @@ TD void pg_table_add(PagedDoc<T> &pd, int lo, int hi, int pg2) {
     const bool add = v && unsettled<T>(a, w.min_seq);
     const u64 m = ballot(add);
     if (pd.ut_n + __popcll(m) > pd.UT) {
-        fail(w, MT_DOC_CAPACITY);
+        pg_fail_cap(w, 8);
         return;
     }
     const int at = pd.ut_n + __popcll(m & ((1ull << lane()) - 1ull));
@@ -218,23 +261,21 @@ TD void pg_split_page(PagedDoc<T> &pd) {
     int s0 = 0;
     for (int q = 0; q < sp; q++) s0 += cntr(w, 0, q);
     if (pd.nfree == 0) {
-        fail(w, MT_DOC_CAPACITY);
+        pg_fail_cap(w, 7);
         return;
     }
     pd.nfree--;
     const int np = uni(pd.freel[pd.nfree]);
-    const int cur = pd.cur;
-    const int pos = pg_pos(pd, cur);
-    // table: entries of cur are rebuilt for both halves
-    pg_table_purge(pd, cur);
-    pg_table_add(pd, 0, s0, cur);
+    const int pos = pg_cur_pos(pd);
+    // table: the second half's unsettled segments move to the new page (the window's own
+    // entries are rebuilt when it is flushed)
     pg_table_add(pd, s0, w.n, np);
     if (w.status) return;
     pg_write_page(pd, np, s0, w.n, sp, nbk);
     // level 1: new node after cur (blk_split_up grows the parents / the root)
     blk_split_up(up, 1, pos);
     if (up.status) {
-        fail(w, MT_DOC_CAPACITY);
+        pg_fail_cap(w, 7);
         return;
     }
     if (lane() == 0) {
@@ -253,8 +294,9 @@ TD void pg_split_page(PagedDoc<T> &pd) {
     wsync<T>();
 }
 
-// Stores the window's page (after any pending page split) and refreshes its table entries.
-TD void pg_win_store(PagedDoc<T> &pd) {
+// After a step that modified the window: resolves a pending page split and brings the
+// page's metadata and level-1 count up to date (LDS only; the slots stay in the window).
+TD void pg_win_sync(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     if (pd.cur < 0) return;
@@ -265,21 +307,55 @@ TD void pg_win_store(PagedDoc<T> &pd) {
     if (w.pend_split) {
         pg_split_page(pd);
         if (w.status) return;
-    } else {
-        pg_table_purge(pd, pd.cur);
-        pg_table_add(pd, 0, w.n, pd.cur);
-        if (w.status) return;
     }
     const int nbk = nbr(w, 0);
-    pg_write_page(pd, pd.cur, 0, w.n, 0, nbk);
-    const int pos = pg_pos(pd, pd.cur);
-    if (lane() == 0) lvl(up, 1)[pos] = (uint8_t)nbk;
+    const int i = lane();
+    int ol = 0;
+    if (i < w.n) ol = obs_len(w.A[i]);
+    const int obs = wave_sum(ol);
+    const int pg = pd.cur;
+    if (i < 8) {
+        pd.meta[pg].bcnt[i] = i < nbk ? lvl(w, 0)[i] : 0;
+        pd.meta[pg].flg[i] = i < nbk ? w.flg[i] : (int8_t)0;
+    }
+    const int pos = pg_cur_pos(pd);
+    if (i == 0) {
+        pd.meta[pg].nseg = (uint8_t)w.n;
+        pd.meta[pg].nblk = (uint8_t)nbk;
+        pd.meta[pg].obs = obs;
+        lvl(up, 1)[pos] = (uint8_t)nbk;
+    }
+    pd.dirty = 1;
     wsync<T>();
+}
+
+// Writes a dirty window back: slots and uid map to HBM, its unsettled-table entries rebuilt.
+TD void pg_win_flush_impl(PagedDoc<T> &pd);
+TD void pg_win_flush(PagedDoc<T> &pd) {
+    PG_T0(11)
+    pg_win_flush_impl(pd);
+    PG_T1(11)
+}
+TD void pg_win_flush_impl(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    if (pd.cur < 0 || !pd.dirty) return;
+    pg_table_purge(pd, pd.cur);
+    pg_table_add(pd, 0, w.n, pd.cur);
+    if (w.status) return;
+    pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0));
+    pd.dirty = 0;
 }
 
 // ------------------------------------------------------------------ page view lengths
 // pvl[page] = view length of every page for (c, r); returns the total.
+TD int pg_views_impl(PagedDoc<T> &pd, int r, int c);
 TD int pg_views(PagedDoc<T> &pd, int r, int c) {
+    PG_T0(9)
+    const int r_ = pg_views_impl(pd, r, c);
+    PG_T1(9)
+    return r_;
+}
+TD int pg_views_impl(PagedDoc<T> &pd, int r, int c) {
     const int np = nbr(pd.up, 1);
     int tot = 0;
     for (int base = 0; base < np; base += MT_WAVE) {
@@ -290,13 +366,24 @@ TD int pg_views(PagedDoc<T> &pd, int r, int c) {
         }
     }
     wsync<T>();
+    const int cur = pd.cur;
     for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
         const int e = base + lane();
         if (e < pd.ut_n) {
+            const int pg = pd.upage[e];
             const v4i a = pd.uA[e];
             const int dlt = view_len(a, pd.uO[e], r, c) - obs_len(a);
-            if (dlt) atomicAdd((int *)(pd.pvl + pd.upage[e]), dlt);
+            if (dlt && pg != cur) atomicAdd((int *)(pd.pvl + pg), dlt);
         }
+    }
+    if (cur >= 0) {   // the window's page: its own slots are authoritative
+        DocT<T> &w = pd.w;
+        const int i = lane();
+        v4i a;
+        u64 o;
+        load_ao(w, i, i < w.n, a, o);
+        const int dlt = wave_sum(i < w.n ? view_len(a, o, r, c) - obs_len(a) : 0);
+        if (i == 0) pd.pvl[cur] += dlt;
     }
     wsync<T>();
     for (int base = 0; base < np; base += MT_WAVE) {
@@ -307,7 +394,14 @@ TD int pg_views(PagedDoc<T> &pd, int r, int c) {
 }
 // First level-1 position whose cumulative view end is >= p (strict: > p); start = its
 // view start.  -1 (start = total) if none.
+TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start);
 TD int pg_find(PagedDoc<T> &pd, int p, bool strict, int &start) {
+    PG_T0(13)
+    const int r_ = pg_find_impl(pd, p, strict, start);
+    PG_T1(13)
+    return r_;
+}
+TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start) {
     const int np = nbr(pd.up, 1);
     int carry = 0;
     for (int base = 0; base < np; base += MT_WAVE) {
@@ -337,9 +431,10 @@ TD int pg_obs_start(PagedDoc<T> &pd, int pos) {
 TD void pg_load_pos(PagedDoc<T> &pd, int pos) {
     const int pg = uni(pd.up.dir[pos]);
     if (pd.cur != pg) {
-        pg_win_store(pd);
+        pg_win_flush(pd);
         pg_win_load(pd, pg);
     }
+    pd.cur_pos = pos;
     pd.w.obs_base = pg_obs_start(pd, pos);
 }
 
@@ -347,15 +442,21 @@ TD void pg_load_pos(PagedDoc<T> &pd, int pos) {
 // pack :1401-1453 for the underflowing page at level-1 position pos: the leaf blocks of
 // every child of its parent are regrouped into max(1, min(7, n/4)) pages (copied in HBM
 // into fresh pages); then the parent may underflow in turn (counts only above level 1).
+TD void pg_pack1_impl(PagedDoc<T> &pd, int pos);
 TD void pg_pack1(PagedDoc<T> &pd, int pos) {
+    PG_T0(14)
+    pg_pack1_impl(pd, pos);
+    PG_T1(14)
+}
+TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
-    pg_win_store(pd);
+    pg_win_flush(pd);
     pd.cur = -1;
     int c0;
     const int P = blk_find(up, 2, pos, true, c0);
     if (P < 0) {
-        fail(w, MT_DOC_INTERNAL);
+        FAIL_INTERNAL(w);
         return;
     }
     const int nch = cntr(up, 2, P);
@@ -369,7 +470,7 @@ TD void pg_pack1(PagedDoc<T> &pd, int pos) {
     if (k < 1) k = 1;
     const int base = TB / k, extra = TB % k;
     if (pd.nfree < k) {
-        fail(w, MT_DOC_CAPACITY);
+        pg_fail_cap(w, 7);
         return;
     }
     // per lane: one leaf block of the concatenation (TB <= 49): its old page / index
@@ -395,18 +496,17 @@ TD void pg_pack1(PagedDoc<T> &pd, int pos) {
     const int8_t bflg = opg >= 0 ? pd.meta[opg].flg[ob] : (int8_t)0;
     // new page m gets blocks [nb0(m), nb0(m) + base + (m < extra))
     auto nb0 = [&](int m) { return m * base + min(m, extra); };
-    uint16_t newp[MT_MAXN];
-#pragma unroll
-    for (int m = 0; m < MT_MAXN; m++) newp[m] = 0;
+    LDS_AS int32_t *newp = w.scr;   // scratch: the new page ids
     for (int m = 0; m < k; m++) {
         pd.nfree--;
-        newp[m] = (uint16_t)uni(pd.freel[pd.nfree]);
+        if (lane() == 0) newp[m] = pd.freel[pd.nfree];
     }
+    wsync<T>();
     // table entries of the old pages go; the copy pass re-adds the unsettled ones
     for (int j = 0; j < nch; j++) pg_table_purge(pd, uni(up.dir[c0 + j]));
     // copy, one new page at a time (<= 7 * 8 segments each)
     for (int m = 0; m < k; m++) {
-        const int npg = newp[m];
+        const int npg = uni(newp[m]);
         const int blo = nb0(m), bhi = nb0(m + 1);
         const int s_lo = bcast(bseg0, blo);
         const int s_hi = bhi < TB ? bcast(bseg0, bhi) : TS;
@@ -441,7 +541,7 @@ TD void pg_pack1(PagedDoc<T> &pd, int pos) {
         }
         const u64 am = ballot(add);
         if (pd.ut_n + __popcll(am) > pd.UT) {
-            fail(w, MT_DOC_CAPACITY);
+            pg_fail_cap(w, 8);
             return;
         }
         if (add) {
@@ -485,20 +585,29 @@ TD void pg_pack1(PagedDoc<T> &pd, int pos) {
     // level 1: nch entries -> k entries of base (+1) blocks; then the page ids
     blk_replace(up, 1, c0, nch, k, base, extra);
     if (up.status) {
-        fail(w, MT_DOC_CAPACITY);
+        pg_fail_cap(w, 7);
         return;
     }
     for (int m = 0; m < k; m++)
-        if (lane() == 0) up.dir[c0 + m] = newp[m];
+        if (lane() == 0) up.dir[c0 + m] = (uint16_t)newp[m];
     if (lane() == 0) lvl(up, 2)[P] = (uint8_t)k;
     wsync<T>();
-    if (k < MT_HALF && 3 < up.depth) pack(up, 2, P);   // counts only above level 1
-    if (up.status) fail(w, MT_DOC_INTERNAL);
+    if (k < MT_HALF && 3 < up.depth) pack_counts(up, 2, P);   // counts only above level 1
+    if (up.status) {
+        if (w.status == 0) w.cap_cause = up.cap_cause;
+        fail(w, MT_DOC_INTERNAL);
+    }
 }
 
 // ------------------------------------------------------------------ zamboni (paged)
 // zamboniSegments :1455-1511 with the heap in LDS and the uid -> page map in HBM.
+TD void pg_zamboni_impl(PagedDoc<T> &pd);
 TD void pg_zamboni(PagedDoc<T> &pd) {
+    PG_T0(12)
+    pg_zamboni_impl(pd);
+    PG_T1(12)
+}
+TD void pg_zamboni_impl(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     for (int it = 0; it < MT_ZAMBONI && w.status == 0; it++) {
         if (w.heap_n == 0) break;
@@ -507,20 +616,25 @@ TD void pg_zamboni(PagedDoc<T> &pd) {
         heap_pop(w);
         wsync<T>();
         const uint32_t uid = (uint32_t)top.y;
-        if (uid >= (uint32_t)pd.UM) continue;
-        const int pg = uni(pd.gumap[uid]);
-        if (pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) continue;
-        if (pd.cur != pg) {
-            pg_win_store(pd);
+        if (uid >= (uint32_t)pd.UM) {
+            pg_fail_cap(w, 9);
+            return;
+        }
+        // the window first (its uid map entries are written when it is flushed)
+        int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
+        if (i < 0) {
+            const int pg = uni(pd.gumap[uid]);
+            if (pg == pd.cur || pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) continue;
+            pg_win_flush(pd);
             if (w.status) return;
             pg_win_load(pd, pg);
+            i = find_uid(w, uid);
+            if (i < 0) continue;
         }
-        const int i = find_uid(w, uid);
-        if (i < 0) continue;
         int bstart;
         const int b = blk_find(w, 0, i, true, bstart);
         if (b < 0) {
-            fail(w, MT_DOC_INTERNAL);
+            FAIL_INTERNAL(w);
             return;
         }
         const int f = flgr(w, b);
@@ -531,14 +645,17 @@ TD void pg_zamboni(PagedDoc<T> &pd) {
         wsync<T>();
         if (lane() == 0) w.flg[b] = 0;
         wsync<T>();
+        bool pk = false;
         if (kept < old && kept < MT_HALF && w.depth > 1) {
             pack(w, 0, b);   // regroups this page's leaf blocks (stops at the window top)
             if (w.status) return;
-            if (nbr(w, 0) < MT_HALF && pd.up.depth > 2) {
-                const int pos = pg_pos(pd, pd.cur);
-                pg_pack1(pd, pos);
-                if (w.status) return;
-            }
+            pk = nbr(w, 0) < MT_HALF && pd.up.depth > 2;
+        }
+        pg_win_sync(pd);
+        if (w.status) return;
+        if (pk) {
+            pg_pack1(pd, pg_cur_pos(pd));
+            if (w.status) return;
         }
     }
 }
@@ -569,7 +686,7 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     rel.op.pos1 = op.pos1 - start;
     op_insert(w, rel, tin, pin);
     if (w.status) return;
-    pg_win_store(pd);
+    pg_win_sync(pd);
 }
 
 TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
@@ -580,7 +697,7 @@ TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
     pg_load_pos(pd, pos);
     boundary(pd.w, p - start, r, c);
     if (pd.w.status) return;
-    pg_win_store(pd);
+    pg_win_sync(pd);
 }
 
 TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
@@ -609,17 +726,23 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
             w.obs_base = ocarry;
             const bool done = range_mark(w, op, rec, carry, ocarry, cb);
             if (w.status) return;
-            pg_win_store(pd);
+            pg_win_sync(pd);
             if (w.status) return;
             if (done) break;
-            pos = pg_pos(pd, pd.cur) + 1;   // a page split may have inserted after cur
+            pos = pg_cur_pos(pd) + 1;
         }
     }
     cb_end(w, cb);
 }
 
 // Client.applyMsg (MT/client.ts:797-819) for a paged document; mirrors apply_op.
+TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin);
 TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    PG_T0(15)
+    pg_apply_op_impl(pd, in, tin, pin);
+    PG_T1(15)
+}
+TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
     const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
@@ -670,8 +793,9 @@ TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin,
 // Compacts the live text of every page into the other arena half, page by page.
 TD bool paged_text_ensure(DocT<T> &w, int need) {
     PagedDoc<T> &pd = pdoc(w);
-    const int keep = pd.cur;
-    pg_win_store(pd);
+    const int keep = pd.cur, keep_pos = pd.cur_pos;
+    if (keep >= 0) pd.dirty = 1;   // a scour may have updated flags in the window since its sync
+    pg_win_flush(pd);
     if (w.status) return false;
     gsync_rd();
     const int dh = 1 - w.text_half;
@@ -713,16 +837,20 @@ TD bool paged_text_ensure(DocT<T> &w, int need) {
     w.text_half = dh;
     w.text_top = carry;
     pd.cur = -1;
-    if (keep >= 0) pg_win_load(pd, keep);
+    if (keep >= 0) {
+        pg_win_load(pd, keep);
+        pd.cur_pos = keep_pos;
+    }
     if (w.text_top + need <= w.T_cap) return true;
-    fail(w, MT_DOC_CAPACITY);
+    pg_fail_cap(w, 4);
     return false;
 }
 
 TD bool paged_props_ensure(DocT<T> &w, int need) {
     PagedDoc<T> &pd = pdoc(w);
-    const int keep = pd.cur;
-    pg_win_store(pd);
+    const int keep = pd.cur, keep_pos = pd.cur_pos;
+    if (keep >= 0) pd.dirty = 1;   // a scour may have updated flags in the window since its sync
+    pg_win_flush(pd);
     if (w.status) return false;
     gsync_rd();
     const int dh = 1 - w.props_half;
@@ -752,9 +880,12 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
     w.props_top = carry;
     pd.cur = -1;
     gsync_rd();
-    if (keep >= 0) pg_win_load(pd, keep);
+    if (keep >= 0) {
+        pg_win_load(pd, keep);
+        pd.cur_pos = keep_pos;
+    }
     if (w.props_top + need <= w.P_cap) return true;
-    fail(w, MT_DOC_CAPACITY);
+    pg_fail_cap(w, 5);
     return false;
 }
 
@@ -803,6 +934,10 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.ends = (LDS_AS uint16_t *)(smem + L.offWends);
     w.scr = (LDS_AS int32_t *)(smem + L.offWscr);
     w.nb = (LDS_AS int32_t *)(smem + L.offWnb);
+#ifdef MT_PROF
+    w.prof = (LDS_AS u64 *)(smem + L.offProf);
+    if (lane() < 32) w.prof[lane()] = 0;
+#endif
     const DocHdr h = *w.hp;
     w.n = 0;
     w.depth = h.depth;
@@ -823,10 +958,8 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.pend_split = 0;
     w.pend_second = -1;
     w.dir = nullptr;
-    w.pg = &pd;
     up = w;
     up.paged = 0;
-    up.pg = nullptr;
     up.cnt = smem + L.offUcnt;
     up.nb = (LDS_AS int32_t *)(smem + L.offUnb);
     up.dir = (LDS_AS uint16_t *)(smem + L.offDir);
@@ -839,6 +972,8 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.uA = (LDS_AS v4i *)(smem + L.offUA);
     pd.uO = (LDS_AS u64 *)(smem + L.offUO);
     pd.cur = -1;
+    pd.cur_pos = -1;
+    pd.dirty = 0;
 }
 
 // Builds the free-page list from the directory (pvl as scratch marks).
@@ -901,7 +1036,7 @@ TD void pg_load(PagedDoc<T> &pd) {
 TD void pg_store(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
-    pg_win_store(pd);
+    pg_win_flush(pd);
     wsync<T>();
     const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) pd.gdir[q] = up.dir[q];
@@ -948,6 +1083,7 @@ TD void pg_store(PagedDoc<T> &pd) {
         h.pad[HDR_PAGED] = 1;
         h.pad[HDR_NPAGES] = np;
         h.pad[HDR_UTN] = pd.ut_n;
+        h.pad[HDR_DIAG] = w.status ? w.cap_cause : 0;
         *w.hp = h;
     }
 }
@@ -969,7 +1105,7 @@ TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
     const int depth = h.depth;
     const int np = depth == 1 ? 1 : h.n_blk[1];
     if (np + 8 > pd.PP || h.heap_n > pd.PH) {
-        fail(w, MT_DOC_CAPACITY);
+        pg_fail_cap(w, 7);
         return false;
     }
     up.depth = depth;
@@ -992,7 +1128,7 @@ TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
         int ns = 0;
         for (int q = 0; q < nbk; q++) ns += depth == 1 ? h.n_seg : (int)uni(fc[lb + q]);
         if (nbk > MT_MAXN || ns > MT_PG_SLOTS) {
-            fail(w, MT_DOC_INTERNAL);
+            FAIL_INTERNAL(w);
             return false;
         }
         // stage the page in the window, then write it like any other page

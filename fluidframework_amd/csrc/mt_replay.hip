@@ -394,6 +394,20 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
 }
 
 // ---------------------------------------------------------------- paged kernels
+// high-water marks -> stats[8..11] (mt_last_paged_peaks)
+template <class T>
+__device__ static void pg_peaks(const DevState &st, PagedDoc<T> &pd, int pk_ut, int pk_heap) {
+    const int np = nbr(pd.up, 1);
+    int ns = 0;
+    for (int q = lane(); q < np; q += MT_WAVE) ns += pd.meta[pd.up.dir[q]].nseg;
+    ns = wave_sum(ns);
+    if (lane() == 0) {
+        atomicMax(st.stats + 8, (uint32_t)np);
+        atomicMax(st.stats + 9, (uint32_t)pk_ut);
+        atomicMax(st.stats + 10, (uint32_t)pk_heap);
+        atomicMax(st.stats + 11, (uint32_t)ns);
+    }
+}
 // Replay of the documents flagged by the LDS tier (retry[doc]) in the paged layout: a
 // document seen for the first time is converted from its flat state (initial contents, or
 // what the LDS tier spilled) and stays paged until the next reset.
@@ -430,6 +444,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay_paged(DevState st, const mt_
     const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
+    int pk_ut = 0, pk_heap = 0;
     for (int64_t kb = k0; kb < k1 && w.status == 0; kb += MT_WAVE) {
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
@@ -476,12 +491,18 @@ __global__ void __launch_bounds__(MT_WAVE) k_replay_paged(DevState st, const mt_
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
             in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
             pg_apply_op(pd, in, gt, gp);
+            pk_ut = max(pk_ut, pd.ut_n);
+            pk_heap = max(pk_heap, w.heap_n);
         }
     }
     // a window capacity is a paged-layout capacity: there is no further tier
     if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
     pg_store(pd);
+    pg_peaks(st, pd, pk_ut, pk_heap);
     if (lane() == 0) st.retry[doc] = 0;
+#ifdef MT_PROF
+    if (lane() < 32) atomicAdd(&g_prof[lane()], w.prof[lane()]);
+#endif
 }
 
 // Generator for documents that outgrew the LDS tier: regenerated from the start in the
@@ -512,6 +533,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
     }
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)text_out;
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)props_out;
+    int pk_ut = 0, pk_heap = 0;
     for (int t = 1; t <= cfg.ops && w.status == 0; t++) {
         int r, c, msn;
         gen_pick(g, cfg, t, r, c, msn);
@@ -526,6 +548,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         OpIn in;
         gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
         pg_apply_op(pd, in, gt, gp);
+        pk_ut = max(pk_ut, pd.ut_n);
+        pk_heap = max(pk_heap, w.heap_n);
     }
     if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
     if (lane() == 0) {
@@ -533,6 +557,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         st.retry[doc] = 0;
     }
     pg_store(pd);
+    pg_peaks(st, pd, pk_ut, pk_heap);
 }
 
 // ---------------------------------------------------------------- checksums
@@ -756,9 +781,21 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         st.PH = o.page_heap_capacity > 0 ? o.page_heap_capacity : 1024;
         st.UT = o.unsettled_capacity > 0 ? o.unsettled_capacity : 256;
         st.UM = std::min(o.uid_capacity > 0 ? o.uid_capacity : 65536, 1 << 24);
-        if (paged_layout(st.PP, st.PH, st.UT, 2 * 65).total > 64 * 1024) {
+        // one document's paged state staged in LDS: up to the CU's 160 KiB (fewer
+        // documents per CU above 64 KiB)
+        const size_t lb = paged_layout(st.PP, st.PH, st.UT, 2 * 65).total;
+        if (lb > 160 * 1024) {
             delete h;
             return nullptr;
+        }
+        if (lb > 64 * 1024) {
+            const void *ks[] = {(const void *)k_replay_paged<TierLdsT<true>>, (const void *)k_replay_paged<TierLdsT<false>>,
+                                (const void *)k_generate_paged<TierLdsT<false>>};
+            for (const void *k : ks)
+                if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess) {
+                    delete h;
+                    return nullptr;
+                }
         }
     }
     const size_t N = n_docs;
@@ -959,6 +996,14 @@ int mt_last_hbm_docs(mt_handle *h, uint32_t *out) {
     return 0;
 }
 
+int mt_last_paged_peaks(mt_handle *h, uint32_t *out) {
+    if (!h || !out) return MT_E_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(out, h->st.stats + 8, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, uint64_t n_ops,
                  const uint16_t *text, uint64_t text_len, const uint32_t *props,
                  uint64_t props_len) {
@@ -999,6 +1044,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
         ok = hipMemcpy(b->off, off.data(), (N + 1) * 8, hipMemcpyHostToDevice) == hipSuccess &&
              hipMemset(d_fail, 0, N * 4) == hipSuccess;
     }
+    if (ok) ok = hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream) == hipSuccess;
     if (ok) {
         const int gw = 2 * (cfg->writers + 1);
         if (h->lds.S > 0) {
@@ -1027,7 +1073,10 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
         ok = hipMemcpy(f.data(), d_fail, N * 4, hipMemcpyDeviceToHost) == hipSuccess;
         for (int64_t i = 0; ok && i < N; i++)
             if (f[i]) {
-                h->err = "mt_generate: document " + std::to_string(i) + " failed with status " + std::to_string(f[i]);
+                DocHdr hd;
+                hipMemcpy(&hd, h->st.hdr + i, sizeof(DocHdr), hipMemcpyDeviceToHost);
+                h->err = "mt_generate: document " + std::to_string(i) + " failed with status " + std::to_string(f[i]) +
+                         " (diagnostic " + std::to_string(hd.pad[HDR_DIAG]) + ")";
                 ok = false;
             }
     }

@@ -103,6 +103,10 @@ float mt_last_kernel_ms(const mt_handle *h);
    out[8] = {total, spilled before a message, segments, blocks, heap, text, property
    records, at load} (the causes count LDS capacities hit inside a message). */
 int mt_last_hbm_docs(mt_handle *h, uint32_t *out);
+/* High-water marks of the paged documents of the most recent batch (or generation):
+   out[4] = {pages, unsettled-table entries, zamboni heap entries, segments}; sizing aid for
+   page_capacity / unsettled_capacity / page_heap_capacity. */
+int mt_last_paged_peaks(mt_handle *h, uint32_t *out);
 
 /* Generates ops_per_doc synthetic messages per document on the device, applying them as
    it goes (the generator reads each writer's view length from the live replica), and
