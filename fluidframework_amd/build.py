@@ -6,7 +6,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "mt_replay.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", "mt_device.h")] + [
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", "mt_device.h", "mt_paged.h")] + [
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mt_replay.h", "mt_types.h")]
 OUT = os.path.join(HERE, "libmtreplay.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

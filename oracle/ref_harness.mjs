@@ -16,8 +16,12 @@
 // Usage:
 //   node oracle/ref_harness.mjs gen  <config.json> <doc_begin> <doc_end> <out.json>
 //   node oracle/ref_harness.mjs replay <logs.json> <out.json>
+//   node oracle/ref_harness.mjs snap <config.json> <doc_begin> <doc_end> <out.json>
+//   node oracle/ref_harness.mjs loadfile <config.json> <out.json> <snapshot.json>...
 import fs from "fs";
 import * as MT from "./_ref/mt/index.mjs";
+import { SnapshotV1 } from "./_ref/mt/snapshotV1.mjs";
+import { MockStorage } from "./_ref/shims/test-runtime-utils.mjs";
 
 const { Client, TextSegment, Marker } = MT;
 
@@ -323,18 +327,193 @@ function replayDoc(log) {
     return collectOutputs(c, deltas);
 }
 
-const [mode, ...rest] = process.argv.slice(2);
-if (mode === "gen") {
-    const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
-    const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
-    const docs = [];
-    for (let d = d0; d < d1; d++) { docs.push(cfg.ext ? genDocExt(cfg, d) : genDoc(cfg, d)); }
-    fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
-} else if (mode === "replay") {
-    const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
-    const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
-    fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
-} else {
-    console.error("usage: ref_harness.mjs gen|replay ...");
-    process.exit(2);
+// ---------------------------------------------------------------- snapshots (config C5)
+// Cold catch-up = SnapshotV1 summary + tail ops (SURVEY.md S4): the observer after K ops is
+// summarised with the reference's own SnapshotV1.extractSync/emit (MT/snapshotV1.ts:87-252),
+// a fresh Client loads it through Client.load -> SnapshotLoader (MT/snapshotLoader.ts:36-228),
+// then the tail ops are generated against (and applied to) the loaded replica.
+const loaderLogger = { ...logger, shipAssert() {}, debugAssert() {} };
+
+function treeChunks(tree) {
+    // path -> contents of the merge-tree blobs (a SharedString snapshot nests them under
+    // "content"; SnapshotV1.emit puts them at the top)
+    const out = {};
+    const walk = (t) => {
+        for (const e of t.entries) {
+            if (e.type === "Blob") { out[e.path] = e.value.contents; }
+        }
+    };
+    const content = tree.entries.find((e) => e.type === "Tree" && e.path === "content");
+    walk(content ? content.value : tree);
+    return out;
 }
+
+async function loadClient(tree, options) {
+    const c = new Client(segmentFromSpec, logger, options || {});
+    const runtime = { logger: loaderLogger, clientId: "loader", options: {} };
+    const content = tree.entries.find((e) => e.type === "Tree" && e.path === "content");
+    const storage = new MockStorage(content ? content.value : tree);
+    const { catchupOpsP } = await c.load(runtime, storage);
+    const catchup = await catchupOpsP;
+    return { c, catchup };
+}
+
+function attachDeltas(c) {
+    const deltas = [];
+    c.mergeTreeDeltaCallback = (opArgs, dargs) => {
+        const mt = c.mergeTree;
+        const cw = mt.getCollabWindow();
+        const rec = [opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1,
+            dargs.operation, dargs.deltaSegments.length];
+        const segs = [];
+        for (const d of dargs.deltaSegments) {
+            const seg = d.segment;
+            const pos = seg.parent ? mt.getPosition(seg, cw.currentSeq, cw.clientId) : -1;
+            segs.push(d.propertyDeltas !== undefined ? [pos, seg.cachedLength, d.propertyDeltas]
+                : [pos, seg.cachedLength]);
+        }
+        rec.push(segs);
+        deltas.push(rec);
+    };
+    return deltas;
+}
+
+// One generated message (the generator of genDoc) against replica c at seq t.
+function genStep(rng, cfg, c, t, lastRef, cseq) {
+    const W = cfg.writers;
+    const k = 1 + rng.uniform(W);
+    let lo = Math.max(lastRef[k], t - 1 - cfg.lag);
+    if (lo < 0) { lo = 0; }
+    const r = lo + rng.uniform(t - 1 - lo + 1);
+    lastRef[k] = r;
+    let msn = Infinity;
+    for (let j = 1; j <= W; j++) { msn = Math.min(msn, lastRef[j]); }
+    const shortId = c.getOrAddShortClientId(`client-${k}`);
+    const len = c.mergeTree.getLength(r, shortId);
+    const u = rng.next();
+    let op;
+    if (len === 0 || u < frac(cfg.p_insert)) {
+        const pos = rng.uniform(len + 1);
+        const tl = 1 + rng.uniform(cfg.text_max);
+        const text = genText(rng, tl, frac(cfg.p_newline));
+        let seg = text;
+        if (cfg.p_insert_props > 0 && rng.next() < frac(cfg.p_insert_props)) {
+            seg = { text, props: genProps(rng, cfg) };
+        }
+        op = { pos1: pos, seg, type: 0 };
+    } else {
+        const p1 = rng.uniform(len);
+        let n = 1;
+        while (n < 64 && rng.next() < frac(cfg.p_len_continue)) { n++; }
+        const p2 = Math.min(p1 + n, len);
+        if (u < frac(cfg.p_insert + cfg.p_remove)) {
+            op = { pos1: p1, pos2: p2, type: 1 };
+        } else {
+            op = { pos1: p1, pos2: p2, props: genProps(rng, cfg), type: 2 };
+        }
+    }
+    return [k, t, r, msn, op, ++cseq[k]];
+}
+
+async function snapDoc(cfg, doc) {
+    const rng = new Rng(cfg.seed >>> 0, doc);
+    const seedText = genText(rng, cfg.seed_len, 0);
+    const opts = { mergeTreeSnapshotChunkSize: cfg.chunk };
+    const c = new Client(segmentFromSpec, logger, opts);
+    if (seedText.length > 0) { c.insertSegmentLocal(0, TextSegment.make(seedText)); }
+    c.startOrUpdateCollaboration("observer");
+    const W = cfg.writers;
+    const lastRef = new Array(W + 1).fill(0);
+    const cseq = new Array(W + 1).fill(0);
+    for (let t = 1; t <= cfg.ops; t++) {
+        const [k, tt, r, msn, op, cs] = genStep(rng, cfg, c, t, lastRef, cseq);
+        c.applyMsg(JSON.parse(JSON.stringify(makeMsg(k, tt, r, msn, cs, op))));
+    }
+    const snap = new SnapshotV1(c.mergeTree, logger);
+    snap.extractSync();
+    const tree = snap.emit();
+    const chunks = treeChunks(tree);
+    const rec = { doc, chunks };
+    let loaded;
+    try {
+        loaded = await loadClient(tree, {});
+    } catch (e) {
+        rec.error = String(e.message || e).split(":")[0];
+        return rec;
+    }
+    const c2 = loaded.c;
+    rec.load_out = collectOutputs(c2, []);
+    const deltas = attachDeltas(c2);
+    const tail = [];
+    for (let t = cfg.ops + 1; t <= cfg.ops + cfg.tail; t++) {
+        const [k, tt, r, msn, op, cs] = genStep(rng, cfg, c2, t, lastRef, cseq);
+        tail.push([k, tt, r, msn, op]);
+        try {
+            c2.applyMsg(JSON.parse(JSON.stringify(makeMsg(k, tt, r, msn, cs, op))));
+        } catch (e) {
+            rec.tail = tail;
+            rec.error = String(e.message || e).split(":")[0];
+            if (process.env.SNAP_DEBUG) { console.error(e.stack); }
+            return rec;
+        }
+    }
+    rec.tail = tail;
+    rec.out = collectOutputs(c2, deltas);
+    return rec;
+}
+
+// A snapshot file of the reference's own tests (SEQ/test/snapshots/*/*.json: an ITree of a
+// SharedString) loaded the same way, then a generated tail.
+async function loadFileDoc(path, cfg, doc) {
+    const tree = JSON.parse(fs.readFileSync(path, "utf8"));
+    const chunks = treeChunks(tree);
+    const rec = { doc, file: path.split("/").slice(-2).join("/"), chunks };
+    const { c, catchup } = await loadClient(tree, {});
+    rec.catchup = catchup.length;
+    rec.load_out = collectOutputs(c, []);
+    const deltas = attachDeltas(c);
+    const rng = new Rng(cfg.seed >>> 0, doc);
+    const base = c.getCurrentSeq();
+    const W = cfg.writers;
+    const lastRef = new Array(W + 1).fill(base);
+    const cseq = new Array(W + 1).fill(0);
+    const tail = [];
+    for (let t = base + 1; t <= base + cfg.tail; t++) {
+        const [k, tt, r, msn, op, cs] = genStep(rng, cfg, c, t, lastRef, cseq);
+        tail.push([k, tt, r, msn, op]);
+        c.applyMsg(JSON.parse(JSON.stringify(makeMsg(k, tt, r, msn, cs, op))));
+    }
+    rec.tail = tail;
+    rec.out = collectOutputs(c, deltas);
+    return rec;
+}
+
+const [mode, ...rest] = process.argv.slice(2);
+async function main() {
+    if (mode === "gen") {
+        const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
+        const docs = [];
+        for (let d = d0; d < d1; d++) { docs.push(cfg.ext ? genDocExt(cfg, d) : genDoc(cfg, d)); }
+        fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
+    } else if (mode === "replay") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
+        fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
+    } else if (mode === "snap") {
+        const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
+        const docs = [];
+        for (let d = d0; d < d1; d++) { docs.push(await snapDoc(cfg, d)); }
+        fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
+    } else if (mode === "loadfile") {
+        const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        const docs = [];
+        for (let i = 2; i < rest.length; i++) { docs.push(await loadFileDoc(rest[i], cfg, i - 2)); }
+        fs.writeFileSync(rest[1], JSON.stringify({ config: cfg, docs }));
+    } else {
+        console.error("usage: ref_harness.mjs gen|replay|snap|loadfile ...");
+        process.exit(2);
+    }
+}
+main().catch((e) => { console.error(e); process.exit(1); });
