@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="0 = all docs of rank 0")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
+    ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
     return ap.parse_args()
 
 
@@ -83,7 +85,12 @@ def main():
         cfg["ops"] = args.ops
     doc_base = rank * docs
 
-    mt = MergeTreeBatch(docs, device=local_rank, **capacities(cfg))
+    caps = capacities(cfg)
+    if args.lds_cap:
+        caps["lds_seg_capacity"] = args.lds_cap
+    if args.heap_cap:
+        caps["heap_capacity"] = args.heap_cap
+    mt = MergeTreeBatch(docs, device=local_rank, **caps)
     t_gen = time.time()
     batch = mt.generate(cfg, doc_base)              # untimed: inputs resident in HBM
     gen_sums = mt.checksums()

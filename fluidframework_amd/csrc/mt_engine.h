@@ -25,6 +25,7 @@
 template <bool kLogT> struct TierLdsT {
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
+    static constexpr bool kPaged = false;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS u64 *O_t;
     typedef LDS_AS v4u *B_t;
@@ -33,10 +34,23 @@ template <bool kLogT> struct TierLdsT {
 template <bool kLogT> struct TierGlbT {
     static constexpr bool kLds = false;
     static constexpr bool kLog = kLogT;
+    static constexpr bool kPaged = false;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
     typedef GLB_AS v4u *B_t;
     typedef GLB_AS v2i *H_t;
+};
+
+// The paged layout (mt_paged.h): LDS-staged window and upper levels.  kPaged compiles the
+// page bookkeeping in; the flat tiers carry none of it.
+template <bool kLogT> struct TierPagedT {
+    static constexpr bool kLds = true;
+    static constexpr bool kLog = kLogT;
+    static constexpr bool kPaged = true;
+    typedef LDS_AS v4i *A_t;
+    typedef LDS_AS u64 *O_t;
+    typedef LDS_AS v4u *B_t;
+    typedef LDS_AS v2i *H_t;
 };
 
 // Cross-lane ordering inside one wavefront.  LDS instructions of a wave execute in order,
@@ -447,7 +461,7 @@ TD int blk_prefix(DocT<T> &d, int l, int b) {
 TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
     LDS_AS uint8_t *c = lvl(d, l);
     const int nb = nbr(d, l);
-    if (d.dir && l == 1 && delta) {   // paged upper instance: page ids move with level 1
+    if (T::kPaged && d.dir && l == 1 && delta) {   // paged upper instance: page ids move with level 1
         LDS_AS uint16_t *dr = d.dir;
         if (delta > 0) {
             for (int hi = nb; hi > from; hi -= MT_WAVE) {
@@ -516,9 +530,9 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
     // paged window: level 1 is the page itself; its split (a new level-1 node) is done by
     // the paged driver after the op.  A second leaf split while it is pending is recorded:
     // it decides which half ends up with 5 blocks (reference order: split page, then leaf).
-    if (d.paged && l == 0 && d.pend_split) d.pend_second = b;
+    if (T::kPaged && d.paged && l == 0 && d.pend_split) d.pend_second = b;
     while (true) {
-        if (d.paged && l == 1) {
+        if (T::kPaged && d.paged && l == 1) {
             d.pend_split = 1;
             return;
         }
@@ -754,7 +768,9 @@ TD bool paged_text_ensure(DocT<T> &d, int need);
 TD bool paged_props_ensure(DocT<T> &d, int need);
 TD bool text_ensure(DocT<T> &d, int need) {
     if (d.text_top + need <= d.T_cap) return true;
-    if (d.paged) return paged_text_ensure(d, need);
+    if constexpr (T::kPaged) {
+        if (d.paged) return paged_text_ensure(d, need);
+    }
     text_gc(d);
     if (d.status) return false;
     if (d.text_top + need <= d.T_cap) return true;
@@ -792,7 +808,9 @@ TD void props_gc(DocT<T> &d) {
 }
 TD bool props_ensure(DocT<T> &d, int need) {
     if (d.props_top + need <= d.P_cap) return true;
-    if (d.paged) return paged_props_ensure(d, need);
+    if constexpr (T::kPaged) {
+        if (d.paged) return paged_props_ensure(d, need);
+    }
     props_gc(d);
     if (d.status) return false;
     if (d.props_top + need <= d.P_cap) return true;
@@ -1629,7 +1647,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     if (seq > d.min_seq) add_to_lru_block(d, lb, uid, seq);  // saveIfLocal :2197-2212
     if (d.status) return;
     // delta callback: position of the new segment in the observer view
-    const int pos = d.obs_base + obs_prefix(d, x);
+    const int pos = (T::kPaged ? d.obs_base : 0) + obs_prefix(d, x);
     cb.n = 1;
     cb_log(d, pos);
     cb_log(d, slen);

@@ -789,8 +789,8 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
             return nullptr;
         }
         if (lb > 64 * 1024) {
-            const void *ks[] = {(const void *)k_replay_paged<TierLdsT<true>>, (const void *)k_replay_paged<TierLdsT<false>>,
-                                (const void *)k_generate_paged<TierLdsT<false>>};
+            const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true>>, (const void *)k_replay_paged<TierPagedT<false>>,
+                                (const void *)k_generate_paged<TierPagedT<false>>};
             for (const void *k : ks)
                 if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess) {
                     delete h;
@@ -944,10 +944,10 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         const size_t lb = paged_layout(h->st.PP, h->st.PH, h->st.UT, 0).total;
         const int use_resume = h->lds.S > 0 ? 1 : 0;
         if (h->st.DL)
-            hipLaunchKernelGGL(k_replay_paged<TierLdsT<true>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+            hipLaunchKernelGGL(k_replay_paged<TierPagedT<true>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
                                b->ops, b->off, b->text, b->props, use_resume);
         else
-            hipLaunchKernelGGL(k_replay_paged<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+            hipLaunchKernelGGL(k_replay_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
                                b->ops, b->off, b->text, b->props, use_resume);
     } else if (h->st.DL)
         hipLaunchKernelGGL(k_replay<TierGlbT<true>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
@@ -1057,7 +1057,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
         }
         if (ok && h->st.PP > 0) {
             const size_t lb = paged_layout(h->st.PP, h->st.PH, h->st.UT, gw).total;
-            hipLaunchKernelGGL(k_generate_paged<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
+            hipLaunchKernelGGL(k_generate_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
                                h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride, pstride, d_fail,
                                d_trace);
             ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;

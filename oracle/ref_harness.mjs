@@ -429,6 +429,16 @@ async function snapDoc(cfg, doc) {
         const [k, tt, r, msn, op, cs] = genStep(rng, cfg, c, t, lastRef, cseq);
         c.applyMsg(JSON.parse(JSON.stringify(makeMsg(k, tt, r, msn, cs, op))));
     }
+    let t0 = cfg.ops;
+    if (cfg.settle === true || (cfg.settle === "alternate" && doc % 2 === 0)) {
+        // every writer caught up: a non-op message moves minSeq to the current seq, so the
+        // summary holds no merge info (MT/snapshotV1.ts:196-215)
+        t0 += 1;
+        for (let j = 1; j <= W; j++) { lastRef[j] = t0; }
+        const m = makeMsg(1, t0, t0 - 1, t0, ++cseq[1], null);
+        m.type = "noop";
+        c.applyMsg(m);
+    }
     const snap = new SnapshotV1(c.mergeTree, logger);
     snap.extractSync();
     const tree = snap.emit();
@@ -445,7 +455,7 @@ async function snapDoc(cfg, doc) {
     rec.load_out = collectOutputs(c2, []);
     const deltas = attachDeltas(c2);
     const tail = [];
-    for (let t = cfg.ops + 1; t <= cfg.ops + cfg.tail; t++) {
+    for (let t = t0 + 1; t <= t0 + cfg.tail; t++) {
         const [k, tt, r, msn, op, cs] = genStep(rng, cfg, c2, t, lastRef, cseq);
         tail.push([k, tt, r, msn, op]);
         try {
