@@ -84,9 +84,9 @@ class Interner:
 class DocEncoder:
     """Encodes one document's messages; arenas are shared by a Batch."""
 
-    def __init__(self, batch):
+    def __init__(self, batch, short=None):
         self.batch = batch
-        self.short = {}
+        self.short = dict(short) if short else {}
 
     def client(self, long_id):
         s = self.short.get(long_id)
@@ -162,8 +162,10 @@ class Batch:
             raise ValueError(f"unsupported op type {t}")
         self.recs.append(base)
 
-    def add_doc(self, seed_text, msgs):
-        enc = DocEncoder(self)
+    def add_doc(self, seed_text, msgs, clients=None):
+        """clients: long id -> short id already known for this document (a loaded summary's
+        writers, snapshot.SnapshotBatch.clients); new ids continue after them."""
+        enc = DocEncoder(self, clients)
         s = seed_text.encode("utf-16-le")
         self.seed.extend(np.frombuffer(s, dtype="<u2").tolist())
         self.seed_off.append(len(self.seed))

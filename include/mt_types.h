@@ -26,12 +26,18 @@ enum mt_op_kind {
     MT_OP_INSERT = 0,     /* MergeTreeDeltaType.INSERT   MT/ops.ts:30 */
     MT_OP_REMOVE = 1,     /* MergeTreeDeltaType.REMOVE   MT/ops.ts:31 */
     MT_OP_ANNOTATE = 2,   /* MergeTreeDeltaType.ANNOTATE MT/ops.ts:32 */
-    MT_OP_NOOP = 3        /* non-"op" message: seq/msn update only */
+    MT_OP_NOOP = 3,       /* non-"op" message: seq/msn update only */
+    MT_OP_LOAD_REMOVED = 4 /* internal (summary load): removal info of the segment the
+                              preceding MT_F_LOAD insert appended */
 };
 
 enum mt_op_flags {
     MT_F_GROUP_MORE = 1,  /* another member of the same GROUP message follows */
-    MT_F_MARKER = 2       /* insert of a Marker (length 1); payload = refType */
+    MT_F_MARKER = 2,      /* insert of a Marker (length 1); payload = refType */
+    MT_F_LOAD = 4         /* internal (summary load): a body segment appended by
+                             SnapshotLoader.loadBody (MT/snapshotLoader.ts:195-227) --
+                             insertSegments with opArgs undefined: no delta callback, no
+                             seq/msn update */
 };
 
 #define MT_NO_PROPS 0xFFFFFFFFu      /* props field: no property set */
@@ -55,6 +61,22 @@ typedef struct mt_op_rec {
     uint8_t kind;       /* enum mt_op_kind */
     uint8_t flags;      /* enum mt_op_flags */
 } mt_op_rec;
+
+/* One segment of a decoded SnapshotV1 summary (SnapshotLoader.specToSegment,
+   MT/snapshotLoader.ts:86-118): header segments first, then body segments, per document.
+   A spec without merge info has seq 0 (UniversalSequenceNumber) and client -2
+   (NonCollabClient). */
+typedef struct mt_seg_rec {
+    int32_t len;            /* UTF-16 units (Marker: 1) */
+    int32_t seq;            /* spec.seq, default 0 */
+    int32_t removed_seq;    /* spec.removedSeq, INT32_MIN when undefined */
+    uint32_t payload;       /* text arena offset (UTF-16 units); Marker: refType */
+    uint32_t props;         /* props record [count, (key, value) x count] or MT_NO_PROPS */
+    int16_t client;         /* short id of spec.client, or -2 */
+    int16_t removed_client; /* short id of spec.removedClient (when removed_seq is set) */
+    uint8_t flags;          /* MT_F_MARKER */
+    uint8_t pad[7];
+} mt_seg_rec;
 
 /* Per-document verification checksum: all-gathered across ranks. */
 typedef struct mt_checksum {

@@ -786,6 +786,109 @@ int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
     return d->status;
 }
 
+/* ------------------------------------------------------------------ summary load (C5) */
+/* SnapshotLoader.specToSegment MT/snapshotLoader.ts:86-118 (the host resolved client ids) */
+static Seg *seg_from_rec(orc_doc *d, const mt_seg_rec *r, const uint16_t *text_arena,
+                         const uint32_t *props_arena) {
+    Seg *s;
+    if (r->flags & MT_F_MARKER) {
+        s = make_text_seg(d, NULL, 0);
+        s->marker = (int32_t)r->payload;
+        s->len = 1;
+    } else {
+        s = make_text_seg(d, text_arena + r->payload, r->len);
+    }
+    if (r->props != MT_NO_PROPS) {          /* TextSegment.make(text, props): nulls dropped */
+        const uint32_t *rec = props_arena + r->props;
+        uint32_t count = rec[0] & 0xFFFF;
+        s->props = props_new(d);
+        for (uint32_t j = 0; j < count; j++)
+            if (rec[2 + 2 * j] != MT_VAL_NULL) props_set(d, s->props, rec[1 + 2 * j], rec[2 + 2 * j]);
+    }
+    s->seq = r->seq;
+    s->client = r->client;
+    if (r->removed_seq != RSEQ_NONE) {
+        s->rseq = r->removed_seq;
+        s->rclient = r->removed_client;
+    }
+    return s;
+}
+
+/* reloadFromSegments :1229-1284: blocks of MaxNodesInBlock - 1 children, bottom-up */
+static Block *build_merge_block(orc_doc *d, Node **nodes, int n) {
+    const int max_children = MAXN - 1;
+    const int nb = (n + max_children - 1) / max_children;
+    Node **blocks = (Node **)malloc(sizeof(Node *) * (nb > 0 ? nb : 1));
+    for (int bi = 0, ni = 0; bi < nb; bi++) {
+        Block *b = make_block(d, 0);
+        for (int ci = 0; ci < max_children && ni < n; ci++, ni++) {
+            assign_child(b, nodes[ni], ci);
+            b->count++;
+        }
+        blocks[bi] = &b->n;
+    }
+    Block *root = nb == 1 ? (Block *)blocks[0] : build_merge_block(d, blocks, nb);
+    free(blocks);
+    return root;
+}
+
+/* loadBody's append helper :197-205: insertSegments(root.cachedLength, segs, refSeq 0,
+   cli, seq, opArgs undefined) -- insertSegments :2001-2031 with blockInsert :2174-2257 */
+static int load_append(orc_doc *d, Seg **segs, int n, int32_t cli, int32_t seq) {
+    const int32_t pos = orc_length(d);
+    ensure_boundary(d, pos, 0, cli);
+    int32_t ins = pos;
+    for (int i = 0; i < n; i++) {
+        Seg *s = segs[i];
+        if (s->len <= 0) continue;
+        s->seq = seq;
+        s->client = cli;
+        Block *sn = inserting_walk(d, d->root, ins, 0, cli, WALK_INSERT, s);
+        if (s->n.parent == NULL) return d->status = MT_DOC_INSERT_FAILED;
+        update_root(d, sn);
+        if (seq > d->min_seq) add_to_lru(d, s, seq);   /* saveIfLocal :2197-2212 */
+        ins += s->len;
+    }
+    zamboni(d);                                         /* collaborating :2027-2030 */
+    return 0;
+}
+
+/* Client.load -> SnapshotLoader.initialize (MT/snapshotLoader.ts:36-228) for one decoded
+   summary: loadHeader (reloadFromSegments + startOrUpdateCollaboration(minSeq, seq)), then
+   loadBody (plain below-MSN specs appended in batches, the others one by one). */
+orc_doc *orc_load(const mt_seg_rec *recs, int32_t n_header, int32_t n_total, const uint16_t *text_arena,
+                  const uint32_t *props_arena, int32_t min_seq, int32_t cur_seq) {
+    orc_doc *d = (orc_doc *)calloc(1, sizeof(orc_doc));
+    d->delta_hash = FNV_OFF;
+    if (n_header > 0) {
+        Node **nodes = (Node **)malloc(sizeof(Node *) * n_header);
+        for (int i = 0; i < n_header; i++) nodes[i] = &seg_from_rec(d, &recs[i], text_arena, props_arena)->n;
+        d->root = build_merge_block(d, nodes, n_header);
+        free(nodes);
+    } else {
+        d->root = make_block(d, 0);
+    }
+    d->root->n.parent = NULL;
+    d->min_seq = min_seq;                   /* startCollaboration :1287-1304 */
+    d->current_seq = cur_seq;
+    int nb = n_total - n_header;
+    Seg **batch = (Seg **)malloc(sizeof(Seg *) * (nb > 0 ? nb : 1));
+    int nbatch = 0;
+    for (int i = n_header; i < n_total && !d->status; i++) {
+        Seg *s = seg_from_rec(d, &recs[i], text_arena, props_arena);
+        if (s->client == -2 && s->seq == 0) {
+            batch[nbatch++] = s;
+        } else {
+            if (nbatch) load_append(d, batch, nbatch, -2, 0);
+            nbatch = 0;
+            if (!d->status) load_append(d, &s, 1, s->client, s->seq);
+        }
+    }
+    if (nbatch && !d->status) load_append(d, batch, nbatch, -2, 0);
+    free(batch);
+    return d;
+}
+
 /* ------------------------------------------------------------------ lifecycle / output */
 orc_doc *orc_new(const uint16_t *seed_text, int32_t seed_len) {
     orc_doc *d = (orc_doc *)calloc(1, sizeof(orc_doc));

@@ -25,6 +25,9 @@ typedef struct orc_gen_cfg {
 
 orc_doc *orc_new(const uint16_t *seed_text, int32_t seed_len);
 void orc_free(orc_doc *d);
+/* Load a decoded SnapshotV1 summary (header records first, then body records). */
+orc_doc *orc_load(const mt_seg_rec *recs, int32_t n_header, int32_t n_total, const uint16_t *text_arena,
+                  const uint32_t *props_arena, int32_t min_seq, int32_t cur_seq);
 /* Apply one record; returns mt_doc_status.  Once a doc has failed it stays failed. */
 int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
                   const uint32_t *props_arena);

@@ -63,6 +63,8 @@ def lib():
         L.orc_generate.restype = i32
         L.orc_replay_batch.argtypes = [i32, P, P, P, P, P, P, P, P, i32]
         L.orc_replay_batch.restype = i32
+        L.orc_load.restype = P
+        L.orc_load.argtypes = [P, i32, i32, P, P, i32, i32]
         _lib = L
     return _lib
 
@@ -91,6 +93,16 @@ class OracleDoc:
     def new(cls, seed):
         seed = np.ascontiguousarray(seed, dtype=np.uint16)
         d = cls(lib().orc_new(_p(seed), len(seed)))
+        lib().orc_set_record_deltas(d.h, 1)
+        return d
+
+    @classmethod
+    def load(cls, segs, n_header, text, props, min_seq, cur_seq):
+        """A replica loaded from a decoded summary (orc_load = Client.load, MT/snapshotLoader.ts)."""
+        segs = np.ascontiguousarray(segs)
+        text = np.ascontiguousarray(text, dtype=np.uint16)
+        props = np.ascontiguousarray(props, dtype=np.uint32)
+        d = cls(lib().orc_load(_p(segs), int(n_header), len(segs), _p(text), _p(props), int(min_seq), int(cur_seq)))
         lib().orc_set_record_deltas(d.h, 1)
         return d
 

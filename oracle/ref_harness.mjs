@@ -149,7 +149,8 @@ function collectOutputs(c, deltas) {
             rcli: seg.removedClientId === undefined ? null : seg.removedClientId,
             ovl: seg.removedClientOverlap ? [...seg.removedClientOverlap] : [],
             marker: Marker.is(seg) ? seg.refType : null,
-            props: seg.properties === undefined ? null : seg.properties,
+            // copied now: a later annotate mutates the live object (outputs taken mid-run)
+            props: seg.properties === undefined ? null : JSON.parse(JSON.stringify(seg.properties)),
         };
         segs.push(rec);
         if (seg.removedSeq === undefined) {
@@ -452,6 +453,7 @@ async function snapDoc(cfg, doc) {
         return rec;
     }
     const c2 = loaded.c;
+    rec.observer = c2.getShortClientId("loader");
     rec.load_out = collectOutputs(c2, []);
     const deltas = attachDeltas(c2);
     const tail = [];
@@ -480,6 +482,7 @@ async function loadFileDoc(path, cfg, doc) {
     const rec = { doc, file: path.split("/").slice(-2).join("/"), chunks };
     const { c, catchup } = await loadClient(tree, {});
     rec.catchup = catchup.length;
+    rec.observer = c.getShortClientId("loader");
     rec.load_out = collectOutputs(c, []);
     const deltas = attachDeltas(c);
     const rng = new Rng(cfg.seed >>> 0, doc);

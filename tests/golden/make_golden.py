@@ -7,7 +7,7 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py
+    python3 tests/golden/make_golden.py [--snapshots]
 """
 import gzip
 import json
@@ -37,9 +37,64 @@ FIXTURES = {
                             "p_group": 0.05, "p_noop": 0.02, "p_empty": 0.01, "p_oob": 0.02}, 3),
 }
 
+# Cold catch-up (config C5): observer after `ops` messages -> SnapshotV1 summary
+# (chunkSize `chunk`) -> fresh Client.load -> `tail` generated messages (harness "snap").
+# settle: every writer caught up before the summary (no merge info); "alternate" = even docs.
+SNAP_BASE = {"seed": 5150, "writers": 4, "lag": 32, "seed_len": 64, "p_insert": 0.5, "p_remove": 0.3,
+             "text_max": 8, "p_newline": 0.02, "p_len_continue": 0.75, "p_insert_props": 0.2, "n_keys": 8,
+             "n_values": 16, "p_null": 0.1, "max_keys_per_op": 2}
+SNAP_FIXTURES = {
+    # header-only summaries (2-8 KB documents fit one 10000-unit chunk), 64-op tails as in C5
+    "ref_snap": (dict(SNAP_BASE, ops=500, tail=64, chunk=10000, settle="alternate"), 16),
+    # header + body chunks: settled documents load; unsettled ones hit SURVEY Q6 (the body
+    # append resolves root.cachedLength in view (NonCollabClient, 0): "insert failed")
+    "ref_snap_body": (dict(SNAP_BASE, seed=5151, writers=3, ops=300, tail=64, chunk=150, settle="alternate"), 16),
+}
+# The reference's own summary fixtures (SEQ/test/snapshots, data files of its tests),
+# loaded and followed by a generated tail (harness "loadfile").
+SNAP_FILES = ["v1/headerOnly", "v1/headerAndBody", "v1/largeBody", "v1/withMarkers", "v1/withAnnotations",
+              "legacy/headerOnly", "legacy/withAnnotations", "legacyWithCatchUp/headerAndBody"]
+SNAP_FILE_CFG = dict(SNAP_BASE, seed=5152, tail=40)
+SNAP_DIR = "/root/reference/packages/dds/sequence/src/test/snapshots"
+
+
+def _dump(name, data):
+    with gzip.open(os.path.join(HERE, name + ".json.gz"), "wt") as fh:
+        json.dump(data, fh, separators=(",", ":"))
+
+
+def make_snapshot_fixtures():
+    for name, (cfg, ndocs) in SNAP_FIXTURES.items():
+        with tempfile.TemporaryDirectory() as td:
+            cp, op = os.path.join(td, "cfg.json"), os.path.join(td, "out.json")
+            json.dump(cfg, open(cp, "w"))
+            subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "snap", cp, "0",
+                                   str(ndocs), op])
+            data = json.load(open(op))
+        for d in data["docs"]:
+            for k in ("out", "load_out"):
+                if k in d:
+                    d[k].pop("tree", None)
+        _dump(name, data)
+        print(name, ndocs, "docs", sum("error" in d for d in data["docs"]), "reference errors")
+    with tempfile.TemporaryDirectory() as td:
+        cp, op = os.path.join(td, "cfg.json"), os.path.join(td, "out.json")
+        json.dump(SNAP_FILE_CFG, open(cp, "w"))
+        files = [os.path.join(SNAP_DIR, f + ".json") for f in SNAP_FILES]
+        subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "loadfile", cp, op] + files)
+        data = json.load(open(op))
+    for d in data["docs"]:
+        for k in ("out", "load_out"):
+            d[k].pop("tree", None)
+    _dump("ref_snap_files", data)
+    print("ref_snap_files", len(data["docs"]), "docs")
+
 
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
+    if "--snapshots" in sys.argv[1:]:
+        make_snapshot_fixtures()
+        return
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
     for name, (base, over, ndocs) in FIXTURES.items():
         cfg = dict(configs[base]) if base else {}
@@ -57,6 +112,7 @@ def main():
         with gzip.open(os.path.join(HERE, name + ".json.gz"), "wt") as fh:
             json.dump(data, fh, separators=(",", ":"))
         print(name, ndocs, "docs")
+    make_snapshot_fixtures()
 
 
 if __name__ == "__main__":

@@ -7,11 +7,13 @@ import os
 
 import numpy as np
 
+from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks
 from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INT_MIN = -2 ** 31
 ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long"]
+SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
 
 
 def load(name):
@@ -76,3 +78,44 @@ def compare_oracle(o, exp):
     if o["deltas"] != exp["deltas"]:
         errs.append("deltas")
     return errs
+
+
+# ---------------------------------------------------------------- summaries (config C5)
+def encode_snap_docs(fixture, interner, docs=None):
+    """(load arrays for mt_load_snapshots / orc_load, op arrays of the catch-up + tail
+    messages) for snapshot fixtures (tests/golden/make_golden.py SNAP_*)."""
+    sb, b = SnapshotBatch(interner), Batch(interner)
+    for d in (fixture["docs"] if docs is None else docs):
+        snap = decode_chunks(d["chunks"])
+        clients = sb.add_doc(snap)
+        b.add_doc("", list(snap.catchup) + compact_msgs_to_dicts(d.get("tail", [])), clients=clients)
+    return sb.arrays(), b.arrays()
+
+
+def snap_status(doc):
+    """Expected document status: 0, MT_DOC_INSERT_FAILED for the reference's load failure
+    (SURVEY Q6), None when the reference threw something the engine does not model."""
+    err = doc.get("error")
+    if err is None:
+        return 0
+    if err.startswith("MergeTree insert failed"):
+        return 1
+    return None
+
+
+def expected_snap(doc, interner, key="out"):
+    """expected() for a loaded replica: the reference numbers the loading client after the
+    header's writers (specToSegment runs before startOrUpdateCollaboration); the engine
+    numbers it 0 and keeps first-seen order for the others."""
+    obs = doc["observer"]
+
+    def remap(r):
+        if r is None or r < 0:
+            return r
+        return 0 if r == obs else (r + 1 if r < obs else r)
+
+    out = json.loads(json.dumps(doc[key]))
+    for r in out["segs"]:
+        r["cli"] = remap(r["cli"])
+        r["rcli"] = remap(r["rcli"])
+    return expected(dict(out=out), interner)
