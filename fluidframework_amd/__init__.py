@@ -70,6 +70,23 @@ class MergeTreeBatch:
                                           _native.ptr(text), len(text), _native.ptr(props), len(props)),
                     "mt_apply_ops")
 
+    def load_snapshots(self, la):
+        """Client.load of a decoded SnapshotV1 summary into every document
+        (snapshot.SnapshotBatch.arrays(); MT/snapshotLoader.ts:36-228)."""
+        from .snapshot import SEG_DTYPE
+        segs = np.ascontiguousarray(la["segs"], dtype=SEG_DTYPE)
+        off = np.ascontiguousarray(la["doc_off"], dtype=np.int64)
+        nh = np.ascontiguousarray(la["n_header"], dtype=np.int32)
+        text = np.ascontiguousarray(la["text"], dtype=np.uint16)
+        props = np.ascontiguousarray(la["props"], dtype=np.uint32)
+        mn = np.ascontiguousarray(la["min_seq"], dtype=np.int32)
+        cu = np.ascontiguousarray(la["cur_seq"], dtype=np.int32)
+        if len(off) != self.n_docs + 1:
+            raise ValueError("one summary per document")
+        self._check(self.lib.mt_load_snapshots(self.h, _native.ptr(off), _native.ptr(nh), _native.ptr(segs), len(segs),
+                                               _native.ptr(text), len(text), _native.ptr(props), len(props),
+                                               _native.ptr(mn), _native.ptr(cu)), "mt_load_snapshots")
+
     def upload(self, a):
         return DeviceBatch(self, a)
 

@@ -1500,6 +1500,9 @@ struct OpIn {
     bool nl;
 };
 
+// writer short id (sign-extended: loaded summaries append as NonCollabClient = -2)
+__device__ __forceinline__ int op_cli(const mt_op_rec &op) { return (int)(int16_t)op.client; }
+
 __device__ __forceinline__ uint16_t pay_unit(const OpIn &in, int j) {
     const u64 w = j < 4 ? (in.pay_lo >> (16 * j)) : (in.pay_hi >> (16 * (j - 4)));
     return (uint16_t)(w & 0xFFFF);
@@ -1519,7 +1522,8 @@ TD void op_insert_impl(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, c
 TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
 #endif
     const mt_op_rec &op = in.op;
-    const int r = op.ref_seq, c = op.client, seq = op.seq, p = op.pos1;
+    const int r = op.ref_seq, c = op_cli(op), seq = op.seq, p = op.pos1;
+    const bool quiet = (op.flags & MT_F_LOAD) != 0;   // SnapshotLoader.loadBody append
     const bool marker = (op.flags & MT_F_MARKER) != 0;
     const int slen = marker ? 1 : op.pos2;
     // arena room first (a compaction changes no structure, so doing it before the boundary
@@ -1561,8 +1565,10 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     } else if (ip < 0 && carry == p) {
         ip = d.n;
     }
-    Cb cb = cb_begin(d, seq, MT_OP_INSERT);
+    Cb cb;
+    if (!quiet) cb = cb_begin(d, seq, MT_OP_INSERT);
     if (slen == 0) {  // zero-length segment: boundary only, not inserted (:2229)
+        if (quiet) return;
         cb.n = 1;
         cb_log(d, -1);
         cb_log(d, 0);
@@ -1646,6 +1652,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     }
     if (seq > d.min_seq) add_to_lru_block(d, lb, uid, seq);  // saveIfLocal :2197-2212
     if (d.status) return;
+    if (quiet) return;   // insertSegments with opArgs undefined fires no callback (:2013-2021)
     // delta callback: position of the new segment in the observer view
     const int pos = (T::kPaged ? d.obs_base : 0) + obs_prefix(d, x);
     cb.n = 1;
@@ -1740,7 +1747,7 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
 // Returns true when the range ended inside d (or on failure: check d.status).
 TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, int &carry, int &ocarry,
                    Cb &cb) {
-    const int r = op.ref_seq, c = op.client, seq = op.seq, p1 = op.pos1, p2 = op.pos2;
+    const int r = op.ref_seq, c = op_cli(op), seq = op.seq, p1 = op.pos1, p2 = op.pos2;
     const bool rem = op.kind == MT_OP_REMOVE;
     compute_ends(d);
     if (!rem) gsync_rd();   // property records written earlier in this launch are read below
@@ -1857,7 +1864,7 @@ TD void op_range_impl(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pi
 #else
 TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
 #endif
-    const int r = op.ref_seq, c = op.client, seq = op.seq, p1 = op.pos1, p2 = op.pos2;
+    const int r = op.ref_seq, c = op_cli(op), seq = op.seq, p1 = op.pos1, p2 = op.pos2;
     const bool rem = op.kind == MT_OP_REMOVE;
     const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
     if (rec && (rec[0] >> 16) == MT_COMBINE_OTHER) {
@@ -1882,8 +1889,37 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
 // asserts (:451-479), then updateSeqNumbers -> setMinSeq (:821-828, 991-1004,
 // MT/mergeTree.ts:1751-1769) whose zamboni runs when minSeq advances.  Both zamboni passes
 // share one call site so the (large) zamboni/scour/pack code is inlined once.
+// Summary load: the removal info of the body segment the preceding MT_F_LOAD insert
+// appended (specToSegment sets removedSeq/removedClientId before insertion,
+// MT/snapshotLoader.ts:102-107; the segment's own insertion walk never reads them).
+TD void load_removed(DocT<T> &d, const mt_op_rec &op) {
+    const int i = find_uid(d, (uint32_t)(d.next_uid - 1));
+    if (i < 0) {
+        FAIL_INTERNAL(d);
+        return;
+    }
+    if (lane() == 0) {
+        v4i a = d.A[i];
+        a.z = op.seq;
+        a.w = pack_cli(seg_cli(a), op_cli(op));
+        d.A[i] = a;
+    }
+    wsync<T>();
+}
+
 TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     const mt_op_rec &op = in.op;
+    if (op.flags & MT_F_LOAD) {
+        // SnapshotLoader.loadBody (MT/snapshotLoader.ts:195-227): insertSegments at
+        // root.cachedLength in view (client, refSeq 0), no callback, no seq/msn update.  Its
+        // zamboniSegments has nothing to do: the heap is new (startCollaboration) and body
+        // segments are never newer than currentSeq (addToLRUSet :1312).
+        if (op.kind == MT_OP_INSERT)
+            op_insert(d, in, tin, pin);
+        else if (op.kind == MT_OP_LOAD_REMOVED)
+            load_removed(d, op);
+        return;
+    }
     const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
     if (op.kind == MT_OP_INSERT) {
         op_insert(d, in, tin, pin);

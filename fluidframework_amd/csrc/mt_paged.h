@@ -665,11 +665,12 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
     const int slen = (op.flags & MT_F_MARKER) ? 1 : op.pos2;
-    pg_views(pd, op.ref_seq, op.client);
+    pg_views(pd, op.ref_seq, op_cli(op));
     int start;
     const int pos = pg_find(pd, op.pos1, false, start);
     if (pos < 0) {
         if (slen == 0) {   // boundary only; nothing splits past the end
+            if (op.flags & MT_F_LOAD) return;
             Cb cb = cb_begin(w, op.seq, MT_OP_INSERT);
             cb.n = 1;
             cb_log(w, -1);
@@ -702,7 +703,7 @@ TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
 
 TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
     DocT<T> &w = pd.w;
-    const int r = op.ref_seq, c = op.client, p1 = op.pos1, p2 = op.pos2;
+    const int r = op.ref_seq, c = op_cli(op), p1 = op.pos1, p2 = op.pos2;
     const bool rem = op.kind == MT_OP_REMOVE;
     const GLB_AS uint32_t *rec = (!rem && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
     if (rec && (rec[0] >> 16) == MT_COMBINE_OTHER) {
@@ -742,9 +743,42 @@ TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin,
     pg_apply_op_impl(pd, in, tin, pin);
     PG_T1(15)
 }
+// load_removed for a paged document: the appended segment is in the window, or (after a
+// page split) in the page the uid map names.
+TD void pg_load_removed(PagedDoc<T> &pd, const mt_op_rec &op) {
+    DocT<T> &w = pd.w;
+    const uint32_t uid = (uint32_t)(w.next_uid - 1);
+    int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
+    if (i < 0) {
+        const int pg = uid < (uint32_t)pd.UM ? uni(pd.gumap[uid]) : -1;
+        if (pg < 0 || pg >= pd.PP) {
+            FAIL_INTERNAL(w);
+            return;
+        }
+        pg_win_flush(pd);
+        if (w.status) return;
+        pg_win_load(pd, pg);
+        i = find_uid(w, uid);
+        if (i < 0) {
+            FAIL_INTERNAL(w);
+            return;
+        }
+    }
+    load_removed(w, op);
+    if (w.status) return;
+    pg_win_sync(pd);
+}
+
 TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
+    if (op.flags & MT_F_LOAD) {   // summary body append (apply_op)
+        if (op.kind == MT_OP_INSERT)
+            pg_op_insert(pd, in, tin, pin);
+        else if (op.kind == MT_OP_LOAD_REMOVED)
+            pg_load_removed(pd, op);
+        return;
+    }
     const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
     if (op.kind == MT_OP_INSERT) {
         pg_op_insert(pd, in, tin, pin);

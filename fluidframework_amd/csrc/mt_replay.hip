@@ -51,6 +51,122 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
     }
 }
 
+// ---------------------------------------------------------------- summary load (config C5)
+// Client.load -> SnapshotLoader.loadHeader (MT/snapshotLoader.ts:120-159): the header's
+// segments become the leaves of a tree built bottom-up in blocks of MaxNodesInBlock - 1 = 7
+// (reloadFromSegments MT/mergeTree.ts:1229-1284; new blocks: needsScour undefined), then
+// startOrUpdateCollaboration(minSeq, seq) (MT/mergeTree.ts:1287-1304: fresh zamboni heap).
+// Body segments are appended afterwards by replaying MT_F_LOAD records (mt_load_snapshots).
+#define MT_LOAD_FANOUT (MT_MAXN - 1)
+__global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int64_t *off, const int32_t *nh,
+                                                         const mt_seg_rec *segs, const uint16_t *tin,
+                                                         const uint32_t *pin, const int32_t *min_seq,
+                                                         const int32_t *cur_seq) {
+    const int doc = blockIdx.x;
+    if (doc >= st.n_docs) return;
+    const int n = nh[doc];
+    const mt_seg_rec *rs = segs + off[doc];
+    const size_t S = st.S, B = st.B;
+    uint16_t *text = st.text + (size_t)doc * 2 * st.T;
+    uint32_t *props = st.props + (size_t)doc * 2 * st.P * MT_PREC;
+    int status = n > st.S ? MT_DOC_CAPACITY : 0;
+    const int nb0 = n > 0 ? (n + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT : 1;
+    if (nb0 > st.B) status = MT_DOC_CAPACITY;
+    int ttop = 0, ptop = 1;
+    for (int base = 0; base < n && status == 0; base += MT_WAVE) {
+        const int i = base + lane();
+        const bool v = i < n;
+        mt_seg_rec r;
+        memset(&r, 0, sizeof(r));
+        if (v) r = rs[i];
+        const bool marker = (r.flags & MT_F_MARKER) != 0;
+        const int tl = v && !marker ? r.len : 0;
+        const int hp = v && r.props != MT_NO_PROPS ? 1 : 0;
+        const int tinc = wave_scan_incl(tl), pinc = wave_scan_incl(hp);
+        const int toff = ttop + tinc - tl, ph = ptop + pinc - hp;
+        const int tend = ttop + bcast(tinc, MT_WAVE - 1), pend = ptop + bcast(pinc, MT_WAVE - 1);
+        if (tend > st.T || pend > st.P) {
+            status = MT_DOC_CAPACITY;
+            break;
+        }
+        bool bad = false;
+        if (hp) {   // TextSegment.make / Marker.make(props): keys with null dropped (Q5)
+            const uint32_t *rec = pin + r.props;
+            const uint32_t cnt = rec[0] & 0xFFFF;
+            uint32_t *t = props + (size_t)ph * MT_PREC;
+            uint32_t k = 0;
+            for (uint32_t j = 0; j < cnt; j++) {
+                if (rec[2 + 2 * j] == MT_VAL_NULL) continue;
+                if (k >= MT_KMAX) {
+                    bad = true;
+                    break;
+                }
+                t[1 + 2 * k] = rec[1 + 2 * j];
+                t[2 + 2 * k] = rec[2 + 2 * j];
+                k++;
+            }
+            t[0] = k;
+        }
+        if (ballot(bad)) {
+            status = MT_DOC_CAPACITY;
+            break;
+        }
+        // text: one wave-wide copy per segment of this chunk
+        for (u64 m = ballot(tl > 0); m; m &= m - 1) {
+            const int j = first_lane(m);
+            const int lj = bcast(tl, j), oj = bcast(toff, j);
+            const uint32_t sj = (uint32_t)bcast((int)r.payload, j);
+            for (int q = lane(); q < lj; q += MT_WAVE) text[oj + q] = tin[sj + q];
+        }
+        if (v) {
+            const bool rem = r.removed_seq != MT_RSEQ_NONE;
+            uint32_t w = 0;
+            if (tl > 0) w = SEGF_NL_KNOWN | (tin[r.payload + tl - 1] == '\n' ? SEGF_NL : 0u);
+            st.segA[doc * S + i] = v4i{r.len, r.seq, r.removed_seq, pack_cli(r.client, rem ? r.removed_client : 0)};
+            st.segO[doc * S + i] = 0ull;
+            st.segB[doc * S + i] = v4u{marker ? r.payload : (uint32_t)toff, hp ? (uint32_t)ph : 0u,
+                                       (uint32_t)(i + 1) | (marker ? MT_MARKER_BIT : 0u), w};
+        }
+        ttop = tend;
+        ptop = pend;
+    }
+    // block counts, level by level (blocks of 7, the last one takes the rest)
+    int nbl[MT_LV];
+    int depth = 0, cnt_below = n > 0 ? n : 0, nl = nb0;
+    uint8_t *cnt = st.cnt + (size_t)doc * MT_LV * B;
+    for (int l = 0; l < MT_LV; l++) nbl[l] = 0;
+    while (status == 0) {
+        if (depth >= MT_LV) {
+            status = MT_DOC_CAPACITY;
+            break;
+        }
+        for (int b = lane(); b < nl; b += MT_WAVE)
+            cnt[depth * B + b] = (uint8_t)min(MT_LOAD_FANOUT, cnt_below - MT_LOAD_FANOUT * b);
+        nbl[depth] = nl;
+        depth++;
+        if (nl == 1) break;
+        cnt_below = nl;
+        nl = (nl + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT;
+    }
+    for (int b = lane(); b < nb0 && b < st.B; b += MT_WAVE) st.flg[doc * B + b] = MT_SCOUR_UNDEF;
+    if (lane() == 0) {
+        DocHdr h;
+        memset(&h, 0, sizeof(h));
+        h.n_seg = status ? 0 : n;
+        h.depth = status ? 1 : depth;
+        h.cur_seq = cur_seq[doc];
+        h.min_seq = min_seq[doc];
+        h.text_top = ttop;
+        h.props_top = ptop;
+        h.next_uid = n + 1;
+        h.status = status;
+        h.delta_hash = MT_FNV_OFF;
+        for (int l = 0; l < MT_LV; l++) h.n_blk[l] = status ? (l == 0) : nbl[l];
+        st.hdr[doc] = h;
+        st.retry[doc] = 0;
+    }
+}
+
 // Per-launch LDS capacities of the tier (the HBM tier keeps only the B-tree counts in LDS).
 struct TierCaps {
     int S, B, H;
@@ -1015,6 +1131,127 @@ int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, 
     int rc = mt_batch_apply_async(h, b);
     if (rc == 0) rc = mt_sync(h);
     mt_batch_free(b);
+    return rc;
+}
+
+int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,
+                      uint64_t n_segs, const uint16_t *text, uint64_t text_len, const uint32_t *props,
+                      uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq) {
+    if (!h || !doc_seg_off || !n_header || !min_seq || !cur_seq || (n_segs && !segs)) return MT_E_INVALID;
+    const uint32_t N = h->n_docs;
+    for (uint32_t d = 0; d < N; d++)
+        if (n_header[d] < 0 || doc_seg_off[d] + n_header[d] > doc_seg_off[d + 1] ||
+            doc_seg_off[d + 1] > (int64_t)n_segs) {
+            h->err = "mt_load_snapshots: bad document segment ranges";
+            return MT_E_INVALID;
+        }
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    int64_t *d_off = nullptr;
+    int32_t *d_nh = nullptr, *d_min = nullptr, *d_cur = nullptr;
+    mt_seg_rec *d_segs = nullptr;
+    uint16_t *d_text = nullptr;
+    uint32_t *d_props = nullptr;
+    auto cleanup = [&]() {
+        void *ps[] = {d_off, d_nh, d_min, d_cur, d_segs, d_text, d_props};
+        for (void *p : ps)
+            if (p) hipFree(p);
+    };
+    bool ok = hipMalloc(&d_off, (N + 1) * 8) == hipSuccess && hipMalloc(&d_nh, N * 4) == hipSuccess &&
+              hipMalloc(&d_min, N * 4) == hipSuccess && hipMalloc(&d_cur, N * 4) == hipSuccess &&
+              hipMalloc(&d_segs, std::max<uint64_t>(n_segs, 1) * sizeof(mt_seg_rec)) == hipSuccess &&
+              hipMalloc(&d_text, std::max<uint64_t>(text_len, 1) * 2) == hipSuccess &&
+              hipMalloc(&d_props, std::max<uint64_t>(props_len, 1) * 4) == hipSuccess;
+    ok = ok && hipMemcpy(d_off, doc_seg_off, (N + 1) * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_nh, n_header, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_min, min_seq, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_cur, cur_seq, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         (!n_segs || hipMemcpy(d_segs, segs, n_segs * sizeof(mt_seg_rec), hipMemcpyHostToDevice) == hipSuccess) &&
+         (!text_len || hipMemcpy(d_text, text, text_len * 2, hipMemcpyHostToDevice) == hipSuccess) &&
+         (!props_len || hipMemcpy(d_props, props, props_len * 4, hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) {
+        cleanup();
+        h->err = "mt_load_snapshots: device allocation/copy failed";
+        return MT_E_NOMEM;
+    }
+    if (h->st.DL) (void)hipMemsetAsync(h->st.dlog, 0, (size_t)N * h->st.DL * 4, h->stream);
+    hipLaunchKernelGGL(k_load_header, dim3(N), dim3(MT_WAVE), 0, h->stream, h->st, d_off, d_nh, d_segs, d_text,
+                       d_props, d_min, d_cur);
+    hipError_t e = hipGetLastError();
+    // loadBody (MT/snapshotLoader.ts:161-228): specs without merge info (NonCollabClient,
+    // seq 0) are appended in batches -- one insertSegments: one boundary at the batch start
+    // (root.cachedLength), then each segment at insertPos += cachedLength -- the others one
+    // by one at root.cachedLength.  Each append becomes an MT_F_LOAD insert record (refSeq
+    // 0, the append's client and seq) plus MT_OP_LOAD_REMOVED when the spec carries removal
+    // info; replayed by the ordinary replay kernels (every tier).
+    std::vector<mt_op_rec> ops;
+    std::vector<int64_t> ooff(N + 1, 0);
+    for (uint32_t d = 0; d < N; d++) {
+        ooff[d] = (int64_t)ops.size();
+        const int64_t s0 = doc_seg_off[d], sh = s0 + n_header[d], s1 = doc_seg_off[d + 1];
+        int64_t obs = 0;   // root.cachedLength: observer length (removed segments count 0)
+        for (int64_t i = s0; i < sh; i++)
+            if (segs[i].removed_seq == MT_RSEQ_NONE) obs += (segs[i].flags & MT_F_MARKER) ? 1 : segs[i].len;
+        bool in_batch = false;
+        int64_t ins = 0;
+        for (int64_t i = sh; i < s1; i++) {
+            const mt_seg_rec &r = segs[i];
+            const int len = (r.flags & MT_F_MARKER) ? 1 : r.len;
+            const bool plain = r.client == -2 && r.seq == 0;
+            const bool removed = r.removed_seq != MT_RSEQ_NONE;
+            if (plain) {
+                if (!in_batch) ins = obs;
+                in_batch = true;
+            } else {
+                in_batch = false;
+                ins = obs;
+            }
+            if (len > 0) {   // blockInsert skips empty segments (:2229)
+                mt_op_rec o;
+                memset(&o, 0, sizeof(o));
+                o.seq = plain ? 0 : r.seq;
+                o.ref_seq = 0;
+                o.min_seq = 0;
+                o.pos1 = (int32_t)ins;
+                o.pos2 = len;
+                o.payload = r.payload;
+                o.props = r.props;
+                o.client = (uint16_t)(plain ? -2 : r.client);
+                o.kind = MT_OP_INSERT;
+                o.flags = (uint8_t)(MT_F_LOAD | (r.flags & MT_F_MARKER));
+                ops.push_back(o);
+                if (removed) {
+                    mt_op_rec q;
+                    memset(&q, 0, sizeof(q));
+                    q.seq = r.removed_seq;
+                    q.client = (uint16_t)r.removed_client;
+                    q.kind = MT_OP_LOAD_REMOVED;
+                    q.flags = MT_F_LOAD;
+                    ops.push_back(q);
+                }
+                ins += len;
+            }
+            if (!removed) obs += len;
+        }
+    }
+    ooff[N] = (int64_t)ops.size();
+    int rc = e == hipSuccess ? 0 : MT_E_HIP;
+    if (rc) h->err = std::string("k_load_header: ") + hipGetErrorString(e);
+    if (!rc && !ops.empty()) {
+        mt_batch *b = mt_batch_upload(h, ooff.data(), ops.data(), ops.size(), text, text_len, props, props_len);
+        if (!b) {
+            rc = MT_E_NOMEM;
+        } else {
+            rc = mt_batch_apply_async(h, b);
+            if (rc == 0) rc = mt_sync(h);
+            mt_batch_free(b);
+        }
+    }
+    if (!rc && hipStreamSynchronize(h->stream) != hipSuccess) {
+        h->err = "mt_load_snapshots: stream synchronisation failed";
+        rc = MT_E_HIP;
+    }
+    cleanup();
     return rc;
 }
 

@@ -89,6 +89,19 @@ int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, 
                  const uint16_t *text, uint64_t text_len, const uint32_t *props,
                  uint64_t props_len);
 
+/* Cold catch-up (config C5): replaces every document's state with a decoded SnapshotV1
+   summary -- Client.load -> SnapshotLoader.initialize (packages/dds/merge-tree/src/
+   snapshotLoader.ts:36-228): loadHeader = reloadFromSegments (mergeTree.ts:1229-1284) +
+   startOrUpdateCollaboration(min_seq, cur_seq) (client.ts:1053-1073), then loadBody's
+   appends (snapshotLoader.ts:195-227).  Document d's records are
+   segs[doc_seg_off[d] .. doc_seg_off[d+1]), the first n_header[d] from the header chunk;
+   payload / props index the text (UTF-16) and props arenas.  A document whose load fails
+   like the reference's ("MergeTree insert failed") gets that status.  Catch-up
+   and tail messages then go through mt_apply_ops as usual.  Synchronous. */
+int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,
+                      uint64_t n_segs, const uint16_t *text, uint64_t text_len, const uint32_t *props,
+                      uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq);
+
 /* Device-resident batches (bench / pipelined path). */
 mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops,
                           uint64_t n_ops, const uint16_t *text, uint64_t text_len,

@@ -130,3 +130,38 @@ def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     b.apply_async()
     mt.sync()
     assert np.array_equal(mt.checksums(), gsums)
+
+
+@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged"])
+@pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
+def test_gpu_snapshot_load_matches_reference(name, tier):
+    """Config C5 (cold catch-up) through mt_load_snapshots: after the load the device tree
+    equals the reference's (reloadFromSegments shape, body appends, segments, properties);
+    after the tail the outputs and every delta callback equal the reference's; summaries the
+    reference fails to load fail with the same status."""
+    fx = gu.load(name)
+    docs = [d for d in fx["docs"] if gu.snap_status(d) is not None]
+    interner = gu.Interner()
+    la, oa = gu.encode_snap_docs(fx, interner, docs)
+    mt = _gpu_batch(len(docs), **TIERS[tier])
+    mt.load_snapshots(la)
+    st = mt.status()
+    bad = []
+    for i, doc in enumerate(docs):
+        want = gu.snap_status(doc)
+        if want:
+            if st[i] != want:
+                bad.append((doc["doc"], "load status", int(st[i])))
+            continue
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected_snap(doc, interner, "load_out"))
+        if errs:
+            bad.append((doc["doc"], "after load", errs))
+    assert not bad, f"{name}: {bad[:4]}"
+    mt.apply_arrays(oa)
+    for i, doc in enumerate(docs):
+        if gu.snap_status(doc):
+            continue
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected_snap(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, f"{name}: {bad[:4]}"
