@@ -65,6 +65,99 @@ def capacities(cfg):
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
 
+def run_c5(args, cfg, rank, world, local_rank, dist):
+    """Config C5 (cold catch-up): every document's SnapshotV1 summary is loaded
+    (mt_snapshots_load_async: reloadFromSegments + loadBody) and its tail of `tail` sequenced
+    messages replayed.  Inputs (decoded summaries as mt_seg_rec records, tail batch) are
+    resident in HBM; the summaries are SnapshotV1.extractSync of the observer after `ops`
+    generated messages (mt_extract_snapshots, untimed), the tail is messages ops+1..ops+tail
+    of the same generated streams."""
+    import numpy as np
+    from fluidframework_amd import MergeTreeBatch
+    from fluidframework_amd.snapshot import load_arrays_from_extract
+    docs = args.docs or cfg["docs"] // 8          # the 1M summaries shard over 8 GPUs
+    K, tail = cfg["ops"], cfg["tail"]
+    caps = dict(seg_capacity=1024, text_capacity=1 << 14, heap_capacity=1024, props_capacity=1024,
+                lds_seg_capacity=args.lds_cap or 256)
+    mt = MergeTreeBatch(docs, device=local_rank, **caps)
+    base = rank * docs
+    t_prep = time.time()
+    g1 = mt.generate(dict(cfg, ops=K), base)
+    counts, recs, text, props, mn, cu = mt.extract_snapshots_raw()
+    g1.free()
+    load = load_arrays_from_extract(counts, recs, text, props, mn, cu, cfg["chunk"])
+    g2 = mt.generate(dict(cfg, ops=K + tail), base)
+    host = g2.download()
+    g2.free()
+    idx = (np.arange(docs)[:, None] * (K + tail) + K + np.arange(tail)[None, :]).ravel()
+    tail_arr = dict(ops=host["ops"][idx], doc_off=np.arange(docs + 1, dtype=np.int64) * tail,
+                    text=host["text"], props=host["props"])
+    snaps = mt.upload_snapshots(load)
+    tb = mt.upload(tail_arr)
+    t_prep = time.time() - t_prep
+
+    def step():
+        snaps.load_async()
+        tb.apply_async()
+
+    for _ in range(args.warmup):
+        step()
+        mt.sync()
+    if dist is not None:
+        dist.barrier()
+    mt.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    mt.sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = mt.status()
+    sums = mt.checksums()
+    if rank != 0:
+        return
+    n_tail = int(len(idx))
+    cpu = parity = None
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import pyoracle                            # the checker, timed as the CPU baseline
+        n_sample = args.cpu_sample_docs or min(docs, 20000)
+        lo = {k: v for k, v in load.items()}
+        lo["doc_off"] = load["doc_off"][: n_sample + 1]
+        sa = dict(tail_arr, doc_off=tail_arr["doc_off"][: n_sample + 1])
+        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        t_c = time.perf_counter()
+        osums, ost = pyoracle.load_replay_batch(lo, sa, threads=threads)
+        t_c = time.perf_counter() - t_c
+        cpu = dict(value=round(n_sample / t_c, 1), unit="docs/s", cores=threads, kind="port",
+                   sample=f"oracle/mt_oracle.c orc_load + tail replay of docs [0,{n_sample}) on {threads} host threads, "
+                          f"{t_c:.2f} s ({n_sample * tail / t_c:.0f} tail ops/s)")
+        parity = dict(docs_checked=n_sample, mismatches=int((osums != sums[:n_sample]).sum() + (ost != status[:n_sample]).sum()))
+    docs_total = docs * world
+    print(json.dumps({
+        "metric": "cold catch-up: SnapshotV1 summaries loaded + tail ops replayed per second (config C5)",
+        "value": round(docs_total * args.steps / elapsed, 1), "unit": "docs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000 / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "tail_ops_per_s": round(n_tail * world * args.steps / elapsed, 1),
+        "config": {"workload": f"c5: {docs} summaries/GPU (doc {cfg['seed_len']} units + {K} generated ops, "
+                               f"chunkSize {cfg['chunk']}), {tail}-op tails, {cfg['writers']} writers",
+                   "docs_total": docs_total, "summary_segments": int(len(load["segs"])),
+                   "summary_text_units": int(counts[:, 1].sum()), "body_docs": int((load["n_header"] <
+                                                                                     np.diff(load["doc_off"])).sum()),
+                   "parallelism": f"doc-shard x{world}"},
+        "cpu_baseline": cpu,
+        "parity": {"status_nonzero": int((status != 0).sum()), "oracle_sample": parity},
+        "prep_s": round(t_prep, 2),
+    }))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,6 +173,11 @@ def main():
     from fluidframework_amd import MergeTreeBatch
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
     cfg = dict(configs[args.config])
+    if args.config == "c5":
+        run_c5(args, cfg, rank, world, local_rank, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     docs = args.docs or (cfg["docs"] if args.config == "c2" else min(cfg["docs"], 16384))
     if args.ops:
         cfg["ops"] = args.ops

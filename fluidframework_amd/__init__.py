@@ -70,22 +70,77 @@ class MergeTreeBatch:
                                           _native.ptr(text), len(text), _native.ptr(props), len(props)),
                     "mt_apply_ops")
 
+    @staticmethod
+    def _snap_args(la):
+        from .snapshot import SEG_DTYPE
+        return [np.ascontiguousarray(la["doc_off"], dtype=np.int64), np.ascontiguousarray(la["n_header"], dtype=np.int32),
+                np.ascontiguousarray(la["segs"], dtype=SEG_DTYPE), np.ascontiguousarray(la["text"], dtype=np.uint16),
+                np.ascontiguousarray(la["props"], dtype=np.uint32), np.ascontiguousarray(la["min_seq"], dtype=np.int32),
+                np.ascontiguousarray(la["cur_seq"], dtype=np.int32)]
+
     def load_snapshots(self, la):
         """Client.load of a decoded SnapshotV1 summary into every document
         (snapshot.SnapshotBatch.arrays(); MT/snapshotLoader.ts:36-228)."""
-        from .snapshot import SEG_DTYPE
-        segs = np.ascontiguousarray(la["segs"], dtype=SEG_DTYPE)
-        off = np.ascontiguousarray(la["doc_off"], dtype=np.int64)
-        nh = np.ascontiguousarray(la["n_header"], dtype=np.int32)
-        text = np.ascontiguousarray(la["text"], dtype=np.uint16)
-        props = np.ascontiguousarray(la["props"], dtype=np.uint32)
-        mn = np.ascontiguousarray(la["min_seq"], dtype=np.int32)
-        cu = np.ascontiguousarray(la["cur_seq"], dtype=np.int32)
+        off, nh, segs, text, props, mn, cu = self._snap_args(la)
         if len(off) != self.n_docs + 1:
             raise ValueError("one summary per document")
         self._check(self.lib.mt_load_snapshots(self.h, _native.ptr(off), _native.ptr(nh), _native.ptr(segs), len(segs),
                                                _native.ptr(text), len(text), _native.ptr(props), len(props),
                                                _native.ptr(mn), _native.ptr(cu)), "mt_load_snapshots")
+
+    def upload_snapshots(self, la):
+        """Device-resident summaries (mt_snapshots_upload); .load_async() enqueues a load."""
+        off, nh, segs, text, props, mn, cu = self._snap_args(la)
+        s = self.lib.mt_snapshots_upload(self.h, _native.ptr(off), _native.ptr(nh), _native.ptr(segs), len(segs),
+                                         _native.ptr(text), len(text), _native.ptr(props), len(props),
+                                         _native.ptr(mn), _native.ptr(cu))
+        if not s:
+            raise RuntimeError(f"mt_snapshots_upload failed: {self.lib.mt_last_error(self.h).decode()}")
+        return DeviceSnapshots(self, s)
+
+    def extract_snapshots_raw(self):
+        """mt_extract_snapshots as concatenated arrays: (counts[n_docs, 3], records, text,
+        props, min_seq, cur_seq); record offsets are relative to their document's arenas."""
+        from .snapshot import SEG_DTYPE
+        io = np.zeros(3 * self.n_docs, dtype=np.int64)
+        self._check(self.lib.mt_extract_snapshots(self.h, _native.ptr(io), None, None, None, None, None),
+                    "mt_extract_snapshots")
+        tot = io.reshape(-1, 3).sum(axis=0)
+        recs = np.zeros(max(int(tot[0]), 1), dtype=SEG_DTYPE)
+        text = np.zeros(max(int(tot[1]), 1), dtype=np.uint16)
+        props = np.zeros(max(int(tot[2]), 1), dtype=np.uint32)
+        mn = np.zeros(self.n_docs, dtype=np.int32)
+        cu = np.zeros(self.n_docs, dtype=np.int32)
+        self._check(self.lib.mt_extract_snapshots(self.h, _native.ptr(io), _native.ptr(recs), _native.ptr(text),
+                                                  _native.ptr(props), _native.ptr(mn), _native.ptr(cu)),
+                    "mt_extract_snapshots")
+        return io.reshape(-1, 3), recs[: int(tot[0])], text, props, mn, cu
+
+    def extract_snapshots(self):
+        """SnapshotV1.extractSync of every document (mt_extract_snapshots): per document
+        (records, text, props, min_seq, cur_seq); records index that document's arenas."""
+        from .snapshot import SEG_DTYPE
+        io = np.zeros(3 * self.n_docs, dtype=np.int64)
+        self._check(self.lib.mt_extract_snapshots(self.h, _native.ptr(io), None, None, None, None, None),
+                    "mt_extract_snapshots")
+        tot = io.reshape(-1, 3).sum(axis=0)
+        recs = np.zeros(max(int(tot[0]), 1), dtype=SEG_DTYPE)
+        text = np.zeros(max(int(tot[1]), 1), dtype=np.uint16)
+        props = np.zeros(max(int(tot[2]), 1), dtype=np.uint32)
+        mn = np.zeros(self.n_docs, dtype=np.int32)
+        cu = np.zeros(self.n_docs, dtype=np.int32)
+        self._check(self.lib.mt_extract_snapshots(self.h, _native.ptr(io), _native.ptr(recs), _native.ptr(text),
+                                                  _native.ptr(props), _native.ptr(mn), _native.ptr(cu)),
+                    "mt_extract_snapshots")
+        out = []
+        c = io.reshape(-1, 3)
+        r0 = t0 = p0 = 0
+        for d in range(self.n_docs):
+            nr, nt, np_ = (int(x) for x in c[d])
+            out.append(dict(segs=recs[r0:r0 + nr], text=text[t0:t0 + nt], props=props[p0:p0 + np_],
+                            min_seq=int(mn[d]), cur_seq=int(cu[d])))
+            r0, t0, p0 = r0 + nr, t0 + nt, p0 + np_
+        return out
 
     def upload(self, a):
         return DeviceBatch(self, a)
@@ -259,6 +314,27 @@ class DeviceBatch:
         if self.b:
             self.owner.lib.mt_batch_free(self.b)
             self.b = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceSnapshots:
+    """Decoded summaries resident in HBM (mt_snapshots)."""
+
+    def __init__(self, owner, handle):
+        self.owner, self.s = owner, handle
+
+    def load_async(self):
+        self.owner._check(self.owner.lib.mt_snapshots_load_async(self.owner.h, self.s), "mt_snapshots_load_async")
+
+    def free(self):
+        if self.s:
+            self.owner.lib.mt_snapshots_free(self.s)
+            self.s = None
 
     def __del__(self):
         try:

@@ -43,6 +43,10 @@ SIGNATURES = [
     ("mt_reset", _I, [_P]),
     ("mt_apply_ops", _I, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),
     ("mt_load_snapshots", _I, [_P, _P, _P, _P, _U64, _P, _U64, _P, _U64, _P, _P]),
+    ("mt_extract_snapshots", _I, [_P, _P, _P, _P, _P, _P, _P]),
+    ("mt_snapshots_upload", _P, [_P, _P, _P, _P, _U64, _P, _U64, _P, _U64, _P, _P]),
+    ("mt_snapshots_load_async", _I, [_P, _P]),
+    ("mt_snapshots_free", None, [_P]),
     ("mt_batch_upload", _P, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),
     ("mt_batch_apply_async", _I, [_P, _P]),
     ("mt_batch_num_ops", _U64, [_P]),

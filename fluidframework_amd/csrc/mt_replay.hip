@@ -745,6 +745,126 @@ __device__ static SegRanges seg_ranges(const DevState &st, int doc, const DocHdr
     return R;
 }
 
+// SnapshotV1.extractSync (MT/snapshotV1.ts:156-252) of a document's current state: walk the
+// leaves in order; drop unacked segments and those removed at or below minSeq; coalesce runs
+// of below-minSeq, unremoved segments while TextSegment.canAppend and matchProperties hold
+// (MT/textSegment.ts:62-67, MT/properties.ts:61-92: the run's text is copied out once, as
+// the clone + append chain builds it); everything else is emitted with its merge info.
+// mode 0 counts {records, text units, props words} per document into io[3*doc]; mode 1
+// writes them at the offsets io holds (the host's prefix sums).  One wave per document; the
+// per-segment decisions are uniform, text copies are wave-wide.
+__device__ static bool props_equal_set(const uint32_t *pr, uint32_t ha, uint32_t hb) {
+    if (ha == 0 || hb == 0) return ha == hb;
+    if (ha == hb) return true;
+    const uint32_t *a = pr + (size_t)ha * MT_PREC, *b = pr + (size_t)hb * MT_PREC;
+    if (a[0] != b[0]) return false;
+    for (uint32_t i = 0; i < a[0]; i++) {
+        bool ok = false;
+        for (uint32_t j = 0; j < b[0]; j++)
+            if (b[1 + 2 * j] == a[1 + 2 * i]) ok = b[2 + 2 * j] == a[2 + 2 * i];
+        if (!ok) return false;
+    }
+    return true;
+}
+__global__ void __launch_bounds__(MT_WAVE) k_extract(DevState st, int mode, int64_t *io, mt_seg_rec *recs,
+                                                     uint16_t *text_out, uint32_t *props_out, int32_t *win) {
+    const int doc = blockIdx.x;
+    if (doc >= st.n_docs) return;
+    const DocHdr h = st.hdr[doc];
+    const SegRanges R = seg_ranges(st, doc, h);
+    const uint16_t *tb = st.text + ((size_t)doc * 2 + h.text_half) * st.T;
+    const uint32_t *pr = st.props + ((size_t)doc * 2 + h.props_half) * st.P * MT_PREC;
+    const int ms = h.min_seq;
+    int64_t nrec = 0, ntext = 0, nprop = 0;
+    const int64_t rbase = mode ? io[3 * doc] : 0, tbase = mode ? io[3 * doc + 1] : 0, pbase = mode ? io[3 * doc + 2] : 0;
+    // the coalescing candidate ("prev"): an open record
+    bool open = false, p_marker = false, p_nl = false;
+    int p_len = 0;
+    uint32_t p_props = 0;
+    int64_t p_rec = 0;
+    auto emit = [&](const v4i a, const v4u b, uint32_t flags, int seq, int cli) {
+        // a new record for segment (a, b); returns nothing, advances the counters
+        const bool marker = (b.z & MT_MARKER_BIT) != 0;
+        const int len = a.x;
+        if (mode && lane() == 0) {
+            mt_seg_rec r;
+            memset(&r, 0, sizeof(r));
+            r.len = len;
+            r.seq = seq;
+            r.removed_seq = a.z;
+            r.client = (int16_t)cli;
+            r.removed_client = a.z != MT_RSEQ_NONE ? (int16_t)seg_rcli(a) : (int16_t)0;
+            r.flags = (uint8_t)(flags | (marker ? MT_F_MARKER : 0));
+            r.payload = marker ? b.x : (uint32_t)(ntext);
+            r.props = MT_NO_PROPS;
+            if (b.y) {
+                const uint32_t *src = pr + (size_t)b.y * MT_PREC;
+                r.props = (uint32_t)nprop;
+                uint32_t *dst = props_out + pbase + nprop;
+                dst[0] = src[0];
+                for (uint32_t k = 0; k < 2 * src[0]; k++) dst[1 + k] = src[1 + k];
+            }
+            recs[rbase + nrec] = r;
+        }
+        if (b.y) nprop += 1 + 2 * (int64_t)pr[(size_t)b.y * MT_PREC];
+        if (!marker) {
+            if (mode)
+                for (int q = lane(); q < len; q += MT_WAVE) text_out[tbase + ntext + q] = tb[b.x + q];
+            ntext += len;
+        }
+        nrec++;
+    };
+    for (int rr = 0; rr < R.count(); rr++) {
+        const v4i *A;
+        const v4u *Bv;
+        int n;
+        R.get(rr, A, Bv, n);
+        for (int i = 0; i < n; i++) {
+            const v4i a = uni4(A[i]);
+            const v4u b = uni4(Bv[i]);
+            const int seq = a.y, rseq = a.z;
+            const bool removed = rseq != MT_RSEQ_NONE;
+            if (seq == -1 || (removed && rseq <= ms)) continue;            // :189-191
+            const bool marker = (b.z & MT_MARKER_BIT) != 0;
+            if (seq <= ms && (!removed || rseq == -1)) {                   // :196-215 coalesce
+                const bool nl = !marker && a.x > 0 && tb[b.x + a.x - 1] == '\n';
+                const bool can = open && !p_marker && !marker && !p_nl &&
+                                 (p_len <= MT_GRAN || a.x <= MT_GRAN) && props_equal_set(pr, p_props, b.y);
+                if (can) {   // prev.clone().append(segment.clone())
+                    if (mode)
+                        for (int q = lane(); q < a.x; q += MT_WAVE) text_out[tbase + ntext + q] = tb[b.x + q];
+                    ntext += a.x;
+                    p_len += a.x;
+                    if (a.x > 0) p_nl = nl;   // "".endsWith("\n") leaves the run's ending
+                    if (mode && lane() == 0) recs[rbase + p_rec].len = p_len;
+                } else {     // pushSeg(prev); prev = segment
+                    p_rec = nrec;
+                    emit(a, b, 0u, 0, -2);
+                    open = true;
+                    p_marker = marker;
+                    p_nl = nl;
+                    p_len = a.x;
+                    p_props = b.y;
+                }
+            } else {                                                        // :216-242 merge info
+                open = false;
+                const bool above = seq > ms;
+                uint32_t f = MT_SEG_MERGE_INFO | (above ? MT_SEG_HAS_SEQ : 0u);
+                emit(a, b, f, above ? seq : 0, above ? seg_cli(a) : -2);
+            }
+        }
+    }
+    if (mode == 0 && lane() == 0) {
+        io[3 * doc] = nrec;
+        io[3 * doc + 1] = ntext;
+        io[3 * doc + 2] = nprop;
+    }
+    if (lane() == 0 && win) {
+        win[2 * doc] = h.min_seq;
+        win[2 * doc + 1] = h.cur_seq;
+    }
+}
+
 // mt_checksum per document (definitions: DESIGN.md "Checksums", oracle/mt_oracle.c).
 __global__ void __launch_bounds__(MT_WAVE) k_checksum(DevState st, mt_checksum *out) {
     const int doc = blockIdx.x;
@@ -828,7 +948,7 @@ struct mt_handle {
     uint32_t n_docs = 0;
     DevState st{};
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_load = nullptr;
     float last_ms = 0.f;
     bool timed = false;      // ev0/ev1 bracket a launch not yet read by mt_sync
     std::string err;
@@ -952,7 +1072,8 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         alloc((void **)&st.pgUmap, N * (size_t)st.UM * sizeof(uint16_t));
     }
     if (!ok || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+        hipEventCreate(&h->ev_load) != hipSuccess) {
         mt_destroy(h);
         return nullptr;
     }
@@ -974,6 +1095,7 @@ void mt_destroy(mt_handle *h) {
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
+    if (h->ev_load) hipEventDestroy(h->ev_load);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1134,56 +1256,66 @@ int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, 
     return rc;
 }
 
-int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,
-                      uint64_t n_segs, const uint16_t *text, uint64_t text_len, const uint32_t *props,
-                      uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq) {
-    if (!h || !doc_seg_off || !n_header || !min_seq || !cur_seq || (n_segs && !segs)) return MT_E_INVALID;
+struct mt_snapshots {
+    int device = 0;
+    uint32_t n_docs = 0;
+    int64_t *off = nullptr;
+    int32_t *nh = nullptr, *min_seq = nullptr, *cur_seq = nullptr;
+    mt_seg_rec *segs = nullptr;
+    uint16_t *text = nullptr;
+    uint32_t *props = nullptr;
+    mt_batch *body = nullptr;   // loadBody appends as MT_F_LOAD records (nullptr: none)
+};
+
+void mt_snapshots_free(mt_snapshots *s) {
+    if (!s) return;
+    hipSetDevice(s->device);
+    void *ps[] = {s->off, s->nh, s->min_seq, s->cur_seq, s->segs, s->text, s->props};
+    for (void *p : ps)
+        if (p) hipFree(p);
+    mt_batch_free(s->body);
+    delete s;
+}
+
+mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header,
+                                  const mt_seg_rec *segs, uint64_t n_segs, const uint16_t *text, uint64_t text_len,
+                                  const uint32_t *props, uint64_t props_len, const int32_t *min_seq,
+                                  const int32_t *cur_seq) {
+    if (!h || !doc_seg_off || !n_header || !min_seq || !cur_seq || (n_segs && !segs)) return nullptr;
     const uint32_t N = h->n_docs;
     for (uint32_t d = 0; d < N; d++)
         if (n_header[d] < 0 || doc_seg_off[d] + n_header[d] > doc_seg_off[d + 1] ||
             doc_seg_off[d + 1] > (int64_t)n_segs) {
-            h->err = "mt_load_snapshots: bad document segment ranges";
-            return MT_E_INVALID;
+            h->err = "mt_snapshots_upload: bad document segment ranges";
+            return nullptr;
         }
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    int64_t *d_off = nullptr;
-    int32_t *d_nh = nullptr, *d_min = nullptr, *d_cur = nullptr;
-    mt_seg_rec *d_segs = nullptr;
-    uint16_t *d_text = nullptr;
-    uint32_t *d_props = nullptr;
-    auto cleanup = [&]() {
-        void *ps[] = {d_off, d_nh, d_min, d_cur, d_segs, d_text, d_props};
-        for (void *p : ps)
-            if (p) hipFree(p);
-    };
-    bool ok = hipMalloc(&d_off, (N + 1) * 8) == hipSuccess && hipMalloc(&d_nh, N * 4) == hipSuccess &&
-              hipMalloc(&d_min, N * 4) == hipSuccess && hipMalloc(&d_cur, N * 4) == hipSuccess &&
-              hipMalloc(&d_segs, std::max<uint64_t>(n_segs, 1) * sizeof(mt_seg_rec)) == hipSuccess &&
-              hipMalloc(&d_text, std::max<uint64_t>(text_len, 1) * 2) == hipSuccess &&
-              hipMalloc(&d_props, std::max<uint64_t>(props_len, 1) * 4) == hipSuccess;
-    ok = ok && hipMemcpy(d_off, doc_seg_off, (N + 1) * 8, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(d_nh, n_header, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(d_min, min_seq, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(d_cur, cur_seq, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
-         (!n_segs || hipMemcpy(d_segs, segs, n_segs * sizeof(mt_seg_rec), hipMemcpyHostToDevice) == hipSuccess) &&
-         (!text_len || hipMemcpy(d_text, text, text_len * 2, hipMemcpyHostToDevice) == hipSuccess) &&
-         (!props_len || hipMemcpy(d_props, props, props_len * 4, hipMemcpyHostToDevice) == hipSuccess);
+    if (hipSetDevice(h->device) != hipSuccess) return nullptr;
+    auto *s = new mt_snapshots();
+    s->device = h->device;
+    s->n_docs = N;
+    bool ok = hipMalloc(&s->off, (N + 1) * 8) == hipSuccess && hipMalloc(&s->nh, N * 4) == hipSuccess &&
+              hipMalloc(&s->min_seq, N * 4) == hipSuccess && hipMalloc(&s->cur_seq, N * 4) == hipSuccess &&
+              hipMalloc(&s->segs, std::max<uint64_t>(n_segs, 1) * sizeof(mt_seg_rec)) == hipSuccess &&
+              hipMalloc(&s->text, std::max<uint64_t>(text_len, 1) * 2) == hipSuccess &&
+              hipMalloc(&s->props, std::max<uint64_t>(props_len, 1) * 4) == hipSuccess;
+    ok = ok && hipMemcpy(s->off, doc_seg_off, (N + 1) * 8, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(s->nh, n_header, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(s->min_seq, min_seq, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(s->cur_seq, cur_seq, N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         (!n_segs || hipMemcpy(s->segs, segs, n_segs * sizeof(mt_seg_rec), hipMemcpyHostToDevice) == hipSuccess) &&
+         (!text_len || hipMemcpy(s->text, text, text_len * 2, hipMemcpyHostToDevice) == hipSuccess) &&
+         (!props_len || hipMemcpy(s->props, props, props_len * 4, hipMemcpyHostToDevice) == hipSuccess);
     if (!ok) {
-        cleanup();
-        h->err = "mt_load_snapshots: device allocation/copy failed";
-        return MT_E_NOMEM;
+        h->err = "mt_snapshots_upload: device allocation/copy failed";
+        mt_snapshots_free(s);
+        return nullptr;
     }
-    if (h->st.DL) (void)hipMemsetAsync(h->st.dlog, 0, (size_t)N * h->st.DL * 4, h->stream);
-    hipLaunchKernelGGL(k_load_header, dim3(N), dim3(MT_WAVE), 0, h->stream, h->st, d_off, d_nh, d_segs, d_text,
-                       d_props, d_min, d_cur);
-    hipError_t e = hipGetLastError();
     // loadBody (MT/snapshotLoader.ts:161-228): specs without merge info (NonCollabClient,
     // seq 0) are appended in batches -- one insertSegments: one boundary at the batch start
     // (root.cachedLength), then each segment at insertPos += cachedLength -- the others one
     // by one at root.cachedLength.  Each append becomes an MT_F_LOAD insert record (refSeq
     // 0, the append's client and seq) plus MT_OP_LOAD_REMOVED when the spec carries removal
-    // info; replayed by the ordinary replay kernels (every tier).
+    // info; the ordinary replay kernels apply them (every tier).
     std::vector<mt_op_rec> ops;
     std::vector<int64_t> ooff(N + 1, 0);
     for (uint32_t d = 0; d < N; d++) {
@@ -1210,8 +1342,6 @@ int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n
                 mt_op_rec o;
                 memset(&o, 0, sizeof(o));
                 o.seq = plain ? 0 : r.seq;
-                o.ref_seq = 0;
-                o.min_seq = 0;
                 o.pos1 = (int32_t)ins;
                 o.pos2 = len;
                 o.payload = r.payload;
@@ -1235,24 +1365,101 @@ int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n
         }
     }
     ooff[N] = (int64_t)ops.size();
-    int rc = e == hipSuccess ? 0 : MT_E_HIP;
-    if (rc) h->err = std::string("k_load_header: ") + hipGetErrorString(e);
-    if (!rc && !ops.empty()) {
-        mt_batch *b = mt_batch_upload(h, ooff.data(), ops.data(), ops.size(), text, text_len, props, props_len);
-        if (!b) {
-            rc = MT_E_NOMEM;
-        } else {
-            rc = mt_batch_apply_async(h, b);
-            if (rc == 0) rc = mt_sync(h);
-            mt_batch_free(b);
+    if (!ops.empty()) {
+        s->body = mt_batch_upload(h, ooff.data(), ops.data(), ops.size(), text, text_len, props, props_len);
+        if (!s->body) {
+            mt_snapshots_free(s);
+            return nullptr;
         }
     }
-    if (!rc && hipStreamSynchronize(h->stream) != hipSuccess) {
-        h->err = "mt_load_snapshots: stream synchronisation failed";
-        rc = MT_E_HIP;
-    }
-    cleanup();
+    return s;
+}
+
+int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
+    if (!h || !s || s->n_docs != h->n_docs) return MT_E_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
+    HIPCHK(h, hipEventRecord(h->ev_load, h->stream));
+    hipLaunchKernelGGL(k_load_header, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, s->off, s->nh, s->segs,
+                       s->text, s->props, s->min_seq, s->cur_seq);
+    HIPCHK(h, hipGetLastError());
+    if (s->body) return mt_batch_apply_async(h, s->body);
+    return 0;
+}
+
+int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,
+                      uint64_t n_segs, const uint16_t *text, uint64_t text_len, const uint32_t *props,
+                      uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq) {
+    if (!h) return MT_E_INVALID;
+    if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess) return MT_E_HIP;
+    mt_snapshots *s = mt_snapshots_upload(h, doc_seg_off, n_header, segs, n_segs, text, text_len, props, props_len,
+                                          min_seq, cur_seq);
+    if (!s) return MT_E_INVALID;
+    int rc = mt_snapshots_load_async(h, s);
+    if (rc == 0) rc = mt_sync(h);
+    if (rc == 0 && hipStreamSynchronize(h->stream) != hipSuccess) rc = MT_E_HIP;
+    mt_snapshots_free(s);
     return rc;
+}
+
+int mt_extract_snapshots(mt_handle *h, int64_t *io, mt_seg_rec *recs, uint16_t *text, uint32_t *props,
+                         int32_t *min_seq, int32_t *cur_seq) {
+    if (!h || !io) return MT_E_INVALID;
+    const uint32_t N = h->n_docs;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    int64_t *d_io = nullptr;
+    HIPCHK(h, hipMalloc(&d_io, (size_t)N * 3 * 8));
+    const int mode = recs ? 1 : 0;
+    uint64_t nr = 0, nt = 0, np = 0;
+    std::vector<int64_t> off;
+    if (mode) {   // io holds the counts of the first call: exclusive prefix sums
+        off.resize((size_t)N * 3);
+        for (uint32_t d = 0; d < N; d++) {
+            off[3 * d] = (int64_t)nr;
+            off[3 * d + 1] = (int64_t)nt;
+            off[3 * d + 2] = (int64_t)np;
+            nr += io[3 * d];
+            nt += io[3 * d + 1];
+            np += io[3 * d + 2];
+        }
+    }
+    mt_seg_rec *d_recs = nullptr;
+    uint16_t *d_text = nullptr;
+    uint32_t *d_props = nullptr;
+    int32_t *d_win = nullptr;
+    bool ok = hipMalloc(&d_win, (size_t)N * 8) == hipSuccess;
+    if (ok && mode)
+        ok = hipMalloc(&d_recs, std::max<uint64_t>(nr, 1) * sizeof(mt_seg_rec)) == hipSuccess &&
+             hipMalloc(&d_text, std::max<uint64_t>(nt, 1) * 2) == hipSuccess &&
+             hipMalloc(&d_props, std::max<uint64_t>(np, 1) * 4) == hipSuccess &&
+             hipMemcpy(d_io, off.data(), (size_t)N * 3 * 8, hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_extract, dim3(N), dim3(MT_WAVE), 0, h->stream, h->st, mode, d_io, d_recs, d_text, d_props,
+                           d_win);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+    }
+    if (ok && !mode) ok = hipMemcpy(io, d_io, (size_t)N * 3 * 8, hipMemcpyDeviceToHost) == hipSuccess;
+    if (ok && mode) {
+        ok = (!nr || hipMemcpy(recs, d_recs, nr * sizeof(mt_seg_rec), hipMemcpyDeviceToHost) == hipSuccess) &&
+             (!nt || !text || hipMemcpy(text, d_text, nt * 2, hipMemcpyDeviceToHost) == hipSuccess) &&
+             (!np || !props || hipMemcpy(props, d_props, np * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    }
+    std::vector<int32_t> win((size_t)N * 2);
+    if (ok) ok = hipMemcpy(win.data(), d_win, (size_t)N * 8, hipMemcpyDeviceToHost) == hipSuccess;
+    if (ok)
+        for (uint32_t d = 0; d < N; d++) {
+            if (min_seq) min_seq[d] = win[2 * d];
+            if (cur_seq) cur_seq[d] = win[2 * d + 1];
+        }
+    void *ps[] = {d_io, d_recs, d_text, d_props, d_win};
+    for (void *p : ps)
+        if (p) hipFree(p);
+    if (!ok) {
+        h->err = "mt_extract_snapshots failed";
+        return MT_E_HIP;
+    }
+    return 0;
 }
 
 mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,

@@ -30,6 +30,8 @@ UNIVERSAL_SEQ = 0            # UniversalSequenceNumber    MT/constants.ts:11
 RSEQ_NONE = -2 ** 31         # removedSeq === undefined
 NO_PROPS = 0xFFFFFFFF
 F_MARKER = 2
+SEG_MERGE_INFO = 0x10        # mt_types.h MT_SEG_MERGE_INFO
+SEG_HAS_SEQ = 0x20           # mt_types.h MT_SEG_HAS_SEQ
 HEADER = "header"            # SnapshotLegacy.header      MT/snapshotlegacy.ts
 BODY = "body"                # SnapshotLegacy.body
 CHUNK_SIZE = 10000           # SnapshotV1.chunkSize       MT/snapshotV1.ts:42
@@ -180,6 +182,7 @@ class SnapshotBatch:
         if isinstance(props, dict):    # TextSegment.make / Marker.make `if (props)`: {} too (Q5)
             r["props"] = self._props(props)
         if has_merge_info(spec):
+            r["flags"] |= SEG_MERGE_INFO | (SEG_HAS_SEQ if spec.get("seq") is not None else 0)
             if spec.get("client") is not None:
                 r["client"] = self._short(short, spec["client"])
             if spec.get("seq") is not None:
@@ -214,3 +217,110 @@ class SnapshotBatch:
                     props=np.asarray(self.props if self.props else [0], dtype=np.uint32),
                     min_seq=np.asarray(self.min_seq, dtype=np.int32),
                     cur_seq=np.asarray(self.cur_seq, dtype=np.int32))
+
+
+# ---------------------------------------------------------------- emission
+def js_key_order(items):
+    """V8 own-key order of an object built by insertion: integer-like keys ascending first."""
+    def is_index(k):
+        return k.isdigit() and (k == "0" or not k.startswith("0")) and int(k) < 4294967295
+    ints = sorted((kv for kv in items if is_index(kv[0])), key=lambda kv: int(kv[0]))
+    return ints + [kv for kv in items if not is_index(kv[0])]
+
+
+def js_stringify(v):
+    """JSON.stringify for the values a summary holds (key order as given)."""
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
+
+
+def record_specs(recs, text, props, interner, client_names):
+    """ISegment.toJSONObject (MT/textSegment.ts:48-54, MT/mergeTree.ts:478-482, 690-694) and
+    the merge-info wrapper of extractSync (MT/snapshotV1.ts:222-241) for extracted records.
+    Returns (specs, lengths)."""
+    specs, lengths = [], []
+    for r in recs:
+        props_obj = None
+        if int(r["props"]) != NO_PROPS:
+            o = int(r["props"])
+            n = int(props[o])
+            items = [(interner.key_name(int(props[o + 1 + 2 * j])), interner.val_value(int(props[o + 2 + 2 * j])))
+                     for j in range(n)]
+            props_obj = dict(js_key_order(items))
+        if r["flags"] & F_MARKER:
+            js = {"marker": {"refType": int(r["payload"])}}
+            if props_obj is not None:
+                js["props"] = props_obj
+        else:
+            p0, ln = int(r["payload"]), int(r["len"])
+            t = np.asarray(text[p0:p0 + ln], dtype="<u2").tobytes().decode("utf-16-le", errors="surrogatepass")
+            js = t if props_obj is None else {"text": t, "props": props_obj}
+        if r["flags"] & SEG_MERGE_INFO:
+            raw = {"json": js}
+            if r["flags"] & SEG_HAS_SEQ:
+                raw["seq"] = int(r["seq"])
+                raw["client"] = client_names[int(r["client"])]
+            if int(r["removed_seq"]) != RSEQ_NONE:
+                raw["removedSeq"] = int(r["removed_seq"])
+                raw["removedClient"] = client_names[int(r["removed_client"])]
+            js = raw
+        specs.append(js)
+        lengths.append(int(r["len"]))
+    return specs, lengths
+
+
+def encode_chunks(specs, lengths, min_seq, cur_seq, chunk_size=CHUNK_SIZE):
+    """SnapshotV1.emit (MT/snapshotV1.ts:59-154): chunks of >= chunk_size units
+    (getSeqLengthSegs), the first is the header with the metadata; {path: JSON text} as
+    serializeAsMaxSupportedVersion writes it (JSON.stringify of the v1 chunk)."""
+    chunks = []
+    total_n = total_len = 0
+    while True:
+        seg, length, count = [], 0, 0
+        while length < chunk_size and total_n + count < len(specs):
+            seg.append(specs[total_n + count])
+            length += lengths[total_n + count]
+            count += 1
+        chunks.append(dict(version="1", segmentCount=count, length=length, segments=seg, startIndex=total_n))
+        total_n += count
+        total_len += length
+        if not total_n < len(specs):
+            break
+    head = chunks[0]
+    ids = [{"id": HEADER}] + [{"id": f"{BODY}_{i}"} for i in range(len(chunks) - 1)]
+    head["headerMetadata"] = dict(minSequenceNumber=min_seq, sequenceNumber=cur_seq, orderedChunkMetadata=ids,
+                                  totalLength=total_len, totalSegmentCount=total_n)
+    out = {HEADER: js_stringify(head)}
+    for i, ch in enumerate(chunks[1:]):
+        out[f"{BODY}_{i}"] = js_stringify(ch)
+    return out
+
+
+def load_arrays_from_extract(counts, recs, text, props, min_seq, cur_seq, chunk_size=CHUNK_SIZE):
+    """mt_extract_snapshots output -> mt_load_snapshots input without a JSON round trip:
+    offsets rebased to the concatenated arenas, and the header/body split emit() would make
+    (a record is in the header chunk iff the lengths before it sum to < chunk_size,
+    getSeqLengthSegs MT/snapshotV1.ts:59-81)."""
+    counts = np.asarray(counts, dtype=np.int64)
+    n_docs = len(counts)
+    doc_off = np.zeros(n_docs + 1, dtype=np.int64)
+    doc_off[1:] = np.cumsum(counts[:, 0])
+    t_off = np.concatenate([[0], np.cumsum(counts[:, 1])[:-1]]).astype(np.int64)
+    p_off = np.concatenate([[0], np.cumsum(counts[:, 2])[:-1]]).astype(np.int64)
+    segs = np.array(recs, copy=True)
+    doc_of = np.repeat(np.arange(n_docs), counts[:, 0])
+    text_rec = (segs["flags"] & F_MARKER) == 0
+    segs["payload"][text_rec] += t_off[doc_of[text_rec]].astype(np.uint32)
+    has_p = segs["props"] != NO_PROPS
+    segs["props"][has_p] += p_off[doc_of[has_p]].astype(np.uint32)
+    lens = segs["len"].astype(np.int64)
+    cinc = np.cumsum(lens)
+    start = np.zeros(n_docs, dtype=np.int64)                      # lengths before each document
+    if len(cinc):
+        nz = doc_off[:-1] > 0
+        start[nz] = cinc[doc_off[:-1][nz] - 1]
+    before = (cinc - lens) - start[doc_of]                       # within the document
+    in_header = before < chunk_size
+    n_header = np.zeros(n_docs, dtype=np.int32)
+    np.add.at(n_header, doc_of, in_header.astype(np.int32))
+    return dict(segs=segs, doc_off=doc_off, n_header=n_header, text=text, props=props,
+                min_seq=np.asarray(min_seq, dtype=np.int32), cur_seq=np.asarray(cur_seq, dtype=np.int32))

@@ -106,6 +106,7 @@ class Batch:
         self.doc_off = [0]
         self.seed_off = [0]
         self.seed = []
+        self.clients = []          # per document: long client id -> short id
 
     def _props_rec(self, props, combine=COMBINE_NONE):
         off = len(self.props)
@@ -166,6 +167,7 @@ class Batch:
         """clients: long id -> short id already known for this document (a loaded summary's
         writers, snapshot.SnapshotBatch.clients); new ids continue after them."""
         enc = DocEncoder(self, clients)
+        self.clients.append(enc.short)
         s = seed_text.encode("utf-16-le")
         self.seed.extend(np.frombuffer(s, dtype="<u2").tolist())
         self.seed_off.append(len(self.seed))

@@ -101,6 +101,25 @@ int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, 
 int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,
                       uint64_t n_segs, const uint16_t *text, uint64_t text_len, const uint32_t *props,
                       uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq);
+/* The same in two steps: a device-resident set of decoded summaries (uploaded once), then
+   loads enqueued on the handle's stream (mt_sync waits). */
+typedef struct mt_snapshots mt_snapshots;
+mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header,
+                                  const mt_seg_rec *segs, uint64_t n_segs, const uint16_t *text, uint64_t text_len,
+                                  const uint32_t *props, uint64_t props_len, const int32_t *min_seq,
+                                  const int32_t *cur_seq);
+int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s);
+void mt_snapshots_free(mt_snapshots *s);
+
+/* Summary emission: SnapshotV1.extractSync (snapshotV1.ts:156-252) of every document's
+   current state as mt_seg_rec records in summary order (runs below minSeq coalesced, merge
+   info above it; flags MT_SEG_*), text and props arenas as for mt_load_snapshots (client
+   ids are the documents' short ids).  Two calls: with recs == NULL, io[3*n_docs] receives
+   per document {records, text units, props words}; then, io unchanged, the arrays sized by
+   their sums are filled (documents back to back).  min_seq/cur_seq (nullable) receive the
+   collaboration window -- the header metadata. */
+int mt_extract_snapshots(mt_handle *h, int64_t *io, mt_seg_rec *recs, uint16_t *text, uint32_t *props,
+                         int32_t *min_seq, int32_t *cur_seq);
 
 /* Device-resident batches (bench / pipelined path). */
 mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops,

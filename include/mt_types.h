@@ -74,9 +74,14 @@ typedef struct mt_seg_rec {
     uint32_t props;         /* props record [count, (key, value) x count] or MT_NO_PROPS */
     int16_t client;         /* short id of spec.client, or -2 */
     int16_t removed_client; /* short id of spec.removedClient (when removed_seq is set) */
-    uint8_t flags;          /* MT_F_MARKER */
+    uint8_t flags;          /* MT_F_MARKER | MT_SEG_MERGE_INFO | MT_SEG_HAS_SEQ */
     uint8_t pad[7];
 } mt_seg_rec;
+/* mt_seg_rec.flags written by mt_extract_snapshots (SnapshotV1.extractSync): the spec carries
+   merge info {json, seq?, client?, removedSeq?, removedClient?} (MT/snapshotChunks.ts:61-67);
+   HAS_SEQ: seq/client present (inserted above minSeq) */
+#define MT_SEG_MERGE_INFO 0x10
+#define MT_SEG_HAS_SEQ 0x20
 
 /* Per-document verification checksum: all-gathered across ranks. */
 typedef struct mt_checksum {

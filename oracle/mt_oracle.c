@@ -1283,3 +1283,69 @@ int32_t orc_replay_batch(int32_t n_docs, const int64_t *doc_op_off, const mt_op_
     free(args);
     return 0;
 }
+
+/* ------------------------------------------------------------------ batch load + replay (C5) */
+typedef struct LoadArg {
+    int32_t d0, d1;
+    const int64_t *seg_off;
+    const int32_t *n_header;
+    const mt_seg_rec *segs;
+    const uint16_t *stext;
+    const uint32_t *sprops;
+    const int32_t *min_seq, *cur_seq;
+    const int64_t *doc_op_off;
+    const mt_op_rec *ops;
+    const uint16_t *text;
+    const uint32_t *props;
+    mt_checksum *sum;
+    int32_t *status;
+} LoadArg;
+
+static void *load_worker(void *p) {
+    LoadArg *a = (LoadArg *)p;
+    for (int32_t doc = a->d0; doc < a->d1; doc++) {
+        const int64_t s0 = a->seg_off[doc];
+        orc_doc *d = orc_load(a->segs + s0, a->n_header[doc], (int32_t)(a->seg_off[doc + 1] - s0), a->stext,
+                              a->sprops, a->min_seq[doc], a->cur_seq[doc]);
+        for (int64_t i = a->doc_op_off[doc]; i < a->doc_op_off[doc + 1] && !d->status; i++)
+            if (orc_apply(d, &a->ops[i], a->text, a->props)) break;
+        orc_checksum(d, &a->sum[doc]);
+        a->status[doc] = d->status;
+        orc_free(d);
+    }
+    return NULL;
+}
+
+int32_t orc_load_replay_batch(int32_t n_docs, const int64_t *seg_off, const int32_t *n_header,
+                              const mt_seg_rec *segs, const uint16_t *seg_text, const uint32_t *seg_props,
+                              const int32_t *min_seq, const int32_t *cur_seq, const int64_t *doc_op_off,
+                              const mt_op_rec *ops, const uint16_t *text_arena, const uint32_t *props_arena,
+                              mt_checksum *out_sum, int32_t *out_status, int32_t threads) {
+    if (threads < 1) threads = 1;
+    if (threads > n_docs) threads = n_docs > 0 ? n_docs : 1;
+    pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
+    LoadArg *args = (LoadArg *)calloc(threads, sizeof(LoadArg));
+    for (int t = 0; t < threads; t++) {
+        LoadArg *a = &args[t];
+        a->d0 = (int32_t)((int64_t)n_docs * t / threads);
+        a->d1 = (int32_t)((int64_t)n_docs * (t + 1) / threads);
+        a->seg_off = seg_off;
+        a->n_header = n_header;
+        a->segs = segs;
+        a->stext = seg_text;
+        a->sprops = seg_props;
+        a->min_seq = min_seq;
+        a->cur_seq = cur_seq;
+        a->doc_op_off = doc_op_off;
+        a->ops = ops;
+        a->text = text_arena;
+        a->props = props_arena;
+        a->sum = out_sum;
+        a->status = out_status;
+        pthread_create(&th[t], NULL, load_worker, a);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(args);
+    return 0;
+}

@@ -63,6 +63,13 @@ int32_t orc_replay_batch(int32_t n_docs, const int64_t *doc_op_off, const mt_op_
                          const int64_t *seed_off, const uint16_t *seed_arena,
                          mt_checksum *out_sum, int32_t *out_status, int32_t threads);
 
+/* Config C5 on `threads` host threads: load each document's summary, replay its ops. */
+int32_t orc_load_replay_batch(int32_t n_docs, const int64_t *seg_off, const int32_t *n_header,
+                              const mt_seg_rec *segs, const uint16_t *seg_text, const uint32_t *seg_props,
+                              const int32_t *min_seq, const int32_t *cur_seq, const int64_t *doc_op_off,
+                              const mt_op_rec *ops, const uint16_t *text_arena, const uint32_t *props_arena,
+                              mt_checksum *out_sum, int32_t *out_status, int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

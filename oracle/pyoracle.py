@@ -63,6 +63,8 @@ def lib():
         L.orc_generate.restype = i32
         L.orc_replay_batch.argtypes = [i32, P, P, P, P, P, P, P, P, i32]
         L.orc_replay_batch.restype = i32
+        L.orc_load_replay_batch.argtypes = [i32, P, P, P, P, P, P, P, P, P, P, P, P, P, i32]
+        L.orc_load_replay_batch.restype = i32
         L.orc_load.restype = P
         L.orc_load.argtypes = [P, i32, i32, P, P, i32, i32]
         _lib = L
@@ -174,4 +176,17 @@ def replay_batch(arrays, threads=1):
     a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
     lib().orc_replay_batch(n_docs, _p(a["doc_off"]), _p(a["ops"]), _p(a["text"]), _p(a["props"]),
                            _p(a["seed_off"]), _p(a["seed"]), _p(sums), _p(status), threads)
+    return sums, status
+
+
+def load_replay_batch(load, arrays, threads=1):
+    """Config C5 on the CPU: every document's summary loaded (orc_load), then its ops."""
+    n_docs = len(arrays["doc_off"]) - 1
+    sums = np.zeros(n_docs, dtype=CHECKSUM_DTYPE)
+    status = np.zeros(n_docs, dtype=np.int32)
+    la = {k: np.ascontiguousarray(v) for k, v in load.items()}
+    a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+    lib().orc_load_replay_batch(n_docs, _p(la["doc_off"]), _p(la["n_header"]), _p(la["segs"]), _p(la["text"]),
+                                _p(la["props"]), _p(la["min_seq"]), _p(la["cur_seq"]), _p(a["doc_off"]),
+                                _p(a["ops"]), _p(a["text"]), _p(a["props"]), _p(sums), _p(status), threads)
     return sums, status

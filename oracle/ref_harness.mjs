@@ -426,8 +426,10 @@ async function snapDoc(cfg, doc) {
     const W = cfg.writers;
     const lastRef = new Array(W + 1).fill(0);
     const cseq = new Array(W + 1).fill(0);
+    const msgs = [];
     for (let t = 1; t <= cfg.ops; t++) {
         const [k, tt, r, msn, op, cs] = genStep(rng, cfg, c, t, lastRef, cseq);
+        msgs.push([k, tt, r, msn, op]);
         c.applyMsg(JSON.parse(JSON.stringify(makeMsg(k, tt, r, msn, cs, op))));
     }
     let t0 = cfg.ops;
@@ -438,13 +440,14 @@ async function snapDoc(cfg, doc) {
         for (let j = 1; j <= W; j++) { lastRef[j] = t0; }
         const m = makeMsg(1, t0, t0 - 1, t0, ++cseq[1], null);
         m.type = "noop";
+        msgs.push([1, t0, t0 - 1, t0, null, "noop"]);
         c.applyMsg(m);
     }
     const snap = new SnapshotV1(c.mergeTree, logger);
     snap.extractSync();
     const tree = snap.emit();
     const chunks = treeChunks(tree);
-    const rec = { doc, chunks };
+    const rec = { doc, seed_text: seedText, msgs, chunks };
     let loaded;
     try {
         loaded = await loadClient(tree, {});

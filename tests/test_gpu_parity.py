@@ -165,3 +165,30 @@ def test_gpu_snapshot_load_matches_reference(name, tier):
         if errs:
             bad.append((doc["doc"], errs))
     assert not bad, f"{name}: {bad[:4]}"
+
+
+@pytest.mark.parametrize("tier", ["lds", "paged"])
+@pytest.mark.parametrize("name", ["ref_snap", "ref_snap_body"])
+def test_gpu_snapshot_emission_matches_reference(name, tier):
+    """SnapshotV1 emission from device state (mt_extract_snapshots = extractSync, then
+    snapshot.encode_chunks = emit): the summary of the replayed observer equals, byte for
+    byte, the one the reference wrote for the same op stream."""
+    from fluidframework_amd.snapshot import encode_chunks, record_specs
+    from fluidframework_amd.wire import Batch, compact_msgs_to_dicts
+    fx = gu.load(name)
+    interner = gu.Interner()
+    b = Batch(interner)
+    for doc in fx["docs"]:
+        b.add_doc(doc["seed_text"], compact_msgs_to_dicts(doc["msgs"]))
+    a = b.arrays()
+    mt = _gpu_batch(len(fx["docs"]), **TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    snaps = mt.extract_snapshots()
+    for i, doc in enumerate(fx["docs"]):
+        names = {v: k for k, v in b.clients[i].items()}
+        s = snaps[i]
+        specs, lengths = record_specs(s["segs"], s["text"], s["props"], interner, names)
+        got = encode_chunks(specs, lengths, s["min_seq"], s["cur_seq"], fx["config"]["chunk"])
+        assert got == doc["chunks"], (name, doc["doc"])

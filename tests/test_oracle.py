@@ -81,3 +81,21 @@ def test_snapshot_decoder_totals():
             snap = decode_chunks(doc["chunks"])
             meta = to_latest_version("header", _json.loads(doc["chunks"]["header"]))["headerMetadata"]
             assert len(snap.header_specs) + len(snap.body_specs) == meta["totalSegmentCount"]
+
+
+@pytest.mark.parametrize("name", ["ref_snap", "ref_snap_body"])
+def test_snapshot_encoder_round_trip(name):
+    """encode_chunks(decode(summary)) reproduces the reference's SnapshotV1.emit output
+    byte for byte (the summaries in the fixtures were written by the reference)."""
+    from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks, encode_chunks, record_specs
+    fx = gu.load(name)
+    cs = fx["config"]["chunk"]
+    for doc in fx["docs"]:
+        interner = gu.Interner()
+        sb = SnapshotBatch(interner)
+        snap = decode_chunks(doc["chunks"])
+        short = sb.add_doc(snap)
+        a = sb.arrays()
+        names = {v: k for k, v in short.items()}
+        specs, lengths = record_specs(a["segs"], a["text"], a["props"], interner, names)
+        assert encode_chunks(specs, lengths, snap.min_seq, snap.cur_seq, cs) == doc["chunks"], doc["doc"]
