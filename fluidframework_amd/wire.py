@@ -87,11 +87,13 @@ class DocEncoder:
     def __init__(self, batch, short=None):
         self.batch = batch
         self.short = dict(short) if short else {}
+        self.next = 1 + max(self.short.values(), default=0)   # the observer is 0
 
     def client(self, long_id):
         s = self.short.get(long_id)
         if s is None:
-            s = self.short[long_id] = len(self.short) + 1     # observer is 0
+            s = self.short[long_id] = self.next
+            self.next += 1
         return s
 
 

@@ -18,10 +18,15 @@
 //   node oracle/ref_harness.mjs replay <logs.json> <out.json>
 //   node oracle/ref_harness.mjs snap <config.json> <doc_begin> <doc_end> <out.json>
 //   node oracle/ref_harness.mjs loadfile <config.json> <out.json> <snapshot.json>...
+//   node oracle/ref_harness.mjs farm <out.json> <maxClients> <minLength>...
 import fs from "fs";
 import * as MT from "./_ref/mt/index.mjs";
 import { SnapshotV1 } from "./_ref/mt/snapshotV1.mjs";
 import { MockStorage } from "./_ref/shims/test-runtime-utils.mjs";
+import random from "./_ref/shims/random-js.mjs";
+import { annotateRange, insertAtRefPos, removeRange, runMergeTreeOperationRunner, generateClientNames }
+    from "./_ref/mt/test/mergeTreeOperationRunner.mjs";
+import { TestClient } from "./_ref/mt/test/testClient.mjs";
 
 const { Client, TextSegment, Marker } = MT;
 
@@ -504,6 +509,45 @@ async function loadFileDoc(path, cfg, doc) {
     return rec;
 }
 
+// ---------------------------------------------------------------- conflict farm (config C1)
+// The reference's own randomized convergence farm (MTT/client.conflictFarm.spec.ts with its
+// defaultOptions and seeds), run unchanged; client 0 only applies remote ops (the observer
+// baseline, MTT/mergeTreeOperationRunner.ts:107-109).  Every message it receives -- and its
+// direct updateMinSeq(seq) calls between runner passes, recorded as non-op messages -- is
+// the op log; its final state is the expected output.
+async function farmDoc(minLength, maxClients, doc) {
+    const opts = {
+        minLength: { min: minLength, max: minLength }, clients: { min: 1, max: maxClients },
+        opsPerRoundRange: { min: 1, max: 128 }, rounds: 8,
+        operations: [removeRange, annotateRange, insertAtRefPos], growthFunc: (x) => x * 2,
+    };
+    const clientNames = generateClientNames();
+    const mt = random.engines.mt19937();
+    mt.seedWithArray([0xDEADBEEF, 0xFEEDBED, minLength]);
+    const clients = [new TestClient({ blockUpdateMarkers: true })];
+    clients.forEach((c, i) => c.startOrUpdateCollaboration(clientNames[i]));
+    const obs = clients[0];
+    const msgs = [];
+    const apply = obs.applyMsg.bind(obs);
+    obs.applyMsg = (m) => {
+        msgs.push([m.clientId, m.sequenceNumber, m.referenceSequenceNumber, m.minimumSequenceNumber,
+            JSON.parse(JSON.stringify(m.contents)), m.type]);
+        return apply(m);
+    };
+    const deltas = attachDeltas(obs);
+    let seq = 0;
+    while (clients.length < opts.clients.max) {
+        clients.forEach((c) => c.updateMinSeq(seq));
+        msgs.push(["A", seq, seq, seq, null, "noop"]);
+        const target = Math.max(opts.clients.min, opts.growthFunc(clients.length));
+        for (let cc = clients.length; cc < target; cc++) {
+            clients.push(await TestClient.createFromClientSnapshot(clients[0], clientNames[cc]));
+        }
+        seq = runMergeTreeOperationRunner(mt, seq, clients, minLength, opts);
+    }
+    return { doc, minLength, seed_text: "", msgs, observer_name: clientNames[0], out: collectOutputs(obs, deltas) };
+}
+
 const [mode, ...rest] = process.argv.slice(2);
 async function main() {
     if (mode === "gen") {
@@ -522,6 +566,12 @@ async function main() {
         const docs = [];
         for (let d = d0; d < d1; d++) { docs.push(await snapDoc(cfg, d)); }
         fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
+    } else if (mode === "farm") {
+        // farm <out.json> <maxClients> <minLength>...
+        const docs = [];
+        const maxClients = parseInt(rest[1], 10);
+        for (let i = 2; i < rest.length; i++) { docs.push(await farmDoc(parseInt(rest[i], 10), maxClients, i - 2)); }
+        fs.writeFileSync(rest[0], JSON.stringify({ config: { farm: true, clients: maxClients }, docs }));
     } else if (mode === "loadfile") {
         const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const docs = [];

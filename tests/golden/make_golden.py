@@ -7,7 +7,7 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py [--snapshots]
+    python3 tests/golden/make_golden.py [--snapshots | --farm]
 """
 import gzip
 import json
@@ -90,10 +90,32 @@ def make_snapshot_fixtures():
     print("ref_snap_files", len(data["docs"]), "docs")
 
 
+# Config C1: the reference's conflict farm (MTT/client.conflictFarm.spec.ts defaultOptions,
+# its seeds) run unchanged; the fixture is client 0's (the observer's) message stream.
+FARM_MIN_LENGTHS = [1, 16, 512]
+FARM_MAX_CLIENTS = 8
+
+
+def make_farm_fixture():
+    with tempfile.TemporaryDirectory() as td:
+        op = os.path.join(td, "out.json")
+        subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "farm", op,
+                               str(FARM_MAX_CLIENTS)] + [str(m) for m in FARM_MIN_LENGTHS])
+        data = json.load(open(op))
+    data["config"]["ext"] = True          # real (non-synthetic) property interning
+    for d in data["docs"]:
+        d["out"].pop("tree", None)
+    _dump("ref_farm", data)
+    print("ref_farm", len(data["docs"]), "docs", sum(len(d["msgs"]) for d in data["docs"]), "messages")
+
+
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
     if "--snapshots" in sys.argv[1:]:
         make_snapshot_fixtures()
+        return
+    if "--farm" in sys.argv[1:]:
+        make_farm_fixture()
         return
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
     for name, (base, over, ndocs) in FIXTURES.items():
@@ -113,6 +135,7 @@ def main():
             json.dump(data, fh, separators=(",", ":"))
         print(name, ndocs, "docs")
     make_snapshot_fixtures()
+    make_farm_fixture()
 
 
 if __name__ == "__main__":

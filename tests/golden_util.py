@@ -12,7 +12,7 @@ from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INT_MIN = -2 ** 31
-ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long"]
+ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm"]
 SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
 
 
@@ -28,7 +28,9 @@ def interner_for(fixture):
 def encode_docs(fixture, interner, docs=None):
     b = Batch(interner)
     for d in (fixture["docs"] if docs is None else docs):
-        b.add_doc(d["seed_text"], compact_msgs_to_dicts(d["msgs"]))
+        # a farm's observer (client 0) has its own long id: short id 0, as in the reference
+        own = {f"client-{d['observer_name']}": 0} if "observer_name" in d else None
+        b.add_doc(d["seed_text"], compact_msgs_to_dicts(d["msgs"]), clients=own)
     return b.arrays()
 
 
