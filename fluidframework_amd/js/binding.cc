@@ -181,6 +181,38 @@ napi_value ApplyOps(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// loadSnapshots(h, docSegOff: BigInt64Array, nHeader: Int32Array, segs: Uint8Array (32-byte
+//               mt_seg_rec), text: Uint16Array, props: Uint32Array, minSeq: Int32Array,
+//               curSeq: Int32Array) -- Client.load of a decoded summary into every document
+//               (mt_load_snapshots; snapshotLoader.ts:36-228)
+napi_value LoadSnapshots(napi_env env, napi_callback_info info) {
+    napi_value argv[8];
+    if (!get_args(env, info, 8, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *off, *nh, *segs, *txt, *props, *mn, *cu;
+    size_t noff, nnh, nsegs, ntxt, nprops, nmn, ncu;
+    if (!typed(env, argv[1], &off, &noff) || !typed(env, argv[2], &nh, &nnh) || !typed(env, argv[3], &segs, &nsegs) ||
+        !typed(env, argv[4], &txt, &ntxt) || !typed(env, argv[5], &props, &nprops) || !typed(env, argv[6], &mn, &nmn) ||
+        !typed(env, argv[7], &cu, &ncu))
+        return nullptr;
+    const uint32_t nd = mt_num_docs(hd->h);
+    if (noff != nd + 1 || nnh != nd || nmn != nd || ncu != nd || nsegs % sizeof(mt_seg_rec) != 0) {
+        napi_throw_range_error(env, nullptr, "one summary per document; segs whole 32-byte records");
+        return nullptr;
+    }
+    const uint64_t n_recs = (uint64_t)((const int64_t *)off)[nd];
+    if (n_recs * sizeof(mt_seg_rec) > nsegs) {
+        napi_throw_range_error(env, nullptr, "docSegOff exceeds segs");
+        return nullptr;
+    }
+    const int rc = mt_load_snapshots(hd->h, (const int64_t *)off, (const int32_t *)nh, (const mt_seg_rec *)segs, n_recs,
+                                     (const uint16_t *)txt, ntxt, (const uint32_t *)props, nprops,
+                                     (const int32_t *)mn, (const int32_t *)cu);
+    if (rc) return throw_rc(env, hd, rc, "mt_load_snapshots");
+    return nullptr;
+}
+
 // status(h) -> Int32Array[nDocs]   (enum mt_doc_status)
 napi_value Status(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -307,7 +339,7 @@ napi_value Init(napi_env env, napi_value exports) {
         const char *name;
         napi_callback fn;
     } fns[] = {{"create", Create},         {"destroy", Destroy},           {"loadInitialText", LoadInitialText},
-               {"applyOps", ApplyOps},     {"status", Status},             {"getLength", GetLength},
+               {"applyOps", ApplyOps},     {"loadSnapshots", LoadSnapshots},     {"status", Status},             {"getLength", GetLength},
                {"getText", GetText},       {"getPropRuns", GetPropRuns},   {"getDeltaLog", GetDeltaLog},
                {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs}};
     for (auto &f : fns) {

@@ -221,6 +221,6 @@ class BatchEncoder {
 }
 
 module.exports = {
-    BatchEncoder, Interner, canonical,
+    BatchEncoder, Interner, Grow, canonical,
     OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_GROUP_MORE, F_MARKER, NO_PROPS, VAL_NULL, VAL_FALSY_BIT,
 };

@@ -18,7 +18,8 @@
  */
 const assert = require("assert");
 const path = require("path");
-const { BatchEncoder, Interner, VAL_NULL } = require("./encode");
+const { BatchEncoder, Interner, Grow, VAL_NULL } = require("./encode");
+const { SnapshotEncoder, decodeChunks, treeChunks } = require("./snapshot");
 
 const native = require(path.join(__dirname, "mtreplay.node"));
 
@@ -71,6 +72,35 @@ class GpuMergeTreeBatch {
         off[this.nDocs] = BigInt(k);
         native.loadInitialText(this.h, off, seed);
         this.logPos.fill(0);
+    }
+
+    /**
+     * Client.load for every document (client.ts:938-946 -> SnapshotLoader.initialize,
+     * snapshotLoader.ts:36-228): summaries[d] is a summary ITree (a SharedString's, or
+     * SnapshotV1.emit's) or its {path: contents} blobs.  Replaces every document's state;
+     * legacy catch-up messages are queued like SharedSegmentSequence.loadCore applies them.
+     * A summary the reference cannot load fails that document the same way.
+     */
+    loadSnapshots(summaries) {
+        assert(summaries.length === this.nDocs);
+        this.flush();
+        const enc = new SnapshotEncoder(this.interner, Grow);
+        const decoded = summaries.map((s) => decodeChunks(s.entries ? treeChunks(s) : s));
+        decoded.forEach((snap, d) => {
+            this.clients[d] = new Map();
+            enc.addDoc(snap, this.clients[d]);
+        });
+        const a = enc.arrays();
+        native.loadSnapshots(this.h, a.docSegOff, a.nHeader, a.segs, a.text, a.props, a.minSeq, a.curSeq);
+        this.failed.fill(0);
+        this.logPos.fill(0);
+        const st = native.status(this.h);
+        for (let d = 0; d < this.nDocs; d++) {
+            if (st[d] !== 0) { this.failed[d] = st[d]; }
+            const v = this.views.get(d);
+            if (v) { v.currentSeq = decoded[d].curSeq; }
+            for (const m of decoded[d].catchup) { this.pending[d].push(m); this.queued++; }
+        }
     }
 
     client(doc) {

@@ -2,6 +2,7 @@
 // Test driver for the Node facade (fluidframework_amd/js).  Usage:
 //   node tests/js/fixture_tool.js encode <fixture.json.gz>   -> JSON {ops,text,props,docOff} (hex)
 //   node tests/js/fixture_tool.js replay <fixture.json.gz>   -> JSON per doc {text,length,status,props}
+//   node tests/js/fixture_tool.js loadsnap <snapshot fixture> -> the same after loadSnapshots + tail
 // The fixtures were produced by the reference itself (tests/golden/make_golden.py).
 const fs = require("fs");
 const zlib = require("zlib");
@@ -51,4 +52,36 @@ if (mode === "encode") {
         }
     });
     process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }));
+} else if (mode === "snapenc") {
+    const { SnapshotEncoder, decodeChunks } = require(path.join(repo, "fluidframework_amd", "js", "snapshot.js"));
+    const { Grow } = require(path.join(repo, "fluidframework_amd", "js", "encode.js"));
+    const enc = new SnapshotEncoder(new Interner(), Grow);
+    for (const d of fx.docs) { enc.addDoc(decodeChunks(d.chunks), new Map()); }
+    const a = enc.arrays();
+    process.stdout.write(JSON.stringify({
+        segs: hex(a.segs.subarray(0, a.nSegs * 32)), text: hex(a.text), props: hex(a.props),
+        docSegOff: Array.from(a.docSegOff, Number), nHeader: Array.from(a.nHeader),
+        minSeq: Array.from(a.minSeq), curSeq: Array.from(a.curSeq),
+    }));
+} else if (mode === "loadsnap") {
+    // summaries (snapshot fixtures: reference-written chunks) loaded through
+    // GpuMergeTreeBatch.loadSnapshots, then the tail messages through GpuClient.applyMsg
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const docs = fx.docs.filter((d) => !d.error || d.error.startsWith("MergeTree insert failed"));
+    const batch = new GpuMergeTreeBatch(docs.length, { segCapacity: 4096, textCapacity: 1 << 17 });
+    batch.loadSnapshots(docs.map((d) => d.chunks));
+    const out = docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("loader");
+        try {
+            for (const m of msgs({ msgs: d.tail || [] })) { c.applyMsg(m); }
+            const len = c.getLength();
+            const probe = [];
+            for (let p = 0; p < len; p += Math.max(1, Math.floor(len / 7))) { probe.push([p, c.getPropertiesAtPosition(p) || null]); }
+            return { doc: d.doc, text: c.getText(), length: len, props: probe };
+        } catch (e) {
+            return { doc: d.doc, error: e.message, type: e.constructor.name };
+        }
+    });
+    process.stdout.write(JSON.stringify({ docs: out }));
 }

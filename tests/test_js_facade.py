@@ -76,3 +76,52 @@ def test_js_facade_replays_fixture_like_reference(name):
         for p, props in g["props"]:
             exp = next((r[2] for r in runs if r[0] <= p < r[0] + r[1]), None)
             assert props == exp, (p, props, exp)
+
+
+@pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
+def test_js_snapshot_decoder_matches_python(name):
+    """The Node facade's summary decoder (js/snapshot.js) writes exactly the mt_seg_rec records
+    and arenas of fluidframework_amd/snapshot.py for the reference-written summaries."""
+    fx = gu.load(name)
+    got = _node("snapenc", os.path.join(gu.GOLDEN, name + ".json.gz"))
+    from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks
+    sb = SnapshotBatch(gu.Interner())
+    for d in fx["docs"]:
+        sb.add_doc(decode_chunks(d["chunks"]))
+    a = sb.arrays()
+    assert bytes.fromhex(got["segs"]) == a["segs"].tobytes()
+    assert got["docSegOff"] == a["doc_off"].tolist() and got["nHeader"] == a["n_header"].tolist()
+    assert got["minSeq"] == a["min_seq"].tolist() and got["curSeq"] == a["cur_seq"].tolist()
+    n_text = len(bytes.fromhex(got["text"])) // 2
+    assert bytes.fromhex(got["text"]) == a["text"][:n_text].tobytes()
+    n_props = len(bytes.fromhex(got["props"])) // 4
+    assert bytes.fromhex(got["props"]) == a["props"][:n_props].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
+def test_js_facade_loads_snapshots_like_reference(name):
+    """GpuMergeTreeBatch.loadSnapshots (Client.load for every document) + GpuClient.applyMsg of
+    the tails: text, length and properties equal the reference's; the reference's load
+    failures throw "MergeTree insert failed"."""
+    _addon()
+    fx = gu.load(name)
+    got = {g["doc"]: g for g in _node("loadsnap", os.path.join(gu.GOLDEN, name + ".json.gz"))["docs"]}
+    for d in fx["docs"]:
+        want = gu.snap_status(d)
+        if want is None:
+            continue
+        g = got[d["doc"]]
+        if want:
+            assert g.get("error", "").startswith("MergeTree insert failed"), g
+            continue
+        assert "error" not in g, g
+        assert g["text"] == d["out"]["text"] and g["length"] == d["out"]["length"]
+        runs, pos = [], 0
+        for s in d["out"]["segs"]:
+            if s["rseq"] is None:
+                runs.append((pos, s["len"], s["props"]))
+                pos += s["len"]
+        for p, props in g["props"]:
+            exp = next((r[2] for r in runs if r[0] <= p < r[0] + r[1]), None)
+            assert props == exp, (p, props, exp)
