@@ -148,6 +148,9 @@ __device__ __forceinline__ u64 fnv_u64(u64 h, u64 x) {
     return fnv_u32(h, (uint32_t)(x >> 32));
 }
 
+// writer short id (sign-extended: loaded summaries append as NonCollabClient = -2)
+__device__ __forceinline__ int op_cli(const mt_op_rec &op) { return (int)(int16_t)op.client; }
+
 // ------------------------------------------------------------------ segment fields
 __device__ __forceinline__ int seg_cli(v4i a) { return (int)(short)(a.w & 0xFFFF); }
 __device__ __forceinline__ int seg_rcli(v4i a) { return (int)(short)((uint32_t)a.w >> 16); }

@@ -26,8 +26,12 @@ template <bool kLogT> struct TierLdsT {
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = false;
+    // removedClientOverlap masks of short ids 1..32 (4 bytes per segment in LDS); a
+    // document that needs ids 33..64 continues in the next tier (lds_room / load_doc)
+    static constexpr int kOvlBits = 32;
+    typedef uint32_t O_v;
     typedef LDS_AS v4i *A_t;
-    typedef LDS_AS u64 *O_t;
+    typedef LDS_AS uint32_t *O_t;
     typedef LDS_AS v4u *B_t;
     typedef LDS_AS v2i *H_t;
 };
@@ -35,6 +39,8 @@ template <bool kLogT> struct TierGlbT {
     static constexpr bool kLds = false;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = false;
+    static constexpr int kOvlBits = 64;
+    typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
     typedef GLB_AS v4u *B_t;
@@ -47,6 +53,8 @@ template <bool kLogT> struct TierPagedT {
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;
+    static constexpr int kOvlBits = 64;
+    typedef u64 O_v;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS u64 *O_t;
     typedef LDS_AS v4u *B_t;
@@ -129,6 +137,19 @@ __device__ unsigned long long g_prof[32];
     }
 #endif
 
+// MT_PROF2 (with MT_PROF, flat documents only): finer timers in paged slots 9..15
+#if defined(MT_PROF) && defined(MT_PROF2)
+#define P2_T0(k) const unsigned long long _p2##k = __builtin_amdgcn_s_memtime();
+#define P2_T1(k)                                                         \
+    if (lane() == 0) {                                                   \
+        d.prof[k] += __builtin_amdgcn_s_memtime() - _p2##k;              \
+        d.prof[16 + k] += 1ull;                                          \
+    }
+#else
+#define P2_T0(k)
+#define P2_T1(k)
+#endif
+
 // Makes the document's uniform state opaque to the optimiser at the top of every message:
 // nothing derived from it is hoisted across messages (hoisted loop invariants of the fully
 // inlined engine were spilling hundreds of SGPRs).
@@ -158,6 +179,15 @@ TD void opaque(DocT<T> &d) {
     opq_ptr(d.A); opq_ptr(d.O); opq_ptr(d.Bv); opq_ptr(d.heap);
 }
 
+// B-tree counts of the flat tiers: level 0 holds up to B blocks, level 1 B/2, higher
+// levels B/4 (each level has at most ~1/4 of the blocks below plus the lds_room margin); the
+// paged upper instance keeps MT_LV x B (its level 1 = pages).
+static __host__ __device__ inline int cnt_cap(int B, int l) { return l == 0 ? B : (l == 1 ? B / 2 : B / 4); }
+static __host__ __device__ inline int cnt_off(int B, int l) { return l == 0 ? 0 : (l == 1 ? B : B + B / 2 + (l - 2) * (B / 4)); }
+static __host__ __device__ inline int cnt_bytes(int B) { return cnt_off(B, MT_LV); }
+// level-0 block ends alias the 256-byte scratch when they fit (range_mark only)
+static __host__ __device__ inline bool ends_in_scr(bool seg_in_lds, int B) { return seg_in_lds && 2 * B <= 256; }
+
 // Per-launch LDS layout of one document (host and device agree on it).
 struct LdsLayout {
     uint32_t offA, offO, offB, offH, offCnt, offFlg, offEnds, offScr, offNb, offGen, offProf, total;
@@ -168,7 +198,7 @@ static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, i
     if (seg_in_lds) {
         L.offA = o; o += 16u * S;
         L.offB = o; o += 16u * S;
-        L.offO = o; o += 8u * S;
+        L.offO = o; o += 4u * S;   // u32 overlap masks (TierLdsT::kOvlBits)
         L.offH = o; o += 8u * (H + 1);
     } else {
         L.offA = L.offB = L.offO = L.offH = 0;
@@ -176,8 +206,9 @@ static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, i
     L.offScr = o; o += 64u * 4;
     L.offNb = o; o += MT_LV * 4;
     L.offGen = o; o += 4u * gen_words;
-    L.offEnds = o; o += 2u * B;
-    L.offCnt = o; o += (uint32_t)MT_LV * B;
+    L.offEnds = ends_in_scr(seg_in_lds, B) ? L.offScr : o;
+    if (!ends_in_scr(seg_in_lds, B)) o += 2u * B;
+    L.offCnt = o; o += (uint32_t)cnt_bytes(B);
     L.offFlg = o; o += (uint32_t)B;
 #ifdef MT_PROF
     o = (o + 7u) & ~7u;
@@ -206,7 +237,19 @@ TD void fail_cap(DocT<T> &d, int cause) {
     fail(d, T::kLds ? MT_DOC_RETRY : MT_DOC_CAPACITY);
 }
 
-TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) { return d.cnt + l * d.B_cap; }
+TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) {
+    if constexpr (T::kPaged)
+        return d.cnt + l * d.B_cap;
+    else
+        return d.cnt + cnt_off(d.B_cap, l);
+}
+// capacity of level l
+TD int bcap(DocT<T> &d, int l) {
+    if constexpr (T::kPaged)
+        return d.B_cap;
+    else
+        return cnt_cap(d.B_cap, l);
+}
 // wave-uniform reads of LDS state (kept in SGPRs)
 TD int nbr(DocT<T> &d, int l) { return uni(d.nb[l]); }
 TD int cntr(DocT<T> &d, int l, int b) { return uni(lvl(d, l)[b]); }
@@ -272,14 +315,19 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
         d.cap_cause = 6;
         return false;
     }
-    int maxnb = 0;
+    bool over = false;
 #pragma unroll
-    for (int l = 0; l < MT_LV; l++) maxnb = max(maxnb, h.n_blk[l]);
+    for (int l = 0; l < MT_LV; l++) over = over || h.n_blk[l] > cnt_cap(T::kLds ? B_l : st.B, l);
+    if (!T::kLds && over) {   // cannot happen: the HBM tier's levels are sized for st.B
+        d.status = MT_DOC_CAPACITY;
+        d.cap_cause = 2;
+        return true;
+    }
     if (T::kLds) {
         d.S_cap = S_l;
         d.B_cap = B_l;
         d.H_cap = H_l;
-        if (d.n > S_l || maxnb > B_l || d.heap_n > H_l) {
+        if (d.n > S_l || over || d.heap_n > H_l) {
             d.status = MT_DOC_RETRY;
             d.cap_cause = 6;
             return false;
@@ -292,10 +340,18 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
         GLB_AS const v4u *gB = (GLB_AS const v4u *)(st.segB + doc * S);
         GLB_AS const u64 *gO = (GLB_AS const u64 *)(st.segO + doc * S);
         GLB_AS const v2i *gH = (GLB_AS const v2i *)(st.heap + doc * (size_t)(st.H + 1));
+        bool wide = false;
         for (int i = lane(); i < d.n; i += MT_WAVE) {
             d.A[i] = gA[i];
             d.Bv[i] = gB[i];
-            d.O[i] = gO[i];
+            const u64 o = gO[i];
+            wide = wide || (o >> T::kOvlBits) != 0ull;
+            d.O[i] = (typename T::O_v)o;
+        }
+        if (ballot(wide)) {   // overlap ids above the LDS tier's masks
+            d.status = MT_DOC_RETRY;
+            d.cap_cause = 6;
+            return false;
         }
         for (int i = 1 + lane(); i <= d.heap_n; i += MT_WAVE) d.heap[i] = gH[i];
     } else {
@@ -536,7 +592,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
             d.pend_split = 1;
             return;
         }
-        if (nbr(d, l) + 1 > d.B_cap) {
+        if (nbr(d, l) + 1 > bcap(d, l)) {
             fail_cap(d, 2);
             return;
         }
@@ -583,7 +639,7 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
 // Replace entries [b0, b0 + nold) of level l with k entries sized base (+1 for the first
 // `extra`), as pack :1414-1446 does; new level-0 blocks have needsScour undefined.
 TD void blk_replace(DocT<T> &d, int l, int b0, int nold, int k, int base, int extra) {
-    if (nbr(d, l) + (k - nold) > d.B_cap) {
+    if (nbr(d, l) + (k - nold) > bcap(d, l)) {
         fail_cap(d, 2);
         return;
     }
@@ -1204,6 +1260,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
         const bool need_nl = cand && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
         if (ballot(need_nl)) {
+            P2_T0(9)
             gsync_rd();
             if (need_nl) {
                 const uint16_t ch = text_base(d, d.text_half)[b.x + a.x - 1];
@@ -1211,6 +1268,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
                 d.Bv[s + k].w = b.w;
             }
             wsync<T>();
+            P2_T1(9)
         }
     }
     const u64 m_cand = ballot(cand);
@@ -1243,6 +1301,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     const u64 m_surv = ballot(surv);
     const u64 above = (k < 63) ? (m_join >> (k + 1)) : 0ull;
     const u64 m_grp = ballot(surv && (above & 1ull));
+    P2_T0(10)
     if (m_grp) {
         // group length of each keeper: inclusive lengths up to the group's last member
         const int L = wave_scan_incl(in ? a.x : 0);
@@ -1324,6 +1383,8 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
             wsync<T>();
         }
     }
+    P2_T1(10)
+    P2_T0(11)
     const int keep = __popcll(m_surv);
     if (keep < tot) {
         // compaction: survivors to the front, tail moved left
@@ -1346,6 +1407,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         seg_move_left(d, s + tot, tot - keep);
         d.n -= tot - keep;
     }
+    P2_T1(11)
     // survivors per block
     {
         int st = 0;
@@ -1452,10 +1514,12 @@ TD void zamboni(DocT<T> &d) {
         if (top.x > d.min_seq) break;
         heap_pop(d);
         wsync<T>();
+        P2_T0(12)
         const int i = find_uid(d, (uint32_t)top.y);
         if (i < 0) continue;
         int bstart;
         const int b = blk_find(d, 0, i, true, bstart);
+        P2_T1(12)
         if (b < 0) {
             FAIL_INTERNAL(d);
             return;
@@ -1487,7 +1551,10 @@ TD bool lds_room(DocT<T> &d, const mt_op_rec &op) {
     int need_heap = op.kind == MT_OP_INSERT ? 1 : nb0 + 3;
     if (d.heap_n + need_heap > d.H_cap) return false;
     bool ok = true;
-    for (int l = 0; l < d.depth; l++) ok = ok && nbr(d, l) + 3 + 24 <= d.B_cap;
+    for (int l = 0; l < d.depth; l++) ok = ok && nbr(d, l) + 3 + 24 <= bcap(d, l);
+    // an overlapping remove by a short id above the LDS tier's u32 masks
+    const int oc = op_cli(op);
+    if (op.kind == MT_OP_REMOVE && oc > T::kOvlBits && oc <= 64) ok = false;
     return ok;
 }
 
@@ -1499,9 +1566,6 @@ struct OpIn {
     bool pay_ok;
     bool nl;
 };
-
-// writer short id (sign-extended: loaded summaries append as NonCollabClient = -2)
-__device__ __forceinline__ int op_cli(const mt_op_rec &op) { return (int)(int16_t)op.client; }
 
 __device__ __forceinline__ uint16_t pay_unit(const OpIn &in, int j) {
     const u64 w = j < 4 ? (in.pay_lo >> (16 * j)) : (in.pay_hi >> (16 * (j - 4)));
@@ -1531,6 +1595,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     if (slen > 0 && !marker && !text_ensure(d, slen)) return;
     if (slen > 0 && op.props != MT_NO_PROPS && !props_ensure(d, 1)) return;
     // pass: split point, first index with prefix >= p, first tie-able index at prefix == p
+    P2_T0(13)
     int carry = 0, split_i = -1, split_q = 0, ip = -1, js = -1;
     for (int base = 0; base < d.n; base += MT_WAVE) {
         const int i = base + lane();
@@ -1558,6 +1623,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         carry += bcast(inc, MT_WAVE - 1);
         if (ballot(v && pex > p)) break;
     }
+    P2_T1(13)
     if (split_i >= 0) {
         split_seg(d, split_i, split_q);
         if (d.status) return;
@@ -1631,7 +1697,9 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         d.text_top += slen;
         segw = SEGF_NL_KNOWN | (in.nl ? SEGF_NL : 0u);
     }
+    P2_T0(15)
     seg_move_right(d, x, 1);
+    P2_T1(15)
     const uint32_t uid = (uint32_t)d.next_uid;
     if (lane() == 0) {
         d.A[x] = v4i{slen, seq, MT_RSEQ_NONE, pack_cli(c, 0)};
@@ -1767,13 +1835,15 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         const int pex = carry + inc - vl, pin_ = carry + inc;
         const bool sel = v && vl > 0 && pex < p2 && pin_ > p1;
         const u64 sel_m = ballot(sel);
-        bool newly = false, bad = false;
+        bool newly = false, bad = false, spill = false;
         if (rem && sel) {
             if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
                 if (c < 1 || c > 64)
                     bad = true;
+                else if (c > T::kOvlBits)
+                    spill = true;
                 else
-                    d.O[i] = o | (1ull << (c - 1));
+                    d.O[i] = (typename T::O_v)(o | (1ull << (c - 1)));
             } else {
                 newly = true;
                 a.z = seq;
@@ -1796,6 +1866,10 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         }
         if (ballot(bad)) {
             fail(d, MT_DOC_CAPACITY);
+            return true;
+        }
+        if (ballot(spill)) {   // (the generator's LDS tier: the document restarts in HBM)
+            fail_cap(d, 1);
             return true;
         }
         if (!rem) d.props_top += __popcll(sel_m);
@@ -1878,7 +1952,9 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
     if (d.status) return;
     Cb cb = cb_begin(d, seq, op.kind);
     int carry = 0, ocarry = 0;
+    P2_T0(14)
     range_mark(d, op, rec, carry, ocarry, cb);
+    P2_T1(14)
     if (d.status) return;
     cb_end(d, cb);
     // zamboni runs in apply_op (single inlined site)
