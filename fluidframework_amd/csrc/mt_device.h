@@ -99,7 +99,9 @@ struct DevState {
 };
 
 // ------------------------------------------------------------------ wave primitives
-__device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+// lane within the wavefront (the LDS-tier replay may hold several documents per workgroup,
+// one per wave)
+__device__ __forceinline__ int lane() { return (int)(threadIdx.x & (MT_WAVE - 1)); }
 
 // Inclusive prefix sum over the wavefront with DPP row shifts + row broadcasts (6 VALU
 // ops, no LDS traffic).  Lanes that have no source read the identity (bound_ctrl off,

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -181,17 +182,22 @@ struct TierCaps {
 // LDS capacities cannot overflow while applying it.  If they could, the LDS state is
 // spilled to HBM and the document continues from that message in the TierGlb launch
 // (retry[doc] = 1, resume[doc] = message index).
-template <class T>
-__global__ void __launch_bounds__(MT_WAVE) k_replay(DevState st, const mt_op_rec *ops,
-                                                    const int64_t *off, const uint16_t *tin,
-                                                    const uint32_t *pin, TierCaps caps) {
+//
+// WPG documents per workgroup, one per wave, each with its own LDS slice; the waves never
+// synchronise (more documents per CU than its workgroup limit of 16 would allow).
+template <class T, int WPG>
+__global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_op_rec *ops,
+                                                          const int64_t *off, const uint16_t *tin,
+                                                          const uint32_t *pin, TierCaps caps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
-    const int doc = blockIdx.x;
+    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 0);
+    // wave-uniform (SGPR) document index and LDS slice
+    const int wv = WPG == 1 ? 0 : uni((int)(threadIdx.x >> 6));
+    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw + (uint32_t)(wv * (int)L.total);
+    const int doc = (int)blockIdx.x * WPG + wv;
     if (doc >= st.n_docs) return;
     if (!T::kLds && !st.retry[doc]) return;
     if (!T::kLds && lane() == 0) atomicAdd(st.stats, 1u);
-    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 0);
     const int64_t k1 = off[doc + 1];
     const int64_t k0 = (T::kLds || !caps.resume) ? off[doc] : st.resume[doc];
     DocT<T> d;
@@ -949,6 +955,9 @@ struct mt_handle {
     DevState st{};
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_load = nullptr;
+    // documents per workgroup of the LDS-tier replay (env MT_WPG=2 for two): measured on C2
+    // the CU saturates at 16 resident documents (16 -> 18 per CU: 61.8 -> 64.6 ms)
+    int wpg = 1;
     float last_ms = 0.f;
     bool timed = false;      // ev0/ev1 bracket a launch not yet read by mt_sync
     std::string err;
@@ -1004,6 +1013,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.T = o.text_capacity > 0 ? o.text_capacity : 32768;
     st.P = o.props_capacity > 0 ? o.props_capacity : st.S + 2 * MT_WAVE;
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
+    if (const char *e = getenv("MT_WPG")) h->wpg = atoi(e) == 1 ? 1 : 2;
     if (o.lds_seg_capacity >= 0) {
         int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 192;
         S_l = std::min(S_l, st.S);
@@ -1171,10 +1181,14 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         // LDS tier for every document; the ones that outgrow it are flagged and replayed
         // from HBM by the second launch (whose other workgroups exit at once)
         if (h->st.DL)
-            hipLaunchKernelGGL(k_replay<TierLdsT<true>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+            hipLaunchKernelGGL((k_replay<TierLdsT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
                                h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
+        else if (h->wpg == 2)
+            hipLaunchKernelGGL((k_replay<TierLdsT<false>, 2>), dim3((h->n_docs + 1) / 2), dim3(2 * MT_WAVE),
+                               2 * tier_lds_bytes(true, h->lds, 0), h->stream, h->st, b->ops, b->off, b->text, b->props,
+                               h->lds);
         else
-            hipLaunchKernelGGL(k_replay<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+            hipLaunchKernelGGL((k_replay<TierLdsT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
                                h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
         HIPCHK(h, hipGetLastError());
     } else {
@@ -1191,10 +1205,10 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
             hipLaunchKernelGGL(k_replay_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
                                b->ops, b->off, b->text, b->props, use_resume);
     } else if (h->st.DL)
-        hipLaunchKernelGGL(k_replay<TierGlbT<true>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+        hipLaunchKernelGGL((k_replay<TierGlbT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     else
-        hipLaunchKernelGGL(k_replay<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+        hipLaunchKernelGGL((k_replay<TierGlbT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
