@@ -3,13 +3,16 @@
 
 One *step* = replaying one batch of synthetic sequenced messages through the observer
 replicas of every document on the GPU (Client.applyMsg semantics, bit-exact with the
-reference), starting from the documents' initial contents.  At N=1 the workload is
-BASELINE.json configs[1] (C2): 10k documents x 2k ops, 4 writers, refSeq lag <= 32,
-insert 0.6 / remove 0.4.  With N ranks every rank replays its own 10k-document shard
-(weak scaling; documents are independent, so there is no data-path collective); the only
-collective is an RCCL all-gather of per-document checksums after the timed region.
+reference), starting from the documents' initial contents.  The default workload is the
+one the metric is quoted on, BASELINE.json configs[2] (C3: 100k documents x 10k ops,
+8 writers, refSeq lag <= 64, insert 0.5 / remove 0.3 / annotate 0.2 with property sets,
+sharded over 8 GPUs): every rank replays its own 12,500-document shard, so N=8 is exactly
+the 100k-document job and N=1 is one GPU's share of it (weak scaling; documents are
+independent, so there is no data-path collective).  The only collective is an RCCL
+all-gather of per-document checksums after the timed region.  `--config c2` runs configs[1]
+(10k documents x 2k insert/remove ops per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--docs D] [--ops O]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--docs D] [--ops O]
 
 Inputs are generated on the GPU (untimed) and stay resident in HBM; the timed region is
 reset + replay kernels only.  Rank 0 prints one JSON line.
@@ -36,7 +39,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--config", default="c3")
     ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: config)")
     ap.add_argument("--ops", type=int, default=0, help="ops per document (default: config)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -44,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
+    ap.add_argument("--page-caps", default="", help="paged layout LDS capacities 'pages,unsettled,heap' (sweeps)")
     return ap.parse_args()
 
 
@@ -178,7 +182,8 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    docs = args.docs or (cfg["docs"] if args.config == "c2" else min(cfg["docs"], 16384))
+    # per-GPU shard: C2 is a single-GPU config; C3's 100k documents shard over 8 GPUs
+    docs = args.docs or {"c2": cfg["docs"], "c3": cfg["docs"] // 8}.get(args.config, min(cfg["docs"], 16384))
     if args.ops:
         cfg["ops"] = args.ops
     doc_base = rank * docs
@@ -188,6 +193,9 @@ def main():
         caps["lds_seg_capacity"] = args.lds_cap
     if args.heap_cap:
         caps["heap_capacity"] = args.heap_cap
+    if args.page_caps:
+        pp, ut, ph = (int(x) for x in args.page_caps.split(","))
+        caps.update(page_capacity=pp, unsettled_capacity=ut, page_heap_capacity=ph)
     mt = MergeTreeBatch(docs, device=local_rank, **caps)
     t_gen = time.time()
     batch = mt.generate(cfg, doc_base)              # untimed: inputs resident in HBM
@@ -263,8 +271,8 @@ def main():
     traffic = None
     if os.path.exists(PROFILE_PMC):
         try:
-            pm = json.load(open(PROFILE_PMC))
-            if pm.get("config") == args.config and pm.get("docs") == docs and pm.get("ops") == cfg["ops"]:
+            pm = json.load(open(PROFILE_PMC)).get(args.config, {})
+            if pm.get("docs") == docs and pm.get("ops") == cfg["ops"]:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -313,7 +321,9 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "k_replay<TierLdsT<false>> + k_replay<TierGlbT<false>> (HBM-tier hand-over)",
+            "kernel": ("k_replay<TierLdsT<false>> (first ops) + k_replay_paged<TierPagedT<false>> (rest)"
+                       if "page_capacity" in caps else
+                       "k_replay<TierLdsT<false>> + k_replay<TierGlbT<false>> (HBM-tier hand-over)"),
             "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
             "docs_replayed_from_hbm": hbm_docs,
         },

@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
 // ---------------------------------------------------------------- paged kernels
 // high-water marks -> stats[8..11] (mt_last_paged_peaks)
 template <class T>
-__device__ static void pg_peaks(const DevState &st, PagedDoc<T> &pd, int pk_ut, int pk_heap) {
+__device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, int pk_ut, int pk_heap) {
     const int np = nbr(pd.up, 1);
     int ns = 0;
     for (int q = lane(); q < np; q += MT_WAVE) ns += pd.meta[pd.up.dir[q]].nseg;

@@ -26,23 +26,25 @@ def main():
     stats = {r["Name"]: dict(calls=int(r["Calls"]), avg_ms=float(r["AverageNs"]) / 1e6,
                               pct=float(r["Percentage"]))
              for r in rows(os.path.join(src, "trace", "**", "*kernel_stats.csv"))}
-    counters, dispatches = {}, {}
+    counters, steps = {}, {}
     for r in rows(os.path.join(src, "pmc*", "**", "*counter_collection.csv")):
-        if "k_replay<TierLdsT<false>" not in r["Kernel_Name"]:
+        # one step = the LDS-tier launch + (paged / HBM tier) hand-over launch; all replay
+        # kernels are summed and divided by the number of LDS-tier dispatches
+        if not r["Kernel_Name"].startswith("void k_replay"):
             continue
         counters[r["Counter_Name"]] = counters.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        dispatches.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
-    # average per dispatch (one dispatch = one replay of the whole batch)
-    counters = {k: v / max(len(dispatches[k]), 1) for k, v in counters.items()}
+        if "k_replay<TierLdsT" in r["Kernel_Name"]:
+            steps.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
+    counters = {k: v / max(len(steps.get(k, ())), 1) for k, v in counters.items()}
     per_op = {k: v / ops for k, v in counters.items() if k.startswith("SQ_INSTS") or k.startswith("SQ_WAIT")
               or k in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT",
                        "SQ_LDS_IDX_ACTIVE", "SQ_ACTIVE_INST_VALU")}
     hbm = None
     if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         hbm = 2 * counters["FETCH_SIZE"] * 1024 + counters["WRITE_SIZE"] * 1024
-    out = dict(bench=bench, kernels=stats, lds_tier_counters=counters, lds_tier_per_op=per_op,
-               hbm_bytes_per_launch_lds_tier=hbm,
-               note="counters averaged per k_replay<TierLdsT<false>> dispatch (one replay of the batch);"
+    out = dict(bench=bench, kernels=stats, replay_counters_per_step=counters, replay_per_op=per_op,
+               hbm_bytes_per_step=hbm,
+               note="counters of every k_replay* dispatch summed per step (LDS-tier launch + hand-over launch);"
                     " FETCH_SIZE doubled per the gfx950 correction; KB = 1024 B")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
