@@ -51,7 +51,7 @@ def parse():
     return ap.parse_args()
 
 
-def capacities(cfg):
+def capacities(cfg, tight=True):
     """Per-document capacities sized for the workload (DESIGN.md 'HBM layout')."""
     if cfg["writers"] > 8 or cfg["lag"] > 64 or cfg["p_insert_props"] > 0 or cfg["ops"] > 4000:
         # annotate keeps segments apart (property sets differ): ~0.4 live segments per op.
@@ -59,13 +59,20 @@ def capacities(cfg):
         # HBM arrays only hold what the LDS tier spills.
         segs = max(1024, int(cfg["ops"] * 0.5) + 512)
         deep = cfg["lag"] > 64
-        return dict(seg_capacity=256, text_capacity=1 << 16, heap_capacity=512, props_capacity=segs + 256,
-                    # high-water marks (mt_last_paged_peaks) at 10k ops: C3 174 pages, 178
-                    # table entries, 153 heap entries; C4 (minSeq ~1k ops behind) far more
+        caps = dict(seg_capacity=256, text_capacity=1 << 16, heap_capacity=512, props_capacity=segs + 256,
+                    # high-water marks (mt_last_paged_peaks) at 10k ops: C3 180 pages, 195
+                    # table entries, 159 heap entries (12.5k documents); C4 (minSeq ~1k ops
+                    # behind) far more
                     page_capacity=max(64, segs // 20 if not deep else segs // 14),
                     page_heap_capacity=2560 if deep else 512,
                     unsettled_capacity=2560 if deep else 320,
                     uid_capacity=min(1 << 16, 3 * cfg["ops"] + 1024))
+        if tight and not deep and cfg["ops"] <= 10000:
+            # the paged layout's LDS footprint sets documents per CU: 27 KB at the loose
+            # capacities (6 per CU) vs 19.9 KB here (8 per CU, the VGPR limit too); a document
+            # that outgrows them fails generation and the run falls back to the loose ones
+            caps.update(page_capacity=208, unsettled_capacity=240, page_heap_capacity=224)
+        return caps
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
 
@@ -196,9 +203,18 @@ def main():
     if args.page_caps:
         pp, ut, ph = (int(x) for x in args.page_caps.split(","))
         caps.update(page_capacity=pp, unsettled_capacity=ut, page_heap_capacity=ph)
-    mt = MergeTreeBatch(docs, device=local_rank, **caps)
     t_gen = time.time()
-    batch = mt.generate(cfg, doc_base)              # untimed: inputs resident in HBM
+    mt = MergeTreeBatch(docs, device=local_rank, **caps)
+    try:
+        batch = mt.generate(cfg, doc_base)          # untimed: inputs resident in HBM
+    except RuntimeError as e:
+        if "status 4" not in str(e) or args.page_caps or caps == capacities(cfg, tight=False):
+            raise
+        # a document outgrew the tight paged capacities (MT_DOC_CAPACITY): loose ones
+        del mt
+        caps = dict(caps, **{k: v for k, v in capacities(cfg, tight=False).items() if "page" in k or "unsettled" in k})
+        mt = MergeTreeBatch(docs, device=local_rank, **caps)
+        batch = mt.generate(cfg, doc_base)
     gen_sums = mt.checksums()
     t_gen = time.time() - t_gen
     seed_off, seed = mt.generated_seeds(cfg, doc_base)
@@ -235,6 +251,7 @@ def main():
         elapsed = float(t.item())
 
     hbm_docs = mt.last_hbm_docs()
+    peaks = mt.last_paged_peaks() if "page_capacity" in caps else None
     status = mt.status()
     sums = mt.checksums()
     replay_consistent = bool(np.array_equal(sums, gen_sums)) and int((status != 0).sum()) == 0
@@ -326,6 +343,8 @@ def main():
                        "k_replay<TierLdsT<false>> + k_replay<TierGlbT<false>> (HBM-tier hand-over)"),
             "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
             "docs_replayed_from_hbm": hbm_docs,
+            "paged_peaks": peaks,
+            "paged_caps": [caps.get("page_capacity"), caps.get("unsettled_capacity"), caps.get("page_heap_capacity")],
         },
         "cpu_baseline": cpu,
         "parity": {"replay_equals_generation": replay_consistent, "oracle_sample": parity,

@@ -533,8 +533,17 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 // Replay of the documents flagged by the LDS tier (retry[doc]) in the paged layout: a
 // document seen for the first time is converted from its flat state (initial contents, or
 // what the LDS tier spilled) and stays paged until the next reset.
+// waves per SIMD the paged kernel is compiled for (VGPR budget 512 / n); 0 = compiler choice
+#ifndef MT_PAGED_WAVES
+#define MT_PAGED_WAVES 0
+#endif
+#if MT_PAGED_WAVES > 0
+#define MT_PAGED_WPE __attribute__((amdgpu_waves_per_eu(MT_PAGED_WAVES)))
+#else
+#define MT_PAGED_WPE
+#endif
 template <class T>
-__global__ void __launch_bounds__(MT_WAVE) k_replay_paged(DevState st, const mt_op_rec *ops,
+__global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState st, const mt_op_rec *ops,
                                                           const int64_t *off, const uint16_t *tin,
                                                           const uint32_t *pin, int use_resume) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
