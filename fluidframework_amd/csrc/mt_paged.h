@@ -58,6 +58,8 @@ template <class T> struct PagedDoc {
     int cur;                  // page id staged in the window (-1: none)
     int cur_pos;              // its level-1 position (-1: not known yet)
     int dirty;                // the window differs from the page in HBM (slots, uid map, table)
+    int uid_lo;               // next_uid when the window was loaded: older segments of the
+                              // window are already mapped to its page
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
@@ -162,6 +164,7 @@ TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
     pd.cur = pg;
     pd.cur_pos = -1;
     pd.dirty = 0;
+    pd.uid_lo = w.next_uid;
     wsync<T>();
 }
 
@@ -234,7 +237,9 @@ TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1) {
         gO[i] = w.O[lo + i];
         gB[i] = b;
         const uint32_t uid = b.z & ~MT_MARKER_BIT;
-        if (uid < (uint32_t)pd.UM) pd.gumap[uid] = (uint16_t)pg;
+        // the uid -> page map changes only for segments created since the window was
+        // loaded, or moved to another page (scattered 2-byte writes: one sector each)
+        if (uid < (uint32_t)pd.UM && (pg != pd.cur || uid >= (uint32_t)pd.uid_lo)) pd.gumap[uid] = (uint16_t)pg;
         ol = obs_len(a);
     }
     const int obs = wave_sum(ol);
@@ -613,8 +618,11 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         if (w.heap_n == 0) break;
         const v2i top = heap_top(w);
         if (top.x > w.min_seq) break;
+        PG_T0(5)
         heap_pop(w);
         wsync<T>();
+        PG_T1(5)
+        PG_T0(4)
         const uint32_t uid = (uint32_t)top.y;
         if (uid >= (uint32_t)pd.UM) {
             pg_fail_cap(w, 9);
@@ -631,6 +639,7 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
             i = find_uid(w, uid);
             if (i < 0) continue;
         }
+        PG_T1(4)
         int bstart;
         const int b = blk_find(w, 0, i, true, bstart);
         if (b < 0) {
@@ -640,7 +649,9 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         const int f = flgr(w, b);
         const int old = cntr(w, 0, b);
         if (f == 0) continue;
+        PG_T0(2)
         const int kept = scour_range(w, bstart, b, 1);
+        PG_T1(2)
         if (w.status) return;
         wsync<T>();
         if (lane() == 0) w.flg[b] = 0;

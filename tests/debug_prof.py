@@ -25,8 +25,9 @@ b.apply_async()
 mt.sync()
 print("kernel ms", mt.last_kernel_ms(), "hbm", mt.last_hbm_docs(), "peaks", mt.last_paged_peaks())
 mt.lib.mt_debug_prof(mt.h, _native.ptr(out), 0)
-names = ["split_seg", "boundary", "scour_block", "pack", "zamboni", "text_gc", "op_insert", "op_range", "obs_prefix",
+# paged documents reuse slots 2, 4, 5 for pg_zamboni internals (scour_range, locate, heap pop)
+names = ["split_seg", "boundary", "scour|pg_scour", "pack", "zamboni|pg_locate", "text_gc|pg_heap_pop", "op_insert", "op_range", "obs_prefix",
          "pg_views", "pg_win_load", "pg_win_flush", "pg_zamboni", "pg_find", "pg_pack1", "pg_apply_op"]
 ops = docs * cfg["ops"]
 for i, n in enumerate(names):
-    print(f"{n:12s} ticks/op {out[i] / ops:10.1f}  calls/op {out[16 + i] / ops:8.3f}  ticks/call {out[i] / max(out[16 + i], 1):10.1f}")
+    print(f"{n:20s} ticks/op {out[i] / ops:10.1f}  calls/op {out[16 + i] / ops:8.3f}  ticks/call {out[i] / max(out[16 + i], 1):10.1f}")
