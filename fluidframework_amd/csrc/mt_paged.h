@@ -60,6 +60,8 @@ template <class T> struct PagedDoc {
     int dirty;                // the window differs from the page in HBM (slots, uid map, table)
     int uid_lo;               // next_uid when the window was loaded: older segments of the
                               // window are already mapped to its page
+    int vvalid, vr, vc;       // pvl holds the page view lengths of view (vr, vc): boundary
+                              // splits keep them (lengths are preserved), any other change drops them
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
@@ -277,6 +279,18 @@ TD void pg_split_page(PagedDoc<T> &pd) {
     pg_table_add(pd, s0, w.n, np);
     if (w.status) return;
     pg_write_page(pd, np, s0, w.n, sp, nbk);
+    if (pd.vvalid) {   // the moved half's view length goes with it
+        const int i = lane() + s0;
+        v4i a;
+        u64 o;
+        load_ao(w, i, i < w.n, a, o);
+        const int dl = wave_sum(i < w.n ? view_len(a, o, pd.vr, pd.vc) : 0);
+        if (lane() == 0) {
+            pd.pvl[np] = dl;
+            pd.pvl[pd.cur] -= dl;
+        }
+        wsync<T>();
+    }
     // level 1: new node after cur (blk_split_up grows the parents / the root)
     blk_split_up(up, 1, pos);
     if (up.status) {
@@ -358,7 +372,14 @@ TD int pg_views(PagedDoc<T> &pd, int r, int c) {
     PG_T0(9)
     const int r_ = pg_views_impl(pd, r, c);
     PG_T1(9)
+    pd.vvalid = 1;
+    pd.vr = r;
+    pd.vc = c;
     return r_;
+}
+// pvl for view (r, c): recomputed only if a change other than a boundary split happened
+TD void pg_views_cached(PagedDoc<T> &pd, int r, int c) {
+    if (!(pd.vvalid && pd.vr == r && pd.vc == c)) pg_views(pd, r, c);
 }
 TD int pg_views_impl(PagedDoc<T> &pd, int r, int c) {
     const int np = nbr(pd.up, 1);
@@ -614,6 +635,7 @@ TD void pg_zamboni(PagedDoc<T> &pd) {
 }
 TD void pg_zamboni_impl(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
+    pd.vvalid = 0;
     for (int it = 0; it < MT_ZAMBONI && w.status == 0; it++) {
         if (w.heap_n == 0) break;
         const v2i top = heap_top(w);
@@ -676,7 +698,7 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
     const int slen = (op.flags & MT_F_MARKER) ? 1 : op.pos2;
-    pg_views(pd, op.ref_seq, op_cli(op));
+    pg_views_cached(pd, op.ref_seq, op_cli(op));
     int start;
     const int pos = pg_find(pd, op.pos1, false, start);
     if (pos < 0) {
@@ -696,13 +718,14 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     pg_load_pos(pd, pos);
     OpIn rel = in;
     rel.op.pos1 = op.pos1 - start;
+    pd.vvalid = 0;
     op_insert(w, rel, tin, pin);
     if (w.status) return;
     pg_win_sync(pd);
 }
 
 TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
-    pg_views(pd, r, c);
+    pg_views_cached(pd, r, c);
     int start;
     const int pos = pg_find(pd, p, true, start);
     if (pos < 0 || start >= p) return;   // p is at a page boundary or past the end
@@ -727,7 +750,8 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
     pg_boundary(pd, p2, r, c);
     if (w.status) return;
     Cb cb = cb_begin(w, op.seq, op.kind);
-    pg_views(pd, r, c);
+    pg_views_cached(pd, r, c);
+    pd.vvalid = 0;   // range_mark changes view lengths
     int start;
     int pos = pg_find(pd, p1, true, start);
     if (pos >= 0) {
@@ -758,6 +782,7 @@ TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin,
 // page split) in the page the uid map names.
 TD void pg_load_removed(PagedDoc<T> &pd, const mt_op_rec &op) {
     DocT<T> &w = pd.w;
+    pd.vvalid = 0;
     const uint32_t uid = (uint32_t)(w.next_uid - 1);
     int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
     if (i < 0) {
@@ -1019,11 +1044,13 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.cur = -1;
     pd.cur_pos = -1;
     pd.dirty = 0;
+    pd.vvalid = 0;
 }
 
 // Builds the free-page list from the directory (pvl as scratch marks).
 TD void pg_build_free(PagedDoc<T> &pd) {
     const int np = nbr(pd.up, 1);
+    pd.vvalid = 0;
     for (int base = 0; base < pd.PP; base += MT_WAVE)
         if (base + lane() < pd.PP) pd.pvl[base + lane()] = 0;
     wsync<T>();
