@@ -69,9 +69,9 @@ def capacities(cfg, tight=True):
                     uid_capacity=min(1 << 16, 3 * cfg["ops"] + 1024))
         if tight and not deep and cfg["ops"] <= 10000:
             # the paged layout's LDS footprint sets documents per CU: 27 KB at the loose
-            # capacities (6 per CU) vs 19.9 KB here (8 per CU, the VGPR limit too); a document
+            # capacities (6 per CU) vs 16.1 KB here (10 per CU; the kernel is compiled for 3 waves/SIMD); a document
             # that outgrows them fails generation and the run falls back to the loose ones
-            caps.update(page_capacity=208, unsettled_capacity=240, page_heap_capacity=224)
+            caps.update(page_capacity=208, unsettled_capacity=240, page_heap_capacity=224)   # 16.1 KB: 10 per CU
         return caps
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 

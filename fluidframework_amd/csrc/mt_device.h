@@ -53,13 +53,15 @@ static_assert(sizeof(DocHdr) == 128, "DocHdr size");
 
 // Paged documents (mt_paged.h): a document that outgrows the LDS tier is kept as pages =
 // level-1 nodes of the reference B-tree (<= 7 leaf blocks, <= 64 segment slots each).
-struct PageMeta {             // 24 bytes, indexed by page id
-    uint8_t nseg, nblk, pad0, pad1;
-    uint8_t bcnt[8];          // segments per leaf block
-    int8_t flg[8];            // needsScour per leaf block
+struct PageMeta {             // 12 bytes, indexed by page id (LDS footprint: documents per CU)
+    uint8_t nseg, nblk;
+    uint16_t flg2;            // needsScour per leaf block, 2 bits each (value + 1: -1/0/1 -> 0/1/2)
+    uint32_t bc;              // segments per leaf block, 4 bits each (<= MaxNodesInBlock)
     int32_t obs;              // observer length of the page
 };
-static_assert(sizeof(PageMeta) == 24, "PageMeta size");
+static_assert(sizeof(PageMeta) == 12, "PageMeta size");
+static __host__ __device__ inline int pm_bcnt(const PageMeta &m, int q) { return (int)((m.bc >> (4 * q)) & 15u); }
+static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { return (int8_t)((int)((m.flg2 >> (2 * q)) & 3u) - 1); }
 #define MT_PG_SLOTS 64
 // DocHdr.pad[] words used by paged documents
 #define HDR_PAGED 0           // 1: the document lives in the paged layout

@@ -237,16 +237,23 @@ TD void fail_cap(DocT<T> &d, int cause) {
     fail(d, T::kLds ? MT_DOC_RETRY : MT_DOC_CAPACITY);
 }
 
+// paged instances (window: levels 0-1; upper levels: 1.. with level 1 = pages): B entries
+// for levels 0 and 1, B/2 for level 2, B/4 above (growth is checked against bcap)
+static __host__ __device__ inline int pcnt_cap(int B, int l) { return l <= 1 ? B : (l == 2 ? B / 2 : B / 4); }
+static __host__ __device__ inline int pcnt_off(int B, int l) {
+    return l <= 1 ? l * B : (l == 2 ? 2 * B : 2 * B + B / 2 + (l - 3) * (B / 4));
+}
+static __host__ __device__ inline int pcnt_bytes(int B) { return pcnt_off(B, MT_LV); }
 TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) {
     if constexpr (T::kPaged)
-        return d.cnt + l * d.B_cap;
+        return d.cnt + pcnt_off(d.B_cap, l);
     else
         return d.cnt + cnt_off(d.B_cap, l);
 }
 // capacity of level l
 TD int bcap(DocT<T> &d, int l) {
     if constexpr (T::kPaged)
-        return d.B_cap;
+        return pcnt_cap(d.B_cap, l);
     else
         return cnt_cap(d.B_cap, l);
 }

@@ -39,7 +39,7 @@ template <class T> struct PagedDoc {
     LDS_AS PageMeta *meta;    // [PP] by page id
     LDS_AS int *pvl;          // [PP] by page id: view length of the current view
     LDS_AS uint16_t *freel;   // [PP] free page ids
-    LDS_AS int *upage;        // [UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
+    LDS_AS uint16_t *upage;   // [UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
     LDS_AS v4i *uA;
     LDS_AS u64 *uO;
     GLB_AS v4i *gA;           // this document's pages (slot 0 of page 0)
@@ -80,8 +80,8 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     L.offUA = o; o += 16u * UT;
     L.offUO = o; o += 8u * UT;
     L.offHeap = o; o += 8u * (PH + 1);
-    L.offMeta = o; o += 24u * PP;
-    L.offUpage = o; o += 4u * UT;
+    L.offMeta = o; o += (uint32_t)sizeof(PageMeta) * PP;
+    L.offUpage = o; o += (2u * UT + 3u) & ~3u;
     L.offPvl = o; o += 4u * PP;
     L.offWscr = o; o += 64u * 4;
     L.offWnb = o; o += MT_LV * 4;
@@ -92,7 +92,7 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     L.offWends = o; o += 2u * PW_B;
     L.offWcnt = o; o += (uint32_t)MT_LV * PW_B;
     L.offWflg = o; o += PW_B;
-    L.offUcnt = o; o += (uint32_t)MT_LV * PP;
+    L.offUcnt = o; o += (uint32_t)pcnt_bytes(PP);
 #ifdef MT_PROF
     o = (o + 7u) & ~7u;
     L.offProf = o; o += 32u * 8;
@@ -111,6 +111,20 @@ TD PagedDoc<T> &pdoc(DocT<T> &w) { return *reinterpret_cast<PagedDoc<T> *>(&w); 
 TD void pg_fail_cap(DocT<T> &w, int cause) {
     if (w.status == 0) w.cap_cause = cause;
     fail(w, MT_DOC_CAPACITY);
+}
+__device__ __forceinline__ int pm_bcnt_l(const LDS_AS PageMeta *m, int q) { return (int)((m->bc >> (4 * q)) & 15u); }
+__device__ __forceinline__ int8_t pm_flg_l(const LDS_AS PageMeta *m, int q) {
+    return (int8_t)((int)((m->flg2 >> (2 * q)) & 3u) - 1);
+}
+// Packs the leaf-block counts / needsScour flags of page pg from lanes holding block q (v):
+// all lanes call it (wave-uniform control flow); fields are disjoint, so the sum is an OR.
+TD void pm_set_blocks(PagedDoc<T> &pd, int pg, int q, bool v, int cnt, int flg) {
+    const uint32_t bc = (uint32_t)wave_sum(v ? (int)((uint32_t)cnt << (4 * q)) : 0);
+    const uint32_t f2 = (uint32_t)wave_sum(v ? (flg + 1) << (2 * q) : 0);
+    if (lane() == 0) {
+        pd.meta[pg].bc = bc;
+        pd.meta[pg].flg2 = (uint16_t)f2;
+    }
 }
 TD bool unsettled(const v4i a, int min_seq) {
     return a.y > min_seq || (a.z != MT_RSEQ_NONE && a.z > min_seq);
@@ -151,8 +165,8 @@ TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
         w.Bv[i] = gB[i];
     }
     if (i < PW_B) {
-        lvl(w, 0)[i] = i < nb ? pd.meta[pg].bcnt[i & 7] : 0;
-        w.flg[i] = i < nb ? pd.meta[pg].flg[i & 7] : (int8_t)0;
+        lvl(w, 0)[i] = i < nb ? (uint8_t)pm_bcnt_l(pd.meta + pg, i & 7) : 0;
+        w.flg[i] = i < nb ? pm_flg_l(pd.meta + pg, i & 7) : (int8_t)0;
     }
     if (i == 0) {
         w.nb[0] = nb;
@@ -245,10 +259,8 @@ TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1) {
         ol = obs_len(a);
     }
     const int obs = wave_sum(ol);
-    if (i < 8) {
-        pd.meta[pg].bcnt[i] = b0 + i < b1 ? lvl(w, 0)[b0 + i] : 0;
-        pd.meta[pg].flg[i] = b0 + i < b1 ? w.flg[b0 + i] : (int8_t)0;
-    }
+    const bool vb = i < 8 && b0 + i < b1;
+    pm_set_blocks(pd, pg, i, vb, vb ? lvl(w, 0)[b0 + i] : 0, vb ? w.flg[b0 + i] : 0);
     if (i == 0) {
         pd.meta[pg].nseg = (uint8_t)(hi - lo);
         pd.meta[pg].nblk = (uint8_t)(b1 - b0);
@@ -333,10 +345,8 @@ TD void pg_win_sync(PagedDoc<T> &pd) {
     if (i < w.n) ol = obs_len(w.A[i]);
     const int obs = wave_sum(ol);
     const int pg = pd.cur;
-    if (i < 8) {
-        pd.meta[pg].bcnt[i] = i < nbk ? lvl(w, 0)[i] : 0;
-        pd.meta[pg].flg[i] = i < nbk ? w.flg[i] : (int8_t)0;
-    }
+    const bool vb = i < 8 && i < nbk;
+    pm_set_blocks(pd, pg, i, vb, vb ? lvl(w, 0)[i] : 0, vb ? w.flg[i] : 0);
     const int pos = pg_cur_pos(pd);
     if (i == 0) {
         pd.meta[pg].nseg = (uint8_t)w.n;
@@ -511,15 +521,15 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
                 opg = pg;
                 ob = bl - acc_b;
                 int s = acc_s;
-                for (int q = 0; q < ob; q++) s += pd.meta[pg].bcnt[q];
+                for (int q = 0; q < ob; q++) s += pm_bcnt_l(pd.meta + pg, q);
                 bseg0 = s;
             }
             acc_b += nb;
             acc_s += uni(pd.meta[pg].nseg);
         }
     }
-    const int bcnt = opg >= 0 ? pd.meta[opg].bcnt[ob] : 0;
-    const int8_t bflg = opg >= 0 ? pd.meta[opg].flg[ob] : (int8_t)0;
+    const int bcnt = opg >= 0 ? pm_bcnt_l(pd.meta + opg, ob) : 0;
+    const int8_t bflg = opg >= 0 ? pm_flg_l(pd.meta + opg, ob) : (int8_t)0;
     // new page m gets blocks [nb0(m), nb0(m) + base + (m < extra))
     auto nb0 = [&](int m) { return m * base + min(m, extra); };
     LDS_AS int32_t *newp = w.scr;   // scratch: the new page ids
@@ -579,17 +589,8 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
         pd.ut_n += __popcll(am);
         const int obs = wave_sum(ol);
         // meta of the new page: blocks blo..bhi of the concatenation
-        const int q = lane() - blo;
-        if (lane() >= blo && lane() < bhi) {
-            pd.meta[npg].bcnt[q] = (uint8_t)bcnt;
-            pd.meta[npg].flg[q] = bflg;
-        } else if (lane() >= 64 - 8) {
-            const int qq = lane() - (64 - 8);
-            if (qq >= bhi - blo) {
-                pd.meta[npg].bcnt[qq] = 0;
-                pd.meta[npg].flg[qq] = 0;
-            }
-        }
+        const bool vb = lane() >= blo && lane() < bhi;
+        pm_set_blocks(pd, npg, lane() - blo, vb, bcnt, bflg);
         if (lane() == 0) {
             pd.meta[npg].nseg = (uint8_t)(s_hi - s_lo);
             pd.meta[npg].nblk = (uint8_t)(bhi - blo);
@@ -1038,7 +1039,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
     pd.pvl = (LDS_AS int *)(smem + L.offPvl);
     pd.freel = (LDS_AS uint16_t *)(smem + L.offFree);
-    pd.upage = (LDS_AS int *)(smem + L.offUpage);
+    pd.upage = (LDS_AS uint16_t *)(smem + L.offUpage);
     pd.uA = (LDS_AS v4i *)(smem + L.offUA);
     pd.uO = (LDS_AS u64 *)(smem + L.offUO);
     pd.cur = -1;
@@ -1088,7 +1089,7 @@ TD void pg_load(PagedDoc<T> &pd) {
     {
         GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)pd.gmeta;
         LDS_AS uint32_t *lm = (LDS_AS uint32_t *)pd.meta;
-        for (int i = lane(); i < pd.PP * 6; i += MT_WAVE) lm[i] = gm[i];
+        for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) lm[i] = gm[i];
     }
     for (int l = 1; l < up.depth; l++) {
         const int nl = nbr(up, l);
@@ -1097,7 +1098,7 @@ TD void pg_load(PagedDoc<T> &pd) {
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = pd.gheap[i];
     pd.ut_n = h.pad[HDR_UTN];
     for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
-        pd.upage[e] = pd.gupage[e];
+        pd.upage[e] = (uint16_t)pd.gupage[e];
         pd.uA[e] = pd.guA[e];
         pd.uO[e] = pd.guO[e];
     }
@@ -1115,7 +1116,7 @@ TD void pg_store(PagedDoc<T> &pd) {
     {
         GLB_AS uint32_t *gm = (GLB_AS uint32_t *)pd.gmeta;
         LDS_AS const uint32_t *lm = (LDS_AS const uint32_t *)pd.meta;
-        for (int i = lane(); i < pd.PP * 6; i += MT_WAVE) gm[i] = lm[i];
+        for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) gm[i] = lm[i];
     }
     for (int l = 1; l < up.depth; l++) {
         const int nl = nbr(up, l);

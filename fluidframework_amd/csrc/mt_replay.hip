@@ -535,7 +535,7 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 // what the LDS tier spilled) and stays paged until the next reset.
 // waves per SIMD the paged kernel is compiled for (VGPR budget 512 / n); 0 = compiler choice
 #ifndef MT_PAGED_WAVES
-#define MT_PAGED_WAVES 0
+#define MT_PAGED_WAVES 3
 #endif
 #if MT_PAGED_WAVES > 0
 #define MT_PAGED_WPE __attribute__((amdgpu_waves_per_eu(MT_PAGED_WAVES)))
@@ -1643,7 +1643,7 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
                 hd.O.push_back(pO[b0 + i]);
                 hd.B.push_back(pB[b0 + i]);
             }
-            for (int k = 0; k < m.nblk; k++) hd.cnt.push_back(m.bcnt[k]);
+            for (int k = 0; k < m.nblk; k++) hd.cnt.push_back((uint8_t)pm_bcnt(m, k));
         }
         hd.hdr.n_seg = (int)hd.A.size();
         hd.hdr.n_blk[0] = (int)hd.cnt.size();
