@@ -32,6 +32,7 @@ HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 SEG_BYTES = 40             # segA 16 + segO 8 + segB 16
 OP_BYTES = 32              # mt_op_rec
 PROFILE_PMC = os.path.join(REPO, "profiles", "pmc_summary.json")
+CALIBRATION = os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")
 
 
 def parse():
@@ -314,6 +315,18 @@ def main():
                           f"{args.config} batch ({sel_end} ops) on {threads} host threads, {t_c:.2f} s")
         parity = dict(docs_checked=n_sample,
                       mismatches=int((osums != sums[:n_sample]).sum() + (ost != 0).sum()))
+        # the reference itself cannot travel: its single-thread speed relative to the port on
+        # the same streams is measured in the build container (oracle/calibrate.py)
+        try:
+            cal = json.load(open(CALIBRATION)).get(args.config)
+        except (OSError, ValueError):
+            cal = None
+        if cal:
+            r = cal["ratio_port_over_reference"]
+            cpu["reference_estimate"] = dict(
+                value=round(cpu["value"] / r, 1), unit="ops/s", cores=threads,
+                how=f"port value / {r} (port vs transpiled reference MergeTree under {cal['reference_runtime']}, "
+                    f"one thread each, {cal['ops']} {args.config} ops; {os.path.relpath(CALIBRATION, REPO)})")
 
     out = {
         "metric": "sequenced merge-tree ops applied/sec (node) at 100k docs; bit-exact text+props",

@@ -560,6 +560,31 @@ async function main() {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
+    } else if (mode === "time") {
+        // time <gen.json> <out.json> [repeats]: the reference's Client.applyMsg replay of
+        // every document's stream (messages pre-built, observer with the delta callback
+        // that records positions, as replayDoc), one thread; the CPU-baseline calibration
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        const reps = rest[2] ? parseInt(rest[2], 10) : 1;
+        let ns = 0n, ops = 0;
+        for (let rep = 0; rep < reps; rep++) {
+            for (const d of logs.docs) {
+                const { c } = makeObserver(d.seed_text);
+                const cseq = {};
+                const msgs = d.msgs.map(([k, t, r, msn, op, type]) => {
+                    cseq[k] = (cseq[k] || 0) + 1;
+                    const m = makeMsg(k, t, r, msn, cseq[k], op);
+                    if (type) { m.type = type; }
+                    return m;
+                });
+                const t0 = process.hrtime.bigint();
+                for (const m of msgs) { c.applyMsg(m); }
+                ns += process.hrtime.bigint() - t0;
+                ops += msgs.length;
+            }
+        }
+        const s = Number(ns) / 1e9;
+        fs.writeFileSync(rest[1], JSON.stringify({ ops, seconds: s, ops_per_s: ops / s, node: process.version }));
     } else if (mode === "snap") {
         const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
