@@ -152,17 +152,32 @@ TD void pg_win_load(PagedDoc<T> &pd, int pg) {
     pg_win_load_impl(pd, pg);
     PG_T1(10)
 }
+// page pg's slots into registers (lane i: slot i)
+TD void pg_win_fetch(PagedDoc<T> &pd, int pg, v4i &a, u64 &o, v4u &b) {
+    const int n = uni(pd.meta[pg].nseg);
+    const int i = lane();
+    if (i < n) {
+        a = pd.gA[(size_t)pg * MT_PG_SLOTS + i];
+        o = pd.gO[(size_t)pg * MT_PG_SLOTS + i];
+        b = pd.gB[(size_t)pg * MT_PG_SLOTS + i];
+    }
+}
+TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b);
 TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
+    v4i a = v4i{0, 0, 0, 0};
+    u64 o = 0;
+    v4u b = v4u{0, 0, 0, 0};
+    pg_win_fetch(pd, pg, a, o, b);
+    pg_win_place(pd, pg, a, o, b);
+}
+TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b) {
     DocT<T> &w = pd.w;
     const int n = uni(pd.meta[pg].nseg), nb = uni(pd.meta[pg].nblk);
     const int i = lane();
-    GLB_AS v4i *gA = pd.gA + (size_t)pg * MT_PG_SLOTS;
-    GLB_AS u64 *gO = pd.gO + (size_t)pg * MT_PG_SLOTS;
-    GLB_AS v4u *gB = pd.gB + (size_t)pg * MT_PG_SLOTS;
     if (i < n) {
-        w.A[i] = gA[i];
-        w.O[i] = gO[i];
-        w.Bv[i] = gB[i];
+        w.A[i] = a;
+        w.O[i] = o;
+        w.Bv[i] = b;
     }
     if (i < PW_B) {
         lvl(w, 0)[i] = i < nb ? (uint8_t)pm_bcnt_l(pd.meta + pg, i & 7) : 0;
@@ -375,6 +390,20 @@ TD void pg_win_flush_impl(PagedDoc<T> &pd) {
     pd.dirty = 0;
 }
 
+// Replaces the window by page pg: its loads are issued before the current window is
+// written back, so their latency hides behind the flush.
+TD void pg_win_switch(PagedDoc<T> &pd, int pg) {
+    v4i a = v4i{0, 0, 0, 0};
+    u64 o = 0;
+    v4u b = v4u{0, 0, 0, 0};
+    pg_win_fetch(pd, pg, a, o, b);
+    pg_win_flush(pd);
+    if (pd.w.status) return;
+    PG_T0(10)
+    pg_win_place(pd, pg, a, o, b);
+    PG_T1(10)
+}
+
 // ------------------------------------------------------------------ page view lengths
 // pvl[page] = view length of every page for (c, r); returns the total.
 TD int pg_views_impl(PagedDoc<T> &pd, int r, int c);
@@ -466,10 +495,7 @@ TD int pg_obs_start(PagedDoc<T> &pd, int pos) {
 }
 TD void pg_load_pos(PagedDoc<T> &pd, int pos) {
     const int pg = uni(pd.up.dir[pos]);
-    if (pd.cur != pg) {
-        pg_win_flush(pd);
-        pg_win_load(pd, pg);
-    }
+    if (pd.cur != pg) pg_win_switch(pd, pg);
     pd.cur_pos = pos;
     pd.w.obs_base = pg_obs_start(pd, pos);
 }
@@ -656,9 +682,8 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         if (i < 0) {
             const int pg = uni(pd.gumap[uid]);
             if (pg == pd.cur || pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) continue;
-            pg_win_flush(pd);
+            pg_win_switch(pd, pg);
             if (w.status) return;
-            pg_win_load(pd, pg);
             i = find_uid(w, uid);
             if (i < 0) continue;
         }
@@ -717,6 +742,7 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
         return;
     }
     pg_load_pos(pd, pos);
+    if (w.status) return;
     OpIn rel = in;
     rel.op.pos1 = op.pos1 - start;
     pd.vvalid = 0;
@@ -731,6 +757,7 @@ TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
     const int pos = pg_find(pd, p, true, start);
     if (pos < 0 || start >= p) return;   // p is at a page boundary or past the end
     pg_load_pos(pd, pos);
+    if (pd.w.status) return;
     boundary(pd.w, p - start, r, c);
     if (pd.w.status) return;
     pg_win_sync(pd);
@@ -760,6 +787,7 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
         const int np = nbr(pd.up, 1);
         while (pos < np && carry < p2) {
             pg_load_pos(pd, pos);
+            if (w.status) return;
             w.obs_base = ocarry;
             const bool done = range_mark(w, op, rec, carry, ocarry, cb);
             if (w.status) return;
@@ -792,9 +820,8 @@ TD void pg_load_removed(PagedDoc<T> &pd, const mt_op_rec &op) {
             FAIL_INTERNAL(w);
             return;
         }
-        pg_win_flush(pd);
+        pg_win_switch(pd, pg);
         if (w.status) return;
-        pg_win_load(pd, pg);
         i = find_uid(w, uid);
         if (i < 0) {
             FAIL_INTERNAL(w);
