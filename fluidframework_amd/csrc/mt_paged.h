@@ -667,20 +667,23 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         if (w.heap_n == 0) break;
         const v2i top = heap_top(w);
         if (top.x > w.min_seq) break;
-        PG_T0(5)
-        heap_pop(w);
-        wsync<T>();
-        PG_T1(5)
-        PG_T0(4)
         const uint32_t uid = (uint32_t)top.y;
         if (uid >= (uint32_t)pd.UM) {
             pg_fail_cap(w, 9);
             return;
         }
+        // the segment's page from the uid map: issued before the heap pop so that its
+        // latency hides behind it; needed only if the segment is not in the window
+        const int gpg = pd.gumap[uid];
+        PG_T0(5)
+        heap_pop(w);
+        wsync<T>();
+        PG_T1(5)
+        PG_T0(4)
         // the window first (its uid map entries are written when it is flushed)
         int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
         if (i < 0) {
-            const int pg = uni(pd.gumap[uid]);
+            const int pg = uni(gpg);
             if (pg == pd.cur || pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) continue;
             pg_win_switch(pd, pg);
             if (w.status) return;
