@@ -1,0 +1,58 @@
+"""CPU checks of bench.py's workload contract: the default is the metric's configuration
+(C3 shard), its paged capacities fit the documents-per-CU budget and fall back to loose
+ones, and the recorded evidence it quotes (PMC traffic, CPU calibration) matches it."""
+import json
+import os
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    import bench as b
+    return b
+
+
+def _configs():
+    return json.load(open(os.path.join(REPO, "bench", "configs.json")))
+
+
+def test_default_workload_is_the_metric_config(bench, monkeypatch):
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    args = bench.parse()
+    assert args.config == "c3" and args.gpus == 1
+    cfg = _configs()["c3"]
+    # 100k documents over 8 GPUs: each rank replays a 12.5k-document shard
+    assert cfg["docs"] == 100000 and cfg["docs"] // 8 == 12500 and cfg["ops"] == 10000
+
+
+def test_paged_capacities_tight_then_loose(bench):
+    cfg = _configs()["c3"]
+    tight, loose = bench.capacities(cfg), bench.capacities(cfg, tight=False)
+    # measured peaks over 12.5k C3 documents: pages 180, table 195, heap 159
+    assert (tight["page_capacity"], tight["unsettled_capacity"], tight["page_heap_capacity"]) == (208, 240, 224)
+    for k in ("page_capacity", "unsettled_capacity", "page_heap_capacity"):
+        assert loose[k] >= tight[k]
+    # the deep-lag stress config keeps its large capacities
+    c4 = bench.capacities(_configs()["c4"])
+    assert c4["unsettled_capacity"] >= 2048
+
+
+def test_recorded_traffic_matches_default_workload():
+    pm = json.load(open(os.path.join(REPO, "profiles", "pmc_summary.json")))
+    e = pm["c3"]
+    assert e["docs"] == 12500 and e["ops"] == 10000 and e["hbm_bytes_per_launch"] > 0
+    src = os.path.join(REPO, e["note"].split("source ")[-1])
+    assert os.path.exists(src)
+
+
+def test_cpu_calibration_recorded():
+    cal = json.load(open(os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")))
+    for name in ("c2", "c3"):
+        c = cal[name]
+        assert c["threads"] == 1 and c["ops"] > 0
+        assert c["ratio_port_over_reference"] > 0
+        assert abs(c["port_ops_per_s"] / c["reference_ops_per_s"] - c["ratio_port_over_reference"]) < 0.01 * c[
+            "ratio_port_over_reference"]
