@@ -68,6 +68,10 @@ def capacities(cfg, tight=True):
                     page_heap_capacity=2560 if deep else 512,
                     unsettled_capacity=2560 if deep else 320,
                     uid_capacity=min(1 << 16, 3 * cfg["ops"] + 1024))
+        if tight and deep and cfg["ops"] <= 10000 and cfg["writers"] <= 64:
+            # C4 peaks over 1024 documents: 205 pages, 1764 table entries, 785 heap entries;
+            # 99 KB per document at the loose capacities (1 per CU) vs 69 KB here (2 per CU)
+            caps.update(page_capacity=256, unsettled_capacity=2048, page_heap_capacity=1024)
         if tight and not deep and cfg["ops"] <= 10000:
             # the paged layout's LDS footprint sets documents per CU: 27 KB at the loose
             # capacities (6 per CU) vs 16.1 KB here (10 per CU; the kernel is compiled for 3 waves/SIMD); a document
