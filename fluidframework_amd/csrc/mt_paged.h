@@ -459,45 +459,48 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c) {
 }
 // First level-1 position whose cumulative view end is >= p (strict: > p); start = its
 // view start.  -1 (start = total) if none.
-TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start);
-TD int pg_find(PagedDoc<T> &pd, int p, bool strict, int &start) {
+TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart);
+TD int pg_find(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart) {
     PG_T0(13)
-    const int r_ = pg_find_impl(pd, p, strict, start);
+    const int r_ = pg_find_impl(pd, p, strict, start, ostart);
     PG_T1(13)
     return r_;
 }
-TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start) {
+// ... and ostart = its observer start (the same pass over the directory)
+TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart) {
     const int np = nbr(pd.up, 1);
-    int carry = 0;
+    int carry = 0, ocarry = 0;
     for (int base = 0; base < np; base += MT_WAVE) {
         const int q = base + lane();
-        const int v = q < np ? pd.pvl[pd.up.dir[q]] : 0;
+        int v = 0, ov = 0;
+        if (q < np) {
+            const int pg = pd.up.dir[q];
+            v = pd.pvl[pg];
+            ov = pd.meta[pg].obs;
+        }
         const int inc = wave_scan_incl(v);
         const int end = carry + inc;
         const u64 m = ballot(q < np && (strict ? end > p : end >= p));
+        const int oinc = wave_scan_incl(ov);
         if (m) {
             const int fl = first_lane(m);
             start = bcast(end - v, fl);
+            ostart = ocarry + bcast(oinc - ov, fl);
             return base + fl;
         }
         carry += bcast(inc, MT_WAVE - 1);
+        ocarry += bcast(oinc, MT_WAVE - 1);
     }
     start = carry;
+    ostart = ocarry;
     return -1;
 }
-TD int pg_obs_start(PagedDoc<T> &pd, int pos) {
-    int s = 0;
-    for (int base = 0; base < pos; base += MT_WAVE) {
-        const int q = base + lane();
-        s += q < pos ? pd.meta[pd.up.dir[q]].obs : 0;
-    }
-    return wave_sum(s);
-}
-TD void pg_load_pos(PagedDoc<T> &pd, int pos) {
+// the window onto level-1 position pos, whose observer start is obs_base
+TD void pg_load_pos(PagedDoc<T> &pd, int pos, int obs_base) {
     const int pg = uni(pd.up.dir[pos]);
     if (pd.cur != pg) pg_win_switch(pd, pg);
     pd.cur_pos = pos;
-    pd.w.obs_base = pg_obs_start(pd, pos);
+    pd.w.obs_base = obs_base;
 }
 
 // ------------------------------------------------------------------ pack at level 1
@@ -729,7 +732,8 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     const int slen = (op.flags & MT_F_MARKER) ? 1 : op.pos2;
     pg_views_cached(pd, op.ref_seq, op_cli(op));
     int start;
-    const int pos = pg_find(pd, op.pos1, false, start);
+    int ostart;
+    const int pos = pg_find(pd, op.pos1, false, start, ostart);
     if (pos < 0) {
         if (slen == 0) {   // boundary only; nothing splits past the end
             if (op.flags & MT_F_LOAD) return;
@@ -744,7 +748,7 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
         fail(w, MT_DOC_INSERT_FAILED);
         return;
     }
-    pg_load_pos(pd, pos);
+    pg_load_pos(pd, pos, ostart);
     if (w.status) return;
     OpIn rel = in;
     rel.op.pos1 = op.pos1 - start;
@@ -757,9 +761,10 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
 TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
     pg_views_cached(pd, r, c);
     int start;
-    const int pos = pg_find(pd, p, true, start);
+    int ostart;
+    const int pos = pg_find(pd, p, true, start, ostart);
     if (pos < 0 || start >= p) return;   // p is at a page boundary or past the end
-    pg_load_pos(pd, pos);
+    pg_load_pos(pd, pos, ostart);
     if (pd.w.status) return;
     boundary(pd.w, p - start, r, c);
     if (pd.w.status) return;
@@ -784,14 +789,14 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
     pg_views_cached(pd, r, c);
     pd.vvalid = 0;   // range_mark changes view lengths
     int start;
-    int pos = pg_find(pd, p1, true, start);
+    int ostart;
+    int pos = pg_find(pd, p1, true, start, ostart);
     if (pos >= 0) {
-        int carry = start, ocarry = pg_obs_start(pd, pos);
+        int carry = start, ocarry = ostart;
         const int np = nbr(pd.up, 1);
         while (pos < np && carry < p2) {
-            pg_load_pos(pd, pos);
+            pg_load_pos(pd, pos, ocarry);
             if (w.status) return;
-            w.obs_base = ocarry;
             const bool done = range_mark(w, op, rec, carry, ocarry, cb);
             if (w.status) return;
             pg_win_sync(pd);
