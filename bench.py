@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
+    ap.add_argument("--shard", type=int, default=-1, help="document shard to replay (default: this rank)")
     ap.add_argument("--page-caps", default="", help="paged layout LDS capacities 'pages,unsettled,heap' (sweeps)")
     return ap.parse_args()
 
@@ -198,7 +199,7 @@ def main():
     docs = args.docs or {"c2": cfg["docs"], "c3": cfg["docs"] // 8}.get(args.config, min(cfg["docs"], 16384))
     if args.ops:
         cfg["ops"] = args.ops
-    doc_base = rank * docs
+    doc_base = (args.shard if args.shard >= 0 else rank) * docs
 
     caps = capacities(cfg)
     if args.lds_cap:
