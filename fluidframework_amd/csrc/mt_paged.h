@@ -360,14 +360,17 @@ TD void pg_win_sync(PagedDoc<T> &pd) {
     if (i < w.n) ol = obs_len(w.A[i]);
     const int obs = wave_sum(ol);
     const int pg = pd.cur;
+    // the level-1 count (== meta nblk) changes only with the page's leaf-block count: its
+    // directory position is looked up only then
+    const int old_nb = uni(pd.meta[pg].nblk);
     const bool vb = i < 8 && i < nbk;
     pm_set_blocks(pd, pg, i, vb, vb ? lvl(w, 0)[i] : 0, vb ? w.flg[i] : 0);
-    const int pos = pg_cur_pos(pd);
+    const int pos = nbk != old_nb ? pg_cur_pos(pd) : -1;
     if (i == 0) {
         pd.meta[pg].nseg = (uint8_t)w.n;
         pd.meta[pg].nblk = (uint8_t)nbk;
         pd.meta[pg].obs = obs;
-        lvl(up, 1)[pos] = (uint8_t)nbk;
+        if (pos >= 0) lvl(up, 1)[pos] = (uint8_t)nbk;
     }
     pd.dirty = 1;
     wsync<T>();
