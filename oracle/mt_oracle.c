@@ -85,6 +85,7 @@ struct orc_doc {
     int record;
     IVec dlog;             /* optional flattened delta records */
     uint64_t delta_hash;
+    uint32_t maint[3];     /* mergeTreeMaintenanceCallback events: SPLIT, APPEND, UNLINK */
 };
 
 /* ------------------------------------------------------------------ utilities */
@@ -343,6 +344,7 @@ static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
                     hold[(*nhold)++] = child;
                 } else {
                     s->n.parent = NULL;            /* unlink */
+                    d->maint[2]++;                 /* UNLINK :1343-1348 */
                 }
                 prev = NULL;
             } else if (s->seq <= d->min_seq) {
@@ -351,6 +353,7 @@ static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
                 if (ok) {
                     seg_append(d, prev, s);
                     s->n.parent = NULL;
+                    d->maint[1]++;                 /* APPEND :1368-1373 */
                 } else {
                     hold[(*nhold)++] = child;
                     prev = local_net_length(s) > 0 ? s : NULL;
@@ -499,6 +502,7 @@ static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_
                 } else {
                     Seg *next = split_at(d, s, pos);
                     if (!next) return NULL;
+                    d->maint[0]++;   /* splitLeafSegment SPLIT :2264-2269 */
                     new_node = &next->n;
                     ci++;
                 }
@@ -1060,6 +1064,10 @@ uint64_t orc_text_hash(const uint16_t *t, int32_t n) {
     }
     return h;
 }
+void orc_maintenance(orc_doc *d, uint32_t *out) {
+    for (int i = 0; i < 3; i++) out[i] = d->maint[i];
+}
+
 void orc_checksum(orc_doc *d, mt_checksum *out) {
     SumAcc a;
     memset(&a, 0, sizeof(a));

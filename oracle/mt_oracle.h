@@ -43,6 +43,9 @@ int32_t orc_leaves(orc_doc *d, int32_t *out, int32_t cap);
    segment has no property object; writes (key, value) pairs */
 int32_t orc_segment_props(orc_doc *d, int32_t seg_index, uint32_t *out, int32_t cap_pairs);
 void orc_checksum(orc_doc *d, mt_checksum *out);
+/* mergeTreeMaintenanceCallback event counts since creation: [SPLIT, APPEND, UNLINK]
+   (MT/mergeTree.ts:2264-2269, :1368-1373, :1343-1348) */
+void orc_maintenance(orc_doc *d, uint32_t *out);
 uint64_t orc_text_hash(const uint16_t *t, int32_t n);
 /* delta log: flattened records  [seq, kind, nsegs, (pos, len, ndeltas, (key, oldval)*)*]* */
 int32_t orc_deltas(orc_doc *d, int32_t *out, int32_t cap);

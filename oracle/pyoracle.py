@@ -56,6 +56,7 @@ def lib():
         L.orc_leaves.argtypes = [P, P, i32]
         L.orc_leaves.restype = i32
         L.orc_checksum.argtypes = [P, P]
+        L.orc_maintenance.argtypes = [P, P]
         L.orc_deltas.argtypes = [P, P, i32]
         L.orc_deltas.restype = i32
         L.orc_set_record_deltas.argtypes = [P, i32]
@@ -119,6 +120,12 @@ class OracleDoc:
             if st:
                 return st
         return 0
+
+    def maintenance(self):
+        """[SPLIT, APPEND, UNLINK] mergeTreeMaintenanceCallback counts (orc_maintenance)."""
+        m = np.zeros(3, dtype=np.uint32)
+        lib().orc_maintenance(self.h, _p(m))
+        return m.tolist()
 
     def outputs(self):
         L = lib()

@@ -333,6 +333,26 @@ function replayDoc(log) {
     return collectOutputs(c, deltas);
 }
 
+// Maintenance events (mergeTreeMaintenanceCallback, MT/mergeTree.ts:1343-1373 scourNode
+// UNLINK/APPEND, :2264-2269 splitLeafSegment SPLIT) counted per document over the same
+// observer replay as replayDoc: [SPLIT, APPEND, UNLINK].
+function maintDoc(log) {
+    const { c } = makeObserver(log.seed_text);
+    const counts = [0, 0, 0];
+    c.mergeTreeMaintenanceCallback = (args) => {
+        const i = args.operation === -2 ? 0 : args.operation === -1 ? 1 : args.operation === -3 ? 2 : -1;
+        if (i >= 0) { counts[i]++; }
+    };
+    const cseq = {};
+    for (const [k, t, r, msn, op, type] of log.msgs) {
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        c.applyMsg(msg);
+    }
+    return counts;
+}
+
 // ---------------------------------------------------------------- snapshots (config C5)
 // Cold catch-up = SnapshotV1 summary + tail ops (SURVEY.md S4): the observer after K ops is
 // summarised with the reference's own SnapshotV1.extractSync/emit (MT/snapshotV1.ts:87-252),
@@ -560,6 +580,9 @@ async function main() {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
+    } else if (mode === "maint") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        fs.writeFileSync(rest[1], JSON.stringify(logs.docs.map((d) => maintDoc(d))));
     } else if (mode === "time") {
         // time <gen.json> <out.json> [repeats]: the reference's Client.applyMsg replay of
         // every document's stream (messages pre-built, observer with the delta callback

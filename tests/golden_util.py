@@ -10,6 +10,7 @@ import numpy as np
 from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks
 from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts
 
+MAINT_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm"]
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INT_MIN = -2 ** 31
 ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm"]
@@ -19,6 +20,13 @@ SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
 def load(name):
     with gzip.open(os.path.join(GOLDEN, name + ".json.gz"), "rt") as fh:
         return json.load(fh)
+
+
+def maint_counts(name):
+    """Reference [SPLIT, APPEND, UNLINK] maintenance-event counts per document of a replay
+    fixture (tests/golden/make_maint.py), or None when the fixture has none."""
+    with open(os.path.join(GOLDEN, "ref_maint.json")) as f:
+        return json.load(f).get(name)
 
 
 def interner_for(fixture):

@@ -19,6 +19,21 @@ def test_oracle_matches_reference(oracle_lib, name):
         assert not errs, f"{name} doc {doc['doc']}: {errs}"
 
 
+@pytest.mark.parametrize("name", gu.MAINT_FIXTURES)
+def test_oracle_maintenance_events_match_reference(oracle_lib, name):
+    """mergeTreeMaintenanceCallback SPLIT/APPEND/UNLINK counts (MT/mergeTree.ts:2264-2269,
+    :1343-1373) equal the reference's own callback on every document."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    want = gu.maint_counts(name)
+    assert want is not None and len(want) == len(fx["docs"])
+    for i, doc in enumerate(fx["docs"]):
+        a = gu.encode_docs(fx, interner, [doc])
+        od = oracle_lib.OracleDoc.new(a["seed"][: a["seed_off"][1]])
+        assert od.apply_all(a["ops"], a["text"], a["props"]) == 0
+        assert od.maintenance() == want[i], f"{name} doc {doc['doc']}"
+
+
 @pytest.mark.parametrize("name", ["ref_small", "ref_c2", "ref_c3", "ref_c4"])
 def test_oracle_generator_reproduces_reference_streams(oracle_lib, name):
     """The generator (shared spec) draws identical op streams whether the view
