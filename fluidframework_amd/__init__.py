@@ -266,6 +266,13 @@ class MergeTreeBatch:
                     "mt_get_delta_log")
         return buf[: n.value].tolist()
 
+    def maintenance_counts(self):
+        """[n_docs, 3] SPLIT / APPEND / UNLINK mergeTreeMaintenanceCallback event counts
+        (needs delta_log_capacity > 0)."""
+        out = np.zeros((self.n_docs, 3), dtype=np.uint32)
+        self._check(self.lib.mt_maintenance_counts(self.h, _native.ptr(out)), "mt_maintenance_counts")
+        return out
+
     def checksums(self):
         out = np.zeros(self.n_docs, dtype=CHECKSUM_DTYPE)
         self._check(self.lib.mt_checksums(self.h, _native.ptr(out)), "mt_checksums")

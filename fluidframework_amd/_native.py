@@ -68,6 +68,7 @@ SIGNATURES = [
     ("mt_get_delta_log", _I, [_P, _U32, _P, _U32, _P]),
     ("mt_debug_raw", _I, [_P, _U32, _P, _U32, _P, _P]),
     ("mt_debug_prof", _I, [_P, _P, _I]),
+    ("mt_maintenance_counts", _I, [_P, _P]),
     ("mt_checksums", _I, [_P, _P]),
     ("mt_checksums_device", _I, [_P, _P]),
 ]

@@ -68,6 +68,11 @@ static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { retu
 #define HDR_NPAGES 1          // pages in the directory
 #define HDR_UTN 2             // entries of the unsettled-segment table
 #define HDR_DIAG 3            // failure diagnostic (source line of an internal error)
+// DocHdr.pad[] words of every document kept by delta-logging handles (T::kLog):
+// mergeTreeMaintenanceCallback event counts (MT/mergeTree.ts:2264-2269, :1368-1373, :1343-1348)
+#define HDR_MSPLIT 4
+#define HDR_MAPPEND 5
+#define HDR_MUNLINK 6
 
 struct DevState {
     DocHdr *hdr;

@@ -111,6 +111,7 @@ template <class T> struct DocT {
     int n, depth, heap_n, cur_seq, min_seq, text_top, text_half, props_top, props_half, next_uid,
         status, dlog_n, text_gcs, props_gcs, cap_cause;
     u64 dhash;
+    int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     // paged documents (mt_paged.h): this DocT is a window onto one page, or the instance
     // holding the levels >= 1 of the tree (dir != nullptr); all zero for flat documents
     int paged;              // 1: window onto one page
@@ -308,6 +309,11 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.status = h.status;
     d.dlog_n = h.dlog_n;
     d.dhash = h.delta_hash;
+    if (T::kLog) {
+        d.m_split = h.pad[HDR_MSPLIT];
+        d.m_append = h.pad[HDR_MAPPEND];
+        d.m_unlink = h.pad[HDR_MUNLINK];
+    }
     d.text_gcs = 0;
     d.props_gcs = 0;
     d.cap_cause = 0;
@@ -425,6 +431,11 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
         h.pad0 = 0;
 #pragma unroll
         for (int i = 0; i < 8; i++) h.pad[i] = 0;
+        if (T::kLog) {
+            h.pad[HDR_MSPLIT] = d.m_split;
+            h.pad[HDR_MAPPEND] = d.m_append;
+            h.pad[HDR_MUNLINK] = d.m_unlink;
+        }
         *d.hp = h;
     }
 }
@@ -956,6 +967,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
         return;
     }
     seg_move_right(d, i + 1, 1);
+    if (T::kLog) d.m_split++;   // splitLeafSegment's SPLIT event :2264-2269
     if (lane() == 0) {
         v4i a = d.A[i];
         v4u bb = d.Bv[i];
@@ -1113,6 +1125,10 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     const uint32_t myown = in ? (owners >> (4 * k)) & 0xFu : 0xFu;
     const u64 m_keep = ballot(in && myown == (uint32_t)k);
     const u64 m_app = ballot(in && myown != 0xFu && myown != (uint32_t)k);
+    if (T::kLog) {   // scourNode's UNLINK / APPEND events :1343-1373
+        d.m_unlink += __popcll(m_unlink);
+        d.m_append += __popcll(m_app);
+    }
     if (m_app) {
         // group length per keeper (lanes that are keepers sum their members)
         int glen = 0;
@@ -1305,6 +1321,10 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     }
     const bool unlink = in && removed && a.z <= d.min_seq;
     const bool surv = in && !unlink && !join;
+    if (T::kLog) {   // scourNode's UNLINK / APPEND events :1343-1373
+        d.m_unlink += __popcll(ballot(unlink));
+        d.m_append += __popcll(m_join);
+    }
     const u64 m_surv = ballot(surv);
     const u64 above = (k < 63) ? (m_join >> (k + 1)) : 0ull;
     const u64 m_grp = ballot(surv && (above & 1ull));

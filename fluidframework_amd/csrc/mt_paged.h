@@ -1061,6 +1061,11 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.status = h.status;
     w.dlog_n = h.dlog_n;
     w.dhash = h.delta_hash;
+    if (T::kLog) {
+        w.m_split = h.pad[HDR_MSPLIT];
+        w.m_append = h.pad[HDR_MAPPEND];
+        w.m_unlink = h.pad[HDR_MUNLINK];
+    }
     w.text_gcs = w.props_gcs = w.cap_cause = 0;
     w.paged = 1;
     w.obs_base = 0;
@@ -1195,6 +1200,11 @@ TD void pg_store(PagedDoc<T> &pd) {
         h.pad[HDR_NPAGES] = np;
         h.pad[HDR_UTN] = pd.ut_n;
         h.pad[HDR_DIAG] = w.status ? w.cap_cause : 0;
+        if (T::kLog) {
+            h.pad[HDR_MSPLIT] = w.m_split;
+            h.pad[HDR_MAPPEND] = w.m_append;
+            h.pad[HDR_MUNLINK] = w.m_unlink;
+        }
         *w.hp = h;
     }
 }

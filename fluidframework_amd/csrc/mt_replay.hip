@@ -1877,6 +1877,20 @@ int mt_checksums_device(mt_handle *h, void *device_out) {
     return 0;
 }
 
+int mt_maintenance_counts(mt_handle *h, uint32_t *out) {
+    if (!h || !out || !h->st.DL) return MT_E_INVALID;   // kept by delta-logging handles only
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::vector<DocHdr> hd(h->n_docs);
+    HIPCHK(h, hipMemcpy(hd.data(), h->st.hdr, h->n_docs * sizeof(DocHdr), hipMemcpyDeviceToHost));
+    for (uint32_t d = 0; d < h->n_docs; d++) {
+        out[3 * d] = (uint32_t)hd[d].pad[HDR_MSPLIT];
+        out[3 * d + 1] = (uint32_t)hd[d].pad[HDR_MAPPEND];
+        out[3 * d + 2] = (uint32_t)hd[d].pad[HDR_MUNLINK];
+    }
+    return 0;
+}
+
 int mt_checksums(mt_handle *h, mt_checksum *out) {
     if (!h || !out) return MT_E_INVALID;
     int rc = mt_checksums_device(h, h->d_sums);

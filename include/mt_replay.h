@@ -180,6 +180,12 @@ int mt_debug_prof(mt_handle *h, uint64_t *out /* [32] */, int reset);
 /* Delta log (only with delta_log_capacity > 0), oracle layout. */
 int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uint32_t *n);
 
+/* mergeTreeMaintenanceCallback events per document since its creation (only with
+   delta_log_capacity > 0, MT_E_INVALID otherwise): out[3*doc + {0,1,2}] = SPLIT
+   (splitLeafSegment, MT/mergeTree.ts:2260-2272), APPEND and UNLINK (scourNode,
+   MT/mergeTree.ts:1322-1398).  Counts, not event objects: segments are device rows. */
+int mt_maintenance_counts(mt_handle *h, uint32_t *out);
+
 /* Per-document checksums (mt_types.h), to host memory or straight into device memory
    on the handle's device (e.g. a torch tensor's data_ptr() before an RCCL all-gather). */
 int mt_checksums(mt_handle *h, mt_checksum *out);

@@ -102,6 +102,22 @@ def test_gpu_split_batches_equal_single_batch(oracle_lib, tier):
         assert any(mt2.is_paged(i) for i in range(len(fx["docs"])))
 
 
+@pytest.mark.parametrize("tier", list(TIERS))
+@pytest.mark.parametrize("name", gu.MAINT_FIXTURES)
+def test_gpu_maintenance_events_match_reference(name, tier):
+    """mergeTreeMaintenanceCallback SPLIT / APPEND / UNLINK counts per document equal the
+    reference's own callback (tests/golden/ref_maint.json) on every storage tier."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), **TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    got = mt.maintenance_counts().tolist()
+    assert got == gu.maint_counts(name), name
+
+
 @pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged"])
 @pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6), ("c3", 3000, 4)])
 def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
@@ -115,6 +131,7 @@ def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     b = mt.generate(cfg)
     got = b.download()
     gsums = mt.checksums()
+    omaint = []
     for d in range(docs):
         g = oracle_lib.generate(cfg, d, keep=True)
         lo, hi = got["doc_off"][d], got["doc_off"][d + 1]
@@ -124,12 +141,15 @@ def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
         osum = g["doc"].outputs()["checksum"]
         for f in ("length", "text_hash", "props_hash", "delta_hash"):
             assert gsums[d][f] == osum[f], (d, f)
+        omaint.append(g["doc"].maintenance())
     # replaying the generated batch from the seeds reproduces the same final state
     seed_off, seed = mt.generated_seeds(cfg)
     mt.load_initial_text(seed_off, seed)
     b.apply_async()
     mt.sync()
     assert np.array_equal(mt.checksums(), gsums)
+    # the generator kernels keep no event counts; the (delta-logging) replay does
+    assert mt.maintenance_counts().tolist() == omaint
 
 
 @pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged"])
