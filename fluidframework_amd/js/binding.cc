@@ -302,6 +302,23 @@ napi_value GetDeltaLog(napi_env env, napi_callback_info info) {
     return arr;
 }
 
+// maintenanceCounts(h) -> Uint32Array [nDocs * 3]: SPLIT, APPEND, UNLINK per document
+// (mergeTreeMaintenanceCallback events; only with deltaLogCapacity > 0)
+napi_value MaintenanceCounts(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const uint32_t n = 3u * mt_num_docs(hd->h);
+    void *d;
+    napi_value ab, arr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 4, &d, &ab));
+    const int rc = mt_maintenance_counts(hd->h, (uint32_t *)d);
+    if (rc) return throw_rc(env, hd, rc, "mt_maintenance_counts");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, n, ab, 0, &arr));
+    return arr;
+}
+
 // checksums(h) -> ArrayBuffer of mt_checksum[nDocs] (32 B each)
 napi_value Checksums(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -341,6 +358,7 @@ napi_value Init(napi_env env, napi_value exports) {
     } fns[] = {{"create", Create},         {"destroy", Destroy},           {"loadInitialText", LoadInitialText},
                {"applyOps", ApplyOps},     {"loadSnapshots", LoadSnapshots},     {"status", Status},             {"getLength", GetLength},
                {"getText", GetText},       {"getPropRuns", GetPropRuns},   {"getDeltaLog", GetDeltaLog},
+               {"maintenanceCounts", MaintenanceCounts},
                {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs}};
     for (auto &f : fns) {
         napi_value v;

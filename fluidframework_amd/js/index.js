@@ -223,6 +223,17 @@ class GpuClient {
     }
 
     /**
+     * mergeTreeMaintenanceCallback events of this document so far (MergeTreeMaintenanceType
+     * SPLIT / APPEND / UNLINK, mergeTreeDeltaCallback.ts:15-35), as counts; needs a batch
+     * created with deltaLogCapacity > 0.
+     */
+    getMaintenanceCounts() {
+        this._sync();
+        const m = native.maintenanceCounts(this.batch.h);
+        return { split: m[3 * this.doc], append: m[3 * this.doc + 1], unlink: m[3 * this.doc + 2] };
+    }
+
+    /**
      * Replays the device delta log into mergeTreeDeltaCallback(opArgs, deltaArgs) calls
      * (mergeTreeDeltaCallback.ts:33-41): one per op, deltaSegments carrying the segment's
      * cachedLength, its observer position at callback time (what SequenceDeltaEvent.ranges

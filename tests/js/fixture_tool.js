@@ -52,6 +52,20 @@ if (mode === "encode") {
         }
     });
     process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }));
+} else if (mode === "maint") {
+    // maint <fixture.json.gz> -> [[split, append, unlink] per doc] through the facade
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const batch = new GpuMergeTreeBatch(fx.docs.length,
+        { segCapacity: 4096, textCapacity: 1 << 17, deltaLogCapacity: 1 << 18 });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const views = fx.docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        for (const m of msgs(d)) { c.applyMsg(m); }
+        return c;
+    });
+    const out = views.map((c) => { const m = c.getMaintenanceCounts(); return [m.split, m.append, m.unlink]; });
+    process.stdout.write(JSON.stringify({ docs: out }));
 } else if (mode === "snapenc") {
     const { SnapshotEncoder, decodeChunks } = require(path.join(repo, "fluidframework_amd", "js", "snapshot.js"));
     const { Grow } = require(path.join(repo, "fluidframework_amd", "js", "encode.js"));

@@ -78,6 +78,14 @@ def test_js_facade_replays_fixture_like_reference(name):
             assert props == exp, (p, props, exp)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_ext", "ref_c3"])
+def test_js_facade_maintenance_counts_match_reference(name):
+    _addon()
+    got = _node("maint", os.path.join(gu.GOLDEN, name + ".json.gz"))
+    assert got["docs"] == gu.maint_counts(name)
+
+
 @pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
 def test_js_snapshot_decoder_matches_python(name):
     """The Node facade's summary decoder (js/snapshot.js) writes exactly the mt_seg_rec records
