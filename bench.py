@@ -75,9 +75,11 @@ def capacities(cfg, tight=True):
             caps.update(page_capacity=256, unsettled_capacity=2048, page_heap_capacity=1024)
         if tight and not deep and cfg["ops"] <= 10000:
             # the paged layout's LDS footprint sets documents per CU: 27 KB at the loose
-            # capacities (6 per CU) vs 16.1 KB here (10 per CU; the kernel is compiled for 3 waves/SIMD); a document
-            # that outgrows them fails generation and the run falls back to the loose ones
-            caps.update(page_capacity=208, unsettled_capacity=240, page_heap_capacity=224)   # 16.1 KB: 10 per CU
+            # capacities (6 per CU), 16.0 KB at 208/240/224 (10 per CU), 14.9 KB here (11 per
+            # CU; the kernel is compiled for 3 waves/SIMD): peaks over all 100k C3 documents
+            # are 183 pages, 208 table entries, 173 heap entries.  A document that outgrows
+            # them fails generation and the run falls back to the loose ones
+            caps.update(page_capacity=192, unsettled_capacity=220, page_heap_capacity=192)   # 14.9 KB: 11 per CU
         return caps
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 

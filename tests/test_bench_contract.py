@@ -32,7 +32,7 @@ def test_paged_capacities_tight_then_loose(bench):
     cfg = _configs()["c3"]
     tight, loose = bench.capacities(cfg), bench.capacities(cfg, tight=False)
     # measured peaks over 12.5k C3 documents: pages 180, table 195, heap 159
-    assert (tight["page_capacity"], tight["unsettled_capacity"], tight["page_heap_capacity"]) == (208, 240, 224)
+    assert (tight["page_capacity"], tight["unsettled_capacity"], tight["page_heap_capacity"]) == (192, 220, 192)
     for k in ("page_capacity", "unsettled_capacity", "page_heap_capacity"):
         assert loose[k] >= tight[k]
     # the deep-lag stress config keeps its large capacities
