@@ -43,14 +43,88 @@ def parse():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: config)")
     ap.add_argument("--ops", type=int, default=0, help="ops per document (default: config)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = every core this process may use)")
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="0 = all docs of rank 0")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
     ap.add_argument("--shard", type=int, default=-1, help="document shard to replay (default: this rank)")
     ap.add_argument("--page-caps", default="", help="paged layout LDS capacities 'pages,unsettled,heap' (sweeps)")
+    ap.add_argument("--verify-per-rank", type=int, default=4,
+                    help="N > 1: documents of every rank's shard re-derived by the CPU oracle on rank 0")
     return ap.parse_args()
+
+
+def host_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota (a GPU
+    box shows the whole machine in os.cpu_count() but grants a share of it)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def launch(args):
+    """`--gpus N` without a torch.distributed launcher: start N ranks (one process per GPU)
+    through torch.distributed.run as a child process -- before this process touches the GPU
+    -- and exit with its status.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def oracle_checksums(cfg, global_docs, threads):
+    """mt_checksum of each generated document re-derived on the CPU by the oracle (the
+    checker: oracle/mt_oracle.c generates the same stream and replays it)."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    from fluidframework_amd.wire import CHECKSUM_DTYPE
+
+    def one(d):
+        g = pyoracle.generate(cfg, int(d), keep=True)
+        return g["doc"].outputs()["checksum"]
+
+    out = np.zeros(len(global_docs), dtype=CHECKSUM_DTYPE)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        for i, cs in enumerate(ex.map(one, global_docs)):
+            out[i] = cs
+    return out
+
+
+def verify_shards(dist, rank, world, docs, cfg, local, gen_sums, device, per_rank, threads):
+    """The multi-GPU exchange step and its check.  Every rank's replay checksums (`local`:
+    a uint8 tensor filled on the device, or a CHECKSUM_DTYPE array) and generation checksums
+    are all-gathered (RCCL over xGMI with backend nccl); rank 0 then checks that the timed
+    replay reproduced the generation for every document of every shard, and that
+    `per_rank` documents of every shard equal the CPU oracle's replay of the same global
+    documents.  Returns the report on rank 0, None elsewhere."""
+    from fluidframework_amd.shard import digest, gather_checksums
+    n_total = docs * world
+    got = gather_checksums(local, dist, device=device, n_total=n_total)
+    gen = gather_checksums(gen_sums, dist, device=device, n_total=n_total)
+    if rank != 0:
+        return None
+    pick = sorted({int(x) for x in np.linspace(0, docs - 1, num=max(1, min(per_rank, docs)))})
+    gdocs = [r * docs + i for r in range(world) for i in pick]
+    orc = oracle_checksums(cfg, gdocs, threads) if per_rank > 0 else None
+    mism = int(sum(got[g] != orc[j] for j, g in enumerate(gdocs))) if orc is not None else None
+    return dict(docs_gathered=int(len(got)), replay_equals_generation=bool(np.array_equal(got, gen)),
+                oracle_docs=len(gdocs) if orc is not None else 0, oracle_mismatches=mism,
+                digest=digest(got))
 
 
 def capacities(cfg, tight=True):
@@ -150,7 +224,7 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
         lo = {k: v for k, v in load.items()}
         lo["doc_off"] = load["doc_off"][: n_sample + 1]
         sa = dict(tail_arr, doc_off=tail_arr["doc_off"][: n_sample + 1])
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        threads = args.cpu_threads or host_cores()
         t_c = time.perf_counter()
         osums, ost = pyoracle.load_replay_batch(lo, sa, threads=threads)
         t_c = time.perf_counter() - t_c
@@ -179,9 +253,13 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but {world} rank(s) were launched")
     dist = None
     if world > 1:
         import torch
@@ -264,17 +342,20 @@ def main():
     sums = mt.checksums()
     replay_consistent = bool(np.array_equal(sums, gen_sums)) and int((status != 0).sum()) == 0
 
-    # the only collective: all-gather of per-document checksums over RCCL/xGMI
-    digest = None
+    threads = args.cpu_threads or host_cores()
+    # the only collective: all-gather of per-document checksums over RCCL/xGMI, verified
+    shards = None
     if dist is not None:
         import torch
-        from fluidframework_amd.shard import digest as sum_digest, gather_checksums
         local = torch.empty(docs * 32, dtype=torch.uint8, device="cuda")
         mt.checksums_device(local.data_ptr())
-        digest = sum_digest(gather_checksums(local, dist))
+        shards = verify_shards(dist, rank, world, docs, cfg, local, gen_sums, torch.device("cuda", local_rank),
+                               args.verify_per_rank, threads)
         ok = torch.tensor([1 if replay_consistent else 0], device="cuda")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         replay_consistent = bool(ok.item())
+        if rank == 0 and not (shards["replay_equals_generation"] and shards["oracle_mismatches"] in (0, None)):
+            replay_consistent = False
 
     if rank != 0:
         if dist is not None:
@@ -313,11 +394,11 @@ def main():
         sel_end = int(off[n_sample])
         arrays = dict(ops=host["ops"][:sel_end], doc_off=off[: n_sample + 1], text=host["text"],
                       props=host["props"], seed_off=seed_off[: n_sample + 1], seed=seed)
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
         t_c = time.perf_counter()
         osums, ost = pyoracle.replay_batch(arrays, threads=threads)
         t_c = time.perf_counter() - t_c
         cpu = dict(value=round(sel_end / t_c, 1), unit="ops/s", cores=threads, kind="port",
+                   host_cpus=os.cpu_count(),
                    sample=f"oracle/mt_oracle.c replay of rank-0 docs [0,{n_sample}) of the same "
                           f"{args.config} batch ({sel_end} ops) on {threads} host threads, {t_c:.2f} s")
         parity = dict(docs_checked=n_sample,
@@ -335,6 +416,7 @@ def main():
                 how=f"port value / {r} (port vs transpiled reference MergeTree under {cal['reference_runtime']}, "
                     f"one thread each, {cal['ops']} {args.config} ops; {os.path.relpath(CALIBRATION, REPO)})")
 
+    assert world == args.gpus
     out = {
         "metric": "sequenced merge-tree ops applied/sec (node) at 100k docs; bit-exact text+props",
         "value": round(value, 1),
@@ -368,7 +450,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "parity": {"replay_equals_generation": replay_consistent, "oracle_sample": parity,
-                   "checksum_allgather_digest": digest},
+                   "shards": shards},
         "gen_s": round(t_gen, 2),
     }
     print(json.dumps(out))

@@ -11,7 +11,16 @@ import numpy as np
 from . import _native
 from .wire import CHECKSUM_DTYPE, OP_DTYPE, Batch, Interner  # noqa: F401
 
-__all__ = ["MergeTreeBatch", "DeviceBatch", "Batch", "Interner"]
+__all__ = ["MergeTreeBatch", "DeviceBatch", "Batch", "Interner", "DeltaLogOverflow"]
+
+
+class DeltaLogOverflow(RuntimeError):
+    """A document's delta log dropped records (mt_get_delta_log -> MT_E_OVERFLOW); `records`
+    holds the whole records that were kept."""
+
+    def __init__(self, msg, records):
+        super().__init__(msg)
+        self.records = records
 
 
 class MergeTreeBatch:
@@ -259,12 +268,23 @@ class MergeTreeBatch:
         return bool(self.debug_raw(doc)[1][24])
 
     def get_delta_log(self, doc):
+        """The document's delta-log records since the last reset (oracle layout); raises
+        DeltaLogOverflow when records were dropped (delta_log_capacity too small)."""
         n = ctypes.c_uint32()
-        self._check(self.lib.mt_get_delta_log(self.h, doc, None, 0, ctypes.byref(n)), "mt_get_delta_log")
+        buf = np.zeros(1, dtype=np.int32)
+        rc = self.lib.mt_get_delta_log(self.h, doc, None, 0, ctypes.byref(n))
+        if rc not in (0, _native.MT_E_OVERFLOW):
+            self._check(rc, "mt_get_delta_log")
         buf = np.zeros(max(n.value, 1), dtype=np.int32)
-        self._check(self.lib.mt_get_delta_log(self.h, doc, _native.ptr(buf), n.value, ctypes.byref(n)),
-                    "mt_get_delta_log")
+        rc = self.lib.mt_get_delta_log(self.h, doc, _native.ptr(buf), n.value, ctypes.byref(n))
+        if rc == _native.MT_E_OVERFLOW:
+            raise DeltaLogOverflow(self.lib.mt_last_error(self.h).decode(), buf[: n.value].tolist())
+        self._check(rc, "mt_get_delta_log")
         return buf[: n.value].tolist()
+
+    def delta_log_reset(self):
+        """Empties every document's delta log (after its records were consumed)."""
+        self._check(self.lib.mt_delta_log_reset(self.h), "mt_delta_log_reset")
 
     def maintenance_counts(self):
         """[n_docs, 3] SPLIT / APPEND / UNLINK mergeTreeMaintenanceCallback event counts

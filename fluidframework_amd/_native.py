@@ -10,6 +10,7 @@ import numpy as np
 from .wire import CHECKSUM_DTYPE, OP_DTYPE
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+MT_E_INVALID, MT_E_HIP, MT_E_NOMEM, MT_E_NODEVICE, MT_E_OVERFLOW = -1, -2, -3, -4, -5
 LIB_PATH = os.path.join(HERE, "libmtreplay.so")
 
 
@@ -66,6 +67,7 @@ SIGNATURES = [
     ("mt_get_segments", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
     ("mt_get_segment_props", _I, [_P, _U32, _U32, _P, _U32, _P]),
     ("mt_get_delta_log", _I, [_P, _U32, _P, _U32, _P]),
+    ("mt_delta_log_reset", _I, [_P]),
     ("mt_debug_raw", _I, [_P, _U32, _P, _U32, _P, _P]),
     ("mt_debug_prof", _I, [_P, _P, _I]),
     ("mt_maintenance_counts", _I, [_P, _P]),

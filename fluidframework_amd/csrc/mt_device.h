@@ -73,6 +73,7 @@ static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { retu
 #define HDR_MSPLIT 4
 #define HDR_MAPPEND 5
 #define HDR_MUNLINK 6
+#define HDR_DLOG_OVF 7        // the delta log overflowed (records dropped since the last reset)
 
 struct DevState {
     DocHdr *hdr;

@@ -112,6 +112,7 @@ template <class T> struct DocT {
         status, dlog_n, text_gcs, props_gcs, cap_cause;
     u64 dhash;
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
+    int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
     // paged documents (mt_paged.h): this DocT is a window onto one page, or the instance
     // holding the levels >= 1 of the tree (dir != nullptr); all zero for flat documents
     int paged;              // 1: window onto one page
@@ -313,6 +314,8 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
         d.m_split = h.pad[HDR_MSPLIT];
         d.m_append = h.pad[HDR_MAPPEND];
         d.m_unlink = h.pad[HDR_MUNLINK];
+        d.dlog_ovf = h.pad[HDR_DLOG_OVF];
+        d.dlog_rec = -1;
     }
     d.text_gcs = 0;
     d.props_gcs = 0;
@@ -435,6 +438,7 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
             h.pad[HDR_MSPLIT] = d.m_split;
             h.pad[HDR_MAPPEND] = d.m_append;
             h.pad[HDR_MUNLINK] = d.m_unlink;
+            h.pad[HDR_DLOG_OVF] = d.dlog_ovf;
         }
         *d.hp = h;
     }
@@ -908,33 +912,57 @@ TD bool match_props(DocT<T> &d, uint32_t ha, uint32_t hb) {
 }
 
 // ------------------------------------------------------------------ delta callbacks
+// Every mergeTreeDeltaCallback folds into the document's delta hash.  Delta-logging handles
+// (T::kLog) also append the record [seq, kind, n, entries...] to the document's log.  A
+// record is written whole or not at all: when the next words of the open record do not fit,
+// the partial record is dropped and the log is marked overflowed (sticky until
+// mt_delta_log_reset), so a reader never sees a count without its entries.
 struct Cb {
     u64 h;
     int n;
-    int log_hdr;  // dlog index of the record header, -1 if not logging
 };
 TD Cb cb_begin(DocT<T> &d, int seq, int kind) {
     Cb cb;
     cb.h = fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)seq), (uint32_t)kind);
     cb.n = 0;
-    cb.log_hdr = -1;
-    if (T::kLog && d.dlog && d.dlog_n + 3 <= d.DL_cap) {
-        cb.log_hdr = d.dlog_n;
-        if (lane() == 0) {
-            d.dlog[d.dlog_n] = seq;
-            d.dlog[d.dlog_n + 1] = kind;
+    if constexpr (T::kLog) {
+        d.dlog_rec = -1;
+        if (d.dlog) {
+            if (!d.dlog_ovf && d.dlog_n + 3 <= d.DL_cap) {
+                d.dlog_rec = d.dlog_n;
+                if (lane() == 0) {
+                    d.dlog[d.dlog_n] = seq;
+                    d.dlog[d.dlog_n + 1] = kind;
+                }
+                d.dlog_n += 3;
+            } else {
+                d.dlog_ovf = 1;
+            }
         }
-        d.dlog_n += 3;
     }
     return cb;
+}
+// Room for `words` more words of the open record; on overflow the record is dropped.
+TD bool cb_room(DocT<T> &d, int words) {
+    if constexpr (T::kLog) {
+        if (!d.dlog || d.dlog_rec < 0) return false;
+        if (d.dlog_n + words <= d.DL_cap) return true;
+        d.dlog_n = d.dlog_rec;
+        d.dlog_rec = -1;
+        d.dlog_ovf = 1;
+    }
+    return false;
 }
 TD void cb_end(DocT<T> &d, Cb &cb) {
     cb.h = fnv_u32(cb.h, (uint32_t)cb.n);
     d.dhash = fnv_u64(d.dhash, cb.h);
-    if (T::kLog && cb.log_hdr >= 0 && lane() == 0) d.dlog[cb.log_hdr + 2] = cb.n;
+    if constexpr (T::kLog) {
+        if (d.dlog && d.dlog_rec >= 0 && lane() == 0) d.dlog[d.dlog_rec + 2] = cb.n;
+        d.dlog_rec = -1;
+    }
 }
 TD void cb_log(DocT<T> &d, int32_t v) {
-    if (T::kLog && d.dlog && d.dlog_n + 1 <= d.DL_cap) {
+    if (cb_room(d, 1)) {
         if (lane() == 0) d.dlog[d.dlog_n] = v;
         d.dlog_n++;
     }
@@ -1916,15 +1944,18 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                     const uint32_t ohj = (uint32_t)bcast((int)bv.y, j), nhj = (uint32_t)bcast((int)nh, j);
                     int nl = 0;
                     u64 dummy = 0;
-                    const int at = d.dlog_n + 1;
                     gsync_rd();
-                    if (L == 0 && at + 4 * MT_KMAX + 2 <= d.DL_cap) {
-                        // old record is untouched (new record went to a fresh handle)
-                        annotate_record(d, ohj, nhj, rec, dummy, d.dlog + at, nl);
-                        d.dlog[at - 1] = nl / 2;
+                    // propertyDeltas: <= one per old key (rewrite) plus one per op key
+                    if (cb_room(d, 1 + 2 * (MT_KMAX + (int)(rec[0] & 0xFFFF)))) {
+                        const int at = d.dlog_n + 1;
+                        if (L == 0) {
+                            // old record is untouched (new record went to a fresh handle)
+                            annotate_record(d, ohj, nhj, rec, dummy, d.dlog + at, nl);
+                            d.dlog[at - 1] = nl / 2;
+                        }
+                        nl = bcast(nl, 0);
+                        d.dlog_n += 1 + nl;
                     }
-                    nl = bcast(nl, 0);
-                    d.dlog_n += 1 + nl;
                 }
             }
         }
@@ -2049,13 +2080,17 @@ TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const G
         }
         z = false;
         if (!(op.flags & MT_F_GROUP_MORE)) {
-            if (!(d.cur_seq <= op.seq)) {
-                fail(d, MT_DOC_SEQ_ORDER);
+            if (!(d.cur_seq <= op.seq)) {   // updateSeqNumbers MT/client.ts:824
+                fail(d, MT_DOC_SEQ_BACKWARDS);
                 return;
             }
             d.cur_seq = op.seq;
-            if (!(op.min_seq <= op.seq) || !(d.min_seq <= op.min_seq)) {
-                fail(d, MT_DOC_MINSEQ_ORDER);
+            if (!(op.min_seq <= op.seq)) {    // MT/client.ts:826
+                fail(d, MT_DOC_MSN_ABOVE_SEQ);
+                return;
+            }
+            if (!(d.min_seq <= op.min_seq)) {   // setMinSeq MT/mergeTree.ts:1755
+                fail(d, MT_DOC_MSN_BACKWARDS);
                 return;
             }
             if (op.min_seq > d.min_seq) {

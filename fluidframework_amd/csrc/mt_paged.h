@@ -880,13 +880,17 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
         }
         z = false;
         if (!(op.flags & MT_F_GROUP_MORE)) {
-            if (!(w.cur_seq <= op.seq)) {
-                fail(w, MT_DOC_SEQ_ORDER);
+            if (!(w.cur_seq <= op.seq)) {   // updateSeqNumbers MT/client.ts:824
+                fail(w, MT_DOC_SEQ_BACKWARDS);
                 return;
             }
             w.cur_seq = op.seq;
-            if (!(op.min_seq <= op.seq) || !(w.min_seq <= op.min_seq)) {
-                fail(w, MT_DOC_MINSEQ_ORDER);
+            if (!(op.min_seq <= op.seq)) {    // MT/client.ts:826
+                fail(w, MT_DOC_MSN_ABOVE_SEQ);
+                return;
+            }
+            if (!(w.min_seq <= op.min_seq)) {   // setMinSeq MT/mergeTree.ts:1755
+                fail(w, MT_DOC_MSN_BACKWARDS);
                 return;
             }
             if (op.min_seq > w.min_seq) {
@@ -1065,6 +1069,8 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
         w.m_split = h.pad[HDR_MSPLIT];
         w.m_append = h.pad[HDR_MAPPEND];
         w.m_unlink = h.pad[HDR_MUNLINK];
+        w.dlog_ovf = h.pad[HDR_DLOG_OVF];
+        w.dlog_rec = -1;
     }
     w.text_gcs = w.props_gcs = w.cap_cause = 0;
     w.paged = 1;
@@ -1204,6 +1210,7 @@ TD void pg_store(PagedDoc<T> &pd) {
             h.pad[HDR_MSPLIT] = w.m_split;
             h.pad[HDR_MAPPEND] = w.m_append;
             h.pad[HDR_MUNLINK] = w.m_unlink;
+            h.pad[HDR_DLOG_OVF] = w.dlog_ovf;
         }
         *w.hp = h;
     }

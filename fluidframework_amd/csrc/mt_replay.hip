@@ -995,6 +995,35 @@ struct mt_batch {
     } while (0)
 
 static TierCaps glb_caps(const mt_handle *h) { return TierCaps{0, h->st.B, 0, h->lds.S > 0 ? 1 : 0}; }
+
+// A props record [count | combine << 16, (key, value) x count] lies inside the arena.
+static bool props_rec_ok(const uint32_t *props, uint64_t props_len, uint32_t off) {
+    if (off == MT_NO_PROPS) return true;
+    if ((uint64_t)off >= props_len) return false;
+    const uint64_t cnt = props[off] & 0xFFFFu;
+    return (uint64_t)off + 1 + 2 * cnt <= props_len;
+}
+// Host-side bounds check of a batch (MT_E_INVALID instead of a device fault): per-document
+// offsets monotonic inside [0, n_ops], every insert payload inside the text arena, every
+// props record inside the props arena, known op kinds.
+static std::string validate_batch(uint32_t n_docs, const int64_t *off, const mt_op_rec *ops, uint64_t n_ops,
+                                  uint64_t text_len, const uint32_t *props, uint64_t props_len) {
+    if (off[0] < 0) return "doc_op_off[0] < 0";
+    for (uint32_t d = 0; d < n_docs; d++)
+        if (off[d + 1] < off[d]) return "doc_op_off not monotonic at document " + std::to_string(d);
+    if ((uint64_t)off[n_docs] > n_ops) return "doc_op_off exceeds n_ops";
+    for (uint64_t k = (uint64_t)off[0]; k < (uint64_t)off[n_docs]; k++) {
+        const mt_op_rec &o = ops[k];
+        if (o.kind > MT_OP_LOAD_REMOVED) return "op " + std::to_string(k) + ": unknown kind";
+        if (o.kind == MT_OP_INSERT && !(o.flags & MT_F_MARKER)) {
+            if (o.pos2 < 0 || (uint64_t)o.payload + (uint64_t)o.pos2 > text_len)
+                return "op " + std::to_string(k) + ": insert payload outside the text arena";
+        }
+        if ((o.kind == MT_OP_INSERT || o.kind == MT_OP_ANNOTATE) && !props_rec_ok(props, props_len, o.props))
+            return "op " + std::to_string(k) + ": props record outside the props arena";
+    }
+    return std::string();
+}
 static size_t tier_lds_bytes(bool seg_in_lds, const TierCaps &c, int gen_words) {
     return lds_layout(seg_in_lds, c.S, c.B, c.H, gen_words).total;
 }
@@ -1131,6 +1160,19 @@ int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *
     h->d_seed_off = nullptr;
     h->d_seed = nullptr;
     if (seed_off) {
+        if (seed_off[0] != 0) {
+            h->err = "mt_load_initial_text: seed_off[0] != 0";
+            return MT_E_INVALID;
+        }
+        for (uint32_t d = 0; d < h->n_docs; d++)
+            if (seed_off[d + 1] < seed_off[d]) {
+                h->err = "mt_load_initial_text: seed_off not monotonic";
+                return MT_E_INVALID;
+            }
+        if (seed_off[h->n_docs] > 0 && !seed_text) {
+            h->err = "mt_load_initial_text: null seed_text";
+            return MT_E_INVALID;
+        }
         const size_t n = seed_off[h->n_docs];
         HIPCHK(h, hipMalloc(&h->d_seed_off, (h->n_docs + 1) * sizeof(int64_t)));
         HIPCHK(h, hipMalloc(&h->d_seed, std::max<size_t>(n, 1) * sizeof(uint16_t)));
@@ -1155,7 +1197,18 @@ int mt_reset(mt_handle *h) {
 mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops,
                           uint64_t n_ops, const uint16_t *text, uint64_t text_len,
                           const uint32_t *props, uint64_t props_len) {
-    if (!h || !doc_op_off) return nullptr;
+    if (!h || !doc_op_off || (n_ops && !ops) || (text_len && !text) || (props_len && !props)) {
+        if (h) h->err = "mt_batch_upload: null array";
+        return nullptr;
+    }
+    // the kernels index ops, text and props straight from these values: reject anything
+    // that would read outside the arrays (remote ops are trusted for their semantics, not
+    // for memory safety)
+    std::string bad = validate_batch(h->n_docs, doc_op_off, ops, n_ops, text_len, props, props_len);
+    if (!bad.empty()) {
+        h->err = "mt_batch_upload: " + bad;
+        return nullptr;
+    }
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *b = new mt_batch();
     b->device = h->device;
@@ -1271,8 +1324,10 @@ int mt_last_paged_peaks(mt_handle *h, uint32_t *out) {
 int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, uint64_t n_ops,
                  const uint16_t *text, uint64_t text_len, const uint32_t *props,
                  uint64_t props_len) {
+    if (!h) return MT_E_INVALID;
+    h->err.clear();
     mt_batch *b = mt_batch_upload(h, doc_op_off, ops, n_ops, text, text_len, props, props_len);
-    if (!b) return MT_E_NOMEM;
+    if (!b) return h->err.rfind("mt_batch_upload: device", 0) == 0 ? MT_E_NOMEM : MT_E_INVALID;
     int rc = mt_batch_apply_async(h, b);
     if (rc == 0) rc = mt_sync(h);
     mt_batch_free(b);
@@ -1312,6 +1367,15 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
             h->err = "mt_snapshots_upload: bad document segment ranges";
             return nullptr;
         }
+    for (uint64_t i = 0; i < (uint64_t)doc_seg_off[N]; i++) {
+        const mt_seg_rec &r = segs[i];
+        const bool marker = (r.flags & MT_F_MARKER) != 0;
+        if (r.len < 0 || (!marker && (uint64_t)r.payload + (uint64_t)r.len > text_len) ||
+            !props_rec_ok(props, props_len, r.props)) {
+            h->err = "mt_snapshots_upload: segment record " + std::to_string(i) + " outside the arenas";
+            return nullptr;
+        }
+    }
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *s = new mt_snapshots();
     s->device = h->device;
@@ -1843,9 +1907,32 @@ int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uin
     HIPCHK(h, hipStreamSynchronize(h->stream));
     DocHdr hdr;
     HIPCHK(h, hipMemcpy(&hdr, h->st.hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
-    const uint32_t cnt = std::min<uint32_t>((uint32_t)hdr.dlog_n, cap);
+    // only whole records are ever counted; clamp anyway (never read past this document)
+    const uint32_t have = (uint32_t)std::min<int64_t>(std::max<int32_t>(hdr.dlog_n, 0), h->st.DL);
+    const uint32_t cnt = std::min<uint32_t>(have, cap);
     if (out && cnt) HIPCHK(h, hipMemcpy(out, h->st.dlog + (size_t)doc * h->st.DL, cnt * 4, hipMemcpyDeviceToHost));
-    if (n) *n = (uint32_t)hdr.dlog_n;
+    if (n) *n = have;
+    if (hdr.pad[HDR_DLOG_OVF]) {
+        h->err = "mt_get_delta_log: document " + std::to_string(doc) +
+                 " overflowed its delta log (delta_log_capacity) since the last mt_delta_log_reset";
+        return MT_E_OVERFLOW;
+    }
+    return 0;
+}
+
+__global__ void __launch_bounds__(MT_WAVE) k_dlog_reset(DevState st) {
+    const int doc = blockIdx.x * MT_WAVE + threadIdx.x;
+    if (doc >= st.n_docs) return;
+    st.hdr[doc].dlog_n = 0;
+    st.hdr[doc].pad[HDR_DLOG_OVF] = 0;
+}
+
+int mt_delta_log_reset(mt_handle *h) {
+    if (!h) return MT_E_INVALID;
+    if (!h->st.DL) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipLaunchKernelGGL(k_dlog_reset, dim3((h->n_docs + MT_WAVE - 1) / MT_WAVE), dim3(MT_WAVE), 0, h->stream, h->st);
+    HIPCHK(h, hipGetLastError());
     return 0;
 }
 

@@ -154,6 +154,11 @@ napi_value LoadInitialText(napi_env env, napi_callback_info info) {
         napi_throw_range_error(env, nullptr, "seedOff must hold nDocs + 1 offsets");
         return nullptr;
     }
+    const int64_t *so = (const int64_t *)off;
+    if (so[0] != 0 || so[noff - 1] < 0 || (uint64_t)so[noff - 1] > ntxt) {
+        napi_throw_range_error(env, nullptr, "seedOff exceeds the seed text");
+        return nullptr;
+    }
     const int rc = mt_load_initial_text(hd->h, (const int64_t *)off, (const uint16_t *)txt);
     if (rc) return throw_rc(env, hd, rc, "mt_load_initial_text");
     return nullptr;
@@ -292,7 +297,7 @@ napi_value GetDeltaLog(napi_env env, napi_callback_info info) {
     const uint32_t doc = (uint32_t)get_i32(env, argv[1]);
     uint32_t n = 0;
     int rc = mt_get_delta_log(hd->h, doc, nullptr, 0, &n);
-    if (rc) return throw_rc(env, hd, rc, "mt_get_delta_log");
+    if (rc) return throw_rc(env, hd, rc, "mt_get_delta_log");   // incl. MT_E_OVERFLOW: fail loudly
     void *d;
     napi_value ab, arr;
     NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 4, &d, &ab));
@@ -300,6 +305,17 @@ napi_value GetDeltaLog(napi_env env, napi_callback_info info) {
     if (rc) return throw_rc(env, hd, rc, "mt_get_delta_log");
     NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab, 0, &arr));
     return arr;
+}
+
+// deltaLogReset(h) -- empties every document's delta log (mt_delta_log_reset)
+napi_value DeltaLogReset(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const int rc = mt_delta_log_reset(hd->h);
+    if (rc) return throw_rc(env, hd, rc, "mt_delta_log_reset");
+    return nullptr;
 }
 
 // maintenanceCounts(h) -> Uint32Array [nDocs * 3]: SPLIT, APPEND, UNLINK per document
@@ -358,6 +374,7 @@ napi_value Init(napi_env env, napi_value exports) {
     } fns[] = {{"create", Create},         {"destroy", Destroy},           {"loadInitialText", LoadInitialText},
                {"applyOps", ApplyOps},     {"loadSnapshots", LoadSnapshots},     {"status", Status},             {"getLength", GetLength},
                {"getText", GetText},       {"getPropRuns", GetPropRuns},   {"getDeltaLog", GetDeltaLog},
+               {"deltaLogReset", DeltaLogReset},
                {"maintenanceCounts", MaintenanceCounts},
                {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs}};
     for (auto &f : fns) {

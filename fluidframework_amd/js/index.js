@@ -28,8 +28,13 @@ const DOC_STATUS = {
     2: () => new assert.AssertionError({ message: "Incoming remote op sequence# <= local collabWindow's currentSequence#" }),
     3: () => new assert.AssertionError({ message: "Incoming remote op minSequence# < local collabWindow's minSequence#" }),
     4: () => new Error("merge-tree replay: a per-document capacity was exceeded"),
-    5: () => new Error("merge-tree replay: combiningOp other than rewrite is not supported"),
+    5: () => new Error("merge-tree replay: combiningOp result not modelled"),
     6: () => new Error("merge-tree replay: internal error"),
+    // updateSeqNumbers (client.ts:824-826) and setMinSeq (mergeTree.ts:1755, no message)
+    7: () => new assert.AssertionError({ message: "Incoming op sequence# < local collabWindow's currentSequence#" }),
+    8: () => new assert.AssertionError({ message: "Incoming op sequence# < minSequence#" }),
+    // (Node's message for a bare assert(): what the reference throws on this runtime)
+    9: () => new assert.AssertionError({ message: "false == true" }),
 };
 
 /** JS own-key order: integer-like keys ascending first, then insertion order. */
@@ -128,7 +133,14 @@ class GpuMergeTreeBatch {
             if (st[d] !== 0 && this.failed[d] === 0) { this.failed[d] = st[d]; }
         }
         if (this.wantsDeltas) {
-            for (const v of this.views.values()) { v._emitDeltas(); }
+            // every view drains its records, then the device logs restart empty: a long-lived
+            // batch never runs out of log capacity (a single flush that overflows it throws)
+            try {
+                for (const v of this.views.values()) { v._emitDeltas(); }
+            } finally {
+                native.deltaLogReset(this.h);
+                this.logPos.fill(0);
+            }
         }
     }
 
@@ -261,7 +273,9 @@ class GpuClient {
                     delta.propertyDeltas = {};
                     for (const [k, v] of pd) { delta.propertyDeltas[k] = v === undefined ? null : v; }
                 }
-                if (pos >= 0) { deltaSegments.push(delta); }
+                // a zero-length insert's segment is never linked (blockInsert skips it,
+                // mergeTree.ts:2229) but is still in the callback: position -1
+                deltaSegments.push(delta);
             }
             if (cb) { cb({ sequencedMessage: { sequenceNumber: seq } }, { operation: kind, deltaSegments }); }
         }

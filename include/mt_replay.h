@@ -31,6 +31,7 @@ extern "C" {
 #define MT_E_HIP (-2)        /* HIP runtime error */
 #define MT_E_NOMEM (-3)      /* device allocation failed */
 #define MT_E_NODEVICE (-4)   /* no HIP device visible: the product has no CPU fallback */
+#define MT_E_OVERFLOW (-5)   /* a document's delta log overflowed (mt_get_delta_log) */
 
 typedef struct mt_handle mt_handle;
 typedef struct mt_batch mt_batch;
@@ -177,8 +178,16 @@ int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, 
                  int32_t *hdr_words);
 /* Debug: section timers of a build with -DMT_PROF (MT_E_INVALID otherwise). */
 int mt_debug_prof(mt_handle *h, uint64_t *out /* [32] */, int reset);
-/* Delta log (only with delta_log_capacity > 0), oracle layout. */
+/* Delta log (only with delta_log_capacity > 0), oracle layout: one record per
+   mergeTreeDeltaCallback (MT/mergeTreeDeltaCallback.ts:33-41; call sites MT/mergeTree.ts:
+   2014-2021, 2625-2632, 2738-2745) = [seq, kind, n, (position, cachedLength
+   [, npd, (key, old value) x npd]) x n].  Records are whole: when a record does not fit
+   the remaining capacity it is dropped, the document's log stops and this call returns
+   MT_E_OVERFLOW (after filling out / n with the records that were kept). */
 int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uint32_t *n);
+/* Empties every document's delta log and clears its overflow flag (asynchronous, on the
+   handle's stream): a reader that has consumed the records calls it before the next batch. */
+int mt_delta_log_reset(mt_handle *h);
 
 /* mergeTreeMaintenanceCallback events per document since its creation (only with
    delta_log_capacity > 0, MT_E_INVALID otherwise): out[3*doc + {0,1,2}] = SPLIT

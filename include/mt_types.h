@@ -97,11 +97,14 @@ typedef struct mt_checksum {
 enum mt_doc_status {
     MT_DOC_OK = 0,
     MT_DOC_INSERT_FAILED = 1,   /* "MergeTree insert failed" MT/mergeTree.ts:2243-2249 */
-    MT_DOC_SEQ_ORDER = 2,       /* assert currentSeq < seq     MT/client.ts:462-463 */
-    MT_DOC_MINSEQ_ORDER = 3,    /* assert minSeq <= msn        MT/client.ts:464-465 */
+    MT_DOC_SEQ_ORDER = 2,       /* assert currentSeq < seq     MT/client.ts:462-463 (completeAndLogOp) */
+    MT_DOC_MINSEQ_ORDER = 3,    /* assert minSeq <= msn        MT/client.ts:464-465 (completeAndLogOp) */
     MT_DOC_CAPACITY = 4,        /* a per-document capacity was exceeded */
-    MT_DOC_UNSUPPORTED = 5,     /* combining op other than rewrite */
-    MT_DOC_INTERNAL = 6         /* engine invariant violated (bug) */
+    MT_DOC_UNSUPPORTED = 5,     /* a combining op whose result the engine does not model */
+    MT_DOC_INTERNAL = 6,        /* engine invariant violated (bug) */
+    MT_DOC_SEQ_BACKWARDS = 7,   /* assert currentSeq <= seq    MT/client.ts:824 (updateSeqNumbers) */
+    MT_DOC_MSN_ABOVE_SEQ = 8,   /* assert min <= seq           MT/client.ts:826 (updateSeqNumbers) */
+    MT_DOC_MSN_BACKWARDS = 9    /* assert minSeq <= msn        MT/mergeTree.ts:1755 (setMinSeq) */
 };
 
 #ifdef __cplusplus

@@ -722,10 +722,10 @@ static Seg *segment_from_op(orc_doc *d, const mt_op_rec *op, const uint16_t *tex
 /* updateSeqNumbers / updateMinSeq / setMinSeq  MT/client.ts:821-828, 991-1004;
    MT/mergeTree.ts:1751-1769 */
 static int update_seq_numbers(orc_doc *d, int32_t msn, int32_t seq) {
-    if (!(d->current_seq <= seq)) return MT_DOC_SEQ_ORDER;
+    if (!(d->current_seq <= seq)) return MT_DOC_SEQ_BACKWARDS;   /* client.ts:824 */
     d->current_seq = seq;
-    if (!(msn <= seq)) return MT_DOC_MINSEQ_ORDER;
-    if (!(d->min_seq <= msn)) return MT_DOC_MINSEQ_ORDER;
+    if (!(msn <= seq)) return MT_DOC_MSN_ABOVE_SEQ;              /* client.ts:826 */
+    if (!(d->min_seq <= msn)) return MT_DOC_MSN_BACKWARDS;        /* mergeTree.ts:1755 */
     if (msn > d->min_seq) {
         d->min_seq = msn;
         zamboni(d);

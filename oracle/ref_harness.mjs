@@ -16,6 +16,7 @@
 // Usage:
 //   node oracle/ref_harness.mjs gen  <config.json> <doc_begin> <doc_end> <out.json>
 //   node oracle/ref_harness.mjs replay <logs.json> <out.json>
+//   node oracle/ref_harness.mjs replayerr <logs.json> <out.json>
 //   node oracle/ref_harness.mjs snap <config.json> <doc_begin> <doc_end> <out.json>
 //   node oracle/ref_harness.mjs loadfile <config.json> <out.json> <snapshot.json>...
 //   node oracle/ref_harness.mjs farm <out.json> <maxClients> <minLength>...
@@ -333,6 +334,30 @@ function replayDoc(log) {
     return collectOutputs(c, deltas);
 }
 
+// replayDoc that stops at the first exception (the reference's asserts / throws, e.g.
+// completeAndLogOp MT/client.ts:462-465, updateSeqNumbers :824-826, setMinSeq
+// MT/mergeTree.ts:1752-1755): records the error and the observer's state at the throw.
+function replayErrDoc(log) {
+    const { c, deltas } = makeObserver(log.seed_text);
+    const cseq = {};
+    let error = null;
+    for (let i = 0; i < log.msgs.length; i++) {
+        const [k, t, r, msn, op, type] = log.msgs[i];
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        try {
+            c.applyMsg(msg);
+        } catch (e) {
+            error = { name: e.name, message: e.message, at: i };
+            break;
+        }
+    }
+    const out = collectOutputs(c, deltas);
+    delete out.tree;
+    return { out, error };
+}
+
 // Maintenance events (mergeTreeMaintenanceCallback, MT/mergeTree.ts:1343-1373 scourNode
 // UNLINK/APPEND, :2264-2269 splitLeafSegment SPLIT) counted per document over the same
 // observer replay as replayDoc: [SPLIT, APPEND, UNLINK].
@@ -580,6 +605,9 @@ async function main() {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
+    } else if (mode === "replayerr") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => replayErrDoc(d)) }));
     } else if (mode === "maint") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         fs.writeFileSync(rest[1], JSON.stringify(logs.docs.map((d) => maintDoc(d))));

@@ -7,7 +7,7 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py [--snapshots | --farm]
+    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --only name,name]
 """
 import gzip
 import json
@@ -24,6 +24,10 @@ FIXTURES = {
     "ref_c2": ("c2", {"ops": 2000}, 4),
     "ref_c3": ("c3", {"ops": 2500}, 4),
     "ref_c4": ("c4", {"ops": 3000}, 3),
+    # the configs' full stream lengths (C3 / C4 at 10k messages): thousands of live segments,
+    # deep paged layouts, page splits and repacks late in the stream
+    "ref_c3_full": ("c3", {"ops": 10000}, 4),
+    "ref_c4_full": ("c4", {"ops": 10000}, 2),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),
     "ref_ext": (None, {"ext": True, "seed": 77, "ops": 700, "writers": 5, "lag": 40, "seed_len": 40,
                        "p_insert": 0.5, "p_remove": 0.3, "text_max": 12, "p_newline": 0.08,
@@ -109,6 +113,61 @@ def make_farm_fixture():
     print("ref_farm", len(data["docs"]), "docs", sum(len(d["msgs"]) for d in data["docs"]), "messages")
 
 
+# Error model: generated streams with one fault injected per document, replayed by the
+# reference until its first throw (harness "replayerr"); the fixture holds the error and the
+# observer's state at the throw.  Faults trigger completeAndLogOp (MT/client.ts:462-465),
+# updateSeqNumbers (:824-826) and setMinSeq (MT/mergeTree.ts:1755).
+ERR_CFG = {"ops": 80, "seed_len": 12, "writers": 3, "lag": 6}
+ERR_KINDS = ["seq_dup_op", "msn_back_op", "seq_back_noop", "msn_above_seq", "msn_back_noop", "group_seq_dup"]
+
+
+def _inject(msgs, kind, t0):
+    """msgs: compact [k, seq, ref, msn, op(, type)]; returns the faulted stream (cut after the
+    fault: the reference stops there)."""
+    msgs = [list(m) for m in msgs]
+    k, seq, ref, msn, op = msgs[t0][:5]
+    pseq, pmsn = msgs[t0 - 1][1], msgs[t0 - 1][3]
+    if kind == "seq_dup_op":
+        msgs[t0][1] = pseq
+    elif kind == "msn_back_op":
+        msgs[t0][3] = pmsn - 1
+    elif kind == "seq_back_noop":
+        msgs[t0] = [k, pseq - 1, ref, pmsn, None, "noop"]
+    elif kind == "msn_above_seq":
+        msgs[t0][3] = seq + 1
+    elif kind == "msn_back_noop":
+        msgs[t0] = [k, seq, ref, pmsn - 1, None, "noop"]
+    elif kind == "group_seq_dup":
+        msgs[t0][1] = pseq
+        msgs[t0][4] = {"type": 3, "ops": [op, {"pos1": 0, "seg": "zz", "type": 0}]}
+    return msgs[: t0 + 1]
+
+
+def make_error_fixture():
+    configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
+    cfg = dict(configs["c3"], **ERR_CFG)
+    ndocs = 3 * len(ERR_KINDS)
+    with tempfile.TemporaryDirectory() as td:
+        cp, gp, lp, op = (os.path.join(td, f) for f in ("cfg.json", "gen.json", "logs.json", "out.json"))
+        json.dump(cfg, open(cp, "w"))
+        subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "gen", cp, "0", str(ndocs), gp])
+        gen = json.load(open(gp))
+        docs = []
+        for d in gen["docs"]:
+            i = d["doc"]
+            kind = ERR_KINDS[i % len(ERR_KINDS)]
+            t0 = 30 + 7 * (i // len(ERR_KINDS))
+            docs.append(dict(doc=i, fault=kind, seed_text=d["seed_text"], msgs=_inject(d["msgs"], kind, t0)))
+        json.dump({"docs": docs}, open(lp, "w"))
+        subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "replayerr", lp, op])
+        outs = json.load(open(op))["docs"]
+    for d, o in zip(docs, outs):
+        d["out"], d["error"] = o["out"], o["error"]
+        assert d["error"] is not None, d["fault"]
+    _dump("ref_errors", dict(config=cfg, docs=docs))
+    print("ref_errors", len(docs), "docs", sorted({d["error"]["message"][:40] for d in docs}))
+
+
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
     if "--snapshots" in sys.argv[1:]:
@@ -117,8 +176,16 @@ def main():
     if "--farm" in sys.argv[1:]:
         make_farm_fixture()
         return
+    if "--errors" in sys.argv[1:]:
+        make_error_fixture()
+        return
+    only = None
+    if "--only" in sys.argv[1:]:
+        only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
     for name, (base, over, ndocs) in FIXTURES.items():
+        if only is not None and name not in only:
+            continue
         cfg = dict(configs[base]) if base else {}
         cfg.update(over)
         with tempfile.TemporaryDirectory() as td:
@@ -134,8 +201,11 @@ def main():
         with gzip.open(os.path.join(HERE, name + ".json.gz"), "wt") as fh:
             json.dump(data, fh, separators=(",", ":"))
         print(name, ndocs, "docs")
+    if only is not None:
+        return
     make_snapshot_fixtures()
     make_farm_fixture()
+    make_error_fixture()
 
 
 if __name__ == "__main__":

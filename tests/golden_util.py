@@ -10,11 +10,27 @@ import numpy as np
 from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks
 from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts
 
-MAINT_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm"]
+MAINT_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm", "ref_c3_full",
+                  "ref_c4_full"]
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INT_MIN = -2 ** 31
-ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm"]
+ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm", "ref_c3_full",
+                "ref_c4_full"]
+# the configs' full stream lengths (10k messages per document)
+FULL_FIXTURES = ["ref_c3_full", "ref_c4_full"]
 SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
+# error model (tests/golden/make_golden.py --errors): the reference's throw -> mt_doc_status
+ERROR_STATUS = {
+    "Incoming remote op sequence# <= local collabWindow's currentSequence#": 2,   # MT/client.ts:462-463
+    "Incoming remote op minSequence# < local collabWindow's minSequence#": 3,      # MT/client.ts:464-465
+    "Incoming op sequence# < local collabWindow's currentSequence#": 7,            # MT/client.ts:824
+    "Incoming op sequence# < minSequence#": 8,                                     # MT/client.ts:826
+    "false == true": 9,                                                            # MT/mergeTree.ts:1755
+}
+
+
+def error_status(doc):
+    return ERROR_STATUS[doc["error"]["message"]]
 
 
 def load(name):
@@ -71,10 +87,10 @@ def expected(doc, interner):
                 seg_props=seg_props, deltas=flat)
 
 
-def compare_oracle(o, exp):
+def compare_oracle(o, exp, status=0):
     errs = []
-    if o["status"]:
-        errs.append(f"status {o['status']}")
+    if o["status"] != status:
+        errs.append(f"status {o['status']} != {status}")
     if o["text"] != exp["text"]:
         errs.append("text")
     if o["length"] != exp["length"]:

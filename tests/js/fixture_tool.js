@@ -21,7 +21,7 @@ function msgs(doc) {
 }
 const hex = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("hex");
 
-const [mode, file] = process.argv.slice(2);
+const [mode, file, ...extra] = process.argv.slice(2);
 const fx = load(file);
 if (mode === "encode") {
     const enc = new BatchEncoder(new Interner());
@@ -52,6 +52,38 @@ if (mode === "encode") {
         }
     });
     process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }));
+} else if (mode === "deltas") {
+    // deltas <fixture> <deltaLogCapacity> <flushEvery>: every mergeTreeDeltaCallback the
+    // facade fires while the messages are applied in flushes of <flushEvery> messages per
+    // document (the device log is drained and reset at every flush)
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const cap = parseInt(extra[0], 10), every = parseInt(extra[1], 10);
+    const batch = new GpuMergeTreeBatch(fx.docs.length,
+        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: cap });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const calls = fx.docs.map(() => []);
+    const views = fx.docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        c.mergeTreeDeltaCallback = (opArgs, args) => {
+            calls[i].push([opArgs.sequencedMessage.sequenceNumber, args.operation,
+                args.deltaSegments.map((s) => (s.propertyDeltas !== undefined ? [s.position, s.segment.cachedLength, s.propertyDeltas]
+                    : [s.position, s.segment.cachedLength]))]);
+        };
+        return c;
+    });
+    const all = fx.docs.map((d) => msgs(d));
+    let error = null;
+    try {
+        const longest = Math.max(...all.map((m) => m.length));
+        for (let t = 0; t < longest; t += every) {
+            all.forEach((m, i) => { for (const x of m.slice(t, t + every)) { views[i].applyMsg(x); } });
+            batch.flush();
+        }
+    } catch (e) {
+        error = e.message;
+    }
+    process.stdout.write(JSON.stringify({ calls, error }));
 } else if (mode === "maint") {
     // maint <fixture.json.gz> -> [[split, append, unlink] per doc] through the facade
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 def _gpu_batch(n_docs, **kw):
     from fluidframework_amd import MergeTreeBatch
     kw.setdefault("delta_log_capacity", 1 << 18)
-    kw.setdefault("seg_capacity", 4096)
+    kw.setdefault("seg_capacity", 8192)       # flat tiers: the 10k-op fixtures hold ~4.5k segments
     kw.setdefault("text_capacity", 1 << 17)
     return MergeTreeBatch(n_docs, **kw)
 
@@ -212,3 +212,139 @@ def test_gpu_snapshot_emission_matches_reference(name, tier):
         specs, lengths = record_specs(s["segs"], s["text"], s["props"], interner, names)
         got = encode_chunks(specs, lengths, s["min_seq"], s["cur_seq"], fx["config"]["chunk"])
         assert got == doc["chunks"], (name, doc["doc"])
+
+
+# ---------------------------------------------------------------- error model
+@pytest.mark.parametrize("tier", list(TIERS))
+def test_gpu_error_model_matches_reference(tier):
+    """Faulted streams (tests/golden/ref_errors, made by the reference): each document stops
+    with the status of the reference's throw -- completeAndLogOp (MT/client.ts:462-465),
+    updateSeqNumbers (:824-826), setMinSeq (MT/mergeTree.ts:1755) -- and its state at that
+    point (the op applied, zamboni run, every delta record) equals the reference's at the
+    throw; the other documents of the batch are unaffected."""
+    fx = gu.load("ref_errors")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), **TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner), status=gu.error_status(doc))
+        if errs:
+            bad.append((doc["doc"], doc["fault"], errs))
+    assert not bad, bad[:4]
+
+
+def test_gpu_capacity_status_isolates_the_document():
+    """A document that outgrows a per-document capacity stops with MT_DOC_CAPACITY; the other
+    documents of the batch still equal the reference."""
+    small, big = gu.load("ref_small"), gu.load("ref_c3")
+    interner = gu.interner_for(small)
+    docs = small["docs"][:6] + big["docs"][:2]
+    a = gu.encode_docs(small, interner, docs)
+    mt = _gpu_batch(len(docs), lds_seg_capacity=-1, page_capacity=16, unsettled_capacity=1024)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    st = mt.status()
+    assert st[6:].tolist() == [4, 4]
+    for i, doc in enumerate(docs[:6]):
+        assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
+
+
+# ---------------------------------------------------------------- full-length streams
+def _bench_caps(fx):
+    import bench
+    cfg = dict(fx["config"])
+    return bench.capacities(cfg)
+
+
+@pytest.mark.parametrize("name", gu.FULL_FIXTURES)
+def test_gpu_full_streams_at_bench_capacities(name):
+    """The configs' full stream lengths (10k messages per document, made by the reference)
+    replayed with exactly the capacities bench.py runs (C3: paged LDS capacities 192/220/192,
+    C4: 256/2048/1024): every output and every delta record equals the reference's."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    caps = _bench_caps(fx)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 19, **caps)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, f"{name} at {caps}: {bad}"
+    assert all(mt.is_paged(i) for i in range(len(fx["docs"])))
+    assert mt.maintenance_counts().tolist() == gu.maint_counts(name)
+
+
+# ---------------------------------------------------------------- delta log bounds
+def test_gpu_delta_log_overflow_keeps_whole_records():
+    """A delta log smaller than the stream: the kept records are whole and equal the
+    reference's first records; the read reports the overflow (MT_E_OVERFLOW) instead of
+    handing out a header without its entries; a reset empties it."""
+    from fluidframework_amd import DeltaLogOverflow
+    fx = gu.load("ref_ext")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=301)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    for i, doc in enumerate(fx["docs"]):
+        want = gu.expected(doc, interner)["deltas"]
+        with pytest.raises(DeltaLogOverflow) as ei:
+            mt.get_delta_log(i)
+        kept = ei.value.records
+        assert 0 < len(kept) <= 301 and kept == want[: len(kept)]
+        # the kept words end exactly at a record boundary
+        j = 0
+        while j < len(kept):
+            seq, kind, n = kept[j: j + 3]
+            j += 3
+            for _ in range(n):
+                j += 2
+                if kind == 2:
+                    j += 1 + 2 * kept[j]
+        assert j == len(kept)
+    assert (mt.status() == 0).all()
+    mt.delta_log_reset()
+    mt.sync()
+    assert mt.get_delta_log(0) == []
+
+
+# ---------------------------------------------------------------- C-ABI input validation
+def test_gpu_abi_rejects_out_of_bounds_batches():
+    """Malformed batches fail with MT_E_INVALID on the host instead of faulting the device:
+    non-monotonic or oversized offsets, payloads / props records outside their arenas."""
+    fx = gu.load("ref_small")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]))
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    ins = np.nonzero(a["ops"]["kind"] == 0)[0][0]
+    cases = []
+    off = a["doc_off"].copy()
+    off[3], off[4] = off[4], off[3]
+    cases.append(dict(a, doc_off=off))
+    off = a["doc_off"].copy()
+    off[-1] += 5
+    cases.append(dict(a, doc_off=off))
+    ops = a["ops"].copy()
+    ops[ins]["payload"] = len(a["text"])
+    cases.append(dict(a, ops=ops))
+    ops = a["ops"].copy()
+    ops[ins]["props"] = len(a["props"]) + 7
+    cases.append(dict(a, ops=ops))
+    ops = a["ops"].copy()
+    ops[ins]["kind"] = 9
+    cases.append(dict(a, ops=ops))
+    for c in cases:
+        with pytest.raises(RuntimeError, match=r"\(-1\)"):
+            mt.apply_arrays(c)
+    mt.apply_arrays(a)   # the handle is still usable
+    assert (mt.status() == 0).all()
+    for i, doc in enumerate(fx["docs"]):
+        assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i

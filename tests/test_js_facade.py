@@ -133,3 +133,47 @@ def test_js_facade_loads_snapshots_like_reference(name):
         for p, props in g["props"]:
             exp = next((r[2] for r in runs if r[0] <= p < r[0] + r[1]), None)
             assert props == exp, (p, props, exp)
+
+
+@pytest.mark.gpu
+def test_js_facade_throws_the_reference_errors():
+    """Faulted streams (tests/golden/ref_errors): the facade throws the reference's
+    AssertionError with the reference's message (completeAndLogOp MT/client.ts:462-465,
+    updateSeqNumbers :824-826, setMinSeq MT/mergeTree.ts:1755)."""
+    _addon()
+    fx = gu.load("ref_errors")
+    got = _node("replay", os.path.join(gu.GOLDEN, "ref_errors.json.gz"))
+    for d, g in zip(fx["docs"], got["docs"]):
+        assert g.get("type") == d["error"]["name"] == "AssertionError", (d["fault"], g)
+        assert g["error"] == d["error"]["message"], (d["fault"], g)
+
+
+def _ref_calls(doc):
+    return [[seq, kind, [list(x) for x in segs]] for seq, kind, n, segs in doc["out"]["deltas"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,cap,every", [("ref_ext", 2048, 37), ("ref_c3", 4096, 100), ("ref_c4_full", 1 << 16, 1000)])
+def test_js_facade_delta_callbacks_match_reference_across_flushes(name, cap, every):
+    """mergeTreeDeltaCallback(opArgs, {operation, deltaSegments}) as the facade fires it equals
+    the reference's raw callback stream (MT/mergeTree.ts:2014-2021, 2625-2632, 2738-2745):
+    same records, positions, lengths and propertyDeltas -- with a device log far smaller than
+    the whole stream, drained and reset at every flush."""
+    _addon()
+    fx = gu.load(name)
+    got = _node("deltas", os.path.join(gu.GOLDEN, name + ".json.gz"), str(cap), str(every), timeout=600)
+    assert got["error"] is None, got["error"]
+    total = 0
+    for d, calls in zip(fx["docs"], got["calls"]):
+        want = _ref_calls(d)
+        assert calls == want, (name, d["doc"], next(i for i, (a, b) in enumerate(zip(calls, want)) if a != b))
+        total += sum(3 + sum(2 + (1 + 2 * len(s[2]) if len(s) > 2 else 0) for s in c[2]) for c in want)
+    assert total > cap * len(fx["docs"])   # the stream is longer than the log: it was drained
+
+
+@pytest.mark.gpu
+def test_js_facade_delta_log_overflow_throws():
+    """A single flush larger than the device log fails loudly instead of dropping callbacks."""
+    _addon()
+    got = _node("deltas", os.path.join(gu.GOLDEN, "ref_c3.json.gz"), "512", "100000")
+    assert got["error"] and "overflowed its delta log" in got["error"]

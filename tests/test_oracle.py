@@ -19,6 +19,24 @@ def test_oracle_matches_reference(oracle_lib, name):
         assert not errs, f"{name} doc {doc['doc']}: {errs}"
 
 
+def test_oracle_error_model_matches_reference(oracle_lib):
+    """Faulted streams (tests/golden/ref_errors): the oracle stops with the status of the
+    reference's throw (completeAndLogOp / updateSeqNumbers / setMinSeq asserts) and its state
+    at that point -- op applied, zamboni run -- equals the reference's state at the throw."""
+    fx = gu.load("ref_errors")
+    interner = gu.interner_for(fx)
+    seen = set()
+    for doc in fx["docs"]:
+        a = gu.encode_docs(fx, interner, [doc])
+        od = oracle_lib.OracleDoc.new(a["seed"][: a["seed_off"][1]])
+        od.apply_all(a["ops"], a["text"], a["props"])
+        want = gu.error_status(doc)
+        seen.add(want)
+        errs = gu.compare_oracle(od.outputs(), gu.expected(doc, interner), status=want)
+        assert not errs, f"doc {doc['doc']} ({doc['fault']}): {errs}"
+    assert seen == {2, 3, 7, 8, 9}
+
+
 @pytest.mark.parametrize("name", gu.MAINT_FIXTURES)
 def test_oracle_maintenance_events_match_reference(oracle_lib, name):
     """mergeTreeMaintenanceCallback SPLIT/APPEND/UNLINK counts (MT/mergeTree.ts:2264-2269,
@@ -34,7 +52,7 @@ def test_oracle_maintenance_events_match_reference(oracle_lib, name):
         assert od.maintenance() == want[i], f"{name} doc {doc['doc']}"
 
 
-@pytest.mark.parametrize("name", ["ref_small", "ref_c2", "ref_c3", "ref_c4"])
+@pytest.mark.parametrize("name", ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_c3_full", "ref_c4_full"])
 def test_oracle_generator_reproduces_reference_streams(oracle_lib, name):
     """The generator (shared spec) draws identical op streams whether the view
     lengths come from the reference or from the oracle."""
