@@ -128,7 +128,10 @@ def verify_shards(dist, rank, world, docs, cfg, local, gen_sums, device, per_ran
 
 
 def capacities(cfg, tight=True):
-    """Per-document capacities sized for the workload (DESIGN.md 'HBM layout')."""
+    """Per-document capacities sized for the workload (DESIGN.md 'HBM layout').  The paged
+    capacities (page / unsettled / page heap) size the HBM arrays and the full-capacity paged
+    tier; with `tight`, smaller LDS capacities run first (lds_*: more documents per CU) and
+    the library hands any document that could outgrow them to the full tier by itself."""
     if cfg["writers"] > 8 or cfg["lag"] > 64 or cfg["p_insert_props"] > 0 or cfg["ops"] > 4000:
         # annotate keeps segments apart (property sets differ): ~0.4 live segments per op.
         # Documents outgrow the LDS tier early and continue in the paged layout; the flat
@@ -136,24 +139,22 @@ def capacities(cfg, tight=True):
         segs = max(1024, int(cfg["ops"] * 0.5) + 512)
         deep = cfg["lag"] > 64
         caps = dict(seg_capacity=256, text_capacity=1 << 16, heap_capacity=512, props_capacity=segs + 256,
-                    # high-water marks (mt_last_paged_peaks) at 10k ops: C3 180 pages, 195
-                    # table entries, 159 heap entries (12.5k documents); C4 (minSeq ~1k ops
+                    # high-water marks (mt_last_paged_peaks) at 10k ops: C3 183 pages, 208
+                    # table entries, 173 heap entries (all 100k documents); C4 (minSeq ~1k ops
                     # behind) far more
                     page_capacity=max(64, segs // 20 if not deep else segs // 14),
                     page_heap_capacity=2560 if deep else 512,
                     unsettled_capacity=2560 if deep else 320,
-                    uid_capacity=min(1 << 16, 3 * cfg["ops"] + 1024))
+                    uid_capacity=1 << 16)
         if tight and deep and cfg["ops"] <= 10000 and cfg["writers"] <= 64:
-            # C4 peaks over 1024 documents: 205 pages, 1764 table entries, 785 heap entries;
-            # 99 KB per document at the loose capacities (1 per CU) vs 69 KB here (2 per CU)
-            caps.update(page_capacity=256, unsettled_capacity=2048, page_heap_capacity=1024)
+            # C4 peaks over 4096 documents: 208 pages, 1810 table entries, 841 heap entries;
+            # 99 KB per document at the full capacities (1 per CU) vs 70.6 KB here (2 per CU)
+            caps.update(lds_page_capacity=256, lds_unsettled_capacity=2048, lds_page_heap_capacity=1024)
         if tight and not deep and cfg["ops"] <= 10000:
-            # the paged layout's LDS footprint sets documents per CU: 27 KB at the loose
-            # capacities (6 per CU), 16.0 KB at 208/240/224 (10 per CU), 14.9 KB here (11 per
-            # CU; the kernel is compiled for 3 waves/SIMD): peaks over all 100k C3 documents
-            # are 183 pages, 208 table entries, 173 heap entries.  A document that outgrows
-            # them fails generation and the run falls back to the loose ones
-            caps.update(page_capacity=192, unsettled_capacity=220, page_heap_capacity=192)   # 14.9 KB: 11 per CU
+            # the paged layout's LDS footprint sets documents per CU: 27 KB at the full
+            # capacities (6 per CU), 14.9 KB here (11 per CU; the kernel is compiled for 3
+            # waves/SIMD)
+            caps.update(lds_page_capacity=192, lds_unsettled_capacity=220, lds_page_heap_capacity=192)
         return caps
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
@@ -288,19 +289,11 @@ def main():
         caps["heap_capacity"] = args.heap_cap
     if args.page_caps:
         pp, ut, ph = (int(x) for x in args.page_caps.split(","))
-        caps.update(page_capacity=pp, unsettled_capacity=ut, page_heap_capacity=ph)
+        caps.update(lds_page_capacity=pp, lds_unsettled_capacity=ut, lds_page_heap_capacity=ph)
     t_gen = time.time()
     mt = MergeTreeBatch(docs, device=local_rank, **caps)
-    try:
-        batch = mt.generate(cfg, doc_base)          # untimed: inputs resident in HBM
-    except RuntimeError as e:
-        if "status 4" not in str(e) or args.page_caps or caps == capacities(cfg, tight=False):
-            raise
-        # a document outgrew the tight paged capacities (MT_DOC_CAPACITY): loose ones
-        del mt
-        caps = dict(caps, **{k: v for k, v in capacities(cfg, tight=False).items() if "page" in k or "unsettled" in k})
-        mt = MergeTreeBatch(docs, device=local_rank, **caps)
-        batch = mt.generate(cfg, doc_base)
+    batch = mt.generate(cfg, doc_base)          # untimed: inputs resident in HBM
+    gen_peaks = mt.last_paged_peaks() if "page_capacity" in caps else None
     gen_sums = mt.checksums()
     t_gen = time.time() - t_gen
     seed_off, seed = mt.generated_seeds(cfg, doc_base)
@@ -446,7 +439,10 @@ def main():
             "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
             "docs_replayed_from_hbm": hbm_docs,
             "paged_peaks": peaks,
-            "paged_caps": [caps.get("page_capacity"), caps.get("unsettled_capacity"), caps.get("page_heap_capacity")],
+            "paged_caps": {"lds": [caps.get("lds_page_capacity"), caps.get("lds_unsettled_capacity"),
+                                   caps.get("lds_page_heap_capacity")],
+                           "hbm": [caps.get("page_capacity"), caps.get("unsettled_capacity"),
+                                   caps.get("page_heap_capacity")]},
         },
         "cpu_baseline": cpu,
         "parity": {"replay_equals_generation": replay_consistent, "oracle_sample": parity,

@@ -33,12 +33,14 @@ class MergeTreeBatch:
 
     def __init__(self, n_docs, device=0, seg_capacity=0, block_capacity=0, heap_capacity=0,
                  text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0,
-                 page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0):
+                 page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0,
+                 lds_page_capacity=0, lds_unsettled_capacity=0, lds_page_heap_capacity=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
                                 text_capacity, props_capacity, delta_log_capacity,
                                 lds_seg_capacity, page_capacity, page_heap_capacity,
-                                unsettled_capacity, uid_capacity)
+                                unsettled_capacity, uid_capacity, lds_page_capacity,
+                                lds_unsettled_capacity, lds_page_heap_capacity)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")
@@ -183,9 +185,10 @@ class MergeTreeBatch:
 
     def last_paged_peaks(self):
         """High-water marks of the paged documents of the last batch / generation."""
-        out = np.zeros(4, dtype=np.uint32)
+        out = np.zeros(5, dtype=np.uint32)
         self._check(self.lib.mt_last_paged_peaks(self.h, _native.ptr(out)), "mt_last_paged_peaks")
-        return dict(pages=int(out[0]), unsettled=int(out[1]), heap=int(out[2]), segments=int(out[3]))
+        return dict(pages=int(out[0]), unsettled=int(out[1]), heap=int(out[2]), segments=int(out[3]),
+                    tight_handovers=int(out[4]))
 
     def last_kernel_ms(self):
         return float(self.lib.mt_last_kernel_ms(self.h))

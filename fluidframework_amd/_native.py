@@ -20,7 +20,9 @@ class MtOptions(ctypes.Structure):
                 ("text_capacity", ctypes.c_int32), ("props_capacity", ctypes.c_int32),
                 ("delta_log_capacity", ctypes.c_int32), ("lds_seg_capacity", ctypes.c_int32),
                 ("page_capacity", ctypes.c_int32), ("page_heap_capacity", ctypes.c_int32),
-                ("unsettled_capacity", ctypes.c_int32), ("uid_capacity", ctypes.c_int32)]
+                ("unsettled_capacity", ctypes.c_int32), ("uid_capacity", ctypes.c_int32),
+                ("lds_page_capacity", ctypes.c_int32), ("lds_unsettled_capacity", ctypes.c_int32),
+                ("lds_page_heap_capacity", ctypes.c_int32)]
 
 
 class MtGenCfg(ctypes.Structure):

@@ -53,7 +53,8 @@ template <class T> struct PagedDoc {
     GLB_AS v4i *guA;
     GLB_AS u64 *guO;
     GLB_AS uint16_t *gumap;
-    int PP, PH, UT, UM;
+    int PP, PH, UT, UM;       // LDS capacities of this launch (pages, heap, table); uid map size
+    int PPh;                  // page capacity of the HBM arrays (stride; >= PP)
     int nfree, ut_n;
     int cur;                  // page id staged in the window (-1: none)
     int cur_pos;              // its level-1 position (-1: not known yet)
@@ -62,6 +63,19 @@ template <class T> struct PagedDoc {
                               // window are already mapped to its page
     int vvalid, vr, vc;       // pvl holds the page view lengths of view (vr, vc): boundary
                               // splits keep them (lengths are preserved), any other change drops them
+    int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
+                              // window's entries since they were last rebuilt); the current
+                              // message's bound (pg_room)
+};
+
+// LDS capacities of one paged launch.  The HBM arrays are sized for the handle's paged
+// capacities; a "tight" launch stages documents at smaller LDS capacities (more documents per
+// CU) and hands a document over to the next launch, at full capacities, before a message
+// that could outgrow them (pg_room) -- or at load, when it no longer fits.
+struct PagedCaps {
+    int PP, PH, UT;
+    int tight;   // 1: hand over instead of failing; 0: the HBM capacities (last tier)
+    int stage;   // retry[doc] value this launch serves (1: from the LDS tier, 2: from the tight tier)
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
@@ -196,6 +210,8 @@ TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const 
     pd.cur_pos = -1;
     pd.dirty = 0;
     pd.uid_lo = w.next_uid;
+    // the table holds >= as many entries for this page as it has unsettled segments now
+    pd.wgrow = max(pd.wgrow, pd.opbound);
     wsync<T>();
 }
 
@@ -301,10 +317,14 @@ TD void pg_split_page(PagedDoc<T> &pd) {
     pd.nfree--;
     const int np = uni(pd.freel[pd.nfree]);
     const int pos = pg_cur_pos(pd);
-    // table: the second half's unsettled segments move to the new page (the window's own
-    // entries are rebuilt when it is flushed)
+    // table: the window's entries are rebuilt now (first half under this page, second half
+    // under the new one), so it never holds both a stale and a fresh copy of a segment
+    pg_table_purge(pd, pd.cur);
+    pg_table_add(pd, 0, s0, pd.cur);
+    if (w.status) return;
     pg_table_add(pd, s0, w.n, np);
     if (w.status) return;
+    pd.wgrow = pd.opbound;
     pg_write_page(pd, np, s0, w.n, sp, nbk);
     if (pd.vvalid) {   // the moved half's view length goes with it
         const int i = lane() + s0;
@@ -391,6 +411,7 @@ TD void pg_win_flush_impl(PagedDoc<T> &pd) {
     if (w.status) return;
     pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0));
     pd.dirty = 0;
+    pd.wgrow = pd.opbound;   // exact again, up to the rest of the current message
 }
 
 // Replaces the window by page pg: its loads are issued before the current window is
@@ -674,8 +695,8 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         const v2i top = heap_top(w);
         if (top.x > w.min_seq) break;
         const uint32_t uid = (uint32_t)top.y;
-        if (uid >= (uint32_t)pd.UM) {
-            pg_fail_cap(w, 9);
+        if (uid >= (uint32_t)pd.UM) {   // ids stay below the map size (pg_renumber)
+            FAIL_INTERNAL(w);
             return;
         }
         // the segment's page from the uid map: issued before the heap pop so that its
@@ -686,6 +707,7 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         wsync<T>();
         PG_T1(5)
         PG_T0(4)
+        if (uid == 0) continue;   // its segment was merged or unlinked before a renumbering
         // the window first (its uid map entries are written when it is flushed)
         int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
         if (i < 0) {
@@ -811,6 +833,94 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
     cb_end(w, cb);
 }
 
+// ------------------------------------------------------------------ segment ids
+// Renumbers the document's segment ids densely in document order.  Every split and insert
+// creates an id, so a long-lived document creates far more ids than it ever holds; the
+// uid -> page map (zamboni's only way to find a segment's page) has pd.UM entries, and ids are
+// compacted when they run out.  Zamboni heap entries follow their segments; an entry whose
+// segment is gone (merged or unlinked: the reference skips it, its parent is undefined)
+// gets id 0, which matches nothing.  Runs between messages, from the pages in HBM.
+TD void pg_renumber(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    pg_win_flush(pd);
+    if (w.status) return;
+    pd.cur = -1;
+    pd.cur_pos = -1;
+    pd.vvalid = 0;
+    gsync();
+    const int np = nbr(pd.up, 1);
+    // first new id of every page (pvl as scratch, by page id): segments before it + 1
+    int carry = 1;
+    for (int base = 0; base < np; base += MT_WAVE) {
+        const int q = base + lane();
+        const int pg = q < np ? (int)pd.up.dir[q] : 0;
+        const int ns = q < np ? (int)pd.meta[pg].nseg : 0;
+        const int inc = wave_scan_incl(ns);
+        if (q < np) pd.pvl[pg] = carry + inc - ns;
+        carry += bcast(inc, MT_WAVE - 1);
+    }
+    wsync<T>();
+    // heap entries: old id -> page (map) -> slot -> new id.  Ids at or above the map size
+    // (a document converted from the flat tiers after many creations) are searched for.
+    const int i = lane();
+    for (int e = 1; e <= w.heap_n; e++) {
+        const uint32_t uid = (uint32_t)uni(w.heap[e].y);
+        int nid = 0;
+        if (uid != 0) {
+            const int mp = uid < (uint32_t)pd.UM ? uni((int)pd.gumap[uid]) : -1;
+            for (int q = (mp >= 0 ? -1 : 0); q < (mp >= 0 ? 0 : np); q++) {
+                const int pg = q < 0 ? mp : uni((int)pd.up.dir[q]);
+                if (pg >= pd.PP) continue;
+                const int ns = uni((int)pd.meta[pg].nseg);
+                const bool hit = i < ns && (pd.gB[(size_t)pg * MT_PG_SLOTS + i].z & ~MT_MARKER_BIT) == uid;
+                const u64 m = ballot(hit);
+                if (m) {
+                    nid = uni(pd.pvl[pg]) + first_lane(m);
+                    break;
+                }
+            }
+        }
+        if (lane() == 0) w.heap[e].y = nid;
+    }
+    // every slot gets its new id; the map follows
+    for (int q = 0; q < np; q++) {
+        const int pg = uni((int)pd.up.dir[q]);
+        const int ns = uni((int)pd.meta[pg].nseg);
+        if (i < ns) {
+            GLB_AS v4u *b = pd.gB + (size_t)pg * MT_PG_SLOTS + i;
+            const uint32_t nid = (uint32_t)(uni(pd.pvl[pg]) + i);
+            v4u bv = *b;
+            bv.z = nid | (bv.z & MT_MARKER_BIT);
+            *b = bv;
+            if (nid < (uint32_t)pd.UM) pd.gumap[nid] = (uint16_t)pg;
+        }
+    }
+    w.next_uid = carry;
+    if (w.next_uid + 8 > pd.UM) pg_fail_cap(w, 9);   // more live segments than map entries
+    gsync();
+    wsync<T>();
+}
+
+// Tight paged tier: can this message be applied without outgrowing the launch's LDS
+// capacities?  Bounds per message: the unsettled table grows by <= 3 for an insert (the two
+// halves of a split unsettled segment and the new one) and by <= 2 + (pos2 - pos1) for a
+// range op (two splits and the marked segments: only segments of positive view length are
+// marked); the heap by <= 1 / <= 1 + (pos2 - pos1) (one entry per touched leaf block); a
+// message splits or repacks a few pages (8 kept in reserve).  pd.wgrow bounds what the
+// window added since its table entries were last rebuilt.
+TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
+    const bool range = op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
+    const int span = range ? min(max(op.pos2 - op.pos1, 0), 1 << 20) : 0;
+    const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
+    const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
+    if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
+    if (pd.w.heap_n + hp_b > pd.PH) return false;
+    if (nbr(pd.up, 1) + 8 > pd.PP) return false;
+    pd.opbound = ut_b;
+    pd.wgrow += ut_b;
+    return true;
+}
+
 // Client.applyMsg (MT/client.ts:797-819) for a paged document; mirrors apply_op.
 TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin);
 TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
@@ -847,6 +957,11 @@ TD void pg_load_removed(PagedDoc<T> &pd, const mt_op_rec &op) {
 TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
+    // a message creates <= 3 ids (load_removed finds the id its insert just created)
+    if (w.next_uid + 4 > pd.UM && op.kind != MT_OP_LOAD_REMOVED) {
+        pg_renumber(pd);
+        if (w.status) return;
+    }
     if (op.flags & MT_F_LOAD) {   // summary body append (apply_op)
         if (op.kind == MT_OP_INSERT)
             pg_op_insert(pd, in, tin, pin);
@@ -1017,17 +1132,19 @@ TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
     pd.guA = (GLB_AS v4i *)(st.pgUtA + (size_t)doc * st.UT);
     pd.guO = (GLB_AS u64 *)(st.pgUtO + (size_t)doc * st.UT);
     pd.gumap = (GLB_AS uint16_t *)(st.pgUmap + (size_t)doc * st.UM);
-    pd.PP = st.PP;
-    pd.PH = st.PH;
-    pd.UT = st.UT;
+    pd.PPh = st.PP;
     pd.UM = st.UM;
 }
 
 // Window + upper DocT instances over the LDS layout; scalars from the document header.
-TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *smem, const PagedLayout &L) {
+TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *smem, const PagedLayout &L,
+              const PagedCaps &pc) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     pg_bases(pd, st, doc);
+    pd.PP = pc.PP;
+    pd.PH = pc.PH;
+    pd.UT = pc.UT;
     w.hp = st.hdr + doc;
     w.text = (GLB_AS uint16_t *)(st.text + doc * (size_t)2 * st.T);
     w.props = (GLB_AS uint32_t *)(st.props + doc * (size_t)2 * st.P * MT_PREC);
@@ -1037,7 +1154,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.DL_cap = st.DL;
     w.S_cap = MT_PG_SLOTS;
     w.B_cap = PW_B;
-    w.H_cap = st.PH;
+    w.H_cap = pc.PH;
     w.A = (typename T::A_t)(smem + L.offWA);
     w.Bv = (typename T::B_t)(smem + L.offWB);
     w.O = (typename T::O_t)(smem + L.offWO);
@@ -1083,7 +1200,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     up.cnt = smem + L.offUcnt;
     up.nb = (LDS_AS int32_t *)(smem + L.offUnb);
     up.dir = (LDS_AS uint16_t *)(smem + L.offDir);
-    up.B_cap = st.PP;
+    up.B_cap = pc.PP;
     up.status = 0;
     pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
     pd.pvl = (LDS_AS int *)(smem + L.offPvl);
@@ -1095,6 +1212,8 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.cur_pos = -1;
     pd.dirty = 0;
     pd.vvalid = 0;
+    pd.wgrow = 0;
+    pd.opbound = 0;
 }
 
 // Builds the free-page list from the directory (pvl as scratch marks).
@@ -1126,14 +1245,19 @@ TD void pg_build_free(PagedDoc<T> &pd) {
     wsync<T>();
 }
 
-// Loads a paged document's directory, meta, upper counts, heap and table into LDS.
-TD void pg_load(PagedDoc<T> &pd) {
+// Loads a paged document's directory, meta, upper counts, heap and table into LDS.  Returns
+// false (nothing staged) when the document does not fit this launch's LDS capacities.
+TD bool pg_load(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     const DocHdr h = *w.hp;
+    const int np = h.n_blk[1];
+    if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
+    int mx = 0;
+    for (int q = lane(); q < np; q += MT_WAVE) mx = max(mx, (int)pd.gdir[q]);
+    if (wave_max(mx) >= pd.PP) return false;   // a page id allocated by a wider launch
     if (lane() < MT_LV) up.nb[lane()] = w.hp->n_blk[lane()];
     wsync<T>();
-    const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = pd.gdir[q];
     {
         GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)pd.gmeta;
@@ -1142,7 +1266,7 @@ TD void pg_load(PagedDoc<T> &pd) {
     }
     for (int l = 1; l < up.depth; l++) {
         const int nl = nbr(up, l);
-        for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = pd.gcnt[l * pd.PP + b];
+        for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = pd.gcnt[l * pd.PPh + b];
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = pd.gheap[i];
     pd.ut_n = h.pad[HDR_UTN];
@@ -1153,12 +1277,18 @@ TD void pg_load(PagedDoc<T> &pd) {
     }
     wsync<T>();
     pg_build_free(pd);
+    return true;
 }
 
 TD void pg_store(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
+    // a document that failed keeps the state it had at the failure (the reference's state at
+    // its throw): the window is written back regardless of the status
+    const int failed = w.status;
+    w.status = 0;
     pg_win_flush(pd);
+    if (failed) w.status = failed;
     wsync<T>();
     const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) pd.gdir[q] = up.dir[q];
@@ -1169,7 +1299,7 @@ TD void pg_store(PagedDoc<T> &pd) {
     }
     for (int l = 1; l < up.depth; l++) {
         const int nl = nbr(up, l);
-        for (int b = lane(); b < nl; b += MT_WAVE) pd.gcnt[l * pd.PP + b] = lvl(up, l)[b];
+        for (int b = lane(); b < nl; b += MT_WAVE) pd.gcnt[l * pd.PPh + b] = lvl(up, l)[b];
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) pd.gheap[i] = w.heap[i];
     for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
@@ -1233,7 +1363,7 @@ TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
     const int depth = h.depth;
     const int np = depth == 1 ? 1 : h.n_blk[1];
     if (np + 8 > pd.PP || h.heap_n > pd.PH) {
-        pg_fail_cap(w, 7);
+        pg_fail_cap(w, np + 8 > pd.PP ? 7 : 3);
         return false;
     }
     up.depth = depth;
@@ -1284,5 +1414,8 @@ TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
     }
     pg_build_free(pd);
     pd.cur = -1;
-    return true;
+    pd.wgrow = pd.opbound = 0;
+    // the flat tiers number ids without bound: compact them for the uid -> page map
+    if (w.next_uid + 4 > pd.UM) pg_renumber(pd);
+    return w.status == 0;
 }

@@ -542,31 +542,53 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 #else
 #define MT_PAGED_WPE
 #endif
+// A tight launch (pc.tight) hands a document to the next launch -- retry[doc] = 2 from
+// message resume[doc] -- when it does not fit its LDS capacities at load, or before a message
+// that could outgrow them (pg_room); stats[12] counts those hand-overs.
+template <class T>
+__device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t k) {
+    if (lane() == 0) {
+        st.retry[doc] = 2;
+        st.resume[doc] = k;
+        atomicAdd(st.stats + 12, 1u);
+    }
+}
 template <class T>
 __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState st, const mt_op_rec *ops,
                                                           const int64_t *off, const uint16_t *tin,
-                                                          const uint32_t *pin, int use_resume) {
+                                                          const uint32_t *pin, int use_resume, PagedCaps pc) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
-    if (!st.retry[doc]) return;
+    if (st.retry[doc] != pc.stage) return;
     if (lane() == 0) atomicAdd(st.stats, 1u);
-    const PagedLayout L = paged_layout(st.PP, st.PH, st.UT, 0);
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0);
     const int64_t k1 = off[doc + 1];
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
     PagedDoc<T> pd;
-    pg_setup(pd, st, doc, smem, L);
+    pg_setup(pd, st, doc, smem, L, pc);
     DocT<T> &w = pd.w;
     if (w.status) {
         if (lane() == 0) st.retry[doc] = 0;
         return;
     }
     if (st.hdr[doc].pad[HDR_PAGED]) {
-        pg_load(pd);
+        if (!pg_load(pd)) {
+            if (pc.tight) {
+                pg_handover<T>(st, doc, k0);
+            } else if (lane() == 0) {   // cannot happen: the last tier has the HBM capacities
+                st.hdr[doc].status = MT_DOC_CAPACITY;
+                st.retry[doc] = 0;
+            }
+            return;
+        }
     } else if (!pg_convert(pd, st, doc)) {
-        // stays flat: only the status changes
-        if (lane() == 0) {
+        // stays flat (the pages written so far are unreferenced): the next tier converts it
+        // again, or only the status changes
+        if (pc.tight && w.status == MT_DOC_CAPACITY) {
+            pg_handover<T>(st, doc, k0);
+        } else if (lane() == 0) {
             st.hdr[doc].status = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
             st.retry[doc] = 0;
         }
@@ -576,7 +598,8 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
     int pk_ut = 0, pk_heap = 0;
-    for (int64_t kb = k0; kb < k1 && w.status == 0; kb += MT_WAVE) {
+    int64_t spill_at = -1;
+    for (int64_t kb = k0; kb < k1 && w.status == 0 && spill_at < 0; kb += MT_WAVE) {
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
         uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
@@ -621,6 +644,10 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
             in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
+            if (pc.tight && !pg_room(pd, in.op)) {
+                spill_at = kb + j;
+                break;
+            }
             pg_apply_op(pd, in, gt, gp);
             pk_ut = max(pk_ut, pd.ut_n);
             pk_heap = max(pk_heap, w.heap_n);
@@ -630,7 +657,10 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
     pg_store(pd);
     pg_peaks(st, pd, pk_ut, pk_heap);
-    if (lane() == 0) st.retry[doc] = 0;
+    if (spill_at >= 0 && w.status == 0)
+        pg_handover<T>(st, doc, spill_at);
+    else if (lane() == 0)
+        st.retry[doc] = 0;
 #ifdef MT_PROF
     if (lane() < 32) atomicAdd(&g_prof[lane()], w.prof[lane()]);
 #endif
@@ -638,27 +668,34 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
 
 // Generator for documents that outgrew the LDS tier: regenerated from the start in the
 // paged layout (the draws are identical, so the op stream is the same).
+// A tight launch hands a document that could outgrow its LDS capacities to the next launch,
+// which regenerates it from the start (the draws are identical).
 template <class T>
 __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_cfg cfg, uint32_t doc_base,
                                                             mt_op_rec *ops_out, uint16_t *text_out,
                                                             uint32_t *props_out, int64_t tstride,
                                                             int64_t pstride, int32_t *fail_out,
-                                                            int32_t *dbg_len) {
+                                                            int32_t *dbg_len, PagedCaps pc) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
-    if (!st.retry[doc]) return;
-    const PagedLayout L = paged_layout(st.PP, st.PH, st.UT, 2 * (cfg.writers + 1));
+    if (st.retry[doc] != pc.stage) return;
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 2 * (cfg.writers + 1));
     GenCtx g;
     gen_begin(g, st, cfg, (int)(doc_base + doc), doc, smem + L.offGen, tstride, pstride);
     PagedDoc<T> pd;
-    pg_setup(pd, st, doc, smem, L);
+    pg_setup(pd, st, doc, smem, L, pc);
     DocT<T> &w = pd.w;
     if (w.status || !pg_convert(pd, st, doc)) {
         if (lane() == 0) {
-            fail_out[doc] = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
-            st.retry[doc] = 0;
+            if (pc.tight && w.status == MT_DOC_CAPACITY) {
+                st.retry[doc] = 2;
+                atomicAdd(st.stats + 12, 1u);
+            } else {
+                fail_out[doc] = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
+                st.retry[doc] = 0;
+            }
         }
         return;
     }
@@ -678,6 +715,13 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         }
         OpIn in;
         gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
+        if (pc.tight && !pg_room(pd, in.op)) {
+            if (lane() == 0) {
+                st.retry[doc] = 2;
+                atomicAdd(st.stats + 12, 1u);
+            }
+            return;
+        }
         pg_apply_op(pd, in, gt, gp);
         pk_ut = max(pk_ut, pd.ut_n);
         pk_heap = max(pk_heap, w.heap_n);
@@ -974,6 +1018,8 @@ struct mt_handle {
     int64_t *d_seed_off = nullptr;   // initial contents kept on device for mt_reset
     uint16_t *d_seed = nullptr;
     TierCaps lds{0, 0, 0, 0};        // LDS-tier capacities (S == 0: tier disabled)
+    PagedCaps pg_tight{0, 0, 0, 1, 1};   // tight paged tier (PP == 0: off)
+    PagedCaps pg_full{0, 0, 0, 0, 1};    // paged tier at the HBM capacities
 };
 struct mt_batch {
     int device = 0;
@@ -1068,6 +1114,15 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         st.PH = o.page_heap_capacity > 0 ? o.page_heap_capacity : 1024;
         st.UT = o.unsettled_capacity > 0 ? o.unsettled_capacity : 256;
         st.UM = std::min(o.uid_capacity > 0 ? o.uid_capacity : 65536, 1 << 24);
+        st.UM = std::max(st.UM, 256);
+        h->pg_full = PagedCaps{st.PP, st.PH, st.UT, 0, 1};
+        const PagedCaps t{o.lds_page_capacity > 0 ? std::min(o.lds_page_capacity, st.PP) : st.PP,
+                          o.lds_page_heap_capacity > 0 ? std::min(o.lds_page_heap_capacity, st.PH) : st.PH,
+                          o.lds_unsettled_capacity > 0 ? std::min(o.lds_unsettled_capacity, st.UT) : st.UT, 1, 1};
+        if (t.PP < st.PP || t.PH < st.PH || t.UT < st.UT) {
+            h->pg_tight = t;
+            h->pg_full.stage = 2;
+        }
         // one document's paged state staged in LDS: up to the CU's 160 KiB (fewer
         // documents per CU above 64 KiB)
         const size_t lb = paged_layout(st.PP, st.PH, st.UT, 2 * 65).total;
@@ -1257,15 +1312,22 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream));
     }
     if (h->st.PP > 0) {
-        // documents that outgrew the LDS tier continue in the paged layout
-        const size_t lb = paged_layout(h->st.PP, h->st.PH, h->st.UT, 0).total;
+        // documents that outgrew the LDS tier continue in the paged layout: the tight tier
+        // first (when configured), then the full capacities for the documents it handed over
         const int use_resume = h->lds.S > 0 ? 1 : 0;
-        if (h->st.DL)
-            hipLaunchKernelGGL(k_replay_paged<TierPagedT<true>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
-                               b->ops, b->off, b->text, b->props, use_resume);
-        else
-            hipLaunchKernelGGL(k_replay_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
-                               b->ops, b->off, b->text, b->props, use_resume);
+        const PagedCaps *tiers[2] = {h->pg_tight.PP ? &h->pg_tight : nullptr, &h->pg_full};
+        for (const PagedCaps *pc : tiers) {
+            if (!pc) continue;
+            const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, 0).total;
+            const int res = pc->stage == 2 ? 1 : use_resume;
+            if (h->st.DL)
+                hipLaunchKernelGGL(k_replay_paged<TierPagedT<true>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                                   b->ops, b->off, b->text, b->props, res, *pc);
+            else
+                hipLaunchKernelGGL(k_replay_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
+                                   h->st, b->ops, b->off, b->text, b->props, res, *pc);
+            HIPCHK(h, hipGetLastError());
+        }
     } else if (h->st.DL)
         hipLaunchKernelGGL((k_replay<TierGlbT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
@@ -1317,7 +1379,7 @@ int mt_last_paged_peaks(mt_handle *h, uint32_t *out) {
     if (!h || !out) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(out, h->st.stats + 8, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(out, h->st.stats + 8, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -1590,11 +1652,16 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
             ok = hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream) == hipSuccess;
         }
         if (ok && h->st.PP > 0) {
-            const size_t lb = paged_layout(h->st.PP, h->st.PH, h->st.UT, gw).total;
-            hipLaunchKernelGGL(k_generate_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
-                               h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride, pstride, d_fail,
-                               d_trace);
-            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+            const PagedCaps *tiers[2] = {h->pg_tight.PP ? &h->pg_tight : nullptr, &h->pg_full};
+            for (const PagedCaps *pc : tiers) {
+                if (!pc || !ok) continue;
+                const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, gw).total;
+                hipLaunchKernelGGL(k_generate_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
+                                   h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride, pstride, d_fail,
+                                   d_trace, *pc);
+                ok = hipGetLastError() == hipSuccess;
+            }
+            ok = ok && hipStreamSynchronize(h->stream) == hipSuccess;
         } else if (ok) {
             hipLaunchKernelGGL(k_generate<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(false, glb_caps(h), gw), h->stream, h->st, *cfg, doc_index_base,

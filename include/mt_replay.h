@@ -56,7 +56,16 @@ typedef struct mt_options {
     int32_t page_heap_capacity; /* zamboni heap entries of a paged document (default 1024) */
     int32_t unsettled_capacity; /* segments of a paged document inserted or removed above
                                    minSeq (default 256) */
-    int32_t uid_capacity;       /* segment ids of a paged document (default 65536) */
+    int32_t uid_capacity;       /* entries of a paged document's segment-id -> page map
+                                   (default 65536): ids are renumbered when they run out, so
+                                   this bounds the live segments, not the segments created */
+    /* Tight paged tier (0 = off): LDS capacities below the three above.  Documents are
+       replayed at these first (a smaller LDS footprint: more documents per CU); one that
+       does not fit, or whose next message could outgrow them, continues -- from that
+       message -- in a second launch at the full capacities. */
+    int32_t lds_page_capacity;
+    int32_t lds_unsettled_capacity;
+    int32_t lds_page_heap_capacity;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the
@@ -137,8 +146,8 @@ float mt_last_kernel_ms(const mt_handle *h);
    records, at load} (the causes count LDS capacities hit inside a message). */
 int mt_last_hbm_docs(mt_handle *h, uint32_t *out);
 /* High-water marks of the paged documents of the most recent batch (or generation):
-   out[4] = {pages, unsettled-table entries, zamboni heap entries, segments}; sizing aid for
-   page_capacity / unsettled_capacity / page_heap_capacity. */
+   out[5] = {pages, unsettled-table entries, zamboni heap entries, segments, documents handed
+   from the tight to the full-capacity paged tier}; sizing aid for the paged capacities. */
 int mt_last_paged_peaks(mt_handle *h, uint32_t *out);
 
 /* Generates ops_per_doc synthetic messages per document on the device, applying them as

@@ -28,6 +28,8 @@ FIXTURES = {
     # deep paged layouts, page splits and repacks late in the stream
     "ref_c3_full": ("c3", {"ops": 10000}, 4),
     "ref_c4_full": ("c4", {"ops": 10000}, 2),
+    # a long-lived document: 30k messages (~45k segment ids created, ~12k live segments)
+    "ref_c3_long": ("c3", {"ops": 30000}, 2),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),
     "ref_ext": (None, {"ext": True, "seed": 77, "ops": 700, "writers": 5, "lag": 40, "seed_len": 40,
                        "p_insert": 0.5, "p_remove": 0.3, "text_max": 12, "p_newline": 0.08,

@@ -18,6 +18,8 @@ ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_l
                 "ref_c4_full"]
 # the configs' full stream lengths (10k messages per document)
 FULL_FIXTURES = ["ref_c3_full", "ref_c4_full"]
+# long-lived documents (30k messages)
+LONG_FIXTURES = ["ref_c3_long"]
 SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
 # error model (tests/golden/make_golden.py --errors): the reference's throw -> mt_doc_status
 ERROR_STATUS = {

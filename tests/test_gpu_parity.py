@@ -34,6 +34,10 @@ TIERS = {
     "tiny": dict(lds_seg_capacity=16),
     "paged": dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=1024),
     "tiny_paged": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024),
+    # a tight paged tier far below the documents' needs: documents are handed to the
+    # full-capacity paged launch mid-batch (and at load), generators regenerate there
+    "tight": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024, page_heap_capacity=1024,
+                  lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40),
 }
 
 
@@ -55,7 +59,7 @@ def test_gpu_matches_reference(name, tier):
     paged = [mt.is_paged(i) for i in range(len(fx["docs"]))]
     if tier == "paged":
         assert all(paged)
-    elif "paged" not in tier:
+    elif "paged" not in tier and tier != "tight":
         assert not any(paged)
 
 
@@ -118,7 +122,7 @@ def test_gpu_maintenance_events_match_reference(name, tier):
     assert got == gu.maint_counts(name), name
 
 
-@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged"])
+@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged", "tight"])
 @pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6), ("c3", 3000, 4)])
 def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     import json
@@ -346,5 +350,39 @@ def test_gpu_abi_rejects_out_of_bounds_batches():
             mt.apply_arrays(c)
     mt.apply_arrays(a)   # the handle is still usable
     assert (mt.status() == 0).all()
+    for i, doc in enumerate(fx["docs"]):
+        assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
+
+
+# ---------------------------------------------------------------- drop-in ceilings
+def test_gpu_tight_tier_hands_documents_over():
+    """LDS capacities of the tight paged tier far below the documents' peaks: the library
+    moves each document to the full-capacity launch before the message that could outgrow
+    them (no generation fallback in the caller); every output equals the reference's."""
+    fx = gu.load("ref_c3_full")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    caps = dict(_bench_caps(fx), lds_page_capacity=40, lds_unsettled_capacity=64, lds_page_heap_capacity=64)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 19, **caps)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert mt.last_paged_peaks()["tight_handovers"] == len(fx["docs"])
+    for i, doc in enumerate(fx["docs"]):
+        assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
+
+
+@pytest.mark.parametrize("uid_capacity", [65536, 16384])
+def test_gpu_long_documents_match_reference(uid_capacity):
+    """30k-message documents (~45k segment ids created, ~10.5k live segments at the end):
+    segment ids are renumbered when the uid -> page map runs out (uid_capacity 16384 forces
+    it several times), and every output still equals the reference's."""
+    import bench
+    fx = gu.load("ref_c3_long")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    caps = dict(bench.capacities(dict(fx["config"])), uid_capacity=uid_capacity, text_capacity=1 << 17)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 20, **caps)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
     for i, doc in enumerate(fx["docs"]):
         assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
