@@ -154,7 +154,8 @@ def capacities(cfg, tight=True):
             # the paged layout's LDS footprint sets documents per CU: 27 KB at the full
             # capacities (6 per CU), 14.9 KB here (11 per CU; the kernel is compiled for 3
             # waves/SIMD)
-            caps.update(lds_page_capacity=192, lds_unsettled_capacity=220, lds_page_heap_capacity=192)
+            caps.update(lds_page_capacity=192, lds_unsettled_capacity=220, lds_page_heap_capacity=192,
+                        lds_narrow_overlap=1 if cfg["writers"] <= 32 else 0)
         return caps
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 

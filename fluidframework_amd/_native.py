@@ -11,7 +11,9 @@ from .wire import CHECKSUM_DTYPE, OP_DTYPE
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 MT_E_INVALID, MT_E_HIP, MT_E_NOMEM, MT_E_NODEVICE, MT_E_OVERFLOW = -1, -2, -3, -4, -5
-LIB_PATH = os.path.join(HERE, "libmtreplay.so")
+# MT_LIB_PATH: an instrumented build of the same sources (e.g. the -DMT_PROF section timers,
+# tools/debug_prof.py); the product library otherwise
+LIB_PATH = os.environ.get("MT_LIB_PATH") or os.path.join(HERE, "libmtreplay.so")
 
 
 class MtOptions(ctypes.Structure):
@@ -22,7 +24,7 @@ class MtOptions(ctypes.Structure):
                 ("page_capacity", ctypes.c_int32), ("page_heap_capacity", ctypes.c_int32),
                 ("unsettled_capacity", ctypes.c_int32), ("uid_capacity", ctypes.c_int32),
                 ("lds_page_capacity", ctypes.c_int32), ("lds_unsettled_capacity", ctypes.c_int32),
-                ("lds_page_heap_capacity", ctypes.c_int32)]
+                ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32)]
 
 
 class MtGenCfg(ctypes.Structure):

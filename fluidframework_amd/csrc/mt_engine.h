@@ -15,6 +15,8 @@
 // CPU restatement this engine is tested against.  Reference paths below are relative to
 // /root/reference/packages/dds/merge-tree/src/ ("MT/").
 #pragma once
+#include <type_traits>
+
 #include "mt_device.h"
 
 #define LDS_AS __attribute__((address_space(3)))
@@ -48,15 +50,18 @@ template <bool kLogT> struct TierGlbT {
 };
 
 // The paged layout (mt_paged.h): LDS-staged window and upper levels.  kPaged compiles the
-// page bookkeeping in; the flat tiers carry none of it.
-template <bool kLogT> struct TierPagedT {
+// page bookkeeping in; the flat tiers carry none of it.  kNarrow: removedClientOverlap masks
+// of short ids 1..32 in LDS (window and unsettled table: 4 bytes per segment instead of 8) --
+// a tight tier for documents with few writers; one whose clients above 32 remove overlapping
+// ranges continues in the full tier.
+template <bool kLogT, bool kNarrowT = false> struct TierPagedT {
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;
-    static constexpr int kOvlBits = 64;
-    typedef u64 O_v;
+    static constexpr int kOvlBits = kNarrowT ? 32 : 64;
+    typedef typename std::conditional<kNarrowT, uint32_t, u64>::type O_v;
     typedef LDS_AS v4i *A_t;
-    typedef LDS_AS u64 *O_t;
+    typedef LDS_AS O_v *O_t;
     typedef LDS_AS v4u *B_t;
     typedef LDS_AS v2i *H_t;
 };
@@ -113,6 +118,7 @@ template <class T> struct DocT {
     u64 dhash;
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
+    int wide;               // an overlap mask holds a short id above 32 (DocHdr.pad0 bit 0)
     // paged documents (mt_paged.h): this DocT is a window onto one page, or the instance
     // holding the levels >= 1 of the tree (dir != nullptr); all zero for flat documents
     int paged;              // 1: window onto one page
@@ -240,10 +246,12 @@ TD void fail_cap(DocT<T> &d, int cause) {
 }
 
 // paged instances (window: levels 0-1; upper levels: 1.. with level 1 = pages): B entries
-// for levels 0 and 1, B/2 for level 2, B/4 above (growth is checked against bcap)
-static __host__ __device__ inline int pcnt_cap(int B, int l) { return l <= 1 ? B : (l == 2 ? B / 2 : B / 4); }
+// for levels 0 and 1, B/2 for level 2, B/8 above -- a node holds >= 4 children after a split
+// or a repack, so level l + 1 has about a quarter of level l (growth is checked against bcap)
+static __host__ __device__ inline int pcnt_cap3(int B) { return B / 8 > 2 ? B / 8 : 2; }
+static __host__ __device__ inline int pcnt_cap(int B, int l) { return l <= 1 ? B : (l == 2 ? B / 2 : pcnt_cap3(B)); }
 static __host__ __device__ inline int pcnt_off(int B, int l) {
-    return l <= 1 ? l * B : (l == 2 ? 2 * B : 2 * B + B / 2 + (l - 3) * (B / 4));
+    return l <= 1 ? l * B : (l == 2 ? 2 * B : 2 * B + B / 2 + (l - 3) * pcnt_cap3(B));
 }
 static __host__ __device__ inline int pcnt_bytes(int B) { return pcnt_off(B, MT_LV); }
 TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) {
@@ -310,6 +318,7 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.status = h.status;
     d.dlog_n = h.dlog_n;
     d.dhash = h.delta_hash;
+    d.wide = h.pad0 & 1;
     if (T::kLog) {
         d.m_split = h.pad[HDR_MSPLIT];
         d.m_append = h.pad[HDR_MAPPEND];
@@ -431,7 +440,7 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
         for (int l = 0; l < MT_LV; l++) h.n_blk[l] = nbl[l];
         h.delta_hash = d.dhash;
         h.n_ops = d.hp->n_ops;
-        h.pad0 = 0;
+        h.pad0 = d.wide;
 #pragma unroll
         for (int i = 0; i < 8; i++) h.pad[i] = 0;
         if (T::kLog) {
@@ -1927,6 +1936,7 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
             fail_cap(d, 1);
             return true;
         }
+        if (rem && c > 32 && ballot(sel && a.z != MT_RSEQ_NONE && !newly)) d.wide = 1;
         if (!rem) d.props_top += __popcll(sel_m);
         wsync<T>();
         // fold the callback records in document order

@@ -38,10 +38,9 @@ template <class T> struct PagedDoc {
     DocT<T> up;   // levels >= 1 of the tree (level 1 = pages, counted in leaf blocks)
     LDS_AS PageMeta *meta;    // [PP] by page id
     LDS_AS int *pvl;          // [PP] by page id: view length of the current view
-    LDS_AS uint16_t *freel;   // [PP] free page ids
     LDS_AS uint16_t *upage;   // [UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
     LDS_AS v4i *uA;
-    LDS_AS u64 *uO;
+    LDS_AS typename T::O_v *uO;
     GLB_AS v4i *gA;           // this document's pages (slot 0 of page 0)
     GLB_AS u64 *gO;
     GLB_AS v4u *gB;
@@ -55,7 +54,7 @@ template <class T> struct PagedDoc {
     GLB_AS uint16_t *gumap;
     int PP, PH, UT, UM;       // LDS capacities of this launch (pages, heap, table); uid map size
     int PPh;                  // page capacity of the HBM arrays (stride; >= PP)
-    int nfree, ut_n;
+    int ut_n;
     int cur;                  // page id staged in the window (-1: none)
     int cur_pos;              // its level-1 position (-1: not known yet)
     int dirty;                // the window differs from the page in HBM (slots, uid map, table)
@@ -76,23 +75,25 @@ struct PagedCaps {
     int PP, PH, UT;
     int tight;   // 1: hand over instead of failing; 0: the HBM capacities (last tier)
     int stage;   // retry[doc] value this launch serves (1: from the LDS tier, 2: from the tight tier)
+    int narrow;  // TierPagedT<., true>: 32-bit overlap masks in LDS (tight tier only)
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
 
 struct PagedLayout {
     uint32_t offWA, offWB, offWO, offWcnt, offWflg, offWends, offWscr, offWnb;
-    uint32_t offUcnt, offUnb, offDir, offMeta, offPvl, offFree, offHeap, offUpage, offUA, offUO, offGen, offProf,
+    uint32_t offUcnt, offUnb, offDir, offMeta, offPvl, offHeap, offUpage, offUA, offUO, offGen, offProf,
         total;
 };
-static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words) {
+// ob: bytes per overlap mask in LDS (8, or 4 for a narrow tier)
+static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words, int ob) {
     PagedLayout L;
     uint32_t o = 0;
     L.offWA = o; o += 16u * MT_PG_SLOTS;
     L.offWB = o; o += 16u * MT_PG_SLOTS;
-    L.offWO = o; o += 8u * MT_PG_SLOTS;
+    L.offWO = o; o += (uint32_t)ob * MT_PG_SLOTS;
     L.offUA = o; o += 16u * UT;
-    L.offUO = o; o += 8u * UT;
+    L.offUO = o; o += (((uint32_t)ob * UT) + 7u) & ~7u;
     L.offHeap = o; o += 8u * (PH + 1);
     L.offMeta = o; o += (uint32_t)sizeof(PageMeta) * PP;
     L.offUpage = o; o += (2u * UT + 3u) & ~3u;
@@ -102,11 +103,10 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     L.offUnb = o; o += MT_LV * 4;
     L.offGen = o; o += 4u * gen_words;
     L.offDir = o; o += 2u * PP;
-    L.offFree = o; o += 2u * PP;
     L.offWends = o; o += 2u * PW_B;
     L.offWcnt = o; o += (uint32_t)MT_LV * PW_B;
     L.offWflg = o; o += PW_B;
-    L.offUcnt = o; o += (uint32_t)pcnt_bytes(PP);
+    L.offUcnt = o; o += (uint32_t)(pcnt_bytes(PP) - PP);   // levels >= 1 (level 0 is the window's)
 #ifdef MT_PROF
     o = (o + 7u) & ~7u;
     L.offProf = o; o += 32u * 8;
@@ -143,6 +143,23 @@ TD void pm_set_blocks(PagedDoc<T> &pd, int pg, int q, bool v, int cnt, int flg) 
 TD bool unsettled(const v4i a, int min_seq) {
     return a.y > min_seq || (a.z != MT_RSEQ_NONE && a.z > min_seq);
 }
+// Lowest page id not in use (-1: none).  Pages in the directory always hold >= 1 leaf block,
+// free ones none; the id is marked taken (its meta is written by the caller).  Allocation
+// is rare (page split, repack), so a scan of the meta replaces a free list.
+TD int pg_alloc(PagedDoc<T> &pd) {
+    for (int base = 0; base < pd.PP; base += MT_WAVE) {
+        const int pg = base + lane();
+        const u64 m = ballot(pg < pd.PP && pd.meta[pg].nblk == 0);
+        if (m) {
+            const int r = base + first_lane(m);
+            if (lane() == 0) pd.meta[r].nblk = 1;
+            wsync<T>();
+            return r;
+        }
+    }
+    return -1;
+}
+
 // dir position of page id pg (-1 if not in the directory)
 TD int pg_pos(PagedDoc<T> &pd, int pg) {
     const int np = nbr(pd.up, 1);
@@ -310,12 +327,11 @@ TD void pg_split_page(PagedDoc<T> &pd) {
     const int sp = (nbk == MT_MAXN + 1 && w.pend_second >= 0 && w.pend_second < MT_HALF) ? MT_HALF + 1 : MT_HALF;
     int s0 = 0;
     for (int q = 0; q < sp; q++) s0 += cntr(w, 0, q);
-    if (pd.nfree == 0) {
+    const int np = pg_alloc(pd);
+    if (np < 0) {
         pg_fail_cap(w, 7);
         return;
     }
-    pd.nfree--;
-    const int np = uni(pd.freel[pd.nfree]);
     const int pos = pg_cur_pos(pd);
     // table: the window's entries are rebuilt now (first half under this page, second half
     // under the new one), so it never holds both a stale and a fresh copy of a segment
@@ -558,7 +574,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
     if (k > MT_MAXN - 1) k = MT_MAXN - 1;
     if (k < 1) k = 1;
     const int base = TB / k, extra = TB % k;
-    if (pd.nfree < k) {
+    if (nbr(up, 1) + k > pd.PP) {   // the new pages are taken before the old ones are freed
         pg_fail_cap(w, 7);
         return;
     }
@@ -587,8 +603,12 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
     auto nb0 = [&](int m) { return m * base + min(m, extra); };
     LDS_AS int32_t *newp = w.scr;   // scratch: the new page ids
     for (int m = 0; m < k; m++) {
-        pd.nfree--;
-        if (lane() == 0) newp[m] = pd.freel[pd.nfree];
+        const int pg = pg_alloc(pd);
+        if (pg < 0) {
+            pg_fail_cap(w, 7);
+            return;
+        }
+        if (lane() == 0) newp[m] = pg;
     }
     wsync<T>();
     // table entries of the old pages go; the copy pass re-adds the unsettled ones
@@ -657,9 +677,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
         if (lane() == 0) {
             pd.meta[pg].nseg = 0;
             pd.meta[pg].nblk = 0;
-            pd.freel[pd.nfree] = (uint16_t)pg;
         }
-        pd.nfree++;
         wsync<T>();
     }
     // level 1: nch entries -> k entries of base (+1) blocks; then the page ids
@@ -913,9 +931,13 @@ TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const int span = range ? min(max(op.pos2 - op.pos1, 0), 1 << 20) : 0;
     const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
+    // a narrow tier holds overlap masks of short ids 1..32 only
+    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && op_cli(op) > T::kOvlBits) return false;
     if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
     if (pd.w.heap_n + hp_b > pd.PH) return false;
     if (nbr(pd.up, 1) + 8 > pd.PP) return false;
+    for (int l = 2; l < pd.up.depth; l++)
+        if (nbr(pd.up, l) + 4 > bcap(pd.up, l)) return false;
     pd.opbound = ut_b;
     pd.wgrow += ut_b;
     return true;
@@ -1182,6 +1204,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.status = h.status;
     w.dlog_n = h.dlog_n;
     w.dhash = h.delta_hash;
+    w.wide = h.pad0 & 1;
     if (T::kLog) {
         w.m_split = h.pad[HDR_MSPLIT];
         w.m_append = h.pad[HDR_MAPPEND];
@@ -1197,17 +1220,16 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.dir = nullptr;
     up = w;
     up.paged = 0;
-    up.cnt = smem + L.offUcnt;
+    up.cnt = smem + L.offUcnt - pc.PP;   // lvl(up, l) for l >= 1 only
     up.nb = (LDS_AS int32_t *)(smem + L.offUnb);
     up.dir = (LDS_AS uint16_t *)(smem + L.offDir);
     up.B_cap = pc.PP;
     up.status = 0;
     pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
     pd.pvl = (LDS_AS int *)(smem + L.offPvl);
-    pd.freel = (LDS_AS uint16_t *)(smem + L.offFree);
     pd.upage = (LDS_AS uint16_t *)(smem + L.offUpage);
     pd.uA = (LDS_AS v4i *)(smem + L.offUA);
-    pd.uO = (LDS_AS u64 *)(smem + L.offUO);
+    pd.uO = (LDS_AS typename T::O_v *)(smem + L.offUO);
     pd.cur = -1;
     pd.cur_pos = -1;
     pd.dirty = 0;
@@ -1216,8 +1238,9 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.opbound = 0;
 }
 
-// Builds the free-page list from the directory (pvl as scratch marks).
-TD void pg_build_free(PagedDoc<T> &pd) {
+// Pages not in the directory are free (meta cleared; pvl as scratch marks): the HBM meta of
+// ids above a narrower launch's capacity may never have been written.
+TD void pg_mark_free(PagedDoc<T> &pd) {
     const int np = nbr(pd.up, 1);
     pd.vvalid = 0;
     for (int base = 0; base < pd.PP; base += MT_WAVE)
@@ -1226,22 +1249,13 @@ TD void pg_build_free(PagedDoc<T> &pd) {
     for (int base = 0; base < np; base += MT_WAVE)
         if (base + lane() < np) pd.pvl[pd.up.dir[base + lane()]] = 1;
     wsync<T>();
-    int nf = 0;
     for (int base = 0; base < pd.PP; base += MT_WAVE) {
         const int pg = base + lane();
-        const bool fr = pg < pd.PP && pd.pvl[pg] == 0;
-        const u64 m = ballot(fr);
-        // free pages are popped from the top: keep ascending ids at the top
-        if (fr) pd.freel[nf + __popcll(m & ((1ull << lane()) - 1ull))] = (uint16_t)pg;
-        nf += __popcll(m);
+        if (pg < pd.PP && pd.pvl[pg] == 0) {
+            pd.meta[pg].nseg = 0;
+            pd.meta[pg].nblk = 0;
+        }
     }
-    // reverse so that the lowest ids come first
-    for (int i = lane(); i < nf / 2; i += MT_WAVE) {
-        const uint16_t a = pd.freel[i], b = pd.freel[nf - 1 - i];
-        pd.freel[i] = b;
-        pd.freel[nf - 1 - i] = a;
-    }
-    pd.nfree = nf;
     wsync<T>();
 }
 
@@ -1253,6 +1267,7 @@ TD bool pg_load(PagedDoc<T> &pd) {
     const DocHdr h = *w.hp;
     const int np = h.n_blk[1];
     if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
+    if (T::kOvlBits < 64 && w.wide) return false;
     int mx = 0;
     for (int q = lane(); q < np; q += MT_WAVE) mx = max(mx, (int)pd.gdir[q]);
     if (wave_max(mx) >= pd.PP) return false;   // a page id allocated by a wider launch
@@ -1276,7 +1291,7 @@ TD bool pg_load(PagedDoc<T> &pd) {
         pd.uO[e] = pd.guO[e];
     }
     wsync<T>();
-    pg_build_free(pd);
+    pg_mark_free(pd);
     return true;
 }
 
@@ -1332,6 +1347,7 @@ TD void pg_store(PagedDoc<T> &pd) {
         for (int l = 0; l < MT_LV; l++) h.n_blk[l] = nbl[l];
         h.delta_hash = w.dhash;
         h.n_ops = w.hp->n_ops;
+        h.pad0 = w.wide;
         h.pad[HDR_PAGED] = 1;
         h.pad[HDR_NPAGES] = np;
         h.pad[HDR_UTN] = pd.ut_n;
@@ -1391,10 +1407,17 @@ TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
         }
         // stage the page in the window, then write it like any other page
         const int i = lane();
+        bool wide = false;
         if (i < ns) {
             w.A[i] = fA[s + i];
-            w.O[i] = fO[s + i];
+            const u64 o = fO[s + i];
+            wide = T::kOvlBits < 64 && (o >> T::kOvlBits) != 0ull;
+            w.O[i] = (typename T::O_v)o;
             w.Bv[i] = fB[s + i];
+        }
+        if (ballot(wide)) {   // overlap ids above a narrow tier's masks
+            pg_fail_cap(w, 10);
+            return false;
         }
         if (i < PW_B) {
             lvl(w, 0)[i] = i < nbk ? (depth == 1 ? (uint8_t)h.n_seg : fc[lb + i]) : 0;
@@ -1412,7 +1435,7 @@ TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
         lb += nbk;
         s += ns;
     }
-    pg_build_free(pd);
+    pg_mark_free(pd);
     pd.cur = -1;
     pd.wgrow = pd.opbound = 0;
     // the flat tiers number ids without bound: compact them for the uid -> page map

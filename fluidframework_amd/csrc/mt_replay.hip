@@ -23,7 +23,7 @@ __device__ static void init_doc_hdr(const DevState &st, int doc, int len) {
     h.n_blk[0] = 1;
     h.text_top = len;
     h.props_top = 1;
-    h.next_uid = 1;
+    h.next_uid = 2;   // segment ids start at 1 (0 marks a heap entry whose segment is gone)
     h.delta_hash = MT_FNV_OFF;
     h.status = len > st.T ? MT_DOC_CAPACITY : 0;
     const size_t S = st.S;
@@ -31,7 +31,7 @@ __device__ static void init_doc_hdr(const DevState &st, int doc, int len) {
         h.n_seg = 1;
         st.segA[doc * S] = v4i{len, 0, MT_RSEQ_NONE, pack_cli(-1, 0)};
         st.segO[doc * S] = 0ull;
-        st.segB[doc * S] = v4u{0u, 0u, 0u, 0u};
+        st.segB[doc * S] = v4u{0u, 0u, 1u, 0u};
     }
     st.cnt[(size_t)doc * MT_LV * st.B] = len > 0 ? 1 : 0;
     st.flg[(size_t)doc * st.B] = MT_SCOUR_UNDEF;
@@ -563,7 +563,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     if (doc >= st.n_docs) return;
     if (st.retry[doc] != pc.stage) return;
     if (lane() == 0) atomicAdd(st.stats, 1u);
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0);
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v));
     const int64_t k1 = off[doc + 1];
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
     PagedDoc<T> pd;
@@ -681,7 +681,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     if (st.retry[doc] != pc.stage) return;
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 2 * (cfg.writers + 1));
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 2 * (cfg.writers + 1), (int)sizeof(typename T::O_v));
     GenCtx g;
     gen_begin(g, st, cfg, (int)(doc_base + doc), doc, smem + L.offGen, tstride, pstride);
     PagedDoc<T> pd;
@@ -1018,8 +1018,8 @@ struct mt_handle {
     int64_t *d_seed_off = nullptr;   // initial contents kept on device for mt_reset
     uint16_t *d_seed = nullptr;
     TierCaps lds{0, 0, 0, 0};        // LDS-tier capacities (S == 0: tier disabled)
-    PagedCaps pg_tight{0, 0, 0, 1, 1};   // tight paged tier (PP == 0: off)
-    PagedCaps pg_full{0, 0, 0, 0, 1};    // paged tier at the HBM capacities
+    PagedCaps pg_tight{0, 0, 0, 1, 1, 0};   // tight paged tier (PP == 0: off)
+    PagedCaps pg_full{0, 0, 0, 0, 1, 0};    // paged tier at the HBM capacities
 };
 struct mt_batch {
     int device = 0;
@@ -1115,24 +1115,28 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         st.UT = o.unsettled_capacity > 0 ? o.unsettled_capacity : 256;
         st.UM = std::min(o.uid_capacity > 0 ? o.uid_capacity : 65536, 1 << 24);
         st.UM = std::max(st.UM, 256);
-        h->pg_full = PagedCaps{st.PP, st.PH, st.UT, 0, 1};
+        h->pg_full = PagedCaps{st.PP, st.PH, st.UT, 0, 1, 0};
         const PagedCaps t{o.lds_page_capacity > 0 ? std::min(o.lds_page_capacity, st.PP) : st.PP,
                           o.lds_page_heap_capacity > 0 ? std::min(o.lds_page_heap_capacity, st.PH) : st.PH,
-                          o.lds_unsettled_capacity > 0 ? std::min(o.lds_unsettled_capacity, st.UT) : st.UT, 1, 1};
-        if (t.PP < st.PP || t.PH < st.PH || t.UT < st.UT) {
+                          o.lds_unsettled_capacity > 0 ? std::min(o.lds_unsettled_capacity, st.UT) : st.UT, 1, 1,
+                          o.lds_narrow_overlap ? 1 : 0};
+        if (t.PP < st.PP || t.PH < st.PH || t.UT < st.UT || t.narrow) {
             h->pg_tight = t;
             h->pg_full.stage = 2;
         }
         // one document's paged state staged in LDS: up to the CU's 160 KiB (fewer
         // documents per CU above 64 KiB)
-        const size_t lb = paged_layout(st.PP, st.PH, st.UT, 2 * 65).total;
+        const size_t lb = paged_layout(st.PP, st.PH, st.UT, 2 * 65, 8).total;
         if (lb > 160 * 1024) {
             delete h;
             return nullptr;
         }
         if (lb > 64 * 1024) {
             const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true>>, (const void *)k_replay_paged<TierPagedT<false>>,
-                                (const void *)k_generate_paged<TierPagedT<false>>};
+                                (const void *)k_generate_paged<TierPagedT<false>>,
+                                (const void *)k_replay_paged<TierPagedT<true, true>>,
+                                (const void *)k_replay_paged<TierPagedT<false, true>>,
+                                (const void *)k_generate_paged<TierPagedT<false, true>>};
             for (const void *k : ks)
                 if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess) {
                     delete h;
@@ -1318,14 +1322,21 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         const PagedCaps *tiers[2] = {h->pg_tight.PP ? &h->pg_tight : nullptr, &h->pg_full};
         for (const PagedCaps *pc : tiers) {
             if (!pc) continue;
-            const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, 0).total;
+            const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, 0, pc->narrow ? 4 : 8).total;
             const int res = pc->stage == 2 ? 1 : use_resume;
-            if (h->st.DL)
-                hipLaunchKernelGGL(k_replay_paged<TierPagedT<true>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
-                                   b->ops, b->off, b->text, b->props, res, *pc);
+            const dim3 g(h->n_docs), blk(MT_WAVE);
+            if (h->st.DL && pc->narrow)
+                hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+                                   b->text, b->props, res, *pc);
+            else if (h->st.DL)
+                hipLaunchKernelGGL((k_replay_paged<TierPagedT<true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+                                   b->text, b->props, res, *pc);
+            else if (pc->narrow)
+                hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+                                   b->off, b->text, b->props, res, *pc);
             else
-                hipLaunchKernelGGL(k_replay_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
-                                   h->st, b->ops, b->off, b->text, b->props, res, *pc);
+                hipLaunchKernelGGL((k_replay_paged<TierPagedT<false>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+                                   b->text, b->props, res, *pc);
             HIPCHK(h, hipGetLastError());
         }
     } else if (h->st.DL)
@@ -1655,10 +1666,15 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
             const PagedCaps *tiers[2] = {h->pg_tight.PP ? &h->pg_tight : nullptr, &h->pg_full};
             for (const PagedCaps *pc : tiers) {
                 if (!pc || !ok) continue;
-                const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, gw).total;
-                hipLaunchKernelGGL(k_generate_paged<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream,
-                                   h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride, pstride, d_fail,
-                                   d_trace, *pc);
+                const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, gw, pc->narrow ? 4 : 8).total;
+                if (pc->narrow)
+                    hipLaunchKernelGGL((k_generate_paged<TierPagedT<false, true>>), dim3(h->n_docs), dim3(MT_WAVE), lb,
+                                       h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
+                                       pstride, d_fail, d_trace, *pc);
+                else
+                    hipLaunchKernelGGL((k_generate_paged<TierPagedT<false>>), dim3(h->n_docs), dim3(MT_WAVE), lb,
+                                       h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
+                                       pstride, d_fail, d_trace, *pc);
                 ok = hipGetLastError() == hipSuccess;
             }
             ok = ok && hipStreamSynchronize(h->stream) == hipSuccess;

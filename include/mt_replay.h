@@ -66,6 +66,10 @@ typedef struct mt_options {
     int32_t lds_page_capacity;
     int32_t lds_unsettled_capacity;
     int32_t lds_page_heap_capacity;
+    /* 1: the tight tier keeps removedClientOverlap masks of short ids 1..32 only (4 bytes
+       per LDS segment instead of 8); a document one of whose clients above 32 removes an
+       already-removed segment continues in the full tier.  For documents with few writers. */
+    int32_t lds_narrow_overlap;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

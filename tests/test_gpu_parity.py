@@ -38,6 +38,11 @@ TIERS = {
     # full-capacity paged launch mid-batch (and at load), generators regenerate there
     "tight": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024, page_heap_capacity=1024,
                   lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40),
+    # a narrow tight tier (32-bit overlap masks): documents whose clients above 32 remove
+    # overlapping ranges (C4: 64 writers) move to the full tier
+    "narrow": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024, page_heap_capacity=1024,
+                   lds_page_capacity=200, lds_unsettled_capacity=600, lds_page_heap_capacity=600,
+                   lds_narrow_overlap=1),
 }
 
 
@@ -59,7 +64,7 @@ def test_gpu_matches_reference(name, tier):
     paged = [mt.is_paged(i) for i in range(len(fx["docs"]))]
     if tier == "paged":
         assert all(paged)
-    elif "paged" not in tier and tier != "tight":
+    elif "paged" not in tier and tier not in ("tight", "narrow"):
         assert not any(paged)
 
 
@@ -122,7 +127,7 @@ def test_gpu_maintenance_events_match_reference(name, tier):
     assert got == gu.maint_counts(name), name
 
 
-@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged", "tight"])
+@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged", "tight", "narrow"])
 @pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6), ("c3", 3000, 4)])
 def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     import json
