@@ -119,6 +119,8 @@ template <class T> struct DocT {
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
     int wide;               // an overlap mask holds a short id above 32 (DocHdr.pad0 bit 0)
+    int dlo;                // paged window: lowest slot written since the page was loaded /
+                            // written back (only [dlo, n) goes back to HBM)
     // paged documents (mt_paged.h): this DocT is a window onto one page, or the instance
     // holding the levels >= 1 of the tree (dir != nullptr); all zero for flat documents
     int paged;              // 1: window onto one page
@@ -272,6 +274,7 @@ TD int nbr(DocT<T> &d, int l) { return uni(d.nb[l]); }
 TD int cntr(DocT<T> &d, int l, int b) { return uni(lvl(d, l)[b]); }
 TD int flgr(DocT<T> &d, int b) { return uni(d.flg[b]); }
 __device__ __forceinline__ v4i uni4(v4i a) { return v4i{uni(a.x), uni(a.y), uni(a.z), uni(a.w)}; }
+__device__ __forceinline__ v2i uni2(v2i a) { return v2i{uni(a.x), uni(a.y)}; }
 __device__ __forceinline__ v4u uni4(v4u a) {
     return v4u{(uint32_t)uni((int)a.x), (uint32_t)uni((int)a.y), (uint32_t)uni((int)a.z), (uint32_t)uni((int)a.w)};
 }
@@ -453,9 +456,16 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
     }
 }
 
+// A paged window records the lowest slot an engine step writes (mark_dirty); the flat
+// tiers compile it out.
+TD void mark_dirty(DocT<T> &d, int i) {
+    if constexpr (T::kPaged) d.dlo = min(d.dlo, i);
+}
+
 // ------------------------------------------------------------------ segment table moves
 // [from, n) -> [from + k, n + k)
 TD void seg_move_right(DocT<T> &d, int from, int k) {
+    mark_dirty(d, from);
     for (int hi = d.n; hi > from; hi -= MT_WAVE) {
         const int lo = max(from, hi - MT_WAVE);
         const int i = lo + lane();
@@ -478,6 +488,7 @@ TD void seg_move_right(DocT<T> &d, int from, int k) {
 }
 // [from, n) -> [from - k, n - k)
 TD void seg_move_left(DocT<T> &d, int from, int k) {
+    mark_dirty(d, from - k);
     for (int lo = from; lo < d.n; lo += MT_WAVE) {
         const int i = lo + lane();
         v4i a;
@@ -711,25 +722,33 @@ TD int block_of(DocT<T> &d, int i, int nb) {
 }
 
 // ------------------------------------------------------------------ zamboni heap
-// Collections.Heap add/get (MT/collections.ts:212-265); touched by lane 0 only.
+// Collections.Heap add/get (MT/collections.ts:212-265), comparer maxSeq (LRUSegmentComparer
+// MT/mergeTree.ts:957-960).  The binary heap is reproduced exactly (its tie order decides the
+// zamboni schedule), but each sift is resolved by the whole wave: instead of one
+// dependent LDS round trip per level, lanes load all ancestors (fixup) or the next five
+// levels below the sift position (fixdown) at once and the path is followed with readlane.
 TD void heap_add(DocT<T> &d, int max_seq, int uid) {
     if (d.heap_n + 1 > d.H_cap) {
         fail_cap(d, 3);
         return;
     }
     d.heap_n++;
-    if (lane() == 0) {
-        typename T::H_t h = d.heap;
-        int k = d.heap_n;
-        const v2i e = v2i{max_seq, uid};
-        while (k > 1) {
-            const v2i p = h[k >> 1];
-            if (!(p.x - e.x > 0)) break;
-            h[k] = p;
-            k >>= 1;
-        }
-        h[k] = e;
-    }
+    typename T::H_t h = d.heap;
+    const int k = d.heap_n;
+    const v2i e = v2i{max_seq, uid};
+    // fixup: lane l holds the ancestor k >> (l + 1); values do not increase towards the root,
+    // so the ancestors that move down (compare(parent, e) > 0) are the lanes below the first
+    // one that stays
+    const int l = lane();
+    const int a = l < 30 ? (k >> (l + 1)) : 0;
+    v2i p = v2i{0, 0};
+    if (a >= 1) p = h[a];
+    const u64 mv = ballot(a >= 1 && p.x - e.x > 0);
+    const int s = __builtin_ctzll(~mv);
+    wsync<T>();
+    if (l < s) h[k >> l] = p;
+    if (l == 0) h[k >> s] = e;
+    wsync<T>();
 }
 TD v2i heap_top(DocT<T> &d) {
     int x = 0, y = 0;
@@ -741,27 +760,49 @@ TD v2i heap_top(DocT<T> &d) {
     return v2i{bcast(x, 0), bcast(y, 0)};
 }
 TD void heap_pop(DocT<T> &d) {
-    if (lane() == 0) {
-        typename T::H_t h = d.heap;
-        const int n = d.heap_n - 1;
-        const v2i e = h[d.heap_n];
-        int k = 1;
-        while ((k << 1) <= n) {
-            int j = k << 1;
-            v2i cj = h[j];
-            if (j < n) {
-                const v2i cj1 = h[j + 1];
-                if (cj.x - cj1.x > 0) {
-                    j++;
-                    cj = cj1;
+    typename T::H_t h = d.heap;
+    const int n = d.heap_n - 1;   // entries once the last one has moved to the root
+    const v2i e = uni2(h[d.heap_n]);
+    // lane q <-> node (level m, position t) of the 5 levels below the sift position:
+    // q = 2^m - 2 + t, m = 1..5, t < 2^m
+    const int q = lane();
+    const int m = 31 - __clz(q + 2);
+    const int t = q + 2 - (1 << m);
+    int k = 1;
+    bool done = false;
+    while (!done) {
+        const int idx = (k << m) + t;
+        v2i v = v2i{0, 0};
+        if (q < 62 && idx <= n) v = h[idx];
+        int tt = 0;
+        for (int mm = 1; mm <= 5; mm++) {
+            const int jl = k << 1;
+            if (jl > n) {
+                done = true;
+                break;
+            }
+            const int ll = (1 << mm) - 2 + 2 * tt;
+            int cx = bcast(v.x, ll), cy = bcast(v.y, ll), j = jl, tj = 2 * tt;
+            if (jl < n) {
+                const int rx = bcast(v.x, ll + 1);
+                if (cx - rx > 0) {
+                    cx = rx;
+                    cy = bcast(v.y, ll + 1);
+                    j = jl + 1;
+                    tj++;
                 }
             }
-            if (e.x - cj.x <= 0) break;
-            h[k] = cj;
+            if (e.x - cx <= 0) {
+                done = true;
+                break;
+            }
+            if (lane() == 0) h[k] = v2i{cx, cy};
             k = j;
+            tt = tj;
         }
-        h[k] = e;
     }
+    if (lane() == 0) h[k] = e;
+    wsync<T>();
     d.heap_n--;
 }
 
@@ -1004,6 +1045,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
         return;
     }
     seg_move_right(d, i + 1, 1);
+    mark_dirty(d, i);
     if (T::kLog) d.m_split++;   // splitLeafSegment's SPLIT event :2264-2269
     if (lane() == 0) {
         v4i a = d.A[i];
@@ -1167,6 +1209,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
         d.m_append += __popcll(m_app);
     }
     if (m_app) {
+        mark_dirty(d, s);
         // group length per keeper (lanes that are keepers sum their members)
         int glen = 0;
         if (in && myown == (uint32_t)k) {
@@ -1264,6 +1307,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     }
     const int keep = __popcll(m_keep);
     if (keep < cntb) {
+        mark_dirty(d, s);
         // compaction: survivors to the front of the block, tail moved left
         const bool surv = (m_keep >> k) & 1ull;
         v4i sa;
@@ -1367,6 +1411,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     const u64 m_grp = ballot(surv && (above & 1ull));
     P2_T0(10)
     if (m_grp) {
+        mark_dirty(d, s);
         // group length of each keeper: inclusive lengths up to the group's last member
         const int L = wave_scan_incl(in ? a.x : 0);
         const int gend = k + __ffsll((long long)~above) - 1;   // last member (above has a 0)
@@ -1451,6 +1496,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     P2_T0(11)
     const int keep = __popcll(m_surv);
     if (keep < tot) {
+        mark_dirty(d, s);
         // compaction: survivors to the front, tail moved left
         v4i sa;
         u64 so;
@@ -1764,6 +1810,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     P2_T0(15)
     seg_move_right(d, x, 1);
     P2_T1(15)
+    mark_dirty(d, x);
     const uint32_t uid = (uint32_t)d.next_uid;
     if (lane() == 0) {
         d.A[x] = v4i{slen, seq, MT_RSEQ_NONE, pack_cli(c, 0)};
@@ -1899,6 +1946,7 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         const int pex = carry + inc - vl, pin_ = carry + inc;
         const bool sel = v && vl > 0 && pex < p2 && pin_ > p1;
         const u64 sel_m = ballot(sel);
+        if (sel_m) mark_dirty(d, base + first_lane(sel_m));
         bool newly = false, bad = false, spill = false;
         if (rem && sel) {
             if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
@@ -2042,6 +2090,7 @@ TD void load_removed(DocT<T> &d, const mt_op_rec &op) {
         FAIL_INTERNAL(d);
         return;
     }
+    mark_dirty(d, i);
     if (lane() == 0) {
         v4i a = d.A[i];
         a.z = op.seq;

@@ -223,6 +223,7 @@ TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const 
     w.depth = pd.up.depth == 1 ? 1 : 2;
     w.pend_split = 0;
     w.pend_second = -1;
+    w.dlo = MT_PG_SLOTS;
     pd.cur = pg;
     pd.cur_pos = -1;
     pd.dirty = 0;
@@ -286,8 +287,9 @@ TD void pg_table_add(PagedDoc<T> &pd, int lo, int hi, int pg2) {
 }
 
 // Writes window slots [lo, hi) to page pg (slot 0 = lo) with its meta (blocks [b0, b1) of
-// the window) and the uid -> page map.
-TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1) {
+// the window) and the uid -> page map.  Slots below `from` (relative to lo) are unchanged
+// in HBM and are not written.
+TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1, int from = 0) {
     DocT<T> &w = pd.w;
     const int i = lane();
     GLB_AS v4i *gA = pd.gA + (size_t)pg * MT_PG_SLOTS;
@@ -296,14 +298,16 @@ TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1) {
     int ol = 0;
     if (lo + i < hi) {
         const v4i a = w.A[lo + i];
-        const v4u b = w.Bv[lo + i];
-        gA[i] = a;
-        gO[i] = w.O[lo + i];
-        gB[i] = b;
-        const uint32_t uid = b.z & ~MT_MARKER_BIT;
-        // the uid -> page map changes only for segments created since the window was
-        // loaded, or moved to another page (scattered 2-byte writes: one sector each)
-        if (uid < (uint32_t)pd.UM && (pg != pd.cur || uid >= (uint32_t)pd.uid_lo)) pd.gumap[uid] = (uint16_t)pg;
+        if (i >= from) {
+            const v4u b = w.Bv[lo + i];
+            gA[i] = a;
+            gO[i] = w.O[lo + i];
+            gB[i] = b;
+            const uint32_t uid = b.z & ~MT_MARKER_BIT;
+            // the uid -> page map changes only for segments created since the window was
+            // loaded, or moved to another page (scattered 2-byte writes: one sector each)
+            if (uid < (uint32_t)pd.UM && (pg != pd.cur || uid >= (uint32_t)pd.uid_lo)) pd.gumap[uid] = (uint16_t)pg;
+        }
         ol = obs_len(a);
     }
     const int obs = wave_sum(ol);
@@ -422,10 +426,13 @@ TD void pg_win_flush(PagedDoc<T> &pd) {
 TD void pg_win_flush_impl(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     if (pd.cur < 0 || !pd.dirty) return;
-    pg_table_purge(pd, pd.cur);
-    pg_table_add(pd, 0, w.n, pd.cur);
-    if (w.status) return;
-    pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0));
+    if (w.dlo < w.n) {   // some slot changed: its table entries and the slots from dlo on
+        pg_table_purge(pd, pd.cur);
+        pg_table_add(pd, 0, w.n, pd.cur);
+        if (w.status) return;
+        pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0), w.dlo);
+    }
+    w.dlo = MT_PG_SLOTS;
     pd.dirty = 0;
     pd.wgrow = pd.opbound;   // exact again, up to the rest of the current message
 }
@@ -445,11 +452,12 @@ TD void pg_win_switch(PagedDoc<T> &pd, int pg) {
 }
 
 // ------------------------------------------------------------------ page view lengths
-// pvl[page] = view length of every page for (c, r); returns the total.
-TD int pg_views_impl(PagedDoc<T> &pd, int r, int c);
-TD int pg_views(PagedDoc<T> &pd, int r, int c) {
+// pvl[page] = view length of every page for (c, r); returns the total when asked (the
+// generator draws positions from it; replay only needs pvl).
+TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total);
+TD int pg_views(PagedDoc<T> &pd, int r, int c, bool total = true) {
     PG_T0(9)
-    const int r_ = pg_views_impl(pd, r, c);
+    const int r_ = pg_views_impl(pd, r, c, total);
     PG_T1(9)
     pd.vvalid = 1;
     pd.vr = r;
@@ -458,9 +466,9 @@ TD int pg_views(PagedDoc<T> &pd, int r, int c) {
 }
 // pvl for view (r, c): recomputed only if a change other than a boundary split happened
 TD void pg_views_cached(PagedDoc<T> &pd, int r, int c) {
-    if (!(pd.vvalid && pd.vr == r && pd.vc == c)) pg_views(pd, r, c);
+    if (!(pd.vvalid && pd.vr == r && pd.vc == c)) pg_views(pd, r, c, false);
 }
-TD int pg_views_impl(PagedDoc<T> &pd, int r, int c) {
+TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
     const int np = nbr(pd.up, 1);
     int tot = 0;
     for (int base = 0; base < np; base += MT_WAVE) {
@@ -491,6 +499,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c) {
         if (i == 0) pd.pvl[cur] += dlt;
     }
     wsync<T>();
+    if (!total) return 0;
     for (int base = 0; base < np; base += MT_WAVE) {
         const int q = base + lane();
         tot += q < np ? pd.pvl[pd.up.dir[q]] : 0;
@@ -1213,6 +1222,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
         w.dlog_rec = -1;
     }
     w.text_gcs = w.props_gcs = w.cap_cause = 0;
+    w.dlo = MT_PG_SLOTS;
     w.paged = 1;
     w.obs_base = 0;
     w.pend_split = 0;
