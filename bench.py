@@ -160,6 +160,50 @@ def capacities(cfg, tight=True):
     return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
 
 
+def _decode_slice(chunk_list):
+    """Worker: SnapshotLoader's host half for a slice of summaries -- JSON chunks parsed and
+    specToSegment'ed into mt_seg_rec records (snapshot.decode_chunks + SnapshotBatch)."""
+    from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks
+    from fluidframework_amd.wire import Interner
+    sb = SnapshotBatch(Interner(synthetic=True))
+    for ch in chunk_list:
+        sb.add_doc(decode_chunks(ch))
+    a = sb.arrays()
+    return len(chunk_list), int(len(a["segs"]))
+
+
+def c5_decode_rate(counts, recs, text, props, mn, cu, chunk, n_sample, threads):
+    """Summary decode as its own line: the sample's summaries are emitted as SnapshotV1 JSON
+    chunks (untimed), then decoded back to device records on the host cores (timed).  The
+    device load (mt_snapshots_load_async) starts from records; this is the step before it."""
+    from concurrent.futures import ProcessPoolExecutor
+    from fluidframework_amd.snapshot import encode_chunks, record_specs
+    from fluidframework_amd.wire import Interner
+    it = Interner(synthetic=True)
+    c = np.asarray(counts, dtype=np.int64)
+    r0 = np.concatenate([[0], np.cumsum(c[:, 0])])
+    t0 = np.concatenate([[0], np.cumsum(c[:, 1])])
+    p0 = np.concatenate([[0], np.cumsum(c[:, 2])])
+    names = {i: f"client-{i}" for i in range(-2, 4096)}
+    docs = []
+    for d in range(n_sample):
+        rs = recs[r0[d]:r0[d + 1]]
+        specs, lengths = record_specs(rs, text[t0[d]:t0[d + 1]], props[p0[d]:p0[d + 1]], it, names)
+        docs.append(encode_chunks(specs, lengths, int(mn[d]), int(cu[d]), chunk))
+    nbytes = sum(len(v) for ch in docs for v in ch.values())
+    per = -(-len(docs) // threads)
+    parts = [docs[i:i + per] for i in range(0, len(docs), per)]
+    with ProcessPoolExecutor(len(parts)) as ex:
+        list(ex.map(_decode_slice, parts[:1]))          # warm the workers' imports
+        t = time.perf_counter()
+        done = list(ex.map(_decode_slice, parts))
+        t = time.perf_counter() - t
+    n = sum(x[0] for x in done)
+    return dict(value=round(n / t, 1), unit="docs/s", cores=len(parts), kind="port",
+                sample=f"{n} summaries ({nbytes / 1e6:.1f} MB of chunk JSON, {sum(x[1] for x in done)} segment specs) "
+                       f"decoded by fluidframework_amd/snapshot.py on {len(parts)} host processes, {t:.2f} s")
+
+
 def run_c5(args, cfg, rank, world, local_rank, dist):
     """Config C5 (cold catch-up): every document's SnapshotV1 summary is loaded
     (mt_snapshots_load_async: reloadFromSegments + loadBody) and its tail of `tail` sequenced
@@ -218,8 +262,10 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
     if rank != 0:
         return
     n_tail = int(len(idx))
-    cpu = parity = None
+    cpu = parity = decode = None
     if not args.no_cpu:
+        threads = args.cpu_threads or host_cores()
+        decode = c5_decode_rate(counts, recs, text, props, mn, cu, cfg["chunk"], min(docs, 4000), threads)
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import pyoracle                            # the checker, timed as the CPU baseline
         n_sample = args.cpu_sample_docs or min(docs, 20000)
@@ -248,6 +294,7 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
                                                                                      np.diff(load["doc_off"])).sum()),
                    "parallelism": f"doc-shard x{world}"},
         "cpu_baseline": cpu,
+        "summary_decode": decode,
         "parity": {"status_nonzero": int((status != 0).sum()), "oracle_sample": parity},
         "prep_s": round(t_prep, 2),
     }))

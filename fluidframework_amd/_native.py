@@ -24,7 +24,8 @@ class MtOptions(ctypes.Structure):
                 ("page_capacity", ctypes.c_int32), ("page_heap_capacity", ctypes.c_int32),
                 ("unsettled_capacity", ctypes.c_int32), ("uid_capacity", ctypes.c_int32),
                 ("lds_page_capacity", ctypes.c_int32), ("lds_unsettled_capacity", ctypes.c_int32),
-                ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32)]
+                ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32),
+                ("delta_log_mode", ctypes.c_int32)]
 
 
 class MtGenCfg(ctypes.Structure):

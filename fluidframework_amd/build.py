@@ -10,8 +10,8 @@ DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", 
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mt_replay.h", "mt_types.h")]
 OUT = os.environ.get("MT_OUT") or os.path.join(HERE, "libmtreplay.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = os.environ.get("MT_EXTRA_FLAGS", "").split() + ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-result",
-         "-Wno-unused-value"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-result",
+         "-Wno-unused-value"] + os.environ.get("MT_EXTRA_FLAGS", "").split()
 
 
 def needs_build():
@@ -49,5 +49,6 @@ def build_node_addon(verbose=False):
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
-    build_node_addon(verbose=True)
+    if not os.environ.get("MT_OUT"):   # variant libraries (MT_OUT) leave the addon alone
+        build_node_addon(verbose=True)
     print(OUT)

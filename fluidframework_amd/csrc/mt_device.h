@@ -103,13 +103,22 @@ struct DevState {
     uint16_t *pgUmap;         // [n_docs][UM] uid -> page
     int32_t PP, PH, UT, UM;
     int32_t S, B, H, T, P, DL;
+    int32_t DLR;              // rich delta log: segment text / properties + maintenance events
     int32_t n_docs;
 };
 
 // ------------------------------------------------------------------ wave primitives
 // lane within the wavefront (the LDS-tier replay may hold several documents per workgroup,
 // one per wave)
+#ifdef MT_LANE_ASM
+__device__ __forceinline__ int lane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+#else
 __device__ __forceinline__ int lane() { return (int)(threadIdx.x & (MT_WAVE - 1)); }
+#endif
 
 // Inclusive prefix sum over the wavefront with DPP row shifts + row broadcasts (6 VALU
 // ops, no LDS traffic).  Lanes that have no source read the identity (bound_ctrl off,

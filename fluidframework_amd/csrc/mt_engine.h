@@ -71,15 +71,16 @@ template <bool kLogT, bool kNarrowT = false> struct TierPagedT {
 // lane and read by another waits for the stores to complete.
 __device__ __forceinline__ void gsync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Before a lane reads global data (text, property records) that another lane of the same
-// wavefront stored earlier.  A wavefront's vector-memory instructions reach the L1/L2 in
-// issue order, so a later load observes an earlier store to the same address: only the
-// compiler must not reorder.  (-DMT_STRICT_GSYNC waits for the stores instead.)
+// wavefront stored earlier: a workgroup-scope acquire-release fence, the memory model's own
+// form for this.  The AMDGPU memory model gives lanes of one wavefront (and waves of one
+// workgroup, outside tgsplit mode) a single coherent vector L1 on gfx950, so the backend
+// lowers this fence to an ordering constraint with no wait; -DMT_STRICT_GSYNC adds
+// s_waitcnt vmcnt(0) anyway (measured: no difference on the C3 bench, r2 A/B).
 __device__ __forceinline__ void gsync_rd() {
 #ifdef MT_STRICT_GSYNC
     gsync();
-#else
-    asm volatile("" ::: "memory");
 #endif
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 }
 template <class T> __device__ __forceinline__ void wsync() {
     if constexpr (T::kLds)
@@ -91,6 +92,8 @@ template <class T> __device__ __forceinline__ void wsync() {
 // segB.w flags
 #define SEGF_NL_KNOWN 1u   // SEGF_NL is valid
 #define SEGF_NL 2u         // the segment's text ends with '\n' (TextSegment.canAppend :63-68)
+#define SEGF_NOMATCH 4u    // its property set holds a value matchProperties never finds equal
+                           // (MT_VAL_NOMATCH_BIT: NaN / undefined from a combining op, Q4)
 #define SEGF_SLACK_SHIFT 16 // bits 16..31: arena units reserved after the text for appends
 __device__ __forceinline__ int text_slack(int len) { return min((len >> 1) + 8, 4096); }
 
@@ -118,6 +121,7 @@ template <class T> struct DocT {
     u64 dhash;
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
+    int rich;                          // rich delta log (segments' state, maintenance events)
     int wide;               // an overlap mask holds a short id above 32 (DocHdr.pad0 bit 0)
     int dlo;                // paged window: lowest slot written since the page was loaded /
                             // written back (only [dlo, n) goes back to HBM)
@@ -296,6 +300,7 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.T_cap = st.T;
     d.P_cap = st.P;
     d.DL_cap = st.DL;
+    d.rich = st.DLR;
     d.scr = (LDS_AS int32_t *)(smem + L.offScr);
     d.nb = (LDS_AS int32_t *)(smem + L.offNb);
     d.ends = (LDS_AS uint16_t *)(smem + L.offEnds);
@@ -459,7 +464,12 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
 // A paged window records the lowest slot an engine step writes (mark_dirty); the flat
 // tiers compile it out.
 TD void mark_dirty(DocT<T> &d, int i) {
+#if defined(MT_NO_DIRTY)
+#elif defined(MT_FULL_WRITEBACK)
+    if constexpr (T::kPaged) d.dlo = 0;
+#else
     if constexpr (T::kPaged) d.dlo = min(d.dlo, i);
+#endif
 }
 
 // ------------------------------------------------------------------ segment table moves
@@ -723,32 +733,27 @@ TD int block_of(DocT<T> &d, int i, int nb) {
 
 // ------------------------------------------------------------------ zamboni heap
 // Collections.Heap add/get (MT/collections.ts:212-265), comparer maxSeq (LRUSegmentComparer
-// MT/mergeTree.ts:957-960).  The binary heap is reproduced exactly (its tie order decides the
-// zamboni schedule), but each sift is resolved by the whole wave: instead of one
-// dependent LDS round trip per level, lanes load all ancestors (fixup) or the next five
-// levels below the sift position (fixdown) at once and the path is followed with readlane.
+// MT/mergeTree.ts:957-960); touched by lane 0 only.  (A wave-parallel fixdown -- five levels
+// loaded at once, the path followed with readlane -- measured slower: 1.8k -> 2.9k cycles
+// per pop on C3, profiles/r2/sections_c3_v2.log.)
 TD void heap_add(DocT<T> &d, int max_seq, int uid) {
     if (d.heap_n + 1 > d.H_cap) {
         fail_cap(d, 3);
         return;
     }
     d.heap_n++;
-    typename T::H_t h = d.heap;
-    const int k = d.heap_n;
-    const v2i e = v2i{max_seq, uid};
-    // fixup: lane l holds the ancestor k >> (l + 1); values do not increase towards the root,
-    // so the ancestors that move down (compare(parent, e) > 0) are the lanes below the first
-    // one that stays
-    const int l = lane();
-    const int a = l < 30 ? (k >> (l + 1)) : 0;
-    v2i p = v2i{0, 0};
-    if (a >= 1) p = h[a];
-    const u64 mv = ballot(a >= 1 && p.x - e.x > 0);
-    const int s = __builtin_ctzll(~mv);
-    wsync<T>();
-    if (l < s) h[k >> l] = p;
-    if (l == 0) h[k >> s] = e;
-    wsync<T>();
+    if (lane() == 0) {
+        typename T::H_t h = d.heap;
+        int k = d.heap_n;
+        const v2i e = v2i{max_seq, uid};
+        while (k > 1) {
+            const v2i p = h[k >> 1];
+            if (!(p.x - e.x > 0)) break;
+            h[k] = p;
+            k >>= 1;
+        }
+        h[k] = e;
+    }
 }
 TD v2i heap_top(DocT<T> &d) {
     int x = 0, y = 0;
@@ -760,49 +765,26 @@ TD v2i heap_top(DocT<T> &d) {
     return v2i{bcast(x, 0), bcast(y, 0)};
 }
 TD void heap_pop(DocT<T> &d) {
-    typename T::H_t h = d.heap;
-    const int n = d.heap_n - 1;   // entries once the last one has moved to the root
-    const v2i e = uni2(h[d.heap_n]);
-    // lane q <-> node (level m, position t) of the 5 levels below the sift position:
-    // q = 2^m - 2 + t, m = 1..5, t < 2^m
-    const int q = lane();
-    const int m = 31 - __clz(q + 2);
-    const int t = q + 2 - (1 << m);
-    int k = 1;
-    bool done = false;
-    while (!done) {
-        const int idx = (k << m) + t;
-        v2i v = v2i{0, 0};
-        if (q < 62 && idx <= n) v = h[idx];
-        int tt = 0;
-        for (int mm = 1; mm <= 5; mm++) {
-            const int jl = k << 1;
-            if (jl > n) {
-                done = true;
-                break;
+    if (lane() == 0) {
+        typename T::H_t h = d.heap;
+        const int n = d.heap_n - 1;
+        const v2i e = h[d.heap_n];
+        int k = 1;
+        while ((k << 1) <= n) {
+            int j = k << 1;
+            // both children in one LDS round trip (h[n + 1] is the entry being moved: in bounds)
+            v2i cj = h[j];
+            const v2i cj1 = h[j + 1];
+            if (j < n && cj.x - cj1.x > 0) {
+                j++;
+                cj = cj1;
             }
-            const int ll = (1 << mm) - 2 + 2 * tt;
-            int cx = bcast(v.x, ll), cy = bcast(v.y, ll), j = jl, tj = 2 * tt;
-            if (jl < n) {
-                const int rx = bcast(v.x, ll + 1);
-                if (cx - rx > 0) {
-                    cx = rx;
-                    cy = bcast(v.y, ll + 1);
-                    j = jl + 1;
-                    tj++;
-                }
-            }
-            if (e.x - cx <= 0) {
-                done = true;
-                break;
-            }
-            if (lane() == 0) h[k] = v2i{cx, cy};
+            if (e.x - cj.x <= 0) break;
+            h[k] = cj;
             k = j;
-            tt = tj;
         }
+        h[k] = e;
     }
-    if (lane() == 0) h[k] = e;
-    wsync<T>();
     d.heap_n--;
 }
 
@@ -868,7 +850,8 @@ TD void text_gc(DocT<T> &d) {
             a = d.A[i];
             b = d.Bv[i];
         }
-        const bool live = i < d.n && a.z == MT_RSEQ_NONE && !(b.z & MT_MARKER_BIT);
+        // (a rich delta log keeps removed segments' text: their UNLINK event reports it)
+        const bool live = i < d.n && (a.z == MT_RSEQ_NONE || (T::kLog && d.rich)) && !(b.z & MT_MARKER_BIT);
         const int len = live ? a.x : 0;
         const int inc = wave_scan_incl(len);
         const int off = carry + inc - len;
@@ -945,9 +928,11 @@ TD bool props_ensure(DocT<T> &d, int need) {
     fail_cap(d, 5);
     return false;
 }
-// Properties.matchProperties MT/properties.ts:61-92 over interned ids
-TD bool match_props(DocT<T> &d, uint32_t ha, uint32_t hb) {
+// Properties.matchProperties MT/properties.ts:61-92 over interned ids; nm: either set holds a
+// NaN / undefined value (SEGF_NOMATCH), which no comparison finds equal
+TD bool match_props(DocT<T> &d, uint32_t ha, uint32_t hb, bool nm) {
     if (ha == 0 || hb == 0) return ha == hb;
+    if (nm) return false;
     if (ha == hb) return true;
     const GLB_AS uint32_t *a = prec(d, d.props_half, ha), *b = prec(d, d.props_half, hb);
     const uint32_t na = a[0], nbb = b[0];
@@ -1018,6 +1003,80 @@ TD void cb_log(DocT<T> &d, int32_t v) {
     }
 }
 
+// Rich delta log (handles with delta_log_mode 1): every logged segment also carries its
+// state at the event -- [flags (1 marker, 2 has properties), marker: refType | text: the
+// UTF-16 units two per word, n (-1: no properties), (key, value) x n] -- and the
+// mergeTreeMaintenanceCallback events are records of their own (kind SPLIT -2, APPEND -1,
+// UNLINK -3; MT/mergeTreeDeltaCallback.ts:15-30): [seq, kind, n, (cachedLength, state) x n].
+// A segment's text is the concatenation of np pieces (an APPEND's merged segment).
+struct TextPieces {
+    uint32_t off[8];
+    int len[8];
+    int np;
+};
+TD void cb_log_state(DocT<T> &d, bool marker, uint32_t ref_type, const TextPieces &tp, const GLB_AS uint32_t *pr) {
+    if constexpr (T::kLog) {
+        int tot = 0;
+        for (int q = 0; q < tp.np; q++) tot += tp.len[q];
+        const int words = marker ? 1 : (tot + 1) / 2;
+        if (pr) gsync_rd();   // a record another lane may just have written
+        const int np = pr ? (int)pr[0] : -1;
+        if (!cb_room(d, 2 + words + 2 * max(np, 0))) return;
+        GLB_AS int32_t *o = d.dlog + d.dlog_n;
+        if (lane() == 0) {
+            o[0] = (marker ? 1 : 0) | (pr ? 2 : 0);
+            if (marker) o[1] = (int32_t)ref_type;
+            o[1 + words] = np;
+        }
+        if (!marker && tot > 0) {
+            gsync_rd();
+            const GLB_AS uint16_t *tb = text_base(d, d.text_half);
+            for (int w = lane(); w < words; w += MT_WAVE) {
+                uint32_t u[2] = {0u, 0u};
+                for (int h = 0; h < 2; h++) {
+                    int t = 2 * w + h, pre = 0;
+                    for (int q = 0; q < tp.np; q++) {
+                        if (t >= pre && t < pre + tp.len[q]) u[h] = tb[tp.off[q] + (t - pre)];
+                        pre += tp.len[q];
+                    }
+                }
+                o[1 + w] = (int32_t)(u[0] | (u[1] << 16));
+            }
+        }
+        for (int q = lane(); q < 2 * np; q += MT_WAVE) o[2 + words + q] = (int32_t)pr[1 + q];
+        d.dlog_n += 2 + words + 2 * max(np, 0);
+    }
+}
+TD void cb_log_seg(DocT<T> &d, v4i a, v4u b) {
+    if constexpr (T::kLog) {
+        if (!d.rich) return;
+        TextPieces tp;
+        tp.np = 1;
+        tp.off[0] = b.x;
+        tp.len[0] = a.x;
+        cb_log_state(d, (b.z & MT_MARKER_BIT) != 0, b.x, tp, b.y ? prec(d, d.props_half, b.y) : nullptr);
+    }
+}
+// a maintenance record of one or two segments
+TD void cb_maint(DocT<T> &d, int kind, int len0, bool mk0, uint32_t ref0, const TextPieces &t0, uint32_t ph0,
+                 int len1, const TextPieces *t1, uint32_t ph1) {
+    if constexpr (T::kLog) {
+        if (!d.rich || !d.dlog) return;
+        Cb cb = cb_begin(d, d.cur_seq, kind);
+        cb_log(d, len0);
+        cb_log_state(d, mk0, ref0, t0, ph0 ? prec(d, d.props_half, ph0) : nullptr);
+        cb.n = 1;
+        if (t1) {
+            cb_log(d, len1);
+            cb_log_state(d, false, 0u, *t1, ph1 ? prec(d, d.props_half, ph1) : nullptr);
+            cb.n = 2;
+        }
+        // maintenance events are not part of the delta hash (the hash pins the delta callbacks)
+        if (d.dlog && d.dlog_rec >= 0 && lane() == 0) d.dlog[d.dlog_rec + 2] = cb.n;
+        d.dlog_rec = -1;
+    }
+}
+
 // ------------------------------------------------------------------ splitting
 // BaseSegment.splitAt :523-567 (right half inserted right after the left half in the same
 // leaf block, which may then split).  Property records are immutable, so both halves share.
@@ -1047,6 +1106,19 @@ TD void split_seg(DocT<T> &d, int i, int q) {
     seg_move_right(d, i + 1, 1);
     mark_dirty(d, i);
     if (T::kLog) d.m_split++;   // splitLeafSegment's SPLIT event :2264-2269
+    if constexpr (T::kLog) {   // SPLIT [left, right] (splitLeafSegment :2260-2272), rich log
+        if (d.rich) {
+            const v4i a0 = uni4(d.A[i]);
+            const v4u b0 = uni4(d.Bv[i]);
+            TextPieces l, rt;
+            l.np = rt.np = 1;
+            l.off[0] = b0.x;
+            l.len[0] = q;
+            rt.off[0] = b0.x + (uint32_t)q;
+            rt.len[0] = a0.x - q;
+            cb_maint(d, -2, q, false, 0u, l, b0.y, a0.x - q, &rt, b0.y);
+        }
+    }
     if (lane() == 0) {
         v4i a = d.A[i];
         v4u bb = d.Bv[i];
@@ -1132,6 +1204,41 @@ __device__ __forceinline__ bool can_append(int plen, bool pmarker, bool p_nl, in
     return plen <= MT_GRAN || slen <= MT_GRAN;
 }
 
+// Rich delta log: scourNode's UNLINK / APPEND events (MT/mergeTree.ts:1343-1373) of a scour,
+// in child order, before any text moves.  Lane j holds entry j (a: lengths, b: text offset /
+// marker refType, props); m_app: entries appended to the run before them, whose keeper is
+// the nearest kept entry below (m_keep).
+TD void scour_events(DocT<T> &d, v4i a, v4u b, u64 m_unlink, u64 m_app, u64 m_keep) {
+    if constexpr (T::kLog) {
+        if (!d.rich) return;
+        for (u64 ev = m_unlink | m_app; ev; ev &= ev - 1) {
+            const int j = first_lane(ev);
+            const int lj = bcast(a.x, j);
+            TextPieces tj;
+            tj.np = 1;
+            tj.off[0] = (uint32_t)bcast((int)b.x, j);
+            tj.len[0] = lj;
+            const uint32_t pj = (uint32_t)bcast((int)b.y, j);
+            if ((m_app >> j) & 1ull) {
+                const int kk = 63 - __clzll((long long)(m_keep & ((1ull << j) - 1ull)));
+                TextPieces tk;
+                tk.np = 0;
+                int tot = 0;
+                for (int q = kk; q <= j && tk.np < 8; q++) {
+                    tk.off[tk.np] = (uint32_t)bcast((int)b.x, q);
+                    tk.len[tk.np] = bcast(a.x, q);
+                    tot += tk.len[tk.np];
+                    tk.np++;
+                }
+                cb_maint(d, -1, tot, false, 0u, tk, (uint32_t)bcast((int)b.y, kk), lj, &tj, pj);
+            } else {
+                const bool mk = (bcast((int)b.z, j) & MT_MARKER_BIT) != 0;
+                cb_maint(d, -3, lj, mk, tj.off[0], tj, pj, 0, (const TextPieces *)nullptr, 0u);
+            }
+        }
+    }
+}
+
 // scourNode :1322-1398 over leaf block [s, e); compacts the table.  Returns survivors.
 #ifdef MT_PROF
 TD int scour_block_impl(DocT<T> &d, int s, int e);
@@ -1172,7 +1279,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     // another index = appended to that keeper, 0xF = unlinked
     uint32_t owners = 0;
     int prev = -1, plen = 0;
-    bool pmark = false, pnl = false;
+    bool pmark = false, pnl = false, pnm = false;
     uint32_t pprops = 0;
     for (int j = 0; j < cntb; j++) {
         uint32_t own = (uint32_t)j;
@@ -1185,8 +1292,9 @@ TD int scour_block(DocT<T> &d, int s, int e) {
             const int lj = bcast(a.x, j);
             const bool mk = (m_mark >> j) & 1ull, nl = (m_nl >> j) & 1ull;
             const uint32_t pj = (uint32_t)bcast((int)b.y, j);
+            const bool nmj = (bcast((int)b.w, j) & SEGF_NOMATCH) != 0;
             const bool ok = prev >= 0 && lj > 0 && can_append(plen, pmark, pnl, lj, mk) &&
-                            match_props(d, pprops, pj);
+                            match_props(d, pprops, pj, pnm || nmj);
             if (ok) {
                 own = (uint32_t)prev;
                 plen += lj;
@@ -1197,6 +1305,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
                 pmark = mk;
                 pnl = !mk && lj > 0 && nl;
                 pprops = pj;
+                pnm = nmj;
             }
         }
         owners |= own << (4 * j);
@@ -1204,6 +1313,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     const uint32_t myown = in ? (owners >> (4 * k)) & 0xFu : 0xFu;
     const u64 m_keep = ballot(in && myown == (uint32_t)k);
     const u64 m_app = ballot(in && myown != 0xFu && myown != (uint32_t)k);
+    scour_events(d, a, b, m_unlink, m_app, m_keep);
     if (T::kLog) {   // scourNode's UNLINK / APPEND events :1343-1373
         d.m_unlink += __popcll(m_unlink);
         d.m_append += __popcll(m_app);
@@ -1382,8 +1492,14 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     const bool pc = k > 0 && ((m_cand >> (k - 1)) & 1ull);
     const bool pm = k > 0 && ((m_mark >> (k - 1)) & 1ull);
     const bool pn = k > 0 && ((m_nl >> (k - 1)) & 1ull);
+#ifdef MT_NO_Q4
+    const u64 m_nm = 0;
+#else
+    const u64 m_nm = ballot(in && (b.w & SEGF_NOMATCH) != 0);
+#endif
+    const bool nm = ((m_nm >> k) & 1ull) || (k > 0 && ((m_nm >> (k - 1)) & 1ull));
     bool join = cand && pc && k != start && !marker && !pm && !pn && a.x > 0;
-    if (join && pprops != b.y) join = match_props(d, pprops, b.y);
+    if (join && (nm || pprops != b.y)) join = match_props(d, pprops, b.y, nm);
     const u64 m_join = ballot(join);
     if (!serial && ballot(join && a.x > MT_GRAN)) serial = true;
     if (serial) {   // rare: per-block serial plan (scour_block)
@@ -1407,6 +1523,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         d.m_append += __popcll(m_join);
     }
     const u64 m_surv = ballot(surv);
+    scour_events(d, a, b, ballot(unlink), m_join, m_surv);
     const u64 above = (k < 63) ? (m_join >> (k + 1)) : 0ull;
     const u64 m_grp = ballot(surv && (above & 1ull));
     P2_T0(10)
@@ -1748,6 +1865,28 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         cb.n = 1;
         cb_log(d, -1);
         cb_log(d, 0);
+        if constexpr (T::kLog) {   // rich: the (never linked) empty segment, props nulls dropped
+            if (d.rich && cb_room(d, 2 + (op.props != MT_NO_PROPS ? 2 * (int)(pin[op.props] & 0xFFFF) : 0))) {
+                int np = -1;
+                if (op.props != MT_NO_PROPS) {
+                    const GLB_AS uint32_t *rec = pin + op.props;
+                    np = 0;
+                    for (uint32_t j = 0; j < (rec[0] & 0xFFFF); j++) {
+                        if (rec[2 + 2 * j] == MT_VAL_NULL) continue;
+                        if (lane() == 0) {
+                            d.dlog[d.dlog_n + 2 + 2 * np] = (int32_t)rec[1 + 2 * j];
+                            d.dlog[d.dlog_n + 3 + 2 * np] = (int32_t)rec[2 + 2 * j];
+                        }
+                        np++;
+                    }
+                }
+                if (lane() == 0) {
+                    d.dlog[d.dlog_n] = np >= 0 ? 2 : 0;
+                    d.dlog[d.dlog_n + 1] = np;
+                }
+                d.dlog_n += 2 + 2 * max(np, 0);
+            }
+        }
         cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)-1), 0u));
         cb_end(d, cb);
         // zamboni runs in apply_op (single inlined site)
@@ -1761,7 +1900,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         fail_cap(d, 1);
         return;
     }
-    uint32_t ph = 0;
+    uint32_t ph = 0, nomatch = 0;
     if (op.props != MT_NO_PROPS) {
         ph = (uint32_t)d.props_top;
         d.props_top++;
@@ -1784,6 +1923,14 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
             }
             t[0] = n;
         }
+#ifndef MT_NO_Q4
+        bool nm = false;
+        for (uint32_t j = 0; j < cntk; j++) {
+            const uint32_t v = rec[2 + 2 * j];
+            nm = nm || (v != MT_VAL_NULL && (v & MT_VAL_NOMATCH_BIT));
+        }
+        if (nm) nomatch = SEGF_NOMATCH;
+#endif
     }
     int bstart;
     const int B = blk_find(d, 0, ip, false, bstart);
@@ -1815,7 +1962,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     if (lane() == 0) {
         d.A[x] = v4i{slen, seq, MT_RSEQ_NONE, pack_cli(c, 0)};
         d.O[x] = 0ull;
-        d.Bv[x] = v4u{toff, ph, uid | (marker ? MT_MARKER_BIT : 0u), segw};
+        d.Bv[x] = v4u{toff, ph, uid | (marker ? MT_MARKER_BIT : 0u), segw | nomatch};
     }
     d.next_uid++;
     d.n++;
@@ -1837,6 +1984,12 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     cb.n = 1;
     cb_log(d, pos);
     cb_log(d, slen);
+    if constexpr (T::kLog) {
+        if (d.rich) {
+            wsync<T>();
+            cb_log_seg(d, uni4(d.A[x]), uni4(d.Bv[x]));
+        }
+    }
     cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)pos), (uint32_t)slen));
     cb_end(d, cb);
     // zamboni runs in apply_op (single inlined site)
@@ -1846,7 +1999,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
 // one lane to its segment: writes the new record nh, returns the seg hash contribution of
 // the propertyDeltas (and logs them when `logp` is set).  Returns false on key overflow.
 TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint32_t *rec, u64 &sh,
-                        GLB_AS int32_t *logp, int &nlog) {
+                        GLB_AS int32_t *logp, int &nlog, bool *nomatch = nullptr) {
     const uint32_t cntk = rec[0] & 0xFFFF, comb = rec[0] >> 16;
     const GLB_AS uint32_t *o = oh ? prec(d, d.props_half, oh) : nullptr;
     GLB_AS uint32_t *t = prec(d, d.props_half, nh);
@@ -1889,8 +2042,10 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
             for (uint32_t i = 0; i < on; i++)
                 if (o[1 + 2 * i] == k) deleted_by_rewrite = true;
         }
+        // a key set to undefined reads as absent: deltas[key] = previousValue ?? null
+        const bool absent = idx < 0 || t[2 + 2 * idx] == MT_VAL_UNDEF;
         if (!deleted_by_rewrite) {
-            const uint32_t dv = idx >= 0 ? t[2 + 2 * idx] : MT_VAL_NULL;
+            const uint32_t dv = absent ? MT_VAL_NULL : t[2 + 2 * idx];
             sh = fnv_u32(fnv_u32(sh, k), dv);
             if (logp) {
                 logp[nlog++] = (int32_t)k;
@@ -1898,7 +2053,26 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
             }
             npd++;
         }
-        if (v == MT_VAL_NULL) {
+        uint32_t nv = v;
+#ifndef MT_NO_Q4
+        if (comb == MT_COMBINE_TABLE) {
+            // newValue = combine(op, previousValue, undefined, seq) (:93-99): the
+            // host tabulated it for every value that can be present
+            const GLB_AS uint32_t *tab = rec + 1 + 2 * cntk;
+            nv = tab[1];
+            if (!absent) {
+                const uint32_t old = t[2 + 2 * idx];
+                bool hit = false;
+                for (uint32_t q = 0; q < tab[0]; q++)
+                    if (tab[2 + 2 * q] == old) {
+                        nv = tab[3 + 2 * q];
+                        hit = true;
+                    }
+                if (!hit) return false;
+            }
+        }
+#endif
+        if (nv == MT_VAL_NULL) {
             if (idx >= 0) {
                 for (uint32_t q = (uint32_t)idx + 1; q < n; q++) {
                     t[2 * q - 1] = t[2 * q + 1];
@@ -1907,16 +2081,22 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
                 n--;
             }
         } else if (idx >= 0) {
-            t[2 + 2 * idx] = v;
+            t[2 + 2 * idx] = nv;
         } else {
             if (n >= MT_KMAX) return false;
             t[1 + 2 * n] = k;
-            t[2 + 2 * n] = v;
+            t[2 + 2 * n] = nv;
             n++;
         }
     }
     t[0] = n;
     sh = fnv_u32(sh, (uint32_t)npd);
+    // *nomatch in: the new set can hold a NaN / undefined value at all; out: it does
+    if (nomatch && *nomatch) {
+        bool nm = false;
+        for (uint32_t q = 0; q < n; q++) nm = nm || (t[2 + 2 * q] & MT_VAL_NOMATCH_BIT) != 0;
+        *nomatch = nm;
+    }
     return true;
 }
 
@@ -1933,6 +2113,17 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
     int last_b = -1;
     const int L = lane();
     const int nblk = nbr(d, 0);
+    // can this op leave a NaN / undefined value in a set?
+    bool rec_nm = false;
+#ifndef MT_NO_Q4
+    if (!rem) {
+        rec_nm = (rec[0] >> 16) == MT_COMBINE_TABLE;
+        for (uint32_t j = 0; j < (rec[0] & 0xFFFFu); j++) {
+            const uint32_t v = rec[2 + 2 * j];
+            rec_nm = rec_nm || (v != MT_VAL_NULL && (v & MT_VAL_NOMATCH_BIT));
+        }
+    }
+#endif
     for (int base = 0; base < d.n; base += MT_WAVE) {
         if (!rem && !props_ensure(d, MT_WAVE)) return true;
         const int i = base + L;
@@ -1973,8 +2164,12 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         u64 sh = fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)opos), (uint32_t)a.x);
         if (!rem && sel) {
             int unused = 0;
-            if (!annotate_record(d, bv.y, nh, rec, sh, (GLB_AS int32_t *)nullptr, unused)) bad = true;
-            d.Bv[i].y = nh;
+            bool nm = rec_nm || (bv.w & SEGF_NOMATCH) != 0;
+            if (!annotate_record(d, bv.y, nh, rec, sh, (GLB_AS int32_t *)nullptr, unused, &nm)) bad = true;
+            v4u nb = bv;
+            nb.y = nh;
+            nb.w = (bv.w & ~SEGF_NOMATCH) | (nm ? SEGF_NOMATCH : 0u);
+            d.Bv[i] = nb;
         }
         if (ballot(bad)) {
             fail(d, MT_DOC_CAPACITY);
@@ -2014,6 +2209,13 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                         nl = bcast(nl, 0);
                         d.dlog_n += 1 + nl;
                     }
+                }
+                if (d.rich) {   // the segment after the op (annotate: its new property set)
+                    const v4i aj = v4i{bcast(a.x, j), bcast(a.y, j), bcast(a.z, j), bcast(a.w, j)};
+                    v4u bj = v4u{(uint32_t)bcast((int)bv.x, j), (uint32_t)bcast((int)bv.y, j),
+                                 (uint32_t)bcast((int)bv.z, j), (uint32_t)bcast((int)bv.w, j)};
+                    if (!rem) bj.y = (uint32_t)bcast((int)nh, j);
+                    cb_log_seg(d, aj, bj);
                 }
             }
         }
@@ -2106,11 +2308,14 @@ TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const G
         // SnapshotLoader.loadBody (MT/snapshotLoader.ts:195-227): insertSegments at
         // root.cachedLength in view (client, refSeq 0), no callback, no seq/msn update.  Its
         // zamboniSegments has nothing to do: the heap is new (startCollaboration) and body
-        // segments are never newer than currentSeq (addToLRUSet :1312).
+        // segments are never newer than currentSeq (addToLRUSet :1312).  No events.
+        const int rich = d.rich;
+        d.rich = 0;
         if (op.kind == MT_OP_INSERT)
             op_insert(d, in, tin, pin);
         else if (op.kind == MT_OP_LOAD_REMOVED)
             load_removed(d, op);
+        d.rich = rich;
         return;
     }
     const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;

@@ -426,6 +426,9 @@ TD void pg_win_flush(PagedDoc<T> &pd) {
 TD void pg_win_flush_impl(PagedDoc<T> &pd) {
     DocT<T> &w = pd.w;
     if (pd.cur < 0 || !pd.dirty) return;
+#ifdef MT_NO_DIRTY
+    w.dlo = 0;
+#endif
     if (w.dlo < w.n) {   // some slot changed: its table entries and the slots from dlo on
         pg_table_purge(pd, pd.cur);
         pg_table_add(pd, 0, w.n, pd.cur);
@@ -499,7 +502,9 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
         if (i == 0) pd.pvl[cur] += dlt;
     }
     wsync<T>();
+#ifndef MT_VIEWS_TOTAL
     if (!total) return 0;
+#endif
     for (int base = 0; base < np; base += MT_WAVE) {
         const int q = base + lane();
         tot += q < np ? pd.pvl[pd.up.dir[q]] : 0;
@@ -993,11 +998,14 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
         pg_renumber(pd);
         if (w.status) return;
     }
-    if (op.flags & MT_F_LOAD) {   // summary body append (apply_op)
+    if (op.flags & MT_F_LOAD) {   // summary body append (apply_op); no events
+        const int rich = w.rich;
+        w.rich = 0;
         if (op.kind == MT_OP_INSERT)
             pg_op_insert(pd, in, tin, pin);
         else if (op.kind == MT_OP_LOAD_REMOVED)
             pg_load_removed(pd, op);
+        w.rich = rich;
         return;
     }
     const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
@@ -1072,7 +1080,7 @@ TD bool paged_text_ensure(DocT<T> &w, int need) {
             a = w.A[i];
             b = w.Bv[i];
         }
-        const bool live = v && a.z == MT_RSEQ_NONE && !(b.z & MT_MARKER_BIT);
+        const bool live = v && (a.z == MT_RSEQ_NONE || (T::kLog && w.rich)) && !(b.z & MT_MARKER_BIT);
         const int len = live ? a.x : 0;
         const int inc = wave_scan_incl(len);
         const int off = carry + inc - len;
@@ -1183,6 +1191,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.T_cap = st.T;
     w.P_cap = st.P;
     w.DL_cap = st.DL;
+    w.rich = st.DLR;
     w.S_cap = MT_PG_SLOTS;
     w.B_cap = PW_B;
     w.H_cap = pc.PH;

@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
             status = MT_DOC_CAPACITY;
             break;
         }
-        bool bad = false;
+        bool bad = false, nm = false;
         if (hp) {   // TextSegment.make / Marker.make(props): keys with null dropped (Q5)
             const uint32_t *rec = pin + r.props;
             const uint32_t cnt = rec[0] & 0xFFFF;
@@ -104,6 +104,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
                 }
                 t[1 + 2 * k] = rec[1 + 2 * j];
                 t[2 + 2 * k] = rec[2 + 2 * j];
+                nm = nm || (rec[2 + 2 * j] & MT_VAL_NOMATCH_BIT) != 0;
                 k++;
             }
             t[0] = k;
@@ -123,6 +124,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
             const bool rem = r.removed_seq != MT_RSEQ_NONE;
             uint32_t w = 0;
             if (tl > 0) w = SEGF_NL_KNOWN | (tin[r.payload + tl - 1] == '\n' ? SEGF_NL : 0u);
+            if (nm) w |= SEGF_NOMATCH;
             st.segA[doc * S + i] = v4i{r.len, r.seq, r.removed_seq, pack_cli(r.client, rem ? r.removed_client : 0)};
             st.segO[doc * S + i] = 0ull;
             st.segB[doc * S + i] = v4u{marker ? r.payload : (uint32_t)toff, hp ? (uint32_t)ph : 0u,
@@ -814,8 +816,12 @@ __device__ static SegRanges seg_ranges(const DevState &st, int doc, const DocHdr
 // per-segment decisions are uniform, text copies are wave-wide.
 __device__ static bool props_equal_set(const uint32_t *pr, uint32_t ha, uint32_t hb) {
     if (ha == 0 || hb == 0) return ha == hb;
-    if (ha == hb) return true;
     const uint32_t *a = pr + (size_t)ha * MT_PREC, *b = pr + (size_t)hb * MT_PREC;
+    for (uint32_t i = 0; i < a[0]; i++)   // NaN / undefined values never match
+        if (a[2 + 2 * i] & MT_VAL_NOMATCH_BIT) return false;
+    for (uint32_t j = 0; j < b[0]; j++)
+        if (b[2 + 2 * j] & MT_VAL_NOMATCH_BIT) return false;
+    if (ha == hb) return true;
     if (a[0] != b[0]) return false;
     for (uint32_t i = 0; i < a[0]; i++) {
         bool ok = false;
@@ -1047,7 +1053,12 @@ static bool props_rec_ok(const uint32_t *props, uint64_t props_len, uint32_t off
     if (off == MT_NO_PROPS) return true;
     if ((uint64_t)off >= props_len) return false;
     const uint64_t cnt = props[off] & 0xFFFFu;
-    return (uint64_t)off + 1 + 2 * cnt <= props_len;
+    uint64_t end = (uint64_t)off + 1 + 2 * cnt;
+    if ((props[off] >> 16) == MT_COMBINE_TABLE) {   // + [n, absent, (old, new) x n]
+        if (end + 2 > props_len) return false;
+        end += 2 + 2 * (uint64_t)props[end];
+    }
+    return end <= props_len;
 }
 // Host-side bounds check of a batch (MT_E_INVALID instead of a device fault): per-document
 // offsets monotonic inside [0, n_ops], every insert payload inside the text arena, every
@@ -1097,6 +1108,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.T = o.text_capacity > 0 ? o.text_capacity : 32768;
     st.P = o.props_capacity > 0 ? o.props_capacity : st.S + 2 * MT_WAVE;
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
+    st.DLR = st.DL > 0 && o.delta_log_mode == 1 ? 1 : 0;
     if (const char *e = getenv("MT_WPG")) h->wpg = atoi(e) == 1 ? 1 : 2;
     if (o.lds_seg_capacity >= 0) {
         int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 192;

@@ -102,12 +102,13 @@ napi_value Create(napi_env env, napi_callback_info info) {
     const char *names[] = {"device", "segCapacity", "blockCapacity", "heapCapacity", "textCapacity",
                            "propsCapacity", "deltaLogCapacity", "ldsSegCapacity", "pageCapacity",
                            "pageHeapCapacity", "unsettledCapacity", "uidCapacity", "ldsPageCapacity",
-                           "ldsUnsettledCapacity", "ldsPageHeapCapacity", "ldsNarrowOverlap"};
+                           "ldsUnsettledCapacity", "ldsPageHeapCapacity", "ldsNarrowOverlap", "deltaLogMode"};
     int32_t *fields[] = {&o.device, &o.seg_capacity, &o.block_capacity, &o.heap_capacity, &o.text_capacity,
                          &o.props_capacity, &o.delta_log_capacity, &o.lds_seg_capacity, &o.page_capacity,
                          &o.page_heap_capacity, &o.unsettled_capacity, &o.uid_capacity, &o.lds_page_capacity,
-                         &o.lds_unsettled_capacity, &o.lds_page_heap_capacity, &o.lds_narrow_overlap};
-    for (int i = 0; i < 16; i++) {
+                         &o.lds_unsettled_capacity, &o.lds_page_heap_capacity, &o.lds_narrow_overlap,
+                         &o.delta_log_mode};
+    for (int i = 0; i < 17; i++) {
         bool has = false;
         napi_has_named_property(env, argv[1], names[i], &has);
         if (has) {

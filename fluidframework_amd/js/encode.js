@@ -22,17 +22,55 @@ const F_GROUP_MORE = 1;
 const F_MARKER = 2;
 const NO_PROPS = 0xFFFFFFFF;
 const VAL_NULL = 0xFFFFFFFF;
+const VAL_UNDEF = 0xFFFFFFFE;       // a key set to the JS value undefined
 const VAL_FALSY_BIT = 0x80000000;
+const VAL_NOMATCH_BIT = 0x40000000; // matchProperties never finds the value equal
 const COMBINE_NONE = 0;
 const COMBINE_REWRITE = 1;
 const COMBINE_OTHER = 2;
+const COMBINE_TABLE = 3;
 const OP_BYTES = 32;
 
-/** Canonical JSON (sorted keys): matchProperties compares nested values structurally. */
+/**
+ * Canonical JSON (sorted keys): matchProperties compares nested values structurally.  NaN and
+ * undefined -- left in property sets by non-rewrite combining ops (SURVEY Q4) -- get tokens
+ * of their own.
+ */
 function canonical(v) {
+    if (v === undefined) { return "undefined"; }
+    if (typeof v === "number" && Number.isNaN(v)) { return "NaN"; }
     if (v === null || typeof v !== "object") { return JSON.stringify(v); }
     if (Array.isArray(v)) { return `[${v.map(canonical).join(",")}]`; }
     return `{${Object.keys(v).sort().map((k) => `${JSON.stringify(k)}:${canonical(v[k])}`).join(",")}}`;
+}
+
+/** matchProperties(a, a) is false for a set holding v (NaN, or undefined at any depth). */
+function noMatch(v) {
+    if (v === undefined || (typeof v === "number" && Number.isNaN(v))) { return true; }
+    if (v !== null && typeof v === "object") { return Object.keys(v).some((k) => noMatch(v[k])); }
+    return false;
+}
+
+class Unsupported extends Error {}
+
+/**
+ * Properties.combine(op, currentValue, undefined, seq) (merge-tree/src/properties.ts:26-59) as
+ * SegmentPropertiesManager.addProperties calls it for a non-rewrite combining op
+ * (segmentPropertiesManager.ts:93-107: the new value is never passed in; SURVEY Q4).
+ */
+function jsCombine(op, cur, seq) {
+    if (cur === undefined) { cur = op.defaultValue; }
+    if (op.name === "incr") {
+        if (op.minValue && typeof op.minValue !== "number") { throw new Unsupported("incr with a non-numeric minValue"); }
+        return cur + undefined;   // NaN, or a string; never below a numeric minValue
+    }
+    if (op.name === "consensus") {
+        if (cur === undefined) { return { value: undefined, seq }; }
+        if (cur === null) { throw new Unsupported("consensus over null"); }
+        if (typeof cur === "object" && cur.seq === -1) { throw new Unsupported("consensus over a shared {seq: -1}"); }
+        return cur;
+    }
+    return cur;
 }
 
 class Interner {
@@ -52,7 +90,8 @@ class Interner {
         return i;
     }
     val(v) {
-        if (v === null || v === undefined) { return VAL_NULL; }
+        if (v === null) { return VAL_NULL; }
+        if (v === undefined) { return VAL_UNDEF; }
         const c = canonical(v);
         let i = this.valIds.get(c);
         if (i === undefined) {
@@ -60,10 +99,14 @@ class Interner {
             this.valIds.set(c, i);
             this.vals.push(v);
         }
-        return (i | (v ? 0 : VAL_FALSY_BIT)) >>> 0;
+        return (i | (v ? 0 : VAL_FALSY_BIT) | (noMatch(v) ? VAL_NOMATCH_BIT : 0)) >>> 0;
     }
     keyName(id) { return this.keys[id]; }
-    value(id) { return id === VAL_NULL ? null : this.vals[(id & ~VAL_FALSY_BIT) >>> 0]; }
+    value(id) {
+        if (id === VAL_NULL) { return null; }
+        if (id === VAL_UNDEF) { return undefined; }
+        return this.vals[(id & ~(VAL_FALSY_BIT | VAL_NOMATCH_BIT)) >>> 0];
+    }
 }
 
 /** Growable typed-array builder. */
@@ -114,6 +157,29 @@ class BatchEncoder {
             this.props.push(this.interner.key(k));
             this.props.push(this.interner.val(p[k]));
         }
+        return off;
+    }
+
+    /**
+     * A non-rewrite combining op's record (SURVEY Q4): the keys, then combine(op, old,
+     * undefined, seq) for every value a key can hold now -- [n, new value of an absent key,
+     * (old, new) x n]; VAL_NULL deletes.  Mirrors wire.py Batch._combine_rec.
+     */
+    _combineProps(p, comb, seq) {
+        const it = this.interner;
+        let absent;
+        const pairs = [];
+        try {
+            absent = it.val(jsCombine(comb, undefined, seq));
+            for (const v of it.vals.slice()) { pairs.push([it.val(v), it.val(jsCombine(comb, v, seq))]); }
+        } catch (e) {
+            if (!(e instanceof Unsupported)) { throw e; }
+            return this._props(p, COMBINE_OTHER);
+        }
+        const off = this._props(p, COMBINE_TABLE);
+        this.props.push(pairs.length);
+        this.props.push(absent);
+        for (const [o, n] of pairs) { this.props.push(o); this.props.push(n); }
         return off;
     }
 
@@ -169,8 +235,11 @@ class BatchEncoder {
             r.pos2 = op.pos2;
             if (op.type === OP_ANNOTATE) {
                 const c = op.combiningOp;
-                const code = !c ? COMBINE_NONE : (c.name === "rewrite" ? COMBINE_REWRITE : COMBINE_OTHER);
-                r.props = this._props(op.props, code);
+                if (c && c.name !== "rewrite") {
+                    r.props = this._combineProps(op.props, c, msg.sequenceNumber);
+                } else {
+                    r.props = this._props(op.props, c ? COMBINE_REWRITE : COMBINE_NONE);
+                }
             }
         } else {
             throw new Error(`unsupported op type ${op.type}`);
@@ -222,5 +291,6 @@ class BatchEncoder {
 
 module.exports = {
     BatchEncoder, Interner, Grow, canonical,
-    OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_GROUP_MORE, F_MARKER, NO_PROPS, VAL_NULL, VAL_FALSY_BIT,
+    OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_GROUP_MORE, F_MARKER, NO_PROPS, VAL_NULL, VAL_UNDEF, VAL_FALSY_BIT,
+    VAL_NOMATCH_BIT, jsCombine,
 };

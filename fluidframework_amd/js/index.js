@@ -50,6 +50,12 @@ class GpuMergeTreeBatch {
      * @param {object} options  mt_options: device, segCapacity, textCapacity, deltaLogCapacity, ...
      */
     constructor(nDocs, options = {}) {
+        // the facade reads the rich delta log: callback segments carry their state, and the
+        // maintenance events are records of their own (mt_options.delta_log_mode 1)
+        if (options.deltaLogCapacity && options.deltaLogMode === undefined) {
+            options = Object.assign({}, options, { deltaLogMode: 1 });
+        }
+        this.rich = !!options.deltaLogCapacity && options.deltaLogMode === 1;
         this.h = native.create(nDocs, options);
         this.nDocs = nDocs;
         this.interner = new Interner();
@@ -121,10 +127,11 @@ class GpuMergeTreeBatch {
     flush() {
         if (this.queued === 0) { return; }
         const enc = new BatchEncoder(this.interner);
+        this.applied = this.pending;   // the messages of this flush, for the callbacks' opArgs
         for (let d = 0; d < this.nDocs; d++) {
             enc.addDoc(this.pending[d], this.clients[d]);
-            this.pending[d] = [];
         }
+        this.pending = Array.from({ length: this.nDocs }, () => []);
         this.queued = 0;
         const a = enc.arrays();
         native.applyOps(this.h, a.docOff, a.ops, a.text, a.props);
@@ -176,6 +183,7 @@ class GpuClient {
         this.longClientId = undefined;
         this.currentSeq = 0;
         this.mergeTreeDeltaCallback = undefined;
+        this.mergeTreeMaintenanceCallback = undefined;
     }
 
     _check() {
@@ -245,24 +253,57 @@ class GpuClient {
         return { split: m[3 * this.doc], append: m[3 * this.doc + 1], unlink: m[3 * this.doc + 2] };
     }
 
+    /** A segment's state at an event (rich log), as the ISegment fields listeners read. */
+    _segment(log, i, len) {
+        const flags = log[i++];
+        let seg;
+        if (flags & 1) {
+            seg = { type: "Marker", refType: log[i++], cachedLength: len };
+        } else {
+            const words = (len + 1) >> 1;
+            const units = new Array(len);
+            for (let u = 0; u < len; u++) { const w = log[i + (u >> 1)]; units[u] = (u & 1) ? (w >>> 16) : (w & 0xFFFF); }
+            i += words;
+            seg = { type: "TextSegment", text: String.fromCharCode(...units), cachedLength: len };
+        }
+        const np = log[i++];
+        if (np >= 0) {
+            const pairs = [];
+            for (let j = 0; j < np; j++) {
+                pairs.push([this.batch.interner.keyName(log[i]), this.batch.interner.value(log[i + 1] >>> 0)]);
+                i += 2;
+            }
+            seg.properties = {};
+            for (const [k, v] of jsKeyOrder(pairs)) { seg.properties[k] = v; }
+        }
+        return [seg, i];
+    }
+
     /**
-     * Replays the device delta log into mergeTreeDeltaCallback(opArgs, deltaArgs) calls
-     * (mergeTreeDeltaCallback.ts:33-41): one per op, deltaSegments carrying the segment's
-     * cachedLength, its observer position at callback time (what SequenceDeltaEvent.ranges
-     * reads through getPosition) and, for annotate, the propertyDeltas.
+     * Replays the device delta log of the last flush into the reference's callbacks:
+     * mergeTreeDeltaCallback(opArgs, {operation, deltaSegments}) (mergeTreeDeltaCallback.ts:
+     * 33-59; call sites mergeTree.ts:2014-2021, 2625-2632, 2738-2745) with opArgs {op,
+     * sequencedMessage, groupOp} and deltaSegments [{segment, propertyDeltas}] -- segment =
+     * the segment's state at the event (cachedLength, text or refType, properties) plus its
+     * observer `position` at callback time (what SequenceDeltaEvent.ranges reads) -- and
+     * mergeTreeMaintenanceCallback({operation: SPLIT -2 | APPEND -1 | UNLINK -3,
+     * deltaSegments}) (mergeTree.ts:1343-1373, 2264-2269), in the reference's order.
      */
     _emitDeltas() {
-        const cb = this.mergeTreeDeltaCallback;
+        const cb = this.mergeTreeDeltaCallback, mcb = this.mergeTreeMaintenanceCallback;
+        const rich = this.batch.rich;
         const log = native.getDeltaLog(this.batch.h, this.doc);
+        const msgs = (this.batch.applied && this.batch.applied[this.doc]) || [];
+        let mi = 0, member = 0, lastSeq = null;
         let i = this.batch.logPos[this.doc];
         while (i + 3 <= log.length) {
             const seq = log[i], kind = log[i + 1], n = log[i + 2];
             i += 3;
             const deltaSegments = [];
             for (let s = 0; s < n; s++) {
-                const pos = log[i], len = log[i + 1];
-                i += 2;
-                const delta = { segment: { cachedLength: len }, position: pos };
+                const pos = kind >= 0 ? log[i++] : -1;
+                const len = log[i++];
+                let delta;
                 if (kind === 2) {
                     const npd = log[i++];
                     const pd = [];
@@ -270,16 +311,54 @@ class GpuClient {
                         pd.push([this.batch.interner.keyName(log[i]), this.batch.interner.value(log[i + 1] >>> 0)]);
                         i += 2;
                     }
-                    delta.propertyDeltas = {};
-                    for (const [k, v] of pd) { delta.propertyDeltas[k] = v === undefined ? null : v; }
+                    delta = { propertyDeltas: {} };
+                    // (a rewrite-deleted key set to undefined reports undefined, as the reference)
+                    for (const [k, v] of pd) { delta.propertyDeltas[k] = v; }
+                } else {
+                    delta = {};
                 }
-                // a zero-length insert's segment is never linked (blockInsert skips it,
-                // mergeTree.ts:2229) but is still in the callback: position -1
+                let segment = { cachedLength: len };
+                if (rich) { [segment, i] = this._segment(log, i, len); }
+                delta.segment = segment;
+                if (kind >= 0) {
+                    // a zero-length insert's segment is never linked (blockInsert skips it,
+                    // mergeTree.ts:2229) but is still in the callback: position -1
+                    delta.position = pos;
+                }
                 deltaSegments.push(delta);
             }
-            if (cb) { cb({ sequencedMessage: { sequenceNumber: seq } }, { operation: kind, deltaSegments }); }
+            if (kind < 0) {
+                if (mcb) { mcb({ operation: kind, deltaSegments }); }
+                continue;
+            }
+            // opArgs: the message with this sequence number; a GROUP's members in order
+            if (seq !== lastSeq) { member = 0; lastSeq = seq; } else { member++; }
+            while (mi < msgs.length && msgs[mi].sequenceNumber !== seq) { mi++; }
+            const msg = mi < msgs.length ? msgs[mi] : { sequenceNumber: seq };
+            const contents = msg.contents;
+            const isGroup = contents && contents.type === 3;
+            const opArgs = { op: isGroup ? contents.ops[member] : contents, sequencedMessage: msg };
+            if (isGroup) { opArgs.groupOp = contents; }
+            if (cb) { cb(opArgs, { operation: kind, deltaSegments }); }
         }
         this.batch.logPos[this.doc] = i;
+    }
+
+    /**
+     * SequenceDeltaEvent (sequence/src/sequenceDeltaEvent.ts:26-118) for a callback's
+     * arguments: ranges in document order with the positions the callback carries.  (The
+     * reference sorts by segment ordinal and drops ranges whose ordinals collide, SURVEY Q8;
+     * the positions here are exact.)
+     */
+    static sequenceDeltaEvent(opArgs, deltaArgs, clientId) {
+        const ranges = deltaArgs.deltaSegments.filter((d) => d.position >= 0)
+            .map((d) => ({ operation: deltaArgs.operation, position: d.position, propertyDeltas: d.propertyDeltas,
+                segment: d.segment }))
+            .sort((a, b) => a.position - b.position);
+        return {
+            opArgs, deltaArgs, isLocal: opArgs.sequencedMessage === undefined, isEmpty: deltaArgs.deltaSegments.length === 0,
+            deltaOperation: deltaArgs.operation, ranges, first: ranges[0], last: ranges[ranges.length - 1], clientId,
+        };
     }
 }
 

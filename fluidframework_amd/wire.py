@@ -14,8 +14,10 @@ OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 3
 F_GROUP_MORE, F_MARKER = 1, 2
 NO_PROPS = 0xFFFFFFFF
 VAL_NULL = 0xFFFFFFFF
+VAL_UNDEF = 0xFFFFFFFE          # a key set to the JS value undefined
 VAL_FALSY_BIT = 0x80000000
-COMBINE_NONE, COMBINE_REWRITE, COMBINE_OTHER = 0, 1, 2
+VAL_NOMATCH_BIT = 0x40000000    # matchProperties never finds the value equal (NaN, undefined inside)
+COMBINE_NONE, COMBINE_REWRITE, COMBINE_OTHER, COMBINE_TABLE = 0, 1, 2, 3
 
 OP_DTYPE = np.dtype([
     ("seq", "<i4"), ("ref_seq", "<i4"), ("min_seq", "<i4"), ("pos1", "<i4"), ("pos2", "<i4"),
@@ -30,14 +32,121 @@ CHECKSUM_DTYPE = np.dtype([
 assert CHECKSUM_DTYPE.itemsize == 32
 
 
+class _JsValue:
+    """The JS values JSON cannot hold that non-rewrite combining ops leave in property sets
+    (SURVEY Q4): NaN (`incr`) and undefined (`consensus`' {value: undefined, seq}, unknown
+    combining-op names on an absent key)."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __repr__(self):
+        return self.name
+
+
+NAN = _JsValue("NaN")
+UNDEF = _JsValue("undefined")
+
+
+def from_fixture(v):
+    """Fixture encoding of JS-only values ({"$nan": 1}, {"$undef": 1}; oracle/ref_harness.mjs
+    jsReplacer) -> NAN / UNDEF."""
+    if isinstance(v, dict):
+        if len(v) == 1 and "$nan" in v:
+            return NAN
+        if len(v) == 1 and "$undef" in v:
+            return UNDEF
+        return {k: from_fixture(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [from_fixture(x) for x in v]
+    return v
+
+
+def _has_js_value(v):
+    if v is NAN or v is UNDEF:
+        return True
+    if isinstance(v, dict):
+        return any(_has_js_value(x) for x in v.values())
+    if isinstance(v, list):
+        return any(_has_js_value(x) for x in v)
+    return False
+
+
 def canonical_json(v):
     """Canonical form used to intern property values: matchProperties
     (MT/properties.ts:61-92) compares nested objects structurally, ignoring key order."""
-    return json.dumps(v, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+    if not _has_js_value(v):
+        return json.dumps(v, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+    if v is NAN or v is UNDEF:
+        return v.name
+    if isinstance(v, list):
+        return "[" + ",".join(canonical_json(x) for x in v) + "]"
+    return "{" + ",".join(json.dumps(k, ensure_ascii=False) + ":" + canonical_json(v[k]) for k in sorted(v)) + "}"
 
 
 def js_falsy(v):
-    return v is None or v is False or v == "" or (isinstance(v, (int, float)) and not isinstance(v, bool) and v == 0)
+    return (v is None or v is False or v == "" or v is NAN or v is UNDEF or
+            (isinstance(v, (int, float)) and not isinstance(v, bool) and v == 0))
+
+
+def js_nomatch(v):
+    """matchProperties(a, a) is false for a property set holding v: NaN !== NaN, and an
+    undefined member fails `b[key] === undefined` (also inside nested objects)."""
+    return _has_js_value(v)
+
+
+def _js_num_str(x):
+    if isinstance(x, bool):
+        return "true" if x else "false"
+    if isinstance(x, float) and x.is_integer() and abs(x) < 1e21:
+        return str(int(x))
+    return str(x)
+
+
+def _js_to_string(v):
+    """String(v) for the values JSON can carry (ToPrimitive of objects / arrays)."""
+    if v is None or v is UNDEF:
+        return ""
+    if v is NAN:
+        return "NaN"
+    if isinstance(v, str):
+        return v
+    if isinstance(v, (bool, int, float)):
+        return _js_num_str(v)
+    if isinstance(v, list):
+        return ",".join("" if x is None or x is UNDEF else _js_to_string(x) for x in v)
+    return "[object Object]"
+
+
+class Unsupported(ValueError):
+    pass
+
+
+def js_combine(op, cur, seq):
+    """Properties.combine(op, currentValue, undefined, seq) (MT/properties.ts:26-59) as
+    SegmentPropertiesManager.addProperties calls it for a non-rewrite combining op
+    (MT/segmentPropertiesManager.ts:93-107: the new value is never passed in)."""
+    if cur is UNDEF:
+        cur = op.get("defaultValue", UNDEF)
+    name = op.get("name")
+    if name == "incr":
+        if cur is UNDEF or cur is None or cur is NAN or isinstance(cur, (bool, int, float)):
+            r = NAN                                     # x + undefined
+        else:
+            r = _js_to_string(cur) + "undefined"
+        mv = op.get("minValue")
+        if mv and not (isinstance(mv, (int, float)) and not isinstance(mv, bool)):
+            raise Unsupported("incr with a non-numeric minValue")
+        return r                                        # NaN / "...undefined" < n is false
+    if name == "consensus":
+        if cur is UNDEF:
+            return {"value": UNDEF, "seq": seq}
+        if cur is None:
+            raise Unsupported("consensus over null (the reference throws a TypeError)")
+        if isinstance(cur, dict) and cur.get("seq") == -1:
+            raise Unsupported("consensus over a shared {seq: -1} value (mutated in place)")
+        return cur
+    return cur
 
 
 class Interner:
@@ -60,6 +169,8 @@ class Interner:
     def val(self, v):
         if v is None:
             return VAL_NULL
+        if v is UNDEF:
+            return VAL_UNDEF
         if self.synthetic:
             return int(v) | (VAL_FALSY_BIT if int(v) == 0 else 0)
         c = canonical_json(v)
@@ -68,7 +179,7 @@ class Interner:
             i = len(self.vals)
             self.val_ids[c] = i
             self.vals.append(v)
-        return i | (VAL_FALSY_BIT if js_falsy(v) else 0)
+        return i | (VAL_FALSY_BIT if js_falsy(v) else 0) | (VAL_NOMATCH_BIT if js_nomatch(v) else 0)
 
     def key_name(self, kid):
         return f"k{kid}" if self.synthetic else self.keys[kid]
@@ -76,9 +187,11 @@ class Interner:
     def val_value(self, vid):
         if vid == VAL_NULL:
             return None
+        if vid == VAL_UNDEF:
+            return UNDEF
         if self.synthetic:
             return vid & ~VAL_FALSY_BIT
-        return self.vals[vid & ~VAL_FALSY_BIT]
+        return self.vals[vid & ~(VAL_FALSY_BIT | VAL_NOMATCH_BIT)]
 
 
 class DocEncoder:
@@ -117,6 +230,31 @@ class Batch:
         for k, v in items:
             self.props.append(self.interner.key(k))
             self.props.append(self.interner.val(v))
+        return off
+
+    def _combine_rec(self, props, comb, seq):
+        """A non-rewrite combining op's record: the keys, then the transform of
+        every value a key can hold at this point -- [n, new value of an absent key,
+        (old, new) x n] -- as combine(op, old, undefined, seq) yields it; new = VAL_NULL
+        deletes the key.  Unsupported results (the reference throws, or mutates a shared
+        value) keep COMBINE_OTHER: the document fails with MT_DOC_UNSUPPORTED."""
+        it = self.interner
+        if it.synthetic:
+            return self._props_rec(props, COMBINE_OTHER)
+        try:
+            absent = it.val(js_combine(comb, UNDEF, seq))
+            pairs = []
+            for i, v in enumerate(list(it.vals)):
+                old = it.val(v)
+                pairs.append((old, it.val(js_combine(comb, v, seq))))
+        except Unsupported:
+            return self._props_rec(props, COMBINE_OTHER)
+        off = self._props_rec(props, COMBINE_TABLE)
+        self.props.append(len(pairs))
+        self.props.append(absent)
+        for o, n in pairs:
+            self.props.append(o)
+            self.props.append(n)
         return off
 
     def _text(self, s):
@@ -158,9 +296,10 @@ class Batch:
             base["pos1"], base["pos2"] = op["pos1"], op["pos2"]
             if t == OP_ANNOTATE:
                 comb = op.get("combiningOp")
-                code = COMBINE_NONE if not comb else (
-                    COMBINE_REWRITE if comb.get("name") == "rewrite" else COMBINE_OTHER)
-                base["props"] = self._props_rec(op["props"], code)
+                if comb and comb.get("name") != "rewrite":
+                    base["props"] = self._combine_rec(op["props"], comb, msg["sequenceNumber"])
+                else:
+                    base["props"] = self._props_rec(op["props"], COMBINE_REWRITE if comb else COMBINE_NONE)
         else:
             raise ValueError(f"unsupported op type {t}")
         self.recs.append(base)

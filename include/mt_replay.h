@@ -70,6 +70,13 @@ typedef struct mt_options {
        per LDS segment instead of 8); a document one of whose clients above 32 removes an
        already-removed segment continues in the full tier.  For documents with few writers. */
     int32_t lds_narrow_overlap;
+    /* Delta log layout (with delta_log_capacity > 0): 0 = the callback records of
+       mt_get_delta_log; 1 = rich: every logged segment also carries its state at the event
+       (text or marker refType, property set), and mergeTreeMaintenanceCallback events
+       (SPLIT / APPEND / UNLINK, MT/mergeTree.ts:1343-1373, 2264-2269) are records too --
+       what the Node facade turns into callback objects.  Removed segments keep their text
+       until they are unlinked. */
+    int32_t delta_log_mode;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

@@ -42,10 +42,18 @@ enum mt_op_flags {
 
 #define MT_NO_PROPS 0xFFFFFFFFu      /* props field: no property set */
 #define MT_VAL_NULL 0xFFFFFFFFu      /* value id of JSON null (delete) */
+#define MT_VAL_UNDEF 0xFFFFFFFEu     /* value id of JS undefined (a key set to undefined) */
 #define MT_VAL_FALSY_BIT 0x80000000u /* value id flag: JS value is falsy */
+#define MT_VAL_NOMATCH_BIT 0x40000000u /* value id flag: matchProperties never finds it equal
+                                          (NaN, undefined, objects holding them) */
 #define MT_COMBINE_NONE 0u
 #define MT_COMBINE_REWRITE 1u        /* ICombiningOp { name: "rewrite" } */
-#define MT_COMBINE_OTHER 2u          /* any other combining op: rejected */
+#define MT_COMBINE_OTHER 2u          /* a combining op whose result is not modelled (the
+                                        reference throws or mutates a shared value) */
+#define MT_COMBINE_TABLE 3u          /* any other combining op: the record
+                                        carries combine(op, old, undefined, seq) for every
+                                        value -- [n, new value of an absent key,
+                                        (old, new) x n] after the (key, value) pairs */
 
 typedef struct mt_op_rec {
     int32_t seq;        /* sequenceNumber */
@@ -56,7 +64,8 @@ typedef struct mt_op_rec {
     uint32_t payload;   /* insert: offset into the text arena (UTF-16 units);
                            marker insert: refType */
     uint32_t props;     /* offset (u32 words) of a props-op record in the props arena, or
-                           MT_NO_PROPS.  record = [count | combine<<16, (key, value) x count] */
+                           MT_NO_PROPS.  record = [count | combine<<16, (key, value) x count
+                           (, transform table: MT_COMBINE_TABLE)] */
     uint16_t client;    /* short client id of the writer (first-seen order, observer = 0) */
     uint8_t kind;       /* enum mt_op_kind */
     uint8_t flags;      /* enum mt_op_flags */

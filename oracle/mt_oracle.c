@@ -173,7 +173,8 @@ static int match_props(const Props *a, const Props *b) {
         if (!b) return 0;
         for (int i = 0; i < a->n; i++) {
             int j = props_find(b, a->key[i]);
-            if (j < 0 || b->val[j] != a->val[i]) return 0;
+            /* NaN !== NaN; an undefined member fails `b[key] === undefined` */
+            if (j < 0 || b->val[j] != a->val[i] || (a->val[i] & MT_VAL_NOMATCH_BIT)) return 0;
         }
         for (int j = 0; j < b->n; j++)
             if (props_find(a, b->key[j]) < 0) return 0;
@@ -649,7 +650,27 @@ static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, uint32_t **pd
     for (uint32_t j = 0; j < count; j++) {
         uint32_t key = rec[1 + 2 * j], val = rec[2 + 2 * j];
         int i = props_find(p, key);
-        PD_SET(key, i >= 0 ? p->val[i] : MT_VAL_NULL);
+        /* deltas[key] = previousValue === undefined ? null : previousValue */
+        const int absent = i < 0 || p->val[i] == MT_VAL_UNDEF;
+        PD_SET(key, absent ? MT_VAL_NULL : p->val[i]);
+        if (combine == MT_COMBINE_TABLE) {
+            /* newValue = combine(op, previousValue, undefined, seq) :93-99 */
+            const uint32_t *tab = rec + 1 + 2 * count;
+            val = tab[1];
+            if (!absent) {
+                int hit = 0;
+                for (uint32_t q = 0; q < tab[0]; q++)
+                    if (tab[2 + 2 * q] == p->val[i]) {
+                        val = tab[3 + 2 * q];
+                        hit = 1;
+                    }
+                if (!hit) {          /* the host tabulated every value: cannot happen */
+                    d->status = MT_DOC_INTERNAL;
+                    *pd_out = pd;
+                    return 0;
+                }
+            }
+        }
         if (val == MT_VAL_NULL)
             props_del(p, key);
         else

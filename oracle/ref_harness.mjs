@@ -112,7 +112,7 @@ function makeObserver(seedText) {
         for (const d of dargs.deltaSegments) {
             const seg = d.segment;
             const pos = seg.parent ? mt.getPosition(seg, cw.currentSeq, cw.clientId) : -1;
-            segs.push(d.propertyDeltas !== undefined ? [pos, seg.cachedLength, d.propertyDeltas]
+            segs.push(d.propertyDeltas !== undefined ? [pos, seg.cachedLength, jsClone(d.propertyDeltas)]
                 : [pos, seg.cachedLength]);
         }
         rec.push(segs);
@@ -127,6 +127,25 @@ function makeMsg(k, seq, ref, msn, cseq, contents) {
         minimumSequenceNumber: msn, clientSequenceNumber: cseq, type: "op", contents,
         timestamp: 0, term: 1, traces: [],
     };
+}
+
+// Property values as the reference holds them, JS-only values included: non-rewrite
+// combining ops leave NaN (incr), undefined and {value: undefined, seq} (consensus) in
+// property sets (SURVEY Q4).  jsClone copies without JSON's loss; jsReplacer writes them as
+// {"$nan": 1} / {"$undef": 1} in fixtures.
+function jsClone(v) {
+    if (Array.isArray(v)) { return v.map(jsClone); }
+    if (v !== null && typeof v === "object") {
+        const o = {};
+        for (const k of Object.keys(v)) { o[k] = jsClone(v[k]); }
+        return o;
+    }
+    return v;
+}
+function jsReplacer(key, v) {
+    if (typeof v === "number" && Number.isNaN(v)) { return { $nan: 1 }; }
+    if (v === undefined && key !== "") { return { $undef: 1 }; }
+    return v;
 }
 
 function collectOutputs(c, deltas) {
@@ -156,7 +175,7 @@ function collectOutputs(c, deltas) {
             ovl: seg.removedClientOverlap ? [...seg.removedClientOverlap] : [],
             marker: Marker.is(seg) ? seg.refType : null,
             // copied now: a later annotate mutates the live object (outputs taken mid-run)
-            props: seg.properties === undefined ? null : JSON.parse(JSON.stringify(seg.properties)),
+            props: seg.properties === undefined ? null : jsClone(seg.properties),
         };
         segs.push(rec);
         if (seg.removedSeq === undefined) {
@@ -272,7 +291,14 @@ function genOpExt(rng, cfg, len) {
     if (rng.next() < frac(cfg.p_oob)) { p2 = len + 1 + rng.uniform(5); }
     if (u < frac(cfg.p_insert + cfg.p_remove)) { return { pos1: p1, pos2: p2, type: 1 }; }
     const op = { pos1: p1, pos2: p2, props: genPropsExt(rng, cfg), type: 2 };
-    if (rng.next() < frac(cfg.p_rewrite)) { op.combiningOp = { name: "rewrite" }; }
+    if (cfg.p_combine && rng.next() < frac(cfg.p_combine)) {
+        // non-rewrite combining ops (MT/properties.ts:26-59 via
+        // MT/segmentPropertiesManager.ts:93-107): incr (with and without default/min),
+        // consensus, and a name combine() does not know
+        const COMBINE = [{ name: "incr" }, { name: "incr", defaultValue: 1, minValue: 0 }, { name: "consensus" },
+            { name: "consensus", defaultValue: 5 }, { name: "max" }, { name: "max", defaultValue: "d" }];
+        op.combiningOp = COMBINE[rng.uniform(COMBINE.length)];
+    } else if (rng.next() < frac(cfg.p_rewrite)) { op.combiningOp = { name: "rewrite" }; }
     return op;
 }
 function genDocExt(cfg, doc) {
@@ -356,6 +382,40 @@ function replayErrDoc(log) {
     const out = collectOutputs(c, deltas);
     delete out.tree;
     return { out, error };
+}
+
+// Every callback the observer fires, in order, with the segments' state at the event:
+// mergeTreeDeltaCallback -> ["D", seq, operation, [[position, cachedLength, propertyDeltas |
+// null, state] ...]] and mergeTreeMaintenanceCallback (SPLIT/APPEND/UNLINK, MT/mergeTree.ts:
+// 1343-1373, 2264-2269) -> ["M", operation, [[cachedLength, state] ...]]; state = {t: text |
+// m: refType, p: properties | null}.
+function segState(seg) {
+    const st = Marker.is(seg) ? { m: seg.refType } : { t: seg.text };
+    st.p = seg.properties === undefined ? null : jsClone(seg.properties);
+    return st;
+}
+function replayRichDoc(log) {
+    const { c } = makeObserver(log.seed_text);
+    const events = [];
+    c.mergeTreeDeltaCallback = (opArgs, dargs) => {
+        const mt = c.mergeTree;
+        const cw = mt.getCollabWindow();
+        events.push(["D", opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, dargs.operation,
+            dargs.deltaSegments.map((d) => [d.segment.parent ? mt.getPosition(d.segment, cw.currentSeq, cw.clientId) : -1,
+                d.segment.cachedLength, d.propertyDeltas === undefined ? null : jsClone(d.propertyDeltas),
+                segState(d.segment)])]);
+    };
+    c.mergeTree.mergeTreeMaintenanceCallback = (args) => {
+        events.push(["M", args.operation, args.deltaSegments.map((d) => [d.segment.cachedLength, segState(d.segment)])]);
+    };
+    const cseq = {};
+    for (const [k, t, r, msn, op, type] of log.msgs) {
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        c.applyMsg(msg);
+    }
+    return { doc: log.doc, events };
 }
 
 // Maintenance events (mergeTreeMaintenanceCallback, MT/mergeTree.ts:1343-1373 scourNode
@@ -600,11 +660,14 @@ async function main() {
         const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
         const docs = [];
         for (let d = d0; d < d1; d++) { docs.push(cfg.ext ? genDocExt(cfg, d) : genDoc(cfg, d)); }
-        fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
+        fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }, cfg.p_combine ? jsReplacer : undefined));
     } else if (mode === "replay") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: outs }));
+    } else if (mode === "rich") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => replayRichDoc(d)) }, jsReplacer));
     } else if (mode === "replayerr") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => replayErrDoc(d)) }));

@@ -7,7 +7,7 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --only name,name]
+    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --only name,name]
 """
 import gzip
 import json
@@ -28,6 +28,13 @@ FIXTURES = {
     # deep paged layouts, page splits and repacks late in the stream
     "ref_c3_full": ("c3", {"ops": 10000}, 4),
     "ref_c4_full": ("c4", {"ops": 10000}, 2),
+    # non-rewrite combining ops: incr / consensus / unknown names leave NaN,
+    # undefined and {value: undefined, seq} in property sets
+    "ref_combine": (None, {"ext": True, "seed": 4242, "ops": 700, "writers": 5, "lag": 40, "seed_len": 40,
+                           "p_insert": 0.4, "p_remove": 0.2, "text_max": 12, "p_newline": 0.05,
+                           "p_len_continue": 0.8, "p_insert_props": 0.3, "n_keys": 4,
+                           "max_keys_per_op": 3, "p_marker": 0.05, "p_rewrite": 0.2, "p_combine": 0.4,
+                           "p_group": 0.05, "p_noop": 0.02, "p_empty": 0.02, "p_oob": 0.02}, 8),
     # a long-lived document: 30k messages (~45k segment ids created, ~12k live segments)
     "ref_c3_long": ("c3", {"ops": 30000}, 2),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),
@@ -170,6 +177,30 @@ def make_error_fixture():
     print("ref_errors", len(docs), "docs", sorted({d["error"]["message"][:40] for d in docs}))
 
 
+# Callback streams with the segments' state (harness "rich"): every mergeTreeDeltaCallback and
+# mergeTreeMaintenanceCallback of replays of existing fixtures' streams (first documents).
+RICH_FROM = [("ref_ext", 4), ("ref_c3", 2), ("ref_combine", 2)]
+
+
+def make_rich_fixture():
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        for name, n in RICH_FROM:
+            with gzip.open(os.path.join(HERE, name + ".json.gz"), "rt") as fh:
+                fx = json.load(fh)
+            docs = [dict(doc=f"{name}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in fx["docs"][:n]]
+            lp, op = os.path.join(td, "logs.json"), os.path.join(td, "out.json")
+            json.dump({"docs": docs}, open(lp, "w"))
+            subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "rich", lp, op])
+            ev = json.load(open(op))["docs"]
+            for d, e in zip(docs, ev):
+                d["events"] = e["events"]
+                d["source"] = name
+                out.append(d)
+    _dump("ref_rich", dict(config={"ext": True, "sources": RICH_FROM}, docs=out))
+    print("ref_rich", len(out), "docs", sum(len(d["events"]) for d in out), "events")
+
+
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
     if "--snapshots" in sys.argv[1:]:
@@ -180,6 +211,9 @@ def main():
         return
     if "--errors" in sys.argv[1:]:
         make_error_fixture()
+        return
+    if "--rich" in sys.argv[1:]:
+        make_rich_fixture()
         return
     only = None
     if "--only" in sys.argv[1:]:
@@ -208,6 +242,7 @@ def main():
     make_snapshot_fixtures()
     make_farm_fixture()
     make_error_fixture()
+    make_rich_fixture()
 
 
 if __name__ == "__main__":

@@ -20,6 +20,9 @@ function msgs(doc) {
     }));
 }
 const hex = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("hex");
+// NaN / undefined property values (combining ops, SURVEY Q4) as the fixtures write them
+const jsReplacer = (key, v) => ((typeof v === "number" && Number.isNaN(v)) ? { $nan: 1 }
+    : (v === undefined && key !== "" ? { $undef: 1 } : v));
 
 const [mode, file, ...extra] = process.argv.slice(2);
 const fx = load(file);
@@ -51,7 +54,7 @@ if (mode === "encode") {
             return { error: e.message, type: e.constructor.name };
         }
     });
-    process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }));
+    process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }, jsReplacer));
 } else if (mode === "deltas") {
     // deltas <fixture> <deltaLogCapacity> <flushEvery>: every mergeTreeDeltaCallback the
     // facade fires while the messages are applied in flushes of <flushEvery> messages per
@@ -59,7 +62,7 @@ if (mode === "encode") {
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
     const cap = parseInt(extra[0], 10), every = parseInt(extra[1], 10);
     const batch = new GpuMergeTreeBatch(fx.docs.length,
-        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: cap });
+        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: cap, deltaLogMode: 0 });
     batch.loadInitialText(fx.docs.map((d) => d.seed_text));
     const calls = fx.docs.map(() => []);
     const views = fx.docs.map((d, i) => {
@@ -84,6 +87,43 @@ if (mode === "encode") {
         error = e.message;
     }
     process.stdout.write(JSON.stringify({ calls, error }));
+} else if (mode === "rich") {
+    // rich <ref_rich fixture> <flushEvery>: every delta and maintenance callback the facade
+    // fires, in the reference harness's format (segments' state at the event)
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const every = parseInt(extra[0], 10);
+    const batch = new GpuMergeTreeBatch(fx.docs.length,
+        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: 1 << 18 });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const events = fx.docs.map(() => []);
+    const st = (seg) => Object.assign(seg.type === "Marker" ? { m: seg.refType } : { t: seg.text },
+        { p: seg.properties === undefined ? null : seg.properties });
+    const views = fx.docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        c.mergeTreeDeltaCallback = (opArgs, args) => {
+            events[i].push(["D", opArgs.sequencedMessage.sequenceNumber, args.operation,
+                args.deltaSegments.map((x) => [x.position, x.segment.cachedLength,
+                    x.propertyDeltas === undefined ? null : x.propertyDeltas, st(x.segment)]),
+                opArgs.op === undefined ? null : opArgs.op.type]);
+        };
+        c.mergeTreeMaintenanceCallback = (args) => {
+            events[i].push(["M", args.operation, args.deltaSegments.map((x) => [x.segment.cachedLength, st(x.segment)])]);
+        };
+        return c;
+    });
+    const all = fx.docs.map((d) => msgs(d));
+    let error = null;
+    try {
+        const longest = Math.max(...all.map((m) => m.length));
+        for (let t = 0; t < longest; t += every) {
+            all.forEach((m, i) => { for (const x of m.slice(t, t + every)) { views[i].applyMsg(x); } });
+            batch.flush();
+        }
+    } catch (e) {
+        error = e.message;
+    }
+    process.stdout.write(JSON.stringify({ events, error }, jsReplacer));
 } else if (mode === "maint") {
     // maint <fixture.json.gz> -> [[split, append, unlink] per doc] through the facade
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));

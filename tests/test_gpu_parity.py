@@ -391,3 +391,30 @@ def test_gpu_long_documents_match_reference(uid_capacity):
     mt.apply_arrays(a)
     for i, doc in enumerate(fx["docs"]):
         assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
+
+
+# ---------------------------------------------------------------- rich callback stream
+@pytest.mark.parametrize("tier", list(TIERS))
+def test_gpu_rich_callback_stream_matches_reference(tier):
+    """delta_log_mode 1: every mergeTreeDeltaCallback with its segments' state (text or marker,
+    properties after the op) and every mergeTreeMaintenanceCallback (SPLIT / APPEND / UNLINK
+    with the segments as the reference passes them, MT/mergeTree.ts:1343-1373, 2264-2269), in
+    the reference's order -- compared with the reference's own callbacks (tests/golden/ref_rich)."""
+    fx = gu.load("ref_rich")
+    interner = gu.Interner()
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_mode=1, delta_log_capacity=1 << 20, **TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    for i, doc in enumerate(fx["docs"]):
+        got, want = gu.parse_rich_log(mt.get_delta_log(i)), gu.expected_rich(doc, interner)
+        bad = next((j for j, (x, y) in enumerate(zip(got, want)) if x != y), None)
+        assert bad is None and len(got) == len(want), (doc["doc"], bad, len(got), len(want),
+                                                       got[bad] if bad is not None else None,
+                                                       want[bad] if bad is not None else None)
+    # the maintenance records are not part of the delta hash
+    plain = _gpu_batch(len(fx["docs"]), **TIERS[tier])
+    plain.load_initial_text(a["seed_off"], a["seed"])
+    plain.apply_arrays(a)
+    assert np.array_equal(plain.checksums(), mt.checksums())

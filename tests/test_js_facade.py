@@ -41,7 +41,7 @@ def test_addon_loads_and_fails_loudly_without_gpu():
     assert r.returncode != 0 and "no CPU fallback" in r.stderr
 
 
-@pytest.mark.parametrize("name", ["ref_ext", "ref_ext_long", "ref_small"])
+@pytest.mark.parametrize("name", ["ref_ext", "ref_ext_long", "ref_small", "ref_combine"])
 def test_js_encoder_matches_python_encoder(name):
     fx = gu.load(name)
     got = _node("encode", os.path.join(gu.GOLDEN, name + ".json.gz"))
@@ -57,7 +57,7 @@ def test_js_encoder_matches_python_encoder(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["ref_ext", "ref_c3"])
+@pytest.mark.parametrize("name", ["ref_ext", "ref_c3", "ref_combine"])
 def test_js_facade_replays_fixture_like_reference(name):
     _addon()
     fx = gu.load(name)
@@ -177,3 +177,21 @@ def test_js_facade_delta_log_overflow_throws():
     _addon()
     got = _node("deltas", os.path.join(gu.GOLDEN, "ref_c3.json.gz"), "512", "100000")
     assert got["error"] and "overflowed its delta log" in got["error"]
+
+
+@pytest.mark.gpu
+def test_js_facade_rich_callbacks_match_reference():
+    """The facade's mergeTreeDeltaCallback / mergeTreeMaintenanceCallback stream -- opArgs.op,
+    segments carrying text / refType and properties at the event, SPLIT / APPEND / UNLINK as
+    event objects -- equals the reference's own callbacks (tests/golden/ref_rich), across
+    flushes that drain and reset the device log."""
+    _addon()
+    fx = gu.load("ref_rich")
+    got = _node("rich", os.path.join(gu.GOLDEN, "ref_rich.json.gz"), "97", timeout=600)
+    assert got["error"] is None, got["error"]
+    for d, ev in zip(fx["docs"], got["events"]):
+        assert all(e[0] == "M" or e[4] in (0, 1, 2) for e in ev)       # opArgs.op is the member op
+        mine = [e[:4] if e[0] == "D" else e for e in ev]
+        bad = next((j for j, (x, y) in enumerate(zip(mine, d["events"])) if x != y), None)
+        assert bad is None and len(mine) == len(d["events"]), (d["doc"], bad, mine[bad] if bad is not None else None,
+                                                               d["events"][bad] if bad is not None else None)
