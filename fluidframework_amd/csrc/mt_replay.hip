@@ -421,7 +421,7 @@ __device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, in
         op.pos1 = (int)rng_uniform(g.rng, (uint32_t)(len + 1));
         const int tl = 1 + (int)rng_uniform(g.rng, (uint32_t)cfg.text_max);
         op.pos2 = tl;
-        op.payload = (uint32_t)(g.tb + g.tu);
+        op.payload = (uint32_t)g.tu;   // local to the document's region (rebased by k_gen_compact)
         uint16_t ch = 0;
         for (int j = 0; j < tl; j++) {
             const uint32_t v = rng_next(g.rng);
@@ -437,7 +437,7 @@ __device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, in
         in.pay_ok = tl <= 8;
         g.tu += tl;
         if (cfg.p_insert_props > 0 && (uint64_t)rng_next(g.rng) < cfg.p_insert_props) {
-            op.props = (uint32_t)(g.pb + g.pu);
+            op.props = (uint32_t)g.pu;
             g.pu += gen_props(g.rng, cfg, props_out + g.pb + g.pu);
         }
     } else {
@@ -450,7 +450,7 @@ __device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, in
             op.kind = MT_OP_REMOVE;
         } else {
             op.kind = MT_OP_ANNOTATE;
-            op.props = (uint32_t)(g.pb + g.pu);
+            op.props = (uint32_t)g.pu;
             g.pu += gen_props(g.rng, cfg, props_out + g.pb + g.pu);
         }
     }
@@ -458,6 +458,13 @@ __device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, in
     in.pay_hi = phi;
     if (lane() == 0) ops_out[doc * cfg.ops + (t - 1)] = op;
     gsync();
+}
+// The document's text / property words used so far (k_gen_compact packs the regions).
+__device__ static void gen_end(const GenCtx &g, int64_t *used_out, int doc) {
+    if (lane() == 0) {
+        used_out[2 * doc] = g.tu;
+        used_out[2 * doc + 1] = g.pu;
+    }
 }
 
 // Generates and applies cfg.ops messages per document; the view length each writer draws
@@ -467,7 +474,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
                                                       mt_op_rec *ops_out, uint16_t *text_out,
                                                       uint32_t *props_out, int64_t tstride,
                                                       int64_t pstride, int32_t *fail_out,
-                                                      int32_t *dbg_len, TierCaps caps) {
+                                                      int32_t *dbg_len, int64_t *used_out, TierCaps caps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
@@ -481,8 +488,9 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
         if (lane() == 0) st.retry[doc] = 1;
         return;
     }
-    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)text_out;
-    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)props_out;
+    // op records carry offsets local to the document's region of the arenas
+    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)(text_out + g.tb);
+    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)(props_out + g.pb);
     for (int t = 1; t <= cfg.ops && d.status == 0; t++) {
         int r, c, msn;
         gen_pick(g, cfg, t, r, c, msn);
@@ -506,6 +514,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
         gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
         apply_op(d, in, gt, gp);
     }
+    gen_end(g, used_out, doc);
     if (T::kLds && d.status == MT_DOC_RETRY) {
         if (lane() == 0) st.retry[doc] = 1;
         return;
@@ -677,7 +686,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
                                                             mt_op_rec *ops_out, uint16_t *text_out,
                                                             uint32_t *props_out, int64_t tstride,
                                                             int64_t pstride, int32_t *fail_out,
-                                                            int32_t *dbg_len, PagedCaps pc) {
+                                                            int32_t *dbg_len, int64_t *used_out, PagedCaps pc) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
@@ -701,8 +710,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         }
         return;
     }
-    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)text_out;
-    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)props_out;
+    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)(text_out + g.tb);
+    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)(props_out + g.pb);
     int pk_ut = 0, pk_heap = 0;
     for (int t = 1; t <= cfg.ops && w.status == 0; t++) {
         int r, c, msn;
@@ -728,6 +737,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         pk_ut = max(pk_ut, pd.ut_n);
         pk_heap = max(pk_heap, w.heap_n);
     }
+    gen_end(g, used_out, doc);
     if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
     if (lane() == 0) {
         if (w.status) fail_out[doc] = w.status;
@@ -1634,6 +1644,30 @@ int mt_extract_snapshots(mt_handle *h, int64_t *io, mt_seg_rec *recs, uint16_t *
     return 0;
 }
 
+// Packs the generated documents' text / property regions (allocated at fixed strides) back
+// to back and rebases their op records, whose offsets the generator wrote local to the
+// document's region: the wire format's u32 offsets address the whole batch, and the strided
+// layout would pass 2^32 units (C3: at document ~53.7k).
+__global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, int64_t ops_per_doc, const uint16_t *text_in,
+                                                     const uint32_t *props_in, int64_t tstride, int64_t pstride,
+                                                     const int64_t *used, const int64_t *base, uint16_t *text_out,
+                                                     uint32_t *props_out, int n_docs) {
+    const int doc = blockIdx.x;
+    if (doc >= n_docs) return;
+    const int64_t tu = used[2 * doc], pu = used[2 * doc + 1], tb = base[2 * doc], pb = base[2 * doc + 1];
+    const uint16_t *ts = text_in + doc * tstride;
+    const uint32_t *ps = props_in + doc * pstride;
+    for (int64_t i = threadIdx.x; i < tu; i += blockDim.x) text_out[tb + i] = ts[i];
+    for (int64_t i = threadIdx.x; i < pu; i += blockDim.x) props_out[pb + i] = ps[i];
+    mt_op_rec *o = ops + doc * ops_per_doc;
+    for (int64_t k = threadIdx.x; k < ops_per_doc; k += blockDim.x) {
+        mt_op_rec op = o[k];
+        if (op.kind == MT_OP_INSERT && !(op.flags & MT_F_MARKER)) op.payload += (uint32_t)tb;
+        if (op.props != MT_NO_PROPS) op.props += (uint32_t)pb;
+        o[k] = op;
+    }
+}
+
 mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                       int32_t *view_len_trace) {
     if (!h || !cfg || cfg->writers < 1 || cfg->ops < 0) return nullptr;
@@ -1648,6 +1682,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
     b->text_len = N * tstride;
     b->props_len = N * pstride;
     int32_t *d_fail = nullptr, *d_trace = nullptr;
+    int64_t *d_used = nullptr;
     if (view_len_trace && hipMalloc(&d_trace, std::max<int64_t>(N * ops, 1) * 16) != hipSuccess) {
         delete b;
         return nullptr;
@@ -1656,7 +1691,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
               hipMalloc(&b->ops, std::max<int64_t>(b->n_ops, 1) * sizeof(mt_op_rec)) == hipSuccess &&
               hipMalloc(&b->text, b->text_len * 2) == hipSuccess &&
               hipMalloc(&b->props, b->props_len * 4) == hipSuccess &&
-              hipMalloc(&d_fail, N * 4) == hipSuccess;
+              hipMalloc(&d_fail, N * 4) == hipSuccess && hipMalloc(&d_used, N * 16) == hipSuccess;
     if (ok) {
         std::vector<int64_t> off(N + 1);
         for (int64_t i = 0; i <= N; i++) off[i] = i * ops;
@@ -1669,7 +1704,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
         if (h->lds.S > 0) {
             hipLaunchKernelGGL(k_generate<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, gw),
                                h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
-                               pstride, d_fail, d_trace, h->lds);
+                               pstride, d_fail, d_trace, d_used, h->lds);
             ok = hipGetLastError() == hipSuccess;
         } else {
             ok = hipMemsetD32Async((hipDeviceptr_t)h->st.retry, 1, h->n_docs, h->stream) == hipSuccess;
@@ -1682,18 +1717,18 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
                 if (pc->narrow)
                     hipLaunchKernelGGL((k_generate_paged<TierPagedT<false, true>>), dim3(h->n_docs), dim3(MT_WAVE), lb,
                                        h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
-                                       pstride, d_fail, d_trace, *pc);
+                                       pstride, d_fail, d_trace, d_used, *pc);
                 else
                     hipLaunchKernelGGL((k_generate_paged<TierPagedT<false>>), dim3(h->n_docs), dim3(MT_WAVE), lb,
                                        h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
-                                       pstride, d_fail, d_trace, *pc);
+                                       pstride, d_fail, d_trace, d_used, *pc);
                 ok = hipGetLastError() == hipSuccess;
             }
             ok = ok && hipStreamSynchronize(h->stream) == hipSuccess;
         } else if (ok) {
             hipLaunchKernelGGL(k_generate<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(false, glb_caps(h), gw), h->stream, h->st, *cfg, doc_index_base,
-                               b->ops, b->text, b->props, tstride, pstride, d_fail, d_trace, glb_caps(h));
+                               b->ops, b->text, b->props, tstride, pstride, d_fail, d_trace, d_used, glb_caps(h));
             ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
         }
     }
@@ -1709,10 +1744,51 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
                 ok = false;
             }
     }
+    if (ok) {   // pack the per-document regions (u32 offsets address the whole batch)
+        std::vector<int64_t> used((size_t)N * 2), base((size_t)N * 2);
+        ok = hipMemcpy(used.data(), d_used, N * 16, hipMemcpyDeviceToHost) == hipSuccess;
+        int64_t tt = 0, tp = 0;
+        for (int64_t i = 0; ok && i < N; i++) {
+            base[2 * i] = tt;
+            base[2 * i + 1] = tp;
+            tt += used[2 * i];
+            tp += used[2 * i + 1];
+        }
+        if (ok && (tt > (int64_t)UINT32_MAX || tp >= (int64_t)MT_NO_PROPS)) {
+            h->err = "mt_generate: the batch's text / property arenas exceed 32-bit offsets";
+            ok = false;
+        }
+        uint16_t *nt = nullptr;
+        uint32_t *np = nullptr;
+        if (ok)
+            ok = hipMalloc(&nt, std::max<int64_t>(tt, 1) * 2) == hipSuccess &&
+                 hipMalloc(&np, std::max<int64_t>(tp, 1) * 4) == hipSuccess;
+        int64_t *d_base = nullptr;
+        if (ok) ok = hipMalloc(&d_base, N * 16) == hipSuccess &&
+                     hipMemcpy(d_base, base.data(), N * 16, hipMemcpyHostToDevice) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(k_gen_compact, dim3(h->n_docs), dim3(256), 0, h->stream, b->ops, ops, b->text,
+                               b->props, tstride, pstride, d_used, d_base, nt, np, h->n_docs);
+            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+        }
+        if (d_base) hipFree(d_base);
+        if (ok) {
+            hipFree(b->text);
+            hipFree(b->props);
+            b->text = nt;
+            b->props = np;
+            b->text_len = tt;
+            b->props_len = tp;
+        } else {
+            if (nt) hipFree(nt);
+            if (np) hipFree(np);
+        }
+    }
     if (ok && d_trace)
         ok = hipMemcpy(view_len_trace, d_trace, N * ops * 16, hipMemcpyDeviceToHost) == hipSuccess;
     if (d_trace) hipFree(d_trace);
     if (d_fail) hipFree(d_fail);
+    if (d_used) hipFree(d_used);
     if (!ok) {
         if (h->err.empty()) h->err = "mt_generate failed";
         mt_batch_free(b);

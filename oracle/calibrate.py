@@ -5,8 +5,10 @@ The reference cannot travel to the GPU box, so bench.py times the C restatement
 op streams and one thread each, the reference itself -- the transpiled TypeScript MergeTree
 (oracle/_ref, built by oracle/build_ref.py) driven through Client.applyMsg by
 oracle/ref_harness.mjs `time` mode under Node -- against the restatement, and writes the ratio
-to profiles/<round>/cpu_calibration.json.  bench.py reports `reference_estimate` = port
-throughput / ratio next to its CPU baseline (est_reference = restatement / r).
+to profiles/<round>/cpu_calibration.json.  The reference is timed twice: with the observer's
+position-recording delta callback (what replayDoc records) and with no callback at all (its
+fastest replay).  bench.py reports `reference_estimate` = port throughput / the no-callback
+ratio, the conservative one (est_reference = restatement / r).
 
     python oracle/calibrate.py [out.json]
 """
@@ -25,8 +27,8 @@ import pyoracle  # noqa: E402
 from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts  # noqa: E402
 
 HARNESS = os.path.join(REPO, "oracle", "ref_harness.mjs")
-# (config, documents, ops per document): a few full-length documents of each bench workload
-CASES = [("c2", 16, 2000), ("c3", 4, 10000)]
+# (config, documents, ops per document): full-length documents of each bench workload
+CASES = [("c2", 64, 2000), ("c3", 24, 10000)]
 
 
 def calibrate(name, ndocs, nops, configs):
@@ -37,6 +39,8 @@ def calibrate(name, ndocs, nops, configs):
         subprocess.check_call(["node", HARNESS, "gen", cp, "0", str(ndocs), gp])
         subprocess.check_call(["node", HARNESS, "time", gp, tp, "2"])
         ref = json.load(open(tp))
+        subprocess.check_call(["node", HARNESS, "time", gp, tp, "2", "nocb"])
+        ref_nocb = json.load(open(tp))
         gen = json.load(open(gp))
     b = Batch(Interner(synthetic=True))
     for d in gen["docs"]:
@@ -52,16 +56,20 @@ def calibrate(name, ndocs, nops, configs):
     assert (st == 0).all()
     port = n_ops / best
     return dict(docs=ndocs, ops_per_doc=nops, ops=n_ops, threads=1,
-                reference_ops_per_s=round(ref["ops_per_s"], 1), reference_runtime=f"node {ref['node']}",
-                port_ops_per_s=round(port, 1), ratio_port_over_reference=round(port / ref["ops_per_s"], 3))
+                reference_ops_per_s=round(ref["ops_per_s"], 1),
+                reference_nocb_ops_per_s=round(ref_nocb["ops_per_s"], 1),
+                reference_runtime=f"node {ref['node']}",
+                port_ops_per_s=round(port, 1), ratio_port_over_reference=round(port / ref["ops_per_s"], 3),
+                ratio_port_over_reference_nocb=round(port / ref_nocb["ops_per_s"], 3))
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r2", "cpu_calibration.json")
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
-    res = {"note": "one thread each, same op streams: the transpiled reference MergeTree (Client.applyMsg "
-                   "with the position-recording delta callback) under Node vs oracle/mt_oracle.c "
-                   "(delta records on); measured in the build container by oracle/calibrate.py"}
+    res = {"note": "one thread each, same op streams: the transpiled reference MergeTree (Client.applyMsg, "
+                   "observer with the position-recording delta callback / with no callback) under Node vs "
+                   "oracle/mt_oracle.c as bench.py times it; measured in the build container by "
+                   "oracle/calibrate.py"}
     for name, nd, no in CASES:
         res[name] = calibrate(name, nd, no, configs)
         print(name, res[name])

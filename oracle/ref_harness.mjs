@@ -675,15 +675,18 @@ async function main() {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         fs.writeFileSync(rest[1], JSON.stringify(logs.docs.map((d) => maintDoc(d))));
     } else if (mode === "time") {
-        // time <gen.json> <out.json> [repeats]: the reference's Client.applyMsg replay of
-        // every document's stream (messages pre-built, observer with the delta callback
-        // that records positions, as replayDoc), one thread; the CPU-baseline calibration
+        // time <gen.json> <out.json> [repeats] [nocb]: the reference's Client.applyMsg replay
+        // of every document's stream (messages pre-built, observer with the delta callback
+        // that records positions, as replayDoc -- or with no callback at all when "nocb"),
+        // one thread; the CPU-baseline calibration
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const reps = rest[2] ? parseInt(rest[2], 10) : 1;
+        const nocb = rest[3] === "nocb";
         let ns = 0n, ops = 0;
         for (let rep = 0; rep < reps; rep++) {
             for (const d of logs.docs) {
                 const { c } = makeObserver(d.seed_text);
+                if (nocb) { c.mergeTreeDeltaCallback = undefined; }
                 const cseq = {};
                 const msgs = d.msgs.map(([k, t, r, msn, op, type]) => {
                     cseq[k] = (cseq[k] || 0) + 1;
@@ -698,7 +701,7 @@ async function main() {
             }
         }
         const s = Number(ns) / 1e9;
-        fs.writeFileSync(rest[1], JSON.stringify({ ops, seconds: s, ops_per_s: ops / s, node: process.version }));
+        fs.writeFileSync(rest[1], JSON.stringify({ ops, seconds: s, ops_per_s: ops / s, node: process.version, nocb }));
     } else if (mode === "snap") {
         const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);

@@ -51,10 +51,13 @@ def test_recorded_traffic_matches_default_workload():
 
 
 def test_cpu_calibration_recorded():
-    cal = json.load(open(os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")))
+    import bench
+    cal = json.load(open(bench.CALIBRATION))
     for name in ("c2", "c3"):
         c = cal[name]
-        assert c["threads"] == 1 and c["ops"] > 0
-        assert c["ratio_port_over_reference"] > 0
-        assert abs(c["port_ops_per_s"] / c["reference_ops_per_s"] - c["ratio_port_over_reference"]) < 0.01 * c[
-            "ratio_port_over_reference"]
+        assert c["threads"] == 1 and c["ops"] > 0 and c["docs"] >= 16
+        for sfx in ("", "_nocb"):
+            r = c["ratio_port_over_reference" + sfx]
+            assert r > 0 and abs(c["port_ops_per_s"] / c["reference" + sfx + "_ops_per_s"] - r) < 0.01 * r
+        # the reference without a callback is at least as fast as with the position-recording one
+        assert c["reference_nocb_ops_per_s"] >= 0.95 * c["reference_ops_per_s"]

@@ -141,12 +141,24 @@ def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     got = b.download()
     gsums = mt.checksums()
     omaint = []
+    # the arenas are packed document after document (u32 offsets address the whole batch):
+    # every insert's payload follows the previous one, and nothing is left between them
+    ops_all = got["ops"]
+    ins = ops_all["kind"] == 0
+    assert np.array_equal(ops_all["payload"][ins][1:], (ops_all["payload"][ins] + ops_all["pos2"][ins])[:-1])
+    assert len(got["text"]) == int(ops_all["pos2"][ins].sum())
+    withp = ops_all["props"] != 0xFFFFFFFF
+    assert np.all(np.diff(ops_all["props"][withp].astype(np.int64)) > 0)
     for d in range(docs):
         g = oracle_lib.generate(cfg, d, keep=True)
         lo, hi = got["doc_off"][d], got["doc_off"][d + 1]
         ops_d = got["ops"][lo:hi].copy()
         assert np.array_equal(ops_d[["seq", "ref_seq", "min_seq", "pos1", "pos2", "client", "kind"]],
                               g["ops"][["seq", "ref_seq", "min_seq", "pos1", "pos2", "client", "kind"]]), d
+        gi = ops_d["kind"] == 0
+        for op, oop in zip(ops_d[gi][:50], g["ops"][gi][:50]):   # the payload text equals the oracle's
+            assert np.array_equal(got["text"][op["payload"]:op["payload"] + op["pos2"]],
+                                  g["text"][oop["payload"]:oop["payload"] + oop["pos2"]]), d
         osum = g["doc"].outputs()["checksum"]
         for f in ("length", "text_hash", "props_hash", "delta_hash"):
             assert gsums[d][f] == osum[f], (d, f)

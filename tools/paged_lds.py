@@ -1,0 +1,26 @@
+"""LDS bytes per document of a paged launch (mirror of csrc/mt_paged.h paged_layout) and the
+documents per CU they allow (160 KB LDS per CU on gfx950).
+    python tools/paged_lds.py PP UT PH [overlap_bytes]"""
+import sys
+
+MT_PG_SLOTS, MT_LV, META, LDS_CU = 64, 8, 12, 160 * 1024
+
+
+def pcnt_bytes(B):
+    c3 = max(B // 8, 2)
+    return 2 * B + B // 2 + (MT_LV - 3) * c3
+
+
+def paged_lds(PP, UT, PH, ob=4, gen_words=0):
+    o = 16 * MT_PG_SLOTS * 2 + ob * MT_PG_SLOTS
+    o += 16 * UT + ((ob * UT + 7) & ~7)
+    o += 8 * (PH + 1) + META * PP + ((2 * UT + 3) & ~3) + 4 * PP
+    o += 64 * 4 + MT_LV * 4 * 2 + 4 * gen_words + 2 * PP + 2 * 16 + MT_LV * 16 + 16
+    o += pcnt_bytes(PP) - PP
+    return (o + 15) & ~15
+
+
+if __name__ == "__main__":
+    a = [int(x) for x in sys.argv[1:]]
+    b = paged_lds(*a)
+    print(b, LDS_CU // b)
