@@ -10,8 +10,10 @@ DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", 
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mt_replay.h", "mt_types.h")]
 OUT = os.environ.get("MT_OUT") or os.path.join(HERE, "libmtreplay.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -amdgpu-use-amdgpu-trackers: the scheduler's AMDGPU register-pressure trackers (A/B on the
+# C3 bench, same registers and spills: 886 -> 870 ms per step; profiles/r2/ab_flags.log)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-result",
-         "-Wno-unused-value"] + os.environ.get("MT_EXTRA_FLAGS", "").split()
+         "-Wno-unused-value", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"] + os.environ.get("MT_EXTRA_FLAGS", "").split()
 
 
 def needs_build():
