@@ -70,6 +70,16 @@ class MergeTreeBatch:
         self._check(self.lib.mt_load_initial_text(self.h, _native.ptr(seed_off), _native.ptr(seed)),
                     "mt_load_initial_text")
 
+    def start_collaboration(self, min_seq, cur_seq):
+        """Client.startOrUpdateCollaboration(id, minSeq, currentSeq) for every document with
+        min_seq[d] >= 0 (before its first message)."""
+        ms = np.ascontiguousarray(min_seq, dtype=np.int32)
+        cs = np.ascontiguousarray(cur_seq, dtype=np.int32)
+        if ms.shape != (self.n_docs,) or cs.shape != (self.n_docs,):
+            raise ValueError("start_collaboration: one minSeq and one currentSeq per document")
+        self._check(self.lib.mt_start_collaboration(self.h, _native.ptr(ms), _native.ptr(cs)),
+                    "mt_start_collaboration")
+
     def reset(self):
         """Asynchronously re-initialise every document from the loaded initial contents."""
         self._check(self.lib.mt_reset(self.h), "mt_reset")

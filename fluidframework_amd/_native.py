@@ -46,6 +46,7 @@ SIGNATURES = [
     ("mt_last_error", ctypes.c_char_p, [_P]),
     ("mt_num_docs", _U32, [_P]),
     ("mt_load_initial_text", _I, [_P, _P, _P]),
+    ("mt_start_collaboration", _I, [_P, _P, _P]),
     ("mt_reset", _I, [_P]),
     ("mt_apply_ops", _I, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),
     ("mt_load_snapshots", _I, [_P, _P, _P, _P, _U64, _P, _U64, _P, _U64, _P, _P]),

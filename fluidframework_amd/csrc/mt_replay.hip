@@ -1232,6 +1232,41 @@ void mt_destroy(mt_handle *h) {
 const char *mt_last_error(const mt_handle *h) { return h ? h->err.c_str() : "null handle"; }
 uint32_t mt_num_docs(const mt_handle *h) { return h ? h->n_docs : 0; }
 
+// startCollaboration's window for the listed documents (mt_start_collaboration)
+__global__ void k_set_window(DevState st, const int32_t *ms, const int32_t *cs) {
+    const uint32_t doc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (doc >= (uint32_t)st.n_docs || ms[doc] < 0) return;
+    st.hdr[doc].min_seq = ms[doc];
+    st.hdr[doc].cur_seq = cs[doc];
+    st.hdr[doc].heap_n = 0;
+}
+
+int mt_start_collaboration(mt_handle *h, const int32_t *min_seq, const int32_t *cur_seq) {
+    if (!h || !min_seq || !cur_seq) return MT_E_INVALID;
+    for (uint32_t d = 0; d < h->n_docs; d++)
+        if (min_seq[d] >= 0 && cur_seq[d] < min_seq[d]) {
+            h->err = "mt_start_collaboration: document " + std::to_string(d) + " has currentSeq < minSeq";
+            return MT_E_INVALID;
+        }
+    HIPCHK(h, hipSetDevice(h->device));
+    int32_t *d_w = nullptr;
+    HIPCHK(h, hipMalloc(&d_w, (size_t)h->n_docs * 8 + 8));
+    bool ok = hipMemcpyAsync(d_w, min_seq, (size_t)h->n_docs * 4, hipMemcpyHostToDevice, h->stream) == hipSuccess &&
+              hipMemcpyAsync(d_w + h->n_docs, cur_seq, (size_t)h->n_docs * 4, hipMemcpyHostToDevice, h->stream) ==
+                  hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_set_window, dim3((h->n_docs + 255) / 256), dim3(256), 0, h->stream, h->st, d_w,
+                           d_w + h->n_docs);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
+    }
+    hipFree(d_w);
+    if (!ok) {
+        h->err = "mt_start_collaboration failed";
+        return MT_E_HIP;
+    }
+    return 0;
+}
+
 int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *seed_text) {
     if (!h) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));

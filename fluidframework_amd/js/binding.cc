@@ -167,6 +167,24 @@ napi_value LoadInitialText(napi_env env, napi_callback_info info) {
     return nullptr;
 }
 
+// startCollaboration(h, minSeq: Int32Array, currentSeq: Int32Array) -- per document, -1 = leave
+napi_value StartCollaboration(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *ms, *cs;
+    size_t nms, ncs;
+    if (!typed(env, argv[1], &ms, &nms) || !typed(env, argv[2], &cs, &ncs)) return nullptr;
+    if (nms != mt_num_docs(hd->h) || ncs != nms) {
+        napi_throw_range_error(env, nullptr, "minSeq / currentSeq must hold one entry per document");
+        return nullptr;
+    }
+    const int rc = mt_start_collaboration(hd->h, (const int32_t *)ms, (const int32_t *)cs);
+    if (rc) return throw_rc(env, hd, rc, "mt_start_collaboration");
+    return nullptr;
+}
+
 // applyOps(h, docOff: BigInt64Array, ops: Uint8Array (32-byte records), text: Uint16Array,
 //          props: Uint32Array) -- Client.applyMsg for every message (mt_apply_ops)
 napi_value ApplyOps(napi_env env, napi_callback_info info) {
@@ -375,6 +393,7 @@ napi_value Init(napi_env env, napi_value exports) {
         const char *name;
         napi_callback fn;
     } fns[] = {{"create", Create},         {"destroy", Destroy},           {"loadInitialText", LoadInitialText},
+                 {"startCollaboration", StartCollaboration},
                {"applyOps", ApplyOps},     {"loadSnapshots", LoadSnapshots},     {"status", Status},             {"getLength", GetLength},
                {"getText", GetText},       {"getPropRuns", GetPropRuns},   {"getDeltaLog", GetDeltaLog},
                {"deltaLogReset", DeltaLogReset},

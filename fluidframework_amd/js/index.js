@@ -196,9 +196,27 @@ class GpuClient {
         this._check();
     }
 
-    /** Client.startOrUpdateCollaboration (client.ts:1053-1073): the observer is short id 0. */
-    startOrUpdateCollaboration(longClientId) {
-        this.longClientId = longClientId;
+    /**
+     * Client.startOrUpdateCollaboration (client.ts:1053-1073): the observer is short id 0.
+     * The first call with an id starts the collab window at (minSeq, currentSeq)
+     * (MergeTree.startCollaboration, mergeTree.ts:1287-1294); later calls only rename it.
+     */
+    startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
+        if (longClientId === undefined) { return; }
+        if (this.longClientId === undefined) {
+            this.longClientId = longClientId;
+            if (minSeq !== 0 || currentSeq !== 0) {
+                this.batch.flush();
+                const ms = new Int32Array(this.batch.nDocs).fill(-1);
+                const cs = new Int32Array(this.batch.nDocs);
+                ms[this.doc] = minSeq;
+                cs[this.doc] = currentSeq;
+                native.startCollaboration(this.batch.h, ms, cs);
+                this.currentSeq = currentSeq;
+            }
+        } else {
+            this.longClientId = longClientId;
+        }
     }
 
     /** Client.applyMsg (client.ts:797-819); applied on the GPU at the next flush. */

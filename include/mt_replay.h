@@ -102,6 +102,13 @@ int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *
 /* Re-initialises every document from the contents last given to mt_load_initial_text
    (kept in HBM); asynchronous on the handle's stream. */
 int mt_reset(mt_handle *h);
+/* Client.startOrUpdateCollaboration(longClientId, minSeq, currentSeq) -> MergeTree.
+   startCollaboration (client.ts:1053-1073, mergeTree.ts:1287-1294): sets every listed
+   document's collab window (minSeq, currentSeq) before its first message; the zamboni heap
+   starts empty.  min_seq[d] < 0 leaves document d as it is; otherwise 0 <= min_seq[d] <=
+   cur_seq[d] (MT_E_INVALID).  Host arrays [n_docs]; mt_reset / mt_load_initial_text
+   return documents to (0, 0). */
+int mt_start_collaboration(mt_handle *h, const int32_t *min_seq, const int32_t *cur_seq);
 
 /* Client.applyMsg for every message of a batch (client.ts:797-819).  Records are grouped
    per document in sequence order: doc_op_off[n_docs+1] indexes ops.  Host buffers; the

@@ -235,6 +235,52 @@ def test_gpu_snapshot_emission_matches_reference(name, tier):
         assert got == doc["chunks"], (name, doc["doc"])
 
 
+@pytest.mark.parametrize("tier", ["lds", "hbm", "paged"])
+def test_gpu_start_collaboration_window(tier):
+    """startOrUpdateCollaboration(id, minSeq, currentSeq): a stream whose sequence numbers are
+    all shifted by K, replayed from window (K, K), ends in the same text, properties and
+    segments as the unshifted one from (0, 0); a message at or below the window's
+    currentSeq / minSeq fails as the reference's asserts (client.ts:824-826,
+    mergeTree.ts:1752-1755)."""
+    fx = gu.load("ref_c3")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    n = len(fx["docs"])
+    K = 1000
+    base = _gpu_batch(n, **TIERS[tier])
+    base.load_initial_text(a["seed_off"], a["seed"])
+    base.apply_arrays(a)
+    sh = dict(a, ops=a["ops"].copy())
+    for f in ("seq", "ref_seq", "min_seq"):
+        sh["ops"][f] += K
+    mt = _gpu_batch(n, **TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.start_collaboration(np.full(n, K, np.int32), np.full(n, K, np.int32))
+    mt.apply_arrays(sh)
+    assert (mt.status() == 0).all()
+    s0, s1 = base.checksums(), mt.checksums()
+    for f in ("length", "text_hash", "props_hash", "n_segments"):
+        assert np.array_equal(s0[f], s1[f]), f
+    for d in range(n):
+        assert mt.get_text(d) == base.get_text(d)
+    # the unshifted stream against window (K, K): its first message is not above currentSeq
+    bad = _gpu_batch(n, **TIERS[tier])
+    bad.load_initial_text(a["seed_off"], a["seed"])
+    bad.start_collaboration(np.full(n, K, np.int32), np.full(n, K, np.int32))
+    bad.apply_arrays(a)
+    assert (bad.status() == 2).all()   # MT_DOC_SEQ_ORDER, client.ts:462-463
+    # a stream above the window's currentSeq whose minSeq is below the window's minSeq
+    low = dict(sh, ops=sh["ops"].copy())
+    low["ops"]["seq"] += K
+    mt2 = _gpu_batch(n, **TIERS[tier])
+    mt2.load_initial_text(a["seed_off"], a["seed"])
+    mt2.start_collaboration(np.full(n, 2 * K, np.int32), np.full(n, 2 * K, np.int32))
+    mt2.apply_arrays(low)
+    assert (mt2.status() == 3).all()   # MT_DOC_MINSEQ_ORDER, client.ts:464-465
+    with pytest.raises(RuntimeError):
+        mt2.start_collaboration(np.full(n, 5, np.int32), np.full(n, 4, np.int32))
+
+
 # ---------------------------------------------------------------- error model
 @pytest.mark.parametrize("tier", list(TIERS))
 def test_gpu_error_model_matches_reference(tier):

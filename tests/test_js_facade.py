@@ -195,3 +195,44 @@ def test_js_facade_rich_callbacks_match_reference():
         bad = next((j for j, (x, y) in enumerate(zip(mine, d["events"])) if x != y), None)
         assert bad is None and len(mine) == len(d["events"]), (d["doc"], bad, mine[bad] if bad is not None else None,
                                                                d["events"][bad] if bad is not None else None)
+
+
+_WINDOW_JS = r"""
+const m = require(process.argv[1]);
+const b = new m.GpuMergeTreeBatch(2, {});
+b.loadInitialText(["abc", "abc"]);
+const c0 = b.client(0), c1 = b.client(1);
+c0.startOrUpdateCollaboration("obs");
+c1.startOrUpdateCollaboration("obs", 10, 10);
+const op = (seq, ref, msn, pos, text) => ({clientId: "w1", sequenceNumber: seq,
+    referenceSequenceNumber: ref, minimumSequenceNumber: msn, clientSequenceNumber: seq,
+    type: "op", contents: {type: 0, pos1: pos, seg: text}});
+c0.applyMsg(op(1, 0, 0, 0, "x")); c0.applyMsg(op(2, 1, 1, 4, "y"));
+c1.applyMsg(op(11, 10, 10, 0, "x")); c1.applyMsg(op(12, 11, 11, 4, "y"));
+const out = {t0: c0.getText(), t1: c1.getText(), s1: c1.getCurrentSeq()};
+c1.startOrUpdateCollaboration("renamed", 50, 50);   // already collaborating: rename only
+c1.applyMsg(op(13, 12, 12, 0, "z"));
+out.t2 = c1.getText();
+const b2 = new m.GpuMergeTreeBatch(1, {});
+b2.loadInitialText(["abc"]);
+const d = b2.client(0);
+d.startOrUpdateCollaboration("obs", 10, 10);
+d.applyMsg(op(5, 0, 0, 0, "q"));
+try { d.getText(); out.err = null; } catch (e) { out.err = e.message; }
+console.log(JSON.stringify(out));
+"""
+
+
+@pytest.mark.gpu
+def test_js_facade_start_collaboration_window():
+    """startOrUpdateCollaboration(id, minSeq, currentSeq) starts the document's collab window
+    there (MT/client.ts:1053-1073, MT/mergeTree.ts:1287-1294): a stream numbered from it
+    replays like the same stream numbered from 0; a later call only renames the client; a
+    message at or below the window fails with the reference's assertion."""
+    _addon()
+    r = subprocess.run(["node", "-e", _WINDOW_JS, JS], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout)
+    assert out["t0"] == out["t1"] == "xabcy" and out["s1"] == 12
+    assert out["t2"] == "zxabcy"
+    assert out["err"] == "Incoming remote op sequence# <= local collabWindow's currentSequence#"
