@@ -62,6 +62,8 @@ struct PageMeta {             // 12 bytes, indexed by page id (LDS footprint: do
 static_assert(sizeof(PageMeta) == 12, "PageMeta size");
 static __host__ __device__ inline int pm_bcnt(const PageMeta &m, int q) { return (int)((m.bc >> (4 * q)) & 15u); }
 static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { return (int8_t)((int)((m.flg2 >> (2 * q)) & 3u) - 1); }
+#define MT_OSLOTS 64
+#define MT_OSLOT_FREE 0x7FFFFFFF
 #define MT_PG_SLOTS 64
 // DocHdr.pad[] words used by paged documents
 #define HDR_PAGED 0           // 1: the document lives in the paged layout
@@ -86,6 +88,7 @@ struct DevState {
     uint16_t *text;
     uint32_t *props;
     int32_t *dlog;
+    int32_t *oslot;           // [n_docs][64][2] overlap slots: {client (MT_OSLOT_FREE), last seq}
     int32_t *retry;           // per document: replay (the rest of) this batch in the HBM tier
     int64_t *resume;          // per document: first op the HBM tier replays
     uint32_t *stats;          // [0]: documents replayed in the HBM tier by the last launch
@@ -176,19 +179,22 @@ __device__ __forceinline__ int seg_rcli(v4i a) { return (int)(short)((uint32_t)a
 __device__ __forceinline__ int pack_cli(int cli, int rcli) {
     return (int)(((uint32_t)(uint16_t)cli) | (((uint32_t)(uint16_t)rcli) << 16));
 }
-__device__ __forceinline__ bool ovl_has(u64 o, int c) {
-    const uint32_t sh = (uint32_t)(c - 1) & 63u;
+// removedClientOverlap (MT/mergeTree.ts:2577-2585) as a bit mask over the document's overlap
+// *slots*: a client that removes an already-removed segment takes a slot (1..64) for as long
+// as a segment it marked is unsettled (DocT.ocli, mt_engine.h oslot_alloc); s = 0: no slot
+__device__ __forceinline__ bool ovl_has(u64 o, int s) {
+    const uint32_t sh = (uint32_t)(s - 1) & 63u;
     const uint32_t w = sh < 32 ? (uint32_t)o : (uint32_t)(o >> 32);
-    return (c >= 1) & (c <= 64) & (((w >> (sh & 31u)) & 1u) != 0);
+    return (s >= 1) & (s <= 64) & (((w >> (sh & 31u)) & 1u) != 0);
 }
 
-// nodeLength for a leaf in a remote view (c, r)   MT/mergeTree.ts:1692-1732
-// (branch-free: every term is evaluated, no shift depends on an unchecked c)
-__device__ __forceinline__ int view_len(v4i a, u64 o, int r, int c) {
+// nodeLength for a leaf in a remote view (c, r)   MT/mergeTree.ts:1692-1732; cs = c's overlap
+// slot.  (branch-free: every term is evaluated, no shift depends on an unchecked slot)
+__device__ __forceinline__ int view_len(v4i a, u64 o, int r, int c, int cs) {
     const int len = a.x, seq = a.y, rseq = a.z;
     const int cli = seg_cli(a), rcli = seg_rcli(a);
     const bool ins = (cli == c) | ((seq != -1) & (seq <= r));
-    const bool gone = (rseq != MT_RSEQ_NONE) & ((rcli == c) | ovl_has(o, c) | ((rseq != -1) & (rseq <= r)));
+    const bool gone = (rseq != MT_RSEQ_NONE) & ((rcli == c) | ovl_has(o, cs) | ((rseq != -1) & (rseq <= r)));
     return (ins & !gone) ? len : 0;
 }
 // localNetLength (observer view)   MT/mergeTree.ts:1195-1206

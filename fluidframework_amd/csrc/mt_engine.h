@@ -122,7 +122,12 @@ template <class T> struct DocT {
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
     int rich;                          // rich delta log (segments' state, maintenance events)
-    int wide;               // an overlap mask holds a short id above 32 (DocHdr.pad0 bit 0)
+    int wide;               // an overlap mask holds a slot above 32 (DocHdr.pad0 bit 0)
+    // overlap slots (mt_device.h ovl_has): lane i holds the client owning slot i + 1
+    // (MT_OSLOT_FREE); ocs = the current message's client's slot (0: none)
+    int ocli;
+    int ocs;
+    GLB_AS int32_t *oslot;  // this document's [64][2] {client, last seq} in HBM
     int dlo;                // paged window: lowest slot written since the page was loaded /
                             // written back (only [dlo, n) goes back to HBM)
     // paged documents (mt_paged.h): this DocT is a window onto one page, or the instance
@@ -251,6 +256,35 @@ TD void fail_cap(DocT<T> &d, int cause) {
     fail(d, T::kLds ? MT_DOC_RETRY : MT_DOC_CAPACITY);
 }
 
+// ------------------------------------------------------------------ overlap slots
+// removedClientOverlap (MT/mergeTree.ts:2577-2585) is an unbounded list of client ids; a
+// segment's overlap set only matters while the segment is unsettled (a view with refSeq >=
+// minSeq sees a segment removed at <= minSeq as removed anyway).  So the masks index slots,
+// not ids: a client takes a slot at its first overlapping remove and keeps it while a segment
+// it marked may be unsettled (the slot's last use > minSeq); after that the slot is reused.
+// Bits a reused slot left on settled segments are never consulted.
+TD int oslot_of(DocT<T> &d, int c) {
+    const u64 m = ballot(d.ocli == c);
+    return m ? first_lane(m) + 1 : 0;
+}
+// A slot for client c (the current message's remover) within T::kOvlBits; 0: none free.
+TD int oslot_take(DocT<T> &d, int c) {
+    const int last = d.oslot[2 * lane() + 1];
+    const u64 m = ballot(lane() < T::kOvlBits && (d.ocli == MT_OSLOT_FREE || last <= d.min_seq));
+    if (!m) return 0;
+    const int s = first_lane(m);
+    if (lane() == s) d.ocli = c;
+    if (lane() == 0) d.oslot[2 * s] = c;
+    return s + 1;
+}
+// Would a remove by client c need a slot none of the first T::kOvlBits can give?
+TD bool oslot_short(DocT<T> &d, int c) {
+    if (oslot_of(d, c)) return false;
+    if (ballot(lane() < T::kOvlBits && d.ocli == MT_OSLOT_FREE)) return false;
+    const int last = d.oslot[2 * lane() + 1];
+    return !ballot(lane() < T::kOvlBits && last <= d.min_seq);
+}
+
 // paged instances (window: levels 0-1; upper levels: 1.. with level 1 = pages): B entries
 // for levels 0 and 1, B/2 for level 2, B/8 above -- a node holds >= 4 children after a split
 // or a repack, so level l + 1 has about a quarter of level l (growth is checked against bcap)
@@ -301,6 +335,9 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.P_cap = st.P;
     d.DL_cap = st.DL;
     d.rich = st.DLR;
+    d.oslot = (GLB_AS int32_t *)(st.oslot + doc * (size_t)(2 * MT_OSLOTS));
+    d.ocli = d.oslot[2 * lane()];
+    d.ocs = 0;
     d.scr = (LDS_AS int32_t *)(smem + L.offScr);
     d.nb = (LDS_AS int32_t *)(smem + L.offNb);
     d.ends = (LDS_AS uint16_t *)(smem + L.offEnds);
@@ -424,6 +461,7 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
         }
         for (int i = 1 + lane(); i <= d.heap_n; i += MT_WAVE) gH[i] = d.heap[i];
     }
+    d.oslot[2 * lane()] = d.ocli;
     for (int l = 0; l < d.depth; l++)
         for (int b = lane(); b < nbr(d, l); b += MT_WAVE) gcnt[l * B + b] = lvl(d, l)[b];
     for (int b = lane(); b < nbr(d, 0); b += MT_WAVE) gflg[b] = d.flg[b];
@@ -451,6 +489,7 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
         h.pad0 = d.wide;
 #pragma unroll
         for (int i = 0; i < 8; i++) h.pad[i] = 0;
+        h.pad[HDR_DIAG] = d.status ? d.cap_cause : 0;
         if (T::kLog) {
             h.pad[HDR_MSPLIT] = d.m_split;
             h.pad[HDR_MAPPEND] = d.m_append;
@@ -1164,7 +1203,7 @@ TD void boundary(DocT<T> &d, int p, int r, int c) {
         v4i a;
         u64 o;
         load_ao(d, i, v, a, o);
-        const int vl = v ? view_len(a, o, r, c) : 0;
+        const int vl = v ? view_len(a, o, r, c, d.ocs) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin = carry + inc;
         const u64 m = ballot(v && pex < p && p < pin);
@@ -1779,9 +1818,8 @@ TD bool lds_room(DocT<T> &d, const mt_op_rec &op) {
     if (d.heap_n + need_heap > d.H_cap) return false;
     bool ok = true;
     for (int l = 0; l < d.depth; l++) ok = ok && nbr(d, l) + 3 + 24 <= bcap(d, l);
-    // an overlapping remove by a short id above the LDS tier's u32 masks
-    const int oc = op_cli(op);
-    if (op.kind == MT_OP_REMOVE && oc > T::kOvlBits && oc <= 64) ok = false;
+    // an overlapping remove that would need a slot above the LDS tier's u32 masks
+    if (op.kind == MT_OP_REMOVE && oslot_short(d, op_cli(op))) ok = false;
     return ok;
 }
 
@@ -1830,7 +1868,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         v4i a;
         u64 o;
         load_ao(d, i, v, a, o);
-        const int vl = v ? view_len(a, o, r, c) : 0;
+        const int vl = v ? view_len(a, o, r, c, d.ocs) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin_ = carry + inc;
         const u64 ms = ballot(v && pex < p && p < pin_);
@@ -2132,21 +2170,29 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         u64 o;
         load_ao(d, i, v, a, o);
         const v4u bv = d.Bv[v ? i : 0];
-        const int vl = v ? view_len(a, o, r, c) : 0;
+        const int vl = v ? view_len(a, o, r, c, d.ocs) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin_ = carry + inc;
         const bool sel = v && vl > 0 && pex < p2 && pin_ > p1;
         const u64 sel_m = ballot(sel);
         if (sel_m) mark_dirty(d, base + first_lane(sel_m));
         bool newly = false, bad = false, spill = false;
+        const bool ovl_any = rem && ballot(sel && a.z != MT_RSEQ_NONE);
+        if (ovl_any) {   // this client's slot (taken at its first overlapping remove)
+            if (d.ocs == 0) d.ocs = oslot_take(d, c);
+            if (d.ocs > 32) d.wide = 1;
+            if (d.ocs && lane() == 0) d.oslot[2 * (d.ocs - 1) + 1] = seq;
+        }
         if (rem && sel) {
             if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
-                if (c < 1 || c > 64)
-                    bad = true;
-                else if (c > T::kOvlBits)
-                    spill = true;
-                else
-                    d.O[i] = (typename T::O_v)(o | (1ull << (c - 1)));
+                if (d.ocs == 0) {
+                    if (T::kOvlBits < 64)
+                        spill = true;
+                    else
+                        bad = true;
+                } else {
+                    d.O[i] = (typename T::O_v)(o | (1ull << (d.ocs - 1)));
+                }
             } else {
                 newly = true;
                 a.z = seq;
@@ -2172,6 +2218,8 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
             d.Bv[i] = nb;
         }
         if (ballot(bad)) {
+            // diagnostic 11: more than 64 clients' overlapping removes unsettled at once
+            if (ovl_any && d.ocs == 0 && d.status == 0) d.cap_cause = 11;
             fail(d, MT_DOC_CAPACITY);
             return true;
         }
@@ -2179,7 +2227,6 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
             fail_cap(d, 1);
             return true;
         }
-        if (rem && c > 32 && ballot(sel && a.z != MT_RSEQ_NONE && !newly)) d.wide = 1;
         if (!rem) d.props_top += __popcll(sel_m);
         wsync<T>();
         // fold the callback records in document order
@@ -2304,6 +2351,7 @@ TD void load_removed(DocT<T> &d, const mt_op_rec &op) {
 
 TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     const mt_op_rec &op = in.op;
+    d.ocs = oslot_of(d, op_cli(op));
     if (op.flags & MT_F_LOAD) {
         // SnapshotLoader.loadBody (MT/snapshotLoader.ts:195-227): insertSegments at
         // root.cachedLength in view (client, refSeq 0), no callback, no seq/msn update.  Its

@@ -351,7 +351,7 @@ TD void pg_split_page(PagedDoc<T> &pd) {
         v4i a;
         u64 o;
         load_ao(w, i, i < w.n, a, o);
-        const int dl = wave_sum(i < w.n ? view_len(a, o, pd.vr, pd.vc) : 0);
+        const int dl = wave_sum(i < w.n ? view_len(a, o, pd.vr, pd.vc, pd.w.ocs) : 0);
         if (lane() == 0) {
             pd.pvl[np] = dl;
             pd.pvl[pd.cur] -= dl;
@@ -488,7 +488,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
         if (e < pd.ut_n) {
             const int pg = pd.upage[e];
             const v4i a = pd.uA[e];
-            const int dlt = view_len(a, pd.uO[e], r, c) - obs_len(a);
+            const int dlt = view_len(a, pd.uO[e], r, c, pd.w.ocs) - obs_len(a);
             if (dlt && pg != cur) atomicAdd((int *)(pd.pvl + pg), dlt);
         }
     }
@@ -498,7 +498,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
         v4i a;
         u64 o;
         load_ao(w, i, i < w.n, a, o);
-        const int dlt = wave_sum(i < w.n ? view_len(a, o, r, c) - obs_len(a) : 0);
+        const int dlt = wave_sum(i < w.n ? view_len(a, o, r, c, w.ocs) - obs_len(a) : 0);
         if (i == 0) pd.pvl[cur] += dlt;
     }
     wsync<T>();
@@ -945,8 +945,8 @@ TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const int span = range ? min(max(op.pos2 - op.pos1, 0), 1 << 20) : 0;
     const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
-    // a narrow tier holds overlap masks of short ids 1..32 only
-    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && op_cli(op) > T::kOvlBits) return false;
+    // a narrow tier holds overlap slots 1..32 only
+    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
     if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
     if (pd.w.heap_n + hp_b > pd.PH) return false;
     if (nbr(pd.up, 1) + 8 > pd.PP) return false;
@@ -993,6 +993,7 @@ TD void pg_load_removed(PagedDoc<T> &pd, const mt_op_rec &op) {
 TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
+    w.ocs = oslot_of(w, op_cli(op));
     // a message creates <= 3 ids (load_removed finds the id its insert just created)
     if (w.next_uid + 4 > pd.UM && op.kind != MT_OP_LOAD_REMOVED) {
         pg_renumber(pd);
@@ -1192,6 +1193,9 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.P_cap = st.P;
     w.DL_cap = st.DL;
     w.rich = st.DLR;
+    w.oslot = (GLB_AS int32_t *)(st.oslot + doc * (size_t)(2 * MT_OSLOTS));
+    w.ocli = w.oslot[2 * lane()];
+    w.ocs = 0;
     w.S_cap = MT_PG_SLOTS;
     w.B_cap = PW_B;
     w.H_cap = pc.PH;
@@ -1323,6 +1327,7 @@ TD void pg_store(PagedDoc<T> &pd) {
     w.status = 0;
     pg_win_flush(pd);
     if (failed) w.status = failed;
+    w.oslot[2 * lane()] = w.ocli;
     wsync<T>();
     const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) pd.gdir[q] = up.dir[q];

@@ -38,10 +38,18 @@ __device__ static void init_doc_hdr(const DevState &st, int doc, int len) {
     st.hdr[doc] = h;
 }
 
+// every overlap slot free (one wave: lane i clears slot i)
+__device__ static void oslot_reset(const DevState &st, int doc) {
+    int32_t *o = st.oslot + (size_t)doc * 2 * MT_OSLOTS;
+    o[2 * lane()] = MT_OSLOT_FREE;
+    o[2 * lane() + 1] = 0;
+}
+
 __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *seed_off,
                                                   const uint16_t *seed) {
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
+    oslot_reset(st, doc);
     const int64_t s0 = seed_off ? seed_off[doc] : 0, s1 = seed_off ? seed_off[doc + 1] : 0;
     const int len = (int)(s1 - s0);
     uint16_t *text = st.text + (size_t)doc * 2 * st.T;
@@ -65,6 +73,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
                                                          const int32_t *cur_seq) {
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
+    oslot_reset(st, doc);
     const int n = nh[doc];
     const mt_seg_rec *rs = segs + off[doc];
     const size_t S = st.S, B = st.B;
@@ -369,6 +378,7 @@ __device__ static void gen_begin(GenCtx &g, const DevState &st, const mt_gen_cfg
         if (lane() == 0) arena[i] = ch;
     }
     if (lane() == 0) init_doc_hdr(st, doc, cfg.seed_len);
+    oslot_reset(st, doc);
     for (int j = lane(); j <= W; j += MT_WAVE) {
         g.last_ref[j] = 0;
         g.short_id[j] = 0;
@@ -494,13 +504,14 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
     for (int t = 1; t <= cfg.ops && d.status == 0; t++) {
         int r, c, msn;
         gen_pick(g, cfg, t, r, c, msn);
+        d.ocs = oslot_of(d, c);
         int vsum = 0;
         for (int base = 0; base < d.n; base += MT_WAVE) {
             const int i = base + lane();
             v4i a;
             u64 o;
             load_ao(d, i, i < d.n, a, o);
-            vsum += i < d.n ? view_len(a, o, r, c) : 0;
+            vsum += i < d.n ? view_len(a, o, r, c, d.ocs) : 0;
         }
         const int len = wave_sum(vsum);
         if (dbg_len && lane() == 0) {
@@ -716,6 +727,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
     for (int t = 1; t <= cfg.ops && w.status == 0; t++) {
         int r, c, msn;
         gen_pick(g, cfg, t, r, c, msn);
+        w.ocs = oslot_of(w, c);
         const int len = pg_views(pd, r, c);
         if (dbg_len && lane() == 0) {
             int32_t *q = dbg_len + ((int64_t)doc * cfg.ops + (t - 1)) * 4;
@@ -1179,6 +1191,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.cnt, N * MT_LV * st.B);
     alloc((void **)&st.flg, N * st.B);
     alloc((void **)&st.heap, N * (size_t)(st.H + 1) * sizeof(int2));
+    alloc((void **)&st.oslot, N * (size_t)(2 * MT_OSLOTS) * sizeof(int32_t));
     alloc((void **)&st.text, N * 2 * (size_t)st.T * sizeof(uint16_t));
     alloc((void **)&st.props, N * 2 * (size_t)st.P * MT_PREC * sizeof(uint32_t));
     if (st.DL) alloc((void **)&st.dlog, N * (size_t)st.DL * sizeof(int32_t));
@@ -1219,7 +1232,7 @@ void mt_destroy(mt_handle *h) {
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
-                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap};
+                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);

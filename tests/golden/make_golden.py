@@ -35,6 +35,9 @@ FIXTURES = {
                            "p_len_continue": 0.8, "p_insert_props": 0.3, "n_keys": 4,
                            "max_keys_per_op": 3, "p_marker": 0.05, "p_rewrite": 0.2, "p_combine": 0.4,
                            "p_group": 0.05, "p_noop": 0.02, "p_empty": 0.02, "p_oob": 0.02}, 8),
+    # 200 writers, lag 100: overlapping removes by short ids far above 64 (removedClientOverlap
+    # is an unbounded list; the device masks index reusable overlap slots)
+    "ref_wide": ("c4", {"ops": 4000, "writers": 200, "lag": 100, "seed": 7171}, 2),
     # a long-lived document: 30k messages (~45k segment ids created, ~12k live segments)
     "ref_c3_long": ("c3", {"ops": 30000}, 2),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),

@@ -15,7 +15,7 @@ MAINT_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INT_MIN = -2 ** 31
 ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_long", "ref_farm", "ref_c3_full",
-                "ref_c4_full", "ref_combine"]
+                "ref_c4_full", "ref_combine", "ref_wide"]
 # the configs' full stream lengths (10k messages per document)
 FULL_FIXTURES = ["ref_c3_full", "ref_c4_full"]
 # long-lived documents (30k messages)

@@ -32,15 +32,15 @@ TIERS = {
     "lds": dict(lds_seg_capacity=0),
     "hbm": dict(lds_seg_capacity=-1),
     "tiny": dict(lds_seg_capacity=16),
-    "paged": dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=1024),
-    "tiny_paged": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024),
+    "paged": dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048),
+    "tiny_paged": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048),
     # a tight paged tier far below the documents' needs: documents are handed to the
     # full-capacity paged launch mid-batch (and at load), generators regenerate there
-    "tight": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024, page_heap_capacity=1024,
+    "tight": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
                   lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40),
     # a narrow tight tier (32-bit overlap masks): documents whose clients above 32 remove
     # overlapping ranges (C4: 64 writers) move to the full tier
-    "narrow": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=1024, page_heap_capacity=1024,
+    "narrow": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
                    lds_page_capacity=200, lds_unsettled_capacity=600, lds_page_heap_capacity=600,
                    lds_narrow_overlap=1),
 }
@@ -128,13 +128,16 @@ def test_gpu_maintenance_events_match_reference(name, tier):
 
 
 @pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged", "tight", "narrow"])
-@pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6), ("c3", 3000, 4)])
+@pytest.mark.parametrize("cfgname,ops,docs", [("c2", 400, 16), ("c3", 400, 16), ("c4", 500, 6), ("c3", 3000, 4),
+                                              ("c4w", 1500, 4)])
 def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     import json
     import os
     if ops > 1000 and tier in ("hbm", "lds"):
         pytest.skip("long streams: paged tiers only")
-    cfg = json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))[cfgname]
+    configs = json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))
+    # c4w: 200 writers -- overlapping removes by short ids far above 64 (reused overlap slots)
+    cfg = dict(configs["c4"], writers=200, lag=100) if cfgname == "c4w" else configs[cfgname]
     cfg = dict(cfg, ops=ops)
     mt = _gpu_batch(docs, **TIERS[tier])
     b = mt.generate(cfg)
@@ -279,6 +282,19 @@ def test_gpu_start_collaboration_window(tier):
     assert (mt2.status() == 3).all()   # MT_DOC_MINSEQ_ORDER, client.ts:464-465
     with pytest.raises(RuntimeError):
         mt2.start_collaboration(np.full(n, 5, np.int32), np.full(n, 4, np.int32))
+
+
+def test_gpu_overlap_slots_exhausted_fail_loudly():
+    """More than 64 clients whose overlapping removes are unsettled at once (200 writers, lag
+    400: ~80) exceed the full tier's overlap slots: the document fails with MT_DOC_CAPACITY,
+    diagnostic 11 -- never a wrong result (DESIGN.md 'Known deviations')."""
+    import json
+    import os
+    cfg = json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))["c4"]
+    cfg = dict(cfg, writers=200, lag=400, ops=3000)
+    mt = _gpu_batch(2, **TIERS["paged"])
+    with pytest.raises(RuntimeError, match=r"status 4 \(diagnostic 11\)"):
+        mt.generate(cfg)
 
 
 # ---------------------------------------------------------------- error model
