@@ -1386,20 +1386,45 @@ TD void pg_store(PagedDoc<T> &pd) {
     }
 }
 
+// A flat document's state: segment table, per-level child counts (level stride B), leaf
+// needsScour flags and heap -- in the flat HBM arrays, or a summary load's staging buffers.
+struct FlatSrc {
+    GLB_AS const v4i *A;
+    GLB_AS const u64 *O;
+    GLB_AS const v4u *Bv;
+    GLB_AS const uint8_t *cnt;
+    GLB_AS const int8_t *flg;
+    GLB_AS const v2i *heap;
+    size_t B;
+};
+__device__ __forceinline__ FlatSrc flat_src(const DevState &st, int doc) {
+    const size_t S = st.S, B = st.B;
+    FlatSrc f;
+    f.A = (GLB_AS const v4i *)(st.segA + doc * S);
+    f.O = (GLB_AS const u64 *)(st.segO + doc * S);
+    f.Bv = (GLB_AS const v4u *)(st.segB + doc * S);
+    f.cnt = (GLB_AS const uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
+    f.flg = (GLB_AS const int8_t *)(st.flg + doc * B);
+    f.heap = (GLB_AS const v2i *)(st.heap + doc * (size_t)(st.H + 1));
+    f.B = B;
+    return f;
+}
+
 // Converts a flat document (state in the flat HBM arrays: initial contents, or spilled by
-// the LDS tier) into the paged layout: page j = level-1 node j (the whole tree when the
-// root is a leaf block).  Leaves the paged state staged in LDS (pg_store writes it).
-TD bool pg_convert(PagedDoc<T> &pd, const DevState &st, int doc) {
+// the LDS tier; or a large summary header staged by k_load_header) into the paged layout:
+// page j = level-1 node j (the whole tree when the root is a leaf block).  Leaves the paged
+// state staged in LDS (pg_store writes it).
+TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     const DocHdr h = *w.hp;
-    const size_t S = st.S, B = st.B;
-    GLB_AS const v4i *fA = (GLB_AS const v4i *)(st.segA + doc * S);
-    GLB_AS const u64 *fO = (GLB_AS const u64 *)(st.segO + doc * S);
-    GLB_AS const v4u *fB = (GLB_AS const v4u *)(st.segB + doc * S);
-    GLB_AS const uint8_t *fc = (GLB_AS const uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
-    GLB_AS const int8_t *ff = (GLB_AS const int8_t *)(st.flg + doc * B);
-    GLB_AS const v2i *fH = (GLB_AS const v2i *)(st.heap + doc * (size_t)(st.H + 1));
+    const size_t B = src.B;
+    GLB_AS const v4i *fA = src.A;
+    GLB_AS const u64 *fO = src.O;
+    GLB_AS const v4u *fB = src.Bv;
+    GLB_AS const uint8_t *fc = src.cnt;
+    GLB_AS const int8_t *ff = src.flg;
+    GLB_AS const v2i *fH = src.heap;
     const int depth = h.depth;
     const int np = depth == 1 ? 1 : h.n_blk[1];
     if (np + 8 > pd.PP || h.heap_n > pd.PH) {

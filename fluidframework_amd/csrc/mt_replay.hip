@@ -67,21 +67,35 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
 // startOrUpdateCollaboration(minSeq, seq) (MT/mergeTree.ts:1287-1304: fresh zamboni heap).
 // Body segments are appended afterwards by replaying MT_F_LOAD records (mt_load_snapshots).
 #define MT_LOAD_FANOUT (MT_MAXN - 1)
+// Staging for summary headers larger than the flat capacities on a paged handle: the flat
+// tree is built here (off[2d] = first segment, off[2d+1] = first leaf block of document d;
+// -1: the document uses the flat HBM arrays), then k_load_convert pages it.
+struct LoadScratch {
+    v4i *A;
+    u64 *O;
+    v4u *B;
+    uint8_t *cnt;   // [MT_LV][nb0] per document
+    int8_t *flg;
+    const int64_t *off;
+};
 __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int64_t *off, const int32_t *nh,
                                                          const mt_seg_rec *segs, const uint16_t *tin,
                                                          const uint32_t *pin, const int32_t *min_seq,
-                                                         const int32_t *cur_seq) {
+                                                         const int32_t *cur_seq, LoadScratch sc) {
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     oslot_reset(st, doc);
     const int n = nh[doc];
     const mt_seg_rec *rs = segs + off[doc];
-    const size_t S = st.S, B = st.B;
+    const bool big = sc.off && sc.off[2 * doc] >= 0;
     uint16_t *text = st.text + (size_t)doc * 2 * st.T;
     uint32_t *props = st.props + (size_t)doc * 2 * st.P * MT_PREC;
-    int status = n > st.S ? MT_DOC_CAPACITY : 0;
     const int nb0 = n > 0 ? (n + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT : 1;
-    if (nb0 > st.B) status = MT_DOC_CAPACITY;
+    int status = !big && (n > st.S || nb0 > st.B) ? MT_DOC_CAPACITY : 0;
+    const size_t B = big ? (size_t)nb0 : st.B;   // stride of a level's counts
+    v4i *dA = big ? sc.A + sc.off[2 * doc] : st.segA + doc * (size_t)st.S;
+    u64 *dO = big ? sc.O + sc.off[2 * doc] : st.segO + doc * (size_t)st.S;
+    v4u *dB = big ? sc.B + sc.off[2 * doc] : st.segB + doc * (size_t)st.S;
     int ttop = 0, ptop = 1;
     for (int base = 0; base < n && status == 0; base += MT_WAVE) {
         const int i = base + lane();
@@ -134,10 +148,10 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
             uint32_t w = 0;
             if (tl > 0) w = SEGF_NL_KNOWN | (tin[r.payload + tl - 1] == '\n' ? SEGF_NL : 0u);
             if (nm) w |= SEGF_NOMATCH;
-            st.segA[doc * S + i] = v4i{r.len, r.seq, r.removed_seq, pack_cli(r.client, rem ? r.removed_client : 0)};
-            st.segO[doc * S + i] = 0ull;
-            st.segB[doc * S + i] = v4u{marker ? r.payload : (uint32_t)toff, hp ? (uint32_t)ph : 0u,
-                                       (uint32_t)(i + 1) | (marker ? MT_MARKER_BIT : 0u), w};
+            dA[i] = v4i{r.len, r.seq, r.removed_seq, pack_cli(r.client, rem ? r.removed_client : 0)};
+            dO[i] = 0ull;
+            dB[i] = v4u{marker ? r.payload : (uint32_t)toff, hp ? (uint32_t)ph : 0u,
+                        (uint32_t)(i + 1) | (marker ? MT_MARKER_BIT : 0u), w};
         }
         ttop = tend;
         ptop = pend;
@@ -145,7 +159,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
     // block counts, level by level (blocks of 7, the last one takes the rest)
     int nbl[MT_LV];
     int depth = 0, cnt_below = n > 0 ? n : 0, nl = nb0;
-    uint8_t *cnt = st.cnt + (size_t)doc * MT_LV * B;
+    uint8_t *cnt = big ? sc.cnt + MT_LV * sc.off[2 * doc + 1] : st.cnt + (size_t)doc * MT_LV * B;
+    int8_t *flg = big ? sc.flg + sc.off[2 * doc + 1] : st.flg + (size_t)doc * B;
     for (int l = 0; l < MT_LV; l++) nbl[l] = 0;
     while (status == 0) {
         if (depth >= MT_LV) {
@@ -160,7 +175,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
         cnt_below = nl;
         nl = (nl + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT;
     }
-    for (int b = lane(); b < nb0 && b < st.B; b += MT_WAVE) st.flg[doc * B + b] = MT_SCOUR_UNDEF;
+    for (int b = lane(); b < nb0 && (big || b < st.B); b += MT_WAVE) flg[b] = MT_SCOUR_UNDEF;
     if (lane() == 0) {
         DocHdr h;
         memset(&h, 0, sizeof(h));
@@ -605,7 +620,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
             }
             return;
         }
-    } else if (!pg_convert(pd, st, doc)) {
+    } else if (!pg_convert(pd, flat_src(st, doc))) {
         // stays flat (the pages written so far are unreferenced): the next tier converts it
         // again, or only the status changes
         if (pc.tight && w.status == MT_DOC_CAPACITY) {
@@ -709,7 +724,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
     PagedDoc<T> pd;
     pg_setup(pd, st, doc, smem, L, pc);
     DocT<T> &w = pd.w;
-    if (w.status || !pg_convert(pd, st, doc)) {
+    if (w.status || !pg_convert(pd, flat_src(st, doc))) {
         if (lane() == 0) {
             if (pc.tight && w.status == MT_DOC_CAPACITY) {
                 st.retry[doc] = 2;
@@ -757,6 +772,35 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
     }
     pg_store(pd);
     pg_peaks(st, pd, pk_ut, pk_heap);
+}
+
+// A summary header staged by k_load_header (LoadScratch) becomes a paged document at the
+// handle's full paged capacities (pg_convert from the staging buffers); the body appends
+// then replay like any paged document's messages.
+template <class T>
+__global__ void __launch_bounds__(MT_WAVE) k_load_convert(DevState st, LoadScratch sc, PagedCaps pc) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
+    const int doc = blockIdx.x;
+    if (doc >= st.n_docs || sc.off[2 * doc] < 0 || st.hdr[doc].status) return;
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v));
+    PagedDoc<T> pd;
+    pg_setup(pd, st, doc, smem, L, pc);
+    DocT<T> &w = pd.w;
+    FlatSrc src;
+    src.A = (GLB_AS const v4i *)(sc.A + sc.off[2 * doc]);
+    src.O = (GLB_AS const u64 *)(sc.O + sc.off[2 * doc]);
+    src.Bv = (GLB_AS const v4u *)(sc.B + sc.off[2 * doc]);
+    src.cnt = (GLB_AS const uint8_t *)(sc.cnt + MT_LV * sc.off[2 * doc + 1]);
+    src.flg = (GLB_AS const int8_t *)(sc.flg + sc.off[2 * doc + 1]);
+    src.heap = nullptr;   // a fresh collaboration: heap_n == 0
+    src.B = (size_t)w.hp->n_blk[0];
+    if (w.status == 0 && pg_convert(pd, src)) {
+        pg_store(pd);
+    } else if (lane() == 0) {
+        st.hdr[doc].status = w.status == MT_DOC_RETRY || w.status == 0 ? MT_DOC_CAPACITY : w.status;
+        st.hdr[doc].pad[HDR_DIAG] = w.cap_cause;
+    }
 }
 
 // ---------------------------------------------------------------- checksums
@@ -1170,7 +1214,8 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
                                 (const void *)k_generate_paged<TierPagedT<false>>,
                                 (const void *)k_replay_paged<TierPagedT<true, true>>,
                                 (const void *)k_replay_paged<TierPagedT<false, true>>,
-                                (const void *)k_generate_paged<TierPagedT<false, true>>};
+                                (const void *)k_generate_paged<TierPagedT<false, true>>,
+                                (const void *)k_load_convert<TierPagedT<false>>};
             for (const void *k : ks)
                 if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess) {
                     delete h;
@@ -1486,12 +1531,17 @@ struct mt_snapshots {
     uint16_t *text = nullptr;
     uint32_t *props = nullptr;
     mt_batch *body = nullptr;   // loadBody appends as MT_F_LOAD records (nullptr: none)
+    // headers larger than the flat capacities on a paged handle (k_load_convert)
+    LoadScratch sc = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    int64_t *sc_off = nullptr;
+    bool any_big = false;
 };
 
 void mt_snapshots_free(mt_snapshots *s) {
     if (!s) return;
     hipSetDevice(s->device);
-    void *ps[] = {s->off, s->nh, s->min_seq, s->cur_seq, s->segs, s->text, s->props};
+    void *ps[] = {s->off, s->nh, s->min_seq, s->cur_seq, s->segs, s->text, s->props, s->sc.A, s->sc.O, s->sc.B,
+                  s->sc.cnt, s->sc.flg, s->sc_off};
     for (void *p : ps)
         if (p) hipFree(p);
     mt_batch_free(s->body);
@@ -1535,6 +1585,31 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
          (!n_segs || hipMemcpy(s->segs, segs, n_segs * sizeof(mt_seg_rec), hipMemcpyHostToDevice) == hipSuccess) &&
          (!text_len || hipMemcpy(s->text, text, text_len * 2, hipMemcpyHostToDevice) == hipSuccess) &&
          (!props_len || hipMemcpy(s->props, props, props_len * 4, hipMemcpyHostToDevice) == hipSuccess);
+    // a header beyond the flat capacities is staged and paged (handles with a paged layout)
+    if (ok && h->st.PP > 0) {
+        std::vector<int64_t> so((size_t)N * 2, -1);
+        int64_t ns = 0, nb = 0;
+        for (uint32_t d = 0; d < N; d++) {
+            const int64_t n = n_header[d], nb0 = n > 0 ? (n + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT : 1;
+            if (n > h->st.S || nb0 > h->st.B) {
+                so[2 * d] = ns;
+                so[2 * d + 1] = nb;
+                ns += n;
+                nb += nb0;
+            }
+        }
+        if (ns > 0) {
+            s->any_big = true;
+            ok = hipMalloc(&s->sc.A, ns * sizeof(int4)) == hipSuccess &&
+                 hipMalloc(&s->sc.O, ns * sizeof(u64)) == hipSuccess &&
+                 hipMalloc(&s->sc.B, ns * sizeof(uint4)) == hipSuccess &&
+                 hipMalloc(&s->sc.cnt, (size_t)nb * MT_LV) == hipSuccess &&
+                 hipMalloc(&s->sc.flg, (size_t)nb) == hipSuccess &&
+                 hipMalloc(&s->sc_off, (size_t)N * 16) == hipSuccess &&
+                 hipMemcpy(s->sc_off, so.data(), (size_t)N * 16, hipMemcpyHostToDevice) == hipSuccess;
+            s->sc.off = s->sc_off;
+        }
+    }
     if (!ok) {
         h->err = "mt_snapshots_upload: device allocation/copy failed";
         mt_snapshots_free(s);
@@ -1611,8 +1686,15 @@ int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
     if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
     HIPCHK(h, hipEventRecord(h->ev_load, h->stream));
     hipLaunchKernelGGL(k_load_header, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, s->off, s->nh, s->segs,
-                       s->text, s->props, s->min_seq, s->cur_seq);
+                       s->text, s->props, s->min_seq, s->cur_seq, s->sc);
     HIPCHK(h, hipGetLastError());
+    if (s->any_big) {
+        const PagedCaps &pc = h->pg_full;
+        const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, 8).total;
+        hipLaunchKernelGGL(k_load_convert<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                           s->sc, pc);
+        HIPCHK(h, hipGetLastError());
+    }
     if (s->body) return mt_batch_apply_async(h, s->body);
     return 0;
 }

@@ -125,7 +125,10 @@ int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, 
    segs[doc_seg_off[d] .. doc_seg_off[d+1]), the first n_header[d] from the header chunk;
    payload / props index the text (UTF-16) and props arenas.  A document whose load fails
    like the reference's ("MergeTree insert failed") gets that status.  Catch-up
-   and tail messages then go through mt_apply_ops as usual.  Synchronous. */
+   and tail messages then go through mt_apply_ops as usual.  On a handle with a paged
+   layout (page_capacity > 0) a header larger than seg_capacity is staged and built
+   straight into pages (its text / property records still need text_capacity /
+   props_capacity); otherwise it fails with MT_DOC_CAPACITY.  Synchronous. */
 int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,
                       uint64_t n_segs, const uint16_t *text, uint64_t text_len, const uint32_t *props,
                       uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq);

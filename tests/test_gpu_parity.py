@@ -176,7 +176,13 @@ def test_gpu_generator_matches_oracle(oracle_lib, cfgname, ops, docs, tier):
     assert mt.maintenance_counts().tolist() == omaint
 
 
-@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged"])
+# summary headers larger than the flat capacities (48 segments) on a paged handle: staged by
+# k_load_header and paged by k_load_convert at load
+SNAP_TIERS = dict(TIERS, paged_load=dict(seg_capacity=48, lds_seg_capacity=16, props_capacity=4096,
+                                         page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048))
+
+
+@pytest.mark.parametrize("tier", ["lds", "hbm", "paged", "tiny_paged", "paged_load"])
 @pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
 def test_gpu_snapshot_load_matches_reference(name, tier):
     """Config C5 (cold catch-up) through mt_load_snapshots: after the load the device tree
@@ -187,9 +193,12 @@ def test_gpu_snapshot_load_matches_reference(name, tier):
     docs = [d for d in fx["docs"] if gu.snap_status(d) is not None]
     interner = gu.Interner()
     la, oa = gu.encode_snap_docs(fx, interner, docs)
-    mt = _gpu_batch(len(docs), **TIERS[tier])
+    mt = _gpu_batch(len(docs), **SNAP_TIERS[tier])
     mt.load_snapshots(la)
     st = mt.status()
+    if tier == "paged_load":   # the large headers were paged at load
+        big = [i for i in range(len(docs)) if la["n_header"][i] > 48 and st[i] == 0]
+        assert big and all(mt.is_paged(i) for i in big)
     bad = []
     for i, doc in enumerate(docs):
         want = gu.snap_status(doc)
