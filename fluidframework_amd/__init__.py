@@ -35,14 +35,14 @@ class MergeTreeBatch:
                  text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0,
                  page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0,
                  lds_page_capacity=0, lds_unsettled_capacity=0, lds_page_heap_capacity=0, lds_narrow_overlap=0,
-                 delta_log_mode=0):
+                 delta_log_mode=0, live_client=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
                                 text_capacity, props_capacity, delta_log_capacity,
                                 lds_seg_capacity, page_capacity, page_heap_capacity,
                                 unsettled_capacity, uid_capacity, lds_page_capacity,
                                 lds_unsettled_capacity, lds_page_heap_capacity, lds_narrow_overlap,
-                                delta_log_mode)
+                                delta_log_mode, live_client)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")
@@ -306,6 +306,27 @@ class MergeTreeBatch:
         (needs delta_log_capacity > 0)."""
         out = np.zeros((self.n_docs, 3), dtype=np.uint32)
         self._check(self.lib.mt_maintenance_counts(self.h, _native.ptr(out)), "mt_maintenance_counts")
+        return out
+
+    # -------------------------------------------------------------- live-client handles
+    def regenerate_pending(self, doc, cap=4096, text_cap=1 << 16, props_cap=1 << 16):
+        """mt_regenerate_pending: the ops rebuilt from the oldest pending segment group
+        (records, text, props), or None when nothing is pending."""
+        out = np.zeros(cap, dtype=_native.REGEN_DTYPE)
+        text = np.zeros(text_cap, dtype=np.uint16)
+        props = np.zeros(props_cap, dtype=np.uint32)
+        n = ctypes.c_int32(0)
+        self._check(self.lib.mt_regenerate_pending(self.h, doc, _native.ptr(out), cap, ctypes.byref(n),
+                                                   _native.ptr(text), text_cap, _native.ptr(props), props_cap),
+                    "mt_regenerate_pending")
+        if n.value < 0:
+            return None
+        return out[:n.value], text, props
+
+    def pending_counts(self):
+        """[n_docs, 2]: collabWindow.localSeq and the pending segment groups per document."""
+        out = np.zeros((self.n_docs, 2), dtype=np.int32)
+        self._check(self.lib.mt_pending_counts(self.h, _native.ptr(out)), "mt_pending_counts")
         return out
 
     def checksums(self):

@@ -25,7 +25,12 @@ class MtOptions(ctypes.Structure):
                 ("unsettled_capacity", ctypes.c_int32), ("uid_capacity", ctypes.c_int32),
                 ("lds_page_capacity", ctypes.c_int32), ("lds_unsettled_capacity", ctypes.c_int32),
                 ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32),
-                ("delta_log_mode", ctypes.c_int32)]
+                ("delta_log_mode", ctypes.c_int32), ("live_client", ctypes.c_int32)]
+
+
+# mt_regen_rec (include/mt_replay.h): one op of regeneratePendingOp
+REGEN_DTYPE = np.dtype([("kind", "<i4"), ("pos1", "<i4"), ("pos2", "<i4"), ("local_seq", "<i4"),
+                        ("text_off", "<u4"), ("text_len", "<u4"), ("props_off", "<u4"), ("flags", "<u4")])
 
 
 class MtGenCfg(ctypes.Structure):
@@ -79,6 +84,9 @@ SIGNATURES = [
     ("mt_maintenance_counts", _I, [_P, _P]),
     ("mt_checksums", _I, [_P, _P]),
     ("mt_checksums_device", _I, [_P, _P]),
+    ("mt_regenerate_pending", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P, _U32]),
+    ("mt_pending_counts", _I, [_P, _P]),
+    ("mt_debug_heap", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
 ]
 
 _lib = None

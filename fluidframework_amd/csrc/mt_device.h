@@ -108,6 +108,9 @@ struct DevState {
     int32_t S, B, H, T, P, DL;
     int32_t DLR;              // rich delta log: segment text / properties + maintenance events
     int32_t n_docs;
+    // live-client handles (mt_options.live_client; null otherwise)
+    int32_t *live;            // [n_docs][4] {collabWindow.localSeq, group queue head id, length, 0}
+    int32_t *grp;             // [n_docs][MT_LIVE_GROUPS + 1][MT_GRP_WORDS] segment-group table
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -204,3 +207,37 @@ __device__ __forceinline__ bool tie(v4i a, int r) {
     const int rs = a.z;
     return !((rs != MT_RSEQ_NONE) & (rs != 0) & (rs <= r) & (rs != -1)) & (a.y != -1);
 }
+
+// ------------------------------------------------------------------ live-client documents
+// A live handle (mt_options.live_client) backs a participant Client: the local client (short
+// id 0) applies its own ops before they are sequenced (MT/client.ts:164-274).  Unacked
+// sequence numbers are encoded above every real one: a pending insert has seq =
+// MT_LOCAL_BASE + localSeq, a pending local remove removedSeq = MT_LOCAL_BASE +
+// localRemovedSeq (UnassignedSequenceNumber + the segment's localSeq / localRemovedSeq,
+// MT/mergeTree.ts:2102-2104, 2669-2670), so every `seq != Unassigned && seq <= refSeq` test
+// of the observer engine holds unchanged.  Segment groups (MT/mergeTree.ts:1955-1962,
+// segmentGroupCollection.ts) are a FIFO of up to 4 group ids (1..255) per segment in bits
+// 32..63 of its segO word (the overlap slots keep bits 0..31); the group table lives in HBM.
+#define MT_LOCAL_BASE 0x40000000
+#define MT_LIVE_GROUPS 255       // group ids 1..255 (outstanding segment groups per document)
+#define MT_GRP_WORDS 12          // group entry {localSeq, kind | rewrite << 8 | nkeys << 16, keys[8], 0, 0}
+__device__ __forceinline__ bool is_local_seq(int s) { return s >= MT_LOCAL_BASE && s != MT_RSEQ_NONE; }
+__device__ __forceinline__ uint32_t pend_word(u64 o) { return (uint32_t)(o >> 32); }
+__device__ __forceinline__ int pend_first(u64 o) { return (int)(pend_word(o) & 0xFFu); }
+__device__ __forceinline__ u64 pend_pop(u64 o) { return (o & 0xFFFFFFFFull) | ((u64)(pend_word(o) >> 8) << 32); }
+// enqueue group g at the tail of the segment's FIFO; false when it holds 4 already
+__device__ __forceinline__ bool pend_push(u64 &o, int g) {
+    const uint32_t w = pend_word(o);
+    const int n = w == 0 ? 0 : (w >> 8) == 0 ? 1 : (w >> 16) == 0 ? 2 : (w >> 24) == 0 ? 3 : 4;
+    if (n == 4) return false;
+    o |= (u64)((uint32_t)g << (8 * n)) << 32;
+    return true;
+}
+// breakTie for the local client's own insert (MT/mergeTree.ts:2290-2298: "local change see
+// everything" after the removed-at-or-below-refSeq test)
+__device__ __forceinline__ bool tie_local(v4i a, int r) {
+    const int rs = a.z;
+    return !((rs != MT_RSEQ_NONE) & (rs != 0) & (rs <= r) & (rs != -1));
+}
+// breakTie for a remote client on a live document: an unacked local segment never ties
+__device__ __forceinline__ bool tie_remote_live(v4i a, int r) { return tie(a, r) & !is_local_seq(a.y); }

@@ -28,6 +28,7 @@ template <bool kLogT> struct TierLdsT {
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = false;
+    static constexpr bool kLive = false;
     // removedClientOverlap masks of short ids 1..32 (4 bytes per segment in LDS); a
     // document that needs ids 33..64 continues in the next tier (lds_room / load_doc)
     static constexpr int kOvlBits = 32;
@@ -41,7 +42,23 @@ template <bool kLogT> struct TierGlbT {
     static constexpr bool kLds = false;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = false;
+    static constexpr bool kLive = false;
     static constexpr int kOvlBits = 64;
+    typedef u64 O_v;
+    typedef GLB_AS v4i *A_t;
+    typedef GLB_AS u64 *O_t;
+    typedef GLB_AS v4u *B_t;
+    typedef GLB_AS v2i *H_t;
+};
+// Live-client documents (mt_device.h MT_LOCAL_BASE): the HBM tier plus the local client's
+// unacked ops and segment groups (MT/client.ts:164-274, 589-626, 709-893).  Overlap slots use
+// bits 0..31 of segO, the segment-group FIFO bits 32..63.
+template <bool kLogT> struct TierLiveT {
+    static constexpr bool kLds = false;
+    static constexpr bool kLog = kLogT;
+    static constexpr bool kPaged = false;
+    static constexpr bool kLive = true;
+    static constexpr int kOvlBits = 32;
     typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
@@ -58,6 +75,7 @@ template <bool kLogT, bool kNarrowT = false> struct TierPagedT {
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;
+    static constexpr bool kLive = false;
     static constexpr int kOvlBits = kNarrowT ? 32 : 64;
     typedef typename std::conditional<kNarrowT, uint32_t, u64>::type O_v;
     typedef LDS_AS v4i *A_t;
@@ -137,6 +155,12 @@ template <class T> struct DocT {
     int pend_split;         // the page reached MaxNodesInBlock leaf blocks: split it after the op
     int pend_second;        // leaf block split while a page split was pending (-1: none)
     LDS_AS uint16_t *dir;   // upper instance: page ids in level-1 order (moved with level 1)
+    // live-client documents (T::kLive): collabWindow.localSeq, the segment-group queue
+    // (head id, length; MT/mergeTree.ts pendingSegments) and the current message's group
+    int local_seq, g_head, g_n;
+    int lop;                // the current message is the local client's own op
+    int lg;                 // its segment group id
+    GLB_AS int32_t *grp;    // [MT_LIVE_GROUPS + 1][MT_GRP_WORDS] group table (index = id)
 #ifdef MT_PROF
     LDS_AS u64 *prof;       // [32] section timers
 #endif
@@ -379,6 +403,15 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.pend_split = 0;
     d.pend_second = -1;
     d.dir = nullptr;
+    d.lop = 0;
+    d.lg = 0;
+    if constexpr (T::kLive) {
+        const GLB_AS int32_t *lv = (const GLB_AS int32_t *)(st.live + 4 * (size_t)doc);
+        d.local_seq = lv[0];
+        d.g_head = lv[1];
+        d.g_n = lv[2];
+        d.grp = (GLB_AS int32_t *)(st.grp + (size_t)doc * (MT_LIVE_GROUPS + 1) * MT_GRP_WORDS);
+    }
     if (d.status) return true;   // failed earlier: the caller leaves it untouched
     if (h.pad[HDR_PAGED]) {      // lives in the paged layout: the paged kernel replays it
         d.status = MT_DOC_RETRY;
@@ -462,6 +495,14 @@ TD void store_doc(DocT<T> &d, const DevState &st, int doc) {
         for (int i = 1 + lane(); i <= d.heap_n; i += MT_WAVE) gH[i] = d.heap[i];
     }
     d.oslot[2 * lane()] = d.ocli;
+    if constexpr (T::kLive) {
+        if (lane() == 0) {
+            GLB_AS int32_t *lv = (GLB_AS int32_t *)(st.live + 4 * (size_t)doc);
+            lv[0] = d.local_seq;
+            lv[1] = d.g_head;
+            lv[2] = d.g_n;
+        }
+    }
     for (int l = 0; l < d.depth; l++)
         for (int b = lane(); b < nbr(d, l); b += MT_WAVE) gcnt[l * B + b] = lvl(d, l)[b];
     for (int b = lane(); b < nbr(d, 0); b += MT_WAVE) gflg[b] = d.flg[b];
@@ -890,7 +931,11 @@ TD void text_gc(DocT<T> &d) {
             b = d.Bv[i];
         }
         // (a rich delta log keeps removed segments' text: their UNLINK event reports it)
-        const bool live = i < d.n && (a.z == MT_RSEQ_NONE || (T::kLog && d.rich)) && !(b.z & MT_MARKER_BIT);
+        // (a live document keeps the text of segments in a pending group: regeneratePendingOp
+        // re-creates an unacked insert the local client has removed since)
+        bool keep = a.z == MT_RSEQ_NONE || (T::kLog && d.rich);
+        if constexpr (T::kLive) keep = keep || (i < d.n && pend_word(d.O[i]) != 0u);
+        const bool live = i < d.n && keep && !(b.z & MT_MARKER_BIT);
         const int len = live ? a.x : 0;
         const int inc = wave_scan_incl(len);
         const int off = carry + inc - len;
@@ -1298,7 +1343,10 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     v4u b = d.Bv[in ? s + k : s];
     const bool removed = a.z != MT_RSEQ_NONE;
     const bool marker = (b.z & MT_MARKER_BIT) != 0;
-    const bool settled = in && !removed && a.y <= d.min_seq;   // merge candidate
+    // a segment in a pending segment group is held (scourNode :1328, :1389-1392)
+    bool pend = false;
+    if constexpr (T::kLive) pend = in && pend_word(d.O[in ? s + k : s]) != 0u;
+    const bool settled = in && !pend && !removed && a.y <= d.min_seq;   // merge candidate
     // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
     const bool need_nl = settled && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
     if (ballot(need_nl)) {
@@ -1310,7 +1358,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
         }
         wsync<T>();
     }
-    const u64 m_unlink = ballot(in && removed && a.z <= d.min_seq);
+    const u64 m_unlink = ballot(in && !pend && removed && a.z <= d.min_seq);
     const u64 m_settled = ballot(settled);
     const u64 m_mark = ballot(in && marker);
     const u64 m_nl = ballot(in && (b.w & SEGF_NL) != 0);
@@ -1508,7 +1556,9 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     }
     const bool removed = a.z != MT_RSEQ_NONE;
     const bool marker = (b.z & MT_MARKER_BIT) != 0;
-    const bool cand = in && !removed && a.y <= d.min_seq;
+    bool pend = false;   // held: in a pending segment group (scourNode :1328)
+    if constexpr (T::kLive) pend = in && pend_word(d.O[in ? s + k : s]) != 0u;
+    const bool cand = in && !pend && !removed && a.y <= d.min_seq;
     if (!serial) {
         // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
         const bool need_nl = cand && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
@@ -1555,7 +1605,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         }
         return kept_all;
     }
-    const bool unlink = in && removed && a.z <= d.min_seq;
+    const bool unlink = in && !pend && removed && a.z <= d.min_seq;
     const bool surv = in && !unlink && !join;
     if (T::kLog) {   // scourNode's UNLINK / APPEND events :1343-1373
         d.m_unlink += __popcll(ballot(unlink));
@@ -1837,6 +1887,24 @@ __device__ __forceinline__ uint16_t pay_unit(const OpIn &in, int j) {
     return (uint16_t)(w & 0xFFFF);
 }
 
+// Live documents: first segment at or after index `from` visible in view
+// (UniversalSequenceNumber, local client) -- the leaf rightExcursion's nodeMap reaches first
+// (MT/mergeTree.ts:2346-2376, nodeMap :2936-2998 visits leaves of length > 0).  The local
+// client's view of a node is its local net length whatever the refSeq (nodeLength
+// :1692-1698): a segment not removed at all.  -1: none.
+TD int first_v0(DocT<T> &d, int from) {
+    for (int base = from; base < d.n; base += MT_WAVE) {
+        const int i = base + lane();
+        const bool v = i < d.n;
+        v4i a;
+        u64 o;
+        load_ao(d, i, v, a, o);
+        const u64 m = ballot(v && obs_len(a) > 0);
+        if (m) return base + first_lane(m);
+    }
+    return -1;
+}
+
 // Client.applyInsertOp MT/client.ts:394-442 -> MergeTree.insertSegments :2001-2031
 #ifdef MT_PROF
 TD void op_insert_impl(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin);
@@ -1880,7 +1948,12 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         }
         const u64 mi = ballot(v && pex >= p);
         if (ip < 0 && mi) ip = base + first_lane(mi);
-        const u64 mj = ballot(v && pex == p && (vl > 0 || tie(a, r)));
+        bool tj;
+        if constexpr (T::kLive)
+            tj = d.lop ? tie_local(a, r) : tie_remote_live(a, r);
+        else
+            tj = tie(a, r);
+        const u64 mj = ballot(v && pex == p && (vl > 0 || tj));
         if (mj) {
             js = base + first_lane(mj);
             break;
@@ -1897,7 +1970,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         ip = d.n;
     }
     Cb cb;
-    if (!quiet) cb = cb_begin(d, seq, MT_OP_INSERT);
+    if (!quiet) cb = cb_begin(d, (T::kLive && d.lop) ? -1 : seq, MT_OP_INSERT);
     if (slen == 0) {  // zero-length segment: boundary only, not inserted (:2229)
         if (quiet) return;
         cb.n = 1;
@@ -1971,13 +2044,28 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
 #endif
     }
     int bstart;
-    const int B = blk_find(d, 0, ip, false, bstart);
+    int B = blk_find(d, 0, ip, false, bstart);
     if (B < 0) {
         FAIL_INTERNAL(d);
         return;
     }
-    const int bend = bstart + cntr(d, 0, B);
-    const int x = (js >= 0 && js < bend) ? js : bend;
+    int bend = bstart + cntr(d, 0, B);
+    int x = (js >= 0 && js < bend) ? js : bend;
+    if constexpr (T::kLive) {
+        // A remote insert that reaches the end of leaf block B continues into the next block
+        // when the first segment after B visible in view (UniversalSequenceNumber, local
+        // client) is an unacked local insert (insertingWalk's continuePredicate,
+        // MT/mergeTree.ts:2464-2469 with blockInsert's checkSegmentIsLocal :2176-2194; the
+        // unfinished node makes the parent walk on with pos 0, :2419-2424).
+        while (!d.lop && x == bend) {
+            const int s0 = first_v0(d, bend);
+            if (s0 < 0 || !is_local_seq(uni(d.A[s0].y)) || B + 1 >= nbr(d, 0)) break;
+            B++;
+            bstart = bend;
+            bend += cntr(d, 0, B);
+            x = (js >= 0 && js < bend) ? js : bend;
+        }
+    }
     uint32_t toff, segw = 0;
     if (marker) {
         toff = op.payload;
@@ -1999,7 +2087,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     const uint32_t uid = (uint32_t)d.next_uid;
     if (lane() == 0) {
         d.A[x] = v4i{slen, seq, MT_RSEQ_NONE, pack_cli(c, 0)};
-        d.O[x] = 0ull;
+        d.O[x] = (T::kLive && d.lop) ? ((u64)(uint32_t)d.lg << 32) : 0ull;   // addToPendingList :2128
         d.Bv[x] = v4u{toff, ph, uid | (marker ? MT_MARKER_BIT : 0u), segw | nomatch};
     }
     d.next_uid++;
@@ -2014,7 +2102,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         if (d.status) return;
         if (x - bstart >= MT_HALF) lb = B + 1;
     }
-    if (seq > d.min_seq) add_to_lru_block(d, lb, uid, seq);  // saveIfLocal :2197-2212
+    if (!(T::kLive && d.lop) && seq > d.min_seq) add_to_lru_block(d, lb, uid, seq);  // saveIfLocal :2197-2212
     if (d.status) return;
     if (quiet) return;   // insertSegments with opArgs undefined fires no callback (:2013-2021)
     // delta callback: position of the new segment in the observer view
@@ -2036,18 +2124,61 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
 // SegmentPropertiesManager.addProperties MT/segmentPropertiesManager.ts:35-111 applied by
 // one lane to its segment: writes the new record nh, returns the seg hash contribution of
 // the propertyDeltas (and logs them when `logp` is set).  Returns false on key overflow.
+// Live documents: the pending-property state of a segment (SegmentPropertiesManager
+// pendingKeyUpdateCount / pendingRewriteCount, MT/segmentPropertiesManager.ts:13-14, 19-33)
+// is the set of unacked local annotate groups in its segment-group FIFO (word pw).
+TD bool grp_pending_rewrite(DocT<T> &d, uint32_t pw) {
+    for (; pw; pw >>= 8) {
+        const int w1 = d.grp[(int)(pw & 0xFFu) * MT_GRP_WORDS + 1];
+        if ((w1 & 0xFF) == MT_OP_ANNOTATE && ((w1 >> 8) & 0xFF)) return true;
+    }
+    return false;
+}
+TD bool grp_pending_key(DocT<T> &d, uint32_t pw, uint32_t k) {
+    for (; pw; pw >>= 8) {
+        const GLB_AS int32_t *g = d.grp + (int)(pw & 0xFFu) * MT_GRP_WORDS;
+        if ((g[1] & 0xFF) != MT_OP_ANNOTATE) continue;
+        const int nk = (g[1] >> 16) & 0xFF;
+        for (int j = 0; j < nk; j++)
+            if ((uint32_t)g[2 + j] == k) return true;
+    }
+    return false;
+}
+
+// pw (live documents, remote ops): the segment's pending-group FIFO -- keys with a pending
+// local update are not modified (shouldModifyKey :56-63), an outstanding local rewrite blocks
+// the whole op (:48-51: *undef = true, propertyDeltas undefined, the set unchanged).
 TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint32_t *rec, u64 &sh,
-                        GLB_AS int32_t *logp, int &nlog, bool *nomatch = nullptr) {
+                        GLB_AS int32_t *logp, int &nlog, bool *nomatch = nullptr, uint32_t pw = 0u,
+                        bool *undef = nullptr) {
     const uint32_t cntk = rec[0] & 0xFFFF, comb = rec[0] >> 16;
     const GLB_AS uint32_t *o = oh ? prec(d, d.props_half, oh) : nullptr;
     GLB_AS uint32_t *t = prec(d, d.props_half, nh);
     const uint32_t on = o ? o[0] : 0;
     uint32_t n = 0;
     int npd = 0;
+    if constexpr (T::kLive) {
+        if (pw && grp_pending_rewrite(d, pw)) {
+            for (uint32_t i = 0; i < 2 * on; i++) t[1 + i] = o[1 + i];
+            t[0] = on;
+            sh = fnv_u32(sh, 0xFFFFFFFFu);
+            if (undef) *undef = true;
+            return true;
+        }
+        if (comb == MT_COMBINE_TABLE) pw = 0;   // a combining op modifies every key
+    }
     // rewrite: delete keys whose new value is not truthy (:66-79)
     for (uint32_t i = 0; i < on; i++) {
         const uint32_t k = o[1 + 2 * i], v = o[2 + 2 * i];
         bool in_new = false, truthy = false;
+        if constexpr (T::kLive) {
+            if (pw && grp_pending_key(d, pw, k)) {   // kept: a pending local update
+                t[1 + 2 * n] = k;
+                t[2 + 2 * n] = v;
+                n++;
+                continue;
+            }
+        }
         if (comb == MT_COMBINE_REWRITE) {
             for (uint32_t j = 0; j < cntk; j++)
                 if (rec[1 + 2 * j] == k) {
@@ -2072,6 +2203,9 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
     }
     for (uint32_t j = 0; j < cntk; j++) {
         const uint32_t k = rec[1 + 2 * j], v = rec[2 + 2 * j];
+        if constexpr (T::kLive) {
+            if (pw && grp_pending_key(d, pw, k)) continue;
+        }
         int idx = -1;
         for (uint32_t q = 0; q < n; q++)
             if (t[1 + 2 * q] == k) idx = (int)q;
@@ -2177,14 +2311,22 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         const u64 sel_m = ballot(sel);
         if (sel_m) mark_dirty(d, base + first_lane(sel_m));
         bool newly = false, bad = false, spill = false;
-        const bool ovl_any = rem && ballot(sel && a.z != MT_RSEQ_NONE);
+        // live documents: a remote remove of a segment the local client removed (unacked)
+        // replaces that removal (:2657-2662): no overlap slot, no callback entry
+        bool lrem = false;
+        if constexpr (T::kLive) lrem = rem && sel && !d.lop && is_local_seq(a.z);
+        const bool ovl_any = rem && ballot(sel && a.z != MT_RSEQ_NONE && !lrem);
         if (ovl_any) {   // this client's slot (taken at its first overlapping remove)
             if (d.ocs == 0) d.ocs = oslot_take(d, c);
             if (d.ocs > 32) d.wide = 1;
             if (d.ocs && lane() == 0) d.oslot[2 * (d.ocs - 1) + 1] = seq;
         }
         if (rem && sel) {
-            if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
+            if (lrem) {
+                a.z = seq;
+                a.w = pack_cli(seg_cli(a), c);
+                d.A[i] = a;
+            } else if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
                 if (d.ocs == 0) {
                     if (T::kOvlBits < 64)
                         spill = true;
@@ -2198,6 +2340,15 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                 a.z = seq;
                 a.w = pack_cli(seg_cli(a), c);
                 d.A[i] = a;
+                if constexpr (T::kLive) {   // the local client's remove: addToPendingList :2683-2684
+                    if (d.lop) {
+                        u64 po = o;
+                        if (pend_push(po, d.lg))
+                            d.O[i] = po;
+                        else
+                            bad = true;
+                    }
+                }
             }
         }
         uint32_t nh = 0;
@@ -2211,7 +2362,19 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         if (!rem && sel) {
             int unused = 0;
             bool nm = rec_nm || (bv.w & SEGF_NOMATCH) != 0;
-            if (!annotate_record(d, bv.y, nh, rec, sh, (GLB_AS int32_t *)nullptr, unused, &nm)) bad = true;
+            uint32_t pw = 0;
+            if constexpr (T::kLive) {
+                if (d.lop) {   // the local client's annotate: addToPendingList :2611-2612
+                    u64 po = o;
+                    if (pend_push(po, d.lg))
+                        d.O[i] = po;
+                    else
+                        bad = true;
+                } else {
+                    pw = pend_word(o);
+                }
+            }
+            if (!annotate_record(d, bv.y, nh, rec, sh, (GLB_AS int32_t *)nullptr, unused, &nm, pw)) bad = true;
             v4u nb = bv;
             nb.y = nh;
             nb.w = (bv.w & ~SEGF_NOMATCH) | (nm ? SEGF_NOMATCH : 0u);
@@ -2248,10 +2411,13 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                     // propertyDeltas: <= one per old key (rewrite) plus one per op key
                     if (cb_room(d, 1 + 2 * (MT_KMAX + (int)(rec[0] & 0xFFFF)))) {
                         const int at = d.dlog_n + 1;
+                        uint32_t pwj = 0;
+                        if constexpr (T::kLive) pwj = d.lop ? 0u : pend_word(bcast64(o, j));
                         if (L == 0) {
                             // old record is untouched (new record went to a fresh handle)
-                            annotate_record(d, ohj, nhj, rec, dummy, d.dlog + at, nl);
-                            d.dlog[at - 1] = nl / 2;
+                            bool undef = false;
+                            annotate_record(d, ohj, nhj, rec, dummy, d.dlog + at, nl, nullptr, pwj, &undef);
+                            d.dlog[at - 1] = undef ? -1 : nl / 2;   // -1: propertyDeltas undefined
                         }
                         nl = bcast(nl, 0);
                         d.dlog_n += 1 + nl;
@@ -2272,7 +2438,8 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         const int prevl = below ? 63 - __clzll((long long)below) : -1;
         const int pb = __shfl(b, prevl < 0 ? 0 : prevl, MT_WAVE);
         const int prev_b = prevl < 0 ? last_b : pb;
-        u64 fm = ballot(sel && b != prev_b);
+        // (the local client's own op: its segments join the pending group instead, :2610-2617, 2680-2689)
+        u64 fm = ballot(sel && b != prev_b && !(T::kLive && d.lop));
         while (fm) {
             const int j = first_lane(fm);
             fm &= fm - 1;
@@ -2315,7 +2482,7 @@ TD void op_range(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *pin) {
     if (d.status) return;
     boundary(d, p2, r, c);
     if (d.status) return;
-    Cb cb = cb_begin(d, seq, op.kind);
+    Cb cb = cb_begin(d, (T::kLive && d.lop) ? -1 : seq, op.kind);
     int carry = 0, ocarry = 0;
     P2_T0(14)
     range_mark(d, op, rec, carry, ocarry, cb);
@@ -2349,9 +2516,140 @@ TD void load_removed(DocT<T> &d, const mt_op_rec &op) {
     wsync<T>();
 }
 
+// ---------------------------------------------------------------- live-client documents
+// The local client's own op (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
+// MT/client.ts:164-211 -> applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp with no
+// sequencedMessage): refSeq = currentSeq, seq = UnassignedSequenceNumber with
+// ++collabWindow.localSeq (MT/mergeTree.ts:2009, 2604, 2646), one new segment group at the
+// tail of the pending queue (addToPendingList :1955-1962); no zamboni, no seq update
+// (completeAndLogOp's asserts are for sequenced messages only, MT/client.ts:456-471).
+TD void live_local(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
+    const mt_op_rec &op = in.op;
+    if (op.kind != MT_OP_INSERT && op.kind != MT_OP_REMOVE && op.kind != MT_OP_ANNOTATE) return;
+    const GLB_AS uint32_t *rec = (op.kind == MT_OP_ANNOTATE && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
+    const int nk = rec ? (int)(rec[0] & 0xFFFFu) : 0;
+    if (d.g_n >= MT_LIVE_GROUPS || nk > MT_KMAX) {
+        if (d.status == 0) d.cap_cause = nk > MT_KMAX ? 13 : 12;
+        fail(d, MT_DOC_CAPACITY);
+        return;
+    }
+    const int ls = ++d.local_seq;
+    const int g = (d.g_head - 1 + d.g_n) % MT_LIVE_GROUPS + 1;
+    GLB_AS int32_t *ge = d.grp + g * MT_GRP_WORDS;
+    const int rw = rec && (rec[0] >> 16) == MT_COMBINE_REWRITE ? 1 : 0;
+    if (lane() == 0) {
+        ge[0] = ls;
+        ge[1] = (int)op.kind | (rw << 8) | (nk << 16);
+    }
+    if (lane() < nk) ge[2 + lane()] = (int)rec[1 + 2 * lane()];
+    d.g_n++;
+    d.lop = 1;
+    d.lg = g;
+    OpIn lin = in;
+    lin.op.seq = MT_LOCAL_BASE + ls;
+    lin.op.ref_seq = d.cur_seq;
+    if (op.kind == MT_OP_INSERT)
+        op_insert(d, lin, tin, pin);
+    else
+        op_range(d, lin.op, pin);
+    // segment ids below this joined the group in the op's walk (document order); a later split
+    // appends its right half -- a new id -- to every group of the left one (SegmentGroup
+    // segments order, segmentGroupCollection.ts copyTo)
+    if (lane() == 0) ge[10] = d.next_uid;
+    d.lop = 0;
+    d.lg = 0;
+}
+
+// ackPendingSegment (MT/client.ts:589-626 -> MT/mergeTree.ts:1926-1953, ISegment.ack
+// :486-521) for one member op: the head group's segments get the sequence number (insert:
+// seq; remove: removedSeq unless a remote remove replaced it), leave the group and enter
+// the zamboni LRU set (addToLRUSet :1306-1316, in document order).
+TD void live_ack(DocT<T> &d, const mt_op_rec &op) {
+    if (d.g_n == 0) return;   // nothing pending: ackPendingSegment dequeues undefined (:1931)
+    const int g = d.g_head;
+    const int kind = d.grp[g * MT_GRP_WORDS + 1] & 0xFF;
+    if (kind != (int)op.kind) {   // the echo does not match the pending op (ack's assert)
+        if (d.status == 0) d.cap_cause = 14;
+        fail(d, MT_DOC_INTERNAL);
+        return;
+    }
+    const uint32_t ustamp = (uint32_t)d.grp[g * MT_GRP_WORDS + 10];
+    compute_ends(d);
+    const int nblk = nbr(d, 0);
+    // The group's segments in its own order (SegmentGroup.segments): first the ones its op
+    // walked, in document order (their ids are below the stamp), then the right halves later
+    // splits appended (segmentGroupCollection.ts copyTo), in split order = id order.
+    int n_late = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const int rounds = pass == 0 ? 1 : n_late;
+        uint32_t last = ustamp;
+        for (int q = 0; q < rounds; q++) {
+            uint32_t pick = 0xFFFFFFFFu;
+            if (pass == 1) {   // the late member with the smallest id above the previous one
+                for (int base = 0; base < d.n; base += MT_WAVE) {
+                    const int i = base + lane();
+                    const bool v = i < d.n;
+                    const uint32_t uid = v ? (d.Bv[i].z & ~MT_MARKER_BIT) : 0xFFFFFFFFu;
+                    const bool c = v && pend_first(d.O[i]) == g && uid >= last;
+                    uint32_t mn = c ? uid : 0xFFFFFFFFu;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, MT_WAVE));
+                    pick = min(pick, (uint32_t)uni((int)mn));
+                }
+                last = pick;
+            }
+            for (int base = 0; base < d.n; base += MT_WAVE) {
+                const int i = base + lane();
+                const bool v = i < d.n;
+                v4i a;
+                u64 o;
+                load_ao(d, i, v, a, o);
+                const v4u bv = d.Bv[v ? i : 0];
+                const uint32_t uid = bv.z & ~MT_MARKER_BIT;
+                const bool mem0 = v && pend_first(o) == g;
+                const bool late = mem0 && uid >= ustamp;
+                if (pass == 0) n_late += __popcll(ballot(late));
+                const bool mem = pass == 0 ? (mem0 && !late) : (mem0 && uid == pick);
+                bool bad = false;
+                if (mem) {
+                    if (kind == MT_OP_INSERT) {
+                        bad = !is_local_seq(a.y);
+                        a.y = op.seq;
+                    } else if (kind == MT_OP_REMOVE && is_local_seq(a.z)) {
+                        a.z = op.seq;   // else a remote remove replaced it: ack returns false
+                    }
+                    d.A[i] = a;
+                    d.O[i] = pend_pop(o);
+                }
+                if (ballot(bad)) {
+                    FAIL_INTERNAL(d);
+                    return;
+                }
+                wsync<T>();
+                const int b = mem ? block_of(d, i, nblk) : -1;
+                for (u64 m = ballot(mem); m; m &= m - 1) {
+                    const int j = first_lane(m);
+                    add_to_lru_block(d, bcast(b, j), (uint32_t)bcast((int)uid, j), op.seq);
+                    if (d.status) return;
+                }
+            }
+        }
+    }
+    d.g_head = g % MT_LIVE_GROUPS + 1;
+    d.g_n--;
+}
+
 TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     const mt_op_rec &op = in.op;
     d.ocs = oslot_of(d, op_cli(op));
+    bool ack = false;
+    if constexpr (T::kLive) {
+        if (op.flags & MT_F_LOCAL) {
+            live_local(d, in, tin, pin);
+            return;
+        }
+        ack = (op.flags & MT_F_ACK) != 0;
+    }
     if (op.flags & MT_F_LOAD) {
         // SnapshotLoader.loadBody (MT/snapshotLoader.ts:195-227): insertSegments at
         // root.cachedLength in view (client, refSeq 0), no callback, no seq/msn update.  Its
@@ -2367,7 +2665,11 @@ TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const G
         return;
     }
     const bool is_op = op.kind == MT_OP_INSERT || op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
-    if (op.kind == MT_OP_INSERT) {
+    if constexpr (T::kLive) {
+        if (ack && is_op) live_ack(d, op);
+    }
+    if (ack) {
+    } else if (op.kind == MT_OP_INSERT) {
         op_insert(d, in, tin, pin);
     } else if (is_op) {
         op_range(d, op, pin);
@@ -2380,7 +2682,7 @@ TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const G
             if (d.status) return;
         }
         if (pass == 1) break;
-        if (op.kind != MT_OP_NOOP) {
+        if (op.kind != MT_OP_NOOP && !ack) {
             if (!(d.cur_seq < op.seq)) {
                 fail(d, MT_DOC_SEQ_ORDER);
                 return;

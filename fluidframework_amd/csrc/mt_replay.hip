@@ -57,6 +57,12 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
     if (lane() == 0) {
         init_doc_hdr(st, doc, len);
         st.retry[doc] = 0;
+        if (st.live) {   // collabWindow.localSeq 0, empty pending queue (next group id 1)
+            st.live[4 * doc] = 0;
+            st.live[4 * doc + 1] = 1;
+            st.live[4 * doc + 2] = 0;
+            st.live[4 * doc + 3] = 0;
+        }
     }
 }
 
@@ -1074,8 +1080,110 @@ __global__ void __launch_bounds__(MT_WAVE) k_checksum(DevState st, mt_checksum *
 }
 
 // ============================================================================ host side
+// ---------------------------------------------------------------- live-client reconnect
+// regeneratePendingOp for the oldest pending segment group of one document (one wave):
+// resetPendingDeltaToOps (MT/client.ts:709-766) with findReconnectionPostition (:675-707) --
+// a segment counts towards the positions when it is inserted (acked, or localSeq <= the
+// group's) and not removed (or removed by a local op newer than the group).  Members in
+// document order (the reference sorts by ordinal); each one that yields an op joins a new
+// group (same localSeq, kind, keys) at the tail of the queue.  io: [0] records written
+// (-1: no pending group, -2: a capacity, -3: the document has failed), [1] text units,
+// [2] props words.
+__global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_regen_rec *out, int cap, uint16_t *otext,
+                                                   int tcap, uint32_t *oprops, int pcap, int32_t *io) {
+    typedef TierLiveT<false> T;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    const LdsLayout L = lds_layout(false, 0, st.B, 0, 0);
+    DocT<T> d;
+    load_doc(d, st, doc, (LDS_AS uint8_t *)smem_raw, L, 0, st.B, 0);
+    if (d.status || d.g_n == 0) {
+        if (lane() == 0) io[0] = d.status ? -3 : -1;
+        return;
+    }
+    const int g = d.g_head;
+    const int gw = lane() < MT_GRP_WORDS ? d.grp[g * MT_GRP_WORDS + lane()] : 0;   // the entry, lane j = word j
+    const int ls = bcast(gw, 0), kind = bcast(gw, 1) & 0xFF;
+    d.g_head = g % MT_LIVE_GROUPS + 1;   // dequeue first: the new groups may reuse its table slot
+    d.g_n--;
+    int carry = 0, nout = 0, tu = 0, pw = 0;
+    bool over = false;
+    for (int base = 0; base < d.n && !over; base += MT_WAVE) {
+        const int i = base + lane();
+        const bool v = i < d.n;
+        v4i a;
+        u64 o;
+        load_ao(d, i, v, a, o);
+        const v4u b = d.Bv[v ? i : 0];
+        const bool ins = !is_local_seq(a.y) || a.y - MT_LOCAL_BASE <= ls;
+        const bool nrem = a.z == MT_RSEQ_NONE || (is_local_seq(a.z) && a.z - MT_LOCAL_BASE > ls);
+        const int cl = v && ins && nrem ? a.x : 0;
+        const int inc = wave_scan_incl(cl);
+        const int pos = carry + inc - cl;
+        const bool mem = v && pend_first(o) == g;
+        for (u64 m = ballot(mem); m && !over; m &= m - 1) {
+            const int j = first_lane(m);
+            const int ij = base + j;
+            u64 oj = pend_pop(bcast64(o, j));
+            const int aj_x = bcast(a.x, j), aj_z = bcast(a.z, j);
+            const bool emit = kind != MT_OP_REMOVE || is_local_seq(aj_z);
+            if (emit) {
+                const uint32_t bx = (uint32_t)bcast((int)b.x, j), by = (uint32_t)bcast((int)b.y, j);
+                const bool mk = (bcast((int)b.z, j) & MT_MARKER_BIT) != 0;
+                const int np = (kind == MT_OP_INSERT && by) ? (int)prec(d, d.props_half, by)[0] : -1;
+                const int ng = (d.g_head - 1 + d.g_n) % MT_LIVE_GROUPS + 1;
+                const int tneed = kind == MT_OP_INSERT && !mk ? aj_x : 0;
+                if (nout >= cap || d.g_n >= MT_LIVE_GROUPS || !pend_push(oj, ng) || tu + tneed > tcap ||
+                    pw + 1 + 2 * max(np, 0) > pcap) {
+                    over = true;
+                    break;
+                }
+                // same localSeq / kind / keys; joined now (its later splits append after it)
+                if (lane() < MT_GRP_WORDS) d.grp[ng * MT_GRP_WORDS + lane()] = lane() == 10 ? d.next_uid : gw;
+                d.g_n++;
+                if (lane() == 0) {
+                    mt_regen_rec r;
+                    r.kind = kind;
+                    r.pos1 = bcast(pos, j);
+                    r.pos2 = kind == MT_OP_INSERT ? r.pos1 : r.pos1 + aj_x;
+                    r.local_seq = ls;
+                    r.text_off = mk ? bx : (uint32_t)tu;
+                    r.text_len = (uint32_t)aj_x;
+                    r.props_off = np >= 0 ? (uint32_t)pw : MT_NO_PROPS;
+                    r.flags = mk ? MT_F_MARKER : 0u;
+                    out[nout] = r;
+                }
+                if (kind == MT_OP_INSERT) {
+                    gsync_rd();
+                    if (!mk)
+                        for (int q = lane(); q < aj_x; q += MT_WAVE) otext[tu + q] = text_base(d, d.text_half)[bx + q];
+                    if (np >= 0) {
+                        const GLB_AS uint32_t *pr = prec(d, d.props_half, by);
+                        for (int q = lane(); q < 1 + 2 * np; q += MT_WAVE) oprops[pw + q] = pr[q];
+                    }
+                    tu += tneed;
+                    pw += np >= 0 ? 1 + 2 * np : 0;
+                }
+                nout++;
+            }
+            if (lane() == 0) d.O[ij] = oj;
+        }
+        carry += bcast(inc, MT_WAVE - 1);
+    }
+    if (over) {   // the group table / a segment's FIFO / the caller's buffers are full
+        d.status = MT_DOC_CAPACITY;
+        d.cap_cause = 15;
+    }
+    store_doc(d, st, doc);
+    if (lane() == 0) {
+        io[0] = over ? -2 : nout;
+        io[1] = tu;
+        io[2] = pw;
+    }
+}
+
 struct mt_handle {
     int device = 0;
+    bool live = false;       // live-client handle (mt_options.live_client)
     uint32_t n_docs = 0;
     DevState st{};
     hipStream_t stream = nullptr;
@@ -1130,7 +1238,7 @@ static bool props_rec_ok(const uint32_t *props, uint64_t props_len, uint32_t off
 // offsets monotonic inside [0, n_ops], every insert payload inside the text arena, every
 // props record inside the props arena, known op kinds.
 static std::string validate_batch(uint32_t n_docs, const int64_t *off, const mt_op_rec *ops, uint64_t n_ops,
-                                  uint64_t text_len, const uint32_t *props, uint64_t props_len) {
+                                  uint64_t text_len, const uint32_t *props, uint64_t props_len, bool live) {
     if (off[0] < 0) return "doc_op_off[0] < 0";
     for (uint32_t d = 0; d < n_docs; d++)
         if (off[d + 1] < off[d]) return "doc_op_off not monotonic at document " + std::to_string(d);
@@ -1138,6 +1246,12 @@ static std::string validate_batch(uint32_t n_docs, const int64_t *off, const mt_
     for (uint64_t k = (uint64_t)off[0]; k < (uint64_t)off[n_docs]; k++) {
         const mt_op_rec &o = ops[k];
         if (o.kind > MT_OP_LOAD_REMOVED) return "op " + std::to_string(k) + ": unknown kind";
+        if ((o.flags & (MT_F_LOCAL | MT_F_ACK)) && !live)
+            return "op " + std::to_string(k) + ": local / ack record on a handle without live_client";
+        if ((o.flags & MT_F_LOCAL) && (o.flags & MT_F_ACK))
+            return "op " + std::to_string(k) + ": both MT_F_LOCAL and MT_F_ACK";
+        if ((o.flags & MT_F_LOCAL) && o.client != 0)
+            return "op " + std::to_string(k) + ": a local op's client must be the local client (short id 0)";
         if (o.kind == MT_OP_INSERT && !(o.flags & MT_F_MARKER)) {
             if (o.pos2 < 0 || (uint64_t)o.payload + (uint64_t)o.pos2 > text_len)
                 return "op " + std::to_string(k) + ": insert payload outside the text arena";
@@ -1176,7 +1290,12 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
     st.DLR = st.DL > 0 && o.delta_log_mode == 1 ? 1 : 0;
     if (const char *e = getenv("MT_WPG")) h->wpg = atoi(e) == 1 ? 1 : 2;
-    if (o.lds_seg_capacity >= 0) {
+    h->live = o.live_client != 0;
+    if (h->live && o.page_capacity > 0) {   // live documents replay from the flat HBM tier
+        delete h;
+        return nullptr;
+    }
+    if (o.lds_seg_capacity >= 0 && !h->live) {
         int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 192;
         S_l = std::min(S_l, st.S);
         h->lds.S = S_l;
@@ -1244,6 +1363,10 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.retry, N * sizeof(int32_t));
     alloc((void **)&st.resume, N * sizeof(int64_t));
     alloc((void **)&st.stats, 16 * sizeof(uint32_t));
+    if (h->live) {
+        alloc((void **)&st.live, N * 4 * sizeof(int32_t));
+        alloc((void **)&st.grp, N * (size_t)(MT_LIVE_GROUPS + 1) * MT_GRP_WORDS * sizeof(int32_t));
+    }
     if (st.PP > 0) {
         const size_t slots = N * (size_t)st.PP * MT_PG_SLOTS;
         alloc((void **)&st.pgA, slots * sizeof(int4));
@@ -1277,7 +1400,8 @@ void mt_destroy(mt_handle *h) {
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
-                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot};
+                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot,
+                  st.live, st.grp};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -1378,7 +1502,7 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
     // the kernels index ops, text and props straight from these values: reject anything
     // that would read outside the arrays (remote ops are trusted for their semantics, not
     // for memory safety)
-    std::string bad = validate_batch(h->n_docs, doc_op_off, ops, n_ops, text_len, props, props_len);
+    std::string bad = validate_batch(h->n_docs, doc_op_off, ops, n_ops, text_len, props, props_len, h->live);
     if (!bad.empty()) {
         h->err = "mt_batch_upload: " + bad;
         return nullptr;
@@ -1454,7 +1578,13 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
                                    b->text, b->props, res, *pc);
             HIPCHK(h, hipGetLastError());
         }
-    } else if (h->st.DL)
+    } else if (h->live && h->st.DL)
+        hipLaunchKernelGGL((k_replay<TierLiveT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
+    else if (h->live)
+        hipLaunchKernelGGL((k_replay<TierLiveT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
+    else if (h->st.DL)
         hipLaunchKernelGGL((k_replay<TierGlbT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     else
@@ -2146,12 +2276,14 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
         const int4 a = hd.A[i];
         const uint4 b = hd.B[i];
         int32_t *r = rows + 8 * i;
+        // live documents: an unacked insert / local remove reads UnassignedSequenceNumber (-1)
+        const bool lins = a.y >= MT_LOCAL_BASE, lrem = a.z >= MT_LOCAL_BASE;
         r[0] = a.x;
-        r[1] = a.y;
+        r[1] = lins ? -1 : a.y;
         r[2] = (int)(short)(a.w & 0xFFFF);
-        r[3] = a.z;
+        r[3] = lrem ? -1 : a.z;
         r[4] = a.z == MT_RSEQ_NONE ? MT_RSEQ_NONE : (int)(short)((uint32_t)a.w >> 16);
-        r[5] = __builtin_popcountll(hd.O[i]);
+        r[5] = __builtin_popcountll(h->live ? (hd.O[i] & 0xFFFFFFFFull) : hd.O[i]);
         r[6] = (b.z & MT_MARKER_BIT) ? (int32_t)b.x : -1;
         r[7] = b.y ? 1 : 0;
     }
@@ -2175,6 +2307,33 @@ int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, 
     }
     if (n_rows) *n_rows = (uint32_t)n;
     if (hdr_words) memcpy(hdr_words, &hd.hdr, sizeof(DocHdr));
+    return 0;
+}
+
+// Debug (flat documents): the zamboni heap in array order as {maxSeq, leaf index of its
+// segment or -1} and the leaf blocks' needsScour flags.
+int mt_debug_heap(mt_handle *h, uint32_t doc, int32_t *heap, uint32_t cap, uint32_t *n_heap, int32_t *flags,
+                  uint32_t cap_flags, uint32_t *n_flags) {
+    HostDoc hd;
+    int rc = fetch_doc(h, doc, hd, false, false);
+    if (rc) return rc;
+    if (hd.hdr.pad[HDR_PAGED]) return MT_E_INVALID;
+    const DevState &st = h->st;
+    std::vector<int2> hp((size_t)st.H + 1);
+    std::vector<int8_t> fl((size_t)st.B);
+    HIPCHK(h, hipMemcpy(hp.data(), st.heap + doc * (size_t)(st.H + 1), hp.size() * sizeof(int2), hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(fl.data(), st.flg + doc * (size_t)st.B, fl.size(), hipMemcpyDeviceToHost));
+    const int n = hd.hdr.n_seg;
+    for (int k = 1; k <= hd.hdr.heap_n && (uint32_t)(k - 1) < cap; k++) {
+        int at = -1;
+        for (int i = 0; i < n; i++)
+            if ((hd.B[i].z & ~MT_MARKER_BIT) == (uint32_t)hp[k].y) at = i;
+        heap[2 * (k - 1)] = hp[k].x;
+        heap[2 * (k - 1) + 1] = at;
+    }
+    if (n_heap) *n_heap = (uint32_t)hd.hdr.heap_n;
+    for (int b = 0; b < hd.hdr.n_blk[0] && (uint32_t)b < cap_flags; b++) flags[b] = fl[b];
+    if (n_flags) *n_flags = (uint32_t)hd.hdr.n_blk[0];
     return 0;
 }
 
@@ -2284,6 +2443,65 @@ int mt_checksums(mt_handle *h, mt_checksum *out) {
     int rc = mt_checksums_device(h, h->d_sums);
     if (rc) return rc;
     HIPCHK(h, hipMemcpy(out, h->d_sums, h->n_docs * sizeof(mt_checksum), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mt_regenerate_pending(mt_handle *h, uint32_t doc, mt_regen_rec *out, uint32_t cap, int32_t *n_out,
+                          uint16_t *out_text, uint32_t text_cap, uint32_t *out_props, uint32_t props_cap) {
+    if (!h || !h->live || doc >= h->n_docs || !n_out || (cap && !out) || (text_cap && !out_text) ||
+        (props_cap && !out_props)) {
+        if (h) h->err = "mt_regenerate_pending: needs a live_client handle, a document and output buffers";
+        return MT_E_INVALID;
+    }
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    mt_regen_rec *d_out = nullptr;
+    uint16_t *d_text = nullptr;
+    uint32_t *d_props = nullptr;
+    int32_t *d_io = nullptr;
+    bool ok = hipMalloc(&d_out, std::max<size_t>(cap, 1) * sizeof(mt_regen_rec)) == hipSuccess &&
+              hipMalloc(&d_text, std::max<size_t>(text_cap, 1) * 2) == hipSuccess &&
+              hipMalloc(&d_props, std::max<size_t>(props_cap, 1) * 4) == hipSuccess &&
+              hipMalloc(&d_io, 16) == hipSuccess;
+    int32_t io[4] = {0, 0, 0, 0};
+    if (ok) {
+        hipLaunchKernelGGL(k_regen, dim3(1), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0), h->stream, h->st,
+                           (int)doc, d_out, (int)cap, d_text, (int)text_cap, d_props, (int)props_cap, d_io);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess &&
+             hipMemcpy(io, d_io, 16, hipMemcpyDeviceToHost) == hipSuccess;
+        if (ok && io[0] > 0)
+            ok = hipMemcpy(out, d_out, (size_t)io[0] * sizeof(mt_regen_rec), hipMemcpyDeviceToHost) == hipSuccess &&
+                 (io[1] == 0 || hipMemcpy(out_text, d_text, (size_t)io[1] * 2, hipMemcpyDeviceToHost) == hipSuccess) &&
+                 (io[2] == 0 || hipMemcpy(out_props, d_props, (size_t)io[2] * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    }
+    for (void *p : {(void *)d_out, (void *)d_text, (void *)d_props, (void *)d_io})
+        if (p) hipFree(p);
+    if (!ok) {
+        h->err = "mt_regenerate_pending: device allocation / launch failed";
+        return MT_E_HIP;
+    }
+    if (io[0] == -3) {
+        h->err = "mt_regenerate_pending: the document has failed";
+        return MT_E_INVALID;
+    }
+    if (io[0] == -2) {
+        h->err = "mt_regenerate_pending: capacity (group table, segment groups or output buffers); document failed";
+        return MT_E_INVALID;
+    }
+    *n_out = io[0];
+    return 0;
+}
+
+int mt_pending_counts(mt_handle *h, int32_t *out) {
+    if (!h || !h->live || !out) return MT_E_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::vector<int32_t> lv((size_t)h->n_docs * 4);
+    HIPCHK(h, hipMemcpy(lv.data(), h->st.live, lv.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t d = 0; d < h->n_docs; d++) {
+        out[2 * d] = lv[4 * d];
+        out[2 * d + 1] = lv[4 * d + 2];
+    }
     return 0;
 }
 

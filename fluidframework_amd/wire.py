@@ -11,7 +11,7 @@ import json
 import numpy as np
 
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 3
-F_GROUP_MORE, F_MARKER = 1, 2
+F_GROUP_MORE, F_MARKER, F_LOCAL, F_ACK = 1, 2, 8, 16
 NO_PROPS = 0xFFFFFFFF
 VAL_NULL = 0xFFFFFFFF
 VAL_UNDEF = 0xFFFFFFFE          # a key set to the JS value undefined
@@ -319,13 +319,47 @@ class Batch:
                                       min_seq=msg["minimumSequenceNumber"], client=enc.client(msg["clientId"]),
                                       kind=OP_NOOP, flags=0, props=NO_PROPS, pos1=0, pos2=0, payload=0))
                 continue
-            op = msg["contents"]
-            if op["type"] == 3:        # GROUP
-                members = op["ops"]
-                for i, m in enumerate(members):
-                    self._op(enc, msg, m, i + 1 < len(members))
+            self._msg(enc, msg)
+        self.doc_off.append(len(self.recs))
+
+    def _msg(self, enc, msg, flags=0):
+        op = msg["contents"]
+        if op["type"] == 3 and not op["ops"]:
+            # an empty GROUP applies nothing; applyMsg still updates seq/msn (MT/client.ts:818)
+            self.recs.append(dict(seq=msg["sequenceNumber"], ref_seq=msg["referenceSequenceNumber"],
+                                  min_seq=msg["minimumSequenceNumber"], client=enc.client(msg["clientId"]),
+                                  kind=OP_NOOP, flags=0, props=NO_PROPS, pos1=0, pos2=0, payload=0))
+            return
+        members = op["ops"] if op["type"] == 3 else [op]      # GROUP
+        for i, m in enumerate(members):
+            self._op(enc, msg, m, i + 1 < len(members))
+            self.recs[-1]["flags"] |= flags
+
+    def add_live_doc(self, seed_text, entries, clients):
+        """One document of a live-client handle (mt_options.live_client).  entries, in order:
+        ("local", op) -- the local client's own op as insertSegmentLocal / removeRangeLocal /
+        annotateRangeLocal return it (MT_F_LOCAL); ("ack", msg) -- the sequenced echo of one
+        (MT_F_ACK, one record per GROUP member); ("msg", msg) -- any other sequenced message.
+        clients maps long ids to short ids, the local client's ids to 0."""
+        enc = DocEncoder(self, clients)
+        self.clients.append(enc.short)
+        s = seed_text.encode("utf-16-le")
+        self.seed.extend(np.frombuffer(s, dtype="<u2").tolist())
+        self.seed_off.append(len(self.seed))
+        local_key = next((k for k, v in enc.short.items() if v == 0), None)
+        for what, x in entries:
+            if what == "local":
+                m = dict(clientId=local_key, sequenceNumber=-1, referenceSequenceNumber=0,
+                         minimumSequenceNumber=0, contents=x)
+                self._msg(enc, m, F_LOCAL)
+            elif what == "ack":
+                self._msg(enc, x, F_ACK)
+            elif x.get("type", "op") != "op":
+                self.recs.append(dict(seq=x["sequenceNumber"], ref_seq=x["referenceSequenceNumber"],
+                                      min_seq=x["minimumSequenceNumber"], client=enc.client(x["clientId"]),
+                                      kind=OP_NOOP, flags=0, props=NO_PROPS, pos1=0, pos2=0, payload=0))
             else:
-                self._op(enc, msg, op, False)
+                self._msg(enc, x)
         self.doc_off.append(len(self.recs))
 
     def arrays(self):

@@ -77,6 +77,15 @@ typedef struct mt_options {
        what the Node facade turns into callback objects.  Removed segments keep their text
        until they are unlinked. */
     int32_t delta_log_mode;
+    /* 1: live-client handle -- every document backs a participant Client whose short id 0 is
+       the local client (startOrUpdateCollaboration's own id, MT/client.ts:1053-1064):
+       records flagged MT_F_LOCAL are its own unsequenced ops, MT_F_ACK records the sequenced
+       echoes of them (ackPendingSegment), and mt_regenerate_pending rebuilds the oldest
+       pending op after a reconnect.  Live handles replay from HBM (no LDS / paged tiers);
+       per document at most 255 segment groups (unacked ops) are outstanding, a segment is in
+       at most 4 of them and 32 clients' overlapping removes are unsettled at once
+       (MT_DOC_CAPACITY beyond). */
+    int32_t live_client;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the
@@ -208,6 +217,10 @@ int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, 
                  int32_t *hdr_words);
 /* Debug: section timers of a build with -DMT_PROF (MT_E_INVALID otherwise). */
 int mt_debug_prof(mt_handle *h, uint64_t *out /* [32] */, int reset);
+/* Debug (flat documents): the zamboni heap in array order ({maxSeq, leaf index of its segment
+   or -1} pairs) and every leaf block's needsScour flag (-1 undefined, 0, 1). */
+int mt_debug_heap(mt_handle *h, uint32_t doc, int32_t *heap, uint32_t cap, uint32_t *n_heap, int32_t *flags,
+                  uint32_t cap_flags, uint32_t *n_flags);
 /* Delta log (only with delta_log_capacity > 0), oracle layout: one record per
    mergeTreeDeltaCallback (MT/mergeTreeDeltaCallback.ts:33-41; call sites MT/mergeTree.ts:
    2014-2021, 2625-2632, 2738-2745) = [seq, kind, n, (position, cachedLength
@@ -228,6 +241,29 @@ int mt_maintenance_counts(mt_handle *h, uint32_t *out);
 /* Per-document checksums (mt_types.h), to host memory or straight into device memory
    on the handle's device (e.g. a torch tensor's data_ptr() before an RCCL all-gather). */
 int mt_checksums(mt_handle *h, mt_checksum *out);
+
+/* Live-client handles: regeneratePendingOp for the oldest pending segment group of one
+   document (MT/client.ts:709-766 resetPendingDeltaToOps + findReconnectionPostition
+   :675-707).  The group is dequeued; every member segment, in document order, yields one op
+   at its position relative to the group's localSeq and joins a new group with the same
+   localSeq at the tail of the queue (a remove whose segment a remote remove has replaced
+   yields none).  Insert ops carry the segment's text (out_text) and property set (out_props:
+   [n, (key, value) x n] or MT_NO_PROPS when it has none); annotate ops carry positions only
+   (their props / combiningOp are the pending op's own).  *n_out = -1: no pending group. */
+typedef struct mt_regen_rec {
+    int32_t kind;        /* MT_OP_INSERT / MT_OP_REMOVE / MT_OP_ANNOTATE */
+    int32_t pos1, pos2;  /* remove / annotate: [pos1, pos2); insert: pos1 */
+    int32_t local_seq;   /* the group's localSeq */
+    uint32_t text_off;   /* insert: offset of the text in out_text (marker: refType) */
+    uint32_t text_len;   /* insert: UTF-16 units (marker: 1) */
+    uint32_t props_off;  /* insert: offset of the property set in out_props, or MT_NO_PROPS */
+    uint32_t flags;      /* MT_F_MARKER */
+} mt_regen_rec;
+int mt_regenerate_pending(mt_handle *h, uint32_t doc, mt_regen_rec *out, uint32_t cap, int32_t *n_out,
+                          uint16_t *out_text, uint32_t text_cap, uint32_t *out_props, uint32_t props_cap);
+/* Live-client handles: {collabWindow.localSeq, pending segment groups} of every document
+   ([n_docs][2]). */
+int mt_pending_counts(mt_handle *h, int32_t *out);
 int mt_checksums_device(mt_handle *h, void *device_out);
 
 #ifdef __cplusplus

@@ -34,10 +34,18 @@ enum mt_op_kind {
 enum mt_op_flags {
     MT_F_GROUP_MORE = 1,  /* another member of the same GROUP message follows */
     MT_F_MARKER = 2,      /* insert of a Marker (length 1); payload = refType */
-    MT_F_LOAD = 4         /* internal (summary load): a body segment appended by
+    MT_F_LOAD = 4,        /* internal (summary load): a body segment appended by
                              SnapshotLoader.loadBody (MT/snapshotLoader.ts:195-227) --
                              insertSegments with opArgs undefined: no delta callback, no
                              seq/msn update */
+    MT_F_LOCAL = 8,       /* live handles: the local client's own unsequenced op
+                             (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
+                             MT/client.ts:164-211): applied at refSeq = currentSeq with
+                             UnassignedSequenceNumber; seq / ref_seq / min_seq are ignored */
+    MT_F_ACK = 16         /* live handles: the sequenced echo of one of the local client's
+                             ops (applyMsg with msg.clientId == longClientId ->
+                             ackPendingSegment, MT/client.ts:589-626, 810-812); kind = the
+                             member op's type, positions ignored */
 };
 
 #define MT_NO_PROPS 0xFFFFFFFFu      /* props field: no property set */

@@ -20,6 +20,7 @@
 //   node oracle/ref_harness.mjs snap <config.json> <doc_begin> <doc_end> <out.json>
 //   node oracle/ref_harness.mjs loadfile <config.json> <out.json> <snapshot.json>...
 //   node oracle/ref_harness.mjs farm <out.json> <maxClients> <minLength>...
+//   node oracle/ref_harness.mjs live <config.json> <doc_begin> <doc_end> <out.json>
 import fs from "fs";
 import * as MT from "./_ref/mt/index.mjs";
 import { SnapshotV1 } from "./_ref/mt/snapshotV1.mjs";
@@ -653,6 +654,176 @@ async function farmDoc(minLength, maxClients, doc) {
     return { doc, minLength, seed_text: "", msgs, observer_name: clientNames[0], out: collectOutputs(obs, deltas) };
 }
 
+// ---------------------------------------------------------------- live client (SURVEY §8f #4)
+// A participant Client ("local", short id 0) with its own unsequenced ops, W remote writers
+// and a sequencer: every step either applies a local op (insertSegmentLocal /
+// removeRangeLocal / annotateRangeLocal, MT/client.ts:164-211), sequences the oldest
+// submitted local op (its echo acks it: applyMsg -> ackPendingSegment, :589-626, 810-812),
+// sequences a remote writer's op (generated in its view (refSeq, client) of this replica,
+// as genStep), or reconnects: the unsequenced ops are dropped, the client takes a new long id
+// (startOrUpdateCollaboration, :1065-1071) and regeneratePendingOp (:855-893) rebuilds each
+// pending op, in order, for resubmission.  Events: ["L", op] | ["M", clientId, seq, refSeq,
+// msn, op] | ["R", newClientId, [regenerated op per pending op]].  msn = the minimum of
+// the writers' last refSeqs and the refSeqs of the local client's unsequenced ops (or the
+// refSeq of its last sequenced op).
+function pendingGroups(c) {
+    const all = [];
+    c.mergeTree.pendingSegments.walk((g) => all.push(g));
+    return all;
+}
+function genLocalOp(rng, cfg, len) {
+    const u = rng.next();
+    if (len === 0 || u < frac(cfg.p_insert)) {
+        const pos = rng.uniform(len + 1);
+        const text = genText(rng, 1 + rng.uniform(cfg.text_max), frac(cfg.p_newline));
+        const props = (cfg.p_insert_props > 0 && rng.next() < frac(cfg.p_insert_props)) ? genProps(rng, cfg) : undefined;
+        return { kind: 0, pos, text, props };
+    }
+    const p1 = rng.uniform(len);
+    let n = 1;
+    while (n < 64 && rng.next() < frac(cfg.p_len_continue)) { n++; }
+    const p2 = Math.min(p1 + n, len);
+    if (u < frac(cfg.p_insert + cfg.p_remove)) { return { kind: 1, p1, p2 }; }
+    const props = genProps(rng, cfg);
+    const rw = cfg.p_rewrite > 0 && rng.next() < frac(cfg.p_rewrite);
+    return { kind: 2, p1, p2, props, comb: rw ? { name: "rewrite" } : undefined };
+}
+function liveDoc(cfg, doc) {
+    const rng = new Rng(cfg.seed >>> 0, doc);
+    const seedText = genText(rng, cfg.seed_len, 0);
+    const c = new Client(segmentFromSpec, logger);
+    if (seedText.length > 0) { c.insertSegmentLocal(0, TextSegment.make(seedText)); }
+    let localId = "local-0";
+    c.startOrUpdateCollaboration(localId);
+    const deltas = attachDeltas(c);
+    const W = cfg.writers;
+    const lastRef = new Array(W + 1).fill(0);
+    const cseq = new Array(W + 1).fill(0);
+    let lcseq = 0;
+    let localRef = 0;          // refSeq of the local client's last sequenced op
+    let t = 0;
+    let prevMsn = 0;
+    const unseq = [];          // [{op, ref, sgs}]
+    const events = [];
+    const nextMsn = () => {
+        let m = localRef;
+        for (const u of unseq) { m = Math.min(m, u.ref); }
+        for (let j = 1; j <= W; j++) { m = Math.min(m, lastRef[j]); }
+        prevMsn = Math.max(prevMsn, m);
+        return prevMsn;
+    };
+    const submit = (op, before) => {
+        const sgs = pendingGroups(c).slice(before);
+        unseq.push({ op, ref: c.getCurrentSeq(), sgs });
+    };
+    const trace = [];          // cfg.trace (debugging): the local text after every event
+    for (let step = 0; step < cfg.steps; step++) {
+        if (cfg.trace && trace.length < events.length) {
+            const t = c.createTextHelper().getText(c.getCurrentSeq(), 0);
+            if (cfg.trace === 2) {       // + the leaf table: [len, seq, removedSeq, #groups] per segment, leaf blocks
+                const segs = [];
+                c.mergeTree.walkAllSegments(c.mergeTree.root, (sg) => {
+                    segs.push(sg.cachedLength, sg.seq, sg.removedSeq === undefined ? null : sg.removedSeq,
+                        sg.segmentGroups.size);
+                    return true;
+                });
+                const leaves = [];
+                const walk = (b) => {
+                    if (b.childCount === 0 || b.children[0].isLeaf()) { leaves.push(b.childCount); return; }
+                    for (let i = 0; i < b.childCount; i++) { walk(b.children[i]); }
+                };
+                walk(c.mergeTree.root);
+                // zamboni heap (array order): [maxSeq, leaf index of the segment or -1]; needsScour per leaf block
+                const idx = new Map();
+                let n = 0;
+                c.mergeTree.walkAllSegments(c.mergeTree.root, (sg) => { idx.set(sg, n++); return true; });
+                const heap = c.mergeTree.segmentsToScour.L.slice(1).map((e) =>
+                    [e.maxSeq, e.segment.parent && idx.has(e.segment) ? idx.get(e.segment) : -1]);
+                const flags = [];
+                const walkf = (b) => {
+                    if (b.childCount === 0 || b.children[0].isLeaf()) {
+                        flags.push(b.needsScour === undefined ? -1 : (b.needsScour ? 1 : 0));
+                        return;
+                    }
+                    for (let i = 0; i < b.childCount; i++) { walkf(b.children[i]); }
+                };
+                walkf(c.mergeTree.root);
+                trace.push([t, segs, leaves, heap, flags]);
+            } else {
+                trace.push(t);
+            }
+        }
+        const u = rng.next();
+        if (u < frac(cfg.p_local)) {
+            const len = c.getLength();
+            const g = genLocalOp(rng, cfg, len);
+            const before = pendingGroups(c).length;
+            let op;
+            if (g.kind === 0) {
+                const seg = TextSegment.make(g.text, g.props);
+                op = c.insertSegmentLocal(g.pos, seg);
+            } else if (g.kind === 1) {
+                op = c.removeRangeLocal(g.p1, g.p2);
+            } else {
+                op = c.annotateRangeLocal(g.p1, g.p2, g.props, g.comb);
+            }
+            if (!op) { continue; }
+            op = JSON.parse(JSON.stringify(op));
+            events.push(["L", op]);
+            submit(op, before);
+        } else if (u < frac(cfg.p_local + cfg.p_reconnect)) {
+            if (unseq.length === 0) { continue; }
+            localId = `local-${events.length}`;
+            c.startOrUpdateCollaboration(localId);
+            const old = unseq.splice(0, unseq.length);
+            const regen = [];
+            for (const e of old) {
+                const before = pendingGroups(c).length;
+                const sg = e.op.type === 3 ? e.sgs : e.sgs[0];
+                const nop = JSON.parse(JSON.stringify(c.regeneratePendingOp(e.op, sg)));
+                regen.push(nop);
+                submit(nop, before - (e.op.type === 3 ? e.op.ops.length : 1));
+            }
+            events.push(["R", localId, regen]);
+        } else if (unseq.length > 0 && rng.next() < frac(cfg.p_ack)) {
+            const e = unseq.shift();
+            t++;
+            localRef = e.ref;
+            const msg = makeMsg(0, t, e.ref, nextMsn(), ++lcseq, e.op);
+            msg.clientId = localId;
+            events.push(["M", localId, t, e.ref, msg.minimumSequenceNumber, e.op]);
+            c.applyMsg(JSON.parse(JSON.stringify(msg)));
+        } else {
+            t++;
+            const k = 1 + rng.uniform(W);
+            let lo = Math.max(lastRef[k], t - 1 - cfg.lag, prevMsn);
+            const r = lo + rng.uniform(t - 1 - lo + 1);
+            lastRef[k] = r;
+            const msn = nextMsn();
+            const shortId = c.getOrAddShortClientId(`client-${k}`);
+            const len = c.mergeTree.getLength(r, shortId);
+            const g = genLocalOp(rng, cfg, len);
+            let op;
+            if (g.kind === 0) {
+                op = { pos1: g.pos, seg: g.props ? { text: g.text, props: g.props } : g.text, type: 0 };
+            } else if (g.kind === 1) {
+                op = { pos1: g.p1, pos2: g.p2, type: 1 };
+            } else {
+                op = { pos1: g.p1, pos2: g.p2, props: g.props, type: 2 };
+                if (g.comb) { op.combiningOp = g.comb; }
+            }
+            const msg = makeMsg(k, t, r, msn, ++cseq[k], op);
+            events.push(["M", `client-${k}`, t, r, msn, op]);
+            c.applyMsg(JSON.parse(JSON.stringify(msg)));
+        }
+    }
+    const out = collectOutputs(c, deltas);
+    if (cfg.trace) { out.trace = trace; }
+    out.pending = pendingGroups(c).length;
+    out.localSeq = c.mergeTree.getCollabWindow().localSeq;
+    return { doc, seed_text: seedText, events, out };
+}
+
 const [mode, ...rest] = process.argv.slice(2);
 async function main() {
     if (mode === "gen") {
@@ -661,6 +832,13 @@ async function main() {
         const docs = [];
         for (let d = d0; d < d1; d++) { docs.push(cfg.ext ? genDocExt(cfg, d) : genDoc(cfg, d)); }
         fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }, cfg.p_combine ? jsReplacer : undefined));
+    } else if (mode === "live") {
+        // live <config.json> <doc_begin> <doc_end> <out.json>
+        const cfg = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        const d0 = parseInt(rest[1], 10), d1 = parseInt(rest[2], 10);
+        const docs = [];
+        for (let d = d0; d < d1; d++) { docs.push(liveDoc(cfg, d)); }
+        fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
     } else if (mode === "replay") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));

@@ -7,7 +7,7 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --only name,name]
+    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --live | --only name,name]
 """
 import gzip
 import json
@@ -204,8 +204,39 @@ def make_rich_fixture():
     print("ref_rich", len(out), "docs", sum(len(d["events"]) for d in out), "events")
 
 
+# Live-client path (harness "live"): a participant client's own unsequenced
+# ops, their acks, remote writers' ops resolved around unacked segments, and reconnects with
+# regeneratePendingOp.  Few keys / values: remote annotates collide with pending local ones.
+LIVE_BASE = {"writers": 4, "lag": 16, "seed_len": 24, "text_max": 6, "p_insert": 0.5, "p_remove": 0.25,
+             "p_newline": 0.02, "p_len_continue": 0.6, "p_insert_props": 0.2, "n_keys": 4, "n_values": 4,
+             "max_keys_per_op": 2, "p_null": 0.1, "p_rewrite": 0.3}
+LIVE_FIXTURES = {
+    "ref_live": (dict(LIVE_BASE, seed=4242, steps=600, p_local=0.35, p_reconnect=0.01, p_ack=0.45), 6),
+    # long runs: thousands of segments, many zamboni passes around pending segments
+    "ref_live_long": (dict(LIVE_BASE, seed=4343, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.004,
+                           p_ack=0.6, n_keys=8, n_values=16), 3),
+}
+
+
+def make_live_fixtures():
+    for name, (cfg, ndocs) in LIVE_FIXTURES.items():
+        with tempfile.TemporaryDirectory() as td:
+            cp, op = os.path.join(td, "cfg.json"), os.path.join(td, "out.json")
+            json.dump(cfg, open(cp, "w"))
+            subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "live", cp, "0",
+                                   str(ndocs), op])
+            data = json.load(open(op))
+        for d in data["docs"]:
+            d["out"].pop("tree", None)
+        _dump(name, data)
+        print(name, ndocs, "docs", sum(len(d["events"]) for d in data["docs"]), "events")
+
+
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
+    if "--live" in sys.argv[1:]:
+        make_live_fixtures()
+        return
     if "--snapshots" in sys.argv[1:]:
         make_snapshot_fixtures()
         return
@@ -246,6 +277,7 @@ def main():
     make_farm_fixture()
     make_error_fixture()
     make_rich_fixture()
+    make_live_fixtures()
 
 
 if __name__ == "__main__":

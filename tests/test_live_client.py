@@ -1,0 +1,202 @@
+"""Live-client path: a participant Client's own unsequenced ops, their acks,
+remote ops resolved around unacked segments and reconnect regeneration, on the GPU
+(live_client handles) against streams the reference itself produced
+(tests/golden/ref_live*.json.gz, oracle/ref_harness.mjs "live").  The C restatement
+(oracle/mt_oracle.c) models the observer only, so these tests are pinned to the reference's
+fixtures alone.  Checked per document: every local op the facade returns, every op
+regeneratePendingOp rebuilds, the final text / length / leaf partition / segment table (unacked
+seq and removedSeq = -1) / property sets, every delta-callback record, localSeq and the
+pending segment groups."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+from fluidframework_amd.wire import F_ACK, F_LOCAL, Batch, Interner
+
+LIVE_FIXTURES = ["ref_live", "ref_live_long"]
+
+
+def _msg(ev):
+    _, cid, seq, ref, msn, op = ev
+    return dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
+                type="op", contents=op)
+
+
+def expected_live(doc, interner):
+    exp = gu.expected(dict(doc, out=dict(doc["out"], deltas=[])), interner)
+    flat = []
+    for seq, kind, n, dsegs in doc["out"]["deltas"]:
+        flat += [seq, kind, n]
+        for s in dsegs:
+            flat += [s[0], s[1]]
+            if kind == 2:
+                if len(s) < 3:          # propertyDeltas undefined: an outstanding local rewrite
+                    flat.append(-1)
+                    continue
+                flat.append(len(s[2]))
+                for k, v in s[2].items():
+                    flat += [interner.key(k), gu._sid(interner.val(v))]
+    exp["deltas"] = flat
+    return exp
+
+
+# ---------------------------------------------------------------- CPU: encoding
+def test_live_encoding_flags():
+    """Local ops -> MT_F_LOCAL records of client 0; the echo of one (the local client's long id,
+    GROUPs member by member) -> MT_F_ACK; an empty GROUP -> a seq/msn-only record."""
+    b = Batch(Interner(synthetic=True))
+    ack = dict(clientId="me", sequenceNumber=5, referenceSequenceNumber=3, minimumSequenceNumber=1, type="op",
+               contents={"type": 3, "ops": [{"pos1": 0, "pos2": 1, "type": 1},
+                                             {"pos1": 0, "seg": "x", "type": 0}]})
+    empty = dict(clientId="other", sequenceNumber=6, referenceSequenceNumber=3, minimumSequenceNumber=1,
+                 type="op", contents={"type": 3, "ops": []})
+    b.add_live_doc("", [("local", {"pos1": 0, "seg": "ab", "type": 0}), ("ack", ack), ("msg", empty)],
+                   {"me": 0})
+    ops = b.arrays()["ops"]
+    assert ops["flags"].tolist() == [F_LOCAL, F_ACK | 1, F_ACK, 0]
+    assert ops["client"].tolist() == [0, 0, 0, 1]
+    assert ops["kind"].tolist() == [0, 1, 0, 3]
+
+
+def test_live_fixtures_are_reference_made():
+    for name in LIVE_FIXTURES:
+        fx = gu.load(name)
+        assert fx["config"]["steps"] > 0 and len(fx["docs"]) >= 3
+        for d in fx["docs"]:
+            kinds = {e[0] for e in d["events"]}
+            assert kinds == {"L", "M", "R"}, kinds
+
+
+# ---------------------------------------------------------------- GPU
+def _run_doc(doc, log=True):
+    from fluidframework_amd.live import LiveClient
+    interner = Interner(synthetic=True)
+    lc = LiveClient(doc["seed_text"], seg_capacity=16384, text_capacity=1 << 17,
+                    delta_log_capacity=(1 << 20) if log else 0, interner=interner)
+    lc.startOrUpdateCollaboration("local-0")
+    unseq = []
+    errs = []
+    for ev in doc["events"]:
+        if ev[0] == "L":
+            op = ev[1]
+            if op["type"] == 0:
+                got = lc.insertSegmentLocal(op["pos1"], op["seg"])
+            elif op["type"] == 1:
+                got = lc.removeRangeLocal(op["pos1"], op["pos2"])
+            else:
+                got = lc.annotateRangeLocal(op["pos1"], op["pos2"], op["props"], op.get("combiningOp"))
+            if got != op:
+                errs.append(f"local op {got} != {op}")
+            unseq.append(op)
+        elif ev[0] == "M":
+            if ev[1] == lc.long_client_id:
+                unseq.pop(0)
+            lc.applyMsg(_msg(ev))
+        else:
+            _, new_id, regen = ev
+            lc.startOrUpdateCollaboration(new_id)
+            got = [lc.regeneratePendingOp(o) for o in unseq]
+            if got != regen:
+                errs.append(f"regenerated ops differ at reconnect {new_id}")
+            unseq = regen
+        if len(errs) > 3:
+            break
+    return lc, interner, errs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", LIVE_FIXTURES)
+def test_live_client_matches_reference(name):
+    fx = gu.load(name)
+    bad = []
+    for doc in fx["docs"]:
+        lc, interner, errs = _run_doc(doc)
+        mt = lc.mt
+        rows, leaves = mt.get_segments(0)
+        o = dict(text=mt.get_text(0), length=mt.get_length(0), leaves=leaves, segs=rows,
+                 seg_props=[mt.get_segment_props(0, i) for i in range(len(rows))],
+                 deltas=mt.get_delta_log(0), status=int(mt.status()[0]))
+        errs += gu.compare_oracle(o, expected_live(doc, interner))
+        ls, ng = lc.pendingCounts()
+        if (ls, ng) != (doc["out"]["localSeq"], doc["out"]["pending"]):
+            errs.append(f"localSeq/pending {(ls, ng)} != {(doc['out']['localSeq'], doc['out']['pending'])}")
+        if errs:
+            bad.append((doc["doc"], errs[:4]))
+        lc.close()
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_live_client_acked_state_equals_observer():
+    """Once every local op is acked, the local replica holds what an observer of the same
+    sequenced stream holds: text and property runs (eventual consistency)."""
+    from fluidframework_amd import MergeTreeBatch
+    fx = gu.load("ref_live")
+    doc = fx["docs"][0]
+    lc, interner, errs = _run_doc(doc, log=False)
+    assert not errs, errs
+    # sequence the remaining local ops (their echoes ack them), then replay the whole sequenced
+    # stream on a plain observer handle
+    seq_msgs = [_msg(e) for e in doc["events"] if e[0] == "M"]
+    t = seq_msgs[-1]["sequenceNumber"]
+    pend = []
+    unseq = []      # (op, refSeq at submission = the local client's currentSeq then)
+    cur = 0
+    for ev in doc["events"]:
+        if ev[0] == "L":
+            unseq.append((ev[1], cur))
+        elif ev[0] == "M":
+            cur = ev[2]
+            if ev[1].startswith("local"):
+                unseq.pop(0)
+        else:
+            unseq = [(o, cur) for o in ev[2]]
+    for op, ref in unseq:
+        t += 1
+        m = dict(clientId=lc.long_client_id, sequenceNumber=t, referenceSequenceNumber=ref,
+                 minimumSequenceNumber=seq_msgs[-1]["minimumSequenceNumber"], type="op", contents=op)
+        pend.append(m)
+        lc.applyMsg(m)
+    assert lc.pendingCounts()[1] == 0
+    obs = MergeTreeBatch(1, seg_capacity=16384, text_capacity=1 << 17, lds_seg_capacity=-1)
+    b = Batch(Interner(synthetic=True))
+    b.add_doc(doc["seed_text"], seq_msgs + pend)
+    a = b.arrays()
+    obs.load_initial_text(a["seed_off"], a["seed"])
+    obs.apply_arrays(a)
+    assert int(obs.status()[0]) == 0
+    assert obs.get_text(0) == lc.getText()
+    assert obs.get_prop_runs(0) == lc.mt.get_prop_runs(0)
+    lc.close()
+    obs.close()
+
+
+@pytest.mark.gpu
+def test_live_flags_rejected_on_observer_handles():
+    from fluidframework_amd import MergeTreeBatch
+    mt = MergeTreeBatch(1, seg_capacity=256)
+    b = Batch(Interner(synthetic=True))
+    b.add_live_doc("", [("local", {"pos1": 0, "seg": "ab", "type": 0})], {"me": 0})
+    with pytest.raises(RuntimeError, match="live_client"):
+        mt.apply_arrays(b.arrays())
+    mt.close()
+
+
+@pytest.mark.gpu
+def test_live_local_ops_and_invalid_ranges():
+    """getValidOpRange (MT/client.ts:486-548): out-of-range local ops return None and change
+    nothing; valid ones apply at once in the local view."""
+    from fluidframework_amd.live import LiveClient
+    lc = LiveClient("hello")
+    lc.startOrUpdateCollaboration("me")
+    assert lc.insertSegmentLocal(6, "x") is None
+    assert lc.removeRangeLocal(5, 6) is None
+    assert lc.removeRangeLocal(2, 2) is None
+    assert lc.insertSegmentLocal(5, " world") == {"pos1": 5, "seg": " world", "type": 0}
+    assert lc.removeRangeLocal(0, 1) == {"pos1": 0, "pos2": 1, "type": 1}
+    assert lc.getText() == "ello world"
+    assert lc.pendingCounts() == (2, 2)
+    lc.applyMsg(dict(clientId="me", sequenceNumber=1, referenceSequenceNumber=0, minimumSequenceNumber=0,
+                     type="op", contents={"pos1": 5, "seg": " world", "type": 0}))
+    assert lc.pendingCounts() == (2, 1)
+    lc.close()
