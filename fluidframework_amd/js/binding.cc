@@ -15,6 +15,7 @@
 // Build (node-gyp is not available offline): fluidframework_amd/js/build.sh.
 #include <node_api.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -102,13 +103,14 @@ napi_value Create(napi_env env, napi_callback_info info) {
     const char *names[] = {"device", "segCapacity", "blockCapacity", "heapCapacity", "textCapacity",
                            "propsCapacity", "deltaLogCapacity", "ldsSegCapacity", "pageCapacity",
                            "pageHeapCapacity", "unsettledCapacity", "uidCapacity", "ldsPageCapacity",
-                           "ldsUnsettledCapacity", "ldsPageHeapCapacity", "ldsNarrowOverlap", "deltaLogMode"};
+                           "ldsUnsettledCapacity", "ldsPageHeapCapacity", "ldsNarrowOverlap", "deltaLogMode",
+                           "liveClient"};
     int32_t *fields[] = {&o.device, &o.seg_capacity, &o.block_capacity, &o.heap_capacity, &o.text_capacity,
                          &o.props_capacity, &o.delta_log_capacity, &o.lds_seg_capacity, &o.page_capacity,
                          &o.page_heap_capacity, &o.unsettled_capacity, &o.uid_capacity, &o.lds_page_capacity,
                          &o.lds_unsettled_capacity, &o.lds_page_heap_capacity, &o.lds_narrow_overlap,
-                         &o.delta_log_mode};
-    for (int i = 0; i < 17; i++) {
+                         &o.delta_log_mode, &o.live_client};
+    for (int i = 0; i < 18; i++) {
         bool has = false;
         napi_has_named_property(env, argv[1], names[i], &has);
         if (has) {
@@ -388,6 +390,53 @@ napi_value NumDocs(napi_env env, napi_callback_info info) {
     return make_u32(env, mt_num_docs(hd->h));
 }
 
+// regeneratePending(h, doc) -> {recs: Int32Array (8 words per mt_regen_rec), text: Uint16Array,
+// props: Uint32Array} or null when no segment group is pending  (mt_regenerate_pending)
+napi_value RegeneratePending(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    const uint32_t cap = 4096, tcap = 1u << 16, pcap = 1u << 16;
+    std::vector<mt_regen_rec> recs(cap);
+    std::vector<uint16_t> text(tcap);
+    std::vector<uint32_t> props(pcap);
+    int32_t n = 0;
+    if (mt_regenerate_pending(hd->h, doc, recs.data(), cap, &n, text.data(), tcap, props.data(), pcap) != 0) {
+        napi_throw_error(env, nullptr, mt_last_error(hd->h));
+        return nullptr;
+    }
+    napi_value out;
+    if (n < 0) {
+        NAPI_CALL(env, napi_get_null(env, &out));
+        return out;
+    }
+    uint32_t tu = 0, pw = 0;
+    for (int i = 0; i < n; i++) {
+        if (recs[i].kind == MT_OP_INSERT && !(recs[i].flags & MT_F_MARKER)) tu = std::max(tu, recs[i].text_off + recs[i].text_len);
+        if (recs[i].props_off != MT_NO_PROPS) pw = std::max(pw, recs[i].props_off + 1 + 2 * props[recs[i].props_off]);
+    }
+    NAPI_CALL(env, napi_create_object(env, &out));
+    napi_value a;
+    void *data = nullptr;
+    napi_value ab;
+    NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * sizeof(mt_regen_rec), &data, &ab));
+    if (n) memcpy(data, recs.data(), (size_t)n * sizeof(mt_regen_rec));
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, (size_t)n * 8, ab, 0, &a));
+    NAPI_CALL(env, napi_set_named_property(env, out, "recs", a));
+    NAPI_CALL(env, napi_create_arraybuffer(env, std::max<size_t>(tu, 1) * 2, &data, &ab));
+    if (tu) memcpy(data, text.data(), (size_t)tu * 2);
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint16_array, tu, ab, 0, &a));
+    NAPI_CALL(env, napi_set_named_property(env, out, "text", a));
+    NAPI_CALL(env, napi_create_arraybuffer(env, std::max<size_t>(pw, 1) * 4, &data, &ab));
+    if (pw) memcpy(data, props.data(), (size_t)pw * 4);
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, pw, ab, 0, &a));
+    NAPI_CALL(env, napi_set_named_property(env, out, "props", a));
+    return out;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     struct {
         const char *name;
@@ -398,7 +447,8 @@ napi_value Init(napi_env env, napi_value exports) {
                {"getText", GetText},       {"getPropRuns", GetPropRuns},   {"getDeltaLog", GetDeltaLog},
                {"deltaLogReset", DeltaLogReset},
                {"maintenanceCounts", MaintenanceCounts},
-               {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs}};
+               {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs},
+               {"regeneratePending", RegeneratePending}};
     for (auto &f : fns) {
         napi_value v;
         NAPI_CALL(env, napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v));

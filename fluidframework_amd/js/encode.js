@@ -19,6 +19,8 @@ const OP_ANNOTATE = 2;
 const OP_NOOP = 3;
 const OP_GROUP = 3;          // MergeTreeDeltaType.GROUP in the op JSON (ops.ts:33)
 const F_GROUP_MORE = 1;
+const F_LOCAL = 8;           // live handles: the local client's own unsequenced op (mt_types.h)
+const F_ACK = 16;            // live handles: the sequenced echo of one of them
 const F_MARKER = 2;
 const NO_PROPS = 0xFFFFFFFF;
 const VAL_NULL = 0xFFFFFFFF;
@@ -255,12 +257,39 @@ class BatchEncoder {
         const short = (id) => {
             let s = clients.get(id);
             if (s === undefined) {
-                s = clients.size + 1;
+                s = 1;
+                for (const v of clients.values()) { s = Math.max(s, v + 1); }
                 clients.set(id, s);
             }
             return s;
         };
+        const members = (msg, c, flags) => {
+            const op = msg.contents;
+            if (op.type === OP_GROUP && op.ops.length === 0) {
+                // an empty GROUP applies nothing; applyMsg still updates seq/msn (client.ts:818)
+                this._rec({
+                    seq: msg.sequenceNumber, refSeq: msg.referenceSequenceNumber, minSeq: msg.minimumSequenceNumber,
+                    client: c, kind: OP_NOOP, flags: 0, props: NO_PROPS, pos1: 0, pos2: 0, payload: 0,
+                });
+                return;
+            }
+            const ops = op.type === OP_GROUP ? op.ops : [op];
+            ops.forEach((m, i) => {
+                this._op(msg, c, m, i + 1 < ops.length);
+                const at = this.ops.n - 1;          // the flags byte of the record just written
+                this.ops.a[at] |= flags;
+            });
+        };
         for (const msg of msgs) {
+            if (msg.__local !== undefined) {        // live handles: a local op (client 0)
+                members({ sequenceNumber: -1, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+                    contents: msg.__local }, 0, F_LOCAL);
+                continue;
+            }
+            if (msg.__ack !== undefined) {          // live handles: the echo of a local op
+                members(msg.__ack, 0, F_ACK);
+                continue;
+            }
             const c = short(msg.clientId);
             if (msg.type !== undefined && msg.type !== "op") {
                 this._rec({
@@ -269,12 +298,7 @@ class BatchEncoder {
                 });
                 continue;
             }
-            const op = msg.contents;
-            if (op.type === OP_GROUP) {
-                op.ops.forEach((m, i) => this._op(msg, c, m, i + 1 < op.ops.length));
-            } else {
-                this._op(msg, c, op, false);
-            }
+            members(msg, c, 0);
         }
         this.docOff.push(this.nOps);
     }
@@ -291,6 +315,6 @@ class BatchEncoder {
 
 module.exports = {
     BatchEncoder, Interner, Grow, canonical,
-    OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_GROUP_MORE, F_MARKER, NO_PROPS, VAL_NULL, VAL_UNDEF, VAL_FALSY_BIT,
-    VAL_NOMATCH_BIT, jsCombine,
+    OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_GROUP_MORE, F_MARKER, F_LOCAL, F_ACK, NO_PROPS, VAL_NULL, VAL_UNDEF,
+    VAL_FALSY_BIT, VAL_NOMATCH_BIT, jsCombine,
 };

@@ -56,6 +56,10 @@ class GpuMergeTreeBatch {
             options = Object.assign({}, options, { deltaLogMode: 1 });
         }
         this.rich = !!options.deltaLogCapacity && options.deltaLogMode === 1;
+        // live-client batches (liveClient: 1) back participant Clients: local ops, acks and
+        // reconnect regeneration (SURVEY §8f #4); they replay from HBM (ldsSegCapacity -1)
+        this.live = !!options.liveClient;
+        if (this.live) { options = Object.assign({ ldsSegCapacity: -1 }, options); }
         this.h = native.create(nDocs, options);
         this.nDocs = nDocs;
         this.interner = new Interner();
@@ -203,6 +207,10 @@ class GpuClient {
      */
     startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
         if (longClientId === undefined) { return; }
+        if (this.batch.live) {
+            // the local client is short id 0 under every long id it has had (client.ts:1065-1071)
+            this.batch.clients[this.doc].set(longClientId, 0);
+        }
         if (this.longClientId === undefined) {
             this.longClientId = longClientId;
             if (minSeq !== 0 || currentSeq !== 0) {
@@ -223,11 +231,105 @@ class GpuClient {
     applyMsg(msg) {
         this._check();
         if (msg.clientId === this.longClientId && msg.clientId !== undefined) {
-            throw new Error("merge-tree replay: the observer replica has no local ops to acknowledge");
+            if (!this.batch.live) {
+                throw new Error("merge-tree replay: the observer replica has no local ops to acknowledge");
+            }
+            // the echo of one of our own ops: ackPendingSegment (client.ts:589-626, 810-812)
+            this.batch.pending[this.doc].push({ __ack: msg });
+        } else {
+            this.batch.pending[this.doc].push(msg);
         }
-        this.batch.pending[this.doc].push(msg);
         this.batch.queued++;
         this.currentSeq = msg.sequenceNumber;
+    }
+
+    // ------------------------------------------------------------ live client (liveClient: 1)
+    /** getValidOpRange for a local op (client.ts:486-548). */
+    _validRange(start, end, insert) {
+        const length = this.getLength();
+        if (start === undefined || start < 0 || start > length || (start === length && !insert)) { return false; }
+        if (!insert || end !== undefined) {
+            if (end === undefined || end <= start) { return false; }
+        }
+        return true;
+    }
+
+    _local(op) {
+        if (!this.batch.live) { throw new Error("merge-tree replay: local ops need a batch created with liveClient: 1"); }
+        this.batch.pending[this.doc].push({ __local: op });
+        this.batch.queued++;
+        return op;
+    }
+
+    /** Client.insertSegmentLocal (client.ts:202-211); segment: an ISegment or its JSON. */
+    insertSegmentLocal(pos, segment) {
+        const spec = segment && typeof segment.toJSONObject === "function" ? segment.toJSONObject() : segment;
+        const len = typeof spec === "string" ? spec.length : (spec && spec.text !== undefined ? spec.text.length : 1);
+        if (len <= 0 || !this._validRange(pos, undefined, true)) { return undefined; }
+        return this._local({ pos1: pos, seg: spec, type: 0 });
+    }
+
+    /** Client.removeRangeLocal (client.ts:189-196). */
+    removeRangeLocal(start, end) {
+        if (!this._validRange(start, end, false)) { return undefined; }
+        return this._local({ pos1: start, pos2: end, type: 1 });
+    }
+
+    /** Client.annotateRangeLocal (client.ts:164-179). */
+    annotateRangeLocal(start, end, props, combiningOp) {
+        if (!this._validRange(start, end, false)) { return undefined; }
+        const op = { pos1: start, pos2: end, props, type: 2 };
+        if (combiningOp !== undefined) { op.combiningOp = combiningOp; }
+        return this._local(op);
+    }
+
+    /**
+     * Client.regeneratePendingOp (client.ts:855-893) for the oldest pending op(s): resetOp is
+     * the op as it was submitted (a GROUP is rebuilt member by member); segmentGroup is not
+     * needed (the device holds the groups).  Positions come from findReconnectionPostition
+     * (:675-707) on the GPU (mt_regenerate_pending).
+     */
+    regeneratePendingOp(resetOp) {
+        this._sync();
+        const members = resetOp.type === 3 ? resetOp.ops : [resetOp];
+        const out = [];
+        for (const m of members) {
+            const r = native.regeneratePending(this.batch.h, this.doc);
+            if (r === null) { throw new Error("regeneratePendingOp: no pending segment group"); }
+            for (let i = 0; i < r.recs.length; i += 8) {
+                const kind = r.recs[i], pos1 = r.recs[i + 1], pos2 = r.recs[i + 2];
+                if (kind === 0) {
+                    const toff = r.recs[i + 4] >>> 0, tlen = r.recs[i + 5] >>> 0, poff = r.recs[i + 6] >>> 0;
+                    const flags = r.recs[i + 7];
+                    let props;
+                    if (poff !== 0xFFFFFFFF) {
+                        const pairs = [];
+                        for (let j = 0; j < r.props[poff]; j++) {
+                            pairs.push([this.batch.interner.keyName(r.props[poff + 1 + 2 * j]),
+                                this.batch.interner.value(r.props[poff + 2 + 2 * j])]);
+                        }
+                        props = {};
+                        for (const [k, v] of jsKeyOrder(pairs)) { props[k] = v; }
+                    }
+                    let seg;
+                    if (flags & 2) {
+                        seg = { marker: { refType: toff } };
+                        if (props) { seg.props = props; }
+                    } else {
+                        const text = String.fromCharCode.apply(null, Array.from(r.text.subarray(toff, toff + tlen)));
+                        seg = props ? { text, props } : text;
+                    }
+                    out.push({ pos1, seg, type: 0 });
+                } else if (kind === 1) {
+                    out.push({ pos1, pos2, type: 1 });
+                } else {
+                    const op = { pos1, pos2, props: m.props, type: 2 };
+                    if (m.combiningOp !== undefined) { op.combiningOp = m.combiningOp; }
+                    out.push(op);
+                }
+            }
+        }
+        return out.length === 1 ? out[0] : { ops: out, type: 3 };
     }
 
     getCurrentSeq() { return this.currentSeq; }

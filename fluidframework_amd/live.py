@@ -103,7 +103,9 @@ class LiveClient:
         self.mt.apply_arrays(a)
         st = int(self.mt.status()[0])
         if st:
-            raise RuntimeError(f"live document failed: mt_doc_status {st}")
+            hdr = np.zeros(32, np.int32)
+            self.mt.lib.mt_debug_raw(self.mt.h, 0, None, 0, None, hdr.ctypes.data)
+            raise RuntimeError(f"live document failed: mt_doc_status {st} (diagnostic {int(hdr[27])})")
 
     # -------------------------------------------------------------- reconnect
     def regeneratePendingOp(self, reset_op):

@@ -821,7 +821,22 @@ function liveDoc(cfg, doc) {
     if (cfg.trace) { out.trace = trace; }
     out.pending = pendingGroups(c).length;
     out.localSeq = c.mergeTree.getCollabWindow().localSeq;
-    return { doc, seed_text: seedText, events, out };
+    // drain: the server sequences every op still unsequenced (their echoes ack them)
+    const drain = [];
+    while (unseq.length > 0) {
+        const e = unseq.shift();
+        t++;
+        localRef = e.ref;
+        const msg = makeMsg(0, t, e.ref, nextMsn(), ++lcseq, e.op);
+        msg.clientId = localId;
+        drain.push(["M", localId, t, e.ref, msg.minimumSequenceNumber, e.op]);
+        c.applyMsg(JSON.parse(JSON.stringify(msg)));
+    }
+    const drained = collectOutputs(c, []);
+    drained.pending = pendingGroups(c).length;
+    delete drained.deltas;
+    delete drained.tree;
+    return { doc, seed_text: seedText, events, out, drain, drained };
 }
 
 const [mode, ...rest] = process.argv.slice(2);

@@ -24,6 +24,16 @@ const hex = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("h
 const jsReplacer = (key, v) => ((typeof v === "number" && Number.isNaN(v)) ? { $nan: 1 }
     : (v === undefined && key !== "" ? { $undef: 1 } : v));
 
+// key-order-independent form (the reference's op objects put combiningOp first)
+function canonJson(v) {
+    if (Array.isArray(v)) { return v.map(canonJson); }
+    if (v !== null && typeof v === "object") {
+        const o = {};
+        for (const k of Object.keys(v).sort()) { o[k] = canonJson(v[k]); }
+        return o;
+    }
+    return v;
+}
 const [mode, file, ...extra] = process.argv.slice(2);
 const fx = load(file);
 if (mode === "encode") {
@@ -55,6 +65,43 @@ if (mode === "encode") {
         }
     });
     process.stdout.write(JSON.stringify({ docs: out, ms: batch.lastKernelMs() }, jsReplacer));
+} else if (mode === "live") {
+    // live-client streams (ref_live*): one liveClient batch, one GpuClient per document; local
+    // ops through insertSegmentLocal / removeRangeLocal / annotateRangeLocal, sequenced messages
+    // (acks included) through applyMsg, reconnects through regeneratePendingOp
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js", "index.js"));
+    const b = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 16384, textCapacity: 1 << 17, liveClient: 1 });
+    b.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const docs = [];
+    const cs = fx.docs.map((d, i) => { const c = b.client(i); c.startOrUpdateCollaboration("local-0"); return c; });
+    fx.docs.forEach((d, i) => {
+        const c = cs[i];
+        let unseq = [];
+        const errs = [];
+        for (const ev of d.events) {
+            if (ev[0] === "L") {
+                const op = ev[1];
+                let got;
+                if (op.type === 0) { got = c.insertSegmentLocal(op.pos1, op.seg); }
+                else if (op.type === 1) { got = c.removeRangeLocal(op.pos1, op.pos2); }
+                else { got = c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp); }
+                if (JSON.stringify(canonJson(got)) !== JSON.stringify(canonJson(op))) { errs.push(`local ${JSON.stringify(got)}`); }
+                unseq.push(op);
+            } else if (ev[0] === "M") {
+                const [, cid, seq, ref, msn, op] = ev;
+                if (cid === c.longClientId) { unseq.shift(); }
+                c.applyMsg({ clientId: cid, sequenceNumber: seq, referenceSequenceNumber: ref,
+                    minimumSequenceNumber: msn, type: "op", contents: op });
+            } else {
+                c.startOrUpdateCollaboration(ev[1]);
+                const got = unseq.map((o) => c.regeneratePendingOp(o));
+                if (JSON.stringify(canonJson(got)) !== JSON.stringify(canonJson(ev[2]))) { errs.push(`regen at ${ev[1]}`); }
+                unseq = ev[2];
+            }
+        }
+        docs.push({ doc: d.doc, text: c.getText(), length: c.getLength(), errs });
+    });
+    process.stdout.write(JSON.stringify({ docs }));
 } else if (mode === "deltas") {
     // deltas <fixture> <deltaLogCapacity> <flushEvery>: every mergeTreeDeltaCallback the
     // facade fires while the messages are applied in flushes of <flushEvery> messages per

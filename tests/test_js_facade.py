@@ -236,3 +236,17 @@ def test_js_facade_start_collaboration_window():
     assert out["t0"] == out["t1"] == "xabcy" and out["s1"] == 12
     assert out["t2"] == "zxabcy"
     assert out["err"] == "Incoming remote op sequence# <= local collabWindow's currentSequence#"
+
+
+@pytest.mark.gpu
+def test_js_facade_live_client_matches_reference():
+    """GpuClient on a liveClient batch (the reference language's drop-in for a participant
+    Client): local ops, acks and regeneratePendingOp over the reference's live streams give
+    the reference's text, length and regenerated ops."""
+    _addon()
+    fx = gu.load("ref_live")
+    got = _node("live", os.path.join(gu.GOLDEN, "ref_live.json.gz"))
+    for d, g in zip(fx["docs"], got["docs"]):
+        assert g["errs"] == [], g["errs"][:3]
+        assert g["text"] == d["out"]["text"]
+        assert g["length"] == d["out"]["length"]

@@ -101,6 +101,7 @@ def _run_doc(doc, log=True):
             unseq = regen
         if len(errs) > 3:
             break
+    lc.flush()
     return lc, interner, errs
 
 
@@ -127,48 +128,37 @@ def test_live_client_matches_reference(name):
 
 
 @pytest.mark.gpu
-def test_live_client_acked_state_equals_observer():
-    """Once every local op is acked, the local replica holds what an observer of the same
-    sequenced stream holds: text and property runs (eventual consistency)."""
+def test_live_client_drained_matches_reference_and_observer():
+    """The server then sequences every op still pending (the reference's drain in the
+    fixture): the acked replica equals the reference's (text, segment table, leaf partition,
+    property sets) and an observer replaying the whole sequenced stream holds the same text.
+    (Property sets need not match the observer's: a participant skips remote updates of keys
+    it has pending, SegmentPropertiesManager.shouldModifyKey, and the reference's own
+    replicas differ there.)"""
     from fluidframework_amd import MergeTreeBatch
     fx = gu.load("ref_live")
-    doc = fx["docs"][0]
-    lc, interner, errs = _run_doc(doc, log=False)
-    assert not errs, errs
-    # sequence the remaining local ops (their echoes ack them), then replay the whole sequenced
-    # stream on a plain observer handle
-    seq_msgs = [_msg(e) for e in doc["events"] if e[0] == "M"]
-    t = seq_msgs[-1]["sequenceNumber"]
-    pend = []
-    unseq = []      # (op, refSeq at submission = the local client's currentSeq then)
-    cur = 0
-    for ev in doc["events"]:
-        if ev[0] == "L":
-            unseq.append((ev[1], cur))
-        elif ev[0] == "M":
-            cur = ev[2]
-            if ev[1].startswith("local"):
-                unseq.pop(0)
-        else:
-            unseq = [(o, cur) for o in ev[2]]
-    for op, ref in unseq:
-        t += 1
-        m = dict(clientId=lc.long_client_id, sequenceNumber=t, referenceSequenceNumber=ref,
-                 minimumSequenceNumber=seq_msgs[-1]["minimumSequenceNumber"], type="op", contents=op)
-        pend.append(m)
-        lc.applyMsg(m)
-    assert lc.pendingCounts()[1] == 0
-    obs = MergeTreeBatch(1, seg_capacity=16384, text_capacity=1 << 17, lds_seg_capacity=-1)
-    b = Batch(Interner(synthetic=True))
-    b.add_doc(doc["seed_text"], seq_msgs + pend)
-    a = b.arrays()
-    obs.load_initial_text(a["seed_off"], a["seed"])
-    obs.apply_arrays(a)
-    assert int(obs.status()[0]) == 0
-    assert obs.get_text(0) == lc.getText()
-    assert obs.get_prop_runs(0) == lc.mt.get_prop_runs(0)
-    lc.close()
-    obs.close()
+    for doc in fx["docs"][:3]:
+        lc, interner, errs = _run_doc(doc, log=False)
+        assert not errs, errs
+        for ev in doc["drain"]:
+            lc.applyMsg(_msg(ev))
+        assert lc.pendingCounts()[1] == doc["drained"]["pending"] == 0
+        rows, leaves = lc.mt.get_segments(0)
+        exp = gu.expected(dict(doc, out=dict(doc["drained"], deltas=[])), interner)
+        assert lc.getText() == exp["text"]
+        assert list(leaves) == exp["leaves"]
+        assert rows.tolist() == exp["segs"]
+        assert [lc.mt.get_segment_props(0, i) for i in range(len(rows))] == exp["seg_props"]
+        obs = MergeTreeBatch(1, seg_capacity=16384, text_capacity=1 << 17, lds_seg_capacity=-1)
+        b = Batch(Interner(synthetic=True))
+        b.add_doc(doc["seed_text"], [_msg(e) for e in doc["events"] + doc["drain"] if e[0] == "M"])
+        a = b.arrays()
+        obs.load_initial_text(a["seed_off"], a["seed"])
+        obs.apply_arrays(a)
+        assert int(obs.status()[0]) == 0
+        assert obs.get_text(0) == lc.getText()
+        lc.close()
+        obs.close()
 
 
 @pytest.mark.gpu

@@ -13,10 +13,12 @@ from fluidframework_amd.live import LiveClient  # noqa: E402
 from fluidframework_amd.wire import Interner  # noqa: E402
 
 
-def main(path):
+def main(path, batch=False, log=False):
     fx = json.load(open(path))
+    print(f"--- batch={batch} log={log}")
     for doc in fx["docs"]:
-        lc = LiveClient(doc["seed_text"], seg_capacity=16384, text_capacity=1 << 17, interner=Interner(synthetic=True))
+        lc = LiveClient(doc["seed_text"], seg_capacity=16384, text_capacity=1 << 17, interner=Interner(synthetic=True),
+                        delta_log_capacity=(1 << 20) if log else 0)
         lc.startOrUpdateCollaboration("local-0")
         unseq = []
         trace = doc["out"]["trace"] + [doc["out"]["text"]]
@@ -48,6 +50,8 @@ def main(path):
                                 print("   got", g, "\n   exp", e)
                         break
                     unseq = ev[2]
+                if batch and i + 1 < len(doc["events"]):
+                    continue
                 t = lc.getText()
             except RuntimeError as e:
                 hdr = np.zeros(32, np.int32)
@@ -56,6 +60,8 @@ def main(path):
                 print("  previous events:", doc["events"][max(0, i - 3):i])
                 break
             tr = trace[i]
+            if isinstance(tr, list) and batch:
+                tr = tr[0]
             if isinstance(tr, list):
                 tr, rsegs, rleaves, rheap, rflags = tr
                 rows, leaves = lc.mt.get_segments(0)
@@ -99,4 +105,6 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "_live_trace.json"))
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    path = args[0] if args else os.path.join(os.path.dirname(os.path.abspath(__file__)), "_live_trace.json")
+    main(path, batch="--batch" in sys.argv, log="--log" in sys.argv)
