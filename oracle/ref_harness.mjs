@@ -677,7 +677,8 @@ function genLocalOp(rng, cfg, len) {
         const pos = rng.uniform(len + 1);
         const text = genText(rng, 1 + rng.uniform(cfg.text_max), frac(cfg.p_newline));
         const props = (cfg.p_insert_props > 0 && rng.next() < frac(cfg.p_insert_props)) ? genProps(rng, cfg) : undefined;
-        return { kind: 0, pos, text, props };
+        const marker = cfg.p_marker > 0 && rng.next() < frac(cfg.p_marker) ? 1 + rng.uniform(3) : 0;
+        return { kind: 0, pos, text, props, marker };
     }
     const p1 = rng.uniform(len);
     let n = 1;
@@ -760,7 +761,7 @@ function liveDoc(cfg, doc) {
             const before = pendingGroups(c).length;
             let op;
             if (g.kind === 0) {
-                const seg = TextSegment.make(g.text, g.props);
+                const seg = g.marker ? Marker.make(g.marker, g.props) : TextSegment.make(g.text, g.props);
                 op = c.insertSegmentLocal(g.pos, seg);
             } else if (g.kind === 1) {
                 op = c.removeRangeLocal(g.p1, g.p2);
@@ -804,7 +805,10 @@ function liveDoc(cfg, doc) {
             const len = c.mergeTree.getLength(r, shortId);
             const g = genLocalOp(rng, cfg, len);
             let op;
-            if (g.kind === 0) {
+            if (g.kind === 0 && g.marker) {
+                op = { pos1: g.pos, seg: g.props ? { marker: { refType: g.marker }, props: g.props }
+                    : { marker: { refType: g.marker } }, type: 0 };
+            } else if (g.kind === 0) {
                 op = { pos1: g.pos, seg: g.props ? { text: g.text, props: g.props } : g.text, type: 0 };
             } else if (g.kind === 1) {
                 op = { pos1: g.p1, pos2: g.p2, type: 1 };
