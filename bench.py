@@ -300,6 +300,93 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
     }))
 
 
+def run_live(args, rank, world, local_rank, dist):
+    """Live-client path: participant replicas applying their own
+    local ops, the acks of them and remote writers' ops, on a live_client handle.  The event
+    streams are the reference's own (tests/golden/ref_live_bench.json.gz: 8 participant
+    streams of 4000 steps, made by oracle/ref_harness.mjs live), each replicated over the
+    documents; one step = reset + one batch of every document's whole stream, resident in
+    HBM.  No CPU baseline: the C restatement models the observer only, and the reference
+    cannot travel."""
+    import gzip
+    import numpy as np
+    from fluidframework_amd import MergeTreeBatch
+    from fluidframework_amd.wire import Batch, Interner
+    fx = json.load(gzip.open(os.path.join(REPO, "tests", "golden", "ref_live_bench.json.gz"), "rt"))
+    streams = fx["docs"]
+    docs = args.docs or 4096
+    b = Batch(Interner(synthetic=True))
+    n_events = 0
+    for d in range(docs):
+        st = streams[(rank * docs + d) % len(streams)]
+        ent = []
+        for ev in st["events"]:
+            if ev[0] == "L":
+                ent.append(("local", ev[1]))
+            else:
+                _, cid, seq, ref, msn, op = ev
+                m = dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
+                         type="op", contents=op)
+                ent.append(("ack" if cid == "local-0" else "msg", m))
+        n_events += len(ent)
+        b.add_live_doc(st["seed_text"], ent, {"local-0": 0})
+    a = b.arrays()
+    mt = MergeTreeBatch(docs, device=local_rank, seg_capacity=4096, text_capacity=1 << 15, props_capacity=4096,
+                        heap_capacity=4096, lds_seg_capacity=-1, live_client=1)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    batch = mt.upload(a)
+
+    def step():
+        mt.reset()
+        batch.apply_async()
+
+    for _ in range(args.warmup):
+        step()
+        mt.sync()
+    if dist is not None:
+        dist.barrier()
+    mt.sync()
+    t0 = time.perf_counter()
+    kms = 0.0
+    for _ in range(args.steps):
+        step()
+        mt.sync()
+        kms += mt.last_kernel_ms()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = mt.status()
+    # parity: every replica ends with the reference participant's text, localSeq and queue
+    sample = list(range(min(docs, 32)))
+    bad = 0
+    counts = mt.pending_counts()
+    for d in sample:
+        st = streams[(rank * docs + d) % len(streams)]
+        bad += int(mt.get_text(d) != st["out"]["text"] or
+                   tuple(counts[d]) != (st["out"]["localSeq"], st["out"]["pending"]))
+    if rank != 0:
+        return
+    print(json.dumps({
+        "metric": "live-client merge-tree events applied/sec (local ops + acks + remote ops)",
+        "value": round(n_events * world * args.steps / elapsed, 1), "unit": "events/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000 / args.steps, 3),
+        "kernel_ms_per_step": round(kms / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "data": "the reference's participant streams (ref_live_bench), replicated",
+        "config": {"workload": f"live: {docs} participant documents/GPU x {n_events // docs} events "
+                               f"(local ops 0.3, acks, remote ops from 8 writers, lag 48)",
+                   "docs_total": docs * world, "events_per_step": n_events * world,
+                   "parallelism": f"doc-shard x{world}"},
+        "cpu_baseline": None,
+        "parity": {"status_nonzero": int((status != 0).sum()), "docs_checked": len(sample), "mismatches": bad},
+    }))
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -318,6 +405,8 @@ def main():
 
     from fluidframework_amd import MergeTreeBatch
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
+    if args.config == "live":
+        return run_live(args, rank, world, local_rank, dist)
     cfg = dict(configs[args.config])
     if args.config == "c5":
         run_c5(args, cfg, rank, world, local_rank, dist)

@@ -215,7 +215,10 @@ LIVE_FIXTURES = {
     # long runs: thousands of segments, many zamboni passes around pending segments
     "ref_live_long": (dict(LIVE_BASE, seed=4343, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.004,
                            p_ack=0.6, n_keys=8, n_values=16), 3),
-    # markers (local and remote) among the text: regenerated marker inserts, marker splits never
+    # bench.py --config live: long streams without reconnects, replicated across documents
+    "ref_live_bench": (dict(LIVE_BASE, seed=4545, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.0,
+                            p_ack=0.6, n_keys=8, n_values=16), 8),
+    # markers (local and remote) among the text: regenerated marker inserts
     "ref_live_markers": (dict(LIVE_BASE, seed=4444, steps=800, p_local=0.4, p_reconnect=0.015, p_ack=0.4,
                               p_marker=0.15), 4),
 }
