@@ -383,8 +383,20 @@ def run_live(args, rank, world, local_rank, dist):
                    "docs_total": docs * world, "events_per_step": n_events * world,
                    "parallelism": f"doc-shard x{world}"},
         "cpu_baseline": None,
+        "reference_calibration": _live_calibration(),
         "parity": {"status_nonzero": int((status != 0).sum()), "docs_checked": len(sample), "mismatches": bad},
     }))
+
+
+def _live_calibration():
+    """The reference participant's own speed on the same streams (one thread, measured in the
+    build container: the reference cannot travel to the GPU box)."""
+    p = os.path.join(REPO, "profiles", "r2", "live_calibration.json")
+    if not os.path.exists(p):
+        return None
+    c = json.load(open(p))
+    return dict(value=round(c["events_per_s"], 1), unit="events/s", cores=1, kind="reference",
+                sample=f"{c['events']} events, {os.path.relpath(p, REPO)}")
 
 
 def main():

@@ -858,6 +858,36 @@ async function main() {
         const docs = [];
         for (let d = d0; d < d1; d++) { docs.push(liveDoc(cfg, d)); }
         fs.writeFileSync(rest[3], JSON.stringify({ config: cfg, docs }));
+    } else if (mode === "livetime") {
+        // livetime <live.json(.gz)> <out.json>: the reference participant Client replaying the
+        // live streams' local ops and sequenced messages (no reconnects), one thread, timed
+        const raw = fs.readFileSync(rest[0]);
+        const fx = JSON.parse((rest[0].endsWith(".gz") ? (await import("zlib")).gunzipSync(raw) : raw).toString());
+        let ns = 0n, events = 0;
+        for (const d of fx.docs) {
+            const c = new Client(segmentFromSpec, logger);
+            if (d.seed_text.length > 0) { c.insertSegmentLocal(0, TextSegment.make(d.seed_text)); }
+            c.startOrUpdateCollaboration("local-0");
+            const evs = d.events.map((ev) => (ev[0] === "L" ? ev : ["M", makeMsg(0, ev[2], ev[3], ev[4], 0, ev[5])]));
+            evs.forEach((ev, i) => { if (ev[0] === "M") { ev[1].clientId = d.events[i][1]; } });
+            const t0 = process.hrtime.bigint();
+            for (const ev of evs) {
+                if (ev[0] === "L") {
+                    const op = ev[1];
+                    if (op.type === 0) { c.insertSegmentLocal(op.pos1, segmentFromSpec(op.seg)); }
+                    else if (op.type === 1) { c.removeRangeLocal(op.pos1, op.pos2); }
+                    else { c.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp); }
+                } else {
+                    c.applyMsg(ev[1]);
+                }
+            }
+            ns += process.hrtime.bigint() - t0;
+            events += evs.length;
+            const text = c.createTextHelper().getText(c.getCurrentSeq(), c.getClientId());
+            if (text !== d.out.text) { throw new Error(`doc ${d.doc}: replay differs from the fixture`); }
+        }
+        const sec = Number(ns) / 1e9;
+        fs.writeFileSync(rest[1], JSON.stringify({ events, seconds: sec, events_per_s: events / sec, node: process.version }));
     } else if (mode === "replay") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         const outs = logs.docs.map((d) => ({ doc: d.doc, out: replayDoc(d) }));
