@@ -110,7 +110,9 @@ struct DevState {
     int32_t n_docs;
     // live-client handles (mt_options.live_client; null otherwise)
     int32_t *live;            // [n_docs][4] {collabWindow.localSeq, group queue head id, length, 0}
-    int32_t *grp;             // [n_docs][MT_LIVE_GROUPS + 1][MT_GRP_WORDS] segment-group table
+    int32_t *grp;             // [n_docs][LG + 1][MT_GRP_WORDS] segment-group table (index = id)
+    struct PendQ *segP;       // [n_docs][S] per segment: its pending segment groups
+    int32_t LG;               // group ids per document (outstanding segment groups)
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -216,22 +218,40 @@ __device__ __forceinline__ bool tie(v4i a, int r) {
 // localRemovedSeq (UnassignedSequenceNumber + the segment's localSeq / localRemovedSeq,
 // MT/mergeTree.ts:2102-2104, 2669-2670), so every `seq != Unassigned && seq <= refSeq` test
 // of the observer engine holds unchanged.  Segment groups (MT/mergeTree.ts:1955-1962,
-// segmentGroupCollection.ts) are a FIFO of up to 4 group ids (1..255) per segment in bits
-// 32..63 of its segO word (the overlap slots keep bits 0..31); the group table lives in HBM.
+// segmentGroupCollection.ts) are a FIFO of up to 16 group ids per segment (DevState.segP,
+// PendQ); the group table (a ring of DevState.LG ids) lives in HBM.
 #define MT_LOCAL_BASE 0x40000000
-#define MT_LIVE_GROUPS 255       // group ids 1..255 (outstanding segment groups per document)
-#define MT_GRP_WORDS 12          // group entry {localSeq, kind | rewrite << 8 | nkeys << 16, keys[8], 0, 0}
+#define MT_GRP_WORDS 12          // group entry {localSeq, kind | rewrite << 8 | nkeys << 16, keys[8], id stamp, 0}
+#define MT_PQ_IDS 16             // pending groups a segment can be in at once
 __device__ __forceinline__ bool is_local_seq(int s) { return s >= MT_LOCAL_BASE && s != MT_RSEQ_NONE; }
-__device__ __forceinline__ uint32_t pend_word(u64 o) { return (uint32_t)(o >> 32); }
-__device__ __forceinline__ int pend_first(u64 o) { return (int)(pend_word(o) & 0xFFu); }
-__device__ __forceinline__ u64 pend_pop(u64 o) { return (o & 0xFFFFFFFFull) | ((u64)(pend_word(o) >> 8) << 32); }
-// enqueue group g at the tail of the segment's FIFO; false when it holds 4 already
-__device__ __forceinline__ bool pend_push(u64 &o, int g) {
-    const uint32_t w = pend_word(o);
-    const int n = w == 0 ? 0 : (w >> 8) == 0 ? 1 : (w >> 16) == 0 ? 2 : (w >> 24) == 0 ? 3 : 4;
-    if (n == 4) return false;
-    o |= (u64)((uint32_t)g << (8 * n)) << 32;
-    return true;
+// A segment's pending segment groups: FIFO of group ids (1..DevState.LG, 16 bits each, the
+// oldest in the low bits of w[0]); all zero: none.
+struct PendQ {
+    u64 w[4];
+};
+__device__ __forceinline__ PendQ pq_zero() { return PendQ{{0ull, 0ull, 0ull, 0ull}}; }
+__device__ __forceinline__ bool pq_any(const PendQ &q) { return (q.w[0] | q.w[1] | q.w[2] | q.w[3]) != 0ull; }
+__device__ __forceinline__ int pq_first(const PendQ &q) { return (int)(q.w[0] & 0xFFFFull); }
+__device__ __forceinline__ int pq_at(const PendQ &q, int k) { return (int)((q.w[k >> 2] >> (16 * (k & 3))) & 0xFFFFull); }
+__device__ __forceinline__ PendQ pq_pop(PendQ q) {
+    PendQ r;
+    r.w[0] = (q.w[0] >> 16) | (q.w[1] << 48);
+    r.w[1] = (q.w[1] >> 16) | (q.w[2] << 48);
+    r.w[2] = (q.w[2] >> 16) | (q.w[3] << 48);
+    r.w[3] = q.w[3] >> 16;
+    return r;
+}
+// enqueue group g at the tail; false when the FIFO is full
+__device__ __forceinline__ bool pq_push(PendQ &q, int g) {
+    for (int k = 0; k < MT_PQ_IDS; k++)
+        if (pq_at(q, k) == 0) {
+            q.w[k >> 2] |= (u64)(uint32_t)g << (16 * (k & 3));
+            return true;
+        }
+    return false;
+}
+__device__ __forceinline__ PendQ pq_bcast(const PendQ &q, int l) {
+    return PendQ{{bcast64(q.w[0], l), bcast64(q.w[1], l), bcast64(q.w[2], l), bcast64(q.w[3], l)}};
 }
 // breakTie for the local client's own insert (MT/mergeTree.ts:2290-2298: "local change see
 // everything" after the removed-at-or-below-refSeq test)

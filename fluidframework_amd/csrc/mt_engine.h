@@ -51,14 +51,14 @@ template <bool kLogT> struct TierGlbT {
     typedef GLB_AS v2i *H_t;
 };
 // Live-client documents (mt_device.h MT_LOCAL_BASE): the HBM tier plus the local client's
-// unacked ops and segment groups (MT/client.ts:164-274, 589-626, 709-893).  Overlap slots use
-// bits 0..31 of segO, the segment-group FIFO bits 32..63.
+// unacked ops and segment groups (MT/client.ts:164-274, 589-626, 709-893); every segment also
+// carries its segment-group FIFO (DocT.P, moved with the segment).
 template <bool kLogT> struct TierLiveT {
     static constexpr bool kLds = false;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = false;
     static constexpr bool kLive = true;
-    static constexpr int kOvlBits = 32;
+    static constexpr int kOvlBits = 64;
     typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
@@ -160,13 +160,27 @@ template <class T> struct DocT {
     int local_seq, g_head, g_n;
     int lop;                // the current message is the local client's own op
     int lg;                 // its segment group id
-    GLB_AS int32_t *grp;    // [MT_LIVE_GROUPS + 1][MT_GRP_WORDS] group table (index = id)
+    GLB_AS int32_t *grp;    // [LG + 1][MT_GRP_WORDS] group table (index = id)
+    GLB_AS u64 *P;          // [S][4] each segment's pending segment groups (mt_device.h PendQ)
+    int LG;                 // group ids 1..LG
 #ifdef MT_PROF
     LDS_AS u64 *prof;       // [32] section timers
 #endif
 };
 
 #define TD template <class T> __device__ __forceinline__
+// live documents: segment i's pending-group FIFO in HBM (4 words)
+TD PendQ pq_get(DocT<T> &d, int i) {
+    const GLB_AS u64 *w = d.P + 4 * (size_t)i;
+    return PendQ{{w[0], w[1], w[2], w[3]}};
+}
+TD void pq_put(DocT<T> &d, int i, const PendQ &q) {
+    GLB_AS u64 *w = d.P + 4 * (size_t)i;
+    w[0] = q.w[0];
+    w[1] = q.w[1];
+    w[2] = q.w[2];
+    w[3] = q.w[3];
+}
 
 #ifdef MT_PROF
 __device__ unsigned long long g_prof[32];
@@ -410,7 +424,9 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
         d.local_seq = lv[0];
         d.g_head = lv[1];
         d.g_n = lv[2];
-        d.grp = (GLB_AS int32_t *)(st.grp + (size_t)doc * (MT_LIVE_GROUPS + 1) * MT_GRP_WORDS);
+        d.LG = st.LG;
+        d.grp = (GLB_AS int32_t *)(st.grp + (size_t)doc * (st.LG + 1) * MT_GRP_WORDS);
+        d.P = (GLB_AS u64 *)(st.segP + (size_t)doc * st.S);
     }
     if (d.status) return true;   // failed earlier: the caller leaves it untouched
     if (h.pad[HDR_PAGED]) {      // lives in the paged layout: the paged kernel replays it
@@ -561,17 +577,20 @@ TD void seg_move_right(DocT<T> &d, int from, int k) {
         const int i = lo + lane();
         v4i a;
         u64 o;
+        PendQ pq = pq_zero();
         v4u b;
         if (i < hi) {
             a = d.A[i];
             o = d.O[i];
             b = d.Bv[i];
+            if constexpr (T::kLive) pq = pq_get(d, i);
         }
         wsync<T>();
         if (i < hi) {
             d.A[i + k] = a;
             d.O[i + k] = o;
             d.Bv[i + k] = b;
+            if constexpr (T::kLive) pq_put(d, i + k, pq);
         }
         wsync<T>();
     }
@@ -583,17 +602,20 @@ TD void seg_move_left(DocT<T> &d, int from, int k) {
         const int i = lo + lane();
         v4i a;
         u64 o;
+        PendQ pq = pq_zero();
         v4u b;
         if (i < d.n) {
             a = d.A[i];
             o = d.O[i];
             b = d.Bv[i];
+            if constexpr (T::kLive) pq = pq_get(d, i);
         }
         wsync<T>();
         if (i < d.n) {
             d.A[i - k] = a;
             d.O[i - k] = o;
             d.Bv[i - k] = b;
+            if constexpr (T::kLive) pq_put(d, i - k, pq);
         }
         wsync<T>();
     }
@@ -934,7 +956,7 @@ TD void text_gc(DocT<T> &d) {
         // (a live document keeps the text of segments in a pending group: regeneratePendingOp
         // re-creates an unacked insert the local client has removed since)
         bool keep = a.z == MT_RSEQ_NONE || (T::kLog && d.rich);
-        if constexpr (T::kLive) keep = keep || (i < d.n && pend_word(d.O[i]) != 0u);
+        if constexpr (T::kLive) keep = keep || (i < d.n && pq_any(pq_get(d, i)));
         const bool live = i < d.n && keep && !(b.z & MT_MARKER_BIT);
         const int len = live ? a.x : 0;
         const int inc = wave_scan_incl(len);
@@ -1218,6 +1240,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
         d.A[i + 1] = r;
         d.O[i + 1] = d.O[i];
         d.Bv[i + 1] = rb;
+        if constexpr (T::kLive) pq_put(d, i + 1, pq_get(d, i));   // the right half joins the left one's groups
     }
     d.next_uid++;
     d.n++;
@@ -1345,7 +1368,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     const bool marker = (b.z & MT_MARKER_BIT) != 0;
     // a segment in a pending segment group is held (scourNode :1328, :1389-1392)
     bool pend = false;
-    if constexpr (T::kLive) pend = in && pend_word(d.O[in ? s + k : s]) != 0u;
+    if constexpr (T::kLive) pend = in && pq_any(pq_get(d, in ? s + k : s));
     const bool settled = in && !pend && !removed && a.y <= d.min_seq;   // merge candidate
     // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
     const bool need_nl = settled && !marker && a.x > 0 && !(b.w & SEGF_NL_KNOWN);
@@ -1509,11 +1532,13 @@ TD int scour_block(DocT<T> &d, int s, int e) {
         const bool surv = (m_keep >> k) & 1ull;
         v4i sa;
         u64 so;
+        PendQ sp = pq_zero();
         v4u sb;
         if (surv) {
             sa = d.A[s + k];
             so = d.O[s + k];
             sb = d.Bv[s + k];
+            if constexpr (T::kLive) sp = pq_get(d, s + k);
         }
         const int dst = s + __popcll(m_keep & ((1ull << k) - 1ull));
         wsync<T>();
@@ -1521,6 +1546,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
             d.A[dst] = sa;
             d.O[dst] = so;
             d.Bv[dst] = sb;
+            if constexpr (T::kLive) pq_put(d, dst, sp);
         }
         wsync<T>();
         seg_move_left(d, e, cntb - keep);
@@ -1557,7 +1583,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
     const bool removed = a.z != MT_RSEQ_NONE;
     const bool marker = (b.z & MT_MARKER_BIT) != 0;
     bool pend = false;   // held: in a pending segment group (scourNode :1328)
-    if constexpr (T::kLive) pend = in && pend_word(d.O[in ? s + k : s]) != 0u;
+    if constexpr (T::kLive) pend = in && pq_any(pq_get(d, in ? s + k : s));
     const bool cand = in && !pend && !removed && a.y <= d.min_seq;
     if (!serial) {
         // resolve unknown trailing-newline flags of merge candidates (lanes in parallel)
@@ -1706,11 +1732,13 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         // compaction: survivors to the front, tail moved left
         v4i sa;
         u64 so;
+        PendQ sp = pq_zero();
         v4u sb;
         if (surv) {
             sa = d.A[s + k];
             so = d.O[s + k];
             sb = d.Bv[s + k];
+            if constexpr (T::kLive) sp = pq_get(d, s + k);
         }
         const int dst = s + __popcll(m_surv & ((1ull << k) - 1ull));
         wsync<T>();
@@ -1718,6 +1746,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
             d.A[dst] = sa;
             d.O[dst] = so;
             d.Bv[dst] = sb;
+            if constexpr (T::kLive) pq_put(d, dst, sp);
         }
         wsync<T>();
         seg_move_left(d, s + tot, tot - keep);
@@ -2087,7 +2116,12 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     const uint32_t uid = (uint32_t)d.next_uid;
     if (lane() == 0) {
         d.A[x] = v4i{slen, seq, MT_RSEQ_NONE, pack_cli(c, 0)};
-        d.O[x] = (T::kLive && d.lop) ? ((u64)(uint32_t)d.lg << 32) : 0ull;   // addToPendingList :2128
+        d.O[x] = 0ull;
+        if constexpr (T::kLive) {   // addToPendingList :2128
+            PendQ q = pq_zero();
+            q.w[0] = d.lop ? (u64)(uint32_t)d.lg : 0ull;
+            pq_put(d, x, q);
+        }
         d.Bv[x] = v4u{toff, ph, uid | (marker ? MT_MARKER_BIT : 0u), segw | nomatch};
     }
     d.next_uid++;
@@ -2127,16 +2161,20 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
 // Live documents: the pending-property state of a segment (SegmentPropertiesManager
 // pendingKeyUpdateCount / pendingRewriteCount, MT/segmentPropertiesManager.ts:13-14, 19-33)
 // is the set of unacked local annotate groups in its segment-group FIFO (word pw).
-TD bool grp_pending_rewrite(DocT<T> &d, uint32_t pw) {
-    for (; pw; pw >>= 8) {
-        const int w1 = d.grp[(int)(pw & 0xFFu) * MT_GRP_WORDS + 1];
+TD bool grp_pending_rewrite(DocT<T> &d, const PendQ &pw) {
+    for (int q = 0; q < MT_PQ_IDS; q++) {
+        const int id = pq_at(pw, q);
+        if (id == 0) break;
+        const int w1 = d.grp[id * MT_GRP_WORDS + 1];
         if ((w1 & 0xFF) == MT_OP_ANNOTATE && ((w1 >> 8) & 0xFF)) return true;
     }
     return false;
 }
-TD bool grp_pending_key(DocT<T> &d, uint32_t pw, uint32_t k) {
-    for (; pw; pw >>= 8) {
-        const GLB_AS int32_t *g = d.grp + (int)(pw & 0xFFu) * MT_GRP_WORDS;
+TD bool grp_pending_key(DocT<T> &d, const PendQ &pw, uint32_t k) {
+    for (int q = 0; q < MT_PQ_IDS; q++) {
+        const int id = pq_at(pw, q);
+        if (id == 0) break;
+        const GLB_AS int32_t *g = d.grp + id * MT_GRP_WORDS;
         if ((g[1] & 0xFF) != MT_OP_ANNOTATE) continue;
         const int nk = (g[1] >> 16) & 0xFF;
         for (int j = 0; j < nk; j++)
@@ -2149,7 +2187,7 @@ TD bool grp_pending_key(DocT<T> &d, uint32_t pw, uint32_t k) {
 // local update are not modified (shouldModifyKey :56-63), an outstanding local rewrite blocks
 // the whole op (:48-51: *undef = true, propertyDeltas undefined, the set unchanged).
 TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint32_t *rec, u64 &sh,
-                        GLB_AS int32_t *logp, int &nlog, bool *nomatch = nullptr, uint32_t pw = 0u,
+                        GLB_AS int32_t *logp, int &nlog, bool *nomatch = nullptr, PendQ pw = pq_zero(),
                         bool *undef = nullptr) {
     const uint32_t cntk = rec[0] & 0xFFFF, comb = rec[0] >> 16;
     const GLB_AS uint32_t *o = oh ? prec(d, d.props_half, oh) : nullptr;
@@ -2158,21 +2196,21 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
     uint32_t n = 0;
     int npd = 0;
     if constexpr (T::kLive) {
-        if (pw && grp_pending_rewrite(d, pw)) {
+        if (pq_any(pw) && grp_pending_rewrite(d, pw)) {
             for (uint32_t i = 0; i < 2 * on; i++) t[1 + i] = o[1 + i];
             t[0] = on;
             sh = fnv_u32(sh, 0xFFFFFFFFu);
             if (undef) *undef = true;
             return true;
         }
-        if (comb == MT_COMBINE_TABLE) pw = 0;   // a combining op modifies every key
+        if (comb == MT_COMBINE_TABLE) pw = pq_zero();   // a combining op modifies every key
     }
     // rewrite: delete keys whose new value is not truthy (:66-79)
     for (uint32_t i = 0; i < on; i++) {
         const uint32_t k = o[1 + 2 * i], v = o[2 + 2 * i];
         bool in_new = false, truthy = false;
         if constexpr (T::kLive) {
-            if (pw && grp_pending_key(d, pw, k)) {   // kept: a pending local update
+            if (pq_any(pw) && grp_pending_key(d, pw, k)) {   // kept: a pending local update
                 t[1 + 2 * n] = k;
                 t[2 + 2 * n] = v;
                 n++;
@@ -2204,7 +2242,7 @@ TD bool annotate_record(DocT<T> &d, uint32_t oh, uint32_t nh, const GLB_AS uint3
     for (uint32_t j = 0; j < cntk; j++) {
         const uint32_t k = rec[1 + 2 * j], v = rec[2 + 2 * j];
         if constexpr (T::kLive) {
-            if (pw && grp_pending_key(d, pw, k)) continue;
+            if (pq_any(pw) && grp_pending_key(d, pw, k)) continue;
         }
         int idx = -1;
         for (uint32_t q = 0; q < n; q++)
@@ -2342,9 +2380,9 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                 d.A[i] = a;
                 if constexpr (T::kLive) {   // the local client's remove: addToPendingList :2683-2684
                     if (d.lop) {
-                        u64 po = o;
-                        if (pend_push(po, d.lg))
-                            d.O[i] = po;
+                        PendQ pq = pq_get(d, i);
+                        if (pq_push(pq, d.lg))
+                            pq_put(d, i, pq);
                         else
                             bad = true;
                     }
@@ -2362,16 +2400,16 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         if (!rem && sel) {
             int unused = 0;
             bool nm = rec_nm || (bv.w & SEGF_NOMATCH) != 0;
-            uint32_t pw = 0;
+            PendQ pw = pq_zero();
             if constexpr (T::kLive) {
+                PendQ pq = pq_get(d, i);
                 if (d.lop) {   // the local client's annotate: addToPendingList :2611-2612
-                    u64 po = o;
-                    if (pend_push(po, d.lg))
-                        d.O[i] = po;
+                    if (pq_push(pq, d.lg))
+                        pq_put(d, i, pq);
                     else
                         bad = true;
                 } else {
-                    pw = pend_word(o);
+                    pw = pq;
                 }
             }
             if (!annotate_record(d, bv.y, nh, rec, sh, (GLB_AS int32_t *)nullptr, unused, &nm, pw)) bad = true;
@@ -2411,8 +2449,10 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                     // propertyDeltas: <= one per old key (rewrite) plus one per op key
                     if (cb_room(d, 1 + 2 * (MT_KMAX + (int)(rec[0] & 0xFFFF)))) {
                         const int at = d.dlog_n + 1;
-                        uint32_t pwj = 0;
-                        if constexpr (T::kLive) pwj = d.lop ? 0u : pend_word(bcast64(o, j));
+                        PendQ pwj = pq_zero();
+                        if constexpr (T::kLive) {
+                            if (!d.lop) pwj = pq_bcast(pq_get(d, v ? i : 0), j);
+                        }
                         if (L == 0) {
                             // old record is untouched (new record went to a fresh handle)
                             bool undef = false;
@@ -2528,13 +2568,13 @@ TD void live_local(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const
     if (op.kind != MT_OP_INSERT && op.kind != MT_OP_REMOVE && op.kind != MT_OP_ANNOTATE) return;
     const GLB_AS uint32_t *rec = (op.kind == MT_OP_ANNOTATE && op.props != MT_NO_PROPS) ? pin + op.props : nullptr;
     const int nk = rec ? (int)(rec[0] & 0xFFFFu) : 0;
-    if (d.g_n >= MT_LIVE_GROUPS || nk > MT_KMAX) {
+    if (d.g_n >= d.LG || nk > MT_KMAX) {
         if (d.status == 0) d.cap_cause = nk > MT_KMAX ? 13 : 12;
         fail(d, MT_DOC_CAPACITY);
         return;
     }
     const int ls = ++d.local_seq;
-    const int g = (d.g_head - 1 + d.g_n) % MT_LIVE_GROUPS + 1;
+    const int g = (d.g_head - 1 + d.g_n) % d.LG + 1;
     GLB_AS int32_t *ge = d.grp + g * MT_GRP_WORDS;
     const int rw = rec && (rec[0] >> 16) == MT_COMBINE_REWRITE ? 1 : 0;
     if (lane() == 0) {
@@ -2590,7 +2630,7 @@ TD void live_ack(DocT<T> &d, const mt_op_rec &op) {
                     const int i = base + lane();
                     const bool v = i < d.n;
                     const uint32_t uid = v ? (d.Bv[i].z & ~MT_MARKER_BIT) : 0xFFFFFFFFu;
-                    const bool c = v && pend_first(d.O[i]) == g && uid >= last;
+                    const bool c = v && pq_first(pq_get(d, i)) == g && uid >= last;
                     uint32_t mn = c ? uid : 0xFFFFFFFFu;
 #pragma unroll
                     for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, MT_WAVE));
@@ -2606,7 +2646,8 @@ TD void live_ack(DocT<T> &d, const mt_op_rec &op) {
                 load_ao(d, i, v, a, o);
                 const v4u bv = d.Bv[v ? i : 0];
                 const uint32_t uid = bv.z & ~MT_MARKER_BIT;
-                const bool mem0 = v && pend_first(o) == g;
+                const PendQ pq = pq_get(d, v ? i : 0);
+                const bool mem0 = v && pq_first(pq) == g;
                 const bool late = mem0 && uid >= ustamp;
                 if (pass == 0) n_late += __popcll(ballot(late));
                 const bool mem = pass == 0 ? (mem0 && !late) : (mem0 && uid == pick);
@@ -2619,7 +2660,7 @@ TD void live_ack(DocT<T> &d, const mt_op_rec &op) {
                         a.z = op.seq;   // else a remote remove replaced it: ack returns false
                     }
                     d.A[i] = a;
-                    d.O[i] = pend_pop(o);
+                    pq_put(d, i, pq_pop(pq));
                 }
                 if (ballot(bad)) {
                     FAIL_INTERNAL(d);
@@ -2635,7 +2676,7 @@ TD void live_ack(DocT<T> &d, const mt_op_rec &op) {
             }
         }
     }
-    d.g_head = g % MT_LIVE_GROUPS + 1;
+    d.g_head = g % d.LG + 1;
     d.g_n--;
 }
 

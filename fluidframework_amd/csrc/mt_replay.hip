@@ -32,6 +32,10 @@ __device__ static void init_doc_hdr(const DevState &st, int doc, int len) {
         st.segA[doc * S] = v4i{len, 0, MT_RSEQ_NONE, pack_cli(-1, 0)};
         st.segO[doc * S] = 0ull;
         st.segB[doc * S] = v4u{0u, 0u, 1u, 0u};
+        if (st.segP) {
+            u64 *w = (u64 *)(st.segP + doc * S);
+            w[0] = w[1] = w[2] = w[3] = 0ull;
+        }
     }
     st.cnt[(size_t)doc * MT_LV * st.B] = len > 0 ? 1 : 0;
     st.flg[(size_t)doc * st.B] = MT_SCOUR_UNDEF;
@@ -156,6 +160,10 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
             if (nm) w |= SEGF_NOMATCH;
             dA[i] = v4i{r.len, r.seq, r.removed_seq, pack_cli(r.client, rem ? r.removed_client : 0)};
             dO[i] = 0ull;
+            if (st.segP && !big) {   // no pending groups
+                u64 *w = (u64 *)(st.segP + doc * (size_t)st.S + i);
+                w[0] = w[1] = w[2] = w[3] = 0ull;
+            }
             dB[i] = v4u{marker ? r.payload : (uint32_t)toff, hp ? (uint32_t)ph : 0u,
                         (uint32_t)(i + 1) | (marker ? MT_MARKER_BIT : 0u), w};
         }
@@ -1103,7 +1111,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
     const int g = d.g_head;
     const int gw = lane() < MT_GRP_WORDS ? d.grp[g * MT_GRP_WORDS + lane()] : 0;   // the entry, lane j = word j
     const int ls = bcast(gw, 0), kind = bcast(gw, 1) & 0xFF;
-    d.g_head = g % MT_LIVE_GROUPS + 1;   // dequeue first: the new groups may reuse its table slot
+    d.g_head = g % d.LG + 1;   // dequeue first: the new groups may reuse its table slot
     d.g_n--;
     int carry = 0, nout = 0, tu = 0, pw = 0;
     bool over = false;
@@ -1119,20 +1127,21 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
         const int cl = v && ins && nrem ? a.x : 0;
         const int inc = wave_scan_incl(cl);
         const int pos = carry + inc - cl;
-        const bool mem = v && pend_first(o) == g;
+        const PendQ pq = pq_get(d, v ? i : 0);
+        const bool mem = v && pq_first(pq) == g;
         for (u64 m = ballot(mem); m && !over; m &= m - 1) {
             const int j = first_lane(m);
             const int ij = base + j;
-            u64 oj = pend_pop(bcast64(o, j));
+            PendQ oj = pq_pop(pq_bcast(pq, j));
             const int aj_x = bcast(a.x, j), aj_z = bcast(a.z, j);
             const bool emit = kind != MT_OP_REMOVE || is_local_seq(aj_z);
             if (emit) {
                 const uint32_t bx = (uint32_t)bcast((int)b.x, j), by = (uint32_t)bcast((int)b.y, j);
                 const bool mk = (bcast((int)b.z, j) & MT_MARKER_BIT) != 0;
                 const int np = (kind == MT_OP_INSERT && by) ? (int)prec(d, d.props_half, by)[0] : -1;
-                const int ng = (d.g_head - 1 + d.g_n) % MT_LIVE_GROUPS + 1;
+                const int ng = (d.g_head - 1 + d.g_n) % d.LG + 1;
                 const int tneed = kind == MT_OP_INSERT && !mk ? aj_x : 0;
-                if (nout >= cap || d.g_n >= MT_LIVE_GROUPS || !pend_push(oj, ng) || tu + tneed > tcap ||
+                if (nout >= cap || d.g_n >= d.LG || !pq_push(oj, ng) || tu + tneed > tcap ||
                     pw + 1 + 2 * max(np, 0) > pcap) {
                     over = true;
                     break;
@@ -1165,7 +1174,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
                 }
                 nout++;
             }
-            if (lane() == 0) d.O[ij] = oj;
+            if (lane() == 0) pq_put(d, ij, oj);
         }
         carry += bcast(inc, MT_WAVE - 1);
     }
@@ -1365,7 +1374,9 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.stats, 16 * sizeof(uint32_t));
     if (h->live) {
         alloc((void **)&st.live, N * 4 * sizeof(int32_t));
-        alloc((void **)&st.grp, N * (size_t)(MT_LIVE_GROUPS + 1) * MT_GRP_WORDS * sizeof(int32_t));
+        st.LG = std::min(std::max(o.live_group_capacity > 0 ? o.live_group_capacity : 1024, 16), 65535);
+        alloc((void **)&st.grp, N * (size_t)(st.LG + 1) * MT_GRP_WORDS * sizeof(int32_t));
+        alloc((void **)&st.segP, N * (size_t)st.S * sizeof(PendQ));
     }
     if (st.PP > 0) {
         const size_t slots = N * (size_t)st.PP * MT_PG_SLOTS;
@@ -1401,7 +1412,7 @@ void mt_destroy(mt_handle *h) {
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
                   st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot,
-                  st.live, st.grp};
+                  st.live, st.grp, st.segP};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -2283,7 +2294,7 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
         r[2] = (int)(short)(a.w & 0xFFFF);
         r[3] = lrem ? -1 : a.z;
         r[4] = a.z == MT_RSEQ_NONE ? MT_RSEQ_NONE : (int)(short)((uint32_t)a.w >> 16);
-        r[5] = __builtin_popcountll(h->live ? (hd.O[i] & 0xFFFFFFFFull) : hd.O[i]);
+        r[5] = __builtin_popcountll(hd.O[i]);
         r[6] = (b.z & MT_MARKER_BIT) ? (int32_t)b.x : -1;
         r[7] = b.y ? 1 : 0;
     }

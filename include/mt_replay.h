@@ -81,11 +81,12 @@ typedef struct mt_options {
        the local client (startOrUpdateCollaboration's own id, MT/client.ts:1053-1064):
        records flagged MT_F_LOCAL are its own unsequenced ops, MT_F_ACK records the sequenced
        echoes of them (ackPendingSegment), and mt_regenerate_pending rebuilds the oldest
-       pending op after a reconnect.  Live handles replay from HBM (no LDS / paged tiers);
-       per document at most 255 segment groups (unacked ops) are outstanding, a segment is in
-       at most 4 of them and 32 clients' overlapping removes are unsettled at once
-       (MT_DOC_CAPACITY beyond). */
+       pending op after a reconnect.  Live handles replay from HBM (no LDS / paged tiers); a
+       segment can be in 16 pending segment groups at once (MT_DOC_CAPACITY beyond). */
     int32_t live_client;
+    /* live handles: segment groups (unacked ops, one per regenerated segment after a
+       reconnect) a document may have outstanding (default 1024, at most 65535) */
+    int32_t live_group_capacity;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

@@ -718,7 +718,14 @@ function liveDoc(cfg, doc) {
         unseq.push({ op, ref: c.getCurrentSeq(), sgs });
     };
     const trace = [];          // cfg.trace (debugging): the local text after every event
+    let maxDepth = 0;          // deepest segment-group queue of any segment (cfg.track_depth)
     for (let step = 0; step < cfg.steps; step++) {
+        if (cfg.track_depth) {
+            c.mergeTree.walkAllSegments(c.mergeTree.root, (sg) => {
+                maxDepth = Math.max(maxDepth, sg.segmentGroups.size);
+                return true;
+            });
+        }
         if (cfg.trace && trace.length < events.length) {
             const t = c.createTextHelper().getText(c.getCurrentSeq(), 0);
             if (cfg.trace === 2) {       // + the leaf table: [len, seq, removedSeq, #groups] per segment, leaf blocks
@@ -825,6 +832,7 @@ function liveDoc(cfg, doc) {
     if (cfg.trace) { out.trace = trace; }
     out.pending = pendingGroups(c).length;
     out.localSeq = c.mergeTree.getCollabWindow().localSeq;
+    if (cfg.track_depth) { out.maxGroupDepth = maxDepth; }
     // drain: the server sequences every op still unsequenced (their echoes ack them)
     const drain = [];
     while (unseq.length > 0) {

@@ -218,6 +218,10 @@ LIVE_FIXTURES = {
     # bench.py --config live: long streams without reconnects, replicated across documents
     "ref_live_bench": (dict(LIVE_BASE, seed=4545, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.0,
                             p_ack=0.6, n_keys=8, n_values=16), 8),
+    # deep segment-group queues: short text, mostly local annotates, few acks -- segments sit in
+    # up to 8 pending groups at once (the device FIFO's depth)
+    "ref_live_deep": (dict(LIVE_BASE, seed=4646, steps=500, seed_len=8, text_max=3, p_local=0.55, p_reconnect=0.005,
+                           p_ack=0.2, p_insert=0.25, p_remove=0.05, track_depth=1), 6),
     # markers (local and remote) among the text: regenerated marker inserts
     "ref_live_markers": (dict(LIVE_BASE, seed=4444, steps=800, p_local=0.4, p_reconnect=0.015, p_ack=0.4,
                               p_marker=0.15), 4),

@@ -13,7 +13,7 @@ import pytest
 import golden_util as gu
 from fluidframework_amd.wire import F_ACK, F_LOCAL, Batch, Interner
 
-LIVE_FIXTURES = ["ref_live", "ref_live_long", "ref_live_markers"]
+LIVE_FIXTURES = ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep"]
 
 
 def _msg(ev):
@@ -59,12 +59,17 @@ def test_live_encoding_flags():
 
 
 def test_live_fixtures_are_reference_made():
+    # ref_live_deep: segments sit in up to 13 pending groups, documents hold up to 478 of them
+    deep = gu.load("ref_live_deep")
+    assert max(d["out"]["maxGroupDepth"] for d in deep["docs"]) > 8
+    assert max(d["out"]["pending"] for d in deep["docs"]) > 255
     for name in LIVE_FIXTURES:
         fx = gu.load(name)
         assert fx["config"]["steps"] > 0 and len(fx["docs"]) >= 3
+        kinds = set()
         for d in fx["docs"]:
-            kinds = {e[0] for e in d["events"]}
-            assert kinds == {"L", "M", "R"}, kinds
+            kinds |= {e[0] for e in d["events"]}
+        assert kinds == {"L", "M", "R"}, (name, kinds)
 
 
 # ---------------------------------------------------------------- GPU
