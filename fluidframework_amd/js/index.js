@@ -283,6 +283,15 @@ class GpuClient {
         return this._local(op);
     }
 
+    /** Client.localTransaction (client.ts:961-981): every member applied as its own local op. */
+    localTransaction(groupOp) {
+        for (const op of groupOp.ops) {
+            if (op.type === 0) { this.insertSegmentLocal(op.pos1, op.seg); }
+            else if (op.type === 1) { this.removeRangeLocal(op.pos1, op.pos2); }
+            else if (op.type === 2) { this.annotateRangeLocal(op.pos1, op.pos2, op.props, op.combiningOp); }
+        }
+    }
+
     /**
      * Client.regeneratePendingOp (client.ts:855-893) for the oldest pending op(s): resetOp is
      * the op as it was submitted (a GROUP is rebuilt member by member); segmentGroup is not

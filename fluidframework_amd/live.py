@@ -88,6 +88,17 @@ class LiveClient:
         self.queue.append(("local", op))
         return op
 
+    def localTransaction(self, group_op):
+        """MT/client.ts:961-981: every member of a local GROUP op applied as its own local op
+        (each with its own segment group; the GROUP's echo acks them member by member)."""
+        for op in group_op["ops"]:
+            if op["type"] == OP_INSERT:
+                self.insertSegmentLocal(op["pos1"], op["seg"])
+            elif op["type"] == OP_REMOVE:
+                self.removeRangeLocal(op["pos1"], op["pos2"])
+            elif op["type"] == OP_ANNOTATE:
+                self.annotateRangeLocal(op["pos1"], op["pos2"], op["props"], op.get("combiningOp"))
+
     # -------------------------------------------------------------- sequenced messages
     def applyMsg(self, msg):
         self.queue.append(("ack" if msg["clientId"] == self.long_client_id else "msg", msg))

@@ -194,4 +194,13 @@ def test_live_local_ops_and_invalid_ranges():
     lc.applyMsg(dict(clientId="me", sequenceNumber=1, referenceSequenceNumber=0, minimumSequenceNumber=0,
                      type="op", contents={"pos1": 5, "seg": " world", "type": 0}))
     assert lc.pendingCounts() == (2, 1)
+    # a local transaction (GROUP) is acked member by member by its echo
+    grp = {"ops": [{"pos1": 0, "seg": "ab", "type": 0}, {"pos1": 2, "pos2": 4, "type": 1}], "type": 3}
+    lc.localTransaction(grp)
+    assert lc.getText() == "ablo world" and lc.pendingCounts() == (4, 3)
+    lc.applyMsg(dict(clientId="me", sequenceNumber=2, referenceSequenceNumber=1, minimumSequenceNumber=0,
+                     type="op", contents={"pos1": 0, "pos2": 1, "type": 1}))
+    lc.applyMsg(dict(clientId="me", sequenceNumber=3, referenceSequenceNumber=2, minimumSequenceNumber=1,
+                     type="op", contents=grp))
+    assert lc.pendingCounts() == (4, 0) and lc.getText() == "ablo world"
     lc.close()
