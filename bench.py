@@ -315,10 +315,9 @@ def run_live(args, rank, world, local_rank, dist):
     fx = json.load(gzip.open(os.path.join(REPO, "tests", "golden", "ref_live_bench.json.gz"), "rt"))
     streams = fx["docs"]
     docs = args.docs or 4096
+    # encode each stream once; the replicas share its records and arenas (offsets into them)
     b = Batch(Interner(synthetic=True))
-    n_events = 0
-    for d in range(docs):
-        st = streams[(rank * docs + d) % len(streams)]
+    for st in streams:
         ent = []
         for ev in st["events"]:
             if ev[0] == "L":
@@ -328,9 +327,17 @@ def run_live(args, rank, world, local_rank, dist):
                 m = dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
                          type="op", contents=op)
                 ent.append(("ack" if cid == "local-0" else "msg", m))
-        n_events += len(ent)
         b.add_live_doc(st["seed_text"], ent, {"local-0": 0})
-    a = b.arrays()
+    e = b.arrays()
+    sid = (rank * docs + np.arange(docs)) % len(streams)
+    lens = np.diff(e["doc_off"])[sid]
+    idx = np.concatenate([np.arange(e["doc_off"][k], e["doc_off"][k + 1]) for k in sid])
+    slen = np.diff(e["seed_off"])[sid]
+    sidx = np.concatenate([np.arange(e["seed_off"][k], e["seed_off"][k + 1]) for k in sid])
+    a = dict(ops=e["ops"][idx], doc_off=np.concatenate([[0], np.cumsum(lens)]).astype(np.int64),
+             text=e["text"], props=e["props"], seed=e["seed"][sidx] if len(sidx) else e["seed"][:1],
+             seed_off=np.concatenate([[0], np.cumsum(slen)]).astype(np.int64))
+    n_events = int(lens.sum())
     mt = MergeTreeBatch(docs, device=local_rank, seg_capacity=4096, text_capacity=1 << 15, props_capacity=4096,
                         heap_capacity=4096, lds_seg_capacity=-1, live_client=1)
     mt.load_initial_text(a["seed_off"], a["seed"])
