@@ -309,7 +309,7 @@ class MergeTreeBatch:
         return out
 
     # -------------------------------------------------------------- live-client handles
-    def regenerate_pending(self, doc, cap=4096, text_cap=1 << 16, props_cap=1 << 16):
+    def regenerate_pending(self, doc, cap=1 << 16, text_cap=1 << 20, props_cap=1 << 20):
         """mt_regenerate_pending: the ops rebuilt from the oldest pending segment group
         (records, text, props), or None when nothing is pending."""
         out = np.zeros(cap, dtype=_native.REGEN_DTYPE)

@@ -399,7 +399,7 @@ napi_value RegeneratePending(napi_env env, napi_callback_info info) {
     if (!hd) return nullptr;
     uint32_t doc = 0;
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
-    const uint32_t cap = 4096, tcap = 1u << 16, pcap = 1u << 16;
+    const uint32_t cap = 1u << 16, tcap = 1u << 20, pcap = 1u << 20;   // a group holds <= one record per segment
     std::vector<mt_regen_rec> recs(cap);
     std::vector<uint16_t> text(tcap);
     std::vector<uint32_t> props(pcap);

@@ -440,9 +440,15 @@ class GpuClient {
                         pd.push([this.batch.interner.keyName(log[i]), this.batch.interner.value(log[i + 1] >>> 0)]);
                         i += 2;
                     }
-                    delta = { propertyDeltas: {} };
-                    // (a rewrite-deleted key set to undefined reports undefined, as the reference)
-                    for (const [k, v] of pd) { delta.propertyDeltas[k] = v; }
+                    if (npd < 0) {
+                        // live client: an outstanding local rewrite blocked the remote annotate
+                        // (segmentPropertiesManager.ts:48-51): propertyDeltas undefined
+                        delta = {};
+                    } else {
+                        delta = { propertyDeltas: {} };
+                        // (a rewrite-deleted key set to undefined reports undefined, as the reference)
+                        for (const [k, v] of pd) { delta.propertyDeltas[k] = v; }
+                    }
                 } else {
                     delta = {};
                 }
@@ -460,9 +466,18 @@ class GpuClient {
                 if (mcb) { mcb({ operation: kind, deltaSegments }); }
                 continue;
             }
+            if (seq === -1) {
+                // live client: the local client's own op (no sequencedMessage), in queue order
+                while (mi < msgs.length && msgs[mi].__local === undefined) { mi++; }
+                const op = mi < msgs.length ? msgs[mi++].__local : undefined;
+                lastSeq = null;
+                if (cb) { cb({ op }, { operation: kind, deltaSegments }); }
+                continue;
+            }
             // opArgs: the message with this sequence number; a GROUP's members in order
             if (seq !== lastSeq) { member = 0; lastSeq = seq; } else { member++; }
-            while (mi < msgs.length && msgs[mi].sequenceNumber !== seq) { mi++; }
+            while (mi < msgs.length && (msgs[mi].__local !== undefined || msgs[mi].__ack !== undefined ||
+                msgs[mi].sequenceNumber !== seq)) { mi++; }
             const msg = mi < msgs.length ? msgs[mi] : { sequenceNumber: seq };
             const contents = msg.contents;
             const isGroup = contents && contents.type === 3;

@@ -70,10 +70,22 @@ if (mode === "encode") {
     // ops through insertSegmentLocal / removeRangeLocal / annotateRangeLocal, sequenced messages
     // (acks included) through applyMsg, reconnects through regeneratePendingOp
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js", "index.js"));
-    const b = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 16384, textCapacity: 1 << 17, liveClient: 1 });
+    const b = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 16384, textCapacity: 1 << 17, liveClient: 1,
+        deltaLogCapacity: 1 << 16 });
     b.loadInitialText(fx.docs.map((d) => d.seed_text));
     const docs = [];
-    const cs = fx.docs.map((d, i) => { const c = b.client(i); c.startOrUpdateCollaboration("local-0"); return c; });
+    const deltas = fx.docs.map(() => []);
+    const cs = fx.docs.map((d, i) => {
+        const c = b.client(i);
+        c.startOrUpdateCollaboration("local-0");
+        // the reference harness's record: [seq or -1, operation, n, [[position, length(, propertyDeltas)]...]]
+        c.mergeTreeDeltaCallback = (opArgs, dargs) => {
+            deltas[i].push([opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, dargs.operation,
+                dargs.deltaSegments.length, dargs.deltaSegments.map((x) => (x.propertyDeltas !== undefined
+                    ? [x.position, x.segment.cachedLength, x.propertyDeltas] : [x.position, x.segment.cachedLength]))]);
+        };
+        return c;
+    });
     fx.docs.forEach((d, i) => {
         const c = cs[i];
         let unseq = [];
@@ -101,6 +113,8 @@ if (mode === "encode") {
         }
         docs.push({ doc: d.doc, text: c.getText(), length: c.getLength(), errs });
     });
+    b.flush();
+    docs.forEach((x, i) => { x.deltas = deltas[i]; });
     process.stdout.write(JSON.stringify({ docs }));
 } else if (mode === "deltas") {
     // deltas <fixture> <deltaLogCapacity> <flushEvery>: every mergeTreeDeltaCallback the

@@ -250,3 +250,6 @@ def test_js_facade_live_client_matches_reference():
         assert g["errs"] == [], g["errs"][:3]
         assert g["text"] == d["out"]["text"]
         assert g["length"] == d["out"]["length"]
+        # mergeTreeDeltaCallback stream: local ops (seq -1, no sequencedMessage), remote ops,
+        # propertyDeltas undefined where an outstanding local rewrite blocked a remote annotate
+        assert g["deltas"] == d["out"]["deltas"]
