@@ -199,9 +199,24 @@ def c5_decode_rate(counts, recs, text, props, mn, cu, chunk, n_sample, threads):
         done = list(ex.map(_decode_slice, parts))
         t = time.perf_counter() - t
     n = sum(x[0] for x in done)
-    return dict(value=round(n / t, 1), unit="docs/s", cores=len(parts), kind="port",
-                sample=f"{n} summaries ({nbytes / 1e6:.1f} MB of chunk JSON, {sum(x[1] for x in done)} segment specs) "
-                       f"decoded by fluidframework_amd/snapshot.py on {len(parts)} host processes, {t:.2f} s")
+    py = dict(value=round(n / t, 1), unit="docs/s", cores=len(parts), kind="port",
+              sample=f"{n} summaries ({nbytes / 1e6:.1f} MB of chunk JSON, {sum(x[1] for x in done)} segment specs) "
+                     f"decoded by fluidframework_amd/snapshot.py on {len(parts)} host processes, {t:.2f} s")
+    # the native decoder (include/mt_snapshot.h) on the same blobs: bytes in, mt_seg_rec out
+    from fluidframework_amd.snapdec import SummaryDecoder
+    dec = SummaryDecoder(Interner(synthetic=True), threads=threads)
+    packed = dec.pack(docs)
+    dec.decode_packed(*packed)                          # warm (page in, allocator)
+    reps = 3
+    t = time.perf_counter()
+    for _ in range(reps):
+        out, _ = dec.decode_packed(*packed)
+    t = (time.perf_counter() - t) / reps
+    return dict(value=round(len(docs) / t, 1), unit="docs/s", cores=threads, kind="native",
+                mb_per_s=round(nbytes / t / 1e6, 1),
+                sample=f"{len(docs)} summaries ({nbytes / 1e6:.1f} MB of chunk JSON, {len(out['segs'])} segment specs) "
+                       f"decoded by libmtsnapdec.so on {threads} host threads, {t * 1e3:.1f} ms (mean of {reps})",
+                python_restatement=py)
 
 
 def run_c5(args, cfg, rank, world, local_rank, dist):

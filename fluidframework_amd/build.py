@@ -1,4 +1,5 @@
-"""Builds the HIP replay library in-tree (fluidframework_amd/libmtreplay.so) for gfx950.
+"""Builds the HIP replay library in-tree (fluidframework_amd/libmtreplay.so) for gfx950, and the
+host summary decoder (libmtsnapdec.so).
 hipcc cross-compiles here without a GPU; the .so travels to the GPU box with the repo."""
 import os
 import subprocess
@@ -34,6 +35,23 @@ def build(force=False, verbose=False):
     return OUT
 
 
+SNAP_SRC = os.path.join(HERE, "csrc", "mt_snapdec.cpp")
+SNAP_OUT = os.path.join(HERE, "libmtsnapdec.so")
+
+
+def build_snapdec(force=False, verbose=False):
+    """The host summary decoder (include/mt_snapshot.h), plain g++ (no device code)."""
+    deps = [SNAP_SRC] + [os.path.join(os.path.dirname(HERE), "include", f) for f in ("mt_snapshot.h", "mt_types.h")]
+    if not force and os.path.exists(SNAP_OUT) and all(os.path.getmtime(d) <= os.path.getmtime(SNAP_OUT) for d in deps):
+        return SNAP_OUT
+    cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-o", SNAP_OUT + ".tmp", SNAP_SRC, "-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(SNAP_OUT + ".tmp", SNAP_OUT)
+    return SNAP_OUT
+
+
 def build_node_addon(verbose=False):
     """The N-API addon for the Node facade (fluidframework_amd/js); skipped without Node headers."""
     js = os.path.join(HERE, "js")
@@ -53,4 +71,5 @@ if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
     if not os.environ.get("MT_OUT"):   # variant libraries (MT_OUT) leave the addon alone
         build_node_addon(verbose=True)
+        build_snapdec(verbose=True)
     print(OUT)

@@ -1,0 +1,834 @@
+// mt_snapdec.cpp -- native host decoder of SnapshotV1 summaries (include/mt_snapshot.h).
+//
+// The host half of a cold catch-up (config C5): summary blobs (JSON text) -> mt_seg_rec
+// records + text / props arenas for mt_load_snapshots.  Semantics follow the reference
+// loader and fluidframework_amd/snapshot.py, its Python restatement:
+//   SnapshotLoader.initialize :36-84, loadHeader :120-159, loadBody :161-228,
+//   specToSegment :86-118 (MT/snapshotLoader.ts); SnapshotV1.processChunk (MT/snapshotV1.ts:
+//   266-277); toLatestVersion / buildHeaderMetadataForLegecyChunk (MT/snapshotChunks.ts:
+//   136-188); hasMergeInfo (:72-74).
+// Phase 1: `threads` workers take documents dynamically; each parses the document's blobs
+// into a flat node array (24-byte nodes in pre-order, strings decoded to UTF-16 units as JS
+// holds them, numbers left as lexemes in the source; the buffers are reused, so a worker
+// allocates almost nothing) and builds its records with document-local property ids.
+// Phase 2 concatenates the documents in order and maps local ids to the batch's ids, which
+// numbers keys / values first-seen in document order, exactly as wire.Interner does.
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mt_snapshot.h"
+
+namespace {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// ---------------------------------------------------------------- JSON (RFC 8259)
+struct Node {
+    enum : uint8_t { NUL, BOOL, NUM, STR, ARR, OBJ };
+    uint8_t t = NUL, b = 0;
+    uint32_t off = 0, len = 0;   // STR: units in Blob::str; NUM: bytes of the source; ARR/OBJ: -, count
+    uint32_t next = 0;           // next sibling (0: none -- the root is never a sibling)
+    uint32_t koff = 0, klen = 0; // object member: its key (units in Blob::str)
+};
+static_assert(sizeof(Node) == 24, "node layout");
+
+struct Blob {
+    const char *src = nullptr;
+    size_t n = 0;
+    std::string path;
+    std::vector<Node> nodes;     // pre-order: a container's first child is the next node
+    std::vector<char16_t> str;
+
+    const char16_t *s(uint32_t off) const { return str.data() + off; }
+    uint32_t first(uint32_t i) const { return nodes[i].len ? i + 1 : NONE; }
+    static bool eq(const char16_t *u, uint32_t n, const char *k) {
+        uint32_t i = 0;
+        for (; i < n && k[i]; i++)
+            if (u[i] != (char16_t)(unsigned char)k[i]) return false;
+        return i == n && !k[i];
+    }
+    bool is_str(uint32_t i, const char *k) const {
+        return i != NONE && nodes[i].t == Node::STR && eq(s(nodes[i].off), nodes[i].len, k);
+    }
+    // member k of object i (a duplicated member: the last value, as JSON.parse)
+    uint32_t get(uint32_t i, const char *k) const {
+        if (i == NONE || nodes[i].t != Node::OBJ) return NONE;
+        uint32_t r = NONE;
+        uint32_t c = first(i);
+        for (uint32_t m = 0; m < nodes[i].len; m++, c = nodes[c].next)
+            if (eq(s(nodes[c].koff), nodes[c].klen, k)) r = c;
+        return r;
+    }
+    bool present(uint32_t i) const { return i != NONE && nodes[i].t != Node::NUL; }
+    std::u16string ustr(uint32_t i) const { return std::u16string(s(nodes[i].off), nodes[i].len); }
+    std::u16string ukey(uint32_t i) const { return std::u16string(s(nodes[i].koff), nodes[i].klen); }
+    bool is_int(uint32_t i) const {
+        const char *p = src + nodes[i].off;
+        for (uint32_t k = 0; k < nodes[i].len; k++)
+            if (p[k] == '.' || p[k] == 'e' || p[k] == 'E') return false;
+        return true;
+    }
+    double num(uint32_t i) const {   // JS Number of the lexeme
+        char b[64];
+        const uint32_t l = std::min<uint32_t>(nodes[i].len, 63);
+        memcpy(b, src + nodes[i].off, l);
+        b[l] = 0;
+        return strtod(b, nullptr);
+    }
+    int64_t as_int(uint32_t i) const {
+        if (i == NONE || nodes[i].t != Node::NUM) return 0;
+        if (!is_int(i) || nodes[i].len > 18) return (int64_t)num(i);
+        const char *p = src + nodes[i].off;
+        const bool neg = *p == '-';
+        int64_t v = 0;
+        for (uint32_t k = neg; k < nodes[i].len; k++) v = v * 10 + (p[k] - '0');
+        return neg ? -v : v;
+    }
+    // own members of object i in insertion order: a duplicated key keeps its first position
+    // and takes its last value (JSON.parse and json.loads agree)
+    void members(uint32_t i, std::vector<uint32_t> &out) const {
+        out.clear();
+        uint32_t c = first(i);
+        for (uint32_t m = 0; m < nodes[i].len; m++, c = nodes[c].next) {
+            bool dup = false;
+            for (auto &x : out)
+                if (nodes[x].klen == nodes[c].klen &&
+                    !memcmp(s(nodes[x].koff), s(nodes[c].koff), nodes[c].klen * sizeof(char16_t))) {
+                    x = c;
+                    dup = true;
+                    break;
+                }
+            if (!dup) out.push_back(c);
+        }
+    }
+};
+
+struct Reader {
+    const char *p, *e;
+    Blob &B;
+    std::string err;
+
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++;
+    }
+    bool fail(const char *m) {
+        if (err.empty()) err = m;
+        return false;
+    }
+    static int hex(char c) {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    }
+    // a string into B.str (UTF-8 -> UTF-16 units; \u escapes kept as units, lone surrogates too)
+    bool str(uint32_t &off, uint32_t &len) {
+        if (p >= e || *p != '"') return fail("expected a string");
+        p++;
+        auto &o = B.str;
+        off = (uint32_t)o.size();
+        for (;;) {
+            const char *q = p;   // ASCII run
+            while (q < e && (unsigned char)*q >= 0x20 && (unsigned char)*q < 0x80 && *q != '"' && *q != '\\') q++;
+            o.insert(o.end(), (const unsigned char *)p, (const unsigned char *)q);
+            p = q;
+            if (p >= e) return fail("unterminated string");
+            const unsigned char c = (unsigned char)*p;
+            if (c == '"') break;
+            if (c == '\\') {
+                if (++p >= e) return fail("bad escape");
+                const char x = *p++;
+                switch (x) {
+                    case '"': o.push_back(u'"'); break;
+                    case '\\': o.push_back(u'\\'); break;
+                    case '/': o.push_back(u'/'); break;
+                    case 'b': o.push_back(u'\b'); break;
+                    case 'f': o.push_back(u'\f'); break;
+                    case 'n': o.push_back(u'\n'); break;
+                    case 'r': o.push_back(u'\r'); break;
+                    case 't': o.push_back(u'\t'); break;
+                    case 'u': {
+                        if (e - p < 4) return fail("bad \\u escape");
+                        int v = 0;
+                        for (int i = 0; i < 4; i++) {
+                            const int h = hex(p[i]);
+                            if (h < 0) return fail("bad \\u escape");
+                            v = v * 16 + h;
+                        }
+                        p += 4;
+                        o.push_back((char16_t)v);
+                        break;
+                    }
+                    default: return fail("bad escape");
+                }
+                continue;
+            }
+            if (c < 0x20) return fail("control character in string");
+            uint32_t cp;
+            int n;
+            if ((c & 0xE0) == 0xC0) { cp = c & 0x1F; n = 1; }
+            else if ((c & 0xF0) == 0xE0) { cp = c & 0x0F; n = 2; }
+            else if ((c & 0xF8) == 0xF0) { cp = c & 0x07; n = 3; }
+            else return fail("bad UTF-8");
+            p++;
+            if (e - p < n) return fail("bad UTF-8");
+            for (int i = 0; i < n; i++) cp = (cp << 6) | ((unsigned char)*p++ & 0x3F);
+            if (cp >= 0x10000) {
+                cp -= 0x10000;
+                o.push_back((char16_t)(0xD800 + (cp >> 10)));
+                o.push_back((char16_t)(0xDC00 + (cp & 0x3FF)));
+            } else {
+                o.push_back((char16_t)cp);
+            }
+        }
+        p++;
+        len = (uint32_t)o.size() - off;
+        return true;
+    }
+    uint32_t node(uint8_t t) {
+        B.nodes.emplace_back();
+        B.nodes.back().t = t;
+        return (uint32_t)B.nodes.size() - 1;
+    }
+    bool val(uint32_t &out, int depth = 0) {
+        if (depth > 512) return fail("nesting too deep");
+        ws();
+        if (p >= e) return fail("unexpected end");
+        const char c = *p;
+        if (c == '{' || c == '[') {
+            const bool obj = c == '{';
+            const uint32_t me = out = node(obj ? Node::OBJ : Node::ARR);
+            p++;
+            ws();
+            if (p < e && *p == (obj ? '}' : ']')) { p++; return true; }
+            uint32_t prev = NONE, count = 0;
+            for (;;) {
+                uint32_t ko = 0, kl = 0, ch;
+                if (obj) {
+                    ws();
+                    if (!str(ko, kl)) return false;
+                    ws();
+                    if (p >= e || *p != ':') return fail("expected ':'");
+                    p++;
+                }
+                if (!val(ch, depth + 1)) return false;
+                B.nodes[ch].koff = ko;
+                B.nodes[ch].klen = kl;
+                if (prev != NONE) B.nodes[prev].next = ch;
+                prev = ch;
+                count++;
+                ws();
+                if (p < e && *p == ',') { p++; continue; }
+                if (p < e && *p == (obj ? '}' : ']')) { p++; break; }
+                return fail(obj ? "expected ',' or '}'" : "expected ',' or ']'");
+            }
+            B.nodes[me].len = count;
+            return true;
+        }
+        if (c == '"') {
+            uint32_t o, l;
+            if (!str(o, l)) return false;
+            out = node(Node::STR);
+            B.nodes[out].off = o;
+            B.nodes[out].len = l;
+            return true;
+        }
+        if (e - p >= 4 && !memcmp(p, "true", 4)) { out = node(Node::BOOL); B.nodes[out].b = 1; p += 4; return true; }
+        if (e - p >= 5 && !memcmp(p, "false", 5)) { out = node(Node::BOOL); p += 5; return true; }
+        if (e - p >= 4 && !memcmp(p, "null", 4)) { out = node(Node::NUL); p += 4; return true; }
+        if (c == '-' || (c >= '0' && c <= '9')) {
+            const char *s = p;
+            if (*p == '-') p++;
+            while (p < e && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '+' || *p == '-')) p++;
+            out = node(Node::NUM);
+            B.nodes[out].off = (uint32_t)(s - B.src);
+            B.nodes[out].len = (uint32_t)(p - s);
+            return true;
+        }
+        return fail("unexpected character");
+    }
+};
+
+bool parse(Blob &b, std::string &err) {
+    b.nodes.clear();
+    b.str.clear();
+    b.nodes.reserve(b.n / 12 + 8);
+    b.str.reserve(b.n);
+    Reader r{b.src, b.src + b.n, b, {}};
+    uint32_t root;
+    if (!r.val(root)) {
+        err = r.err;
+        return false;
+    }
+    r.ws();
+    if (r.p != r.e) {
+        err = "trailing characters";
+        return false;
+    }
+    return true;
+}
+
+void utf8(std::string &o, const char16_t *s, size_t n) {
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c = s[i];
+        if (c >= 0xD800 && c < 0xDC00 && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] < 0xE000) {
+            c = 0x10000 + ((c - 0xD800) << 10) + (s[i + 1] - 0xDC00);
+            i++;
+        }
+        if (c < 0x80) o.push_back((char)c);
+        else if (c < 0x800) { o.push_back((char)(0xC0 | (c >> 6))); o.push_back((char)(0x80 | (c & 0x3F))); }
+        else if (c < 0x10000) {
+            o.push_back((char)(0xE0 | (c >> 12)));
+            o.push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+            o.push_back((char)(0x80 | (c & 0x3F)));
+        } else {
+            o.push_back((char)(0xF0 | (c >> 18)));
+            o.push_back((char)(0x80 | ((c >> 12) & 0x3F)));
+            o.push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+            o.push_back((char)(0x80 | (c & 0x3F)));
+        }
+    }
+}
+std::string utf8(const std::u16string &s) {
+    std::string o;
+    utf8(o, s.data(), s.size());
+    return o;
+}
+void json_str(std::string &o, const char16_t *s, size_t n) {   // JSON text (lone surrogates escaped)
+    o.push_back('"');
+    for (size_t i = 0; i < n; i++) {
+        const char16_t c = s[i];
+        const bool pair = c >= 0xD800 && c < 0xDC00 && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] < 0xE000;
+        if (c == u'"' || c == u'\\') {
+            o.push_back('\\');
+            o.push_back((char)c);
+        } else if (c < 0x20 || (c >= 0xD800 && c < 0xE000 && !pair)) {
+            char b[8];
+            snprintf(b, sizeof b, "\\u%04x", (unsigned)c);
+            o += b;
+        } else if (c < 0x80) {
+            o.push_back((char)c);
+        } else {
+            utf8(o, s + i, pair ? 2 : 1);
+            i += pair;
+        }
+    }
+    o.push_back('"');
+}
+
+// Canonical JSON of a property value: equal iff wire.canonical_json is equal (sorted object
+// keys; an integer lexeme is an int, any other number a float -- Python keeps 1 and 1.0
+// apart).  json.loads of it gives back the value wire.Interner.vals would hold.
+void canon(std::string &o, const Blob &B, uint32_t i) {
+    const Node &v = B.nodes[i];
+    switch (v.t) {
+        case Node::NUL: o += "null"; break;
+        case Node::BOOL: o += v.b ? "true" : "false"; break;
+        case Node::NUM:
+            if (B.is_int(i)) {
+                if (v.len == 2 && !memcmp(B.src + v.off, "-0", 2)) o += "0";
+                else o.append(B.src + v.off, v.len);
+            } else {
+                char b[40];   // a float stays a float ("1.0" != "1", as in Python)
+                snprintf(b, sizeof b, "%.17g", B.num(i));
+                o += b;
+                if (!strpbrk(b, ".en")) o += ".0";
+            }
+            break;
+        case Node::STR: json_str(o, B.s(v.off), v.len); break;
+        case Node::ARR: {
+            o.push_back('[');
+            uint32_t c = B.first(i);
+            for (uint32_t m = 0; m < v.len; m++, c = B.nodes[c].next) {
+                if (m) o.push_back(',');
+                canon(o, B, c);
+            }
+            o.push_back(']');
+            break;
+        }
+        case Node::OBJ: {
+            std::vector<uint32_t> m;
+            B.members(i, m);
+            std::sort(m.begin(), m.end(), [&](uint32_t a, uint32_t b) {
+                return std::u16string_view(B.s(B.nodes[a].koff), B.nodes[a].klen) <
+                       std::u16string_view(B.s(B.nodes[b].koff), B.nodes[b].klen);
+            });
+            o.push_back('{');
+            for (size_t k = 0; k < m.size(); k++) {
+                if (k) o.push_back(',');
+                json_str(o, B.s(B.nodes[m[k]].koff), B.nodes[m[k]].klen);
+                o.push_back(':');
+                canon(o, B, m[k]);
+            }
+            o.push_back('}');
+            break;
+        }
+    }
+}
+// JS truthiness of a JSON value (wire.js_falsy)
+bool falsy(const Blob &B, uint32_t i) {
+    const Node &v = B.nodes[i];
+    if (v.t == Node::NUL) return true;
+    if (v.t == Node::BOOL) return !v.b;
+    if (v.t == Node::STR) return v.len == 0;
+    if (v.t == Node::NUM) return B.num(i) == 0.0;
+    return false;
+}
+
+// toLatestVersion (MT/snapshotChunks.ts:136-167): {segments, segmentCount, headerMetadata}
+// with the legacy header's metadata built as buildHeaderMetadataForLegecyChunk (:169-188)
+struct Chunk {
+    uint32_t segments = NONE;
+    int64_t segment_count = 0;
+    bool has_meta = false;
+    std::vector<std::u16string> ordered;
+    uint32_t min_seq = NONE, seq = NONE;
+    int64_t total_segments = 0;
+};
+void meta_of(const Blob &B, uint32_t m, Chunk &out) {
+    out.has_meta = true;
+    const uint32_t oc = B.get(m, "orderedChunkMetadata");
+    if (oc != NONE && B.nodes[oc].t == Node::ARR) {
+        uint32_t c = B.first(oc);
+        for (uint32_t k = 0; k < B.nodes[oc].len; k++, c = B.nodes[c].next) {
+            const uint32_t id = B.get(c, "id");
+            if (id != NONE && B.nodes[id].t == Node::STR) out.ordered.push_back(B.ustr(id));
+        }
+    }
+    out.min_seq = B.get(m, "minSequenceNumber");
+    out.seq = B.get(m, "sequenceNumber");
+    out.total_segments = B.as_int(B.get(m, "totalSegmentCount"));
+}
+bool latest(const Blob &B, Chunk &out, std::string &err) {
+    const uint32_t root = 0, ver = B.get(root, "version");
+    if (B.is_str(ver, "1")) {
+        out.segments = B.get(root, "segments");
+        out.segment_count = B.as_int(B.get(root, "segmentCount"));
+        const uint32_t m = B.get(root, "headerMetadata");
+        if (B.present(m)) meta_of(B, m, out);
+        return true;
+    }
+    if (B.present(ver)) {
+        std::string v;
+        if (B.nodes[ver].t == Node::STR) utf8(v, B.s(B.nodes[ver].off), B.nodes[ver].len);
+        else if (B.nodes[ver].t == Node::NUM) v.assign(B.src + B.nodes[ver].off, B.nodes[ver].len);
+        err = "Unsupported chunk path: " + B.path + " version: " + v;
+        return false;
+    }
+    out.segments = B.get(root, "segmentTexts");
+    out.segment_count = B.as_int(B.get(root, "chunkSegmentCount"));
+    if (B.path == "header") {
+        const uint32_t m = B.get(root, "headerMetadata");
+        if (B.present(m)) {
+            meta_of(B, m, out);
+        } else {
+            out.has_meta = true;
+            out.ordered.push_back(u"header");
+            if (B.as_int(B.get(root, "chunkLengthChars")) < B.as_int(B.get(root, "totalLengthChars")))
+                out.ordered.push_back(u"body");
+            out.min_seq = B.get(root, "chunkMinSequenceNumber");
+            out.seq = B.get(root, "chunkSequenceNumber");
+            out.total_segments = B.as_int(B.get(root, "totalSegmentCount"));
+        }
+    }
+    return true;
+}
+
+// One document's records, property ids local to the document (first-seen order); the merge
+// maps them to the batch's ids in document order, which keeps wire.Interner's numbering.
+struct DocOut {
+    std::vector<mt_seg_rec> segs;     // payload (text) / props: offsets into this document's arenas
+    std::vector<uint16_t> text;
+    std::vector<uint32_t> props;      // [count, (key, value) x count]: local ids (synthetic: final)
+    std::vector<std::u16string> keys; // local key id -> key
+    std::vector<std::string> vals;    // local value id -> canonical JSON
+    int32_t nh = 0, msn = 0, seq = 0;
+    int64_t cu = -1;
+    std::string clients, err;
+};
+
+struct Blobs {
+    const int64_t *off;
+    const char *const *paths;
+    const uint32_t *path_len;
+    const char *const *json;
+    const uint64_t *json_len;
+};
+
+// Per-thread scratch: SnapshotLoader.initialize for one document at a time.
+struct Worker {
+    bool synthetic = false;
+    std::vector<Blob> blobs;
+    std::unordered_map<std::u16string, uint32_t> key_ids;
+    std::unordered_map<std::string, uint32_t> val_ids;
+    std::unordered_map<std::u16string, int> shortid;
+    std::u16string kbuf;
+    std::string cbuf;
+    std::vector<uint32_t> mbuf;
+    std::vector<std::pair<const Blob *, uint32_t>> specs;
+    std::vector<std::string> ordered8;
+    std::vector<const std::u16string *> names;
+
+    uint32_t key(DocOut &o, const Blob &B, uint32_t m) {
+        const char16_t *k = B.s(B.nodes[m].koff);
+        const uint32_t n = B.nodes[m].klen;
+        if (synthetic) {   // "k<n>" -> n (wire.Interner(synthetic=True))
+            uint32_t v = 0;
+            for (uint32_t i = 1; i < n; i++) v = v * 10 + (uint32_t)(k[i] - u'0');
+            return v;
+        }
+        kbuf.assign(k, n);
+        auto it = key_ids.find(kbuf);
+        if (it != key_ids.end()) return it->second;
+        const uint32_t id = (uint32_t)o.keys.size();
+        key_ids.emplace(kbuf, id);
+        o.keys.push_back(kbuf);
+        return id;
+    }
+    uint32_t val(DocOut &o, const Blob &B, uint32_t i) {
+        if (B.nodes[i].t == Node::NUL) return MT_VAL_NULL;
+        if (synthetic) {
+            const uint32_t x = (uint32_t)B.as_int(i);
+            return x | (x == 0 ? MT_VAL_FALSY_BIT : 0u);
+        }
+        cbuf.clear();
+        canon(cbuf, B, i);
+        uint32_t id;
+        auto it = val_ids.find(cbuf);
+        if (it != val_ids.end()) {
+            id = it->second;
+        } else {
+            id = (uint32_t)o.vals.size();
+            val_ids.emplace(cbuf, id);
+            o.vals.push_back(cbuf);
+        }
+        return id | (falsy(B, i) ? MT_VAL_FALSY_BIT : 0u);
+    }
+    bool bad(DocOut &o, const std::string &m) {
+        o.err = m;
+        return false;
+    }
+
+    bool build(DocOut &o, uint32_t d, const Blobs &in) {
+        o.segs.clear();
+        o.text.clear();
+        o.props.clear();
+        o.keys.clear();
+        o.vals.clear();
+        o.err.clear();
+        o.cu = -1;
+        key_ids.clear();
+        val_ids.clear();
+        const int64_t b0 = in.off[d], b1 = in.off[d + 1];
+        if (blobs.size() < (size_t)(b1 - b0)) blobs.resize((size_t)(b1 - b0));
+        for (int64_t b = b0; b < b1; b++) {   // JSON.parse of every blob (MT/snapshotV1.ts:274)
+            Blob &B = blobs[(size_t)(b - b0)];
+            B.src = in.json[b];
+            B.n = in.json_len[b];
+            B.path.assign(in.paths[b], in.path_len[b]);
+            std::string e;
+            if (!parse(B, e)) return bad(o, "blob " + B.path + ": " + e);
+        }
+        auto find = [&](const std::string &p) -> const Blob * {
+            for (int64_t b = 0; b < b1 - b0; b++)
+                if (blobs[(size_t)b].path == p) return &blobs[(size_t)b];
+            return nullptr;
+        };
+        const Blob *H = find("header");
+        if (!H) return bad(o, "header blob missing");
+        Chunk head;
+        std::string e;
+        if (!latest(*H, head, e)) return bad(o, e);
+        if (!head.has_meta) return bad(o, "header metadata not available");
+        ordered8.clear();
+        for (const auto &x : head.ordered) ordered8.push_back(utf8(x));
+        const int64_t seq = H->as_int(head.seq);
+        const int64_t msn = H->present(head.min_seq) ? H->as_int(head.min_seq) : seq;
+        specs.clear();
+        auto take = [&](const Blob &B, uint32_t arr) {
+            if (arr == NONE || B.nodes[arr].t != Node::ARR) return;
+            uint32_t c = B.first(arr);
+            for (uint32_t k = 0; k < B.nodes[arr].len; k++, c = B.nodes[c].next) specs.emplace_back(&B, c);
+        };
+        take(*H, head.segments);
+        const size_t nh = specs.size();
+        if (head.segment_count != head.total_segments) {   // loadBody :170-172
+            for (size_t k = 1; k < ordered8.size(); k++) {
+                const Blob *C = find(ordered8[k]);
+                if (!C) return bad(o, "body blob missing: " + ordered8[k]);
+                Chunk ch;
+                if (!latest(*C, ch, e)) return bad(o, e);
+                take(*C, ch.segments);
+            }
+        }
+        const int64_t nblobs = b1 - b0;   // the legacy catch-up blob (:72-79)
+        if (nblobs == (int64_t)ordered8.size() + 1) {
+            int n_rest = 0;
+            for (int64_t b = b0; b < b1; b++)
+                if (std::find(ordered8.begin(), ordered8.end(), blobs[(size_t)(b - b0)].path) == ordered8.end()) {
+                    n_rest++;
+                    o.cu = b;
+                }
+            if (n_rest != 1) return bad(o, "There should be only one blob with catch up ops: " + std::to_string(n_rest));
+        } else if (nblobs != (int64_t)ordered8.size()) {
+            return bad(o, "Unexpected blobs in snapshot");
+        }
+        // specToSegment :86-118 (+ segmentFromSpec, SEQ/sequenceFactory.ts:31-37)
+        shortid.clear();
+        auto short_of = [&](const Blob &B, uint32_t c) {
+            kbuf.assign(B.s(B.nodes[c].off), B.nodes[c].len);
+            auto it = shortid.find(kbuf);
+            if (it != shortid.end()) return it->second;
+            const int v = (int)shortid.size() + 1;
+            shortid.emplace(kbuf, v);
+            return v;
+        };
+        o.segs.reserve(specs.size());
+        for (const auto &sp : specs) {
+            const Blob &B = *sp.first;
+            const uint32_t spec = sp.second;
+            mt_seg_rec r;
+            memset(&r, 0, sizeof r);
+            r.removed_seq = INT32_MIN;
+            r.props = MT_NO_PROPS;
+            r.client = -2;
+            const uint32_t jv = B.get(spec, "json");   // hasMergeInfo: `"json" in spec`
+            const bool mi = jv != NONE;
+            const uint32_t js = mi ? jv : spec;
+            uint32_t pr = NONE, tx = NONE, mk = NONE;
+            if (B.nodes[js].t == Node::STR) {
+                tx = js;
+            } else if ((tx = B.get(js, "text")) != NONE) {
+                pr = B.get(js, "props");
+            } else if ((mk = B.get(js, "marker")) != NONE) {
+                r.flags = MT_F_MARKER;
+                r.payload = (uint32_t)B.as_int(B.get(mk, "refType"));
+                r.len = 1;
+                pr = B.get(js, "props");
+            } else {
+                return bad(o, "unsupported segment spec");
+            }
+            if (tx != NONE) {
+                if (B.nodes[tx].t != Node::STR) return bad(o, "segment text is not a string");
+                r.payload = (uint32_t)o.text.size();
+                o.text.insert(o.text.end(), B.s(B.nodes[tx].off), B.s(B.nodes[tx].off) + B.nodes[tx].len);
+                r.len = (int32_t)B.nodes[tx].len;
+            }
+            if (pr != NONE && B.nodes[pr].t == Node::OBJ) {   // `if (props)`: {} too (Q5)
+                r.props = (uint32_t)o.props.size();
+                B.members(pr, mbuf);
+                o.props.push_back((uint32_t)mbuf.size());
+                for (uint32_t kv : mbuf) {
+                    o.props.push_back(key(o, B, kv));
+                    o.props.push_back(val(o, B, kv));
+                }
+            }
+            if (mi) {
+                const uint32_t sq = B.get(spec, "seq"), cl = B.get(spec, "client"), rs = B.get(spec, "removedSeq"),
+                               rc = B.get(spec, "removedClient");
+                r.flags |= MT_SEG_MERGE_INFO | (B.present(sq) ? MT_SEG_HAS_SEQ : 0);
+                if (B.present(cl)) r.client = (int16_t)short_of(B, cl);
+                if (B.present(sq)) r.seq = (int32_t)B.as_int(sq);
+                if (B.present(rs)) r.removed_seq = (int32_t)B.as_int(rs);
+                if (B.present(rc)) r.removed_client = (int16_t)short_of(B, rc);
+            }
+            o.segs.push_back(r);
+        }
+        o.nh = (int32_t)nh;
+        o.msn = (int32_t)msn;
+        o.seq = (int32_t)seq;
+        names.assign(shortid.size(), nullptr);
+        for (const auto &kv : shortid) names[kv.second - 1] = &kv.first;
+        o.clients = "[";
+        for (size_t i = 0; i < names.size(); i++) {
+            if (i) o.clients.push_back(',');
+            json_str(o.clients, names[i]->data(), names[i]->size());
+        }
+        o.clients.push_back(']');
+        return true;
+    }
+};
+
+}  // namespace
+
+struct mt_snapdec {
+    bool synthetic = false;
+    std::string err;
+    std::vector<mt_seg_rec> segs;
+    std::vector<uint16_t> text;
+    std::vector<uint32_t> props;
+    std::vector<int64_t> doc_off;
+    std::vector<int32_t> n_header, min_seq, cur_seq;
+    std::vector<int64_t> catchup;
+    std::vector<std::string> clients;   // per document: JSON array of long ids, short id 1..n
+    std::unordered_map<std::u16string, uint32_t> key_ids;   // the batch's interning
+    std::vector<std::u16string> keys;
+    std::unordered_map<std::string, uint32_t> val_ids;
+    std::vector<std::string> vals;
+    std::vector<DocOut> docs;           // reused between calls
+    std::vector<Worker> workers;
+};
+
+extern "C" {
+
+mt_snapdec *mt_snapdec_create(int synthetic) {
+    auto *s = new mt_snapdec();
+    s->synthetic = synthetic != 0;
+    return s;
+}
+void mt_snapdec_destroy(mt_snapdec *s) { delete s; }
+const char *mt_snapdec_error(const mt_snapdec *s) { return s ? s->err.c_str() : "null decoder"; }
+
+int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, const char *const *paths,
+                      const uint32_t *path_len, const char *const *json, const uint64_t *json_len, int threads) {
+    if (!s || !blob_off || (blob_off[n_docs] > 0 && (!paths || !path_len || !json || !json_len))) return -1;
+    s->err.clear();
+    if (s->docs.size() < n_docs) s->docs.resize(n_docs);
+    const int nt = std::max(1, std::min<int>(threads, (int)std::max<uint32_t>(n_docs, 1)));
+    if ((int)s->workers.size() < nt) s->workers.resize((size_t)nt);
+    const Blobs in{blob_off, paths, path_len, json, json_len};
+    // phase 1: documents parsed and specToSegment'ed on nt threads (dynamic, 8 at a time)
+    std::atomic<uint32_t> next{0};
+    auto work = [&](int t) {
+        Worker &w = s->workers[(size_t)t];
+        w.synthetic = s->synthetic;
+        for (;;) {
+            const uint32_t d0 = next.fetch_add(8);
+            if (d0 >= n_docs) break;
+            for (uint32_t d = d0; d < std::min(n_docs, d0 + 8); d++) w.build(s->docs[d], d, in);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
+    work(0);
+    for (auto &t : pool) t.join();
+    // phase 2: concatenation in document order; local property ids -> the batch's ids
+    size_t ns = 0, ntx = 0, npr = 0;
+    for (uint32_t d = 0; d < n_docs; d++) {
+        const DocOut &o = s->docs[d];
+        if (!o.err.empty()) {   // the first failing document, as a sequential load would report
+            s->err = "document " + std::to_string(d) + ": " + o.err;
+            return -1;
+        }
+        ns += o.segs.size();
+        ntx += o.text.size();
+        npr += o.props.size();
+    }
+    s->segs.resize(ns);
+    s->text.resize(ntx);
+    s->props.resize(npr);
+    s->doc_off.assign(1, 0);
+    s->n_header.resize(n_docs);
+    s->min_seq.resize(n_docs);
+    s->cur_seq.resize(n_docs);
+    s->catchup.resize(n_docs);
+    s->clients.resize(n_docs);
+    std::vector<uint32_t> kmap, vmap;
+    size_t si = 0, ti = 0, pi = 0;
+    for (uint32_t d = 0; d < n_docs; d++) {
+        DocOut &o = s->docs[d];
+        if (!s->synthetic) {
+            kmap.resize(o.keys.size());
+            for (size_t k = 0; k < o.keys.size(); k++) {
+                auto it = s->key_ids.find(o.keys[k]);
+                if (it == s->key_ids.end()) {
+                    it = s->key_ids.emplace(o.keys[k], (uint32_t)s->keys.size()).first;
+                    s->keys.push_back(o.keys[k]);
+                }
+                kmap[k] = it->second;
+            }
+            vmap.resize(o.vals.size());
+            for (size_t k = 0; k < o.vals.size(); k++) {
+                auto it = s->val_ids.find(o.vals[k]);
+                if (it == s->val_ids.end()) {
+                    it = s->val_ids.emplace(o.vals[k], (uint32_t)s->vals.size()).first;
+                    s->vals.push_back(o.vals[k]);
+                }
+                vmap[k] = it->second;
+            }
+        }
+        for (const mt_seg_rec &r0 : o.segs) {
+            mt_seg_rec r = r0;
+            if (!(r.flags & MT_F_MARKER)) r.payload += (uint32_t)ti;
+            if (r.props != MT_NO_PROPS) r.props += (uint32_t)pi;
+            s->segs[si++] = r;
+        }
+        if (!o.text.empty()) memcpy(&s->text[ti], o.text.data(), o.text.size() * sizeof(uint16_t));
+        ti += o.text.size();
+        if (s->synthetic) {
+            if (!o.props.empty()) memcpy(&s->props[pi], o.props.data(), o.props.size() * sizeof(uint32_t));
+            pi += o.props.size();
+        } else {
+            for (size_t i = 0; i < o.props.size();) {
+                const uint32_t n = o.props[i++];
+                s->props[pi++] = n;
+                for (uint32_t j = 0; j < n; j++, i += 2) {
+                    const uint32_t v = o.props[i + 1];
+                    s->props[pi++] = kmap[o.props[i]];
+                    s->props[pi++] = v == MT_VAL_NULL ? v : (vmap[v & ~MT_VAL_FALSY_BIT] | (v & MT_VAL_FALSY_BIT));
+                }
+            }
+        }
+        s->doc_off.push_back((int64_t)si);
+        s->n_header[d] = o.nh;
+        s->min_seq[d] = o.msn;
+        s->cur_seq[d] = o.seq;
+        s->catchup[d] = o.cu;
+        s->clients[d].swap(o.clients);
+    }
+    return 0;
+}
+
+int mt_snapdec_sizes(const mt_snapdec *s, uint64_t *n_segs, uint64_t *text_len, uint64_t *props_len) {
+    if (!s) return -1;
+    if (n_segs) *n_segs = s->segs.size();
+    if (text_len) *text_len = s->text.size();
+    if (props_len) *props_len = s->props.size();
+    return 0;
+}
+
+int mt_snapdec_fetch(const mt_snapdec *s, int64_t *doc_seg_off, int32_t *n_header, mt_seg_rec *segs, uint16_t *text,
+                     uint32_t *props, int32_t *min_seq, int32_t *cur_seq, int64_t *catchup_blob) {
+    if (!s) return -1;
+    auto cp = [](auto *dst, const auto &v) {
+        if (dst && !v.empty()) memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+    };
+    cp(doc_seg_off, s->doc_off);
+    cp(n_header, s->n_header);
+    cp(segs, s->segs);
+    cp(text, s->text);
+    cp(props, s->props);
+    cp(min_seq, s->min_seq);
+    cp(cur_seq, s->cur_seq);
+    cp(catchup_blob, s->catchup);
+    return 0;
+}
+
+static int64_t copy_out(const std::string &v, char *out, uint64_t cap) {
+    if (out) memcpy(out, v.data(), std::min<uint64_t>(cap, v.size()));
+    return (int64_t)v.size();
+}
+int64_t mt_snapdec_key(const mt_snapdec *s, uint32_t i, char *out, uint64_t cap) {
+    if (!s || i >= s->keys.size()) return -1;
+    return copy_out(utf8(s->keys[i]), out, cap);
+}
+int64_t mt_snapdec_value(const mt_snapdec *s, uint32_t i, char *out, uint64_t cap) {
+    if (!s || i >= s->vals.size()) return -1;
+    return copy_out(s->vals[i], out, cap);
+}
+int64_t mt_snapdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint64_t cap) {
+    if (!s || d >= s->clients.size()) return -1;
+    return copy_out(s->clients[d], out, cap);
+}
+uint32_t mt_snapdec_num_keys(const mt_snapdec *s) { return s ? (uint32_t)s->keys.size() : 0; }
+uint32_t mt_snapdec_num_values(const mt_snapdec *s) { return s ? (uint32_t)s->vals.size() : 0; }
+
+}  // extern "C"

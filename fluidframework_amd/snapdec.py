@@ -1,0 +1,137 @@
+"""ctypes binding of the native summary decoder (include/mt_snapshot.h, libmtsnapdec.so).
+
+Same output as ``snapshot.decode_chunks`` + ``SnapshotBatch`` (the Python restatement of
+SnapshotLoader.initialize / loadHeader / loadBody / specToSegment, MT/snapshotLoader.ts:
+36-228): mt_seg_rec records and arenas for ``mt_load_snapshots``, the key / value interning
+of ``wire.Interner`` (first-seen, document order) and the short client maps.  Blob JSON is
+parsed on ``threads`` host threads in C++ (the reference's JSON.parse step).
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+from .snapshot import SEG_DTYPE, SnapshotError
+from .wire import Interner, canonical_json
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmtsnapdec.so")
+
+_P, _I, _U32, _I64, _U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int64, ctypes.c_uint64
+SIGNATURES = [
+    ("mt_snapdec_create", _P, [_I]),
+    ("mt_snapdec_destroy", None, [_P]),
+    ("mt_snapdec_error", ctypes.c_char_p, [_P]),
+    ("mt_snapdec_decode", _I, [_P, _U32, _P, _P, _P, _P, _P, _I]),
+    ("mt_snapdec_sizes", _I, [_P, _P, _P, _P]),
+    ("mt_snapdec_fetch", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("mt_snapdec_key", _I64, [_P, _U32, _P, _U64]),
+    ("mt_snapdec_value", _I64, [_P, _U32, _P, _U64]),
+    ("mt_snapdec_num_keys", _U32, [_P]),
+    ("mt_snapdec_num_values", _U32, [_P]),
+    ("mt_snapdec_doc_clients", _I64, [_P, _U32, _P, _U64]),
+]
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"summary decoder library missing: {LIB_PATH} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _text(fn, h, i):
+    n = fn(h, i, None, 0)
+    buf = ctypes.create_string_buffer(max(n, 1))
+    fn(h, i, buf, n)
+    return buf.raw[:n].decode("utf-8", errors="surrogatepass")
+
+
+class SummaryDecoder:
+    """decode(summaries) -> (arrays, catchup, clients): ``arrays`` as SnapshotBatch.arrays(),
+    ``catchup[d]`` the legacy catch-up blob's text (None: none), ``clients[d]`` the short id
+    map to continue with (wire.Batch.add_doc(..., clients=...)).  ``interner`` is filled in
+    place (first-seen order); a synthetic interner maps k<n> / integers directly."""
+
+    def __init__(self, interner=None, threads=8):
+        self.interner = interner or Interner()
+        self.threads = threads
+        self.lib = load()
+        self.h = self.lib.mt_snapdec_create(1 if self.interner.synthetic else 0)
+        if self.interner.keys or self.interner.vals:
+            raise ValueError("SummaryDecoder numbers keys / values itself: pass an empty interner")
+        self._seen = (0, 0)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.mt_snapdec_destroy(self.h)
+            self.h = None
+
+    @staticmethod
+    def pack(summaries):
+        """Blob tables for mt_snapdec_decode: per document the blobs in insertion order."""
+        paths, blobs, off = [], [], [0]
+        for chunks in summaries:
+            for k, v in chunks.items():
+                paths.append(k.encode("utf-8"))
+                blobs.append(v.encode("utf-8", errors="surrogatepass") if isinstance(v, str) else bytes(v))
+            off.append(len(paths))
+        return paths, blobs, off
+
+    def decode_packed(self, paths, blobs, off):
+        n = len(off) - 1
+        nb = len(paths)
+        offa = np.asarray(off, dtype=np.int64)
+        pp = (ctypes.c_char_p * max(nb, 1))(*paths)
+        pl = np.asarray([len(x) for x in paths] or [0], dtype=np.uint32)
+        jp = (ctypes.c_char_p * max(nb, 1))(*blobs)
+        jl = np.asarray([len(x) for x in blobs] or [0], dtype=np.uint64)
+        rc = self.lib.mt_snapdec_decode(self.h, n, _p(offa), pp, _p(pl), jp, _p(jl), self.threads)
+        if rc != 0:
+            raise SnapshotError(self.lib.mt_snapdec_error(self.h).decode())
+        ns, nt, npr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.mt_snapdec_sizes(self.h, ctypes.byref(ns), ctypes.byref(nt), ctypes.byref(npr))
+        out = dict(segs=np.zeros(ns.value, dtype=SEG_DTYPE), doc_off=np.zeros(n + 1, dtype=np.int64),
+                   n_header=np.zeros(n, dtype=np.int32), text=np.zeros(max(nt.value, 1), dtype=np.uint16),
+                   props=np.zeros(max(npr.value, 1), dtype=np.uint32), min_seq=np.zeros(n, dtype=np.int32),
+                   cur_seq=np.zeros(n, dtype=np.int32))
+        cu = np.zeros(n, dtype=np.int64)
+        self.lib.mt_snapdec_fetch(self.h, _p(out["doc_off"]), _p(out["n_header"]), _p(out["segs"]), _p(out["text"]),
+                                  _p(out["props"]), _p(out["min_seq"]), _p(out["cur_seq"]), _p(cu))
+        return out, cu
+
+    def decode(self, summaries):
+        paths, blobs, off = self.pack(summaries)
+        out, cu = self.decode_packed(paths, blobs, off)
+        it = self.interner
+        if not it.synthetic:   # the names behind the ids, in id order
+            if (len(it.keys), len(it.vals)) != self._seen:
+                raise ValueError("the interner gained ids outside this decoder since its last decode")
+            for i in range(len(it.keys), self.lib.mt_snapdec_num_keys(self.h)):
+                k = _text(self.lib.mt_snapdec_key, self.h, i)
+                it.key_ids[k] = i
+                it.keys.append(k)
+            for i in range(len(it.vals), self.lib.mt_snapdec_num_values(self.h)):
+                v = json.loads(_text(self.lib.mt_snapdec_value, self.h, i))
+                it.val_ids[canonical_json(v)] = i
+                it.vals.append(v)
+            self._seen = (len(it.keys), len(it.vals))
+        catchup = [None if c < 0 else blobs[c].decode("utf-8", errors="surrogatepass") for c in cu]
+        clients = []
+        for d in range(len(off) - 1):
+            names = json.loads(_text(self.lib.mt_snapdec_doc_clients, self.h, d))
+            clients.append({c: i + 1 for i, c in enumerate(names)})
+        return out, catchup, clients

@@ -1,0 +1,60 @@
+/*
+ * mt_snapshot.h -- native host decoder of SnapshotV1 summaries (config C5's host half).
+ *
+ * SnapshotLoader.initialize / loadHeader / loadBody / specToSegment (MT/snapshotLoader.ts:
+ * 36-228), SnapshotV1.processChunk (MT/snapshotV1.ts:266-277) and toLatestVersion /
+ * buildHeaderMetadataForLegecyChunk (MT/snapshotChunks.ts:136-188) over the summaries' blob
+ * texts (JSON), straight into the mt_seg_rec records + text / props arenas that
+ * mt_load_snapshots / mt_snapshots_upload (include/mt_replay.h) take.  Blobs are parsed on
+ * `threads` host threads; records are built in document order so that property keys and
+ * values are interned in the same first-seen order as fluidframework_amd.wire.Interner.
+ * Host-only (libmtsnapdec.so, built with g++); the GPU path is unchanged.
+ */
+#ifndef MT_SNAPSHOT_H
+#define MT_SNAPSHOT_H
+#include <stdint.h>
+
+#include "mt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mt_snapdec mt_snapdec;
+
+/* synthetic: keys "k<n>" -> n and integer values -> themselves (wire.Interner(synthetic=True));
+   otherwise keys and values are interned (values by canonical JSON, sorted object keys). */
+mt_snapdec *mt_snapdec_create(int synthetic);
+void mt_snapdec_destroy(mt_snapdec *s);
+const char *mt_snapdec_error(const mt_snapdec *s);
+
+/* Decodes n_docs summaries.  Document d owns blobs [blob_off[d], blob_off[d + 1]); blob b is
+   its path (paths[b], path_len[b] bytes) and its contents (json[b], json_len[b] bytes of
+   UTF-8 JSON text).  Returns 0, or -1 with the first failing document's message in
+   mt_snapdec_error (the reference throws there).  The result replaces the previous one. */
+int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, const char *const *paths,
+                      const uint32_t *path_len, const char *const *json, const uint64_t *json_len, int threads);
+
+/* sizes of the last result: segment records, text units, props words */
+int mt_snapdec_sizes(const mt_snapdec *s, uint64_t *n_segs, uint64_t *text_len, uint64_t *props_len);
+
+/* the last result: doc_seg_off[n_docs + 1], n_header[n_docs], segs[n_segs], text, props,
+   min_seq[n_docs], cur_seq[n_docs] (the mt_load_snapshots arguments), and per document the
+   index of its legacy catch-up blob (-1: none; the caller parses those messages) */
+int mt_snapdec_fetch(const mt_snapdec *s, int64_t *doc_seg_off, int32_t *n_header, mt_seg_rec *segs, uint16_t *text,
+                     uint32_t *props, int32_t *min_seq, int32_t *cur_seq, int64_t *catchup_blob);
+
+/* interned names (non-synthetic): key / value id i as UTF-8 (values: canonical JSON); the
+   length is returned, the text copied when out is non-null (cap bytes) */
+int64_t mt_snapdec_key(const mt_snapdec *s, uint32_t i, char *out, uint64_t cap);
+int64_t mt_snapdec_value(const mt_snapdec *s, uint32_t i, char *out, uint64_t cap);
+uint32_t mt_snapdec_num_keys(const mt_snapdec *s);
+/* document d's writers as a JSON array of long client ids, short id 1..n in order
+   (specToSegment's getOrAddShortClientId first-seen order; the catch-up ops continue it) */
+int64_t mt_snapdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint64_t cap);
+uint32_t mt_snapdec_num_values(const mt_snapdec *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,106 @@
+"""Native summary decoder (include/mt_snapshot.h, libmtsnapdec.so) against the Python
+restatement of SnapshotLoader (fluidframework_amd/snapshot.py: decode_chunks + SnapshotBatch,
+MT/snapshotLoader.ts:36-228) on the reference-written summaries in tests/golden/ref_snap*.
+Host-only: no GPU.  Records, arenas, interning order, short client maps and catch-up blobs
+must be identical."""
+import json
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+from fluidframework_amd import snapdec
+from fluidframework_amd.snapshot import SnapshotBatch, SnapshotError, decode_chunks, encode_chunks
+from fluidframework_amd.wire import Interner
+
+
+def _python(summaries, interner):
+    sb = SnapshotBatch(interner)
+    catchup, clients = [], []
+    for ch in summaries:
+        snap = decode_chunks(ch)
+        clients.append(sb.add_doc(snap))
+        catchup.append(snap.catchup)
+    return sb.arrays(), catchup, clients
+
+
+def _check(summaries, synthetic=False, threads=4):
+    pi, ni = Interner(synthetic), Interner(synthetic)
+    pa, pc, pcl = _python(summaries, pi)
+    na, nc, ncl = snapdec.SummaryDecoder(ni, threads=threads).decode(summaries)
+    for k in ("doc_off", "n_header", "min_seq", "cur_seq"):
+        assert np.array_equal(pa[k], na[k]), k
+    assert pa["segs"].tobytes() == na["segs"].tobytes()
+    assert np.array_equal(pa["text"], na["text"])
+    assert np.array_equal(pa["props"], na["props"])
+    assert pi.keys == ni.keys and pi.vals == ni.vals and pi.key_ids == ni.key_ids and pi.val_ids == ni.val_ids
+    assert pcl == ncl
+    assert [list(c) for c in pc] == [json.loads(c) if c is not None else [] for c in nc]
+
+
+def test_library_exports_header():
+    """libmtsnapdec.so exports every entry point include/mt_snapshot.h declares."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "mt_snapshot.h")).read()
+    names = set(re.findall(r"\b(mt_snapdec_\w+)\s*\(", hdr))
+    lib = snapdec.load()
+    assert names and all(hasattr(lib, n) for n in names), names
+
+
+@pytest.mark.parametrize("name", ["ref_snap", "ref_snap_body", "ref_snap_files"])
+def test_native_decoder_matches_restatement(name):
+    docs = gu.load(name)["docs"]
+    summaries = [d["chunks"] for d in docs if "chunks" in d]
+    ok = []
+    for ch in summaries:
+        try:
+            decode_chunks(ch)
+            ok.append(ch)
+        except (SnapshotError, KeyError):
+            pass
+    assert ok
+    _check(ok)
+
+
+def test_native_decoder_synthetic_bench_chunks():
+    """The bench's own C5 summaries (snapshot.encode_chunks of generated documents, synthetic
+    interning: k<n> keys, integer values) decode identically."""
+    rng = np.random.default_rng(5)
+    summaries = []
+    for d in range(40):
+        specs, lengths = [], []
+        for i in range(int(rng.integers(1, 60))):
+            t = "".join(chr(int(c)) for c in rng.integers(0x41, 0x5B, int(rng.integers(1, 9))))
+            js = {"text": t, "props": {f"k{int(rng.integers(0, 5))}": int(rng.integers(0, 4))}} if i % 3 == 0 else t
+            spec = {"json": js, "seq": 10 + i, "client": f"c{i % 3}"} if i % 2 else js
+            specs.append(spec)
+            lengths.append(len(t))
+        summaries.append(encode_chunks(specs, lengths, 3, 200, 16))
+    _check(summaries, synthetic=True, threads=3)
+
+
+def test_native_decoder_json_details():
+    """JSON corner cases the reference's JSON.parse handles: escapes, surrogate pairs,
+    duplicate members (first position, last value), 1 vs 1.0, nested values."""
+    hdr = {"version": "1", "segmentCount": 4, "length": 9, "startIndex": 0,
+           "headerMetadata": {"orderedChunkMetadata": [{"id": "header"}], "minSequenceNumber": 0,
+                              "sequenceNumber": 7, "totalLength": 9, "totalSegmentCount": 4},
+           "segments": [{"text": "aé\U0001F600", "props": {"x": 1, "y": 1.0, "z": {"b": [1, None], "a": "s"}}},
+                        {"json": {"marker": {"refType": 1}, "props": {"x": 0}}, "seq": 5, "client": "q"},
+                        {"json": "t\\n\"", "seq": 6, "client": "r", "removedSeq": 7, "removedClient": "q"},
+                        {"text": "", "props": {}}]}
+    raw = json.dumps(hdr).replace('"x": 0}', '"x": 0, "x": 2.5}')
+    _check([{"header": raw}])
+    _check([{"header": raw}, {"header": json.dumps(hdr, ensure_ascii=False)}], threads=2)
+
+
+def test_native_decoder_errors():
+    dec = snapdec.SummaryDecoder(Interner())
+    with pytest.raises(SnapshotError, match="header blob missing"):
+        dec.decode([{"body": "{}"}])
+    with pytest.raises(SnapshotError, match="Unsupported chunk path"):
+        dec.decode([{"header": '{"version": "2"}'}])
+    with pytest.raises(SnapshotError):
+        dec.decode([{"header": '{"version": "1", '}])
