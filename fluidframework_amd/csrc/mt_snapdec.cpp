@@ -15,6 +15,7 @@
 // numbers keys / values first-seen in document order, exactly as wire.Interner does.
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -324,23 +325,26 @@ void json_str(std::string &o, const char16_t *s, size_t n) {   // JSON text (lon
     o.push_back('"');
 }
 
-// Canonical JSON of a property value: equal iff wire.canonical_json is equal (sorted object
-// keys; an integer lexeme is an int, any other number a float -- Python keeps 1 and 1.0
-// apart).  json.loads of it gives back the value wire.Interner.vals would hold.
+// Canonical JSON of a property value: equal iff wire.canonical_json is equal -- numbers as
+// JS Numbers (matchProperties compares with ===), object keys sorted.  json.loads of it
+// gives back an equal value.
 void canon(std::string &o, const Blob &B, uint32_t i) {
     const Node &v = B.nodes[i];
     switch (v.t) {
         case Node::NUL: o += "null"; break;
         case Node::BOOL: o += v.b ? "true" : "false"; break;
         case Node::NUM:
-            if (B.is_int(i)) {
+            if (B.is_int(i) && v.len <= 15) {   // exact in a double: the digits
                 if (v.len == 2 && !memcmp(B.src + v.off, "-0", 2)) o += "0";
                 else o.append(B.src + v.off, v.len);
-            } else {
-                char b[40];   // a float stays a float ("1.0" != "1", as in Python)
-                snprintf(b, sizeof b, "%.17g", B.num(i));
+            } else {   // JS Number: 1.0, 1e0 and 1 are one value
+                const double x = B.num(i);
+                char b[40];
+                if (std::isfinite(x) && x == std::floor(x) && std::fabs(x) < 1e21)
+                    snprintf(b, sizeof b, "%.0f", x == 0 ? 0.0 : x);
+                else
+                    snprintf(b, sizeof b, "%.17g", x);
                 o += b;
-                if (!strpbrk(b, ".en")) o += ".0";
             }
             break;
         case Node::STR: json_str(o, B.s(v.off), v.len); break;

@@ -2,9 +2,10 @@
 
 Same output as ``snapshot.decode_chunks`` + ``SnapshotBatch`` (the Python restatement of
 SnapshotLoader.initialize / loadHeader / loadBody / specToSegment, MT/snapshotLoader.ts:
-36-228): mt_seg_rec records and arenas for ``mt_load_snapshots``, the key / value interning
-of ``wire.Interner`` (first-seen, document order) and the short client maps.  Blob JSON is
-parsed on ``threads`` host threads in C++ (the reference's JSON.parse step).
+36-228): mt_seg_rec records and arenas for ``mt_load_snapshots``, property keys / values
+numbered in the caller's ``wire.Interner`` (first-seen, document order) and the short client
+maps.  Blob JSON is parsed on ``threads`` host threads in C++ (the reference's JSON.parse
+step).
 """
 import ctypes
 import json
@@ -12,8 +13,8 @@ import os
 
 import numpy as np
 
-from .snapshot import SEG_DTYPE, SnapshotError
-from .wire import Interner, canonical_json
+from .snapshot import NO_PROPS, SEG_DTYPE, SnapshotError
+from .wire import VAL_FALSY_BIT, VAL_NULL, Interner
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmtsnapdec.so")
@@ -63,17 +64,16 @@ def _text(fn, h, i):
 class SummaryDecoder:
     """decode(summaries) -> (arrays, catchup, clients): ``arrays`` as SnapshotBatch.arrays(),
     ``catchup[d]`` the legacy catch-up blob's text (None: none), ``clients[d]`` the short id
-    map to continue with (wire.Batch.add_doc(..., clients=...)).  ``interner`` is filled in
-    place (first-seen order); a synthetic interner maps k<n> / integers directly."""
+    map to continue with (wire.Batch.add_doc(..., clients=...)).  Property keys / values are
+    numbered in ``interner`` (shared with the caller's op batches) in the decoder's first-seen
+    order; a synthetic interner maps k<n> / integers directly."""
 
     def __init__(self, interner=None, threads=8):
         self.interner = interner or Interner()
         self.threads = threads
         self.lib = load()
         self.h = self.lib.mt_snapdec_create(1 if self.interner.synthetic else 0)
-        if self.interner.keys or self.interner.vals:
-            raise ValueError("SummaryDecoder numbers keys / values itself: pass an empty interner")
-        self._seen = (0, 0)
+        self._kmap, self._vmap = [], []   # the decoder's ids -> the interner's
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -92,6 +92,7 @@ class SummaryDecoder:
         return paths, blobs, off
 
     def decode_packed(self, paths, blobs, off):
+        """mt_snapdec_decode + fetch: the arrays with the decoder's own property ids."""
         n = len(off) - 1
         nb = len(paths)
         offa = np.asarray(off, dtype=np.int64)
@@ -113,22 +114,36 @@ class SummaryDecoder:
                                   _p(out["props"]), _p(out["min_seq"]), _p(out["cur_seq"]), _p(cu))
         return out, cu
 
+    def _remap(self, out):
+        """The decoder's key / value ids -> the interner's (first-seen order kept)."""
+        it, lib = self.interner, self.lib
+        for i in range(len(self._kmap), lib.mt_snapdec_num_keys(self.h)):
+            self._kmap.append(it.key(_text(lib.mt_snapdec_key, self.h, i)))
+        for i in range(len(self._vmap), lib.mt_snapdec_num_values(self.h)):
+            self._vmap.append(it.val(json.loads(_text(lib.mt_snapdec_value, self.h, i))) & (VAL_FALSY_BIT - 1))
+        km, vm = np.asarray(self._kmap, dtype=np.uint32), np.asarray(self._vmap, dtype=np.uint32)
+        if np.array_equal(km, np.arange(len(km))) and np.array_equal(vm, np.arange(len(vm))):
+            return
+        starts = out["segs"]["props"][out["segs"]["props"] != NO_PROPS].astype(np.int64)
+        p = out["props"]
+        cnt = p[starts].astype(np.int64)
+        tot = int(cnt.sum())
+        if not tot:
+            return
+        first = np.repeat(np.cumsum(cnt) - cnt, cnt)
+        kpos = np.repeat(starts + 1, cnt) + 2 * (np.arange(tot) - first)
+        p[kpos] = km[p[kpos]]
+        v = p[kpos + 1]
+        live = v != VAL_NULL
+        falsy = np.uint32(VAL_FALSY_BIT)
+        v[live] = vm[v[live] & ~falsy] | (v[live] & falsy)
+        p[kpos + 1] = v
+
     def decode(self, summaries):
         paths, blobs, off = self.pack(summaries)
         out, cu = self.decode_packed(paths, blobs, off)
-        it = self.interner
-        if not it.synthetic:   # the names behind the ids, in id order
-            if (len(it.keys), len(it.vals)) != self._seen:
-                raise ValueError("the interner gained ids outside this decoder since its last decode")
-            for i in range(len(it.keys), self.lib.mt_snapdec_num_keys(self.h)):
-                k = _text(self.lib.mt_snapdec_key, self.h, i)
-                it.key_ids[k] = i
-                it.keys.append(k)
-            for i in range(len(it.vals), self.lib.mt_snapdec_num_values(self.h)):
-                v = json.loads(_text(self.lib.mt_snapdec_value, self.h, i))
-                it.val_ids[canonical_json(v)] = i
-                it.vals.append(v)
-            self._seen = (len(it.keys), len(it.vals))
+        if not self.interner.synthetic:
+            self._remap(out)
         catchup = [None if c < 0 else blobs[c].decode("utf-8", errors="surrogatepass") for c in cu]
         clients = []
         for d in range(len(off) - 1):

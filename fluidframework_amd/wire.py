@@ -72,11 +72,24 @@ def _has_js_value(v):
     return False
 
 
+def _js_number(x):
+    """A number as a JS Number (one double type: 1, 1.0 and 1e0 are the same value)."""
+    f = float(x)
+    if f.is_integer() and abs(f) < 1e21:
+        return str(int(f))
+    return repr(f)
+
+
 def canonical_json(v):
     """Canonical form used to intern property values: matchProperties
-    (MT/properties.ts:61-92) compares nested objects structurally, ignoring key order."""
-    if not _has_js_value(v):
-        return json.dumps(v, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+    (MT/properties.ts:61-92) compares with === (numbers as JS Numbers) and nested objects
+    structurally, ignoring key order."""
+    if v is None or isinstance(v, (bool, str)):
+        return json.dumps(v, ensure_ascii=False)
+    if isinstance(v, int):
+        return str(v) if -2 ** 53 < v < 2 ** 53 else _js_number(v)
+    if isinstance(v, float):
+        return _js_number(v)
     if v is NAN or v is UNDEF:
         return v.name
     if isinstance(v, list):

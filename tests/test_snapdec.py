@@ -11,7 +11,7 @@ import pytest
 import golden_util as gu
 from fluidframework_amd import snapdec
 from fluidframework_amd.snapshot import SnapshotBatch, SnapshotError, decode_chunks, encode_chunks
-from fluidframework_amd.wire import Interner
+from fluidframework_amd.wire import Interner, canonical_json
 
 
 def _python(summaries, interner):
@@ -33,7 +33,9 @@ def _check(summaries, synthetic=False, threads=4):
     assert pa["segs"].tobytes() == na["segs"].tobytes()
     assert np.array_equal(pa["text"], na["text"])
     assert np.array_equal(pa["props"], na["props"])
-    assert pi.keys == ni.keys and pi.vals == ni.vals and pi.key_ids == ni.key_ids and pi.val_ids == ni.val_ids
+    assert pi.keys == ni.keys and pi.key_ids == ni.key_ids and pi.val_ids == ni.val_ids
+    for a, b in zip(pi.vals, ni.vals):   # equal as JS values (-0.0 / 0, 1.0 / 1 are one Number)
+        assert canonical_json(a) == canonical_json(b) and type(a) in (type(b), float, int)
     assert pcl == ncl
     assert [list(c) for c in pc] == [json.loads(c) if c is not None else [] for c in nc]
 
@@ -83,7 +85,7 @@ def test_native_decoder_synthetic_bench_chunks():
 
 def test_native_decoder_json_details():
     """JSON corner cases the reference's JSON.parse handles: escapes, surrogate pairs,
-    duplicate members (first position, last value), 1 vs 1.0, nested values."""
+    duplicate members (first position, last value), 1 / 1.0 / 1e0 as one JS Number, nested values."""
     hdr = {"version": "1", "segmentCount": 4, "length": 9, "startIndex": 0,
            "headerMetadata": {"orderedChunkMetadata": [{"id": "header"}], "minSequenceNumber": 0,
                               "sequenceNumber": 7, "totalLength": 9, "totalSegmentCount": 4},
@@ -91,9 +93,39 @@ def test_native_decoder_json_details():
                         {"json": {"marker": {"refType": 1}, "props": {"x": 0}}, "seq": 5, "client": "q"},
                         {"json": "t\\n\"", "seq": 6, "client": "r", "removedSeq": 7, "removedClient": "q"},
                         {"text": "", "props": {}}]}
-    raw = json.dumps(hdr).replace('"x": 0}', '"x": 0, "x": 2.5}')
+    raw = json.dumps(hdr).replace('"x": 0}', '"x": 0, "x": 2.5}').replace('"y": 1.0', '"y": 1e0, "w": -0.0')
     _check([{"header": raw}])
     _check([{"header": raw}, {"header": json.dumps(hdr, ensure_ascii=False)}], threads=2)
+    ni = Interner()
+    snapdec.SummaryDecoder(ni).decode([{"header": raw}])
+    assert ni.vals.count(1) == 1
+    assert ni.val(1) == ni.val(1.0) and ni.val(0) == ni.val(-0.0) | 0   # one id per JS Number
+
+
+def test_native_decoder_shared_interner():
+    """An interner that already numbers other values (the facades keep one per handle): the
+    decoder's ids are mapped into it, so the records equal SnapshotBatch's over that interner,
+    also over two decode calls on one decoder."""
+    docs = [d["chunks"] for d in gu.load("ref_snap_files")["docs"] if "chunks" in d][:4]
+    ok = [c for c in docs if not _raises(c)]
+    pi, ni = Interner(), Interner()
+    for it in (pi, ni):
+        it.key("zz"), it.val("warm"), it.val(7), it.key("k1")
+    dec = snapdec.SummaryDecoder(ni)
+    for part in (ok[:2], ok[2:]):
+        pa, _, _ = _python(part, pi)
+        na, _, _ = dec.decode(part)
+        assert pa["segs"].tobytes() == na["segs"].tobytes()
+        assert np.array_equal(pa["props"], na["props"])
+    assert pi.keys == ni.keys and pi.val_ids == ni.val_ids
+
+
+def _raises(ch):
+    try:
+        decode_chunks(ch)
+        return False
+    except (SnapshotError, KeyError):
+        return True
 
 
 def test_native_decoder_errors():
