@@ -58,7 +58,8 @@ def build_node_addon(verbose=False):
     out = os.path.join(js, "mtreplay.node")
     if not os.path.exists("/usr/include/node/node_api.h"):
         return None
-    deps = [os.path.join(js, "binding.cc"), OUT]
+    build_snapdec(verbose=verbose)
+    deps = [os.path.join(js, "binding.cc"), OUT, SNAP_OUT]
     if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
         return out
     if verbose:

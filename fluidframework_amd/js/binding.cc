@@ -1,4 +1,5 @@
-// binding.cc -- thin N-API addon over the C ABI of include/mt_replay.h (libmtreplay.so).
+// binding.cc -- thin N-API addon over the C ABI of include/mt_replay.h (libmtreplay.so) and
+// the summary decoder of include/mt_snapshot.h (libmtsnapdec.so).
 //
 // The reference's host language is TypeScript on Node; its merge-tree boundary is the
 // class Client (packages/dds/merge-tree/src/client.ts:43) fed by
@@ -22,6 +23,7 @@
 #include <vector>
 
 #include "../../include/mt_replay.h"
+#include "../../include/mt_snapshot.h"
 
 namespace {
 
@@ -437,6 +439,110 @@ napi_value RegeneratePending(napi_env env, napi_callback_info info) {
     return out;
 }
 
+// decodeSummaries(paths: string[], blobs: string[], docBlobOff: number[], threads) ->
+// {docSegOff, nHeader, segs, text, props, minSeq, curSeq, catchup, keys, vals, clients}:
+// SnapshotLoader's host half (include/mt_snapshot.h) over every document's blobs.  Property
+// ids in props are the decoder's (keys[i] / JSON.parse(vals[i])); the facade maps them into
+// its interner.  catchup[d] = index of the document's legacy catch-up blob or -1.
+napi_value DecodeSummaries(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    uint32_t nb = 0, nd1 = 0;
+    NAPI_CALL(env, napi_get_array_length(env, argv[0], &nb));
+    NAPI_CALL(env, napi_get_array_length(env, argv[2], &nd1));
+    if (nd1 == 0) {
+        napi_throw_error(env, nullptr, "decodeSummaries: empty document offsets");
+        return nullptr;
+    }
+    std::vector<std::string> paths(nb), blobs(nb);
+    std::vector<const char *> pp(nb), jp(nb);
+    std::vector<uint32_t> pl(nb);
+    std::vector<uint64_t> jl(nb);
+    auto str = [&](napi_value arr, uint32_t i, std::string &out) -> bool {
+        napi_value v;
+        size_t n = 0;
+        if (napi_get_element(env, arr, i, &v) != napi_ok) return false;
+        if (napi_get_value_string_utf8(env, v, nullptr, 0, &n) != napi_ok) return false;
+        out.resize(n + 1);
+        if (napi_get_value_string_utf8(env, v, &out[0], n + 1, &n) != napi_ok) return false;
+        out.resize(n);
+        return true;
+    };
+    for (uint32_t i = 0; i < nb; i++) {
+        if (!str(argv[0], i, paths[i]) || !str(argv[1], i, blobs[i])) {
+            napi_throw_type_error(env, nullptr, "decodeSummaries: paths and blobs must be strings");
+            return nullptr;
+        }
+        pp[i] = paths[i].data();
+        pl[i] = (uint32_t)paths[i].size();
+        jp[i] = blobs[i].data();
+        jl[i] = blobs[i].size();
+    }
+    std::vector<int64_t> off(nd1);
+    for (uint32_t i = 0; i < nd1; i++) {
+        napi_value v;
+        double x = 0;
+        NAPI_CALL(env, napi_get_element(env, argv[2], i, &v));
+        NAPI_CALL(env, napi_get_value_double(env, v, &x));
+        off[i] = (int64_t)x;
+    }
+    const uint32_t nd = nd1 - 1;
+    if (off[0] != 0 || off[nd] != (int64_t)nb) {
+        napi_throw_range_error(env, nullptr, "decodeSummaries: docBlobOff must run from 0 to blobs.length");
+        return nullptr;
+    }
+    const int threads = get_i32(env, argv[3]);
+    mt_snapdec *dec = mt_snapdec_create(0);
+    if (mt_snapdec_decode(dec, nd, off.data(), pp.data(), pl.data(), jp.data(), jl.data(), threads) != 0) {
+        napi_throw_error(env, nullptr, mt_snapdec_error(dec));
+        mt_snapdec_destroy(dec);
+        return nullptr;
+    }
+    uint64_t ns = 0, nt = 0, npr = 0;
+    mt_snapdec_sizes(dec, &ns, &nt, &npr);
+    napi_value out, a, ab;
+    void *pd[9] = {};
+    NAPI_CALL(env, napi_create_object(env, &out));
+    struct Arr {
+        const char *name;
+        napi_typedarray_type t;
+        size_t n, esz;
+    } arrs[] = {{"docSegOff", napi_bigint64_array, nd + 1u, 8}, {"nHeader", napi_int32_array, nd, 4},
+                {"segs", napi_uint8_array, ns * sizeof(mt_seg_rec), 1}, {"text", napi_uint16_array, nt, 2},
+                {"props", napi_uint32_array, npr, 4},     {"minSeq", napi_int32_array, nd, 4},
+                {"curSeq", napi_int32_array, nd, 4},      {"catchup", napi_bigint64_array, nd, 8}};
+    for (int i = 0; i < 8; i++) {
+        NAPI_CALL(env, napi_create_arraybuffer(env, std::max<size_t>(arrs[i].n * arrs[i].esz, 8), &pd[i], &ab));
+        memset(pd[i], 0, std::max<size_t>(arrs[i].n * arrs[i].esz, 8));
+        NAPI_CALL(env, napi_create_typedarray(env, arrs[i].t, arrs[i].n, ab, 0, &a));
+        NAPI_CALL(env, napi_set_named_property(env, out, arrs[i].name, a));
+    }
+    mt_snapdec_fetch(dec, (int64_t *)pd[0], (int32_t *)pd[1], (mt_seg_rec *)pd[2], (uint16_t *)pd[3], (uint32_t *)pd[4],
+                     (int32_t *)pd[5], (int32_t *)pd[6], (int64_t *)pd[7]);
+    auto strings = [&](const char *name, uint32_t n, int64_t (*get)(const mt_snapdec *, uint32_t, char *, uint64_t)) -> bool {
+        napi_value arr, v;
+        if (napi_create_array_with_length(env, n, &arr) != napi_ok) return false;
+        std::string buf;
+        for (uint32_t i = 0; i < n; i++) {
+            const int64_t len = get(dec, i, nullptr, 0);
+            buf.resize((size_t)std::max<int64_t>(len, 0));
+            get(dec, i, &buf[0], buf.size());
+            if (napi_create_string_utf8(env, buf.data(), buf.size(), &v) != napi_ok) return false;
+            if (napi_set_element(env, arr, i, v) != napi_ok) return false;
+        }
+        return napi_set_named_property(env, out, name, arr) == napi_ok;
+    };
+    const bool ok = strings("keys", mt_snapdec_num_keys(dec), mt_snapdec_key) &&
+                    strings("vals", mt_snapdec_num_values(dec), mt_snapdec_value) &&
+                    strings("clients", nd, mt_snapdec_doc_clients);
+    mt_snapdec_destroy(dec);
+    if (!ok) {
+        napi_throw_error(env, nullptr, "decodeSummaries: N-API string conversion failed");
+        return nullptr;
+    }
+    return out;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     struct {
         const char *name;
@@ -448,7 +554,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"deltaLogReset", DeltaLogReset},
                {"maintenanceCounts", MaintenanceCounts},
                {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs},
-               {"regeneratePending", RegeneratePending}};
+               {"regeneratePending", RegeneratePending}, {"decodeSummaries", DecodeSummaries}};
     for (auto &f : fns) {
         napi_value v;
         NAPI_CALL(env, napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v));

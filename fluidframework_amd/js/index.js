@@ -18,8 +18,8 @@
  */
 const assert = require("assert");
 const path = require("path");
-const { BatchEncoder, Interner, Grow, VAL_NULL } = require("./encode");
-const { SnapshotEncoder, decodeChunks, treeChunks } = require("./snapshot");
+const { BatchEncoder, Interner, VAL_NULL } = require("./encode");
+const { treeChunks } = require("./snapshot");
 
 const native = require(path.join(__dirname, "mtreplay.node"));
 
@@ -42,6 +42,39 @@ function jsKeyOrder(pairs) {
     const isIndex = (k) => /^(0|[1-9][0-9]*)$/.test(k) && Number(k) < 4294967295;
     const ints = pairs.filter(([k]) => isIndex(k)).sort((a, b) => Number(a[0]) - Number(b[0]));
     return ints.concat(pairs.filter(([k]) => !isIndex(k)));
+}
+
+/**
+ * SnapshotLoader's host half for many summaries (snapshotLoader.ts:36-228) in native code
+ * (include/mt_snapshot.h through the addon): the mt_load_snapshots arrays with property ids
+ * mapped into `interner` (first-seen order), the short client maps and the catch-up
+ * messages per document.  snapshot.js (decodeChunks + SnapshotEncoder) is the same in JS.
+ */
+function decodeSummaries(summaries, interner, threads = 8) {
+    const paths = [], blobs = [], off = [0];
+    for (const s of summaries) {
+        const ch = s.entries ? treeChunks(s) : s;
+        for (const k of Object.keys(ch)) { paths.push(k); blobs.push(ch[k]); }
+        off.push(paths.length);
+    }
+    const a = native.decodeSummaries(paths, blobs, off, threads);
+    const km = a.keys.map((k) => interner.key(k));
+    const vm = a.vals.map((v) => (interner.val(JSON.parse(v)) & 0x3FFFFFFF) >>> 0);
+    const dv = new DataView(a.segs.buffer, a.segs.byteOffset, a.segs.byteLength);
+    const p = a.props;
+    for (let r = 0; r < a.segs.byteLength; r += 32) {
+        const o = dv.getUint32(r + 16, true);
+        if (o === 0xFFFFFFFF) { continue; }
+        for (let j = 0, n = p[o]; j < n; j++) {
+            const k = o + 1 + 2 * j;
+            p[k] = km[p[k]];
+            const v = p[k + 1];
+            if (v !== VAL_NULL) { p[k + 1] = (vm[(v & 0x3FFFFFFF) >>> 0] | (v & 0x80000000)) >>> 0; }
+        }
+    }
+    a.clients = a.clients.map((c) => new Map(JSON.parse(c).map((id, i) => [id, i + 1])));
+    a.catchup = Array.from(a.catchup, (b) => (b < 0n ? [] : JSON.parse(blobs[Number(b)])));
+    return a;
 }
 
 class GpuMergeTreeBatch {
@@ -96,25 +129,20 @@ class GpuMergeTreeBatch {
      * legacy catch-up messages are queued like SharedSegmentSequence.loadCore applies them.
      * A summary the reference cannot load fails that document the same way.
      */
-    loadSnapshots(summaries) {
+    loadSnapshots(summaries, threads = 8) {
         assert(summaries.length === this.nDocs);
         this.flush();
-        const enc = new SnapshotEncoder(this.interner, Grow);
-        const decoded = summaries.map((s) => decodeChunks(s.entries ? treeChunks(s) : s));
-        decoded.forEach((snap, d) => {
-            this.clients[d] = new Map();
-            enc.addDoc(snap, this.clients[d]);
-        });
-        const a = enc.arrays();
+        const a = decodeSummaries(summaries, this.interner, threads);
         native.loadSnapshots(this.h, a.docSegOff, a.nHeader, a.segs, a.text, a.props, a.minSeq, a.curSeq);
         this.failed.fill(0);
         this.logPos.fill(0);
         const st = native.status(this.h);
         for (let d = 0; d < this.nDocs; d++) {
+            this.clients[d] = a.clients[d];
             if (st[d] !== 0) { this.failed[d] = st[d]; }
             const v = this.views.get(d);
-            if (v) { v.currentSeq = decoded[d].curSeq; }
-            for (const m of decoded[d].catchup) { this.pending[d].push(m); this.queued++; }
+            if (v) { v.currentSeq = a.curSeq[d]; }
+            for (const m of a.catchup[d]) { this.pending[d].push(m); this.queued++; }
         }
     }
 
@@ -506,4 +534,4 @@ class GpuClient {
     }
 }
 
-module.exports = { GpuMergeTreeBatch, GpuClient, native, VAL_NULL };
+module.exports = { GpuMergeTreeBatch, GpuClient, decodeSummaries, native, VAL_NULL };

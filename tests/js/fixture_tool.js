@@ -210,6 +210,16 @@ if (mode === "encode") {
         docSegOff: Array.from(a.docSegOff, Number), nHeader: Array.from(a.nHeader),
         minSeq: Array.from(a.minSeq), curSeq: Array.from(a.curSeq),
     }));
+} else if (mode === "snapnative") {
+    // the same arrays from the native decoder (include/mt_snapshot.h through the addon)
+    const { decodeSummaries } = require(path.join(repo, "fluidframework_amd", "js"));
+    const a = decodeSummaries(fx.docs.map((d) => d.chunks), new Interner(), 4);
+    process.stdout.write(JSON.stringify({
+        segs: hex(a.segs), text: hex(a.text), props: hex(a.props),
+        docSegOff: Array.from(a.docSegOff, Number), nHeader: Array.from(a.nHeader),
+        minSeq: Array.from(a.minSeq), curSeq: Array.from(a.curSeq),
+        clients: a.clients.map((m) => Array.from(m.entries())), catchup: a.catchup,
+    }));
 } else if (mode === "loadsnap") {
     // summaries (snapshot fixtures: reference-written chunks) loaded through
     // GpuMergeTreeBatch.loadSnapshots, then the tail messages through GpuClient.applyMsg

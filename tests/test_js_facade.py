@@ -27,6 +27,7 @@ def _node(*args, timeout=300):
 def _addon():
     from fluidframework_amd import build
     build.build()
+    build.build_snapdec()
     if not os.path.exists(os.path.join(JS, "mtreplay.node")):
         subprocess.check_call(["sh", os.path.join(JS, "build.sh")])
 
@@ -104,6 +105,31 @@ def test_js_snapshot_decoder_matches_python(name):
     assert bytes.fromhex(got["text"]) == a["text"][:n_text].tobytes()
     n_props = len(bytes.fromhex(got["props"])) // 4
     assert bytes.fromhex(got["props"]) == a["props"][:n_props].tobytes()
+
+
+@pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
+def test_js_native_summary_decoder_matches_python(name):
+    """decodeSummaries (the native decoder, include/mt_snapshot.h, through the addon; what
+    GpuMergeTreeBatch.loadSnapshots uses) gives the records, arenas, client maps and catch-up
+    messages of fluidframework_amd/snapshot.py.  Host-only: no device call."""
+    _addon()
+    fx = gu.load(name)
+    got = _node("snapnative", os.path.join(gu.GOLDEN, name + ".json.gz"))
+    from fluidframework_amd.snapshot import SnapshotBatch, decode_chunks
+    sb = SnapshotBatch(gu.Interner())
+    clients, catchup = [], []
+    for d in fx["docs"]:
+        snap = decode_chunks(d["chunks"])
+        clients.append(sb.add_doc(snap))
+        catchup.append(snap.catchup)
+    a = sb.arrays()
+    assert bytes.fromhex(got["segs"]) == a["segs"].tobytes()
+    assert got["docSegOff"] == a["doc_off"].tolist() and got["nHeader"] == a["n_header"].tolist()
+    assert got["minSeq"] == a["min_seq"].tolist() and got["curSeq"] == a["cur_seq"].tolist()
+    assert bytes.fromhex(got["text"]) == a["text"].tobytes()
+    assert bytes.fromhex(got["props"]) == a["props"].tobytes()
+    assert [dict(c) for c in got["clients"]] == clients
+    assert got["catchup"] == catchup
 
 
 @pytest.mark.gpu
