@@ -111,6 +111,18 @@ class MergeTreeBatch:
                                                _native.ptr(text), len(text), _native.ptr(props), len(props),
                                                _native.ptr(mn), _native.ptr(cu)), "mt_load_snapshots")
 
+    def load_summaries(self, summaries, interner, threads=8):
+        """Client.load of every document from its summary blobs ({path: JSON text}, one dict
+        per document): decoded on the host by the native decoder (snapdec, include/
+        mt_snapshot.h; MT/snapshotLoader.ts:36-228), then loaded as load_snapshots does.
+        Returns (catchup, clients): per document the legacy catch-up messages and the short
+        client map its ops continue with (wire.Batch.add_doc(..., clients=...))."""
+        import json as _json
+        from .snapdec import SummaryDecoder
+        la, catchup, clients = SummaryDecoder(interner, threads).decode(summaries)
+        self.load_snapshots(la)
+        return [_json.loads(c) if c is not None else [] for c in catchup], clients
+
     def upload_snapshots(self, la):
         """Device-resident summaries (mt_snapshots_upload); .load_async() enqueues a load."""
         off, nh, segs, text, props, mn, cu = self._snap_args(la)

@@ -221,6 +221,31 @@ def test_gpu_snapshot_load_matches_reference(name, tier):
 
 
 @pytest.mark.parametrize("tier", ["lds", "paged"])
+@pytest.mark.parametrize("name", gu.SNAP_FIXTURES)
+def test_gpu_summaries_native_decoder_match_reference(name, tier):
+    """MergeTreeBatch.load_summaries: the reference-written blobs decoded by the native
+    decoder (libmtsnapdec.so) and loaded; catch-up + tail ops continue its client maps.  The
+    tree after the tail equals the reference's."""
+    from fluidframework_amd.wire import Batch
+    fx = gu.load(name)
+    docs = [d for d in fx["docs"] if gu.snap_status(d) == 0]
+    interner = gu.Interner()
+    mt = _gpu_batch(len(docs), **SNAP_TIERS[tier])
+    catchup, clients = mt.load_summaries([d["chunks"] for d in docs], interner, threads=4)
+    assert (mt.status() == 0).all()
+    b = Batch(interner)
+    for d, cu, cl in zip(docs, catchup, clients):
+        b.add_doc("", list(cu) + gu.compact_msgs_to_dicts(d.get("tail", [])), clients=cl)
+    mt.apply_arrays(b.arrays())
+    bad = []
+    for i, doc in enumerate(docs):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected_snap(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, f"{name}: {bad[:4]}"
+
+
+@pytest.mark.parametrize("tier", ["lds", "paged"])
 @pytest.mark.parametrize("name", ["ref_snap", "ref_snap_body"])
 def test_gpu_snapshot_emission_matches_reference(name, tier):
     """SnapshotV1 emission from device state (mt_extract_snapshots = extractSync, then
