@@ -44,14 +44,8 @@ template <class T> struct PagedDoc {
     GLB_AS v4i *gA;           // this document's pages (slot 0 of page 0)
     GLB_AS u64 *gO;
     GLB_AS v4u *gB;
-    GLB_AS PageMeta *gmeta;
-    GLB_AS uint16_t *gdir;
-    GLB_AS uint8_t *gcnt;
-    GLB_AS v2i *gheap;
-    GLB_AS int *gupage;
-    GLB_AS v4i *guA;
-    GLB_AS u64 *guO;
-    GLB_AS uint16_t *gumap;
+    GLB_AS uint16_t *gumap;   // (the bases used only at load / store are PgCold's: fewer live SGPRs)
+    int doc;
     int PP, PH, UT, UM;       // LDS capacities of this launch (pages, heap, table); uid map size
     int PPh;                  // page capacity of the HBM arrays (stride; >= PP)
     int ut_n;
@@ -1158,22 +1152,39 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
 }
 
 // ------------------------------------------------------------------ bind / store / convert
-// Per-document HBM bases of the paged arrays.
+// Per-document HBM bases of the paged arrays the op path uses (pages, uid map).
 TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
     const size_t PP = st.PP;
     pd.gA = (GLB_AS v4i *)(st.pgA + (size_t)doc * PP * MT_PG_SLOTS);
     pd.gO = (GLB_AS u64 *)(st.pgO + (size_t)doc * PP * MT_PG_SLOTS);
     pd.gB = (GLB_AS v4u *)(st.pgB + (size_t)doc * PP * MT_PG_SLOTS);
-    pd.gmeta = (GLB_AS PageMeta *)(st.pgMeta + (size_t)doc * PP);
-    pd.gdir = (GLB_AS uint16_t *)(st.pgDir + (size_t)doc * PP);
-    pd.gcnt = (GLB_AS uint8_t *)(st.pgCnt + (size_t)doc * MT_LV * PP);
-    pd.gheap = (GLB_AS v2i *)(st.pgHeap + (size_t)doc * (st.PH + 1));
-    pd.gupage = (GLB_AS int *)(st.pgUtPage + (size_t)doc * st.UT);
-    pd.guA = (GLB_AS v4i *)(st.pgUtA + (size_t)doc * st.UT);
-    pd.guO = (GLB_AS u64 *)(st.pgUtO + (size_t)doc * st.UT);
     pd.gumap = (GLB_AS uint16_t *)(st.pgUmap + (size_t)doc * st.UM);
     pd.PPh = st.PP;
     pd.UM = st.UM;
+    pd.doc = doc;
+}
+
+// The bases only pg_load / pg_store touch, recomputed there from the kernel arguments.
+struct PgCold {
+    GLB_AS PageMeta *gmeta;
+    GLB_AS uint16_t *gdir;
+    GLB_AS uint8_t *gcnt;
+    GLB_AS v2i *gheap;
+    GLB_AS int *gupage;
+    GLB_AS v4i *guA;
+    GLB_AS u64 *guO;
+};
+__device__ __forceinline__ PgCold pg_cold(const DevState &st, int doc) {
+    const size_t PP = st.PP;
+    PgCold c;
+    c.gmeta = (GLB_AS PageMeta *)(st.pgMeta + (size_t)doc * PP);
+    c.gdir = (GLB_AS uint16_t *)(st.pgDir + (size_t)doc * PP);
+    c.gcnt = (GLB_AS uint8_t *)(st.pgCnt + (size_t)doc * MT_LV * PP);
+    c.gheap = (GLB_AS v2i *)(st.pgHeap + (size_t)doc * (st.PH + 1));
+    c.gupage = (GLB_AS int *)(st.pgUtPage + (size_t)doc * st.UT);
+    c.guA = (GLB_AS v4i *)(st.pgUtA + (size_t)doc * st.UT);
+    c.guO = (GLB_AS u64 *)(st.pgUtO + (size_t)doc * st.UT);
+    return c;
 }
 
 // Window + upper DocT instances over the LDS layout; scalars from the document header.
@@ -1284,7 +1295,8 @@ TD void pg_mark_free(PagedDoc<T> &pd) {
 
 // Loads a paged document's directory, meta, upper counts, heap and table into LDS.  Returns
 // false (nothing staged) when the document does not fit this launch's LDS capacities.
-TD bool pg_load(PagedDoc<T> &pd) {
+TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
+    const PgCold g = pg_cold(st, pd.doc);
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     const DocHdr h = *w.hp;
@@ -1292,33 +1304,34 @@ TD bool pg_load(PagedDoc<T> &pd) {
     if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
     if (T::kOvlBits < 64 && w.wide) return false;
     int mx = 0;
-    for (int q = lane(); q < np; q += MT_WAVE) mx = max(mx, (int)pd.gdir[q]);
+    for (int q = lane(); q < np; q += MT_WAVE) mx = max(mx, (int)g.gdir[q]);
     if (wave_max(mx) >= pd.PP) return false;   // a page id allocated by a wider launch
     if (lane() < MT_LV) up.nb[lane()] = w.hp->n_blk[lane()];
     wsync<T>();
-    for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = pd.gdir[q];
+    for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = g.gdir[q];
     {
-        GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)pd.gmeta;
+        GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)g.gmeta;
         LDS_AS uint32_t *lm = (LDS_AS uint32_t *)pd.meta;
         for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) lm[i] = gm[i];
     }
     for (int l = 1; l < up.depth; l++) {
         const int nl = nbr(up, l);
-        for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = pd.gcnt[l * pd.PPh + b];
+        for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = g.gcnt[l * pd.PPh + b];
     }
-    for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = pd.gheap[i];
+    for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = g.gheap[i];
     pd.ut_n = h.pad[HDR_UTN];
     for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
-        pd.upage[e] = (uint16_t)pd.gupage[e];
-        pd.uA[e] = pd.guA[e];
-        pd.uO[e] = pd.guO[e];
+        pd.upage[e] = (uint16_t)g.gupage[e];
+        pd.uA[e] = g.guA[e];
+        pd.uO[e] = g.guO[e];
     }
     wsync<T>();
     pg_mark_free(pd);
     return true;
 }
 
-TD void pg_store(PagedDoc<T> &pd) {
+TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
+    const PgCold g = pg_cold(st, pd.doc);
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     // a document that failed keeps the state it had at the failure (the reference's state at
@@ -1330,21 +1343,21 @@ TD void pg_store(PagedDoc<T> &pd) {
     w.oslot[2 * lane()] = w.ocli;
     wsync<T>();
     const int np = nbr(up, 1);
-    for (int q = lane(); q < np; q += MT_WAVE) pd.gdir[q] = up.dir[q];
+    for (int q = lane(); q < np; q += MT_WAVE) g.gdir[q] = up.dir[q];
     {
-        GLB_AS uint32_t *gm = (GLB_AS uint32_t *)pd.gmeta;
+        GLB_AS uint32_t *gm = (GLB_AS uint32_t *)g.gmeta;
         LDS_AS const uint32_t *lm = (LDS_AS const uint32_t *)pd.meta;
         for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) gm[i] = lm[i];
     }
     for (int l = 1; l < up.depth; l++) {
         const int nl = nbr(up, l);
-        for (int b = lane(); b < nl; b += MT_WAVE) pd.gcnt[l * pd.PPh + b] = lvl(up, l)[b];
+        for (int b = lane(); b < nl; b += MT_WAVE) g.gcnt[l * pd.PPh + b] = lvl(up, l)[b];
     }
-    for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) pd.gheap[i] = w.heap[i];
+    for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) g.gheap[i] = w.heap[i];
     for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
-        pd.gupage[e] = pd.upage[e];
-        pd.guA[e] = pd.uA[e];
-        pd.guO[e] = pd.uO[e];
+        g.gupage[e] = pd.upage[e];
+        g.guA[e] = pd.uA[e];
+        g.guO[e] = pd.uO[e];
     }
     int nbl[MT_LV];
 #pragma unroll

@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
         return;
     }
     if (st.hdr[doc].pad[HDR_PAGED]) {
-        if (!pg_load(pd)) {
+        if (!pg_load(pd, st)) {
             if (pc.tight) {
                 pg_handover<T>(st, doc, k0);
             } else if (lane() == 0) {   // cannot happen: the last tier has the HBM capacities
@@ -706,7 +706,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     }
     // a window capacity is a paged-layout capacity: there is no further tier
     if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
-    pg_store(pd);
+    pg_store(pd, st);
     pg_peaks(st, pd, pk_ut, pk_heap);
     if (spill_at >= 0 && w.status == 0)
         pg_handover<T>(st, doc, spill_at);
@@ -784,7 +784,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         if (w.status) fail_out[doc] = w.status;
         st.retry[doc] = 0;
     }
-    pg_store(pd);
+    pg_store(pd, st);
     pg_peaks(st, pd, pk_ut, pk_heap);
 }
 
@@ -810,7 +810,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_convert(DevState st, LoadScrat
     src.heap = nullptr;   // a fresh collaboration: heap_n == 0
     src.B = (size_t)w.hp->n_blk[0];
     if (w.status == 0 && pg_convert(pd, src)) {
-        pg_store(pd);
+        pg_store(pd, st);
     } else if (lane() == 0) {
         st.hdr[doc].status = w.status == MT_DOC_RETRY || w.status == 0 ? MT_DOC_CAPACITY : w.status;
         st.hdr[doc].pad[HDR_DIAG] = w.cap_cause;
