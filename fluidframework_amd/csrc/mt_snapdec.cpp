@@ -15,6 +15,7 @@
 // numbers keys / values first-seen in document order, exactly as wire.Interner does.
 #include <algorithm>
 #include <atomic>
+#include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -70,19 +71,16 @@ struct Blob {
     }
     bool present(uint32_t i) const { return i != NONE && nodes[i].t != Node::NUL; }
     std::u16string ustr(uint32_t i) const { return std::u16string(s(nodes[i].off), nodes[i].len); }
-    std::u16string ukey(uint32_t i) const { return std::u16string(s(nodes[i].koff), nodes[i].klen); }
     bool is_int(uint32_t i) const {
         const char *p = src + nodes[i].off;
         for (uint32_t k = 0; k < nodes[i].len; k++)
             if (p[k] == '.' || p[k] == 'e' || p[k] == 'E') return false;
         return true;
     }
-    double num(uint32_t i) const {   // JS Number of the lexeme
-        char b[64];
-        const uint32_t l = std::min<uint32_t>(nodes[i].len, 63);
-        memcpy(b, src + nodes[i].off, l);
-        b[l] = 0;
-        return strtod(b, nullptr);
+    double num(uint32_t i) const {   // JS Number of the lexeme (locale-independent)
+        double x = 0;
+        std::from_chars(src + nodes[i].off, src + nodes[i].off + nodes[i].len, x);
+        return x;
     }
     int64_t as_int(uint32_t i) const {
         if (i == NONE || nodes[i].t != Node::NUM) return 0;
@@ -339,12 +337,11 @@ void canon(std::string &o, const Blob &B, uint32_t i) {
                 else o.append(B.src + v.off, v.len);
             } else {   // JS Number: 1.0, 1e0 and 1 are one value
                 const double x = B.num(i);
-                char b[40];
-                if (std::isfinite(x) && x == std::floor(x) && std::fabs(x) < 1e21)
-                    snprintf(b, sizeof b, "%.0f", x == 0 ? 0.0 : x);
-                else
-                    snprintf(b, sizeof b, "%.17g", x);
-                o += b;
+                char b[400];
+                const auto r = std::isfinite(x) && x == std::floor(x) && std::fabs(x) < 1e21
+                                   ? std::to_chars(b, b + sizeof b, x == 0 ? 0.0 : x, std::chars_format::fixed, 0)
+                                   : std::to_chars(b, b + sizeof b, x);   // shortest round trip
+                o.append(b, r.ptr);
             }
             break;
         case Node::STR: json_str(o, B.s(v.off), v.len); break;

@@ -86,19 +86,22 @@ def test_native_decoder_synthetic_bench_chunks():
 def test_native_decoder_json_details():
     """JSON corner cases the reference's JSON.parse handles: escapes, surrogate pairs,
     duplicate members (first position, last value), 1 / 1.0 / 1e0 as one JS Number, nested values."""
-    hdr = {"version": "1", "segmentCount": 4, "length": 9, "startIndex": 0,
+    hdr = {"version": "1", "segmentCount": 5, "length": 9, "startIndex": 0,
            "headerMetadata": {"orderedChunkMetadata": [{"id": "header"}], "minSequenceNumber": 0,
-                              "sequenceNumber": 7, "totalLength": 9, "totalSegmentCount": 4},
+                              "sequenceNumber": 7, "totalLength": 10, "totalSegmentCount": 5},
            "segments": [{"text": "aé\U0001F600", "props": {"x": 1, "y": 1.0, "z": {"b": [1, None], "a": "s"}}},
                         {"json": {"marker": {"refType": 1}, "props": {"x": 0}}, "seq": 5, "client": "q"},
                         {"json": "t\\n\"", "seq": 6, "client": "r", "removedSeq": 7, "removedClient": "q"},
-                        {"text": "", "props": {}}]}
+                        {"text": "", "props": {}},
+                        {"text": "n", "props": {"a": 0.1, "b": 1e300, "c": 12345678901234567890123, "d": 1e21,
+                                                "e": 99999999999999999, "f": -2.5e-7, "g": 100000000000000000}}]}
     raw = json.dumps(hdr).replace('"x": 0}', '"x": 0, "x": 2.5}').replace('"y": 1.0', '"y": 1e0, "w": -0.0')
     _check([{"header": raw}])
     _check([{"header": raw}, {"header": json.dumps(hdr, ensure_ascii=False)}], threads=2)
     ni = Interner()
     snapdec.SummaryDecoder(ni).decode([{"header": raw}])
     assert ni.vals.count(1) == 1
+    assert ni.val(99999999999999999) == ni.val(100000000000000000)   # one double
     assert ni.val(1) == ni.val(1.0) and ni.val(0) == ni.val(-0.0) | 0   # one id per JS Number
 
 
