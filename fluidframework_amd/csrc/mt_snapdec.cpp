@@ -179,7 +179,10 @@ struct Reader {
             else return fail("bad UTF-8");
             p++;
             if (e - p < n) return fail("bad UTF-8");
-            for (int i = 0; i < n; i++) cp = (cp << 6) | ((unsigned char)*p++ & 0x3F);
+            for (int i = 0; i < n; i++, p++) {
+                if (((unsigned char)*p & 0xC0) != 0x80) return fail("bad UTF-8");
+                cp = (cp << 6) | ((unsigned char)*p & 0x3F);
+            }
             if (cp >= 0x10000) {
                 cp -= 0x10000;
                 o.push_back((char16_t)(0xD800 + (cp >> 10)));
@@ -243,10 +246,25 @@ struct Reader {
         if (e - p >= 4 && !memcmp(p, "true", 4)) { out = node(Node::BOOL); B.nodes[out].b = 1; p += 4; return true; }
         if (e - p >= 5 && !memcmp(p, "false", 5)) { out = node(Node::BOOL); p += 5; return true; }
         if (e - p >= 4 && !memcmp(p, "null", 4)) { out = node(Node::NUL); p += 4; return true; }
-        if (c == '-' || (c >= '0' && c <= '9')) {
+        if (c == '-' || (c >= '0' && c <= '9')) {   // -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
             const char *s = p;
+            auto digits = [&]() {
+                const char *q = p;
+                while (p < e && *p >= '0' && *p <= '9') p++;
+                return p > q;
+            };
             if (*p == '-') p++;
-            while (p < e && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '+' || *p == '-')) p++;
+            if (p < e && *p == '0') p++;
+            else if (!digits()) return fail("bad number");
+            if (p < e && *p == '.') {
+                p++;
+                if (!digits()) return fail("bad number");
+            }
+            if (p < e && (*p == 'e' || *p == 'E')) {
+                p++;
+                if (p < e && (*p == '+' || *p == '-')) p++;
+                if (!digits()) return fail("bad number");
+            }
             out = node(Node::NUM);
             B.nodes[out].off = (uint32_t)(s - B.src);
             B.nodes[out].len = (uint32_t)(p - s);
@@ -257,6 +275,10 @@ struct Reader {
 };
 
 bool parse(Blob &b, std::string &err) {
+    if (b.n >= 0xFFFFFFFFull) {   // node offsets are 32-bit
+        err = "blob larger than 4 GiB";
+        return false;
+    }
     b.nodes.clear();
     b.str.clear();
     b.nodes.reserve(b.n / 12 + 8);
@@ -693,7 +715,7 @@ int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, c
     if (!s || !blob_off || (blob_off[n_docs] > 0 && (!paths || !path_len || !json || !json_len))) return -1;
     s->err.clear();
     if (s->docs.size() < n_docs) s->docs.resize(n_docs);
-    const int nt = std::max(1, std::min<int>(threads, (int)std::max<uint32_t>(n_docs, 1)));
+    const int nt = std::max(1, std::min({threads, 256, (int)std::max<uint32_t>(n_docs, 1)}));
     if ((int)s->workers.size() < nt) s->workers.resize((size_t)nt);
     const Blobs in{blob_off, paths, path_len, json, json_len};
     // phase 1: documents parsed and specToSegment'ed on nt threads (dynamic, 8 at a time)
@@ -722,6 +744,10 @@ int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, c
         ns += o.segs.size();
         ntx += o.text.size();
         npr += o.props.size();
+    }
+    if (ntx > 0xFFFFFFFFull || npr > 0xFFFFFFFFull) {   // mt_seg_rec offsets are 32-bit
+        s->err = "decoded text / property arena exceeds 2^32 entries: decode fewer documents per call";
+        return -1;
     }
     s->segs.resize(ns);
     s->text.resize(ntx);

@@ -139,3 +139,13 @@ def test_native_decoder_errors():
         dec.decode([{"header": '{"version": "2"}'}])
     with pytest.raises(SnapshotError):
         dec.decode([{"header": '{"version": "1", '}])
+    for bad in ('{"version": "1", "x": 01}', '{"version": "1", "x": 1.}', '{"version": "1", "x": 1e}',
+                '{"version": "1", "x": -}', '{"version": "1", "x": 1-2}', b'{"version": "1", "x": "\xc3("}',
+                b'{"version": "1", "x": "\x01"}'):
+        with pytest.raises(SnapshotError):   # JSON.parse throws on each of these
+            dec.decode([{"header": bad}])
+        with pytest.raises(ValueError):
+            json.loads(bad)
+    ok = snapdec.SummaryDecoder(Interner(), threads=100000)   # thread count is capped
+    ok.decode([{"header": '{"version": "1", "segmentCount": 0, "segments": [], "headerMetadata": '
+                          '{"orderedChunkMetadata": [{"id": "header"}], "sequenceNumber": 3, "totalSegmentCount": 0}}'}])
