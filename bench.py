@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
     ap.add_argument("--shard", type=int, default=-1, help="document shard to replay (default: this rank)")
     ap.add_argument("--page-caps", default="", help="paged layout LDS capacities 'pages,unsettled,heap' (sweeps)")
+    ap.add_argument("--paged-slices", type=int, default=0,
+                    help="mt_options.paged_slices for paged configs (0 = off; see include/mt_replay.h)")
     ap.add_argument("--verify-per-rank", type=int, default=4,
                     help="N > 1: documents of every rank's shard re-derived by the CPU oracle on rank 0")
     return ap.parse_args()
@@ -461,6 +463,8 @@ def main():
     if args.page_caps:
         pp, ut, ph = (int(x) for x in args.page_caps.split(","))
         caps.update(lds_page_capacity=pp, lds_unsettled_capacity=ut, lds_page_heap_capacity=ph)
+    if args.paged_slices and "page_capacity" in caps:
+        caps["paged_slices"] = args.paged_slices
     t_gen = time.time()
     mt = MergeTreeBatch(docs, device=local_rank, **caps)
     batch = mt.generate(cfg, doc_base)          # untimed: inputs resident in HBM

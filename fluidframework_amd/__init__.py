@@ -35,14 +35,14 @@ class MergeTreeBatch:
                  text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0,
                  page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0,
                  lds_page_capacity=0, lds_unsettled_capacity=0, lds_page_heap_capacity=0, lds_narrow_overlap=0,
-                 delta_log_mode=0, live_client=0, live_group_capacity=0):
+                 delta_log_mode=0, live_client=0, live_group_capacity=0, paged_slices=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
                                 text_capacity, props_capacity, delta_log_capacity,
                                 lds_seg_capacity, page_capacity, page_heap_capacity,
                                 unsettled_capacity, uid_capacity, lds_page_capacity,
                                 lds_unsettled_capacity, lds_page_heap_capacity, lds_narrow_overlap,
-                                delta_log_mode, live_client, live_group_capacity)
+                                delta_log_mode, live_client, live_group_capacity, paged_slices)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")

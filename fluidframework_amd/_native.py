@@ -26,7 +26,7 @@ class MtOptions(ctypes.Structure):
                 ("lds_page_capacity", ctypes.c_int32), ("lds_unsettled_capacity", ctypes.c_int32),
                 ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32),
                 ("delta_log_mode", ctypes.c_int32), ("live_client", ctypes.c_int32),
-                ("live_group_capacity", ctypes.c_int32)]
+                ("live_group_capacity", ctypes.c_int32), ("paged_slices", ctypes.c_int32)]
 
 
 # mt_regen_rec (include/mt_replay.h): one op of regeneratePendingOp

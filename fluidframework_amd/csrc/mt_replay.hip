@@ -604,19 +604,30 @@ __device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t
         atomicAdd(st.stats + 12, 1u);
     }
 }
+// One launch of a sliced paged replay (mt_options.paged_slices): documents in [skip_lo,
+// skip_hi) sit this launch out, the others replay at most `ops` messages (0: all) and keep
+// their stage with resume[doc] at the next one; stats[0] counts documents in [cnt_lo, cnt_hi).
+struct PagedSlice {
+    int64_t ops;
+    int skip_lo, skip_hi, cnt_lo, cnt_hi;
+};
+
 template <class T>
 __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState st, const mt_op_rec *ops,
                                                           const int64_t *off, const uint16_t *tin,
-                                                          const uint32_t *pin, int use_resume, PagedCaps pc) {
+                                                          const uint32_t *pin, int use_resume, PagedCaps pc,
+                                                          PagedSlice sl) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
+    if (doc >= sl.skip_lo && doc < sl.skip_hi) return;
     if (st.retry[doc] != pc.stage) return;
-    if (lane() == 0) atomicAdd(st.stats, 1u);
+    if (lane() == 0 && doc >= sl.cnt_lo && doc < sl.cnt_hi) atomicAdd(st.stats, 1u);
     const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v));
-    const int64_t k1 = off[doc + 1];
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
+    const int64_t kend = off[doc + 1];
+    const int64_t k1 = sl.ops > 0 ? min(kend, k0 + sl.ops) : kend;   // this launch's last message + 1
     PagedDoc<T> pd;
     pg_setup(pd, st, doc, smem, L, pc);
     DocT<T> &w = pd.w;
@@ -710,7 +721,9 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     pg_peaks(st, pd, pk_ut, pk_heap);
     if (spill_at >= 0 && w.status == 0)
         pg_handover<T>(st, doc, spill_at);
-    else if (lane() == 0)
+    else if (k1 < kend && w.status == 0) {   // slice done: the next launch of this stage resumes
+        if (lane() == 0) st.resume[doc] = k1;
+    } else if (lane() == 0)
         st.retry[doc] = 0;
 #ifdef MT_PROF
     if (lane() < 32) atomicAdd(&g_prof[lane()], w.prof[lane()]);
@@ -1209,6 +1222,8 @@ struct mt_handle {
     TierCaps lds{0, 0, 0, 0};        // LDS-tier capacities (S == 0: tier disabled)
     PagedCaps pg_tight{0, 0, 0, 1, 1, 0};   // tight paged tier (PP == 0: off)
     PagedCaps pg_full{0, 0, 0, 0, 1, 0};    // paged tier at the HBM capacities
+    int paged_slices = 0;                   // mt_options.paged_slices
+    int pg_resident = 0;                    // documents resident at once in a tight paged launch
 };
 struct mt_batch {
     int device = 0;
@@ -1349,6 +1364,22 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
                     delete h;
                     return nullptr;
                 }
+        }
+        // documents resident at once in the first paged launch (the sliced schedule's round)
+        h->paged_slices = std::min(std::max(o.paged_slices, 0), 256);
+        if (h->paged_slices > 1) {
+            const PagedCaps &c = h->pg_tight.PP ? h->pg_tight : h->pg_full;
+            const size_t lt = paged_layout(c.PP, c.PH, c.UT, 0, c.narrow ? 4 : 8).total;
+            const void *k = st.DL ? (c.narrow ? (const void *)k_replay_paged<TierPagedT<true, true>>
+                                              : (const void *)k_replay_paged<TierPagedT<true>>)
+                                  : (c.narrow ? (const void *)k_replay_paged<TierPagedT<false, true>>
+                                              : (const void *)k_replay_paged<TierPagedT<false>>);
+            int per_cu = 0, cus = 0;
+            hipDeviceProp_t prop;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, MT_WAVE, lt) == hipSuccess &&
+                hipGetDeviceProperties(&prop, h->device) == hipSuccess)
+                cus = prop.multiProcessorCount;
+            h->pg_resident = per_cu * cus;
         }
     }
     const size_t N = n_docs;
@@ -1570,24 +1601,45 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         // first (when configured), then the full capacities for the documents it handed over
         const int use_resume = h->lds.S > 0 ? 1 : 0;
         const PagedCaps *tiers[2] = {h->pg_tight.PP ? &h->pg_tight : nullptr, &h->pg_full};
+        const int n = (int)h->n_docs;
         for (const PagedCaps *pc : tiers) {
             if (!pc) continue;
             const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, 0, pc->narrow ? 4 : 8).total;
             const int res = pc->stage == 2 ? 1 : use_resume;
             const dim3 g(h->n_docs), blk(MT_WAVE);
-            if (h->st.DL && pc->narrow)
-                hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
-                                   b->text, b->props, res, *pc);
-            else if (h->st.DL)
-                hipLaunchKernelGGL((k_replay_paged<TierPagedT<true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
-                                   b->text, b->props, res, *pc);
-            else if (pc->narrow)
-                hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true>>), g, blk, lb, h->stream, h->st, b->ops,
-                                   b->off, b->text, b->props, res, *pc);
-            else
-                hipLaunchKernelGGL((k_replay_paged<TierPagedT<false>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
-                                   b->text, b->props, res, *pc);
-            HIPCHK(h, hipGetLastError());
+            // the launches of this tier: one over every document, or (paged_slices, first
+            // tier) m slices each leaving out a window of the r = n mod resident left-over
+            // documents -- every launch is then whole rounds -- and a last one without limits
+            std::vector<PagedSlice> sls;
+            const int S = h->pg_resident, m = h->paged_slices;
+            const int r = S > 0 ? n % S : 0;
+            if (pc == tiers[0] && m > 1 && S > 0 && n > S && r > 0 && (int64_t)m * r <= n) {
+                const int64_t q = ((int64_t)b->n_ops / n + m - 1) / m;
+                for (int j = 0; j < m; j++) {
+                    PagedSlice sl{q, j * r, (j + 1) * r, 0, 0};
+                    if (j == 0) sl.cnt_lo = r, sl.cnt_hi = n;   // counted once: window 0 in launch 1
+                    if (j == 1) sl.cnt_lo = 0, sl.cnt_hi = r;
+                    sls.push_back(sl);
+                }
+                sls.push_back(PagedSlice{0, 0, 0, 0, 0});
+            } else {
+                sls.push_back(PagedSlice{0, 0, 0, 0, n});
+            }
+            for (const PagedSlice &sl : sls) {
+                if (h->st.DL && pc->narrow)
+                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops,
+                                       b->off, b->text, b->props, res, *pc, sl);
+                else if (h->st.DL)
+                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+                                       b->text, b->props, res, *pc, sl);
+                else if (pc->narrow)
+                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+                                       b->off, b->text, b->props, res, *pc, sl);
+                else
+                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<false>>), g, blk, lb, h->stream, h->st, b->ops,
+                                       b->off, b->text, b->props, res, *pc, sl);
+                HIPCHK(h, hipGetLastError());
+            }
         }
     } else if (h->live && h->st.DL)
         hipLaunchKernelGGL((k_replay<TierLiveT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),

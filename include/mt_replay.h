@@ -87,6 +87,12 @@ typedef struct mt_options {
     /* live handles: segment groups (unacked ops, one per regenerated segment after a
        reconnect) a document may have outstanding (default 1024, at most 65535) */
     int32_t live_group_capacity;
+    /* paged documents, when the batch's documents are not a whole number of resident rounds
+       (n = R x resident + r, 0 < r): replay them in `paged_slices` slices of their ops,
+       each launch leaving out a different window of r documents, so that every launch is R
+       full rounds and the r left-over documents' work is spread over all of them instead of
+       running as a last, nearly empty round (0 = off).  Results are identical. */
+    int32_t paged_slices;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

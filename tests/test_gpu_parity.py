@@ -484,6 +484,42 @@ def test_gpu_tight_tier_hands_documents_over():
         assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
 
 
+def test_gpu_sliced_paged_schedule_matches_reference():
+    """mt_options.paged_slices: more documents than one tight paged launch holds at once
+    (4 reference documents x 800 replicas = 3200 > 3072 resident), so the paged replay runs
+    as slices that each leave a window of documents out, then a last unlimited launch.  Every
+    replica's checksum equals the unsliced replay's, and sampled replicas equal the
+    reference's outputs."""
+    fx = gu.load("ref_c3_full")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    k = 800
+    nd = len(fx["docs"]) * k
+    lens = np.diff(a["doc_off"])
+    rep = dict(a)
+    rep["ops"] = np.tile(a["ops"], k)
+    rep["doc_off"] = np.concatenate([[0], np.cumsum(np.tile(lens, k))]).astype(np.int64)
+    slen = np.diff(a["seed_off"])
+    seed_off = np.concatenate([[0], np.cumsum(np.tile(slen, k))]).astype(np.int64)
+    seed = np.tile(a["seed"], k)
+    caps = dict(_bench_caps(fx))
+    sums = {}
+    for slices in (0, 8):
+        mt = _gpu_batch(nd, delta_log_capacity=0, paged_slices=slices, **caps)
+        mt.load_initial_text(seed_off, seed)
+        mt.apply_arrays(rep)
+        assert (mt.status() == 0).all()
+        sums[slices] = mt.checksums()
+        if slices:
+            for i in (0, 1, nd - 130, nd - 1):   # first / last windows and the tail
+                out = _gpu_outputs(mt, i)
+                out["deltas"] = gu.expected(fx["docs"][i % 4], interner)["deltas"]   # no log on this handle
+                assert not gu.compare_oracle(out, gu.expected(fx["docs"][i % 4], interner)), i
+        del mt
+    assert sums[0].tobytes() == sums[8].tobytes()
+    assert all(sums[8][i].tobytes() == sums[8][i % 4].tobytes() for i in range(nd))
+
+
 @pytest.mark.parametrize("uid_capacity", [65536, 16384])
 def test_gpu_long_documents_match_reference(uid_capacity):
     """30k-message documents (~45k segment ids created, ~10.5k live segments at the end):
