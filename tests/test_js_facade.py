@@ -28,6 +28,7 @@ def _addon():
     from fluidframework_amd import build
     build.build()
     build.build_snapdec()
+    build.build_node_addon()   # rebuilds when binding.cc or the libraries are newer
     if not os.path.exists(os.path.join(JS, "mtreplay.node")):
         subprocess.check_call(["sh", os.path.join(JS, "build.sh")])
 
