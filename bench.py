@@ -5,12 +5,14 @@ One *step* = replaying one batch of synthetic sequenced messages through the obs
 replicas of every document on the GPU (Client.applyMsg semantics, bit-exact with the
 reference), starting from the documents' initial contents.  The default workload is the
 one the metric is quoted on, BASELINE.json configs[2] (C3: 100k documents x 10k ops,
-8 writers, refSeq lag <= 64, insert 0.5 / remove 0.3 / annotate 0.2 with property sets,
-sharded over 8 GPUs): every rank replays its own 12,500-document shard, so N=8 is exactly
-the 100k-document job and N=1 is one GPU's share of it (weak scaling; documents are
-independent, so there is no data-path collective).  The only collective is an RCCL
-all-gather of per-document checksums after the timed region.  `--config c2` runs configs[1]
-(10k documents x 2k insert/remove ops per GPU).
+8 writers, refSeq lag <= 64, insert 0.5 / remove 0.3 / annotate 0.2 with property sets):
+the fixed 100k-document job is sharded over the ranks (contiguous shards,
+fluidframework_amd.shard.shard_range), so N=1 replays all 100k documents on one GPU and
+N=8 gives every GPU a 12.5k-document shard (strong scaling; documents are independent, so
+there is no data-path collective).  The only collective is an RCCL all-gather of
+per-document checksums after the timed region.  `--docs D` instead gives every rank D
+documents (weak scaling), `--shard r` replays shard r of the 8-way split on one GPU, and
+`--config c2` runs configs[1] (10k documents x 2k insert/remove ops per GPU).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--docs D] [--ops O]
 
@@ -31,6 +33,7 @@ sys.path.insert(0, REPO)
 HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 SEG_BYTES = 40             # segA 16 + segO 8 + segB 16
 OP_BYTES = 32              # mt_op_rec
+RESULT_BYTES = 16          # per-op result record (position, length) in B_op
 PROFILE_PMC = os.path.join(REPO, "profiles", "pmc_summary.json")
 CALIBRATION = os.path.join(REPO, "profiles", "r2", "cpu_calibration.json")
 
@@ -41,14 +44,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: config)")
+    ap.add_argument("--docs", type=int, default=0,
+                    help="documents per GPU (weak scaling; default: the config's whole job sharded over the ranks)")
     ap.add_argument("--ops", type=int, default=0, help="ops per document (default: config)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = every core this process may use)")
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="0 = all docs of rank 0")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
-    ap.add_argument("--shard", type=int, default=-1, help="document shard to replay (default: this rank)")
+    ap.add_argument("--shard", type=int, default=-1,
+                    help="replay shard r of the 8-way split of the config's job on this one GPU")
     ap.add_argument("--page-caps", default="", help="paged layout LDS capacities 'pages,unsettled,heap' (sweeps)")
     ap.add_argument("--paged-slices", type=int, default=0,
                     help="mt_options.paged_slices for paged configs (0 = off; see include/mt_replay.h)")
@@ -107,26 +112,47 @@ def oracle_checksums(cfg, global_docs, threads):
     return out
 
 
-def verify_shards(dist, rank, world, docs, cfg, local, gen_sums, device, per_rank, threads):
-    """The multi-GPU exchange step and its check.  Every rank's replay checksums (`local`:
-    a uint8 tensor filled on the device, or a CHECKSUM_DTYPE array) and generation checksums
-    are all-gathered (RCCL over xGMI with backend nccl); rank 0 then checks that the timed
+def verify_shards(dist, rank, world, n_total, cfg, local, gen_sums, device, per_rank, threads):
+    """The multi-GPU exchange step and its check.  Rank r owns the global documents
+    shard_range(n_total, world, r).  Every rank's replay checksums (`local`: a uint8 tensor
+    filled on the device, or a CHECKSUM_DTYPE array) and generation checksums are
+    all-gathered (RCCL over xGMI with backend nccl); rank 0 then checks that the timed
     replay reproduced the generation for every document of every shard, and that
     `per_rank` documents of every shard equal the CPU oracle's replay of the same global
     documents.  Returns the report on rank 0, None elsewhere."""
-    from fluidframework_amd.shard import digest, gather_checksums
-    n_total = docs * world
+    from fluidframework_amd.shard import digest, gather_checksums, shard_range
     got = gather_checksums(local, dist, device=device, n_total=n_total)
     gen = gather_checksums(gen_sums, dist, device=device, n_total=n_total)
     if rank != 0:
         return None
-    pick = sorted({int(x) for x in np.linspace(0, docs - 1, num=max(1, min(per_rank, docs)))})
-    gdocs = [r * docs + i for r in range(world) for i in pick]
+    gdocs = []
+    for r in range(world):
+        lo, hi = shard_range(n_total, world, r)
+        if hi > lo:
+            gdocs += sorted({lo + int(x) for x in np.linspace(0, hi - lo - 1, num=max(1, min(per_rank, hi - lo)))})
     orc = oracle_checksums(cfg, gdocs, threads) if per_rank > 0 else None
     mism = int(sum(got[g] != orc[j] for j, g in enumerate(gdocs))) if orc is not None else None
     return dict(docs_gathered=int(len(got)), replay_equals_generation=bool(np.array_equal(got, gen)),
                 oracle_docs=len(gdocs) if orc is not None else 0, oracle_mismatches=mism,
                 digest=digest(got))
+
+
+def shard_plan(args, cfg, world, rank):
+    """(documents on this rank, first global document, documents in the whole job,
+    scaling).  Default: the config's whole job split over the ranks (strong scaling; C2 is
+    a single-GPU configuration, so it stays per GPU); `--docs D`: D per rank (weak);
+    `--shard r`: shard r of the job's 8-way split, on one GPU."""
+    from fluidframework_amd.shard import shard_range
+    if args.docs:
+        return args.docs, rank * args.docs, args.docs * world, "weak"
+    if args.config == "c2":
+        return cfg["docs"], rank * cfg["docs"], cfg["docs"] * world, "weak"
+    total = cfg["docs"] if args.config == "c3" else min(cfg["docs"], 16384)
+    if args.shard >= 0:
+        lo, hi = shard_range(total, 8, args.shard)
+        return hi - lo, lo, hi - lo, "weak"
+    lo, hi = shard_range(total, world, rank)
+    return hi - lo, lo, total, "strong"
 
 
 def capacities(cfg, tight=True):
@@ -449,11 +475,9 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    # per-GPU shard: C2 is a single-GPU config; C3's 100k documents shard over 8 GPUs
-    docs = args.docs or {"c2": cfg["docs"], "c3": cfg["docs"] // 8}.get(args.config, min(cfg["docs"], 16384))
+    docs, doc_base, docs_total, scaling = shard_plan(args, cfg, world, rank)
     if args.ops:
         cfg["ops"] = args.ops
-    doc_base = (args.shard if args.shard >= 0 else rank) * docs
 
     caps = capacities(cfg)
     if args.lds_cap:
@@ -503,6 +527,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        t = torch.tensor([n_ops], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)                # shards may differ by one document
+        total_ops = int(t.item())
+    else:
+        total_ops = n_ops
 
     hbm_docs = mt.last_hbm_docs()
     peaks = mt.last_paged_peaks() if "page_capacity" in caps else None
@@ -517,7 +546,7 @@ def main():
         import torch
         local = torch.empty(docs * 32, dtype=torch.uint8, device="cuda")
         mt.checksums_device(local.data_ptr())
-        shards = verify_shards(dist, rank, world, docs, cfg, local, gen_sums, torch.device("cuda", local_rank),
+        shards = verify_shards(dist, rank, world, docs_total, cfg, local, gen_sums, torch.device("cuda", local_rank),
                                args.verify_per_rank, threads)
         ok = torch.tensor([1 if replay_consistent else 0], device="cuda")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -530,7 +559,6 @@ def main():
             dist.destroy_process_group()
         return
 
-    total_ops = n_ops * world
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_ops * args.steps / elapsed
 
@@ -539,14 +567,14 @@ def main():
     ins = host["ops"]["kind"] == 0
     payload_chars = int(host["ops"]["pos2"][ins].sum())
     final_bytes = int(sums["n_segments"].astype(np.int64).sum()) * SEG_BYTES + 2 * int(sums["length"].astype(np.int64).sum())
-    alg_bytes = n_ops * OP_BYTES + 2 * payload_chars + final_bytes
+    alg_bytes = n_ops * (OP_BYTES + RESULT_BYTES) + 2 * payload_chars + final_bytes
     k_ms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (k_ms / 1000.0)
     traffic = None
     if os.path.exists(PROFILE_PMC):
         try:
             pm = json.load(open(PROFILE_PMC)).get(args.config, {})
-            if pm.get("docs") == docs and pm.get("ops") == cfg["ops"]:
+            if pm.get("docs") == docs and pm.get("ops") == cfg["ops"] and pm.get("seed_base", 0) == doc_base:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -597,7 +625,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -605,7 +633,7 @@ def main():
             "workload": f"{args.config}: {docs} docs/GPU x {cfg['ops']} sequenced ops, {cfg['writers']} writers, "
                         f"refSeq lag <= {cfg['lag']}, insert {cfg['p_insert']} / remove {cfg['p_remove']}"
                         f"{' / annotate ' + str(round(1 - cfg['p_insert'] - cfg['p_remove'], 3)) if cfg['p_insert'] + cfg['p_remove'] < 1 else ''}",
-            "docs_total": docs * world, "ops_per_doc": cfg["ops"], "ops_per_step": total_ops,
+            "docs_total": docs_total, "docs_per_gpu": docs, "ops_per_doc": cfg["ops"], "ops_per_step": total_ops,
             "parallelism": f"doc-shard x{world}",
         },
         "roofline": {

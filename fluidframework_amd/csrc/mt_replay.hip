@@ -1625,7 +1625,17 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
             } else {
                 sls.push_back(PagedSlice{0, 0, 0, 0, n});
             }
+            // a sliced tier resumes every launch after its first from resume[doc]; without
+            // the LDS tier nothing has written it yet, so seed it with each document's first
+            // message and resume from the first launch on (a slice must never restart at off)
+            int res_k = res;
+            if (sls.size() > 1 && !res) {
+                HIPCHK(h, hipMemcpyAsync(h->st.resume, b->off, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToDevice,
+                                         h->stream));
+                res_k = 1;
+            }
             for (const PagedSlice &sl : sls) {
+                const int res = res_k;
                 if (h->st.DL && pc->narrow)
                     hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops,
                                        b->off, b->text, b->props, res, *pc, sl);

@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -79,12 +80,35 @@ struct Blob {
     }
     double num(uint32_t i) const {   // JS Number of the lexeme (locale-independent)
         double x = 0;
-        std::from_chars(src + nodes[i].off, src + nodes[i].off + nodes[i].len, x);
+        const char *b = src + nodes[i].off, *e = b + nodes[i].len;
+        const auto r = std::from_chars(b, e, x);
+        if (r.ec == std::errc::result_out_of_range) {
+            // JSON.parse / json.loads: overflow is +-Infinity, underflow +-0
+            bool big = false;
+            for (const char *q = b; q < e; q++)
+                if (*q == 'e' || *q == 'E') {
+                    big = q + 1 < e && q[1] != '-';
+                    break;
+                }
+            if (!big) {   // no exponent or a positive one: too many digits, i.e. overflow
+                bool has_e = false;
+                for (const char *q = b; q < e; q++) has_e |= (*q == 'e' || *q == 'E');
+                big = !has_e;
+            }
+            const bool neg = *b == '-';
+            x = big ? (neg ? -HUGE_VAL : HUGE_VAL) : (neg ? -0.0 : 0.0);
+        }
         return x;
     }
     int64_t as_int(uint32_t i) const {
         if (i == NONE || nodes[i].t != Node::NUM) return 0;
-        if (!is_int(i) || nodes[i].len > 18) return (int64_t)num(i);
+        if (!is_int(i) || nodes[i].len > 18) {   // clamp before the cast (out of range is UB)
+            const double x = num(i);
+            if (!(x == x)) return 0;
+            if (x >= 9.2e18) return INT64_MAX;
+            if (x <= -9.2e18) return INT64_MIN;
+            return (int64_t)x;
+        }
         const char *p = src + nodes[i].off;
         const bool neg = *p == '-';
         int64_t v = 0;
@@ -171,18 +195,27 @@ struct Reader {
                 continue;
             }
             if (c < 0x20) return fail("control character in string");
+            // UTF-8 -> UTF-16 as the reference's Buffer.toString("utf8") (fromBase64ToUtf8):
+            // each maximal ill-formed subsequence becomes one U+FFFD, and the byte that ends it
+            // is read again (WHATWG "UTF-8 decode"; overlong forms, encoded surrogates and code
+            // points above U+10FFFF are ill-formed)
             uint32_t cp;
             int n;
-            if ((c & 0xE0) == 0xC0) { cp = c & 0x1F; n = 1; }
-            else if ((c & 0xF0) == 0xE0) { cp = c & 0x0F; n = 2; }
-            else if ((c & 0xF8) == 0xF0) { cp = c & 0x07; n = 3; }
-            else return fail("bad UTF-8");
+            unsigned lo = 0x80, hi = 0xBF;
+            if (c >= 0xC2 && c <= 0xDF) { cp = c & 0x1F; n = 1; }
+            else if (c >= 0xE0 && c <= 0xEF) { cp = c & 0x0F; n = 2; lo = c == 0xE0 ? 0xA0 : 0x80; hi = c == 0xED ? 0x9F : 0xBF; }
+            else if (c >= 0xF0 && c <= 0xF4) { cp = c & 0x07; n = 3; lo = c == 0xF0 ? 0x90 : 0x80; hi = c == 0xF4 ? 0x8F : 0xBF; }
+            else { p++; o.push_back(u'\uFFFD'); continue; }
             p++;
-            if (e - p < n) return fail("bad UTF-8");
-            for (int i = 0; i < n; i++, p++) {
-                if (((unsigned char)*p & 0xC0) != 0x80) return fail("bad UTF-8");
-                cp = (cp << 6) | ((unsigned char)*p & 0x3F);
+            bool ok = true;
+            for (int i = 0; i < n; i++) {
+                const unsigned x = p < e ? (unsigned char)*p : 0;
+                if (p >= e || x < lo || x > hi) { ok = false; break; }
+                lo = 0x80, hi = 0xBF;
+                cp = (cp << 6) | (x & 0x3F);
+                p++;
             }
+            if (!ok) { o.push_back(u'\uFFFD'); continue; }
             if (cp >= 0x10000) {
                 cp -= 0x10000;
                 o.push_back((char16_t)(0xD800 + (cp >> 10)));
@@ -359,6 +392,10 @@ void canon(std::string &o, const Blob &B, uint32_t i) {
                 else o.append(B.src + v.off, v.len);
             } else {   // JS Number: 1.0, 1e0 and 1 are one value
                 const double x = B.num(i);
+                if (std::isinf(x)) {   // json.loads reads these back (JSON.parse gave Infinity)
+                    o += x > 0 ? "Infinity" : "-Infinity";
+                    break;
+                }
                 char b[400];
                 const auto r = std::isfinite(x) && x == std::floor(x) && std::fabs(x) < 1e21
                                    ? std::to_chars(b, b + sizeof b, x == 0 ? 0.0 : x, std::chars_format::fixed, 0)
@@ -712,8 +749,22 @@ const char *mt_snapdec_error(const mt_snapdec *s) { return s ? s->err.c_str() : 
 
 int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, const char *const *paths,
                       const uint32_t *path_len, const char *const *json, const uint64_t *json_len, int threads) {
-    if (!s || !blob_off || (blob_off[n_docs] > 0 && (!paths || !path_len || !json || !json_len))) return -1;
+    if (!s || !blob_off) return -1;
     s->err.clear();
+    // offsets: monotonic from 0 (each document's blobs are [blob_off[d], blob_off[d+1]))
+    if (blob_off[0] != 0) {
+        s->err = "blob_off[0] must be 0";
+        return -1;
+    }
+    for (uint32_t d = 0; d < n_docs; d++)
+        if (blob_off[d + 1] < blob_off[d]) {
+            s->err = "blob_off must be non-decreasing (document " + std::to_string(d) + ")";
+            return -1;
+        }
+    if (blob_off[n_docs] > 0 && (!paths || !path_len || !json || !json_len)) {
+        s->err = "null blob arrays";
+        return -1;
+    }
     if (s->docs.size() < n_docs) s->docs.resize(n_docs);
     const int nt = std::max(1, std::min({threads, 256, (int)std::max<uint32_t>(n_docs, 1)}));
     if ((int)s->workers.size() < nt) s->workers.resize((size_t)nt);
@@ -726,7 +777,13 @@ int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, c
         for (;;) {
             const uint32_t d0 = next.fetch_add(8);
             if (d0 >= n_docs) break;
-            for (uint32_t d = d0; d < std::min(n_docs, d0 + 8); d++) w.build(s->docs[d], d, in);
+            for (uint32_t d = d0; d < std::min(n_docs, d0 + 8); d++) {
+                try {
+                    w.build(s->docs[d], d, in);
+                } catch (const std::exception &ex) {   // e.g. bad_alloc: the document's error
+                    s->docs[d].err = std::string("decode failed: ") + ex.what();
+                }
+            }
         }
     };
     std::vector<std::thread> pool;

@@ -484,7 +484,16 @@ napi_value DecodeSummaries(napi_env env, napi_callback_info info) {
         double x = 0;
         NAPI_CALL(env, napi_get_element(env, argv[2], i, &v));
         NAPI_CALL(env, napi_get_value_double(env, v, &x));
+        // integers in [0, blobs.length] only (a NaN or out-of-range double is UB to cast)
+        if (!(x >= 0 && x <= (double)nb) || x != (double)(int64_t)x) {
+            napi_throw_range_error(env, nullptr, "decodeSummaries: docBlobOff entries must be integers in [0, blobs.length]");
+            return nullptr;
+        }
         off[i] = (int64_t)x;
+        if (i > 0 && off[i] < off[i - 1]) {
+            napi_throw_range_error(env, nullptr, "decodeSummaries: docBlobOff must be non-decreasing");
+            return nullptr;
+        }
     }
     const uint32_t nd = nd1 - 1;
     if (off[0] != 0 || off[nd] != (int64_t)nb) {

@@ -81,6 +81,28 @@ class Interner {
         this.keyIds = new Map();
         this.vals = [];
         this.valIds = new Map();
+        // the values each key can hold (ids without flag bits), for combining-op tables
+        // (wire.py Interner.note / held_values)
+        this.keyVals = new Map();
+        this.unkeyed = new Set();
+    }
+    note(kid, vid) {
+        if (vid === VAL_NULL || vid === VAL_UNDEF) { return; }
+        let s = this.keyVals.get(kid);
+        if (s === undefined) { s = new Set(); this.keyVals.set(kid, s); }
+        s.add((vid & 0x3FFFFFFF) >>> 0);
+    }
+    noteUnkeyed(vid) {
+        if (vid === VAL_NULL || vid === VAL_UNDEF) { return; }
+        this.unkeyed.add((vid & 0x3FFFFFFF) >>> 0);
+    }
+    heldValues(kids) {
+        const out = new Set(this.unkeyed);
+        for (const k of kids) {
+            const s = this.keyVals.get(k);
+            if (s !== undefined) { for (const v of s) { out.add(v); } }
+        }
+        return Array.from(out).sort((a, b) => a - b);
     }
     key(k) {
         let i = this.keyIds.get(k);
@@ -156,29 +178,39 @@ class BatchEncoder {
         const keys = Object.keys(p);
         this.props.push((keys.length | (combine << 16)) >>> 0);
         for (const k of keys) {
-            this.props.push(this.interner.key(k));
-            this.props.push(this.interner.val(p[k]));
+            const kid = this.interner.key(k), vid = this.interner.val(p[k]);
+            this.interner.note(kid, vid);
+            this.props.push(kid);
+            this.props.push(vid);
         }
         return off;
     }
 
     /**
      * A non-rewrite combining op's record (SURVEY Q4): the keys, then combine(op, old,
-     * undefined, seq) for every value a key can hold now -- [n, new value of an absent key,
+     * undefined, seq) for every value one of its keys can hold now (Interner.heldValues) -- [n, new value of an absent key,
      * (old, new) x n]; VAL_NULL deletes.  Mirrors wire.py Batch._combine_rec.
      */
     _combineProps(p, comb, seq) {
         const it = this.interner;
+        const kids = Object.keys(p).map((k) => it.key(k));
         let absent;
         const pairs = [];
         try {
             absent = it.val(jsCombine(comb, undefined, seq));
-            for (const v of it.vals.slice()) { pairs.push([it.val(v), it.val(jsCombine(comb, v, seq))]); }
+            for (const i of it.heldValues(kids)) {
+                const v = it.vals[i];
+                pairs.push([it.val(v), it.val(jsCombine(comb, v, seq))]);
+            }
         } catch (e) {
             if (!(e instanceof Unsupported)) { throw e; }
             return this._props(p, COMBINE_OTHER);
         }
         const off = this._props(p, COMBINE_TABLE);
+        for (const kid of kids) {
+            it.note(kid, absent);
+            for (const [, n] of pairs) { it.note(kid, n); }
+        }
         this.props.push(pairs.length);
         this.props.push(absent);
         for (const [o, n] of pairs) { this.props.push(o); this.props.push(n); }

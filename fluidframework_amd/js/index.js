@@ -60,6 +60,7 @@ function decodeSummaries(summaries, interner, threads = 8) {
     const a = native.decodeSummaries(paths, blobs, off, threads);
     const km = a.keys.map((k) => interner.key(k));
     const vm = a.vals.map((v) => (interner.val(JSON.parse(v)) & 0x3FFFFFFF) >>> 0);
+    for (const v of vm) { interner.noteUnkeyed(v); }   // held by some key of a loaded summary
     const dv = new DataView(a.segs.buffer, a.segs.byteOffset, a.segs.byteLength);
     const p = a.props;
     for (let r = 0; r < a.segs.byteLength; r += 32) {

@@ -96,8 +96,10 @@ class SnapshotEncoder {
         const keys = Object.keys(p);
         this.props.push(keys.length >>> 0);
         for (const k of keys) {
-            this.props.push(this.interner.key(k));
-            this.props.push(this.interner.val(p[k]));
+            const kid = this.interner.key(k), vid = this.interner.val(p[k]);
+            this.interner.note(kid, vid);
+            this.props.push(kid);
+            this.props.push(vid);
         }
         return off;
     }

@@ -121,6 +121,7 @@ class SummaryDecoder:
             self._kmap.append(it.key(_text(lib.mt_snapdec_key, self.h, i)))
         for i in range(len(self._vmap), lib.mt_snapdec_num_values(self.h)):
             self._vmap.append(it.val(json.loads(_text(lib.mt_snapdec_value, self.h, i))) & (VAL_FALSY_BIT - 1))
+            it.note_unkeyed(self._vmap[-1])   # held by some key of a loaded summary
         km, vm = np.asarray(self._kmap, dtype=np.uint32), np.asarray(self._vmap, dtype=np.uint32)
         if np.array_equal(km, np.arange(len(km))) and np.array_equal(vm, np.arange(len(vm))):
             return

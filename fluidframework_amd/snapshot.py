@@ -93,12 +93,19 @@ class SnapshotDoc:
         self.catchup = list(catchup)
 
 
+def _blob_text(v):
+    """A blob's bytes as the JS string the reference parses: fromBase64ToUtf8 is
+    Buffer.toString("utf8"), which replaces every maximal ill-formed subsequence by U+FFFD --
+    the same rule as Python's "replace" handler."""
+    return v.decode("utf-8", errors="replace") if isinstance(v, (bytes, bytearray)) else v
+
+
 def decode_chunks(chunks):
     """SnapshotLoader.initialize (MT/snapshotLoader.ts:36-84, 120-228) over blob contents
     (JSON text; the reference base64-decodes first, MT/snapshotV1.ts:274)."""
     if HEADER not in chunks:
         raise SnapshotError("header blob missing")
-    header = to_latest_version(HEADER, json.loads(chunks[HEADER]))
+    header = to_latest_version(HEADER, json.loads(_blob_text(chunks[HEADER])))
     meta = header.get("headerMetadata")
     if meta is None:
         raise SnapshotError("header metadata not available")
@@ -108,7 +115,7 @@ def decode_chunks(chunks):
     ordered = meta["orderedChunkMetadata"]
     if header["segmentCount"] != meta["totalSegmentCount"]:        # loadBody :170-172
         for md in ordered[1:]:
-            ch = to_latest_version(md["id"], json.loads(chunks[md["id"]]))
+            ch = to_latest_version(md["id"], json.loads(_blob_text(chunks[md["id"]])))
             body += ch["segments"]
     catchup = []
     blobs = list(chunks)
@@ -116,7 +123,7 @@ def decode_chunks(chunks):
         rest = [b for b in blobs if b not in {m["id"] for m in ordered}]
         if len(rest) != 1:
             raise SnapshotError(f"There should be only one blob with catch up ops: {len(rest)}")
-        catchup = json.loads(chunks[rest[0]])
+        catchup = json.loads(_blob_text(chunks[rest[0]]))
     elif len(blobs) != len(ordered):
         raise SnapshotError("Unexpected blobs in snapshot")
     return SnapshotDoc(header["segments"], body, msn, seq, catchup)
@@ -153,8 +160,10 @@ class SnapshotBatch:
         items = list(props.items())
         self.props.append(len(items))
         for k, v in items:
-            self.props.append(self.interner.key(k))
-            self.props.append(self.interner.val(v))
+            kid, vid = self.interner.key(k), self.interner.val(v)
+            self.interner.note(kid, vid)
+            self.props.append(kid)
+            self.props.append(vid)
         return off
 
     def _rec(self, spec, short):

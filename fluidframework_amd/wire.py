@@ -17,6 +17,7 @@ VAL_NULL = 0xFFFFFFFF
 VAL_UNDEF = 0xFFFFFFFE          # a key set to the JS value undefined
 VAL_FALSY_BIT = 0x80000000
 VAL_NOMATCH_BIT = 0x40000000    # matchProperties never finds the value equal (NaN, undefined inside)
+VAL_ID_MASK = 0x3FFFFFFF
 COMBINE_NONE, COMBINE_REWRITE, COMBINE_OTHER, COMBINE_TABLE = 0, 1, 2, 3
 
 OP_DTYPE = np.dtype([
@@ -74,7 +75,10 @@ def _has_js_value(v):
 
 def _js_number(x):
     """A number as a JS Number (one double type: 1, 1.0 and 1e0 are the same value)."""
-    f = float(x)
+    try:
+        f = float(x)
+    except OverflowError:          # an integer lexeme beyond the double range: +-Infinity
+        f = float("inf") if x > 0 else float("-inf")
     if f.is_integer() and abs(f) < 1e21:
         return str(int(f))
     return repr(f)
@@ -169,6 +173,24 @@ class Interner:
         self.keys, self.key_ids = [], {}
         self.vals, self.val_ids = [], {}
         self.synthetic = synthetic
+        # the values each key can hold (ids without flag bits), for combining-op tables:
+        # every (key, value) written by a record, plus values of unknown key (decoded summaries)
+        self.key_vals, self.unkeyed = {}, set()
+
+    def note(self, kid, vid):
+        if not self.synthetic and vid not in (VAL_NULL, VAL_UNDEF):
+            self.key_vals.setdefault(kid, set()).add(vid & VAL_ID_MASK)
+
+    def note_unkeyed(self, vid):
+        if not self.synthetic and vid not in (VAL_NULL, VAL_UNDEF):
+            self.unkeyed.add(vid & VAL_ID_MASK)
+
+    def held_values(self, kids):
+        """Ids of every value one of the keys `kids` can hold, ascending."""
+        out = set(self.unkeyed)
+        for k in kids:
+            out |= self.key_vals.get(k, set())
+        return sorted(out)
 
     def key(self, k):
         if self.synthetic:
@@ -241,28 +263,37 @@ class Batch:
         items = list(props.items())
         self.props.append(len(items) | (combine << 16))
         for k, v in items:
-            self.props.append(self.interner.key(k))
-            self.props.append(self.interner.val(v))
+            kid, vid = self.interner.key(k), self.interner.val(v)
+            self.interner.note(kid, vid)
+            self.props.append(kid)
+            self.props.append(vid)
         return off
 
     def _combine_rec(self, props, comb, seq):
         """A non-rewrite combining op's record: the keys, then the transform of
-        every value a key can hold at this point -- [n, new value of an absent key,
-        (old, new) x n] -- as combine(op, old, undefined, seq) yields it; new = VAL_NULL
-        deletes the key.  Unsupported results (the reference throws, or mutates a shared
-        value) keep COMBINE_OTHER: the document fails with MT_DOC_UNSUPPORTED."""
+        every value one of the op's keys can hold at this point (Interner.held_values: the
+        values written under those keys so far, plus decoded summaries' values) --
+        [n, new value of an absent key, (old, new) x n] -- as combine(op, old, undefined, seq)
+        yields it; new = VAL_NULL deletes the key.  The results become values those keys can
+        hold.  Unsupported results (the reference throws, or mutates a shared value) keep
+        COMBINE_OTHER: the document fails with MT_DOC_UNSUPPORTED."""
         it = self.interner
         if it.synthetic:
             return self._props_rec(props, COMBINE_OTHER)
+        kids = [it.key(k) for k in props]
         try:
             absent = it.val(js_combine(comb, UNDEF, seq))
             pairs = []
-            for i, v in enumerate(list(it.vals)):
-                old = it.val(v)
-                pairs.append((old, it.val(js_combine(comb, v, seq))))
+            for i in it.held_values(kids):
+                v = it.vals[i]
+                pairs.append((it.val(v), it.val(js_combine(comb, v, seq))))
         except Unsupported:
             return self._props_rec(props, COMBINE_OTHER)
         off = self._props_rec(props, COMBINE_TABLE)
+        for kid in kids:
+            it.note(kid, absent)
+            for _, n in pairs:
+                it.note(kid, n)
         self.props.append(len(pairs))
         self.props.append(absent)
         for o, n in pairs:

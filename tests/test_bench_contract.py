@@ -24,8 +24,31 @@ def test_default_workload_is_the_metric_config(bench, monkeypatch):
     args = bench.parse()
     assert args.config == "c3" and args.gpus == 1
     cfg = _configs()["c3"]
-    # 100k documents over 8 GPUs: each rank replays a 12.5k-document shard
-    assert cfg["docs"] == 100000 and cfg["docs"] // 8 == 12500 and cfg["ops"] == 10000
+    assert cfg["docs"] == 100000 and cfg["ops"] == 10000
+    # the metric's fixed 100k-document job: all of it on one GPU, 12.5k-document shards on 8
+    assert bench.shard_plan(args, cfg, 1, 0) == (100000, 0, 100000, "strong")
+    assert bench.shard_plan(args, cfg, 8, 3) == (12500, 37500, 100000, "strong")
+    plans = [bench.shard_plan(args, cfg, 3, r) for r in range(3)]
+    assert sum(p[0] for p in plans) == 100000 and [p[1] for p in plans] == [0, 33334, 66667]
+    # --docs D: D per rank (weak scaling); --shard r: one shard of the 8-way split on one GPU
+    monkeypatch.setattr("sys.argv", ["bench.py", "--docs", "2048"])
+    assert bench.shard_plan(bench.parse(), cfg, 4, 2) == (2048, 4096, 8192, "weak")
+    monkeypatch.setattr("sys.argv", ["bench.py", "--shard", "7"])
+    assert bench.shard_plan(bench.parse(), cfg, 1, 0) == (12500, 87500, 12500, "weak")
+
+
+def test_gpurun_ignore_keeps_transpiled_reference_home():
+    """The transpiled reference (oracle/_ref, built in this container) must never be pushed to
+    the GPU box: tar's exclude patterns as gpurun applies them leave none of it in the tree."""
+    import subprocess
+    ref = os.path.join(REPO, "oracle", "_ref")
+    if not os.path.isdir(ref):
+        pytest.skip("oracle/_ref not built here")
+    out = subprocess.run(["tar", "--exclude=./.git", "--exclude-from=.gpurunignore", "-cf", "-",
+                          "./oracle"], cwd=REPO, capture_output=True, check=True).stdout
+    names = subprocess.run(["tar", "-t"], input=out, capture_output=True, check=True).stdout.decode()
+    assert "oracle/ref_harness.mjs" in names
+    assert not [n for n in names.split() if "oracle/_ref" in n]
 
 
 def test_paged_capacities_tight_then_full(bench):
@@ -45,7 +68,7 @@ def test_paged_capacities_tight_then_full(bench):
 def test_recorded_traffic_matches_default_workload():
     pm = json.load(open(os.path.join(REPO, "profiles", "pmc_summary.json")))
     e = pm["c3"]
-    assert e["docs"] == 12500 and e["ops"] == 10000 and e["hbm_bytes_per_launch"] > 0
+    assert e["docs"] == 100000 and e["ops"] == 10000 and e["hbm_bytes_per_launch"] > 0
     src = os.path.join(REPO, e["note"].split("source ")[-1])
     assert os.path.exists(src)
 

@@ -484,12 +484,15 @@ def test_gpu_tight_tier_hands_documents_over():
         assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), i
 
 
-def test_gpu_sliced_paged_schedule_matches_reference():
+@pytest.mark.parametrize("lds_tier", [True, False])
+def test_gpu_sliced_paged_schedule_matches_reference(lds_tier):
     """mt_options.paged_slices: more documents than one tight paged launch holds at once
     (4 reference documents x 800 replicas = 3200 > 3072 resident), so the paged replay runs
     as slices that each leave a window of documents out, then a last unlimited launch.  Every
     replica's checksum equals the unsliced replay's, and sampled replicas equal the
-    reference's outputs."""
+    reference's outputs.  Without the LDS tier (lds_seg_capacity -1) nothing has set the
+    documents' resume points before the first slice: every slice after it must still resume,
+    not restart."""
     fx = gu.load("ref_c3_full")
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
@@ -503,6 +506,8 @@ def test_gpu_sliced_paged_schedule_matches_reference():
     seed_off = np.concatenate([[0], np.cumsum(np.tile(slen, k))]).astype(np.int64)
     seed = np.tile(a["seed"], k)
     caps = dict(_bench_caps(fx))
+    if not lds_tier:
+        caps["lds_seg_capacity"] = -1
     sums = {}
     for slices in (0, 8):
         mt = _gpu_batch(nd, delta_log_capacity=0, paged_slices=slices, **caps)

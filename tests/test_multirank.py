@@ -61,7 +61,7 @@ def _bench_worker(rank, world, port, q, corrupt_rank):
     gen = local.copy()
     if rank == corrupt_rank:
         local[1]["text_hash"] ^= np.uint64(1)
-    rep = bench.verify_shards(dist, rank, world, per, cfg, local, gen, None, per, 2)
+    rep = bench.verify_shards(dist, rank, world, per * world, cfg, local, gen, None, per, 2)
     if rank == 0:
         q.put(rep)
     dist.barrier()

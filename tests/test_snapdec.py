@@ -96,6 +96,9 @@ def test_native_decoder_json_details():
                         {"text": "n", "props": {"a": 0.1, "b": 1e300, "c": 12345678901234567890123, "d": 1e21,
                                                 "e": 99999999999999999, "f": -2.5e-7, "g": 100000000000000000}}]}
     raw = json.dumps(hdr).replace('"x": 0}', '"x": 0, "x": 2.5}').replace('"y": 1.0', '"y": 1e0, "w": -0.0')
+    # out-of-range lexemes: JSON.parse / json.loads give +-Infinity and +-0
+    raw = raw.replace('"g": 100000000000000000', '"g": 100000000000000000, "h": 1e400, "i": -1e400, '
+                      '"j": 1e-400, "k": 123456789e999, "l": 1' + '0' * 400)
     _check([{"header": raw}])
     _check([{"header": raw}, {"header": json.dumps(hdr, ensure_ascii=False)}], threads=2)
     ni = Interner()
@@ -140,8 +143,7 @@ def test_native_decoder_errors():
     with pytest.raises(SnapshotError):
         dec.decode([{"header": '{"version": "1", '}])
     for bad in ('{"version": "1", "x": 01}', '{"version": "1", "x": 1.}', '{"version": "1", "x": 1e}',
-                '{"version": "1", "x": -}', '{"version": "1", "x": 1-2}', b'{"version": "1", "x": "\xc3("}',
-                b'{"version": "1", "x": "\x01"}'):
+                '{"version": "1", "x": -}', '{"version": "1", "x": 1-2}', b'{"version": "1", "x": "\x01"}'):
         with pytest.raises(SnapshotError):   # JSON.parse throws on each of these
             dec.decode([{"header": bad}])
         with pytest.raises(ValueError):
@@ -149,3 +151,35 @@ def test_native_decoder_errors():
     ok = snapdec.SummaryDecoder(Interner(), threads=100000)   # thread count is capped
     ok.decode([{"header": '{"version": "1", "segmentCount": 0, "segments": [], "headerMetadata": '
                           '{"orderedChunkMetadata": [{"id": "header"}], "sequenceNumber": 3, "totalSegmentCount": 0}}'}])
+
+
+def test_native_decoder_rejects_bad_blob_offsets():
+    """Document blob offsets must start at 0 and never decrease ([0, 10, 2] used
+    to read past the blob tables)."""
+    dec = snapdec.SummaryDecoder(Interner())
+    hdr = ('{"version": "1", "segmentCount": 0, "segments": [], "headerMetadata": '
+           '{"orderedChunkMetadata": [{"id": "header"}], "sequenceNumber": 3, "totalSegmentCount": 0}}')
+    paths, blobs, off = dec.pack([{"header": hdr}, {"header": hdr}])
+    assert off == [0, 1, 2]
+    for bad in ([0, 2, 1], [1, 1, 2], [0, 3, 2]):
+        with pytest.raises(SnapshotError, match="blob_off"):
+            dec.decode_packed(paths, blobs, bad)
+    out, cu = dec.decode_packed(paths, blobs, off)
+    assert list(out["cur_seq"]) == [3, 3]
+
+
+@pytest.mark.parametrize("bad", [b"\xc3(", b"\xc0\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xe0\x80\xaf",
+                                 b"\xf0\x9f\x98", b"\xff", b"a\xe2\x82", b"\xf8\x88\x80\x80\x80"])
+def test_native_decoder_ill_formed_utf8_as_buffer_tostring(bad):
+    """Ill-formed UTF-8 inside blob strings (a truncated sequence, overlong forms, encoded
+    surrogates, code points above U+10FFFF, stray bytes): the reference turns the blob into a
+    string with Buffer.toString("utf8") (fromBase64ToUtf8), one U+FFFD per maximal ill-formed
+    subsequence, then parses it; the native decoder gives the same segment text as the
+    restatement (bytes.decode("utf-8", "replace"), the same rule)."""
+    hdr = ('{"version": "1", "segmentCount": 1, "length": 1, "headerMetadata": {"orderedChunkMetadata": '
+           '[{"id": "header"}], "sequenceNumber": 3, "totalSegmentCount": 1, "totalLength": 1}, '
+           '"segments": [{"text": "<X>"}]}').encode()
+    raw = hdr.replace(b"<X>", b"q" + bad + b"z")
+    _check([{"header": raw}])
+    text = decode_chunks({"header": raw}).header_specs[0]["text"]
+    assert "\ufffd" in text and text.startswith("q") and text.endswith("z")
