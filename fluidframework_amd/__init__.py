@@ -35,14 +35,15 @@ class MergeTreeBatch:
                  text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0,
                  page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0,
                  lds_page_capacity=0, lds_unsettled_capacity=0, lds_page_heap_capacity=0, lds_narrow_overlap=0,
-                 delta_log_mode=0, live_client=0, live_group_capacity=0, paged_slices=0):
+                 delta_log_mode=0, live_client=0, live_group_capacity=0, paged_slices=0, segment_ordinals=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
                                 text_capacity, props_capacity, delta_log_capacity,
                                 lds_seg_capacity, page_capacity, page_heap_capacity,
                                 unsettled_capacity, uid_capacity, lds_page_capacity,
                                 lds_unsettled_capacity, lds_page_heap_capacity, lds_narrow_overlap,
-                                delta_log_mode, live_client, live_group_capacity, paged_slices)
+                                delta_log_mode, live_client, live_group_capacity, paged_slices,
+                                segment_ordinals)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")
@@ -255,6 +256,47 @@ class MergeTreeBatch:
         if n.value < 0:
             return None
         return [(int(pairs[2 * j]), int(pairs[2 * j + 1])) for j in range(n.value)]
+
+    # -------------------------------------------------------------- segment read-outs
+    @staticmethod
+    def _seg_info(info, text):
+        if info.row < 0:
+            return None
+        out = dict(row=info.row, uid=info.uid, position=info.position, offset=info.offset, length=info.length,
+                   seq=info.seq, client=info.client, removed_seq=info.removed_seq,
+                   removed_client=info.removed_client, marker_ref_type=info.marker_ref_type,
+                   ordinal=list(info.ordinal[:info.ordinal_len]) if info.ordinal_len >= 0 else None)
+        if info.marker_ref_type < 0:
+            out["text"] = text[:info.text_len].tobytes().decode("utf-16-le", errors="surrogatepass")
+        return out
+
+    def get_containing_segment(self, doc, pos, ref_seq=0, client=0, text_cap=1 << 16):
+        """MergeTree.getContainingSegment(pos, refSeq, clientId) (MT/mergeTree.ts:1656-1667):
+        the segment's read-out (dict) with `offset` = pos - its position, or None."""
+        info = _native.MtSegInfo()
+        text = np.zeros(text_cap, dtype=np.uint16)
+        self._check(self.lib.mt_get_containing_segment(self.h, doc, pos, ref_seq, client, ctypes.byref(info),
+                                                       _native.ptr(text), text_cap), "mt_get_containing_segment")
+        return self._seg_info(info, text)
+
+    def get_segment_by_uid(self, doc, uid, ref_seq=0, client=0, text_cap=1 << 16):
+        """MergeTree.getPosition(segment, refSeq, clientId) (:1619-1636) of segment `uid` as
+        the read-out's `position`; None once it left the tree."""
+        info = _native.MtSegInfo()
+        text = np.zeros(text_cap, dtype=np.uint16)
+        self._check(self.lib.mt_get_segment_by_uid(self.h, doc, uid, ref_seq, client, ctypes.byref(info),
+                                                   _native.ptr(text), text_cap), "mt_get_segment_by_uid")
+        return self._seg_info(info, text)
+
+    def get_view_lengths(self, docs, ref_seq, client):
+        """MergeTree.getLength(refSeq, clientId) (:1610-1612) for each (doc, refSeq, client)."""
+        docs = np.ascontiguousarray(docs, dtype=np.uint32)
+        ref = np.ascontiguousarray(ref_seq, dtype=np.int32)
+        cli = np.ascontiguousarray(client, dtype=np.int32)
+        out = np.zeros(len(docs), dtype=np.int32)
+        self._check(self.lib.mt_get_view_lengths(self.h, len(docs), _native.ptr(docs), _native.ptr(ref),
+                                                 _native.ptr(cli), _native.ptr(out)), "mt_get_view_lengths")
+        return out
 
     def get_prop_runs(self, doc):
         nr, nw = ctypes.c_uint32(), ctypes.c_uint32()

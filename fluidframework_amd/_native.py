@@ -26,7 +26,17 @@ class MtOptions(ctypes.Structure):
                 ("lds_page_capacity", ctypes.c_int32), ("lds_unsettled_capacity", ctypes.c_int32),
                 ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32),
                 ("delta_log_mode", ctypes.c_int32), ("live_client", ctypes.c_int32),
-                ("live_group_capacity", ctypes.c_int32), ("paged_slices", ctypes.c_int32)]
+                ("live_group_capacity", ctypes.c_int32), ("paged_slices", ctypes.c_int32),
+                ("segment_ordinals", ctypes.c_int32)]
+
+
+class MtSegInfo(ctypes.Structure):
+    """mt_seg_info (include/mt_replay.h): one segment's read-out."""
+    _fields_ = [("row", ctypes.c_int32), ("uid", ctypes.c_uint32), ("position", ctypes.c_int32),
+                ("offset", ctypes.c_int32), ("length", ctypes.c_int32), ("seq", ctypes.c_int32),
+                ("client", ctypes.c_int32), ("removed_seq", ctypes.c_int32), ("removed_client", ctypes.c_int32),
+                ("marker_ref_type", ctypes.c_int32), ("text_len", ctypes.c_int32),
+                ("ordinal_len", ctypes.c_int32), ("ordinal", ctypes.c_uint16 * 16)]
 
 
 # mt_regen_rec (include/mt_replay.h): one op of regeneratePendingOp
@@ -88,6 +98,9 @@ SIGNATURES = [
     ("mt_regenerate_pending", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P, _U32]),
     ("mt_pending_counts", _I, [_P, _P]),
     ("mt_debug_heap", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
+    ("mt_get_containing_segment", _I, [_P, _U32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _U32]),
+    ("mt_get_segment_by_uid", _I, [_P, _U32, _U32, ctypes.c_int32, ctypes.c_int32, _P, _P, _U32]),
+    ("mt_get_view_lengths", _I, [_P, _U32, _P, _P, _P, _P]),
 ]
 
 _lib = None
@@ -101,6 +114,8 @@ def load():
         raise RuntimeError(f"HIP replay library missing: {LIB_PATH} (run __graft_entry__.build())")
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
+        if os.environ.get("MT_LIB_PATH") and not hasattr(lib, name):
+            continue   # an older variant build (A/B runs) lacks later entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -107,6 +107,11 @@ struct DevState {
     int32_t PP, PH, UT, UM;
     int32_t S, B, H, T, P, DL;
     int32_t DLR;              // rich delta log: segment text / properties + maintenance events
+    // segment ordinals (mt_options.segment_ordinals, flat tiers; null otherwise): every
+    // node's own ordinal character (MergeBlock.setOrdinal, MT/mergeTree.ts:347-372); a
+    // node's ordinal is its ancestors' characters then its own (mt_engine.h "ordinals")
+    uint16_t *ordS;           // [n_docs][S] per segment
+    uint16_t *ordB;           // [n_docs][MT_LV][B] per block of every level
     int32_t n_docs;
     // live-client handles (mt_options.live_client; null otherwise)
     int32_t *live;            // [n_docs][4] {collabWindow.localSeq, group queue head id, length, 0}

@@ -140,6 +140,12 @@ template <class T> struct DocT {
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
     int rich;                          // rich delta log (segments' state, maintenance events)
+    // segment ordinals (DevState.ordS / ordB; flat tiers of logging handles only): each
+    // segment's and each block's own ordinal character, in HBM
+    int ord;
+    int obst;                          // per-level stride of ob (st.B)
+    GLB_AS uint16_t *os;               // [S]
+    GLB_AS uint16_t *ob;               // [MT_LV][obst]
     int wide;               // an overlap mask holds a slot above 32 (DocHdr.pad0 bit 0)
     // overlap slots (mt_device.h ovl_has): lane i holds the client owning slot i + 1
     // (MT_OSLOT_FREE); ocs = the current message's client's slot (0: none)
@@ -373,6 +379,18 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.P_cap = st.P;
     d.DL_cap = st.DL;
     d.rich = st.DLR;
+    if constexpr (T::kLog && !T::kPaged) {
+        d.ord = 0;
+        d.obst = 0;
+        d.os = nullptr;
+        d.ob = nullptr;
+        if (st.ordS) {
+            d.ord = 1;
+            d.obst = st.B;
+            d.os = (GLB_AS uint16_t *)(st.ordS + doc * (size_t)st.S);
+            d.ob = (GLB_AS uint16_t *)(st.ordB + doc * (size_t)MT_LV * st.B);
+        }
+    }
     d.oslot = (GLB_AS int32_t *)(st.oslot + doc * (size_t)(2 * MT_OSLOTS));
     d.ocli = d.oslot[2 * lane()];
     d.ocs = 0;
@@ -568,10 +586,27 @@ TD void mark_dirty(DocT<T> &d, int i) {
 #endif
 }
 
+// Segment ordinals are kept by the logging instantiations of the flat tiers only (the
+// replay fast path and the paged layout compile them out).
+TD bool ordon(DocT<T> &d) {
+    if constexpr (T::kLog && !T::kPaged)
+        return d.ord != 0;
+    else
+        return false;
+}
+// setOrdinal's width for a block of c children (mt_engine.h "segment ordinals")
+__device__ __forceinline__ int ord_w(int c) { return 1 << (7 - min(max(c, 1), 7)); }
+// lane 0 writes one ordinal character (a global store other lanes read after gsync)
+__device__ __forceinline__ void ord_put(GLB_AS uint16_t *p, int v) {
+    if (lane() == 0) *p = (uint16_t)v;
+    gsync();
+}
+
 // ------------------------------------------------------------------ segment table moves
 // [from, n) -> [from + k, n + k)
 TD void seg_move_right(DocT<T> &d, int from, int k) {
     mark_dirty(d, from);
+    const bool om = ordon(d);
     for (int hi = d.n; hi > from; hi -= MT_WAVE) {
         const int lo = max(from, hi - MT_WAVE);
         const int i = lo + lane();
@@ -579,11 +614,13 @@ TD void seg_move_right(DocT<T> &d, int from, int k) {
         u64 o;
         PendQ pq = pq_zero();
         v4u b;
+        uint16_t oc = 0;
         if (i < hi) {
             a = d.A[i];
             o = d.O[i];
             b = d.Bv[i];
             if constexpr (T::kLive) pq = pq_get(d, i);
+            if (om) oc = d.os[i];
         }
         wsync<T>();
         if (i < hi) {
@@ -591,24 +628,29 @@ TD void seg_move_right(DocT<T> &d, int from, int k) {
             d.O[i + k] = o;
             d.Bv[i + k] = b;
             if constexpr (T::kLive) pq_put(d, i + k, pq);
+            if (om) d.os[i + k] = oc;
         }
         wsync<T>();
     }
+    if (om) gsync();
 }
 // [from, n) -> [from - k, n - k)
 TD void seg_move_left(DocT<T> &d, int from, int k) {
     mark_dirty(d, from - k);
+    const bool om = ordon(d);
     for (int lo = from; lo < d.n; lo += MT_WAVE) {
         const int i = lo + lane();
         v4i a;
         u64 o;
         PendQ pq = pq_zero();
         v4u b;
+        uint16_t oc = 0;
         if (i < d.n) {
             a = d.A[i];
             o = d.O[i];
             b = d.Bv[i];
             if constexpr (T::kLive) pq = pq_get(d, i);
+            if (om) oc = d.os[i];
         }
         wsync<T>();
         if (i < d.n) {
@@ -616,9 +658,11 @@ TD void seg_move_left(DocT<T> &d, int from, int k) {
             d.O[i - k] = o;
             d.Bv[i - k] = b;
             if constexpr (T::kLive) pq_put(d, i - k, pq);
+            if (om) d.os[i - k] = oc;
         }
         wsync<T>();
     }
+    if (om) gsync();
 }
 
 // Loads a segment's {A, O} for a scan lane.  The load is unconditional (inactive lanes read
@@ -694,20 +738,25 @@ TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
             }
         }
     }
+    const bool om = ordon(d);
+    GLB_AS uint16_t *oc = om ? d.ob + (size_t)l * d.obst : nullptr;   // block ordinal characters
     if (delta > 0) {
         for (int hi = nb; hi > from; hi -= MT_WAVE) {
             const int lo = max(from, hi - MT_WAVE);
             const int i = lo + lane();
             uint8_t v = 0;
             int8_t f = 0;
+            uint16_t ov = 0;
             if (i < hi) {
                 v = c[i];
                 if (l == 0) f = d.flg[i];
+                if (om) ov = oc[i];
             }
             wsync<T>();
             if (i < hi) {
                 c[i + delta] = v;
                 if (l == 0) d.flg[i + delta] = f;
+                if (om) oc[i + delta] = ov;
             }
             wsync<T>();
         }
@@ -716,18 +765,22 @@ TD void blk_shift(DocT<T> &d, int l, int from, int delta) {
             const int i = lo + lane();
             uint8_t v = 0;
             int8_t f = 0;
+            uint16_t ov = 0;
             if (i < nb) {
                 v = c[i];
                 if (l == 0) f = d.flg[i];
+                if (om) ov = oc[i];
             }
             wsync<T>();
             if (i < nb) {
                 c[i + delta] = v;
                 if (l == 0) d.flg[i + delta] = f;
+                if (om) oc[i + delta] = ov;
             }
             wsync<T>();
         }
     }
+    if (om) gsync();
     wsync<T>();
     if (lane() == 0) d.nb[l] = nb + delta;
     wsync<T>();
@@ -778,13 +831,24 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
                 lvl(d, nl)[0] = 2;
             }
             wsync<T>();
+            if (ordon(d)) ord_canon_all(d);   // updateRoot: nodeUpdateOrdinals(root)
             return;
         }
         const int pc = cntr(d, l + 1, P) + 1;
         wsync<T>();
         if (lane() == 0) lvl(d, l + 1)[P] = (uint8_t)pc;
         wsync<T>();
-        if (pc < MT_MAXN) return;
+        if (pc < MT_MAXN) {
+            // the propagation stops here: the new half is linked after the old one
+            // (setOrdinal) and re-derived (nodeUpdateOrdinals(fromSplit)); the old half was
+            // re-derived by its split -- each re-derivation covers every split below
+            if (ordon(d)) {
+                ord_put(ordl(d, l) + b + 1, uni((int)ordl(d, l)[b]) + ord_w(pc));
+                ord_canon(d, l, b);
+                ord_canon(d, l, b + 1);
+            }
+            return;
+        }
         l = l + 1;
         b = P;
     }
@@ -831,6 +895,70 @@ TD int block_of(DocT<T> &d, int i, int nb) {
             lo = mid + 1;
     }
     return lo;
+}
+
+// ------------------------------------------------------------------ segment ordinals
+// MergeBlock.setOrdinal (MT/mergeTree.ts:347-372): a child's ordinal is its parent's plus one
+// character -- at index 0 width - 1, otherwise the previous sibling's last character + width,
+// width = 1 << (MaxNodesInBlock - (childCount + 1)) with childCount capped at 7 -- and
+// nodeUpdateOrdinals (:2553-2575) re-derives a whole subtree that way (child q of a block
+// with c children: (q + 1) * width(c) - 1).  Only these two write ordinals, and between
+// messages every node's ordinal is its parent's plus its own last character (checked on the
+// reference over C2/C3/C4 streams: oracle/ref_harness.mjs ordprobe, tests/test_events.py; a
+// loaded summary whose body re-inserts segments breaks it -- MT_DOC_ALIASED), so
+// the engine keeps one character per node (DocT.os / DocT.ob) and spells an ordinal out
+// only to log it.
+// Where the reference writes them (Q8: the characters are not unique, SequenceDeltaEvent
+// drops ranges whose ordinals collide):
+//   insert before an existing segment (blockInsert's onLeaf replaceCurrent :2437-2441): the
+//     new segment takes the existing one's character, which gets its own + width;
+//   insert at a block end, or a split's right half (:2483-2486): previous sibling's + width;
+//   a block that overflows (:2487-2503, split :2509-2522): every split half's subtree is
+//     re-derived; the level where the propagation stops gives the new half previous + width;
+//     a new root (updateRoot :1909-1920) re-derives the whole tree;
+//   zamboni's shrunk block (:1486-1501) and pack's topmost parent (:1444-1450) are re-derived.
+TD GLB_AS uint16_t *ordl(DocT<T> &d, int l) { return d.ob + (size_t)l * d.obst; }
+
+// nodeUpdateOrdinals(block b of level l): every node below it gets its canonical character
+TD void ord_canon(DocT<T> &d, int l, int b) {
+    int lo = b, hi = b + 1;
+    for (int j = l; j >= 0; j--) {
+        const int c0 = blk_prefix(d, j, lo);
+        int carry = c0;
+        GLB_AS uint16_t *dst = j == 0 ? d.os : ordl(d, j - 1);
+        const LDS_AS uint8_t *cnt = lvl(d, j);
+        for (int base = lo; base < hi; base += MT_WAVE) {
+            const int p = base + lane();
+            const int c = p < hi ? (int)cnt[p] : 0;
+            const int inc = wave_scan_incl(c);
+            const int first = carry + inc - c;
+            const int w = ord_w(c);
+            for (int q = 0; q < c; q++) dst[first + q] = (uint16_t)((q + 1) * w - 1);
+            carry += bcast(inc, MT_WAVE - 1);
+        }
+        lo = c0;
+        hi = carry;
+    }
+    gsync();
+}
+// the whole tree (updateRoot, reloadFromSegments)
+TD void ord_canon_all(DocT<T> &d) { ord_canon(d, d.depth - 1, 0); }
+
+// the ordinal of segment i: its ancestors' characters below the root, then its own
+// (codes[0 .. depth)); returns the length
+TD int ord_of(DocT<T> &d, int i, int *codes) {
+    const int dep = d.depth;
+    gsync();
+    codes[dep - 1] = uni((int)d.os[i]);
+    int x = i;
+    for (int l = 0; l + 1 < dep; l++) {
+        int st;
+        const int b = blk_find(d, l, x, true, st);
+        if (b < 0) return -1;
+        codes[dep - 2 - l] = uni((int)ordl(d, l)[b]);
+        x = b;
+    }
+    return dep;
 }
 
 // ------------------------------------------------------------------ zamboni heap
@@ -1130,7 +1258,7 @@ TD void cb_log_state(DocT<T> &d, bool marker, uint32_t ref_type, const TextPiece
         if (!cb_room(d, 2 + words + 2 * max(np, 0))) return;
         GLB_AS int32_t *o = d.dlog + d.dlog_n;
         if (lane() == 0) {
-            o[0] = (marker ? 1 : 0) | (pr ? 2 : 0);
+            o[0] = (marker ? 1 : 0) | (pr ? 2 : 0) | (ordon(d) ? 4 : 0);
             if (marker) o[1] = (int32_t)ref_type;
             o[1 + words] = np;
         }
@@ -1153,6 +1281,28 @@ TD void cb_log_state(DocT<T> &d, bool marker, uint32_t ref_type, const TextPiece
         d.dlog_n += 2 + words + 2 * max(np, 0);
     }
 }
+// After a rich entry's state on a segment_ordinals handle (flags bit 4): [uid, observer
+// position of the segment at the event as Client.getPosition reads it then, ordinal length
+// (-1: the segment has none -- never linked), ordinal characters].  zero_suffix: the SPLIT
+// event's right half, whose ordinal is the left half's + "\0" until it is linked
+// (BaseSegment.splitAt :531-535).
+TD void cb_log_ext(DocT<T> &d, uint32_t uid, int pos, int seg_i, bool zero_suffix) {
+    if constexpr (T::kLog) {
+        if (!ordon(d) || !d.rich) return;
+        int codes[MT_LV + 1];
+        int olen = seg_i >= 0 ? ord_of(d, seg_i, codes) : -1;
+        if (olen >= 0 && zero_suffix) codes[olen++] = 0;
+        if (!cb_room(d, 3 + max(olen, 0))) return;
+        GLB_AS int32_t *o = d.dlog + d.dlog_n;
+        if (lane() == 0) {
+            o[0] = (int32_t)uid;
+            o[1] = pos;
+            o[2] = olen;
+            for (int q = 0; q < olen; q++) o[3 + q] = codes[q];
+        }
+        d.dlog_n += 3 + max(olen, 0);
+    }
+}
 TD void cb_log_seg(DocT<T> &d, v4i a, v4u b) {
     if constexpr (T::kLog) {
         if (!d.rich) return;
@@ -1164,17 +1314,26 @@ TD void cb_log_seg(DocT<T> &d, v4i a, v4u b) {
     }
 }
 // a maintenance record of one or two segments
+// (uid / pos / seg index of each segment for cb_log_ext; i1z: the second one is a split's
+// unlinked right half)
+struct MaintExt {
+    uint32_t uid0, uid1;
+    int pos0, pos1, i0, i1;
+    bool z1;
+};
 TD void cb_maint(DocT<T> &d, int kind, int len0, bool mk0, uint32_t ref0, const TextPieces &t0, uint32_t ph0,
-                 int len1, const TextPieces *t1, uint32_t ph1) {
+                 int len1, const TextPieces *t1, uint32_t ph1, const MaintExt &ex) {
     if constexpr (T::kLog) {
         if (!d.rich || !d.dlog) return;
         Cb cb = cb_begin(d, d.cur_seq, kind);
         cb_log(d, len0);
         cb_log_state(d, mk0, ref0, t0, ph0 ? prec(d, d.props_half, ph0) : nullptr);
+        cb_log_ext(d, ex.uid0, ex.pos0, ex.i0, false);
         cb.n = 1;
         if (t1) {
             cb_log(d, len1);
             cb_log_state(d, false, 0u, *t1, ph1 ? prec(d, d.props_half, ph1) : nullptr);
+            cb_log_ext(d, ex.uid1, ex.pos1, ex.i1, ex.z1);
             cb.n = 2;
         }
         // maintenance events are not part of the delta hash (the hash pins the delta callbacks)
@@ -1209,6 +1368,18 @@ TD void split_seg(DocT<T> &d, int i, int q) {
         FAIL_INTERNAL(d);
         return;
     }
+    // SPLIT event positions as getPosition reads them inside the callback (segment_ordinals
+    // handles): the left half's is its own; the right half is not linked yet (its parent is
+    // the leaf block, which does not list it), so getPosition sums every child of the block
+    // -- the block's observer end with the left half already trimmed (:1619-1636)
+    MaintExt ex{0u, 0u, 0, 0, i, i, true};
+    if (ordon(d) && d.rich) {
+        const v4i ai = uni4(d.A[i]);
+        ex.pos0 = obs_prefix(d, i);
+        ex.pos1 = obs_prefix(d, bstart + cntr(d, 0, b)) - (ai.z == MT_RSEQ_NONE ? ai.x - q : 0);
+        ex.uid0 = uni((int)(d.Bv[i].z & ~MT_MARKER_BIT));
+        ex.uid1 = (uint32_t)d.next_uid;
+    }
     seg_move_right(d, i + 1, 1);
     mark_dirty(d, i);
     if (T::kLog) d.m_split++;   // splitLeafSegment's SPLIT event :2264-2269
@@ -1222,7 +1393,7 @@ TD void split_seg(DocT<T> &d, int i, int q) {
             l.len[0] = q;
             rt.off[0] = b0.x + (uint32_t)q;
             rt.len[0] = a0.x - q;
-            cb_maint(d, -2, q, false, 0u, l, b0.y, a0.x - q, &rt, b0.y);
+            cb_maint(d, -2, q, false, 0u, l, b0.y, a0.x - q, &rt, b0.y, ex);
         }
     }
     if (lane() == 0) {
@@ -1248,6 +1419,8 @@ TD void split_seg(DocT<T> &d, int i, int q) {
     wsync<T>();
     if (lane() == 0) lvl(d, 0)[b] = (uint8_t)c;
     wsync<T>();
+    // the right half is linked after the left one: setOrdinal (:2483-2486)
+    if (ordon(d)) ord_put(d.os + i + 1, uni((int)d.os[i]) + ord_w(c));
     if (c == MT_MAXN) blk_split_up(d, 0, b);
 }
 
@@ -1315,9 +1488,31 @@ __device__ __forceinline__ bool can_append(int plen, bool pmarker, bool p_nl, in
 // in child order, before any text moves.  Lane j holds entry j (a: lengths, b: text offset /
 // marker refType, props); m_app: entries appended to the run before them, whose keeper is
 // the nearest kept entry below (m_keep).
-TD void scour_events(DocT<T> &d, v4i a, v4u b, u64 m_unlink, u64 m_app, u64 m_keep) {
+//
+// Positions (segment_ordinals handles), as getPosition reads them inside each callback
+// (:1619-1636): the scoured block's children array is untouched until the scour ends, a
+// keeper has already absorbed the segments appended to it up to the current one, and an
+// appended segment keeps its own length -- so for entry k of a block starting at observer
+// position S, with base(j) its observer length and app(j) "appended":
+//   UNLINK k, APPEND's keeper k:  S + D(k),  D(k) = sum over earlier entries j of the block
+//                                             of base(j) * (1 + app(j))
+//   APPEND's appended segment k:  S + D(k) + base(k)
+// (pack scours several blocks; the ones before keep their cachedLength, so S is the
+// pre-scour observer start).  s: table index of entry 0; ntot: entries; start: the first
+// entry of this lane's block.
+TD void scour_events(DocT<T> &d, v4i a, v4u b, u64 m_unlink, u64 m_app, u64 m_keep, int s, int ntot, int start) {
     if constexpr (T::kLog) {
         if (!d.rich) return;
+        int pos_k = 0, base_k = 0;
+        if (ordon(d) && (m_unlink | m_app)) {
+            const int k = lane();
+            base_k = (k < ntot && a.z == MT_RSEQ_NONE) ? a.x : 0;
+            const int val = base_k * (((m_app >> k) & 1ull) ? 2 : 1);
+            const int dex = wave_scan_incl(val) - val;
+            const int bex = wave_scan_incl(base_k) - base_k;
+            const int s0 = obs_prefix(d, s);
+            pos_k = s0 + __shfl(bex, start, MT_WAVE) + dex - __shfl(dex, start, MT_WAVE);
+        }
         for (u64 ev = m_unlink | m_app; ev; ev &= ev - 1) {
             const int j = first_lane(ev);
             const int lj = bcast(a.x, j);
@@ -1337,10 +1532,15 @@ TD void scour_events(DocT<T> &d, v4i a, v4u b, u64 m_unlink, u64 m_app, u64 m_ke
                     tot += tk.len[tk.np];
                     tk.np++;
                 }
-                cb_maint(d, -1, tot, false, 0u, tk, (uint32_t)bcast((int)b.y, kk), lj, &tj, pj);
+                const MaintExt ex{(uint32_t)bcast((int)(b.z & ~MT_MARKER_BIT), kk),
+                                  (uint32_t)bcast((int)(b.z & ~MT_MARKER_BIT), j), bcast(pos_k, kk),
+                                  bcast(pos_k, j) + bcast(base_k, j), s + kk, s + j, false};
+                cb_maint(d, -1, tot, false, 0u, tk, (uint32_t)bcast((int)b.y, kk), lj, &tj, pj, ex);
             } else {
                 const bool mk = (bcast((int)b.z, j) & MT_MARKER_BIT) != 0;
-                cb_maint(d, -3, lj, mk, tj.off[0], tj, pj, 0, (const TextPieces *)nullptr, 0u);
+                const MaintExt ex{(uint32_t)bcast((int)(b.z & ~MT_MARKER_BIT), j), 0u, bcast(pos_k, j), 0, s + j, -1,
+                                  false};
+                cb_maint(d, -3, lj, mk, tj.off[0], tj, pj, 0, (const TextPieces *)nullptr, 0u, ex);
             }
         }
     }
@@ -1423,7 +1623,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
     const uint32_t myown = in ? (owners >> (4 * k)) & 0xFu : 0xFu;
     const u64 m_keep = ballot(in && myown == (uint32_t)k);
     const u64 m_app = ballot(in && myown != 0xFu && myown != (uint32_t)k);
-    scour_events(d, a, b, m_unlink, m_app, m_keep);
+    scour_events(d, a, b, m_unlink, m_app, m_keep, s, cntb, 0);
     if (T::kLog) {   // scourNode's UNLINK / APPEND events :1343-1373
         d.m_unlink += __popcll(m_unlink);
         d.m_append += __popcll(m_app);
@@ -1534,11 +1734,13 @@ TD int scour_block(DocT<T> &d, int s, int e) {
         u64 so;
         PendQ sp = pq_zero();
         v4u sb;
+        uint16_t soc = 0;   // ordinal character: a pack re-scours before re-deriving them
         if (surv) {
             sa = d.A[s + k];
             so = d.O[s + k];
             sb = d.Bv[s + k];
             if constexpr (T::kLive) sp = pq_get(d, s + k);
+            if (ordon(d)) soc = d.os[s + k];
         }
         const int dst = s + __popcll(m_keep & ((1ull << k) - 1ull));
         wsync<T>();
@@ -1547,8 +1749,10 @@ TD int scour_block(DocT<T> &d, int s, int e) {
             d.O[dst] = so;
             d.Bv[dst] = sb;
             if constexpr (T::kLive) pq_put(d, dst, sp);
+            if (ordon(d)) d.os[dst] = soc;
         }
         wsync<T>();
+        if (ordon(d)) gsync();
         seg_move_left(d, e, cntb - keep);
         d.n -= cntb - keep;
     }
@@ -1638,7 +1842,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         d.m_append += __popcll(m_join);
     }
     const u64 m_surv = ballot(surv);
-    scour_events(d, a, b, ballot(unlink), m_join, m_surv);
+    scour_events(d, a, b, ballot(unlink), m_join, m_surv, s, tot, start);
     const u64 above = (k < 63) ? (m_join >> (k + 1)) : 0ull;
     const u64 m_grp = ballot(surv && (above & 1ull));
     P2_T0(10)
@@ -1734,11 +1938,13 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
         u64 so;
         PendQ sp = pq_zero();
         v4u sb;
+        uint16_t soc = 0;   // ordinal character: a pack re-scours before re-deriving them
         if (surv) {
             sa = d.A[s + k];
             so = d.O[s + k];
             sb = d.Bv[s + k];
             if constexpr (T::kLive) sp = pq_get(d, s + k);
+            if (ordon(d)) soc = d.os[s + k];
         }
         const int dst = s + __popcll(m_surv & ((1ull << k) - 1ull));
         wsync<T>();
@@ -1747,8 +1953,10 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
             d.O[dst] = so;
             d.Bv[dst] = sb;
             if constexpr (T::kLive) pq_put(d, dst, sp);
+            if (ordon(d)) d.os[dst] = soc;
         }
         wsync<T>();
+        if (ordon(d)) gsync();
         seg_move_left(d, s + tot, tot - keep);
         d.n -= tot - keep;
     }
@@ -1808,6 +2016,7 @@ TD void pack(DocT<T> &d, int l, int b) {
             b = P;
             continue;
         }
+        if (ordon(d)) ord_canon(d, l + 1, P);   // nodeUpdateOrdinals(parent) :1449-1450
         return;
     }
 }
@@ -1877,7 +2086,10 @@ TD void zamboni(DocT<T> &d) {
         wsync<T>();
         if (lane() == 0) d.flg[b] = 0;
         wsync<T>();
-        if (kept < old && kept < MT_HALF && d.depth > 1) pack(d, 0, b);
+        if (kept < old && kept < MT_HALF && d.depth > 1)
+            pack(d, 0, b);
+        else if (kept < old && ordon(d))
+            ord_canon(d, 0, b);   // nodeUpdateOrdinals(block) :1500-1501
     }
 }
 
@@ -2021,10 +2233,12 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
                     }
                 }
                 if (lane() == 0) {
-                    d.dlog[d.dlog_n] = np >= 0 ? 2 : 0;
+                    d.dlog[d.dlog_n] = (np >= 0 ? 2 : 0) | (ordon(d) ? 4 : 0);
                     d.dlog[d.dlog_n + 1] = np;
                 }
                 d.dlog_n += 2 + 2 * max(np, 0);
+                // never linked: no ordinal, getPosition walks no parent (0)
+                cb_log_ext(d, 0u, 0, -1, false);
             }
         }
         cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)-1), 0u));
@@ -2127,6 +2341,22 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     d.next_uid++;
     d.n++;
     const int nc = cntr(d, 0, B) + 1;
+    if (ordon(d)) {
+        const int w = ord_w(nc);
+        if (x < bend) {
+            // insert before a segment (blockInsert's onLeaf, :2218-2225): the new segment
+            // replaces it in the block with its ordinal (replaceCurrent, :2437-2441), and it is
+            // linked after the new one (setOrdinal :2486)
+            const int oc = uni((int)d.os[x + 1]);
+            if (lane() == 0) {
+                d.os[x] = (uint16_t)oc;
+                d.os[x + 1] = (uint16_t)(oc + w);
+            }
+            gsync();
+        } else {   // at the block end
+            ord_put(d.os + x, x > bstart ? uni((int)d.os[x - 1]) + w : w - 1);
+        }
+    }
     wsync<T>();
     if (lane() == 0) lvl(d, 0)[B] = (uint8_t)nc;
     wsync<T>();
@@ -2148,6 +2378,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         if (d.rich) {
             wsync<T>();
             cb_log_seg(d, uni4(d.A[x]), uni4(d.Bv[x]));
+            cb_log_ext(d, uid, pos, x, false);
         }
     }
     cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)pos), (uint32_t)slen));
@@ -2469,6 +2700,7 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                                  (uint32_t)bcast((int)bv.z, j), (uint32_t)bcast((int)bv.w, j)};
                     if (!rem) bj.y = (uint32_t)bcast((int)nh, j);
                     cb_log_seg(d, aj, bj);
+                    cb_log_ext(d, bj.z & ~MT_MARKER_BIT, bcast(opos, j), base + j, false);
                 }
             }
         }

@@ -61,6 +61,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
     if (lane() == 0) {
         init_doc_hdr(st, doc, len);
         st.retry[doc] = 0;
+        // the seed segment is the root's only child: setOrdinal(child, 0) with childCount 1
+        if (st.ordS) st.ordS[(size_t)doc * st.S] = 63;
         if (st.live) {   // collabWindow.localSeq 0, empty pending queue (next group id 1)
             st.live[4 * doc] = 0;
             st.live[4 * doc + 1] = 1;
@@ -190,6 +192,22 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
         nl = (nl + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT;
     }
     for (int b = lane(); b < nb0 && (big || b < st.B); b += MT_WAVE) flg[b] = MT_SCOUR_UNDEF;
+    if (st.ordS && !big && status == 0) {
+        // reloadFromSegments ends with nodeUpdateOrdinals(root) (MT/mergeTree.ts:1273-1276):
+        // child q of a block of c children gets (q + 1) * (1 << (7 - c)) - 1; children of
+        // block p are [7p, 7p + c) one level down
+        uint16_t *os = st.ordS + (size_t)doc * st.S;
+        uint16_t *ob = st.ordB + (size_t)doc * MT_LV * st.B;
+        for (int i = lane(); i < n; i += MT_WAVE) {
+            const int c = cnt[i / MT_LOAD_FANOUT];
+            os[i] = (uint16_t)((i % MT_LOAD_FANOUT + 1) * (1 << (7 - c)) - 1);
+        }
+        for (int l = 0; l + 1 < depth; l++)
+            for (int b = lane(); b < nbl[l]; b += MT_WAVE) {
+                const int c = cnt[(l + 1) * B + b / MT_LOAD_FANOUT];
+                ob[(size_t)l * st.B + b] = (uint16_t)((b % MT_LOAD_FANOUT + 1) * (1 << (7 - c)) - 1);
+            }
+    }
     if (lane() == 0) {
         DocHdr h;
         memset(&h, 0, sizeof(h));
@@ -1206,6 +1224,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
 struct mt_handle {
     int device = 0;
     bool live = false;       // live-client handle (mt_options.live_client)
+    bool ordinals = false;   // segment ordinals kept (mt_options.segment_ordinals)
     uint32_t n_docs = 0;
     DevState st{};
     hipStream_t stream = nullptr;
@@ -1313,6 +1332,11 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.P = o.props_capacity > 0 ? o.props_capacity : st.S + 2 * MT_WAVE;
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
     st.DLR = st.DL > 0 && o.delta_log_mode == 1 ? 1 : 0;
+    h->ordinals = o.segment_ordinals != 0;
+    if (h->ordinals && (!st.DLR || o.page_capacity > 0)) {   // needs the rich log and the flat tiers
+        delete h;
+        return nullptr;
+    }
     if (const char *e = getenv("MT_WPG")) h->wpg = atoi(e) == 1 ? 1 : 2;
     h->live = o.live_client != 0;
     if (h->live && o.page_capacity > 0) {   // live documents replay from the flat HBM tier
@@ -1403,6 +1427,10 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.retry, N * sizeof(int32_t));
     alloc((void **)&st.resume, N * sizeof(int64_t));
     alloc((void **)&st.stats, 16 * sizeof(uint32_t));
+    if (h->ordinals) {
+        alloc((void **)&st.ordS, N * (size_t)st.S * sizeof(uint16_t));
+        alloc((void **)&st.ordB, N * (size_t)MT_LV * st.B * sizeof(uint16_t));
+    }
     if (h->live) {
         alloc((void **)&st.live, N * 4 * sizeof(int32_t));
         st.LG = std::min(std::max(o.live_group_capacity > 0 ? o.live_group_capacity : 1024, 16), 65535);
@@ -1443,7 +1471,7 @@ void mt_destroy(mt_handle *h) {
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
                   st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot,
-                  st.live, st.grp, st.segP};
+                  st.live, st.grp, st.segP, st.ordS, st.ordB};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -2004,6 +2032,10 @@ __global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, int64_t ops
 mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                       int32_t *view_len_trace) {
     if (!h || !cfg || cfg->writers < 1 || cfg->ops < 0) return nullptr;
+    if (h->ordinals) {   // the generator's kernels keep no ordinals
+        h->err = "mt_generate: not on a segment_ordinals handle";
+        return nullptr;
+    }
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *b = new mt_batch();
     b->device = h->device;
@@ -2364,6 +2396,152 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
     const int nb0 = hd.hdr.n_blk[0];
     for (int b = 0; b < nb0 && leaves && (uint32_t)b < cap_leaves; b++) leaves[b] = hd.cnt[b];
     if (n_leaves) *n_leaves = (uint32_t)nb0;
+    return 0;
+}
+
+// ---------------------------------------------------------------- segment read-outs
+// Views of one fetched document for mt_get_containing_segment / mt_get_segment_by_uid /
+// mt_get_view_lengths (the device's view_len, MT/mergeTree.ts:1692-1732; client 0 = this
+// replica: its local net length whatever the refSeq).
+struct HostView {
+    int r, c, cs;   // refSeq, short client, c's overlap slot (0: none)
+    bool local;
+};
+static int host_view_setup(mt_handle *h, uint32_t doc, const HostDoc &hd, int32_t ref_seq, int32_t client,
+                           HostView &v) {
+    v.r = ref_seq;
+    v.c = client;
+    v.cs = 0;
+    v.local = client == 0;
+    if (v.local) return 0;
+    if (ref_seq < hd.hdr.min_seq || ref_seq > hd.hdr.cur_seq) {
+        h->err = "remote view: refSeq outside the collab window [minSeq, currentSeq]";
+        return MT_E_INVALID;
+    }
+    int32_t os[2 * MT_OSLOTS];
+    HIPCHK(h, hipMemcpy(os, h->st.oslot + (size_t)doc * 2 * MT_OSLOTS, sizeof(os), hipMemcpyDeviceToHost));
+    for (int i = 0; i < MT_OSLOTS; i++)
+        if (os[2 * i] == client) {
+            v.cs = i + 1;
+            break;
+        }
+    return 0;
+}
+static int host_view_len(const HostDoc &hd, const HostView &v, int i) {
+    const int4 a = hd.A[i];
+    if (v.local) return a.z == MT_RSEQ_NONE ? a.x : 0;
+    const int cli = (int)(short)(a.w & 0xFFFF), rcli = (int)(short)((uint32_t)a.w >> 16);
+    const u64 o = hd.O[i];
+    const bool ovl = v.cs >= 1 && ((o >> (v.cs - 1)) & 1ull);
+    const bool ins = cli == v.c || (a.y != -1 && a.y <= v.r);
+    const bool gone = a.z != MT_RSEQ_NONE && (rcli == v.c || ovl || (a.z != -1 && a.z <= v.r));
+    return ins && !gone ? a.x : 0;
+}
+// the fields of row i (and, on a segment_ordinals handle, its ordinal from the per-node
+// characters: ancestors below the root, then its own)
+static int host_seg_info(mt_handle *h, uint32_t doc, const HostDoc &hd, int i, mt_seg_info *out, uint16_t *text,
+                         uint32_t text_cap) {
+    const int4 a = hd.A[i];
+    const uint4 b = hd.B[i];
+    const bool lins = a.y >= MT_LOCAL_BASE, lrem = a.z >= MT_LOCAL_BASE && a.z != MT_RSEQ_NONE;
+    out->row = i;
+    out->uid = b.z & ~MT_MARKER_BIT;
+    out->length = a.x;
+    out->seq = lins ? -1 : a.y;
+    out->client = (int)(short)(a.w & 0xFFFF);
+    out->removed_seq = lrem ? -1 : a.z;
+    out->removed_client = a.z == MT_RSEQ_NONE ? MT_RSEQ_NONE : (int)(short)((uint32_t)a.w >> 16);
+    const bool marker = (b.z & MT_MARKER_BIT) != 0;
+    out->marker_ref_type = marker ? (int32_t)b.x : -1;
+    out->text_len = 0;
+    if (!marker && text) {
+        for (int j = 0; j < a.x && (uint32_t)j < text_cap; j++) text[j] = hd.text[b.x + j];
+        out->text_len = std::min<int>(a.x, (int)text_cap);
+    }
+    out->ordinal_len = -1;
+    if (h->ordinals && !hd.hdr.pad[HDR_PAGED]) {
+        const size_t S = h->st.S, B = h->st.B;
+        uint16_t code = 0;
+        HIPCHK(h, hipMemcpy(&code, h->st.ordS + doc * S + i, 2, hipMemcpyDeviceToHost));
+        std::vector<uint16_t> ob((size_t)MT_LV * B);
+        HIPCHK(h, hipMemcpy(ob.data(), h->st.ordB + doc * MT_LV * B, ob.size() * 2, hipMemcpyDeviceToHost));
+        const int dep = hd.hdr.depth;
+        out->ordinal[dep - 1] = code;
+        int x = i;
+        for (int l = 0; l + 1 < dep; l++) {
+            int b_ = 0, end = 0;
+            while (b_ < hd.hdr.n_blk[l]) {
+                end += hd.cnt[(size_t)l * B + b_];
+                if (end > x) break;
+                b_++;
+            }
+            out->ordinal[dep - 2 - l] = ob[(size_t)l * B + b_];
+            x = b_;
+        }
+        out->ordinal_len = dep;
+    }
+    return 0;
+}
+
+int mt_get_containing_segment(mt_handle *h, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
+                              mt_seg_info *out, uint16_t *text, uint32_t text_cap) {
+    if (!out) return MT_E_INVALID;
+    HostDoc hd;
+    int rc = fetch_doc(h, doc, hd, text != nullptr, false);
+    if (rc) return rc;
+    HostView v;
+    if ((rc = host_view_setup(h, doc, hd, ref_seq, client, v))) return rc;
+    memset(out, 0, sizeof(*out));
+    out->row = -1;
+    int p = 0;
+    for (int i = 0; i < hd.hdr.n_seg; i++) {   // searchBlock's leaf test: pos < len (:1830-1862)
+        const int l = host_view_len(hd, v, i);
+        if (l > 0 && pos >= p && pos < p + l) {
+            host_seg_info(h, doc, hd, i, out, text, text_cap);
+            out->position = p;
+            out->offset = pos - p;
+            return 0;
+        }
+        p += l;
+    }
+    return 0;
+}
+
+int mt_get_segment_by_uid(mt_handle *h, uint32_t doc, uint32_t uid, int32_t ref_seq, int32_t client,
+                          mt_seg_info *out, uint16_t *text, uint32_t text_cap) {
+    if (!out) return MT_E_INVALID;
+    HostDoc hd;
+    int rc = fetch_doc(h, doc, hd, text != nullptr, false);
+    if (rc) return rc;
+    HostView v;
+    if ((rc = host_view_setup(h, doc, hd, ref_seq, client, v))) return rc;
+    memset(out, 0, sizeof(*out));
+    out->row = -1;
+    int p = 0;
+    for (int i = 0; i < hd.hdr.n_seg; i++) {
+        if ((hd.B[i].z & ~MT_MARKER_BIT) == uid) {
+            host_seg_info(h, doc, hd, i, out, text, text_cap);
+            out->position = p;
+            return 0;
+        }
+        p += host_view_len(hd, v, i);
+    }
+    return 0;
+}
+
+int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const int32_t *ref_seq,
+                        const int32_t *client, int32_t *out) {
+    if (!h || (n && (!docs || !ref_seq || !client || !out))) return MT_E_INVALID;
+    for (uint32_t q = 0; q < n; q++) {
+        HostDoc hd;
+        int rc = fetch_doc(h, docs[q], hd, false, false);
+        if (rc) return rc;
+        HostView v;
+        if ((rc = host_view_setup(h, docs[q], hd, ref_seq[q], client[q], v))) return rc;
+        int len = 0;
+        for (int i = 0; i < hd.hdr.n_seg; i++) len += host_view_len(hd, v, i);
+        out[q] = len;
+    }
     return 0;
 }
 

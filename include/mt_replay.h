@@ -93,6 +93,14 @@ typedef struct mt_options {
        full rounds and the r left-over documents' work is spread over all of them instead of
        running as a last, nearly empty round (0 = off).  Results are identical. */
     int32_t paged_slices;
+    /* 1 (with delta_log_mode 1): keep every segment's ordinal (MergeBlock.setOrdinal /
+       nodeUpdateOrdinals, MT/mergeTree.ts:347-372, 2553-2575) -- the strings
+       SortedSegmentSet and SequenceDeltaEvent order and dedup ranges by (Q8).  Each rich log
+       entry then also carries the segment's id, its position as Client.getPosition reads it
+       inside the callback, and its ordinal; mt_get_segment_info reads the current ones.  The
+       documents stay in the flat tiers (with page_capacity set, mt_create fails); the
+       replay fast path and the synthetic generator keep no ordinals. */
+    int32_t segment_ordinals;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the
@@ -219,6 +227,44 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
                     uint32_t *n_rows, int32_t *leaves, uint32_t cap_leaves, uint32_t *n_leaves);
 int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_t *pairs,
                          uint32_t cap_pairs, int32_t *n_pairs);
+/* ---- segment read-outs of the Client / MergeTree surface SharedSegmentSequence calls
+        (SEQ/sequence.ts:240, 251; MT/mergeTree.ts:1610-1667; MT/client.ts getPosition /
+        getContainingSegment).  A view is (ref_seq, client): client is a short client id as
+        the encoder numbered it, 0 = this replica (its view is the observer view whatever the
+        ref_seq, MT/mergeTree.ts:1692-1698).  A remote view is one the client can still hold:
+        ref_seq at or above the refSeq of its latest message (>= minSeq; MT_E_INVALID below
+        minSeq or above currentSeq).  Below its latest refSeq the reference answers from
+        partial lengths that no longer add up to its segments' view lengths, and the result
+        here -- computed from the segments -- differs. ---- */
+typedef struct mt_seg_info {
+    int32_t row;             /* index in document order (-1: no such segment) */
+    uint32_t uid;            /* segment id: stable for the segment's life (a split's left half
+                                keeps it, the right half gets a new one) */
+    int32_t position;        /* getPosition in the queried view: lengths of the segments before it */
+    int32_t offset;          /* mt_get_containing_segment: pos - position; else 0 */
+    int32_t length;          /* cachedLength */
+    int32_t seq, client;     /* -1 = UnassignedSequenceNumber (live handles) */
+    int32_t removed_seq;     /* MT_RSEQ_NONE when not removed */
+    int32_t removed_client;
+    int32_t marker_ref_type; /* -1: a TextSegment */
+    int32_t text_len;        /* UTF-16 units of its text written to the caller's buffer */
+    int32_t ordinal_len;     /* -1: no ordinals on this handle (mt_options.segment_ordinals) */
+    uint16_t ordinal[16];    /* MergeNode.ordinal's characters (MT/mergeTree.ts:347-372) */
+} mt_seg_info;
+/* MergeTree.getContainingSegment(pos, refSeq, clientId) (MT/mergeTree.ts:1656-1667): the
+   first segment visible in the view whose span holds pos; row -1 when pos is past the end. */
+int mt_get_containing_segment(mt_handle *h, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
+                              mt_seg_info *out, uint16_t *text, uint32_t text_cap);
+/* MergeTree.getPosition(segment, refSeq, clientId) (MT/mergeTree.ts:1619-1636) of the segment
+   with id uid (from a delta-log entry or an earlier read-out); row -1 once it left the tree
+   (unlinked, or appended to its neighbour: the reference's getPosition of such a segment
+   walks no parent and returns 0). */
+int mt_get_segment_by_uid(mt_handle *h, uint32_t doc, uint32_t uid, int32_t ref_seq, int32_t client,
+                          mt_seg_info *out, uint16_t *text, uint32_t text_cap);
+/* MergeTree.getLength(refSeq, clientId) (MT/mergeTree.ts:1610-1612) for n (doc, ref_seq,
+   client) queries. */
+int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const int32_t *ref_seq,
+                        const int32_t *client, int32_t *out);
 /* Debug: raw segment records (8 u32 per segment: segA then segB) and the 32-word header. */
 int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, uint32_t *n_rows,
                  int32_t *hdr_words);
@@ -242,7 +288,8 @@ int mt_delta_log_reset(mt_handle *h);
 /* mergeTreeMaintenanceCallback events per document since its creation (only with
    delta_log_capacity > 0, MT_E_INVALID otherwise): out[3*doc + {0,1,2}] = SPLIT
    (splitLeafSegment, MT/mergeTree.ts:2260-2272), APPEND and UNLINK (scourNode,
-   MT/mergeTree.ts:1322-1398).  Counts, not event objects: segments are device rows. */
+   MT/mergeTree.ts:1322-1398).  (The events themselves, with the segments' state, are
+   records of the rich delta log, delta_log_mode 1.) */
 int mt_maintenance_counts(mt_handle *h, uint32_t *out);
 
 /* Per-document checksums (mt_types.h), to host memory or straight into device memory

@@ -44,6 +44,9 @@ TEST_FILES = [
 ]
 
 
+SEQ_FILES = ["sequenceDeltaEvent.ts"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -61,8 +64,17 @@ def main():
         p = os.path.join(src_dir, "test", name)
         if os.path.exists(p):
             files["mt/test/" + name[:-3]] = (p, open(p, encoding="utf-8").read())
+    # the sequence package's event objects (SequenceDeltaEvent / SequenceMaintenanceEvent:
+    # ranges sorted and deduplicated by segment ordinal through SortedSegmentSet) -- the
+    # reference side of the GPU facade's event parity (oracle/ref_harness.mjs events)
+    seq_dir = os.path.join(args.ref, "packages/dds/sequence/src")
+    for name in SEQ_FILES:
+        p = os.path.join(seq_dir, name)
+        files["seq/" + name[:-3]] = (p, open(p, encoding="utf-8").read())
 
     def resolve(from_mod, spec):
+        if spec == "@fluidframework/merge-tree":
+            return "mt/index"
         if spec in SHIMS:
             return ("shim", os.path.relpath(os.path.join("shims", SHIMS[spec]),
                                             os.path.dirname(from_mod)))

@@ -29,6 +29,7 @@ import random from "./_ref/shims/random-js.mjs";
 import { annotateRange, insertAtRefPos, removeRange, runMergeTreeOperationRunner, generateClientNames }
     from "./_ref/mt/test/mergeTreeOperationRunner.mjs";
 import { TestClient } from "./_ref/mt/test/testClient.mjs";
+import { SequenceDeltaEvent, SequenceMaintenanceEvent } from "./_ref/seq/sequenceDeltaEvent.mjs";
 
 const { Client, TextSegment, Marker } = MT;
 
@@ -417,6 +418,120 @@ function replayRichDoc(log) {
         c.applyMsg(msg);
     }
     return { doc: log.doc, events };
+}
+
+// SharedSegmentSequence's event objects over the observer (SEQ/sequence.ts:139-149): every
+// callback builds the reference's own SequenceDeltaEvent / SequenceMaintenanceEvent and reads
+// it as a synchronous listener does (its ranges are lazy: positions and ordinals at callback
+// time).  Per event: ["D", seq, operation, isLocal, segs, ranges] / ["M", operation, segs,
+// ranges] with segs[i] = [Client.getPosition(segment), segment.ordinal as char codes (null:
+// none), cachedLength] for deltaSegments[i], and ranges = [[index into deltaSegments,
+// position]] in the event's order (SortedSegmentSet: by ordinal, equal ordinals dropped, Q8).
+function ordCodes(seg) {
+    return seg.ordinal === undefined ? null : Array.from(seg.ordinal, (ch) => ch.charCodeAt(0));
+}
+function eventRecord(c, args, ev) {
+    const segs = args.deltaSegments.map((d) => [c.getPosition(d.segment), ordCodes(d.segment), d.segment.cachedLength]);
+    const ranges = ev.ranges.map((r) => [args.deltaSegments.findIndex((d) => d.segment === r.segment), r.position]);
+    return [segs, ranges];
+}
+function replayEventsDoc(log) {
+    const { c } = makeObserver(log.seed_text);
+    const events = [];
+    c.mergeTreeDeltaCallback = (opArgs, dargs) => {
+        const ev = new SequenceDeltaEvent(opArgs, dargs, c);
+        events.push(["D", opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, dargs.operation,
+            ev.isLocal, ...eventRecord(c, dargs, ev)]);
+    };
+    c.mergeTree.mergeTreeMaintenanceCallback = (args) => {
+        const ev = new SequenceMaintenanceEvent(args, c);
+        events.push(["M", args.operation, ...eventRecord(c, args, ev)]);
+    };
+    const cseq = {};
+    for (const [k, t, r, msn, op, type] of log.msgs) {
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        c.applyMsg(msg);
+    }
+    return { doc: log.doc, events };
+}
+
+// Read-outs of the final replica (MT/mergeTree.ts:1610-1667): MergeTree.getLength(refSeq,
+// clientId) and getContainingSegment(pos, refSeq, clientId) for the observer's view and for
+// writers' views, and getPosition of the found segment in that view.  A writer's view is one
+// it can still hold: refSeq at or above the refSeq of its latest message (below it the
+// reference's partial lengths no longer add up to its segments' lengths -- measured: every
+// mismatch between getLength and the sum of nodeLength over the leaves was such a view).
+// Segments are identified by their observer position and contents.
+function readoutsDoc(log) {
+    const { c } = makeObserver(log.seed_text);
+    c.mergeTreeDeltaCallback = undefined;
+    const cseq = {};
+    const lastRef = {};
+    for (const [k, t, r, msn, op, type] of log.msgs) {
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        c.applyMsg(msg);
+        lastRef[c.getShortClientId(msg.clientId)] = r;
+    }
+    const mt = c.mergeTree;
+    const cw = mt.getCollabWindow();
+    const rng = new Rng(777, log.doc.length);
+    const views = [[cw.currentSeq, cw.clientId]];
+    for (let cli = 1; cli < 12; cli++) {
+        if (c.getLongClientId(cli) === undefined || lastRef[cli] === undefined) { break; }
+        const r0 = Math.max(lastRef[cli], cw.minSeq);
+        for (const ref of [r0, Math.floor((r0 + cw.currentSeq) / 2), cw.currentSeq]) { views.push([ref, cli]); }
+    }
+    const lengths = views.map(([ref, cli]) => [ref, cli, mt.getLength(ref, cli)]);
+    const containing = [];
+    for (const [ref, cli] of views) {
+        const len = mt.getLength(ref, cli);
+        for (let q = 0; q < 12; q++) {
+            const pos = q === 11 ? len : rng.uniform(len + 1);
+            const { segment, offset } = mt.getContainingSegment(pos, ref, cli);
+            if (segment === undefined) {
+                containing.push([pos, ref, cli, null]);
+                continue;
+            }
+            containing.push([pos, ref, cli, [offset, mt.getPosition(segment, ref, cli),
+                c.getPosition(segment), segment.cachedLength, ordCodes(segment), segState(segment)]]);
+        }
+    }
+    return { doc: log.doc, minSeq: cw.minSeq, currentSeq: cw.currentSeq, lengths, containing };
+}
+
+// The ordinal invariant the GPU engine's representation rests on (mt_engine.h "segment
+// ordinals"): between messages every node's ordinal is its parent's ordinal plus one
+// character.  Replays each stream and checks the whole tree after every message; returns
+// the number of messages checked and the first violation (null: none).
+function ordProbeDoc(log) {
+    const { c } = makeObserver(log.seed_text);
+    c.mergeTreeDeltaCallback = undefined;
+    const bad = (mt) => {
+        const walk = (b) => {
+            for (let i = 0; i < b.childCount; i++) {
+                const x = b.children[i];
+                if (x.ordinal.length !== b.ordinal.length + 1 || x.ordinal.slice(0, -1) !== b.ordinal) { return true; }
+                if (!x.isLeaf() && walk(x)) { return true; }
+            }
+            return false;
+        };
+        return walk(mt.root);
+    };
+    const cseq = {};
+    let n = 0;
+    for (const [k, t, r, msn, op, type] of log.msgs) {
+        cseq[k] = (cseq[k] || 0) + 1;
+        const msg = makeMsg(k, t, r, msn, cseq[k], op);
+        if (type) { msg.type = type; }
+        c.applyMsg(msg);
+        n++;
+        if (bad(c.mergeTree)) { return { doc: log.doc, messages: n, violation: t }; }
+    }
+    return { doc: log.doc, messages: n, violation: null };
 }
 
 // Maintenance events (mergeTreeMaintenanceCallback, MT/mergeTree.ts:1343-1373 scourNode
@@ -903,6 +1018,15 @@ async function main() {
     } else if (mode === "rich") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => replayRichDoc(d)) }, jsReplacer));
+    } else if (mode === "events") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => replayEventsDoc(d)) }, jsReplacer));
+    } else if (mode === "ordprobe") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => ordProbeDoc(d)) }));
+    } else if (mode === "readouts") {
+        const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
+        fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => readoutsDoc(d)) }, jsReplacer));
     } else if (mode === "replayerr") {
         const logs = JSON.parse(fs.readFileSync(rest[0], "utf8"));
         fs.writeFileSync(rest[1], JSON.stringify({ docs: logs.docs.map((d) => replayErrDoc(d)) }));

@@ -7,7 +7,7 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --live | --only name,name]
+    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --events | --live | --only name,name]
 """
 import gzip
 import json
@@ -204,6 +204,53 @@ def make_rich_fixture():
     print("ref_rich", len(out), "docs", sum(len(d["events"]) for d in out), "events")
 
 
+# SharedSegmentSequence's event objects (harness "events"): the reference's own
+# SequenceDeltaEvent / SequenceMaintenanceEvent built in every callback -- positions and
+# ordinals of the callback segments, and the ranges the events keep (ordinal order, equal
+# ordinals dropped).  Streams: the rich fixture's sources plus deeper trees.
+EVENTS_FROM = RICH_FROM + [("ref_c4", 1), ("ref_wide", 1), ("ref_ext_long", 1)]
+
+
+def make_events_fixture():
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        for name, n in EVENTS_FROM:
+            with gzip.open(os.path.join(HERE, name + ".json.gz"), "rt") as fh:
+                fx = json.load(fh)
+            docs = [dict(doc=f"{name}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in fx["docs"][:n]]
+            lp, op = os.path.join(td, "logs.json"), os.path.join(td, "out.json")
+            json.dump({"docs": docs}, open(lp, "w"))
+            subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "events", lp, op])
+            ev = json.load(open(op))["docs"]
+            for d, e in zip(docs, ev):
+                d["events"] = e["events"]
+                d["source"] = name
+                out.append(d)
+    _dump("ref_events", dict(config={"ext": True, "sources": EVENTS_FROM}, docs=out))
+    print("ref_events", len(out), "docs", sum(len(d["events"]) for d in out), "events")
+
+
+# Read-outs of the final replicas (harness "readouts"): MergeTree.getLength(refSeq, clientId),
+# getContainingSegment(pos, refSeq, clientId) and getPosition in the observer's and the
+# writers' views, on the events fixture's streams.
+def make_readouts_fixture():
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        for name, n in EVENTS_FROM:
+            with gzip.open(os.path.join(HERE, name + ".json.gz"), "rt") as fh:
+                fx = json.load(fh)
+            docs = [dict(doc=f"{name}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in fx["docs"][:n]]
+            lp, op = os.path.join(td, "logs.json"), os.path.join(td, "out.json")
+            json.dump({"docs": docs}, open(lp, "w"))
+            subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "readouts", lp, op])
+            for d, r in zip(docs, json.load(open(op))["docs"]):
+                d.update(r)
+                d["source"] = name
+                out.append(d)
+    _dump("ref_readouts", dict(config={"ext": True, "sources": EVENTS_FROM}, docs=out))
+    print("ref_readouts", len(out), "docs", sum(len(d["containing"]) for d in out), "queries")
+
+
 # Live-client path (harness "live"): a participant client's own unsequenced
 # ops, their acks, remote writers' ops resolved around unacked segments, and reconnects with
 # regeneratePendingOp.  Few keys / values: remote annotates collide with pending local ones.
@@ -259,6 +306,10 @@ def main():
     if "--rich" in sys.argv[1:]:
         make_rich_fixture()
         return
+    if "--events" in sys.argv[1:]:
+        make_events_fixture()
+        make_readouts_fixture()
+        return
     only = None
     if "--only" in sys.argv[1:]:
         only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
@@ -287,6 +338,8 @@ def main():
     make_farm_fixture()
     make_error_fixture()
     make_rich_fixture()
+    make_events_fixture()
+    make_readouts_fixture()
     make_live_fixtures()
 
 

@@ -173,9 +173,13 @@ def expected_rich(doc, interner):
     return out
 
 
-def parse_rich_log(log):
-    """A rich device delta log (mt_options.delta_log_mode 1) -> expected_rich's form."""
+def parse_rich_log(log, ext=None):
+    """A rich device delta log (mt_options.delta_log_mode 1) -> expected_rich's form.  On a
+    segment_ordinals handle every entry also carries [uid, position, ordinal]: with a list
+    `ext`, one (events index, [(uid, position, ordinal tuple | None) per segment]) item per
+    event is appended to it."""
     out, i = [], 0
+    cur = []
 
     def state(ln):
         nonlocal i
@@ -198,11 +202,16 @@ def parse_rich_log(log):
         if np_ >= 0:
             props = tuple((log[i + 2 * q], log[i + 2 * q + 1] & 0xFFFFFFFF) for q in range(np_))
             i += 2 * np_
+        if flags & 4:   # uid, position at the event, ordinal length (-1: none), characters
+            uid, pos, olen = log[i] & 0xFFFFFFFF, log[i + 1], log[i + 2]
+            cur.append((uid, pos, tuple(log[i + 3:i + 3 + olen]) if olen >= 0 else None))
+            i += 3 + max(olen, 0)
         return kind + (props,)
 
     while i < len(log):
         seq, kind, n = log[i:i + 3]
         i += 3
+        cur = []
         if kind >= 0:
             segs = []
             for _ in range(n):
@@ -222,4 +231,42 @@ def parse_rich_log(log):
                 i += 1
                 segs.append((ln, state(ln)))
             out.append(("M", kind, tuple(segs)))
+        if ext is not None:
+            ext.append(cur)
     return out
+
+
+def sorted_segment_ranges(items):
+    """SequenceEvent.ranges (SEQ/sequenceDeltaEvent.ts:40-53): the event's segments added in
+    order to a SortedSegmentSet (MT/sortedSegmentSet.ts:29-84) -- kept sorted by ordinal
+    (JS string order: UTF-16 code units), one whose ordinal is already present dropped (Q8;
+    an undefined ordinal compares false both ways, so it is found "equal" to whatever the
+    binary search probes).  items: [(ordinal tuple | None, payload)]; returns the payloads
+    in the set's order.  (A restatement for the tests, pinned on the reference's own events:
+    tests/test_events.py.)"""
+    out = []
+
+    def lt(a, b):   # a < b as JS compares strings (undefined: never)
+        return a is not None and b is not None and a < b
+
+    for o, payload in items:
+        if not out:
+            out.append((o, payload))
+            continue
+        lo, hi = 0, len(out) - 1
+        while True:
+            mid = lo + (hi - lo) // 2
+            m = out[mid][0]
+            if lt(o, m):             # item at mid > ordinal
+                if lo == mid:
+                    out.insert(mid, (o, payload))
+                    break
+                hi = mid - 1
+            elif lt(m, o):           # item at mid < ordinal
+                if mid == hi:
+                    out.insert(mid + 1, (o, payload))
+                    break
+                lo = mid + 1
+            else:
+                break                # exists: not added
+    return [p for _, p in out]

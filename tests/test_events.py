@@ -1,0 +1,153 @@
+"""SharedSegmentSequence's event objects over the GPU replicas.
+
+The reference builds a SequenceDeltaEvent / SequenceMaintenanceEvent in every callback
+(SEQ/sequence.ts:139-149) whose `ranges` are the callback segments ordered -- and
+deduplicated -- by MergeNode.ordinal through SortedSegmentSet (SEQ/sequenceDeltaEvent.ts:
+40-53, MT/sortedSegmentSet.ts:29-84), each with Client.getPosition(segment) read
+at callback time.  tests/golden/ref_events.json.gz holds, per event of the reference's own
+objects: every callback segment's position and ordinal, and the ranges it kept
+(oracle/ref_harness.mjs events).  A segment_ordinals handle logs each callback segment's id,
+position and ordinal; the events here must equal the reference's exactly."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+
+def _fixture():
+    return gu.load("ref_events")
+
+
+def _split(ev):
+    # ["D", seq, op, isLocal, segs, ranges] / ["M", op, segs, ranges]
+    return (ev[4], ev[5]) if ev[0] == "D" else (ev[2], ev[3])
+
+
+def test_sorted_segment_set_restatement_matches_reference_events():
+    """The test restatement of SortedSegmentSet reproduces the ranges of every reference
+    event from its segments' ordinals (CPU; pins gu.sorted_segment_ranges)."""
+    n = 0
+    for d in _fixture()["docs"]:
+        for ev in d["events"]:
+            segs, ranges = _split(ev)
+            items = [(tuple(o) if o is not None else None, [i, pos]) for i, (pos, o, _) in enumerate(segs)]
+            assert gu.sorted_segment_ranges(items) == ranges, (d["doc"], ev)
+            n += 1
+    assert n > 50000
+
+
+def test_sorted_segment_set_collisions_and_undefined():
+    """Q8 on synthetic ordinals: an equal ordinal is dropped, order follows the ordinal, and an
+    undefined ordinal (a never-linked segment) lands where the binary search stops."""
+    r = gu.sorted_segment_ranges([((63, 7), "a"), ((63, 3), "b"), ((63, 7), "c"), ((31,), "d")])
+    assert r == ["d", "b", "a"]
+    assert gu.sorted_segment_ranges([(None, "x")]) == ["x"]
+    assert gu.sorted_segment_ranges([((5,), "a"), (None, "x")]) == ["a"]
+
+
+# the flat tiers keep ordinals (mt_options.segment_ordinals; the paged layout does not)
+ORD_TIERS = {"lds": dict(lds_seg_capacity=0), "hbm": dict(lds_seg_capacity=-1), "tiny": dict(lds_seg_capacity=16)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tier", list(ORD_TIERS))
+def test_gpu_event_positions_and_ordinals_match_reference(tier):
+    from fluidframework_amd import MergeTreeBatch
+    fx = _fixture()
+    interner = gu.Interner()
+    a = gu.encode_docs(fx, interner)
+    mt = MergeTreeBatch(len(fx["docs"]), delta_log_mode=1, delta_log_capacity=1 << 22, segment_ordinals=1,
+                        seg_capacity=8192, text_capacity=1 << 17, **ORD_TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    for i, doc in enumerate(fx["docs"]):
+        ext = []
+        gu.parse_rich_log(mt.get_delta_log(i), ext)
+        assert len(ext) == len(doc["events"]), doc["doc"]
+        for k, (got, ev) in enumerate(zip(ext, doc["events"])):
+            segs, ranges = _split(ev)
+            want = [(pos, tuple(o) if o is not None else None) for pos, o, _ in segs]
+            assert [(p, o) for _, p, o in got] == want, (doc["doc"], k, ev, got)
+            items = [(o, [j, p]) for j, (_, p, o) in enumerate(got)]
+            assert gu.sorted_segment_ranges(items) == ranges, (doc["doc"], k)
+
+
+@pytest.mark.gpu
+def test_gpu_segment_ordinals_need_flat_tiers():
+    from fluidframework_amd import MergeTreeBatch
+    with pytest.raises(RuntimeError):
+        MergeTreeBatch(2, delta_log_mode=1, delta_log_capacity=1024, segment_ordinals=1, page_capacity=64)
+    with pytest.raises(RuntimeError):   # ordinals ride on the rich log
+        MergeTreeBatch(2, segment_ordinals=1)
+
+
+# ---------------------------------------------------------------- read-outs
+READ_TIERS = dict(ORD_TIERS, paged=dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=2048,
+                                        page_heap_capacity=2048),
+                  tight=dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
+                             lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tier", list(READ_TIERS))
+def test_gpu_readouts_match_reference(tier):
+    """MergeTree.getLength(refSeq, clientId), getContainingSegment(pos, refSeq, clientId) and
+    getPosition (MT/mergeTree.ts:1610-1667, Client.getPosition / getContainingSegment) of the
+    final replicas equal the reference's in the observer's and every writer's views
+    (tests/golden/ref_readouts.json.gz); ordinals too on the flat tiers."""
+    from fluidframework_amd import MergeTreeBatch
+    fx = gu.load("ref_readouts")
+    interner = gu.Interner()
+    a = gu.encode_docs(fx, interner)
+    ords = tier in ORD_TIERS
+    kw = dict(delta_log_mode=1, delta_log_capacity=1 << 22, segment_ordinals=1) if ords else {}
+    mt = MergeTreeBatch(len(fx["docs"]), seg_capacity=8192, text_capacity=1 << 17, **kw, **READ_TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    for i, doc in enumerate(fx["docs"]):
+        refs, clis, want = zip(*doc["lengths"])
+        assert list(mt.get_view_lengths([i] * len(refs), refs, clis)) == list(want), doc["doc"]
+        for pos, ref, cli, exp in doc["containing"]:
+            got = mt.get_containing_segment(i, pos, ref, cli)
+            where = (doc["doc"], pos, ref, cli)
+            if exp is None:
+                assert got is None, where
+                continue
+            offset, vpos, lpos, clen, ordinal, state = exp
+            assert got is not None and (got["offset"], got["position"], got["length"]) == (offset, vpos, clen), (where, got, exp)
+            if "m" in state:
+                assert got["marker_ref_type"] == state["m"], where
+            else:
+                assert got["text"] == state["t"], where
+            if ords:
+                assert got["ordinal"] == ordinal, (where, got["ordinal"], ordinal)
+            # getPosition of the same segment (by id) in the observer's view and in the query's
+            assert mt.get_segment_by_uid(i, got["uid"])["position"] == lpos, where
+            assert mt.get_segment_by_uid(i, got["uid"], ref, cli)["position"] == vpos, where
+    # a segment that left the tree reads as gone (the reference's getPosition walks no parent)
+    assert mt.get_segment_by_uid(0, 0xFFFFFFF) is None
+
+
+def test_reference_ordinal_invariant_holds_on_fixture_streams(tmp_path):
+    """The engine keeps one ordinal character per node because, between messages, every
+    node's ordinal in the reference is its parent's plus one character (checked here on the
+    reference itself over the events streams and the long C3/C4 streams; CPU, needs the
+    transpiled reference of this container)."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not shutil.which("node") or not os.path.isdir(os.path.join(repo, "oracle", "_ref")):
+        pytest.skip("transpiled reference not built here")
+    docs = [dict(doc=d["doc"], seed_text=d["seed_text"], msgs=d["msgs"]) for d in _fixture()["docs"]]
+    for name in ("ref_c3_full", "ref_c4_full"):
+        docs += [dict(doc=f"{name}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in gu.load(name)["docs"][:1]]
+    lp, op = tmp_path / "logs.json", tmp_path / "out.json"
+    lp.write_text(json.dumps({"docs": docs}))
+    subprocess.check_call(["node", os.path.join(repo, "oracle", "ref_harness.mjs"), "ordprobe", str(lp), str(op)])
+    res = json.loads(op.read_text())["docs"]
+    assert sum(r["messages"] for r in res) > 30000
+    assert [r for r in res if r["violation"] is not None] == []
