@@ -2934,6 +2934,8 @@ TD void apply_op(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const G
             op_insert(d, in, tin, pin);
         else if (op.kind == MT_OP_LOAD_REMOVED)
             load_removed(d, op);
+        else if (op.kind == MT_OP_LOAD_ALIASED)
+            fail(d, MT_DOC_ALIASED);
         d.rich = rich;
         return;
     }

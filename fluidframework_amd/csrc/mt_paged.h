@@ -1000,6 +1000,8 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
             pg_op_insert(pd, in, tin, pin);
         else if (op.kind == MT_OP_LOAD_REMOVED)
             pg_load_removed(pd, op);
+        else if (op.kind == MT_OP_LOAD_ALIASED)
+            fail(w, MT_DOC_ALIASED);
         w.rich = rich;
         return;
     }

@@ -1288,7 +1288,9 @@ static std::string validate_batch(uint32_t n_docs, const int64_t *off, const mt_
     if ((uint64_t)off[n_docs] > n_ops) return "doc_op_off exceeds n_ops";
     for (uint64_t k = (uint64_t)off[0]; k < (uint64_t)off[n_docs]; k++) {
         const mt_op_rec &o = ops[k];
-        if (o.kind > MT_OP_LOAD_REMOVED) return "op " + std::to_string(k) + ": unknown kind";
+        if (o.kind > MT_OP_LOAD_ALIASED) return "op " + std::to_string(k) + ": unknown kind";
+        if (o.kind >= MT_OP_LOAD_REMOVED && !(o.flags & MT_F_LOAD))
+            return "op " + std::to_string(k) + ": summary-load record without MT_F_LOAD";
         if ((o.flags & (MT_F_LOCAL | MT_F_ACK)) && !live)
             return "op " + std::to_string(k) + ": local / ack record on a handle without live_client";
         if ((o.flags & MT_F_LOCAL) && (o.flags & MT_F_ACK))
@@ -1862,15 +1864,36 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
             if (segs[i].removed_seq == MT_RSEQ_NONE) obs += (segs[i].flags & MT_F_MARKER) ? 1 : segs[i].len;
         bool in_batch = false;
         int64_t ins = 0;
-        for (int64_t i = sh; i < s1; i++) {
+        // loadBody's batch is never emptied (:207-227): once it was flushed holding a segment
+        // (of non-zero length -- blockInsert skips the others), the next flush (before the
+        // next merge-info spec, or the final one) re-inserts it -> MT_DOC_ALIASED there
+        bool batch_len = false, flushed = false, aliased = false;
+        auto alias = [&]() {
+            mt_op_rec q;
+            memset(&q, 0, sizeof(q));
+            q.kind = MT_OP_LOAD_ALIASED;
+            q.flags = MT_F_LOAD;
+            ops.push_back(q);
+            aliased = true;
+        };
+        for (int64_t i = sh; i < s1 && !aliased; i++) {
             const mt_seg_rec &r = segs[i];
             const int len = (r.flags & MT_F_MARKER) ? 1 : r.len;
             const bool plain = r.client == -2 && r.seq == 0;
             const bool removed = r.removed_seq != MT_RSEQ_NONE;
             if (plain) {
+                if (flushed) continue;   // inserted by the next flush, after the re-insertion
                 if (!in_batch) ins = obs;
                 in_batch = true;
+                batch_len = batch_len || len > 0;
             } else {
+                if (batch_len) {   // flushBatch() before this spec
+                    if (flushed) {
+                        alias();
+                        break;
+                    }
+                    flushed = true;
+                }
                 in_batch = false;
                 ins = obs;
             }
@@ -1899,6 +1922,7 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
             }
             if (!removed) obs += len;
         }
+        if (!aliased && batch_len && flushed) alias();   // the final flushBatch()
     }
     ooff[N] = (int64_t)ops.size();
     if (!ops.empty()) {

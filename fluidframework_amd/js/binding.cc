@@ -106,13 +106,14 @@ napi_value Create(napi_env env, napi_callback_info info) {
                            "propsCapacity", "deltaLogCapacity", "ldsSegCapacity", "pageCapacity",
                            "pageHeapCapacity", "unsettledCapacity", "uidCapacity", "ldsPageCapacity",
                            "ldsUnsettledCapacity", "ldsPageHeapCapacity", "ldsNarrowOverlap", "deltaLogMode",
-                           "liveClient", "liveGroupCapacity", "pagedSlices"};
+                           "liveClient", "liveGroupCapacity", "pagedSlices", "segmentOrdinals"};
     int32_t *fields[] = {&o.device, &o.seg_capacity, &o.block_capacity, &o.heap_capacity, &o.text_capacity,
                          &o.props_capacity, &o.delta_log_capacity, &o.lds_seg_capacity, &o.page_capacity,
                          &o.page_heap_capacity, &o.unsettled_capacity, &o.uid_capacity, &o.lds_page_capacity,
                          &o.lds_unsettled_capacity, &o.lds_page_heap_capacity, &o.lds_narrow_overlap,
-                         &o.delta_log_mode, &o.live_client, &o.live_group_capacity, &o.paged_slices};
-    for (int i = 0; i < 20; i++) {
+                         &o.delta_log_mode, &o.live_client, &o.live_group_capacity, &o.paged_slices,
+                         &o.segment_ordinals};
+    for (int i = 0; i < 21; i++) {
         bool has = false;
         napi_has_named_property(env, argv[1], names[i], &has);
         if (has) {
@@ -209,6 +210,225 @@ napi_value ApplyOps(napi_env env, napi_callback_info info) {
                                 (const uint16_t *)txt, ntxt, (const uint32_t *)props, nprops);
     if (rc) return throw_rc(env, hd, rc, "mt_apply_ops");
     return nullptr;
+}
+
+// applyOpsAsync(h, docOff, ops, text, props) -> Promise: mt_apply_ops on a worker thread
+// (napi_async_work) so the Node thread keeps running while the GPU applies the batch.  The
+// typed arrays are pinned by references until the work completes; the facade issues no other
+// call on the handle meanwhile (a handle is single-writer).
+struct ApplyWork {
+    napi_async_work work = nullptr;
+    napi_deferred deferred = nullptr;
+    napi_ref refs[4] = {nullptr, nullptr, nullptr, nullptr};
+    napi_ref href = nullptr;
+    Handle *hd = nullptr;
+    const int64_t *off = nullptr;
+    const mt_op_rec *ops = nullptr;
+    uint64_t n_ops = 0;
+    const uint16_t *text = nullptr;
+    uint64_t n_text = 0;
+    const uint32_t *props = nullptr;
+    uint64_t n_props = 0;
+    int rc = 0;
+    std::string err;
+};
+void apply_execute(napi_env, void *data) {
+    auto *w = static_cast<ApplyWork *>(data);
+    w->rc = mt_apply_ops(w->hd->h, w->off, w->ops, w->n_ops, w->text, w->n_text, w->props, w->n_props);
+    if (w->rc) w->err = std::string("mt_apply_ops failed (") + std::to_string(w->rc) + "): " + mt_last_error(w->hd->h);
+}
+void apply_complete(napi_env env, napi_status, void *data) {
+    auto *w = static_cast<ApplyWork *>(data);
+    if (w->rc == 0) {
+        napi_value u;
+        napi_get_undefined(env, &u);
+        napi_resolve_deferred(env, w->deferred, u);
+    } else {
+        napi_value msg, e;
+        napi_create_string_utf8(env, w->err.c_str(), NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, nullptr, msg, &e);
+        napi_reject_deferred(env, w->deferred, e);
+    }
+    for (napi_ref r : w->refs)
+        if (r) napi_delete_reference(env, r);
+    if (w->href) napi_delete_reference(env, w->href);
+    napi_delete_async_work(env, w->work);
+    delete w;
+}
+napi_value ApplyOpsAsync(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *off, *ops, *txt, *props;
+    size_t noff, nops, ntxt, nprops;
+    if (!typed(env, argv[1], &off, &noff) || !typed(env, argv[2], &ops, &nops) ||
+        !typed(env, argv[3], &txt, &ntxt) || !typed(env, argv[4], &props, &nprops))
+        return nullptr;
+    if (noff != mt_num_docs(hd->h) + 1 || nops % sizeof(mt_op_rec) != 0) {
+        napi_throw_range_error(env, nullptr, "docOff must hold nDocs + 1 offsets; ops whole 32-byte records");
+        return nullptr;
+    }
+    auto *w = new ApplyWork();
+    w->hd = hd;
+    w->off = (const int64_t *)off;
+    w->ops = (const mt_op_rec *)ops;
+    w->n_ops = nops / sizeof(mt_op_rec);
+    w->text = (const uint16_t *)txt;
+    w->n_text = ntxt;
+    w->props = (const uint32_t *)props;
+    w->n_props = nprops;
+    for (int i = 0; i < 4; i++) NAPI_CALL(env, napi_create_reference(env, argv[1 + i], 1, &w->refs[i]));
+    NAPI_CALL(env, napi_create_reference(env, argv[0], 1, &w->href));
+    napi_value promise, name;
+    NAPI_CALL(env, napi_create_promise(env, &w->deferred, &promise));
+    NAPI_CALL(env, napi_create_string_utf8(env, "mt_apply_ops", NAPI_AUTO_LENGTH, &name));
+    NAPI_CALL(env, napi_create_async_work(env, nullptr, name, apply_execute, apply_complete, w, &w->work));
+    NAPI_CALL(env, napi_queue_async_work(env, w->work));
+    return promise;
+}
+
+// a segment read-out (mt_seg_info) as a JS object, or null
+napi_value seg_info_object(napi_env env, const mt_seg_info &s, const uint16_t *text) {
+    napi_value o, v;
+    if (s.row < 0) {
+        napi_get_null(env, &o);
+        return o;
+    }
+    napi_create_object(env, &o);
+    const struct {
+        const char *k;
+        int64_t v;
+    } fs[] = {{"row", s.row}, {"uid", (int64_t)s.uid}, {"position", s.position}, {"offset", s.offset},
+              {"length", s.length}, {"seq", s.seq}, {"clientId", s.client}, {"removedSeq", s.removed_seq},
+              {"removedClientId", s.removed_client}, {"markerRefType", s.marker_ref_type}};
+    for (const auto &f : fs) {
+        napi_create_int64(env, f.v, &v);
+        napi_set_named_property(env, o, f.k, v);
+    }
+    if (s.marker_ref_type < 0) {
+        napi_create_string_utf16(env, (const char16_t *)text, (size_t)s.text_len, &v);
+        napi_set_named_property(env, o, "text", v);
+    }
+    if (s.ordinal_len >= 0) {
+        napi_create_string_utf16(env, (const char16_t *)s.ordinal, (size_t)s.ordinal_len, &v);
+        napi_set_named_property(env, o, "ordinal", v);
+    }
+    return o;
+}
+// getContainingSegment(h, doc, pos, refSeq, clientId) / getSegmentByUid(h, doc, uid, refSeq,
+// clientId) -> {row, uid, position, offset, length, seq, clientId, removedSeq, removedClientId,
+// markerRefType, text?, ordinal?} | null
+napi_value SegmentQuery(napi_env env, napi_callback_info info, bool by_uid) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    double key = 0;
+    NAPI_CALL(env, napi_get_value_double(env, argv[2], &key));
+    const int32_t ref = get_i32(env, argv[3]), cli = get_i32(env, argv[4]);
+    if (doc >= mt_num_docs(hd->h) || !(key >= 0 && key <= 4294967295.0)) {
+        napi_throw_range_error(env, nullptr, "document index or position out of range");
+        return nullptr;
+    }
+    std::vector<uint16_t> text(1 << 16);
+    mt_seg_info s;
+    const int rc = by_uid ? mt_get_segment_by_uid(hd->h, doc, (uint32_t)key, ref, cli, &s, text.data(), (uint32_t)text.size())
+                          : mt_get_containing_segment(hd->h, doc, (int32_t)key, ref, cli, &s, text.data(),
+                                                      (uint32_t)text.size());
+    if (rc) return throw_rc(env, hd, rc, by_uid ? "mt_get_segment_by_uid" : "mt_get_containing_segment");
+    napi_value o = seg_info_object(env, s, text.data());
+    if (s.row >= 0) {   // its property set: propPairs = [key id, value id]* (null: none)
+        std::vector<uint32_t> pairs(2 * 64);
+        int32_t np = 0;
+        const int rc2 = mt_get_segment_props(hd->h, doc, (uint32_t)s.row, pairs.data(), 64, &np);
+        if (rc2) return throw_rc(env, hd, rc2, "mt_get_segment_props");
+        napi_value v;
+        if (np < 0) {
+            napi_get_null(env, &v);
+        } else {
+            void *pd = nullptr;
+            napi_value ab;
+            NAPI_CALL(env, napi_create_arraybuffer(env, std::max<size_t>(2 * np, 1) * 4, &pd, &ab));
+            memcpy(pd, pairs.data(), 2 * (size_t)np * 4);
+            NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, 2 * (size_t)np, ab, 0, &v));
+        }
+        napi_set_named_property(env, o, "propPairs", v);
+    }
+    return o;
+}
+napi_value GetContainingSegment(napi_env env, napi_callback_info info) { return SegmentQuery(env, info, false); }
+napi_value GetSegmentByUid(napi_env env, napi_callback_info info) { return SegmentQuery(env, info, true); }
+
+// getViewLengths(h, docs: Uint32Array, refSeq: Int32Array, clientId: Int32Array) -> Int32Array
+napi_value GetViewLengths(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    void *docs, *ref, *cli;
+    size_t nd, nr, nc;
+    if (!typed(env, argv[1], &docs, &nd) || !typed(env, argv[2], &ref, &nr) || !typed(env, argv[3], &cli, &nc)) return nullptr;
+    if (nr != nd || nc != nd) {
+        napi_throw_range_error(env, nullptr, "one refSeq and clientId per query");
+        return nullptr;
+    }
+    for (size_t q = 0; q < nd; q++)
+        if (((const uint32_t *)docs)[q] >= mt_num_docs(hd->h)) {
+            napi_throw_range_error(env, nullptr, "document index out of range");
+            return nullptr;
+        }
+    napi_value ab, out;
+    void *pd = nullptr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, std::max<size_t>(nd, 1) * 4, &pd, &ab));
+    const int rc = mt_get_view_lengths(hd->h, (uint32_t)nd, (const uint32_t *)docs, (const int32_t *)ref,
+                                       (const int32_t *)cli, (int32_t *)pd);
+    if (rc) return throw_rc(env, hd, rc, "mt_get_view_lengths");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, nd, ab, 0, &out));
+    return out;
+}
+
+// extractSnapshots(h) -> {counts: BigInt64Array[3 nDocs], segs: Uint8Array (32-byte mt_seg_rec),
+// text: Uint16Array, props: Uint32Array, minSeq: Int32Array, curSeq: Int32Array} --
+// SnapshotV1.extractSync of every document (mt_extract_snapshots; snapshotV1.ts:156-252)
+napi_value ExtractSnapshots(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    Handle *hd = get_handle(env, argv[0]);
+    if (!hd) return nullptr;
+    const uint32_t nd = mt_num_docs(hd->h);
+    std::vector<int64_t> io(3 * (size_t)nd);
+    int rc = mt_extract_snapshots(hd->h, io.data(), nullptr, nullptr, nullptr, nullptr, nullptr);
+    if (rc) return throw_rc(env, hd, rc, "mt_extract_snapshots");
+    uint64_t tr = 0, tt = 0, tp = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+        tr += io[3 * d];
+        tt += io[3 * d + 1];
+        tp += io[3 * d + 2];
+    }
+    struct Arr {
+        const char *name;
+        napi_typedarray_type t;
+        size_t n, esz;
+    } arrs[] = {{"counts", napi_bigint64_array, 3 * (size_t)nd, 8}, {"segs", napi_uint8_array, tr * sizeof(mt_seg_rec), 1},
+                {"text", napi_uint16_array, tt, 2},      {"props", napi_uint32_array, tp, 4},
+                {"minSeq", napi_int32_array, nd, 4},     {"curSeq", napi_int32_array, nd, 4}};
+    napi_value out;
+    NAPI_CALL(env, napi_create_object(env, &out));
+    void *pd[6] = {};
+    for (int i = 0; i < 6; i++) {
+        napi_value ab, a;
+        NAPI_CALL(env, napi_create_arraybuffer(env, std::max<size_t>(arrs[i].n, 1) * arrs[i].esz, &pd[i], &ab));
+        NAPI_CALL(env, napi_create_typedarray(env, arrs[i].t, arrs[i].n, ab, 0, &a));
+        NAPI_CALL(env, napi_set_named_property(env, out, arrs[i].name, a));
+    }
+    memcpy(pd[0], io.data(), io.size() * 8);
+    rc = mt_extract_snapshots(hd->h, (int64_t *)pd[0], (mt_seg_rec *)pd[1], (uint16_t *)pd[2], (uint32_t *)pd[3],
+                              (int32_t *)pd[4], (int32_t *)pd[5]);
+    if (rc) return throw_rc(env, hd, rc, "mt_extract_snapshots");
+    return out;
 }
 
 // loadSnapshots(h, docSegOff: BigInt64Array, nHeader: Int32Array, segs: Uint8Array (32-byte
@@ -563,7 +783,10 @@ napi_value Init(napi_env env, napi_value exports) {
                {"deltaLogReset", DeltaLogReset},
                {"maintenanceCounts", MaintenanceCounts},
                {"checksums", Checksums},   {"lastKernelMs", LastKernelMs}, {"numDocs", NumDocs},
-               {"regeneratePending", RegeneratePending}, {"decodeSummaries", DecodeSummaries}};
+               {"regeneratePending", RegeneratePending}, {"decodeSummaries", DecodeSummaries},
+               {"applyOpsAsync", ApplyOpsAsync},         {"getContainingSegment", GetContainingSegment},
+               {"getSegmentByUid", GetSegmentByUid},     {"getViewLengths", GetViewLengths},
+               {"extractSnapshots", ExtractSnapshots}};
     for (auto &f : fns) {
         napi_value v;
         NAPI_CALL(env, napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v));

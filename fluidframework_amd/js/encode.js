@@ -322,6 +322,13 @@ class BatchEncoder {
                 members(msg.__ack, 0, F_ACK);
                 continue;
             }
+            if (msg.__update !== undefined) {       // Client.updateSeqNumbers(msn, seq) (client.ts:821-828)
+                this._rec({
+                    seq: msg.__update.seq, refSeq: msg.__update.seq, minSeq: msg.__update.msn, client: 0,
+                    kind: OP_NOOP, flags: 0, props: NO_PROPS, pos1: 0, pos2: 0, payload: 0,
+                });
+                continue;
+            }
             const c = short(msg.clientId);
             if (msg.type !== undefined && msg.type !== "op") {
                 this._rec({

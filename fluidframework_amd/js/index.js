@@ -6,9 +6,14 @@
  * include/mt_replay.h, through the N-API addon js/binding.cc).  batch.client(doc) returns a
  * Client-shaped view of one document with the surface SharedSegmentSequence uses on the
  * reference Client (merge-tree/src/client.ts:43; sequence/src/sequence.ts:131-142,
- * 473-600): applyMsg, startOrUpdateCollaboration, getLength, getText (as
- * createTextHelper().getText), getPropertiesAtPosition, getCurrentSeq and the
- * mergeTreeDeltaCallback property.
+ * 240-251, 473-600): applyMsg, startOrUpdateCollaboration, getLength, getText (as
+ * createTextHelper().getText), getPropertiesAtPosition, getPosition, getContainingSegment,
+ * getCurrentSeq, getShortClientId / getLongClientId, snapshot, the mergeTreeDeltaCallback /
+ * mergeTreeMaintenanceCallback properties and a `mergeTree` view (getLength(refSeq,
+ * clientId), getPosition, getContainingSegment).  Callback segments are objects kept per
+ * segment id (a segment is the same object in every event, as in the reference) with the
+ * state, cachedLength and ordinal they had at the event, so SharedSegmentSequence's own
+ * SequenceDeltaEvent (sequence/src/sequenceDeltaEvent.ts) runs unchanged on a GpuClient.
  *
  * applyMsg only queues the message (the GPU applies whole batches); any read, or an
  * explicit batch.flush(), applies everything queued for every document in one launch.
@@ -19,7 +24,10 @@
 const assert = require("assert");
 const path = require("path");
 const { BatchEncoder, Interner, VAL_NULL } = require("./encode");
-const { treeChunks } = require("./snapshot");
+const { treeChunks, recordSpecs, emitTree } = require("./snapshot");
+
+// segment object -> its device id (mt_seg_info.uid) for getPosition outside a callback
+const segUid = new WeakMap();
 
 const native = require(path.join(__dirname, "mtreplay.node"));
 
@@ -35,6 +43,9 @@ const DOC_STATUS = {
     8: () => new assert.AssertionError({ message: "Incoming op sequence# < minSequence#" }),
     // (Node's message for a bare assert(): what the reference throws on this runtime)
     9: () => new assert.AssertionError({ message: "false == true" }),
+    // SnapshotLoader.loadBody re-inserted segments of its never-emptied batch (mt_types.h)
+    10: () => new Error("merge-tree replay: the summary body makes SnapshotLoader insert segments twice " +
+        "(snapshotLoader.ts:207-227); the document is not replayed past that point"),
 };
 
 /** JS own-key order: integer-like keys ascending first, then insertion order. */
@@ -90,6 +101,13 @@ class GpuMergeTreeBatch {
             options = Object.assign({}, options, { deltaLogMode: 1 });
         }
         this.rich = !!options.deltaLogCapacity && options.deltaLogMode === 1;
+        // event handles keep segment ordinals (SequenceDeltaEvent orders ranges by them); the
+        // paged layout keeps none
+        if (this.rich && !options.pageCapacity && options.segmentOrdinals === undefined) {
+            options = Object.assign({}, options, { segmentOrdinals: 1 });
+        }
+        this.ordinals = !!options.segmentOrdinals;
+        this.chunkSize = options.mergeTreeSnapshotChunkSize || 10000;   // SnapshotV1.chunkSize
         // live-client batches (liveClient: 1) back participant Clients: local ops, acks and
         // reconnect regeneration (SURVEY §8f #4); they replay from HBM (ldsSegCapacity -1)
         this.live = !!options.liveClient;
@@ -104,10 +122,17 @@ class GpuMergeTreeBatch {
         this.views = new Map();
         this.logPos = new Int32Array(nDocs);
         this.wantsDeltas = !!options.deltaLogCapacity;
+        this.segObjs = Array.from({ length: nDocs }, () => new Map());   // per document: id -> segment
+        this.inflight = null;
+    }
+
+    _idle() {
+        if (this.inflight) { throw new Error("merge-tree replay: a flushAsync() is in flight on this batch"); }
     }
 
     /** Initial contents of every document (Client.insertSegmentLocal before collaboration). */
     loadInitialText(texts) {
+        this._idle();
         assert(texts.length === this.nDocs);
         let total = 0;
         for (const t of texts) { total += t.length; }
@@ -121,6 +146,7 @@ class GpuMergeTreeBatch {
         off[this.nDocs] = BigInt(k);
         native.loadInitialText(this.h, off, seed);
         this.logPos.fill(0);
+        this.segObjs = Array.from({ length: this.nDocs }, () => new Map());
     }
 
     /**
@@ -137,6 +163,7 @@ class GpuMergeTreeBatch {
         native.loadSnapshots(this.h, a.docSegOff, a.nHeader, a.segs, a.text, a.props, a.minSeq, a.curSeq);
         this.failed.fill(0);
         this.logPos.fill(0);
+        this.segObjs = Array.from({ length: this.nDocs }, () => new Map());
         const st = native.status(this.h);
         for (let d = 0; d < this.nDocs; d++) {
             this.clients[d] = a.clients[d];
@@ -156,9 +183,7 @@ class GpuMergeTreeBatch {
         return v;
     }
 
-    /** Applies every queued message of every document (one mt_apply_ops). */
-    flush() {
-        if (this.queued === 0) { return; }
+    _encodePending() {
         const enc = new BatchEncoder(this.interner);
         this.applied = this.pending;   // the messages of this flush, for the callbacks' opArgs
         for (let d = 0; d < this.nDocs; d++) {
@@ -166,8 +191,37 @@ class GpuMergeTreeBatch {
         }
         this.pending = Array.from({ length: this.nDocs }, () => []);
         this.queued = 0;
-        const a = enc.arrays();
+        return enc.arrays();
+    }
+
+    /** Applies every queued message of every document (one mt_apply_ops). */
+    flush() {
+        this._idle();
+        if (this.queued === 0) { return; }
+        const a = this._encodePending();
         native.applyOps(this.h, a.docOff, a.ops, a.text, a.props);
+        this._afterApply();
+    }
+
+    /**
+     * flush() with the GPU work on a worker thread (napi_async_work): resolves once the batch
+     * is applied and its callbacks have fired.  Messages queued meanwhile wait for the next
+     * flush; any other call on the batch throws until it resolves (a handle is single-writer).
+     */
+    async flushAsync() {
+        while (this.inflight) { await this.inflight.catch(() => undefined); }
+        if (this.queued === 0) { return; }
+        const a = this._encodePending();
+        this.inflight = native.applyOpsAsync(this.h, a.docOff, a.ops, a.text, a.props);
+        try {
+            await this.inflight;
+        } finally {
+            this.inflight = null;
+        }
+        this._afterApply();
+    }
+
+    _afterApply() {
         const st = native.status(this.h);
         for (let d = 0; d < this.nDocs; d++) {
             if (st[d] !== 0 && this.failed[d] === 0) { this.failed[d] = st[d]; }
@@ -185,6 +239,38 @@ class GpuMergeTreeBatch {
     }
 
     status() { this.flush(); return native.status(this.h); }
+
+    /**
+     * Client.snapshot for every document (client.ts:901-937, new summary format): each
+     * document's SnapshotV1 ITree (snapshotV1.ts:87-252), extracted on the GPU
+     * (mt_extract_snapshots) and emitted as the reference's JSON blobs.
+     */
+    snapshots() {
+        this.flush();
+        const ex = native.extractSnapshots(this.h);
+        const out = [];
+        let r0 = 0, t0 = 0, p0 = 0;
+        for (let d = 0; d < this.nDocs; d++) {
+            const nr = Number(ex.counts[3 * d]), nt = Number(ex.counts[3 * d + 1]), np = Number(ex.counts[3 * d + 2]);
+            const segs = ex.segs.subarray(32 * r0, 32 * (r0 + nr));
+            const names = this._clientNames(d);
+            const { specs, lengths } = recordSpecs(segs, ex.text.subarray(t0, t0 + nt), ex.props.subarray(p0, p0 + np),
+                this.interner, names);
+            out.push(emitTree(specs, lengths, ex.minSeq[d], ex.curSeq[d], this.chunkSize));
+            r0 += nr;
+            t0 += nt;
+            p0 += np;
+        }
+        return { trees: out, minSeq: ex.minSeq, curSeq: ex.curSeq };
+    }
+
+    // short client id -> long id of document d (0: the replica's own id)
+    _clientNames(d) {
+        const inv = new Map();
+        for (const [k, v] of this.clients[d]) { if (!inv.has(v)) { inv.set(v, k); } }
+        const v = this.views.get(d);
+        return (id) => (id === 0 && v && v.longClientId !== undefined ? v.longClientId : inv.get(id));
+    }
 
     /** mt_checksum per document: {length, nSegments, textHash, propsHash, deltaHash}. */
     checksums() {
@@ -411,18 +497,32 @@ class GpuClient {
         return { split: m[3 * this.doc], append: m[3 * this.doc + 1], unlink: m[3 * this.doc + 2] };
     }
 
-    /** A segment's state at an event (rich log), as the ISegment fields listeners read. */
+    /**
+     * A segment's state at an event (rich log), as the ISegment fields listeners read.  On an
+     * ordinals handle the entry also names the segment (its id: the same object is reused for
+     * it in every event, as the reference passes one ISegment) and carries the position
+     * Client.getPosition reads at the event and the segment's ordinal.  Returns [seg, i, pos].
+     */
     _segment(log, i, len) {
         const flags = log[i++];
-        let seg;
+        const st = { cachedLength: len };
         if (flags & 1) {
-            seg = { type: "Marker", refType: log[i++], cachedLength: len };
+            st.type = "Marker";
+            st.refType = log[i++];
         } else {
             const words = (len + 1) >> 1;
-            const units = new Array(len);
-            for (let u = 0; u < len; u++) { const w = log[i + (u >> 1)]; units[u] = (u & 1) ? (w >>> 16) : (w & 0xFFFF); }
+            let text = "";
+            for (let u = 0; u < len; u += 2048) {
+                const units = [];
+                for (let k = u; k < Math.min(len, u + 2048); k++) {
+                    const w = log[i + (k >> 1)];
+                    units.push((k & 1) ? (w >>> 16) : (w & 0xFFFF));
+                }
+                text += String.fromCharCode(...units);
+            }
             i += words;
-            seg = { type: "TextSegment", text: String.fromCharCode(...units), cachedLength: len };
+            st.type = "TextSegment";
+            st.text = text;
         }
         const np = log[i++];
         if (np >= 0) {
@@ -431,10 +531,143 @@ class GpuClient {
                 pairs.push([this.batch.interner.keyName(log[i]), this.batch.interner.value(log[i + 1] >>> 0)]);
                 i += 2;
             }
-            seg.properties = {};
-            for (const [k, v] of jsKeyOrder(pairs)) { seg.properties[k] = v; }
+            st.properties = {};
+            for (const [k, v] of jsKeyOrder(pairs)) { st.properties[k] = v; }
         }
-        return [seg, i];
+        let seg = st, pos;
+        if (flags & 4) {   // [uid, position at the event, ordinal length (-1: none), characters]
+            const uid = log[i] >>> 0, olen = log[i + 2];
+            pos = log[i + 1];
+            st.ordinal = olen >= 0 ? String.fromCharCode(...log.subarray(i + 3, i + 3 + olen)) : undefined;
+            i += 3 + Math.max(olen, 0);
+            seg = this._segObject(uid, st);
+        }
+        return [seg, i, pos];
+    }
+
+    // the document's object for segment `uid` (0: never linked -- a fresh object), updated to `st`
+    _segObject(uid, st) {
+        const objs = this.batch.segObjs[this.doc];
+        let seg = uid ? objs.get(uid) : undefined;
+        if (seg === undefined) {
+            seg = {};
+            if (uid) {
+                objs.set(uid, seg);
+                segUid.set(seg, uid);
+            }
+        }
+        for (const k of ["text", "refType", "properties"]) { if (!(k in st)) { delete seg[k]; } }
+        Object.assign(seg, st);
+        return seg;
+    }
+
+    // a read-out (native getContainingSegment / getSegmentByUid) as the segment's object
+    _segFromInfo(r) {
+        const st = { cachedLength: r.length, seq: r.seq, clientId: r.clientId };
+        if (r.markerRefType >= 0) {
+            st.type = "Marker";
+            st.refType = r.markerRefType;
+        } else {
+            st.type = "TextSegment";
+            st.text = r.text;
+        }
+        if (r.removedSeq !== -2147483648) {
+            st.removedSeq = r.removedSeq;
+            st.removedClientId = r.removedClientId;
+        }
+        if (r.propPairs) {
+            const pairs = [];
+            for (let j = 0; j < r.propPairs.length; j += 2) {
+                pairs.push([this.batch.interner.keyName(r.propPairs[j]), this.batch.interner.value(r.propPairs[j + 1])]);
+            }
+            st.properties = {};
+            for (const [k, v] of jsKeyOrder(pairs)) { st.properties[k] = v; }
+        }
+        if (r.ordinal !== undefined) { st.ordinal = r.ordinal; }
+        return this._segObject(r.uid, st);
+    }
+
+    /**
+     * Client.getPosition(segment) (client.ts:291-293, mergeTree.ts:1619-1636).  Inside a
+     * callback, a segment of that event reads the position it had when the reference fired it
+     * (what SequenceDeltaEvent.ranges computes); otherwise the segment's position after the
+     * last flush -- 0 once it left the tree (the reference walks no parent then).
+     */
+    getPosition(segment) {
+        if (this._evPos !== undefined && this._evPos.has(segment)) { return this._evPos.get(segment); }
+        return this.mergeTree.getPosition(segment, this.currentSeq, 0);
+    }
+
+    /** Client.getContainingSegment(pos) (client.ts:1006-1009, mergeTree.ts:1656-1667). */
+    getContainingSegment(pos) {
+        return this.mergeTree.getContainingSegment(pos, this.currentSeq, 0);
+    }
+
+    /** Client.getShortClientId / getLongClientId (client.ts:637-661): the observer is 0. */
+    getShortClientId(longClientId) {
+        if (longClientId === this.longClientId) { return 0; }
+        return this.batch.clients[this.doc].get(longClientId);
+    }
+
+    getLongClientId(shortClientId) { return this.batch._clientNames(this.doc)(shortClientId); }
+
+    getClientId() { return 0; }
+
+    /**
+     * The MergeTree methods SharedSegmentSequence and its users reach through client.mergeTree
+     * (mergeTree.ts:1610-1667): views (refSeq, clientId) with short client ids; a remote view
+     * must be one the client can still hold (include/mt_replay.h "segment read-outs").
+     */
+    get mergeTree() {
+        if (this._mt === undefined) {
+            const self = this;
+            const h = () => self.batch.h;
+            this._mt = {
+                get length() { return self.getLength(); },
+                getLength(refSeq, clientId) {
+                    self._sync();
+                    return native.getViewLengths(h(), Uint32Array.of(self.doc), Int32Array.of(refSeq),
+                        Int32Array.of(clientId))[0];
+                },
+                getPosition(segment, refSeq, clientId) {
+                    const uid = segUid.get(segment);
+                    if (uid === undefined) { return 0; }
+                    self._sync();
+                    const r = native.getSegmentByUid(h(), self.doc, uid, refSeq, clientId);
+                    return r === null ? 0 : r.position;
+                },
+                getContainingSegment(pos, refSeq, clientId) {
+                    self._sync();
+                    const r = native.getContainingSegment(h(), self.doc, pos, refSeq, clientId);
+                    return r === null ? { segment: undefined, offset: undefined }
+                        : { segment: self._segFromInfo(r), offset: r.offset };
+                },
+                get mergeTreeDeltaCallback() { return self.mergeTreeDeltaCallback; },
+                set mergeTreeDeltaCallback(f) { self.mergeTreeDeltaCallback = f; },
+                get mergeTreeMaintenanceCallback() { return self.mergeTreeMaintenanceCallback; },
+                set mergeTreeMaintenanceCallback(f) { self.mergeTreeMaintenanceCallback = f; },
+            };
+        }
+        return this._mt;
+    }
+
+    /**
+     * Client.snapshot(runtime, handle, catchUpMsgs) (client.ts:901-937) in the new summary
+     * format (mergeTree options newMergeTreeSnapshotFormat): updateSeqNumbers(the runtime's
+     * minimumSequenceNumber, lastSequenceNumber), then SnapshotV1.extractSync + emit
+     * (snapshotV1.ts:87-252) -> the ITree, blobs byte-equal with the reference's.
+     */
+    snapshot(runtime, handle, catchUpMsgs) {
+        assert(catchUpMsgs === undefined || catchUpMsgs.length === 0, "New format should not emit catchup ops");
+        const dm = runtime.deltaManager;
+        this._check();
+        this.batch.pending[this.doc].push({ __update: { seq: dm.lastSequenceNumber, msn: dm.minimumSequenceNumber } });
+        this.batch.queued++;
+        this.currentSeq = Math.max(this.currentSeq, dm.lastSequenceNumber);
+        this._sync();
+        const s = this.batch.snapshots();
+        assert.strictEqual(s.minSeq[this.doc], dm.minimumSequenceNumber);
+        return s.trees[this.doc];
     }
 
     /**
@@ -442,8 +675,8 @@ class GpuClient {
      * mergeTreeDeltaCallback(opArgs, {operation, deltaSegments}) (mergeTreeDeltaCallback.ts:
      * 33-59; call sites mergeTree.ts:2014-2021, 2625-2632, 2738-2745) with opArgs {op,
      * sequencedMessage, groupOp} and deltaSegments [{segment, propertyDeltas}] -- segment =
-     * the segment's state at the event (cachedLength, text or refType, properties) plus its
-     * observer `position` at callback time (what SequenceDeltaEvent.ranges reads) -- and
+     * the segment's state at the event (cachedLength, text or refType, properties, ordinal)
+     * plus our `position` field (its observer position at callback time) -- and
      * mergeTreeMaintenanceCallback({operation: SPLIT -2 | APPEND -1 | UNLINK -3,
      * deltaSegments}) (mergeTree.ts:1343-1373, 2264-2269), in the reference's order.
      */
@@ -452,12 +685,14 @@ class GpuClient {
         const rich = this.batch.rich;
         const log = native.getDeltaLog(this.batch.h, this.doc);
         const msgs = (this.batch.applied && this.batch.applied[this.doc]) || [];
+        const objs = this.batch.segObjs[this.doc];
         let mi = 0, member = 0, lastSeq = null;
         let i = this.batch.logPos[this.doc];
         while (i + 3 <= log.length) {
             const seq = log[i], kind = log[i + 1], n = log[i + 2];
             i += 3;
             const deltaSegments = [];
+            const evPos = new Map();
             for (let s = 0; s < n; s++) {
                 const pos = kind >= 0 ? log[i++] : -1;
                 const len = log[i++];
@@ -481,8 +716,9 @@ class GpuClient {
                 } else {
                     delta = {};
                 }
-                let segment = { cachedLength: len };
-                if (rich) { [segment, i] = this._segment(log, i, len); }
+                let segment = { cachedLength: len }, epos;
+                if (rich) { [segment, i, epos] = this._segment(log, i, len); }
+                if (epos !== undefined) { evPos.set(segment, epos); }
                 delta.segment = segment;
                 if (kind >= 0) {
                     // a zero-length insert's segment is never linked (blockInsert skips it,
@@ -491,47 +727,38 @@ class GpuClient {
                 }
                 deltaSegments.push(delta);
             }
-            if (kind < 0) {
-                if (mcb) { mcb({ operation: kind, deltaSegments }); }
-                continue;
+            this._evPos = evPos;
+            try {
+                if (kind < 0) {
+                    if (mcb) { mcb({ operation: kind, deltaSegments }); }
+                    // the segment an UNLINK drops / an APPEND absorbs leaves the tree
+                    const gone = kind === -3 ? deltaSegments[0] : (kind === -1 ? deltaSegments[1] : undefined);
+                    if (gone !== undefined && segUid.has(gone.segment)) { objs.delete(segUid.get(gone.segment)); }
+                    continue;
+                }
+                if (seq === -1) {
+                    // live client: the local client's own op (no sequencedMessage), in queue order
+                    while (mi < msgs.length && msgs[mi].__local === undefined) { mi++; }
+                    const op = mi < msgs.length ? msgs[mi++].__local : undefined;
+                    lastSeq = null;
+                    if (cb) { cb({ op }, { operation: kind, deltaSegments }); }
+                    continue;
+                }
+                // opArgs: the message with this sequence number; a GROUP's members in order
+                if (seq !== lastSeq) { member = 0; lastSeq = seq; } else { member++; }
+                while (mi < msgs.length && (msgs[mi].__local !== undefined || msgs[mi].__ack !== undefined ||
+                    msgs[mi].__update !== undefined || msgs[mi].sequenceNumber !== seq)) { mi++; }
+                const msg = mi < msgs.length ? msgs[mi] : { sequenceNumber: seq };
+                const contents = msg.contents;
+                const isGroup = contents && contents.type === 3;
+                const opArgs = { op: isGroup ? contents.ops[member] : contents, sequencedMessage: msg };
+                if (isGroup) { opArgs.groupOp = contents; }
+                if (cb) { cb(opArgs, { operation: kind, deltaSegments }); }
+            } finally {
+                this._evPos = undefined;
             }
-            if (seq === -1) {
-                // live client: the local client's own op (no sequencedMessage), in queue order
-                while (mi < msgs.length && msgs[mi].__local === undefined) { mi++; }
-                const op = mi < msgs.length ? msgs[mi++].__local : undefined;
-                lastSeq = null;
-                if (cb) { cb({ op }, { operation: kind, deltaSegments }); }
-                continue;
-            }
-            // opArgs: the message with this sequence number; a GROUP's members in order
-            if (seq !== lastSeq) { member = 0; lastSeq = seq; } else { member++; }
-            while (mi < msgs.length && (msgs[mi].__local !== undefined || msgs[mi].__ack !== undefined ||
-                msgs[mi].sequenceNumber !== seq)) { mi++; }
-            const msg = mi < msgs.length ? msgs[mi] : { sequenceNumber: seq };
-            const contents = msg.contents;
-            const isGroup = contents && contents.type === 3;
-            const opArgs = { op: isGroup ? contents.ops[member] : contents, sequencedMessage: msg };
-            if (isGroup) { opArgs.groupOp = contents; }
-            if (cb) { cb(opArgs, { operation: kind, deltaSegments }); }
         }
         this.batch.logPos[this.doc] = i;
-    }
-
-    /**
-     * SequenceDeltaEvent (sequence/src/sequenceDeltaEvent.ts:26-118) for a callback's
-     * arguments: ranges in document order with the positions the callback carries.  (The
-     * reference sorts by segment ordinal and drops ranges whose ordinals collide, SURVEY Q8;
-     * the positions here are exact.)
-     */
-    static sequenceDeltaEvent(opArgs, deltaArgs, clientId) {
-        const ranges = deltaArgs.deltaSegments.filter((d) => d.position >= 0)
-            .map((d) => ({ operation: deltaArgs.operation, position: d.position, propertyDeltas: d.propertyDeltas,
-                segment: d.segment }))
-            .sort((a, b) => a.position - b.position);
-        return {
-            opArgs, deltaArgs, isLocal: opArgs.sequencedMessage === undefined, isEmpty: deltaArgs.deltaSegments.length === 0,
-            deltaOperation: deltaArgs.operation, ranges, first: ranges[0], last: ranges[ranges.length - 1], clientId,
-        };
     }
 }
 

@@ -181,4 +181,88 @@ class SnapshotEncoder {
     }
 }
 
-module.exports = { SnapshotEncoder, decodeChunks, treeChunks, toLatestVersion };
+/**
+ * Summary emission from mt_extract_snapshots records (one document): ISegment.toJSONObject
+ * (textSegment.ts:48-54, mergeTree.ts:478-482, 690-694) with extractSync's merge-info wrapper
+ * (snapshotV1.ts:222-241) -> {specs, lengths}.  `names[short id]` = the long client id.
+ */
+function recordSpecs(segs, text, props, interner, names) {
+    const dv = new DataView(segs.buffer, segs.byteOffset, segs.byteLength);
+    const specs = [], lengths = [];
+    for (let r = 0; r + SEG_BYTES <= segs.byteLength; r += SEG_BYTES) {
+        const len = dv.getInt32(r, true), seq = dv.getInt32(r + 4, true), rseq = dv.getInt32(r + 8, true);
+        const payload = dv.getUint32(r + 12, true), pr = dv.getUint32(r + 16, true);
+        const client = dv.getInt16(r + 20, true), rcli = dv.getInt16(r + 22, true), flags = dv.getUint8(r + 24);
+        let propsObj;
+        if (pr !== NO_PROPS) {
+            propsObj = {};   // V8 orders integer-like keys first, as the reference's objects
+            for (let j = 0; j < props[pr]; j++) {
+                propsObj[interner.keyName(props[pr + 1 + 2 * j])] = interner.value(props[pr + 2 + 2 * j] >>> 0);
+            }
+        }
+        let js;
+        if (flags & F_MARKER) {
+            js = { marker: { refType: payload } };
+            if (propsObj !== undefined) { js.props = propsObj; }
+        } else {
+            let t = "";
+            for (let i = 0; i < len; i += 4096) {
+                t += String.fromCharCode.apply(null, Array.from(text.subarray(payload + i, payload + Math.min(len, i + 4096))));
+            }
+            js = propsObj === undefined ? t : { text: t, props: propsObj };
+        }
+        if (flags & SEG_MERGE_INFO) {
+            const raw = { json: js };
+            if (flags & SEG_HAS_SEQ) {
+                raw.seq = seq;
+                raw.client = names(client);
+            }
+            if (rseq !== RSEQ_NONE) {
+                raw.removedSeq = rseq;
+                raw.removedClient = names(rcli);
+            }
+            js = raw;
+        }
+        specs.push(js);
+        lengths.push(len);
+    }
+    return { specs, lengths };
+}
+
+/**
+ * SnapshotV1.emit (snapshotV1.ts:87-154): chunks of >= chunkSize units (getSeqLengthSegs
+ * :59-81), the first is the header with the metadata; every blob is JSON.stringify of its
+ * MergeTreeChunkV1 (serializeAsMaxSupportedVersion, snapshotChunks.ts:124-134).  Returns the
+ * ITree a summarizer uploads.
+ */
+function emitTree(specs, lengths, minSeq, curSeq, chunkSize = 10000) {
+    const header = { minSequenceNumber: minSeq, sequenceNumber: curSeq, orderedChunkMetadata: [],
+        totalLength: 0, totalSegmentCount: 0 };
+    const chunks = [];
+    do {
+        const start = header.totalSegmentCount;
+        const segments = [];
+        let length = 0, count = 0;
+        while (length < chunkSize && start + count < specs.length) {
+            segments.push(specs[start + count]);
+            length += lengths[start + count];
+            count++;
+        }
+        chunks.push({ version: "1", segmentCount: count, length, segments, startIndex: start });
+        header.totalSegmentCount += count;
+        header.totalLength += length;
+    } while (header.totalSegmentCount < specs.length);
+    const head = chunks.shift();
+    head.headerMetadata = header;
+    header.orderedChunkMetadata = [{ id: "header" }];
+    const blob = (path, chunk) => ({ mode: "100644", path, type: "Blob",
+        value: { contents: JSON.stringify(chunk), encoding: "utf-8" } });
+    const entries = chunks.map((ch, i) => {
+        const id = `body_${i}`;
+        header.orderedChunkMetadata.push({ id });
+        return blob(id, ch);
+    });
+    return { entries: [blob("header", head), ...entries], id: null };
+}
+
+module.exports = { SnapshotEncoder, decodeChunks, treeChunks, toLatestVersion, recordSpecs, emitTree };

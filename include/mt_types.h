@@ -27,8 +27,10 @@ enum mt_op_kind {
     MT_OP_REMOVE = 1,     /* MergeTreeDeltaType.REMOVE   MT/ops.ts:31 */
     MT_OP_ANNOTATE = 2,   /* MergeTreeDeltaType.ANNOTATE MT/ops.ts:32 */
     MT_OP_NOOP = 3,       /* non-"op" message: seq/msn update only */
-    MT_OP_LOAD_REMOVED = 4 /* internal (summary load): removal info of the segment the
+    MT_OP_LOAD_REMOVED = 4, /* internal (summary load): removal info of the segment the
                               preceding MT_F_LOAD insert appended */
+    MT_OP_LOAD_ALIASED = 5 /* internal (summary load): loadBody re-inserts segments that are
+                              already in the tree (MT_DOC_ALIASED) */
 };
 
 enum mt_op_flags {
@@ -121,7 +123,13 @@ enum mt_doc_status {
     MT_DOC_INTERNAL = 6,        /* engine invariant violated (bug) */
     MT_DOC_SEQ_BACKWARDS = 7,   /* assert currentSeq <= seq    MT/client.ts:824 (updateSeqNumbers) */
     MT_DOC_MSN_ABOVE_SEQ = 8,   /* assert min <= seq           MT/client.ts:826 (updateSeqNumbers) */
-    MT_DOC_MSN_BACKWARDS = 9    /* assert minSeq <= msn        MT/mergeTree.ts:1755 (setMinSeq) */
+    MT_DOC_MSN_BACKWARDS = 9,   /* assert minSeq <= msn        MT/mergeTree.ts:1755 (setMinSeq) */
+    /* Summary load: SnapshotLoader.loadBody never empties its batch of plain segments
+       (MT/snapshotLoader.ts:207-227), so a flush after the first one appends segments that
+       are already in the tree -- one ISegment object at two places.  The reference carries
+       on with that tree (its later setOrdinal asserts, MT/mergeTree.ts:366-368, come from
+       it); the engine stops the document at the re-insertion. */
+    MT_DOC_ALIASED = 10
 };
 
 #ifdef __cplusplus

@@ -899,16 +899,28 @@ orc_doc *orc_load(const mt_seg_rec *recs, int32_t n_header, int32_t n_total, con
     int nb = n_total - n_header;
     Seg **batch = (Seg **)malloc(sizeof(Seg *) * (nb > 0 ? nb : 1));
     int nbatch = 0;
+    /* the batch is never emptied (:207-227): once flushed holding a segment of non-zero
+       length, the next flush re-inserts it -- the reference's tree then holds one segment
+       object twice; the restatement stops there (MT_DOC_ALIASED) */
+    int batch_len = 0, flushed = 0;
     for (int i = n_header; i < n_total && !d->status; i++) {
         Seg *s = seg_from_rec(d, &recs[i], text_arena, props_arena);
         if (s->client == -2 && s->seq == 0) {
+            if (flushed) continue;
             batch[nbatch++] = s;
+            batch_len |= s->len > 0;
         } else {
+            if (batch_len && flushed) {
+                d->status = MT_DOC_ALIASED;
+                break;
+            }
             if (nbatch) load_append(d, batch, nbatch, -2, 0);
+            if (batch_len) flushed = 1;
             nbatch = 0;
             if (!d->status) load_append(d, &s, 1, s->client, s->seq);
         }
     }
+    if (!d->status && batch_len && flushed) d->status = MT_DOC_ALIASED;   /* the final flushBatch() */
     if (nbatch && !d->status) load_append(d, batch, nbatch, -2, 0);
     free(batch);
     return d;

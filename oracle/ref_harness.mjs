@@ -575,14 +575,31 @@ function treeChunks(tree) {
     return out;
 }
 
-async function loadClient(tree, options) {
+// `aliased`: loadBody inserted a segment that was already in the tree (its batch of plain
+// segments is never emptied, MT/snapshotLoader.ts:207-227) -- observed on the reference's
+// own insertSegments during the load (MT_DOC_ALIASED)
+async function loadClient(tree, options, probe) {
     const c = new Client(segmentFromSpec, logger, options || {});
     const runtime = { logger: loaderLogger, clientId: "loader", options: {} };
     const content = tree.entries.find((e) => e.type === "Tree" && e.path === "content");
     const storage = new MockStorage(content ? content.value : tree);
-    const { catchupOpsP } = await c.load(runtime, storage);
-    const catchup = await catchupOpsP;
-    return { c, catchup };
+    const mt = c.mergeTree;
+    const insert = mt.insertSegments;
+    if (probe) {
+        mt.insertSegments = function (pos, segments, ...rest) {
+            if (!probe.aliased && segments.some((sg) => sg.parent !== undefined && sg.cachedLength > 0)) {
+                probe.aliased = true;
+            }
+            return insert.call(this, pos, segments, ...rest);
+        };
+    }
+    try {
+        const { catchupOpsP } = await c.load(runtime, storage);
+        const catchup = await catchupOpsP;
+        return { c, catchup };
+    } finally {
+        if (probe) { delete mt.insertSegments; }
+    }
 }
 
 function attachDeltas(c) {
@@ -675,12 +692,15 @@ async function snapDoc(cfg, doc) {
     const chunks = treeChunks(tree);
     const rec = { doc, seed_text: seedText, msgs, chunks };
     let loaded;
+    const probe = { aliased: false };
     try {
-        loaded = await loadClient(tree, {});
+        loaded = await loadClient(tree, {}, probe);
     } catch (e) {
         rec.error = String(e.message || e).split(":")[0];
+        if (probe.aliased) { rec.aliased = true; }
         return rec;
     }
+    if (probe.aliased) { rec.aliased = true; }
     const c2 = loaded.c;
     rec.observer = c2.getShortClientId("loader");
     rec.load_out = collectOutputs(c2, []);
@@ -709,7 +729,9 @@ async function loadFileDoc(path, cfg, doc) {
     const tree = JSON.parse(fs.readFileSync(path, "utf8"));
     const chunks = treeChunks(tree);
     const rec = { doc, file: path.split("/").slice(-2).join("/"), chunks };
-    const { c, catchup } = await loadClient(tree, {});
+    const probe = { aliased: false };
+    const { c, catchup } = await loadClient(tree, {}, probe);
+    if (probe.aliased) { rec.aliased = true; }
     rec.catchup = catchup.length;
     rec.observer = c.getShortClientId("loader");
     rec.load_out = collectOutputs(c, []);

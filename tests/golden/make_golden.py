@@ -64,7 +64,9 @@ SNAP_FIXTURES = {
     "ref_snap": (dict(SNAP_BASE, ops=500, tail=64, chunk=10000, settle="alternate"), 16),
     # header + body chunks: settled documents load; unsettled ones hit SURVEY Q6 (the body
     # append resolves root.cachedLength in view (NonCollabClient, 0): "insert failed")
-    "ref_snap_body": (dict(SNAP_BASE, seed=5151, writers=3, ops=300, tail=64, chunk=150, settle="alternate"), 16),
+    # 64 documents: unsettled bodies that survive the Q6 failure hit loadBody's re-insertion
+    # (MT_DOC_ALIASED; docs 33 and 53)
+    "ref_snap_body": (dict(SNAP_BASE, seed=5151, writers=3, ops=300, tail=64, chunk=150, settle="alternate"), 64),
 }
 # The reference's own summary fixtures (SEQ/test/snapshots, data files of its tests),
 # loaded and followed by a generated tail (harness "loadfile").

@@ -154,7 +154,7 @@ if (mode === "encode") {
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
     const every = parseInt(extra[0], 10);
     const batch = new GpuMergeTreeBatch(fx.docs.length,
-        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: 1 << 18 });
+        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: 1 << 20 });
     batch.loadInitialText(fx.docs.map((d) => d.seed_text));
     const events = fx.docs.map(() => []);
     const st = (seg) => Object.assign(seg.type === "Marker" ? { m: seg.refType } : { t: seg.text },
@@ -185,6 +185,133 @@ if (mode === "encode") {
         error = e.message;
     }
     process.stdout.write(JSON.stringify({ events, error }, jsReplacer));
+} else if (mode === "events") {
+    // events <ref_events fixture> <flushEvery>: a listener's view of every event, built the
+    // way SharedSegmentSequence does (sequence_event.js restates SequenceEvent.ranges) over
+    // the facade's callbacks -> per event [segs: [getPosition, ordinal codes, cachedLength],
+    // ranges: [[index into deltaSegments, position]]], the harness's format
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const { sequenceEventRanges } = require(path.join(__dirname, "sequence_event.js"));
+    const every = parseInt(extra[0], 10);
+    const batch = new GpuMergeTreeBatch(fx.docs.length,
+        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: 1 << 22 });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const events = fx.docs.map(() => []);
+    const codes = (seg) => (seg.ordinal === undefined ? null : Array.from(seg.ordinal, (ch) => ch.charCodeAt(0)));
+    const rec = (c, args) => {
+        const segs = args.deltaSegments.map((d) => [c.getPosition(d.segment), codes(d.segment), d.segment.cachedLength]);
+        const ranges = sequenceEventRanges(args, c).map((r) => [args.deltaSegments.findIndex((d) => d.segment === r.segment),
+            r.position]);
+        return [segs, ranges];
+    };
+    const views = fx.docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        c.mergeTreeDeltaCallback = (opArgs, args) => {
+            events[i].push(["D", opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, args.operation,
+                opArgs.sequencedMessage === undefined, ...rec(c, args)]);
+        };
+        c.mergeTreeMaintenanceCallback = (args) => { events[i].push(["M", args.operation, ...rec(c, args)]); };
+        return c;
+    });
+    const all = fx.docs.map((d) => msgs(d));
+    const longest = Math.max(...all.map((m) => m.length));
+    for (let t = 0; t < longest; t += every) {
+        all.forEach((m, i) => { for (const x of m.slice(t, t + every)) { views[i].applyMsg(x); } });
+        batch.flush();
+    }
+    process.stdout.write(JSON.stringify({ events }));
+} else if (mode === "evpin") {
+    // evpin <ref_events fixture>: sequence_event.js on the fixture's own ordinals and positions
+    // (CPU: pins the restatement on the reference's events)
+    const { sequenceEventRanges } = require(path.join(__dirname, "sequence_event.js"));
+    let bad = 0, n = 0;
+    for (const d of fx.docs) {
+        for (const ev of d.events) {
+            const [segs, ranges] = ev[0] === "D" ? [ev[4], ev[5]] : [ev[2], ev[3]];
+            const objs = segs.map(([pos, ord]) => ({ pos, ordinal: ord === null ? undefined : String.fromCharCode(...ord) }));
+            const args = { operation: ev[0] === "D" ? ev[2] : ev[1], deltaSegments: objs.map((o) => ({ segment: o })) };
+            const got = sequenceEventRanges(args, { getPosition: (seg) => seg.pos })
+                .map((r) => [objs.indexOf(r.segment), r.position]);
+            n++;
+            if (JSON.stringify(got) !== JSON.stringify(ranges)) { bad++; }
+        }
+    }
+    process.stdout.write(JSON.stringify({ events: n, mismatches: bad }));
+} else if (mode === "readouts") {
+    // readouts <ref_readouts fixture>: Client / MergeTree read-outs through the facade
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const batch = new GpuMergeTreeBatch(fx.docs.length,
+        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: 1 << 22 });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const views = fx.docs.map((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        for (const m of msgs(d)) { c.applyMsg(m); }
+        return c;
+    });
+    const out = fx.docs.map((d, i) => {
+        const c = views[i];
+        const mt = c.mergeTree;
+        const lengths = d.lengths.map(([ref, cli]) => [ref, cli, cli === 0 ? c.getLength() : mt.getLength(ref, cli)]);
+        const containing = d.containing.map(([pos, ref, cli]) => {
+            const { segment, offset } = cli === 0 ? c.getContainingSegment(pos) : mt.getContainingSegment(pos, ref, cli);
+            if (segment === undefined) { return [pos, ref, cli, null]; }
+            const st = Object.assign(segment.type === "Marker" ? { m: segment.refType } : { t: segment.text },
+                { p: segment.properties === undefined ? null : segment.properties });
+            return [pos, ref, cli, [offset, mt.getPosition(segment, ref, cli), c.getPosition(segment), segment.cachedLength,
+                segment.ordinal === undefined ? null : Array.from(segment.ordinal, (ch) => ch.charCodeAt(0)), st]];
+        });
+        return { lengths, containing };
+    });
+    process.stdout.write(JSON.stringify({ docs: out }, jsReplacer));
+} else if (mode === "snapemit") {
+    // snapemit <snapshot fixture>: each document's op stream replayed through the facade, then
+    // Client.snapshot (new format) -> {doc: {path: contents}}; the reference summarised the
+    // same replica into doc.chunks
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const batch = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 4096, textCapacity: 1 << 17,
+        mergeTreeSnapshotChunkSize: fx.config.chunk });
+    batch.loadInitialText(fx.docs.map((d) => d.seed_text));
+    const out = {};
+    fx.docs.forEach((d, i) => {
+        const c = batch.client(i);
+        c.startOrUpdateCollaboration("observer");
+        for (const m of msgs(d)) { c.applyMsg(m); }
+    });
+    fx.docs.forEach((d, i) => {
+        const last = d.msgs[d.msgs.length - 1];
+        const tree = batch.client(i).snapshot({ deltaManager: { minimumSequenceNumber: last[3], lastSequenceNumber: last[1] } },
+            undefined, []);
+        out[d.doc] = Object.fromEntries(tree.entries.map((e) => [e.path, e.value.contents]));
+    });
+    process.stdout.write(JSON.stringify(out));
+} else if (mode === "async") {
+    // async <fixture> <flushEvery>: flushAsync() vs flush() on two batches -> equal checksums
+    const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
+    const every = parseInt(extra[0], 10);
+    const mk = () => {
+        const b = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 8192, textCapacity: 1 << 17 });
+        b.loadInitialText(fx.docs.map((d) => d.seed_text));
+        return [b, fx.docs.map((d, i) => { const c = b.client(i); c.startOrUpdateCollaboration("observer"); return c; })];
+    };
+    const [b1, v1] = mk(), [b2, v2] = mk();
+    const all = fx.docs.map((d) => msgs(d));
+    const longest = Math.max(...all.map((m) => m.length));
+    (async () => {
+        let sawBusy = false;
+        for (let t = 0; t < longest; t += every) {
+            all.forEach((m, i) => { for (const x of m.slice(t, t + every)) { v1[i].applyMsg(x); v2[i].applyMsg(x); } });
+            b1.flush();
+            const p = b2.flushAsync();
+            try { b2.status(); } catch (e) { sawBusy = sawBusy || /in flight/.test(e.message); }
+            await p;
+        }
+        const s = (b) => b.checksums().map((x) => [x.length, x.textHash.toString(), x.propsHash.toString(),
+            x.deltaHash.toString()]);
+        process.stdout.write(JSON.stringify({ equal: JSON.stringify(s(b1)) === JSON.stringify(s(b2)), sawBusy,
+            texts: v2.map((c) => c.getText()).every((t, i) => t === v1[i].getText()) }));
+    })().catch((e) => { console.error(e); process.exit(1); });
 } else if (mode === "maint") {
     // maint <fixture.json.gz> -> [[split, append, unlink] per doc] through the facade
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));

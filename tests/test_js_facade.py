@@ -280,3 +280,65 @@ def test_js_facade_live_client_matches_reference():
         # mergeTreeDeltaCallback stream: local ops (seq -1, no sequencedMessage), remote ops,
         # propertyDeltas undefined where an outstanding local rewrite blocked a remote annotate
         assert g["deltas"] == d["out"]["deltas"]
+
+
+# ---------------------------------------------------------------- SharedSegmentSequence events
+def test_js_sequence_event_restatement_matches_reference_events():
+    """tests/js/sequence_event.js (SequenceEvent.ranges over SortedSegmentSet, restated for the
+    GPU box) reproduces every reference event's ranges from its segments' ordinals and
+    positions (CPU)."""
+    got = _node("evpin", os.path.join(gu.GOLDEN, "ref_events.json.gz"))
+    assert got["events"] > 50000 and got["mismatches"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("every", [100000, 37])
+def test_js_facade_sequence_events_match_reference(every):
+    """A listener builds SharedSegmentSequence's event objects over GpuClient callbacks
+    (getPosition + segment ordinals, SEQ/sequence.ts:139-149): every event's positions,
+    ordinals and ranges equal those of the reference's own SequenceDeltaEvent /
+    SequenceMaintenanceEvent (tests/golden/ref_events), in one flush or in flushes of 37
+    messages (segment objects keep their identity across flushes)."""
+    _addon()
+    fx = gu.load("ref_events")
+    got = _node("events", os.path.join(gu.GOLDEN, "ref_events.json.gz"), str(every), timeout=600)["events"]
+    for d, evs in zip(fx["docs"], got):
+        assert len(evs) == len(d["events"]), d["doc"]
+        for k, (g, w) in enumerate(zip(evs, d["events"])):
+            assert g == w, (d["doc"], k, g, w)
+
+
+@pytest.mark.gpu
+def test_js_facade_readouts_match_reference():
+    """GpuClient.getPosition / getContainingSegment and client.mergeTree.getLength /
+    getContainingSegment / getPosition in the observer's and writers' views equal the
+    reference's (tests/golden/ref_readouts)."""
+    _addon()
+    fx = gu.load("ref_readouts")
+    got = _node("readouts", os.path.join(gu.GOLDEN, "ref_readouts.json.gz"), timeout=600)["docs"]
+    for d, g in zip(fx["docs"], got):
+        assert g["lengths"] == d["lengths"], d["doc"]
+        for q, (x, y) in enumerate(zip(g["containing"], d["containing"])):
+            assert x == y, (d["doc"], q, x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_snap", "ref_snap_body"])
+def test_js_facade_snapshot_matches_reference(name):
+    """Client.snapshot through the Node facade (new format: SnapshotV1 extracted on the GPU,
+    emitted by js/snapshot.js): every blob equals, byte for byte, the summary the reference
+    wrote for the same replica (SEQ/sequence.ts:576, MT/snapshotV1.ts:87-252)."""
+    _addon()
+    fx = gu.load(name)
+    got = _node("snapemit", os.path.join(gu.GOLDEN, name + ".json.gz"), timeout=600)
+    for d in fx["docs"]:
+        assert got[d["doc"] if isinstance(d["doc"], str) else str(d["doc"])] == d["chunks"], (name, d["doc"])
+
+
+@pytest.mark.gpu
+def test_js_facade_flush_async_equals_flush():
+    """flushAsync (napi_async_work: the GPU batch runs off the Node thread) gives the same
+    documents as flush, and the batch refuses other calls while it is in flight."""
+    _addon()
+    got = _node("async", os.path.join(gu.GOLDEN, "ref_c3.json.gz"), "250", timeout=600)
+    assert got["equal"] and got["texts"] and got["sawBusy"]
