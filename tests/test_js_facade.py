@@ -138,15 +138,18 @@ def test_js_native_summary_decoder_matches_python(name):
 def test_js_facade_loads_snapshots_like_reference(name):
     """GpuMergeTreeBatch.loadSnapshots (Client.load for every document) + GpuClient.applyMsg of
     the tails: text, length and properties equal the reference's; the reference's load
-    failures throw "MergeTree insert failed"."""
+    failures throw "MergeTree insert failed", and a body that loadBody
+    re-inserts (MT_DOC_ALIASED) throws the facade's own error -- every document compared."""
     _addon()
     fx = gu.load(name)
     got = {g["doc"]: g for g in _node("loadsnap", os.path.join(gu.GOLDEN, name + ".json.gz"))["docs"]}
+    assert len(got) == len(fx["docs"])
     for d in fx["docs"]:
         want = gu.snap_status(d)
-        if want is None:
-            continue
         g = got[d["doc"]]
+        if want == 10:
+            assert "insert segments twice" in g.get("error", ""), g
+            continue
         if want:
             assert g.get("error", "").startswith("MergeTree insert failed"), g
             continue
