@@ -247,6 +247,55 @@ def c5_decode_rate(counts, recs, text, props, mn, cu, chunk, n_sample, threads):
                 python_restatement=py)
 
 
+def c5_end_to_end(mt, counts, recs, text, props, mn, cu, chunk, tail_arr, tail, sums, status, n_emit, threads,
+                  slice_docs=16384):
+    """Cold catch-up end to end, from summary JSON bytes to replayed tails, for every document
+    of the handle: MergeTreeBatch.catch_up (native decode of slice k + 1 on the host while
+    slice k uploads and loads on the GPU) followed by the tails.  n_emit distinct summaries
+    are emitted as SnapshotV1 JSON chunks (untimed) and document d takes summary d % n_emit
+    and its tail, so document d must end as the device-only step left document d % n_emit."""
+    from fluidframework_amd.snapdec import SummaryDecoder
+    from fluidframework_amd.snapshot import encode_chunks, record_specs
+    from fluidframework_amd.wire import Interner
+    it = Interner(synthetic=True)
+    c = np.asarray(counts, dtype=np.int64)
+    r0 = np.concatenate([[0], np.cumsum(c[:, 0])])
+    t0 = np.concatenate([[0], np.cumsum(c[:, 1])])
+    p0 = np.concatenate([[0], np.cumsum(c[:, 2])])
+    names = {i: f"client-{i}" for i in range(-2, 4096)}
+    emitted = []
+    for d in range(n_emit):
+        specs, lengths = record_specs(recs[r0[d]:r0[d + 1]], text[t0[d]:t0[d + 1]], props[p0[d]:p0[d + 1]], it, names)
+        emitted.append(SummaryDecoder.pack([encode_chunks(specs, lengths, int(mn[d]), int(cu[d]), chunk)]))
+    n = mt.n_docs
+    paths, blobs, off = [], [], [0]
+    for d in range(n):
+        ep, eb, _ = emitted[d % n_emit]
+        paths += ep
+        blobs += eb
+        off.append(len(paths))
+    nbytes = sum(len(b) for b in blobs)
+    src = np.arange(n) % n_emit
+    ops = tail_arr["ops"].reshape(-1, tail)[src].ravel()
+    tb = mt.upload(dict(tail_arr, ops=ops, doc_off=np.arange(n + 1, dtype=np.int64) * tail))
+    rates = []
+    for rep in range(3):   # the first run warms the decoder's buffers and the workers
+        mt.sync()
+        t = time.perf_counter()
+        mt.catch_up(None, Interner(synthetic=True), threads=threads, slice_docs=slice_docs, packed=(paths, blobs, off))
+        tb.apply_async()
+        mt.sync()
+        rates.append(time.perf_counter() - t)
+    el = min(rates[1:])
+    tb.free()
+    ok = bool(np.array_equal(mt.checksums(), sums[src]) and np.array_equal(mt.status(), status[src]))
+    return dict(value=round(n / el, 1), unit="docs/s", cores=threads, json_mb_per_s=round(nbytes / el / 1e6, 1),
+                slice_docs=slice_docs, equals_device_only_step=ok,
+                sample=f"{n} documents ({nbytes / 1e6:.0f} MB of summary JSON, {n_emit} distinct summaries) "
+                       f"decoded on {threads} host threads, uploaded, loaded and their {tail}-op tails replayed: "
+                       f"{el:.3f} s (best of 2 after a warm-up run)")
+
+
 def run_c5(args, cfg, rank, world, local_rank, dist):
     """Config C5 (cold catch-up): every document's SnapshotV1 summary is loaded
     (mt_snapshots_load_async: reloadFromSegments + loadBody) and its tail of `tail` sequenced
@@ -305,10 +354,12 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
     if rank != 0:
         return
     n_tail = int(len(idx))
-    cpu = parity = decode = None
+    cpu = parity = decode = e2e = None
     if not args.no_cpu:
         threads = args.cpu_threads or host_cores()
         decode = c5_decode_rate(counts, recs, text, props, mn, cu, cfg["chunk"], min(docs, 4000), threads)
+        e2e = c5_end_to_end(mt, counts, recs, text, props, mn, cu, cfg["chunk"], tail_arr, tail, sums, status,
+                            min(docs, 4000), threads)
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import pyoracle                            # the checker, timed as the CPU baseline
         n_sample = args.cpu_sample_docs or min(docs, 20000)
@@ -338,6 +389,7 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
                    "parallelism": f"doc-shard x{world}"},
         "cpu_baseline": cpu,
         "summary_decode": decode,
+        "end_to_end": e2e,
         "parity": {"status_nonzero": int((status != 0).sum()), "oracle_sample": parity},
         "prep_s": round(t_prep, 2),
     }))

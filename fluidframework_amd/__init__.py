@@ -124,15 +124,70 @@ class MergeTreeBatch:
         self.load_snapshots(la)
         return [_json.loads(c) if c is not None else [] for c in catchup], clients
 
-    def upload_snapshots(self, la):
-        """Device-resident summaries (mt_snapshots_upload); .load_async() enqueues a load."""
+    def upload_snapshots(self, la, doc_lo=0):
+        """Device-resident summaries (mt_snapshots_upload); .load_async() enqueues a load.  With
+        fewer summaries than documents, summary d is for document doc_lo + d
+        (mt_snapshots_upload_range)."""
         off, nh, segs, text, props, mn, cu = self._snap_args(la)
-        s = self.lib.mt_snapshots_upload(self.h, _native.ptr(off), _native.ptr(nh), _native.ptr(segs), len(segs),
-                                         _native.ptr(text), len(text), _native.ptr(props), len(props),
-                                         _native.ptr(mn), _native.ptr(cu))
+        n = len(off) - 1
+        s = self.lib.mt_snapshots_upload_range(self.h, doc_lo, n, _native.ptr(off), _native.ptr(nh), _native.ptr(segs),
+                                               len(segs), _native.ptr(text), len(text), _native.ptr(props), len(props),
+                                               _native.ptr(mn), _native.ptr(cu))
         if not s:
             raise RuntimeError(f"mt_snapshots_upload failed: {self.lib.mt_last_error(self.h).decode()}")
         return DeviceSnapshots(self, s)
+
+    def catch_up(self, summaries, interner, threads=8, slice_docs=8192, packed=None):
+        """Cold catch-up of every document from its summary blobs ({path: JSON text} per
+        document; or `packed` = snapdec.SummaryDecoder.pack(summaries)), as load_summaries,
+        in slices of `slice_docs` documents: the native decoder parses slice k + 1 on the
+        host (a worker thread; the decoder's own threads inside) while slice k is uploaded
+        and its load runs on the GPU (mt_snapshots_upload_range + mt_snapshots_load_async).
+        Returns (catchup, clients) as load_summaries; the loads are enqueued on the handle's
+        stream (sync() waits)."""
+        import json as _json
+        import queue
+        import threading
+        from .snapdec import SummaryDecoder
+        paths, blobs, off = packed if packed is not None else SummaryDecoder.pack(summaries)
+        if len(off) != self.n_docs + 1:
+            raise ValueError("one summary per document")
+        dec = SummaryDecoder(interner, threads)
+        q = queue.Queue(maxsize=2)   # decoded slices waiting for their upload
+
+        def produce():
+            try:
+                for d0 in range(0, self.n_docs, slice_docs):
+                    d1 = min(self.n_docs, d0 + slice_docs)
+                    b0, b1 = off[d0], off[d1]
+                    sub = (paths[b0:b1], blobs[b0:b1], [o - b0 for o in off[d0:d1 + 1]])
+                    out, catchup, clients = dec.decode_packed_full(*sub)
+                    q.put((d0, out, catchup, clients))
+                q.put(None)
+            except BaseException as e:   # surfaces in the consumer
+                q.put(e)
+
+        t = threading.Thread(target=produce, daemon=True)
+        t.start()
+        catchup_all, clients_all, held = [], [], []
+        while True:
+            item = q.get()
+            if item is None:
+                break
+            if isinstance(item, BaseException):
+                t.join()
+                raise item
+            d0, out, catchup, clients = item
+            snaps = self.upload_snapshots(out, doc_lo=d0)
+            snaps.load_async()
+            held.append(snaps)   # device copies stay alive until the loads have run
+            catchup_all += [_json.loads(c) if c is not None else [] for c in catchup]
+            clients_all += clients
+        t.join()
+        self.sync()
+        for s_ in held:
+            s_.free()
+        return catchup_all, clients_all
 
     def extract_snapshots_raw(self):
         """mt_extract_snapshots as concatenated arrays: (counts[n_docs, 3], records, text,

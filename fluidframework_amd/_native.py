@@ -68,6 +68,7 @@ SIGNATURES = [
     ("mt_load_snapshots", _I, [_P, _P, _P, _P, _U64, _P, _U64, _P, _U64, _P, _P]),
     ("mt_extract_snapshots", _I, [_P, _P, _P, _P, _P, _P, _P]),
     ("mt_snapshots_upload", _P, [_P, _P, _P, _P, _U64, _P, _U64, _P, _U64, _P, _P]),
+    ("mt_snapshots_upload_range", _P, [_P, _U32, _U32, _P, _P, _P, _U64, _P, _U64, _P, _U64, _P, _P]),
     ("mt_snapshots_load_async", _I, [_P, _P]),
     ("mt_snapshots_free", None, [_P]),
     ("mt_batch_upload", _P, [_P, _P, _P, _U64, _P, _U64, _P, _U64]),

@@ -93,21 +93,22 @@ struct LoadScratch {
 __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int64_t *off, const int32_t *nh,
                                                          const mt_seg_rec *segs, const uint16_t *tin,
                                                          const uint32_t *pin, const int32_t *min_seq,
-                                                         const int32_t *cur_seq, LoadScratch sc) {
-    const int doc = blockIdx.x;
+                                                         const int32_t *cur_seq, LoadScratch sc, int lo) {
+    // summary r of the set (off, nh, min_seq, cur_seq, sc.off index r) -> document lo + r
+    const int r = blockIdx.x, doc = lo + r;
     if (doc >= st.n_docs) return;
     oslot_reset(st, doc);
-    const int n = nh[doc];
-    const mt_seg_rec *rs = segs + off[doc];
-    const bool big = sc.off && sc.off[2 * doc] >= 0;
+    const int n = nh[r];
+    const mt_seg_rec *rs = segs + off[r];
+    const bool big = sc.off && sc.off[2 * r] >= 0;
     uint16_t *text = st.text + (size_t)doc * 2 * st.T;
     uint32_t *props = st.props + (size_t)doc * 2 * st.P * MT_PREC;
     const int nb0 = n > 0 ? (n + MT_LOAD_FANOUT - 1) / MT_LOAD_FANOUT : 1;
     int status = !big && (n > st.S || nb0 > st.B) ? MT_DOC_CAPACITY : 0;
     const size_t B = big ? (size_t)nb0 : st.B;   // stride of a level's counts
-    v4i *dA = big ? sc.A + sc.off[2 * doc] : st.segA + doc * (size_t)st.S;
-    u64 *dO = big ? sc.O + sc.off[2 * doc] : st.segO + doc * (size_t)st.S;
-    v4u *dB = big ? sc.B + sc.off[2 * doc] : st.segB + doc * (size_t)st.S;
+    v4i *dA = big ? sc.A + sc.off[2 * r] : st.segA + doc * (size_t)st.S;
+    u64 *dO = big ? sc.O + sc.off[2 * r] : st.segO + doc * (size_t)st.S;
+    v4u *dB = big ? sc.B + sc.off[2 * r] : st.segB + doc * (size_t)st.S;
     int ttop = 0, ptop = 1;
     for (int base = 0; base < n && status == 0; base += MT_WAVE) {
         const int i = base + lane();
@@ -175,8 +176,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
     // block counts, level by level (blocks of 7, the last one takes the rest)
     int nbl[MT_LV];
     int depth = 0, cnt_below = n > 0 ? n : 0, nl = nb0;
-    uint8_t *cnt = big ? sc.cnt + MT_LV * sc.off[2 * doc + 1] : st.cnt + (size_t)doc * MT_LV * B;
-    int8_t *flg = big ? sc.flg + sc.off[2 * doc + 1] : st.flg + (size_t)doc * B;
+    uint8_t *cnt = big ? sc.cnt + MT_LV * sc.off[2 * r + 1] : st.cnt + (size_t)doc * MT_LV * B;
+    int8_t *flg = big ? sc.flg + sc.off[2 * r + 1] : st.flg + (size_t)doc * B;
     for (int l = 0; l < MT_LV; l++) nbl[l] = 0;
     while (status == 0) {
         if (depth >= MT_LV) {
@@ -213,8 +214,8 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
         memset(&h, 0, sizeof(h));
         h.n_seg = status ? 0 : n;
         h.depth = status ? 1 : depth;
-        h.cur_seq = cur_seq[doc];
-        h.min_seq = min_seq[doc];
+        h.cur_seq = cur_seq[r];
+        h.min_seq = min_seq[r];
         h.text_top = ttop;
         h.props_top = ptop;
         h.next_uid = n + 1;
@@ -823,21 +824,21 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
 // handle's full paged capacities (pg_convert from the staging buffers); the body appends
 // then replay like any paged document's messages.
 template <class T>
-__global__ void __launch_bounds__(MT_WAVE) k_load_convert(DevState st, LoadScratch sc, PagedCaps pc) {
+__global__ void __launch_bounds__(MT_WAVE) k_load_convert(DevState st, LoadScratch sc, PagedCaps pc, int lo) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
-    const int doc = blockIdx.x;
-    if (doc >= st.n_docs || sc.off[2 * doc] < 0 || st.hdr[doc].status) return;
+    const int r = blockIdx.x, doc = lo + r;   // summary r of the set -> document lo + r
+    if (doc >= st.n_docs || sc.off[2 * r] < 0 || st.hdr[doc].status) return;
     const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v));
     PagedDoc<T> pd;
     pg_setup(pd, st, doc, smem, L, pc);
     DocT<T> &w = pd.w;
     FlatSrc src;
-    src.A = (GLB_AS const v4i *)(sc.A + sc.off[2 * doc]);
-    src.O = (GLB_AS const u64 *)(sc.O + sc.off[2 * doc]);
-    src.Bv = (GLB_AS const v4u *)(sc.B + sc.off[2 * doc]);
-    src.cnt = (GLB_AS const uint8_t *)(sc.cnt + MT_LV * sc.off[2 * doc + 1]);
-    src.flg = (GLB_AS const int8_t *)(sc.flg + sc.off[2 * doc + 1]);
+    src.A = (GLB_AS const v4i *)(sc.A + sc.off[2 * r]);
+    src.O = (GLB_AS const u64 *)(sc.O + sc.off[2 * r]);
+    src.Bv = (GLB_AS const v4u *)(sc.B + sc.off[2 * r]);
+    src.cnt = (GLB_AS const uint8_t *)(sc.cnt + MT_LV * sc.off[2 * r + 1]);
+    src.flg = (GLB_AS const int8_t *)(sc.flg + sc.off[2 * r + 1]);
     src.heap = nullptr;   // a fresh collaboration: heap_n == 0
     src.B = (size_t)w.hp->n_blk[0];
     if (w.status == 0 && pg_convert(pd, src)) {
@@ -1757,7 +1758,7 @@ int mt_apply_ops(mt_handle *h, const int64_t *doc_op_off, const mt_op_rec *ops, 
 
 struct mt_snapshots {
     int device = 0;
-    uint32_t n_docs = 0;
+    uint32_t doc_lo = 0, n_docs = 0;   // summary d loads into document doc_lo + d
     int64_t *off = nullptr;
     int32_t *nh = nullptr, *min_seq = nullptr, *cur_seq = nullptr;
     mt_seg_rec *segs = nullptr;
@@ -1781,12 +1782,16 @@ void mt_snapshots_free(mt_snapshots *s) {
     delete s;
 }
 
-mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header,
-                                  const mt_seg_rec *segs, uint64_t n_segs, const uint16_t *text, uint64_t text_len,
-                                  const uint32_t *props, uint64_t props_len, const int32_t *min_seq,
-                                  const int32_t *cur_seq) {
+mt_snapshots *mt_snapshots_upload_range(mt_handle *h, uint32_t doc_lo, uint32_t n_docs, const int64_t *doc_seg_off,
+                                        const int32_t *n_header, const mt_seg_rec *segs, uint64_t n_segs,
+                                        const uint16_t *text, uint64_t text_len, const uint32_t *props,
+                                        uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq) {
     if (!h || !doc_seg_off || !n_header || !min_seq || !cur_seq || (n_segs && !segs)) return nullptr;
-    const uint32_t N = h->n_docs;
+    if (n_docs == 0 || doc_lo > h->n_docs || n_docs > h->n_docs - doc_lo) {
+        h->err = "mt_snapshots_upload_range: documents [doc_lo, doc_lo + n_docs) outside the handle (or empty)";
+        return nullptr;
+    }
+    const uint32_t N = n_docs;   // summary d of this set loads into document doc_lo + d
     for (uint32_t d = 0; d < N; d++)
         if (n_header[d] < 0 || doc_seg_off[d] + n_header[d] > doc_seg_off[d + 1] ||
             doc_seg_off[d + 1] > (int64_t)n_segs) {
@@ -1806,6 +1811,7 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
     auto *s = new mt_snapshots();
     s->device = h->device;
     s->n_docs = N;
+    s->doc_lo = doc_lo;
     bool ok = hipMalloc(&s->off, (N + 1) * 8) == hipSuccess && hipMalloc(&s->nh, N * 4) == hipSuccess &&
               hipMalloc(&s->min_seq, N * 4) == hipSuccess && hipMalloc(&s->cur_seq, N * 4) == hipSuccess &&
               hipMalloc(&s->segs, std::max<uint64_t>(n_segs, 1) * sizeof(mt_seg_rec)) == hipSuccess &&
@@ -1855,9 +1861,9 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
     // 0, the append's client and seq) plus MT_OP_LOAD_REMOVED when the spec carries removal
     // info; the ordinary replay kernels apply them (every tier).
     std::vector<mt_op_rec> ops;
-    std::vector<int64_t> ooff(N + 1, 0);
+    std::vector<int64_t> ooff(h->n_docs + 1, 0);   // the body batch spans the handle's documents
     for (uint32_t d = 0; d < N; d++) {
-        ooff[d] = (int64_t)ops.size();
+        ooff[doc_lo + d] = (int64_t)ops.size();
         const int64_t s0 = doc_seg_off[d], sh = s0 + n_header[d], s1 = doc_seg_off[d + 1];
         int64_t obs = 0;   // root.cachedLength: observer length (removed segments count 0)
         for (int64_t i = s0; i < sh; i++)
@@ -1924,7 +1930,7 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
         }
         if (!aliased && batch_len && flushed) alias();   // the final flushBatch()
     }
-    ooff[N] = (int64_t)ops.size();
+    for (uint32_t d = doc_lo + N; d <= h->n_docs; d++) ooff[d] = (int64_t)ops.size();
     if (!ops.empty()) {
         s->body = mt_batch_upload(h, ooff.data(), ops.data(), ops.size(), text, text_len, props, props_len);
         if (!s->body) {
@@ -1935,19 +1941,30 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
     return s;
 }
 
+mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header,
+                                  const mt_seg_rec *segs, uint64_t n_segs, const uint16_t *text, uint64_t text_len,
+                                  const uint32_t *props, uint64_t props_len, const int32_t *min_seq,
+                                  const int32_t *cur_seq) {
+    if (!h) return nullptr;
+    return mt_snapshots_upload_range(h, 0, h->n_docs, doc_seg_off, n_header, segs, n_segs, text, text_len, props,
+                                     props_len, min_seq, cur_seq);
+}
+
 int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
-    if (!h || !s || s->n_docs != h->n_docs) return MT_E_INVALID;
+    if (!h || !s || s->doc_lo > h->n_docs || s->n_docs > h->n_docs - s->doc_lo) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
+    if (h->st.DL)
+        HIPCHK(h, hipMemsetAsync(h->st.dlog + (size_t)s->doc_lo * h->st.DL, 0, (size_t)s->n_docs * h->st.DL * 4,
+                                 h->stream));
     HIPCHK(h, hipEventRecord(h->ev_load, h->stream));
-    hipLaunchKernelGGL(k_load_header, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, s->off, s->nh, s->segs,
-                       s->text, s->props, s->min_seq, s->cur_seq, s->sc);
+    hipLaunchKernelGGL(k_load_header, dim3(s->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, s->off, s->nh, s->segs,
+                       s->text, s->props, s->min_seq, s->cur_seq, s->sc, (int)s->doc_lo);
     HIPCHK(h, hipGetLastError());
     if (s->any_big) {
         const PagedCaps &pc = h->pg_full;
         const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, 8).total;
-        hipLaunchKernelGGL(k_load_convert<TierPagedT<false>>, dim3(h->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
-                           s->sc, pc);
+        hipLaunchKernelGGL(k_load_convert<TierPagedT<false>>, dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                           s->sc, pc, (int)s->doc_lo);
         HIPCHK(h, hipGetLastError());
     }
     if (s->body) return mt_batch_apply_async(h, s->body);

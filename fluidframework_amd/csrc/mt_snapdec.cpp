@@ -11,8 +11,10 @@
 // into a flat node array (24-byte nodes in pre-order, strings decoded to UTF-16 units as JS
 // holds them, numbers left as lexemes in the source; the buffers are reused, so a worker
 // allocates almost nothing) and builds its records with document-local property ids.
-// Phase 2 concatenates the documents in order and maps local ids to the batch's ids, which
-// numbers keys / values first-seen in document order, exactly as wire.Interner does.
+// Phase 2 maps local ids to the batch's ids, which numbers keys / values first-seen in
+// document order, exactly as wire.Interner does, and places every document in the output;
+// mt_snapdec_fetch then concatenates the documents straight into the caller's arrays, in
+// parallel (each document's slice is known).
 #include <algorithm>
 #include <atomic>
 #include <charconv>
@@ -48,7 +50,8 @@ struct Blob {
     size_t n = 0;
     std::string path;
     std::vector<Node> nodes;     // pre-order: a container's first child is the next node
-    std::vector<char16_t> str;
+    std::vector<char16_t> str;   // decoded string units [0, slen); sized once per blob to an
+    uint32_t slen = 0;           // upper bound (a byte never yields more than one unit)
 
     const char16_t *s(uint32_t off) const { return str.data() + off; }
     uint32_t first(uint32_t i) const { return nodes[i].len ? i + 1 : NONE; }
@@ -69,6 +72,17 @@ struct Blob {
         for (uint32_t m = 0; m < nodes[i].len; m++, c = nodes[c].next)
             if (eq(s(nodes[c].koff), nodes[c].klen, k)) r = c;
         return r;
+    }
+    // members of object i named keys[0 .. n) -> out[0 .. n) (NONE if absent; the last of
+    // duplicated members, as get)
+    void fields(uint32_t i, const char *const *keys, int n, uint32_t *out) const {
+        uint32_t c = first(i);
+        for (uint32_t m = 0; m < nodes[i].len; m++, c = nodes[c].next)
+            for (int k = 0; k < n; k++)
+                if (eq(s(nodes[c].koff), nodes[c].klen, keys[k])) {
+                    out[k] = c;
+                    break;
+                }
     }
     bool present(uint32_t i) const { return i != NONE && nodes[i].t != Node::NUL; }
     std::u16string ustr(uint32_t i) const { return std::u16string(s(nodes[i].off), nodes[i].len); }
@@ -156,13 +170,35 @@ struct Reader {
     bool str(uint32_t &off, uint32_t &len) {
         if (p >= e || *p != '"') return fail("expected a string");
         p++;
-        auto &o = B.str;
-        off = (uint32_t)o.size();
+        char16_t *o = B.str.data();   // room for every remaining byte (parse sizes it)
+        uint32_t w = B.slen;
+        off = w;
         for (;;) {
-            const char *q = p;   // ASCII run
-            while (q < e && (unsigned char)*q >= 0x20 && (unsigned char)*q < 0x80 && *q != '"' && *q != '\\') q++;
-            o.insert(o.end(), (const unsigned char *)p, (const unsigned char *)q);
-            p = q;
+            {   // ASCII run: 8 bytes at a time up to the first '"', '\\', control or non-ASCII byte
+                const char *q = p;
+                while (e - q >= 8) {
+                    uint64_t x;
+                    memcpy(&x, q, 8);
+                    const uint64_t hi = 0x8080808080808080ull, one = 0x0101010101010101ull;
+                    const uint64_t qt = x ^ (one * 0x22), bs = x ^ (one * 0x5C);
+                    const uint64_t stop = (x | ((qt - one) & ~qt) | ((bs - one) & ~bs) | ((x - one * 0x20) & ~x)) & hi;
+                    if (stop) {
+                        q += __builtin_ctzll(stop) >> 3;
+                        goto run_end;
+                    }
+                    q += 8;
+                }
+                while (q < e) {
+                    const unsigned char c = (unsigned char)*q;
+                    if (c < 0x20 || c >= 0x80 || c == '"' || c == '\\') break;
+                    q++;
+                }
+            run_end:
+                const size_t k = (size_t)(q - p);
+                for (size_t i = 0; i < k; i++) o[w + i] = (char16_t)(unsigned char)p[i];
+                w += (uint32_t)k;
+                p = q;
+            }
             if (p >= e) return fail("unterminated string");
             const unsigned char c = (unsigned char)*p;
             if (c == '"') break;
@@ -170,14 +206,14 @@ struct Reader {
                 if (++p >= e) return fail("bad escape");
                 const char x = *p++;
                 switch (x) {
-                    case '"': o.push_back(u'"'); break;
-                    case '\\': o.push_back(u'\\'); break;
-                    case '/': o.push_back(u'/'); break;
-                    case 'b': o.push_back(u'\b'); break;
-                    case 'f': o.push_back(u'\f'); break;
-                    case 'n': o.push_back(u'\n'); break;
-                    case 'r': o.push_back(u'\r'); break;
-                    case 't': o.push_back(u'\t'); break;
+                    case '"': o[w++] = u'"'; break;
+                    case '\\': o[w++] = u'\\'; break;
+                    case '/': o[w++] = u'/'; break;
+                    case 'b': o[w++] = u'\b'; break;
+                    case 'f': o[w++] = u'\f'; break;
+                    case 'n': o[w++] = u'\n'; break;
+                    case 'r': o[w++] = u'\r'; break;
+                    case 't': o[w++] = u'\t'; break;
                     case 'u': {
                         if (e - p < 4) return fail("bad \\u escape");
                         int v = 0;
@@ -187,7 +223,7 @@ struct Reader {
                             v = v * 16 + h;
                         }
                         p += 4;
-                        o.push_back((char16_t)v);
+                        o[w++] = (char16_t)v;
                         break;
                     }
                     default: return fail("bad escape");
@@ -205,7 +241,7 @@ struct Reader {
             if (c >= 0xC2 && c <= 0xDF) { cp = c & 0x1F; n = 1; }
             else if (c >= 0xE0 && c <= 0xEF) { cp = c & 0x0F; n = 2; lo = c == 0xE0 ? 0xA0 : 0x80; hi = c == 0xED ? 0x9F : 0xBF; }
             else if (c >= 0xF0 && c <= 0xF4) { cp = c & 0x07; n = 3; lo = c == 0xF0 ? 0x90 : 0x80; hi = c == 0xF4 ? 0x8F : 0xBF; }
-            else { p++; o.push_back(u'\uFFFD'); continue; }
+            else { p++; o[w++] = u'\uFFFD'; continue; }
             p++;
             bool ok = true;
             for (int i = 0; i < n; i++) {
@@ -215,17 +251,18 @@ struct Reader {
                 cp = (cp << 6) | (x & 0x3F);
                 p++;
             }
-            if (!ok) { o.push_back(u'\uFFFD'); continue; }
-            if (cp >= 0x10000) {
+            if (!ok) { o[w++] = u'\uFFFD'; continue; }
+            if (cp >= 0x10000) {   // 4 bytes -> 2 units
                 cp -= 0x10000;
-                o.push_back((char16_t)(0xD800 + (cp >> 10)));
-                o.push_back((char16_t)(0xDC00 + (cp & 0x3FF)));
+                o[w++] = (char16_t)(0xD800 + (cp >> 10));
+                o[w++] = (char16_t)(0xDC00 + (cp & 0x3FF));
             } else {
-                o.push_back((char16_t)cp);
+                o[w++] = (char16_t)cp;
             }
         }
         p++;
-        len = (uint32_t)o.size() - off;
+        B.slen = w;
+        len = w - off;
         return true;
     }
     uint32_t node(uint8_t t) {
@@ -313,9 +350,9 @@ bool parse(Blob &b, std::string &err) {
         return false;
     }
     b.nodes.clear();
-    b.str.clear();
     b.nodes.reserve(b.n / 12 + 8);
-    b.str.reserve(b.n);
+    b.slen = 0;
+    if (b.str.size() < b.n + 1) b.str.resize(b.n + 1);
     Reader r{b.src, b.src + b.n, b, {}};
     uint32_t root;
     if (!r.val(root)) {
@@ -502,6 +539,9 @@ bool latest(const Blob &B, Chunk &out, std::string &err) {
     return true;
 }
 
+const char *const kSpecKeys[5] = {"json", "seq", "client", "removedSeq", "removedClient"};
+const char *const kSegKeys[3] = {"text", "props", "marker"};
+
 // One document's records, property ids local to the document (first-seen order); the merge
 // maps them to the batch's ids in document order, which keeps wire.Interner's numbering.
 struct DocOut {
@@ -513,6 +553,8 @@ struct DocOut {
     int32_t nh = 0, msn = 0, seq = 0;
     int64_t cu = -1;
     std::string clients, err;
+    std::vector<uint32_t> kmap, vmap;   // phase 2: local key / value id -> the batch's
+    size_t si = 0, ti = 0, pi = 0;      // phase 2: where the document starts in the output
 };
 
 struct Blobs {
@@ -535,7 +577,7 @@ struct Worker {
     std::vector<uint32_t> mbuf;
     std::vector<std::pair<const Blob *, uint32_t>> specs;
     std::vector<std::string> ordered8;
-    std::vector<const std::u16string *> names;
+    std::vector<std::u16string> sid;   // short id k + 1 -> long client id
 
     uint32_t key(DocOut &o, const Blob &B, uint32_t m) {
         const char16_t *k = B.s(B.nodes[m].koff);
@@ -643,11 +685,23 @@ struct Worker {
         }
         // specToSegment :86-118 (+ segmentFromSpec, SEQ/sequenceFactory.ts:31-37)
         shortid.clear();
+        sid.clear();
         auto short_of = [&](const Blob &B, uint32_t c) {
-            kbuf.assign(B.s(B.nodes[c].off), B.nodes[c].len);
+            const char16_t *u = B.s(B.nodes[c].off);
+            const uint32_t n = B.nodes[c].len;
+            if (shortid.empty()) {   // few writers: a linear scan over the first-seen names
+                for (size_t k = 0; k < sid.size(); k++)
+                    if (sid[k].size() == n && !memcmp(sid[k].data(), u, n * sizeof(char16_t))) return (int)k + 1;
+                sid.emplace_back(u, n);
+                if (sid.size() > 32)
+                    for (size_t k = 0; k < sid.size(); k++) shortid.emplace(sid[k], (int)k + 1);
+                return (int)sid.size();
+            }
+            kbuf.assign(u, n);
             auto it = shortid.find(kbuf);
             if (it != shortid.end()) return it->second;
-            const int v = (int)shortid.size() + 1;
+            const int v = (int)sid.size() + 1;
+            sid.emplace_back(kbuf);
             shortid.emplace(kbuf, v);
             return v;
         };
@@ -660,19 +714,24 @@ struct Worker {
             r.removed_seq = INT32_MIN;
             r.props = MT_NO_PROPS;
             r.client = -2;
-            const uint32_t jv = B.get(spec, "json");   // hasMergeInfo: `"json" in spec`
-            const bool mi = jv != NONE;
+            // one pass over each object's members (the last of duplicated members, as B.get)
+            uint32_t sf[5] = {NONE, NONE, NONE, NONE, NONE};   // json, seq, client, removedSeq, removedClient
+            if (B.nodes[spec].t == Node::OBJ) B.fields(spec, kSpecKeys, 5, sf);
+            const uint32_t jv = sf[0], sq = sf[1], cl = sf[2], rs = sf[3], rc = sf[4];
+            const bool mi = jv != NONE;   // hasMergeInfo: `"json" in spec`
             const uint32_t js = mi ? jv : spec;
             uint32_t pr = NONE, tx = NONE, mk = NONE;
+            uint32_t jf[3] = {NONE, NONE, NONE};   // text, props, marker
+            if (B.nodes[js].t == Node::OBJ) B.fields(js, kSegKeys, 3, jf);
             if (B.nodes[js].t == Node::STR) {
                 tx = js;
-            } else if ((tx = B.get(js, "text")) != NONE) {
-                pr = B.get(js, "props");
-            } else if ((mk = B.get(js, "marker")) != NONE) {
+            } else if ((tx = jf[0]) != NONE) {
+                pr = jf[1];
+            } else if ((mk = jf[2]) != NONE) {
                 r.flags = MT_F_MARKER;
                 r.payload = (uint32_t)B.as_int(B.get(mk, "refType"));
                 r.len = 1;
-                pr = B.get(js, "props");
+                pr = jf[1];
             } else {
                 return bad(o, "unsupported segment spec");
             }
@@ -692,8 +751,6 @@ struct Worker {
                 }
             }
             if (mi) {
-                const uint32_t sq = B.get(spec, "seq"), cl = B.get(spec, "client"), rs = B.get(spec, "removedSeq"),
-                               rc = B.get(spec, "removedClient");
                 r.flags |= MT_SEG_MERGE_INFO | (B.present(sq) ? MT_SEG_HAS_SEQ : 0);
                 if (B.present(cl)) r.client = (int16_t)short_of(B, cl);
                 if (B.present(sq)) r.seq = (int32_t)B.as_int(sq);
@@ -705,12 +762,10 @@ struct Worker {
         o.nh = (int32_t)nh;
         o.msn = (int32_t)msn;
         o.seq = (int32_t)seq;
-        names.assign(shortid.size(), nullptr);
-        for (const auto &kv : shortid) names[kv.second - 1] = &kv.first;
         o.clients = "[";
-        for (size_t i = 0; i < names.size(); i++) {
+        for (size_t i = 0; i < sid.size(); i++) {
             if (i) o.clients.push_back(',');
-            json_str(o.clients, names[i]->data(), names[i]->size());
+            json_str(o.clients, sid[i].data(), sid[i].size());
         }
         o.clients.push_back(']');
         return true;
@@ -722,20 +777,34 @@ struct Worker {
 struct mt_snapdec {
     bool synthetic = false;
     std::string err;
-    std::vector<mt_seg_rec> segs;
-    std::vector<uint16_t> text;
-    std::vector<uint32_t> props;
-    std::vector<int64_t> doc_off;
-    std::vector<int32_t> n_header, min_seq, cur_seq;
-    std::vector<int64_t> catchup;
-    std::vector<std::string> clients;   // per document: JSON array of long ids, short id 1..n
     std::unordered_map<std::u16string, uint32_t> key_ids;   // the batch's interning
     std::vector<std::u16string> keys;
     std::unordered_map<std::string, uint32_t> val_ids;
     std::vector<std::string> vals;
     std::vector<DocOut> docs;           // reused between calls
     std::vector<Worker> workers;
+    uint32_t n_docs = 0;                // of the last successful decode
+    int threads = 1;
+    size_t ns = 0, ntx = 0, npr = 0;    // its output sizes
 };
+
+namespace {
+// Runs fn(d) for d in [0, n) on nt threads (dynamic, `grain` documents at a time).
+template <class F> void parallel_docs(uint32_t n, int nt, uint32_t grain, F fn) {
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const uint32_t d0 = next.fetch_add(grain);
+            if (d0 >= n) break;
+            for (uint32_t d = d0; d < std::min(n, d0 + grain); d++) fn(d);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+}
+}  // namespace
 
 extern "C" {
 
@@ -766,133 +835,129 @@ int mt_snapdec_decode(mt_snapdec *s, uint32_t n_docs, const int64_t *blob_off, c
         return -1;
     }
     if (s->docs.size() < n_docs) s->docs.resize(n_docs);
+    s->n_docs = 0;
     const int nt = std::max(1, std::min({threads, 256, (int)std::max<uint32_t>(n_docs, 1)}));
     if ((int)s->workers.size() < nt) s->workers.resize((size_t)nt);
     const Blobs in{blob_off, paths, path_len, json, json_len};
     // phase 1: documents parsed and specToSegment'ed on nt threads (dynamic, 8 at a time)
-    std::atomic<uint32_t> next{0};
-    auto work = [&](int t) {
-        Worker &w = s->workers[(size_t)t];
-        w.synthetic = s->synthetic;
-        for (;;) {
-            const uint32_t d0 = next.fetch_add(8);
-            if (d0 >= n_docs) break;
-            for (uint32_t d = d0; d < std::min(n_docs, d0 + 8); d++) {
-                try {
-                    w.build(s->docs[d], d, in);
-                } catch (const std::exception &ex) {   // e.g. bad_alloc: the document's error
-                    s->docs[d].err = std::string("decode failed: ") + ex.what();
+    {
+        std::atomic<uint32_t> next{0};
+        auto work = [&](int t) {
+            Worker &w = s->workers[(size_t)t];
+            w.synthetic = s->synthetic;
+            for (;;) {
+                const uint32_t d0 = next.fetch_add(8);
+                if (d0 >= n_docs) break;
+                for (uint32_t d = d0; d < std::min(n_docs, d0 + 8); d++) {
+                    try {
+                        w.build(s->docs[d], d, in);
+                    } catch (const std::exception &ex) {   // e.g. bad_alloc: the document's error
+                        s->docs[d].err = std::string("decode failed: ") + ex.what();
+                    }
                 }
             }
-        }
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
-    work(0);
-    for (auto &t : pool) t.join();
-    // phase 2: concatenation in document order; local property ids -> the batch's ids
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
+        work(0);
+        for (auto &t : pool) t.join();
+    }
+    // phase 2 (sequential, small): the first failing document, each document's place in the
+    // output and its local -> batch id maps, numbered first-seen in document order; the
+    // concatenation itself runs in parallel straight into the caller's arrays (fetch)
     size_t ns = 0, ntx = 0, npr = 0;
     for (uint32_t d = 0; d < n_docs; d++) {
-        const DocOut &o = s->docs[d];
+        DocOut &o = s->docs[d];
         if (!o.err.empty()) {   // the first failing document, as a sequential load would report
             s->err = "document " + std::to_string(d) + ": " + o.err;
             return -1;
         }
+        o.si = ns;
+        o.ti = ntx;
+        o.pi = npr;
         ns += o.segs.size();
         ntx += o.text.size();
         npr += o.props.size();
+        if (s->synthetic) continue;
+        o.kmap.resize(o.keys.size());
+        for (size_t k = 0; k < o.keys.size(); k++) {
+            auto it = s->key_ids.find(o.keys[k]);
+            if (it == s->key_ids.end()) {
+                it = s->key_ids.emplace(o.keys[k], (uint32_t)s->keys.size()).first;
+                s->keys.push_back(o.keys[k]);
+            }
+            o.kmap[k] = it->second;
+        }
+        o.vmap.resize(o.vals.size());
+        for (size_t k = 0; k < o.vals.size(); k++) {
+            auto it = s->val_ids.find(o.vals[k]);
+            if (it == s->val_ids.end()) {
+                it = s->val_ids.emplace(o.vals[k], (uint32_t)s->vals.size()).first;
+                s->vals.push_back(o.vals[k]);
+            }
+            o.vmap[k] = it->second;
+        }
     }
     if (ntx > 0xFFFFFFFFull || npr > 0xFFFFFFFFull) {   // mt_seg_rec offsets are 32-bit
         s->err = "decoded text / property arena exceeds 2^32 entries: decode fewer documents per call";
         return -1;
     }
-    s->segs.resize(ns);
-    s->text.resize(ntx);
-    s->props.resize(npr);
-    s->doc_off.assign(1, 0);
-    s->n_header.resize(n_docs);
-    s->min_seq.resize(n_docs);
-    s->cur_seq.resize(n_docs);
-    s->catchup.resize(n_docs);
-    s->clients.resize(n_docs);
-    std::vector<uint32_t> kmap, vmap;
-    size_t si = 0, ti = 0, pi = 0;
-    for (uint32_t d = 0; d < n_docs; d++) {
-        DocOut &o = s->docs[d];
-        if (!s->synthetic) {
-            kmap.resize(o.keys.size());
-            for (size_t k = 0; k < o.keys.size(); k++) {
-                auto it = s->key_ids.find(o.keys[k]);
-                if (it == s->key_ids.end()) {
-                    it = s->key_ids.emplace(o.keys[k], (uint32_t)s->keys.size()).first;
-                    s->keys.push_back(o.keys[k]);
-                }
-                kmap[k] = it->second;
-            }
-            vmap.resize(o.vals.size());
-            for (size_t k = 0; k < o.vals.size(); k++) {
-                auto it = s->val_ids.find(o.vals[k]);
-                if (it == s->val_ids.end()) {
-                    it = s->val_ids.emplace(o.vals[k], (uint32_t)s->vals.size()).first;
-                    s->vals.push_back(o.vals[k]);
-                }
-                vmap[k] = it->second;
-            }
-        }
-        for (const mt_seg_rec &r0 : o.segs) {
-            mt_seg_rec r = r0;
-            if (!(r.flags & MT_F_MARKER)) r.payload += (uint32_t)ti;
-            if (r.props != MT_NO_PROPS) r.props += (uint32_t)pi;
-            s->segs[si++] = r;
-        }
-        if (!o.text.empty()) memcpy(&s->text[ti], o.text.data(), o.text.size() * sizeof(uint16_t));
-        ti += o.text.size();
-        if (s->synthetic) {
-            if (!o.props.empty()) memcpy(&s->props[pi], o.props.data(), o.props.size() * sizeof(uint32_t));
-            pi += o.props.size();
-        } else {
-            for (size_t i = 0; i < o.props.size();) {
-                const uint32_t n = o.props[i++];
-                s->props[pi++] = n;
-                for (uint32_t j = 0; j < n; j++, i += 2) {
-                    const uint32_t v = o.props[i + 1];
-                    s->props[pi++] = kmap[o.props[i]];
-                    s->props[pi++] = v == MT_VAL_NULL ? v : (vmap[v & ~MT_VAL_FALSY_BIT] | (v & MT_VAL_FALSY_BIT));
-                }
-            }
-        }
-        s->doc_off.push_back((int64_t)si);
-        s->n_header[d] = o.nh;
-        s->min_seq[d] = o.msn;
-        s->cur_seq[d] = o.seq;
-        s->catchup[d] = o.cu;
-        s->clients[d].swap(o.clients);
-    }
+    s->n_docs = n_docs;
+    s->threads = nt;
+    s->ns = ns;
+    s->ntx = ntx;
+    s->npr = npr;
     return 0;
 }
 
 int mt_snapdec_sizes(const mt_snapdec *s, uint64_t *n_segs, uint64_t *text_len, uint64_t *props_len) {
     if (!s) return -1;
-    if (n_segs) *n_segs = s->segs.size();
-    if (text_len) *text_len = s->text.size();
-    if (props_len) *props_len = s->props.size();
+    if (n_segs) *n_segs = s->ns;
+    if (text_len) *text_len = s->ntx;
+    if (props_len) *props_len = s->npr;
     return 0;
 }
 
 int mt_snapdec_fetch(const mt_snapdec *s, int64_t *doc_seg_off, int32_t *n_header, mt_seg_rec *segs, uint16_t *text,
                      uint32_t *props, int32_t *min_seq, int32_t *cur_seq, int64_t *catchup_blob) {
     if (!s) return -1;
-    auto cp = [](auto *dst, const auto &v) {
-        if (dst && !v.empty()) memcpy(dst, v.data(), v.size() * sizeof(v[0]));
-    };
-    cp(doc_seg_off, s->doc_off);
-    cp(n_header, s->n_header);
-    cp(segs, s->segs);
-    cp(text, s->text);
-    cp(props, s->props);
-    cp(min_seq, s->min_seq);
-    cp(cur_seq, s->cur_seq);
-    cp(catchup_blob, s->catchup);
+    const uint32_t n = s->n_docs;
+    // documents back to back, on the decode's threads (64 at a time: a document is ~10 KB)
+    parallel_docs(n, s->threads, 64, [&](uint32_t d) {
+        const DocOut &o = s->docs[d];
+        if (doc_seg_off) doc_seg_off[d] = (int64_t)o.si;
+        if (n_header) n_header[d] = o.nh;
+        if (min_seq) min_seq[d] = o.msn;
+        if (cur_seq) cur_seq[d] = o.seq;
+        if (catchup_blob) catchup_blob[d] = o.cu;
+        if (segs) {
+            mt_seg_rec *dst = segs + o.si;
+            for (size_t k = 0; k < o.segs.size(); k++) {
+                mt_seg_rec r = o.segs[k];
+                if (!(r.flags & MT_F_MARKER)) r.payload += (uint32_t)o.ti;
+                if (r.props != MT_NO_PROPS) r.props += (uint32_t)o.pi;
+                dst[k] = r;
+            }
+        }
+        if (text && !o.text.empty()) memcpy(text + o.ti, o.text.data(), o.text.size() * sizeof(uint16_t));
+        if (props && !o.props.empty()) {
+            if (s->synthetic) {
+                memcpy(props + o.pi, o.props.data(), o.props.size() * sizeof(uint32_t));
+            } else {
+                uint32_t *q = props + o.pi;
+                for (size_t i = 0; i < o.props.size();) {
+                    const uint32_t c = o.props[i++];
+                    *q++ = c;
+                    for (uint32_t j = 0; j < c; j++, i += 2) {
+                        const uint32_t v = o.props[i + 1];
+                        *q++ = o.kmap[o.props[i]];
+                        *q++ = v == MT_VAL_NULL ? v : (o.vmap[v & ~MT_VAL_FALSY_BIT] | (v & MT_VAL_FALSY_BIT));
+                    }
+                }
+            }
+        }
+    });
+    if (doc_seg_off) doc_seg_off[n] = (int64_t)s->ns;
     return 0;
 }
 
@@ -909,8 +974,8 @@ int64_t mt_snapdec_value(const mt_snapdec *s, uint32_t i, char *out, uint64_t ca
     return copy_out(s->vals[i], out, cap);
 }
 int64_t mt_snapdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint64_t cap) {
-    if (!s || d >= s->clients.size()) return -1;
-    return copy_out(s->clients[d], out, cap);
+    if (!s || d >= s->n_docs) return -1;
+    return copy_out(s->docs[d].clients, out, cap);
 }
 uint32_t mt_snapdec_num_keys(const mt_snapdec *s) { return s ? (uint32_t)s->keys.size() : 0; }
 uint32_t mt_snapdec_num_values(const mt_snapdec *s) { return s ? (uint32_t)s->vals.size() : 0; }

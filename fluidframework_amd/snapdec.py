@@ -105,9 +105,11 @@ class SummaryDecoder:
             raise SnapshotError(self.lib.mt_snapdec_error(self.h).decode())
         ns, nt, npr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self.lib.mt_snapdec_sizes(self.h, ctypes.byref(ns), ctypes.byref(nt), ctypes.byref(npr))
-        out = dict(segs=np.zeros(ns.value, dtype=SEG_DTYPE), doc_off=np.zeros(n + 1, dtype=np.int64),
-                   n_header=np.zeros(n, dtype=np.int32), text=np.zeros(max(nt.value, 1), dtype=np.uint16),
-                   props=np.zeros(max(npr.value, 1), dtype=np.uint32), min_seq=np.zeros(n, dtype=np.int32),
+        def arena(m, dt):   # filled whole by fetch; an empty arena is one zero
+            return np.empty(m, dtype=dt) if m else np.zeros(1, dtype=dt)
+        out = dict(segs=np.empty(ns.value, dtype=SEG_DTYPE), doc_off=np.zeros(n + 1, dtype=np.int64),
+                   n_header=np.zeros(n, dtype=np.int32), text=arena(nt.value, np.uint16),
+                   props=arena(npr.value, np.uint32), min_seq=np.zeros(n, dtype=np.int32),
                    cur_seq=np.zeros(n, dtype=np.int32))
         cu = np.zeros(n, dtype=np.int64)
         self.lib.mt_snapdec_fetch(self.h, _p(out["doc_off"]), _p(out["n_header"]), _p(out["segs"]), _p(out["text"]),
@@ -141,7 +143,10 @@ class SummaryDecoder:
         p[kpos + 1] = v
 
     def decode(self, summaries):
-        paths, blobs, off = self.pack(summaries)
+        return self.decode_packed_full(*self.pack(summaries))
+
+    def decode_packed_full(self, paths, blobs, off):
+        """decode() of already packed blob tables (pack())."""
         out, cu = self.decode_packed(paths, blobs, off)
         if not self.interner.synthetic:
             self._remap(out)

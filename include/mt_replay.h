@@ -163,6 +163,15 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
                                   const mt_seg_rec *segs, uint64_t n_segs, const uint16_t *text, uint64_t text_len,
                                   const uint32_t *props, uint64_t props_len, const int32_t *min_seq,
                                   const int32_t *cur_seq);
+/* ... for documents [doc_lo, doc_lo + n_docs) of the handle only (summary d -> document
+   doc_lo + d; the arrays are sized n_docs): a cold catch-up that decodes and loads the
+   handle's documents in slices, each slice's load overlapping the host decode of the next
+   (fluidframework_amd.MergeTreeBatch.catch_up).  mt_snapshots_load_async leaves the other
+   documents untouched. */
+mt_snapshots *mt_snapshots_upload_range(mt_handle *h, uint32_t doc_lo, uint32_t n_docs, const int64_t *doc_seg_off,
+                                        const int32_t *n_header, const mt_seg_rec *segs, uint64_t n_segs,
+                                        const uint16_t *text, uint64_t text_len, const uint32_t *props,
+                                        uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq);
 int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s);
 void mt_snapshots_free(mt_snapshots *s);
 

@@ -40,7 +40,9 @@ int mt_snapdec_sizes(const mt_snapdec *s, uint64_t *n_segs, uint64_t *text_len, 
 
 /* the last result: doc_seg_off[n_docs + 1], n_header[n_docs], segs[n_segs], text, props,
    min_seq[n_docs], cur_seq[n_docs] (the mt_load_snapshots arguments), and per document the
-   index of its legacy catch-up blob (-1: none; the caller parses those messages) */
+   index of its legacy catch-up blob (-1: none; the caller parses those messages).  The
+   documents are copied into the caller's arrays in parallel, on the decode's threads; any
+   pointer may be null (that output is skipped). */
 int mt_snapdec_fetch(const mt_snapdec *s, int64_t *doc_seg_off, int32_t *n_header, mt_seg_rec *segs, uint16_t *text,
                      uint32_t *props, int32_t *min_seq, int32_t *cur_seq, int64_t *catchup_blob);
 

@@ -245,6 +245,38 @@ def test_gpu_summaries_native_decoder_match_reference(name, tier):
     assert not bad, f"{name}: {bad[:4]}"
 
 
+@pytest.mark.parametrize("slice_docs", [1, 7])
+@pytest.mark.parametrize("tier", ["lds", "paged", "paged_load"])
+def test_gpu_catch_up_in_slices_matches_reference(tier, slice_docs):
+    """MergeTreeBatch.catch_up: the reference-written summaries decoded slice by slice on a
+    host thread while earlier slices load into their document ranges on the GPU
+    (mt_snapshots_upload_range); every document, whatever its status (Q6 failures,
+    MT_DOC_ALIASED), ends as load_summaries leaves it, and after the tails as the reference."""
+    from fluidframework_amd.wire import Batch
+    fx = gu.load("ref_snap_body")
+    docs = fx["docs"]
+    ref_i, got_i = gu.Interner(), gu.Interner()
+    ref = _gpu_batch(len(docs), **SNAP_TIERS[tier])
+    got = _gpu_batch(len(docs), **SNAP_TIERS[tier])
+    cu_r, cl_r = ref.load_summaries([d["chunks"] for d in docs], ref_i, threads=4)
+    cu_g, cl_g = got.catch_up([d["chunks"] for d in docs], got_i, threads=3, slice_docs=slice_docs)
+    assert cu_r == cu_g and cl_r == cl_g
+    assert np.array_equal(ref.status(), got.status())
+    assert np.array_equal(ref.checksums(), got.checksums())
+    ok = [i for i, d in enumerate(docs) if gu.snap_status(d) == 0]
+    b = Batch(got_i)
+    for i, d in enumerate(docs):
+        b.add_doc("", (list(cu_g[i]) + gu.compact_msgs_to_dicts(d.get("tail", []))) if i in ok else [],
+                  clients=cl_g[i])
+    got.apply_arrays(b.arrays())
+    bad = []
+    for i in ok:
+        errs = gu.compare_oracle(_gpu_outputs(got, i), gu.expected_snap(docs[i], got_i))
+        if errs:
+            bad.append((docs[i]["doc"], errs))
+    assert not bad, bad[:4]
+
+
 @pytest.mark.parametrize("tier", ["lds", "paged"])
 @pytest.mark.parametrize("name", ["ref_snap", "ref_snap_body"])
 def test_gpu_snapshot_emission_matches_reference(name, tier):
