@@ -267,6 +267,18 @@ def c5_end_to_end(mt, counts, recs, text, props, mn, cu, chunk, tail_arr, tail, 
     for d in range(n_emit):
         specs, lengths = record_specs(recs[r0[d]:r0[d + 1]], text[t0[d]:t0[d + 1]], props[p0[d]:p0[d + 1]], it, names)
         emitted.append(SummaryDecoder.pack([encode_chunks(specs, lengths, int(mn[d]), int(cu[d]), chunk)]))
+    # the tails continue with the short ids the summaries' loads assign (getOrAddShortClientId
+    # in first-seen order, as a reference client loading the summary would): decoded once here
+    remap = np.zeros((n_emit, 4097), dtype=np.uint16)   # writer ids 0..4096 (others unchanged)
+    _, _, cl = SummaryDecoder(Interner(synthetic=True), threads=threads).decode_packed_full(
+        [p for e in emitted for p in e[0]], [b for e in emitted for b in e[1]],
+        list(np.cumsum([0] + [len(e[0]) for e in emitted])))
+    for d in range(n_emit):
+        remap[d] = np.arange(4097, dtype=np.uint16)
+        for name, short in cl[d].items():
+            k = int(name[len("client-"):])
+            if 0 <= k <= 4096:
+                remap[d, k] = short
     n = mt.n_docs
     paths, blobs, off = [], [], [0]
     for d in range(n):
@@ -276,23 +288,31 @@ def c5_end_to_end(mt, counts, recs, text, props, mn, cu, chunk, tail_arr, tail, 
         off.append(len(paths))
     nbytes = sum(len(b) for b in blobs)
     src = np.arange(n) % n_emit
-    ops = tail_arr["ops"].reshape(-1, tail)[src].ravel()
+    ops = tail_arr["ops"].reshape(-1, tail)[src].copy()
+    c = ops["client"].astype(np.int64)
+    ops["client"] = np.where(c <= 4096, remap[src[:, None], np.minimum(c, 4096)], c)
+    ops = ops.ravel()
     tb = mt.upload(dict(tail_arr, ops=ops, doc_off=np.arange(n + 1, dtype=np.int64) * tail))
-    rates = []
-    for rep in range(3):   # the first run warms the decoder's buffers and the workers
-        mt.sync()
-        t = time.perf_counter()
-        mt.catch_up(None, Interner(synthetic=True), threads=threads, slice_docs=slice_docs, packed=(paths, blobs, off))
-        tb.apply_async()
-        mt.sync()
-        rates.append(time.perf_counter() - t)
-    el = min(rates[1:])
+    best = None
+    for dec_threads in sorted({threads, max(1, threads - 1)}):   # all cores, or one left to the uploads
+        times = []
+        for rep in range(3):   # the first run warms the decoder's buffers and the workers
+            mt.sync()
+            t = time.perf_counter()
+            mt.catch_up(None, Interner(synthetic=True), threads=dec_threads, slice_docs=slice_docs,
+                        packed=(paths, blobs, off))
+            tb.apply_async()
+            mt.sync()
+            times.append(time.perf_counter() - t)
+        if best is None or min(times[1:]) < best[0]:
+            best = (min(times[1:]), dec_threads)
+    el, threads = best
     tb.free()
     ok = bool(np.array_equal(mt.checksums(), sums[src]) and np.array_equal(mt.status(), status[src]))
     return dict(value=round(n / el, 1), unit="docs/s", cores=threads, json_mb_per_s=round(nbytes / el / 1e6, 1),
                 slice_docs=slice_docs, equals_device_only_step=ok,
                 sample=f"{n} documents ({nbytes / 1e6:.0f} MB of summary JSON, {n_emit} distinct summaries) "
-                       f"decoded on {threads} host threads, uploaded, loaded and their {tail}-op tails replayed: "
+                       f"decoded on {threads} host threads (+ the upload thread), uploaded, loaded and their {tail}-op tails replayed: "
                        f"{el:.3f} s (best of 2 after a warm-up run)")
 
 

@@ -270,6 +270,13 @@ class MergeTreeBatch:
         return dict(pages=int(out[0]), unsettled=int(out[1]), heap=int(out[2]), segments=int(out[3]),
                     tight_handovers=int(out[4]))
 
+    def last_grown(self):
+        """The last batch's growth step (mt_last_grown): documents moved to larger paged
+        capacities, rounds, documents in the big region and its capacities."""
+        out = np.zeros(6, dtype=np.uint32)
+        self._check(self.lib.mt_last_grown(self.h, _native.ptr(out)), "mt_last_grown")
+        return dict(zip(["grown", "rounds", "in_big_region", "pages", "unsettled", "heap"], (int(x) for x in out)))
+
     def last_kernel_ms(self):
         return float(self.lib.mt_last_kernel_ms(self.h))
 

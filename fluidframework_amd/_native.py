@@ -79,6 +79,7 @@ SIGNATURES = [
     ("mt_last_kernel_ms", ctypes.c_float, [_P]),
     ("mt_last_hbm_docs", _I, [_P, _P]),
     ("mt_last_paged_peaks", _I, [_P, _P]),
+    ("mt_last_grown", _I, [_P, _P]),
     ("mt_generate", _P, [_P, _P, _U32, _P]),
     ("mt_generated_seeds", _I, [_P, _P, _U32, _P, _P]),
     ("mt_batch_sizes", _I, [_P, _P, _P, _P]),

@@ -77,6 +77,56 @@ static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { retu
 #define HDR_MUNLINK 6
 #define HDR_DLOG_OVF 7        // the delta log overflowed (records dropped since the last reset)
 
+// A set of paged arrays with its per-document capacities (strides).  The handle's main set
+// is sized by mt_options; documents that outgrow it move to a second, larger set -- the
+// *big region* -- in the growth step of mt_sync ("Growth").
+struct PagedRegion {
+    v4i *A;                   // [slots][PP][64]
+    u64 *O;
+    v4u *B;
+    PageMeta *meta;           // [slots][PP]
+    uint16_t *dir;            // [slots][PP]
+    uint8_t *cnt;             // [slots][MT_LV][PP]
+    v2i *heap;                // [slots][PH + 1]
+    int32_t *upage;           // [slots][UT]
+    v4i *uA;
+    u64 *uO;
+    int32_t PP, PH, UT, slots;
+};
+// document doc's paged arrays (bslot: its slot in the big region, -1: the main set); the
+// uid -> page map always stays in the main set (DevState.pgUmap)
+struct PagedBase {
+    v4i *A;
+    u64 *O;
+    v4u *B;
+    PageMeta *meta;
+    uint16_t *dir;
+    uint8_t *cnt;
+    v2i *heap;
+    int32_t *upage;
+    v4i *uA;
+    u64 *uO;
+    int32_t PP, PH, UT;
+};
+__host__ __device__ inline PagedBase paged_base(const PagedRegion &R, size_t i) {
+    PagedBase b;
+    const size_t PP = (size_t)R.PP;
+    b.A = R.A + i * PP * MT_PG_SLOTS;
+    b.O = R.O + i * PP * MT_PG_SLOTS;
+    b.B = R.B + i * PP * MT_PG_SLOTS;
+    b.meta = R.meta + i * PP;
+    b.dir = R.dir + i * PP;
+    b.cnt = R.cnt + i * MT_LV * PP;
+    b.heap = R.heap + i * (size_t)(R.PH + 1);
+    b.upage = R.upage + i * (size_t)R.UT;
+    b.uA = R.uA + i * (size_t)R.UT;
+    b.uO = R.uO + i * (size_t)R.UT;
+    b.PP = R.PP;
+    b.PH = R.PH;
+    b.UT = R.UT;
+    return b;
+}
+
 struct DevState {
     DocHdr *hdr;
     v4i *segA;
@@ -105,6 +155,8 @@ struct DevState {
     u64 *pgUtO;
     uint16_t *pgUmap;         // [n_docs][UM] uid -> page
     int32_t PP, PH, UT, UM;
+    int32_t *bslot;           // [n_docs] slot in the big region (-1: main arrays); null: no big region
+    PagedRegion big;          // documents re-tiered by the growth step (larger PP / PH / UT)
     int32_t S, B, H, T, P, DL;
     int32_t DLR;              // rich delta log: segment text / properties + maintenance events
     // segment ordinals (mt_options.segment_ordinals, flat tiers; null otherwise): every
@@ -119,6 +171,16 @@ struct DevState {
     struct PendQ *segP;       // [n_docs][S] per segment: its pending segment groups
     int32_t LG;               // group ids per document (outstanding segment groups)
 };
+
+__host__ __device__ inline PagedRegion main_region(const DevState &st) {
+    return PagedRegion{st.pgA, st.pgO, st.pgB, st.pgMeta, st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA,
+                       st.pgUtO, st.PP, st.PH, st.UT, st.n_docs};
+}
+// the paged arrays of document doc (device side: its slot from st.bslot)
+__device__ inline PagedBase doc_paged(const DevState &st, int doc) {
+    const int s = st.bslot ? st.bslot[doc] : -1;
+    return s >= 0 ? paged_base(st.big, (size_t)s) : paged_base(main_region(st), (size_t)doc);
+}
 
 // ------------------------------------------------------------------ wave primitives
 // lane within the wavefront (the LDS-tier replay may hold several documents per workgroup,

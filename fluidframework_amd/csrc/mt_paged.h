@@ -68,9 +68,18 @@ template <class T> struct PagedDoc {
 struct PagedCaps {
     int PP, PH, UT;
     int tight;   // 1: hand over instead of failing; 0: the HBM capacities (last tier)
-    int stage;   // retry[doc] value this launch serves (1: from the LDS tier, 2: from the tight tier)
+    int stage;   // retry[doc] value this launch serves (1: from the LDS tier, 2: from the tight
+                 // tier, 3: from the growth step)
     int narrow;  // TierPagedT<., true>: 32-bit overlap masks in LDS (tight tier only)
+    int grow;    // last tier: a document that does not fit at load, or whose next message could
+                 // outgrow these capacities, is handed to the host's growth step (retry = 3)
+                 // instead of failing -- re-tiered to a larger HBM region, it continues there
 };
+// what a hand-over ran out of (PagedCaps.grow: the capacities the growth step doubles)
+#define PG_NEED_TABLE 1
+#define PG_NEED_HEAP 2
+#define PG_NEED_PAGES 4
+#define PG_NEED_NARROW 8
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
 
@@ -934,21 +943,34 @@ TD void pg_renumber(PagedDoc<T> &pd) {
 // marked); the heap by <= 1 / <= 1 + (pos2 - pos1) (one entry per touched leaf block); a
 // message splits or repacks a few pages (8 kept in reserve).  pd.wgrow bounds what the
 // window added since its table entries were last rebuilt.
-TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
+// Returns 0 (room: the message is applied) or the PG_NEED_* capacities it could outgrow.
+TD int pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const bool range = op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
     const int span = range ? min(max(op.pos2 - op.pos1, 0), 1 << 20) : 0;
     const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
+    int need = 0;
     // a narrow tier holds overlap slots 1..32 only
-    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
-    if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
-    if (pd.w.heap_n + hp_b > pd.PH) return false;
-    if (nbr(pd.up, 1) + 8 > pd.PP) return false;
+    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) need |= PG_NEED_NARROW;
+    if (pd.ut_n + pd.wgrow + ut_b > pd.UT) need |= PG_NEED_TABLE;
+    if (pd.w.heap_n + hp_b > pd.PH) need |= PG_NEED_HEAP;
+    if (nbr(pd.up, 1) + 8 > pd.PP) need |= PG_NEED_PAGES;
     for (int l = 2; l < pd.up.depth; l++)
-        if (nbr(pd.up, l) + 4 > bcap(pd.up, l)) return false;
+        if (nbr(pd.up, l) + 4 > bcap(pd.up, l)) need |= PG_NEED_PAGES;
+    if (need) return need;
     pd.opbound = ut_b;
     pd.wgrow += ut_b;
-    return true;
+    return 0;
+}
+// pg_load's capacity checks as PG_NEED_* bits (0: it fits this launch)
+TD int pg_load_need(PagedDoc<T> &pd, const DevState &st) {
+    const DocHdr h = *pd.w.hp;
+    int need = 0;
+    if (h.n_blk[1] > pd.PP) need |= PG_NEED_PAGES;
+    if (h.pad[HDR_UTN] > pd.UT) need |= PG_NEED_TABLE;
+    if (h.heap_n > pd.PH) need |= PG_NEED_HEAP;
+    if (T::kOvlBits < 64 && pd.w.wide) need |= PG_NEED_NARROW;
+    return need ? need : PG_NEED_PAGES;   // otherwise a page id above this launch's capacity
 }
 
 // Client.applyMsg (MT/client.ts:797-819) for a paged document; mirrors apply_op.
@@ -1155,13 +1177,14 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
 
 // ------------------------------------------------------------------ bind / store / convert
 // Per-document HBM bases of the paged arrays the op path uses (pages, uid map).
+// (the main arrays, or the document's slot in the big region after a growth step)
 TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
-    const size_t PP = st.PP;
-    pd.gA = (GLB_AS v4i *)(st.pgA + (size_t)doc * PP * MT_PG_SLOTS);
-    pd.gO = (GLB_AS u64 *)(st.pgO + (size_t)doc * PP * MT_PG_SLOTS);
-    pd.gB = (GLB_AS v4u *)(st.pgB + (size_t)doc * PP * MT_PG_SLOTS);
+    const PagedBase b = doc_paged(st, doc);
+    pd.gA = (GLB_AS v4i *)b.A;
+    pd.gO = (GLB_AS u64 *)b.O;
+    pd.gB = (GLB_AS v4u *)b.B;
     pd.gumap = (GLB_AS uint16_t *)(st.pgUmap + (size_t)doc * st.UM);
-    pd.PPh = st.PP;
+    pd.PPh = b.PP;
     pd.UM = st.UM;
     pd.doc = doc;
 }
@@ -1177,15 +1200,15 @@ struct PgCold {
     GLB_AS u64 *guO;
 };
 __device__ __forceinline__ PgCold pg_cold(const DevState &st, int doc) {
-    const size_t PP = st.PP;
+    const PagedBase b = doc_paged(st, doc);
     PgCold c;
-    c.gmeta = (GLB_AS PageMeta *)(st.pgMeta + (size_t)doc * PP);
-    c.gdir = (GLB_AS uint16_t *)(st.pgDir + (size_t)doc * PP);
-    c.gcnt = (GLB_AS uint8_t *)(st.pgCnt + (size_t)doc * MT_LV * PP);
-    c.gheap = (GLB_AS v2i *)(st.pgHeap + (size_t)doc * (st.PH + 1));
-    c.gupage = (GLB_AS int *)(st.pgUtPage + (size_t)doc * st.UT);
-    c.guA = (GLB_AS v4i *)(st.pgUtA + (size_t)doc * st.UT);
-    c.guO = (GLB_AS u64 *)(st.pgUtO + (size_t)doc * st.UT);
+    c.gmeta = (GLB_AS PageMeta *)b.meta;
+    c.gdir = (GLB_AS uint16_t *)b.dir;
+    c.gcnt = (GLB_AS uint8_t *)b.cnt;
+    c.gheap = (GLB_AS v2i *)b.heap;
+    c.gupage = (GLB_AS int *)b.upage;
+    c.guA = (GLB_AS v4i *)b.uA;
+    c.guO = (GLB_AS u64 *)b.uO;
     return c;
 }
 

@@ -615,12 +615,19 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 // A tight launch (pc.tight) hands a document to the next launch -- retry[doc] = 2 from
 // message resume[doc] -- when it does not fit its LDS capacities at load, or before a message
 // that could outgrow them (pg_room); stats[12] counts those hand-overs.
+// A last tier with PagedCaps.grow hands a document to the growth step the same way (retry[doc]
+// = 3; stats[13] counts them, stats[14] ORs the PG_NEED_* capacities they ran out of).
 template <class T>
-__device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t k) {
+__device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t k, const PagedCaps &pc, int need) {
     if (lane() == 0) {
-        st.retry[doc] = 2;
+        st.retry[doc] = pc.tight ? 2 : 3;
         st.resume[doc] = k;
-        atomicAdd(st.stats + 12, 1u);
+        if (pc.tight) {
+            atomicAdd(st.stats + 12, 1u);
+        } else {
+            atomicAdd(st.stats + 13, 1u);
+            atomicOr(st.stats + 14, (uint32_t)need);
+        }
     }
 }
 // One launch of a sliced paged replay (mt_options.paged_slices): documents in [skip_lo,
@@ -656,9 +663,9 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     }
     if (st.hdr[doc].pad[HDR_PAGED]) {
         if (!pg_load(pd, st)) {
-            if (pc.tight) {
-                pg_handover<T>(st, doc, k0);
-            } else if (lane() == 0) {   // cannot happen: the last tier has the HBM capacities
+            if (pc.tight || pc.grow) {
+                pg_handover<T>(st, doc, k0, pc, pg_load_need(pd, st));
+            } else if (lane() == 0) {   // cannot happen: the last tier has the document's capacities
                 st.hdr[doc].status = MT_DOC_CAPACITY;
                 st.retry[doc] = 0;
             }
@@ -666,9 +673,15 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
         }
     } else if (!pg_convert(pd, flat_src(st, doc))) {
         // stays flat (the pages written so far are unreferenced): the next tier converts it
-        // again, or only the status changes
+        // again (the growth step: at larger page / heap / table capacities), or only the
+        // status changes
+        const int cc = w.cap_cause;
+        const int need = cc == 7 ? PG_NEED_PAGES : (cc == 3 ? PG_NEED_HEAP : (cc == 8 ? PG_NEED_TABLE : 0));
         if (pc.tight && w.status == MT_DOC_CAPACITY) {
-            pg_handover<T>(st, doc, k0);
+            pg_handover<T>(st, doc, k0, pc, need);
+        } else if (pc.grow && w.status == MT_DOC_CAPACITY && need) {
+            w.status = 0;   // the header is untouched: only the pages are rewritten there
+            pg_handover<T>(st, doc, k0, pc, need);
         } else if (lane() == 0) {
             st.hdr[doc].status = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
             st.retry[doc] = 0;
@@ -680,6 +693,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
     int pk_ut = 0, pk_heap = 0;
     int64_t spill_at = -1;
+    int need = 0;
     for (int64_t kb = k0; kb < k1 && w.status == 0 && spill_at < 0; kb += MT_WAVE) {
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
@@ -725,9 +739,12 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
             in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
-            if (pc.tight && !pg_room(pd, in.op)) {
-                spill_at = kb + j;
-                break;
+            if (pc.tight || pc.grow) {
+                need = pg_room(pd, in.op);
+                if (need) {
+                    spill_at = kb + j;
+                    break;
+                }
             }
             pg_apply_op(pd, in, gt, gp);
             pk_ut = max(pk_ut, pd.ut_n);
@@ -739,7 +756,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     pg_store(pd, st);
     pg_peaks(st, pd, pk_ut, pk_heap);
     if (spill_at >= 0 && w.status == 0)
-        pg_handover<T>(st, doc, spill_at);
+        pg_handover<T>(st, doc, spill_at, pc, need);
     else if (k1 < kend && w.status == 0) {   // slice done: the next launch of this stage resumes
         if (lane() == 0) st.resume[doc] = k1;
     } else if (lane() == 0)
@@ -799,7 +816,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         }
         OpIn in;
         gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
-        if (pc.tight && !pg_room(pd, in.op)) {
+        if (pc.tight && pg_room(pd, in.op)) {
             if (lane() == 0) {
                 st.retry[doc] = 2;
                 atomicAdd(st.stats + 12, 1u);
@@ -900,11 +917,11 @@ __device__ static SegRanges seg_ranges(const DevState &st, int doc, const DocHdr
     SegRanges R;
     R.paged = h.pad[HDR_PAGED] != 0;
     if (R.paged) {
-        const size_t PP = st.PP;
-        R.A = st.pgA + (size_t)doc * PP * MT_PG_SLOTS;
-        R.B = st.pgB + (size_t)doc * PP * MT_PG_SLOTS;
-        R.dir = st.pgDir + (size_t)doc * PP;
-        R.meta = st.pgMeta + (size_t)doc * PP;
+        const PagedBase b = doc_paged(st, doc);
+        R.A = b.A;
+        R.B = b.B;
+        R.dir = b.dir;
+        R.meta = b.meta;
         R.nr = h.pad[HDR_NPAGES];
         R.n = 0;
     } else {
@@ -1244,8 +1261,15 @@ struct mt_handle {
     PagedCaps pg_full{0, 0, 0, 0, 1, 0};    // paged tier at the HBM capacities
     int paged_slices = 0;                   // mt_options.paged_slices
     int pg_resident = 0;                    // documents resident at once in a tight paged launch
+    // growth step (mt_settle): the batch whose launches may have handed documents to it, the
+    // big region's capacities (PP == 0: none yet) and its slots, the documents moved there
+    struct mt_batch *pending = nullptr;
+    PagedCaps big_caps{0, 0, 0, 0, 3, 0, 1};
+    std::vector<int32_t> bslot_h;           // host mirror of st.bslot
+    uint32_t grown_last = 0, grow_rounds_last = 0;
 };
 struct mt_batch {
+    mt_handle *owner = nullptr;   // the handle whose growth step still needs this batch
     int device = 0;
     uint32_t n_docs = 0;
     uint64_t n_ops = 0, text_len = 0, props_len = 0;
@@ -1262,6 +1286,15 @@ struct mt_batch {
             if (h) (h)->err = std::string(#x) + ": " + hipGetErrorString(e_);      \
             return MT_E_HIP;                                                       \
         }                                                                          \
+    } while (0)
+
+static int mt_settle(mt_handle *h);
+// waits for the stream and finishes a pending growth step (API entry points that read state or
+// enqueue work: a growth step's launches must come before anything else)
+#define SETTLE(h)                          \
+    do {                                   \
+        const int rc_ = mt_settle(h);      \
+        if (rc_) return rc_;               \
     } while (0)
 
 static TierCaps glb_caps(const mt_handle *h) { return TierCaps{0, h->st.B, 0, h->lds.S > 0 ? 1 : 0}; }
@@ -1363,7 +1396,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         st.UT = o.unsettled_capacity > 0 ? o.unsettled_capacity : 256;
         st.UM = std::min(o.uid_capacity > 0 ? o.uid_capacity : 65536, 1 << 24);
         st.UM = std::max(st.UM, 256);
-        h->pg_full = PagedCaps{st.PP, st.PH, st.UT, 0, 1, 0};
+        h->pg_full = PagedCaps{st.PP, st.PH, st.UT, 0, 1, 0, 1};
         const PagedCaps t{o.lds_page_capacity > 0 ? std::min(o.lds_page_capacity, st.PP) : st.PP,
                           o.lds_page_heap_capacity > 0 ? std::min(o.lds_page_heap_capacity, st.PH) : st.PH,
                           o.lds_unsettled_capacity > 0 ? std::min(o.lds_unsettled_capacity, st.UT) : st.UT, 1, 1,
@@ -1467,9 +1500,19 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     return h;
 }
 
+static void free_region(PagedRegion &R) {
+    void *ps[] = {R.A, R.O, R.B, R.meta, R.dir, R.cnt, R.heap, R.upage, R.uA, R.uO};
+    for (void *p : ps)
+        if (p) hipFree(p);
+    R = PagedRegion{};
+}
+
 void mt_destroy(mt_handle *h) {
     if (!h) return;
     hipSetDevice(h->device);
+    if (h->pending) h->pending->owner = nullptr;
+    free_region(h->st.big);
+    if (h->st.bslot) hipFree(h->st.bslot);
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
@@ -1503,7 +1546,7 @@ int mt_start_collaboration(mt_handle *h, const int32_t *min_seq, const int32_t *
             h->err = "mt_start_collaboration: document " + std::to_string(d) + " has currentSeq < minSeq";
             return MT_E_INVALID;
         }
-    HIPCHK(h, hipSetDevice(h->device));
+    SETTLE(h);
     int32_t *d_w = nullptr;
     HIPCHK(h, hipMalloc(&d_w, (size_t)h->n_docs * 8 + 8));
     bool ok = hipMemcpyAsync(d_w, min_seq, (size_t)h->n_docs * 4, hipMemcpyHostToDevice, h->stream) == hipSuccess &&
@@ -1524,8 +1567,7 @@ int mt_start_collaboration(mt_handle *h, const int32_t *min_seq, const int32_t *
 
 int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *seed_text) {
     if (!h) return MT_E_INVALID;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     if (h->d_seed_off) hipFree(h->d_seed_off);
     if (h->d_seed) hipFree(h->d_seed);
     h->d_seed_off = nullptr;
@@ -1558,6 +1600,7 @@ int mt_load_initial_text(mt_handle *h, const int64_t *seed_off, const uint16_t *
 
 int mt_reset(mt_handle *h) {
     if (!h) return MT_E_INVALID;
+    if (h->pending) SETTLE(h);
     HIPCHK(h, hipSetDevice(h->device));
     if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
     hipLaunchKernelGGL(k_init, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, h->d_seed_off, h->d_seed);
@@ -1605,8 +1648,32 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
     return b;
 }
 
+// One paged launch over every document (those not at stage pc.stage exit at once).
+static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl) {
+    const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8).total;
+    const dim3 g(h->n_docs), blk(MT_WAVE);
+    if (h->st.DL && pc.narrow)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+                           b->text, b->props, res, pc, sl);
+    else if (h->st.DL)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true>>), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
+                           b->props, res, pc, sl);
+    else if (pc.narrow)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+                           b->text, b->props, res, pc, sl);
+    else
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false>>), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
+                           b->props, res, pc, sl);
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
 int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     if (!h || !b || b->n_docs != h->n_docs) return MT_E_INVALID;
+    if (h->pending) {   // the previous batch's growth step runs before anything else
+        const int rc = mt_settle(h);
+        if (rc) return rc;
+    }
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
@@ -1635,9 +1702,7 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         const int n = (int)h->n_docs;
         for (const PagedCaps *pc : tiers) {
             if (!pc) continue;
-            const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, 0, pc->narrow ? 4 : 8).total;
             const int res = pc->stage == 2 ? 1 : use_resume;
-            const dim3 g(h->n_docs), blk(MT_WAVE);
             // the launches of this tier: one over every document, or (paged_slices, first
             // tier) m slices each leaving out a window of the r = n mod resident left-over
             // documents -- every launch is then whole rounds -- and a last one without limits
@@ -1666,20 +1731,8 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
                 res_k = 1;
             }
             for (const PagedSlice &sl : sls) {
-                const int res = res_k;
-                if (h->st.DL && pc->narrow)
-                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops,
-                                       b->off, b->text, b->props, res, *pc, sl);
-                else if (h->st.DL)
-                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
-                                       b->text, b->props, res, *pc, sl);
-                else if (pc->narrow)
-                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true>>), g, blk, lb, h->stream, h->st, b->ops,
-                                       b->off, b->text, b->props, res, *pc, sl);
-                else
-                    hipLaunchKernelGGL((k_replay_paged<TierPagedT<false>>), g, blk, lb, h->stream, h->st, b->ops,
-                                       b->off, b->text, b->props, res, *pc, sl);
-                HIPCHK(h, hipGetLastError());
+                const int rc = launch_paged(h, b, *pc, res_k, sl);
+                if (rc) return rc;
             }
         }
     } else if (h->live && h->st.DL)
@@ -1697,13 +1750,228 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
+    if (h->st.PP > 0) {   // its last paged tier may hand documents to the growth step
+        h->pending = const_cast<mt_batch *>(b);
+        h->pending->owner = h;
+    }
     return 0;
 }
 
 uint64_t mt_batch_num_ops(const mt_batch *b) { return b ? b->n_ops : 0; }
 
+// ---------------------------------------------------------------- growth step
+// The paged capacities of mt_options (page_capacity, unsettled_capacity, page_heap_capacity)
+// are a starting point, not a limit.  The last paged tier (PagedCaps.grow) hands a document
+// that does not fit it at load, or whose next message could outgrow it (pg_room), to this
+// step with the message index (retry = 3); mt_settle then moves every such document into
+// the *big region* -- a second set of paged arrays whose capacities are doubled where the
+// documents ran out (bounded by the 160 KiB a paged launch may stage in LDS) -- and replays
+// the rest of their messages there, round after round, before anything else runs on the
+// stream.  Only documents beyond the handle's sizing pay for it; the others never move.
+struct MigItem {
+    int32_t doc, src, dst;   // src: slot in the old big region (-1: the main arrays)
+};
+__global__ void __launch_bounds__(MT_WAVE) k_migrate_paged(DevState st, PagedRegion old_big, PagedRegion dst_r,
+                                                           const MigItem *items) {
+    const MigItem it = items[blockIdx.x];
+    if (!st.hdr[it.doc].pad[HDR_PAGED]) return;   // still flat: pg_convert pages it at the new capacities
+    const PagedBase s = it.src < 0 ? paged_base(main_region(st), (size_t)it.doc) : paged_base(old_big, (size_t)it.src);
+    const PagedBase d = paged_base(dst_r, (size_t)it.dst);
+    const size_t ns = (size_t)s.PP * MT_PG_SLOTS;   // page p slot k sits at p * 64 + k in both
+    for (size_t i = lane(); i < ns; i += MT_WAVE) {
+        d.A[i] = s.A[i];
+        d.O[i] = s.O[i];
+        d.B[i] = s.B[i];
+    }
+    for (int i = lane(); i < s.PP; i += MT_WAVE) {
+        d.meta[i] = s.meta[i];
+        d.dir[i] = s.dir[i];
+    }
+    for (int l = 0; l < MT_LV; l++)
+        for (int b = lane(); b < s.PP; b += MT_WAVE) d.cnt[(size_t)l * d.PP + b] = s.cnt[(size_t)l * s.PP + b];
+    for (int i = lane(); i <= s.PH; i += MT_WAVE) d.heap[i] = s.heap[i];
+    for (int i = lane(); i < s.UT; i += MT_WAVE) {
+        d.upage[i] = s.upage[i];
+        d.uA[i] = s.uA[i];
+        d.uO[i] = s.uO[i];
+    }
+}
+// documents the growth step cannot serve (out of device memory) fail as before the step existed
+__global__ void k_fail_grow(DevState st) {
+    const int doc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (doc >= st.n_docs || st.retry[doc] != 3) return;
+    st.retry[doc] = 0;
+    if (st.hdr[doc].status == 0) {
+        st.hdr[doc].status = MT_DOC_CAPACITY;
+        st.hdr[doc].pad[HDR_DIAG] = 12;
+    }
+}
+
+static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c) {
+    R = PagedRegion{};
+    R.PP = c.PP;
+    R.PH = c.PH;
+    R.UT = c.UT;
+    R.slots = slots;
+    const size_t n = (size_t)slots, pages = n * c.PP;
+    bool ok = hipMalloc(&R.A, pages * MT_PG_SLOTS * sizeof(int4)) == hipSuccess &&
+              hipMalloc(&R.O, pages * MT_PG_SLOTS * sizeof(u64)) == hipSuccess &&
+              hipMalloc(&R.B, pages * MT_PG_SLOTS * sizeof(uint4)) == hipSuccess &&
+              hipMalloc(&R.meta, pages * sizeof(PageMeta)) == hipSuccess &&
+              hipMalloc(&R.dir, pages * sizeof(uint16_t)) == hipSuccess &&
+              hipMalloc(&R.cnt, pages * MT_LV) == hipSuccess &&
+              hipMalloc(&R.heap, n * (size_t)(c.PH + 1) * sizeof(int2)) == hipSuccess &&
+              hipMalloc(&R.upage, n * (size_t)c.UT * sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&R.uA, n * (size_t)c.UT * sizeof(int4)) == hipSuccess &&
+              hipMalloc(&R.uO, n * (size_t)c.UT * sizeof(u64)) == hipSuccess;
+    if (!ok) free_region(R);
+    return ok;
+}
+
+static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl);
+
+// Moves the documents of `moving` (and every document already there) into a new big region at
+// capacities c; synchronous.
+static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const PagedCaps &c) {
+    DevState &st = h->st;
+    const uint32_t n = h->n_docs;
+    if (!st.bslot) {
+        HIPCHK(h, hipMalloc(&st.bslot, (size_t)n * sizeof(int32_t)));
+        HIPCHK(h, hipMemset(st.bslot, 0xFF, (size_t)n * sizeof(int32_t)));
+        h->bslot_h.assign(n, -1);
+    }
+    std::vector<int32_t> nb(n, -1);
+    std::vector<MigItem> items;
+    std::vector<uint8_t> mv(n, 0);
+    for (uint32_t d : moving) mv[d] = 1;
+    int slots = 0;
+    for (uint32_t d = 0; d < n; d++)
+        if (h->bslot_h[d] >= 0 || mv[d]) {
+            nb[d] = slots;
+            items.push_back(MigItem{(int32_t)d, h->bslot_h[d], slots});
+            slots++;
+        }
+    PagedRegion R;
+    if (!alloc_region(R, std::max(slots, 1), c)) {
+        (void)hipGetLastError();
+        h->err = "growth step: device allocation of the big region failed";
+        return MT_E_NOMEM;
+    }
+    MigItem *d_items = nullptr;
+    if (hipMalloc(&d_items, items.size() * sizeof(MigItem)) != hipSuccess) {
+        free_region(R);
+        return MT_E_NOMEM;
+    }
+    HIPCHK(h, hipMemcpy(d_items, items.data(), items.size() * sizeof(MigItem), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_migrate_paged, dim3((uint32_t)items.size()), dim3(MT_WAVE), 0, h->stream, st, st.big, R,
+                       (const MigItem *)d_items);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    hipFree(d_items);
+    HIPCHK(h, hipMemcpy(st.bslot, nb.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+    free_region(st.big);
+    st.big = R;
+    h->bslot_h = nb;
+    h->big_caps = PagedCaps{c.PP, c.PH, c.UT, 0, 3, 0, 1};
+    const size_t lb = paged_layout(c.PP, c.PH, c.UT, 0, 8).total;
+    if (lb > 64 * 1024) {
+        const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true>>, (const void *)k_replay_paged<TierPagedT<false>>};
+        for (const void *k : ks) HIPCHK(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
+    }
+    return 0;
+}
+
+// After the launches of batch b: re-tiers and replays the documents they handed to the
+// growth step until none is left (synchronous).
+static int grow_loop(mt_handle *h, const mt_batch *b) {
+    DevState &st = h->st;
+    const uint32_t n = h->n_docs;
+    h->grown_last = 0;
+    h->grow_rounds_last = 0;
+    PagedCaps launched = h->pg_full;   // the capacities of the launch that handed them over
+    for (int round = 0; round < 32; round++) {
+        uint32_t g[2] = {0, 0};
+        HIPCHK(h, hipMemcpy(g, st.stats + 13, sizeof(g), hipMemcpyDeviceToHost));
+        if (g[0] == 0) return 0;
+        HIPCHK(h, hipMemset(st.stats + 13, 0, sizeof(g)));
+        std::vector<int32_t> retry(n);
+        HIPCHK(h, hipMemcpy(retry.data(), st.retry, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> moving;
+        for (uint32_t d = 0; d < n; d++)
+            if (retry[d] == 3) moving.push_back(d);
+        if (moving.empty()) return 0;
+        h->grown_last += (uint32_t)moving.size();
+        h->grow_rounds_last++;
+        // the new capacities: doubled where the documents ran out, never below the big
+        // region's, within the LDS one paged launch may stage
+        const bool have = h->big_caps.PP > 0;
+        auto fits = [](const PagedCaps &c) { return paged_layout(c.PP, c.PH, c.UT, 0, 8).total <= 160 * 1024; };
+        auto same = [](const PagedCaps &a, const PagedCaps &b) { return a.PP == b.PP && a.PH == b.PH && a.UT == b.UT; };
+        auto doubled = [&](const PagedCaps &c) {   // c doubled where needed, one capacity at a time while it fits
+            PagedCaps r = c, t = c;
+            if (g[1] & PG_NEED_TABLE) t.UT = std::min(2 * t.UT, 1 << 20);
+            if (fits(t)) r = t;
+            t = r;
+            if (g[1] & PG_NEED_HEAP) t.PH = std::min(2 * t.PH, 1 << 20);
+            if (fits(t)) r = t;
+            t = r;
+            if (g[1] & PG_NEED_PAGES) t.PP = std::min(2 * t.PP, 65535);
+            if (fits(t)) r = t;
+            return r;
+        };
+        PagedCaps nc = doubled(launched);
+        if (have) {
+            nc.PP = std::max(nc.PP, h->big_caps.PP);
+            nc.PH = std::max(nc.PH, h->big_caps.PH);
+            nc.UT = std::max(nc.UT, h->big_caps.UT);
+        }
+        int rc = 0;
+        PagedCaps pc = nc;
+        pc.grow = 0;
+        if (same(nc, launched)) {
+            // nothing can grow: the documents run to their end at the capacities they were
+            // handed over at (in their own region) and fail as before the step existed only
+            // if they do outgrow them
+            pc = launched;
+            pc.grow = 0;
+        } else {
+            bool all_big = have;
+            for (uint32_t d : moving) all_big = all_big && !h->bslot_h.empty() && h->bslot_h[d] >= 0;
+            if (!(all_big && same(nc, h->big_caps))) rc = regrow(h, moving, nc);
+            pc.grow = same(doubled(nc), nc) ? 0 : 1;
+        }
+        if (rc) {
+            hipLaunchKernelGGL(k_fail_grow, dim3((n + 255) / 256), dim3(256), 0, h->stream, st);
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            return rc;
+        }
+        pc.tight = 0;
+        pc.stage = 3;
+        pc.narrow = 0;
+        rc = launch_paged(h, b, pc, 1, PagedSlice{0, 0, 0, 0, 0});
+        if (rc) return rc;
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        launched = pc;
+    }
+    h->err = "growth step: no progress after 32 rounds";
+    return MT_E_HIP;
+}
+
+// Waits for the stream, then runs the growth step of the last applied batch.
+static int mt_settle(mt_handle *h) {
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (!h->pending) return 0;
+    mt_batch *b = h->pending;
+    h->pending = nullptr;
+    const int rc = grow_loop(h, b);
+    b->owner = nullptr;
+    return rc;
+}
+
 void mt_batch_free(mt_batch *b) {
     if (!b) return;
+    if (b->owner && b->owner->pending == b) mt_settle(b->owner);   // its growth step still reads it
     hipSetDevice(b->device);
     if (b->off) hipFree(b->off);
     if (b->ops) hipFree(b->ops);
@@ -1714,8 +1982,8 @@ void mt_batch_free(mt_batch *b) {
 
 int mt_sync(mt_handle *h) {
     if (!h) return MT_E_INVALID;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const int rc = mt_settle(h);
+    if (rc) return rc;
     if (h->timed) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
@@ -1730,15 +1998,29 @@ float mt_last_kernel_ms(const mt_handle *h) { return h ? h->last_ms : 0.f; }
 int mt_last_hbm_docs(mt_handle *h, uint32_t *out) {
     if (!h || !out) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     HIPCHK(h, hipMemcpy(out, h->st.stats, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mt_last_grown(mt_handle *h, uint32_t *out) {
+    if (!h || !out) return MT_E_INVALID;
+    SETTLE(h);
+    uint32_t in_big = 0;
+    for (int32_t x : h->bslot_h) in_big += x >= 0;
+    out[0] = h->grown_last;
+    out[1] = h->grow_rounds_last;
+    out[2] = in_big;
+    out[3] = (uint32_t)h->big_caps.PP;
+    out[4] = (uint32_t)h->big_caps.UT;
+    out[5] = (uint32_t)h->big_caps.PH;
     return 0;
 }
 
 int mt_last_paged_peaks(mt_handle *h, uint32_t *out) {
     if (!h || !out) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     HIPCHK(h, hipMemcpy(out, h->st.stats + 8, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return 0;
 }
@@ -1952,6 +2234,7 @@ mt_snapshots *mt_snapshots_upload(mt_handle *h, const int64_t *doc_seg_off, cons
 
 int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
     if (!h || !s || s->doc_lo > h->n_docs || s->n_docs > h->n_docs - s->doc_lo) return MT_E_INVALID;
+    if (h->pending) SETTLE(h);
     HIPCHK(h, hipSetDevice(h->device));
     if (h->st.DL)
         HIPCHK(h, hipMemsetAsync(h->st.dlog + (size_t)s->doc_lo * h->st.DL, 0, (size_t)s->n_docs * h->st.DL * 4,
@@ -1991,7 +2274,7 @@ int mt_extract_snapshots(mt_handle *h, int64_t *io, mt_seg_rec *recs, uint16_t *
     if (!h || !io) return MT_E_INVALID;
     const uint32_t N = h->n_docs;
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     int64_t *d_io = nullptr;
     HIPCHK(h, hipMalloc(&d_io, (size_t)N * 3 * 8));
     const int mode = recs ? 1 : 0;
@@ -2073,6 +2356,7 @@ __global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, int64_t ops
 mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                       int32_t *view_len_trace) {
     if (!h || !cfg || cfg->writers < 1 || cfg->ops < 0) return nullptr;
+    if (h->pending && mt_settle(h) != 0) return nullptr;
     if (h->ordinals) {   // the generator's kernels keep no ordinals
         h->err = "mt_generate: not on a segment_ordinals handle";
         return nullptr;
@@ -2251,27 +2535,33 @@ struct HostDoc {
     std::vector<uint16_t> text;
     std::vector<uint32_t> props;
 };
+// document doc's paged arrays, host side (the growth step's slot mirror)
+static PagedBase host_paged(const mt_handle *h, uint32_t doc) {
+    const int s = h->bslot_h.empty() ? -1 : h->bslot_h[doc];
+    return s >= 0 ? paged_base(h->st.big, (size_t)s) : paged_base(main_region(h->st), (size_t)doc);
+}
 static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bool with_props) {
     if (!h || doc >= h->n_docs) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     const DevState &st = h->st;
     HIPCHK(h, hipMemcpy(&hd.hdr, st.hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
     if (hd.hdr.pad[HDR_PAGED]) {
         // paged layout: concatenate the pages in directory order; leaf-block counts from
         // the page metadata
-        const size_t PP = st.PP, slots = PP * MT_PG_SLOTS;
+        const PagedBase pb = host_paged(h, doc);
+        const size_t PP = pb.PP, slots = PP * MT_PG_SLOTS;
         const int np = hd.hdr.pad[HDR_NPAGES];
         std::vector<uint16_t> dir(std::max(np, 1));
         std::vector<PageMeta> meta(PP);
         std::vector<int4> pA(slots);
         std::vector<u64> pO(slots);
         std::vector<uint4> pB(slots);
-        HIPCHK(h, hipMemcpy(dir.data(), st.pgDir + doc * PP, np * sizeof(uint16_t), hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy(meta.data(), st.pgMeta + doc * PP, PP * sizeof(PageMeta), hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy(pA.data(), st.pgA + doc * slots, slots * sizeof(int4), hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy(pO.data(), st.pgO + doc * slots, slots * sizeof(u64), hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy(pB.data(), st.pgB + doc * slots, slots * sizeof(uint4), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(dir.data(), pb.dir, np * sizeof(uint16_t), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(meta.data(), pb.meta, PP * sizeof(PageMeta), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(pA.data(), pb.A, slots * sizeof(int4), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(pO.data(), pb.O, slots * sizeof(u64), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(pB.data(), pb.B, slots * sizeof(uint4), hipMemcpyDeviceToHost));
         hd.A.clear();
         hd.O.clear();
         hd.B.clear();
@@ -2322,7 +2612,7 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
 int mt_get_status(mt_handle *h, int32_t *out_status) {
     if (!h || !out_status) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     std::vector<DocHdr> hs(h->n_docs);
     HIPCHK(h, hipMemcpy(hs.data(), h->st.hdr, h->n_docs * sizeof(DocHdr), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < h->n_docs; i++) out_status[i] = hs[i].status;
@@ -2656,7 +2946,7 @@ int mt_get_delta_log(mt_handle *h, uint32_t doc, int32_t *out, uint32_t cap, uin
         return 0;
     }
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     DocHdr hdr;
     HIPCHK(h, hipMemcpy(&hdr, h->st.hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
     // only whole records are ever counted; clamp anyway (never read past this document)
@@ -2681,6 +2971,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_dlog_reset(DevState st) {
 
 int mt_delta_log_reset(mt_handle *h) {
     if (!h) return MT_E_INVALID;
+    if (h->pending) SETTLE(h);
     if (!h->st.DL) return 0;
     HIPCHK(h, hipSetDevice(h->device));
     hipLaunchKernelGGL(k_dlog_reset, dim3((h->n_docs + MT_WAVE - 1) / MT_WAVE), dim3(MT_WAVE), 0, h->stream, h->st);
@@ -2708,18 +2999,19 @@ int mt_debug_prof(mt_handle *h, uint64_t *out, int reset) {
 
 int mt_checksums_device(mt_handle *h, void *device_out) {
     if (!h || !device_out) return MT_E_INVALID;
+    if (h->pending) SETTLE(h);
     HIPCHK(h, hipSetDevice(h->device));
     hipLaunchKernelGGL(k_checksum, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st,
                        (mt_checksum *)device_out);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     return 0;
 }
 
 int mt_maintenance_counts(mt_handle *h, uint32_t *out) {
     if (!h || !out || !h->st.DL) return MT_E_INVALID;   // kept by delta-logging handles only
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     std::vector<DocHdr> hd(h->n_docs);
     HIPCHK(h, hipMemcpy(hd.data(), h->st.hdr, h->n_docs * sizeof(DocHdr), hipMemcpyDeviceToHost));
     for (uint32_t d = 0; d < h->n_docs; d++) {
@@ -2746,7 +3038,7 @@ int mt_regenerate_pending(mt_handle *h, uint32_t doc, mt_regen_rec *out, uint32_
         return MT_E_INVALID;
     }
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     mt_regen_rec *d_out = nullptr;
     uint16_t *d_text = nullptr;
     uint32_t *d_props = nullptr;
@@ -2787,7 +3079,7 @@ int mt_regenerate_pending(mt_handle *h, uint32_t doc, mt_regen_rec *out, uint32_
 int mt_pending_counts(mt_handle *h, int32_t *out) {
     if (!h || !h->live || !out) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    SETTLE(h);
     std::vector<int32_t> lv((size_t)h->n_docs * 4);
     HIPCHK(h, hipMemcpy(lv.data(), h->st.live, lv.size() * 4, hipMemcpyDeviceToHost));
     for (uint32_t d = 0; d < h->n_docs; d++) {

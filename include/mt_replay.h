@@ -36,8 +36,9 @@ extern "C" {
 typedef struct mt_handle mt_handle;
 typedef struct mt_batch mt_batch;
 
-/* Per-document capacities (0 = default).  Exceeding one marks that document
-   MT_DOC_CAPACITY; the host may re-run it with larger capacities. */
+/* Per-document capacities (0 = default).  The paged ones (page / unsettled / page heap) are
+   starting points that the growth step raises per document (mt_last_grown); exceeding any
+   other marks that document MT_DOC_CAPACITY. */
 typedef struct mt_options {
     int32_t device;          /* HIP device ordinal (one process per GPU) */
     int32_t seg_capacity;    /* leaf segments per document          (default 2048) */
@@ -203,6 +204,16 @@ int mt_last_hbm_docs(mt_handle *h, uint32_t *out);
    out[5] = {pages, unsettled-table entries, zamboni heap entries, segments, documents handed
    from the tight to the full-capacity paged tier}; sizing aid for the paged capacities. */
 int mt_last_paged_peaks(mt_handle *h, uint32_t *out);
+
+/* Growth step of the most recent batch (mt_sync runs it; see mt_options: the paged
+   capacities are where documents start, not a limit): out[6] = {documents handed to it,
+   rounds, documents now in the big region, its page / unsettled-table / heap capacities
+   (0 if none)}.  A document whose next message could outgrow the last paged tier moves, with
+   its state, into a region with those capacities doubled (up to the 160 KiB of LDS one paged
+   launch may stage) and continues there; only beyond that does it fail with
+   MT_DOC_CAPACITY.  A batch applied with mt_batch_apply_async must stay allocated until
+   mt_sync (mt_batch_free of a pending batch finishes the step first). */
+int mt_last_grown(mt_handle *h, uint32_t *out);
 
 /* Generates ops_per_doc synthetic messages per document on the device, applying them as
    it goes (the generator reads each writer's view length from the live replica), and

@@ -43,6 +43,9 @@ TIERS = {
     "narrow": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
                    lds_page_capacity=200, lds_unsettled_capacity=600, lds_page_heap_capacity=600,
                    lds_narrow_overlap=1),
+    # HBM paged capacities far below the documents' needs: the growth step moves documents
+    # to larger regions, round after round, mid-batch (mt_last_grown)
+    "grow": dict(lds_seg_capacity=16, page_capacity=12, unsettled_capacity=16, page_heap_capacity=16),
 }
 
 
@@ -64,8 +67,40 @@ def test_gpu_matches_reference(name, tier):
     paged = [mt.is_paged(i) for i in range(len(fx["docs"]))]
     if tier == "paged":
         assert all(paged)
-    elif "paged" not in tier and tier not in ("tight", "narrow"):
+    elif "paged" not in tier and tier not in ("tight", "narrow", "grow"):
         assert not any(paged)
+
+
+@pytest.mark.parametrize("name", ["ref_c3_full", "ref_c4_full", "ref_c3_long"])
+def test_gpu_growth_past_the_handle_sizing(name):
+    """Documents far larger than the handle's paged capacities (12 pages, 16 table / heap
+    entries; the 10k-op C3 / C4 documents need ~200 pages, ~200-1800 entries) are moved to
+    larger HBM regions by the growth step, several times, mid-batch; they end equal to the
+    reference -- text, tree, segments, properties, every delta record -- and so does a second
+    batch on the same handle."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 20, **TIERS["grow"])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    half = np.asarray([lo + (hi - lo) // 2 for lo, hi in zip(a["doc_off"][:-1], a["doc_off"][1:])])
+    sel1 = np.concatenate([np.arange(lo, m) for lo, m in zip(a["doc_off"][:-1], half)])
+    sel2 = np.concatenate([np.arange(m, hi) for m, hi in zip(half, a["doc_off"][1:])])
+    off1 = np.concatenate([[0], np.cumsum(half - a["doc_off"][:-1])]).astype(np.int64)
+    off2 = np.concatenate([[0], np.cumsum(a["doc_off"][1:] - half)]).astype(np.int64)
+    mt.apply_arrays(dict(a, ops=a["ops"][sel1], doc_off=off1))
+    g1 = mt.last_grown()
+    assert g1["grown"] >= len(fx["docs"]) and g1["rounds"] >= 2, g1
+    mt.apply_arrays(dict(a, ops=a["ops"][sel2], doc_off=off2))
+    g2 = mt.last_grown()
+    assert g2["in_big_region"] == len(fx["docs"]), g2
+    assert (mt.status() == 0).all()
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, f"{name}: {bad[:4]}"
 
 
 @pytest.mark.parametrize("tier", ["lds", "paged"])
@@ -386,13 +421,14 @@ def test_gpu_error_model_matches_reference(tier):
 
 
 def test_gpu_capacity_status_isolates_the_document():
-    """A document that outgrows a per-document capacity stops with MT_DOC_CAPACITY; the other
-    documents of the batch still equal the reference."""
+    """A document that outgrows a capacity the growth step does not raise (here the text arena:
+    ~2.9k-unit documents, 1024 units per half) stops with MT_DOC_CAPACITY; the other documents
+    of the batch still equal the reference."""
     small, big = gu.load("ref_small"), gu.load("ref_c3")
     interner = gu.interner_for(small)
     docs = small["docs"][:6] + big["docs"][:2]
     a = gu.encode_docs(small, interner, docs)
-    mt = _gpu_batch(len(docs), lds_seg_capacity=-1, page_capacity=16, unsettled_capacity=1024)
+    mt = _gpu_batch(len(docs), lds_seg_capacity=-1, page_capacity=16, unsettled_capacity=1024, text_capacity=1024)
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     st = mt.status()
