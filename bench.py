@@ -288,6 +288,16 @@ def c5_end_to_end(mt, counts, recs, text, props, mn, cu, chunk, tail_arr, tail, 
         off.append(len(paths))
     nbytes = sum(len(b) for b in blobs)
     src = np.arange(n) % n_emit
+    # a tail writer the summary does not name gets the next short id (first seen in the tail)
+    t_emit = tail_arr["ops"].reshape(-1, tail)[:n_emit]
+    for d in range(n_emit):
+        nxt = len(cl[d]) + 1
+        named = {int(k[len("client-"):]) for k in cl[d]}
+        for k in t_emit[d]["client"].tolist():
+            if k <= 4096 and k not in named:
+                named.add(k)
+                remap[d, k] = nxt
+                nxt += 1
     ops = tail_arr["ops"].reshape(-1, tail)[src].copy()
     c = ops["client"].astype(np.int64)
     ops["client"] = np.where(c <= 4096, remap[src[:, None], np.minimum(c, 4096)], c)

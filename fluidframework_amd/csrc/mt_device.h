@@ -176,10 +176,17 @@ __host__ __device__ inline PagedRegion main_region(const DevState &st) {
     return PagedRegion{st.pgA, st.pgO, st.pgB, st.pgMeta, st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA,
                        st.pgUtO, st.PP, st.PH, st.UT, st.n_docs};
 }
-// the paged arrays of document doc (device side: its slot from st.bslot)
+// the paged arrays of document doc (device side: its slot from st.bslot; readers outside the
+// replay kernels, which are instantiated per region)
 __device__ inline PagedBase doc_paged(const DevState &st, int doc) {
     const int s = st.bslot ? st.bslot[doc] : -1;
     return s >= 0 ? paged_base(st.big, (size_t)s) : paged_base(main_region(st), (size_t)doc);
+}
+template <bool kBig> __device__ __forceinline__ PagedBase tier_paged(const DevState &st, int doc) {
+    if constexpr (kBig)
+        return paged_base(st.big, (size_t)st.bslot[doc]);
+    else
+        return paged_base(main_region(st), (size_t)doc);
 }
 
 // ------------------------------------------------------------------ wave primitives

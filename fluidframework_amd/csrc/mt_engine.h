@@ -71,7 +71,11 @@ template <bool kLogT> struct TierLiveT {
 // of short ids 1..32 in LDS (window and unsettled table: 4 bytes per segment instead of 8) --
 // a tight tier for documents with few writers; one whose clients above 32 remove overlapping
 // ranges continues in the full tier.
-template <bool kLogT, bool kNarrowT = false> struct TierPagedT {
+// kBigT: the instantiation the growth step launches for documents in the big region (their
+// paged arrays at DevState.big[bslot[doc]], mt_replay.hip "growth step"); every other
+// launch reads the main arrays and never sees such a document.
+template <bool kLogT, bool kNarrowT = false, bool kBigT = false> struct TierPagedT {
+    static constexpr bool kBig = kBigT;
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;

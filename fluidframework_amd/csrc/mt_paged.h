@@ -75,11 +75,6 @@ struct PagedCaps {
                  // outgrow these capacities, is handed to the host's growth step (retry = 3)
                  // instead of failing -- re-tiered to a larger HBM region, it continues there
 };
-// what a hand-over ran out of (PagedCaps.grow: the capacities the growth step doubles)
-#define PG_NEED_TABLE 1
-#define PG_NEED_HEAP 2
-#define PG_NEED_PAGES 4
-#define PG_NEED_NARROW 8
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
 
@@ -943,36 +938,22 @@ TD void pg_renumber(PagedDoc<T> &pd) {
 // marked); the heap by <= 1 / <= 1 + (pos2 - pos1) (one entry per touched leaf block); a
 // message splits or repacks a few pages (8 kept in reserve).  pd.wgrow bounds what the
 // window added since its table entries were last rebuilt.
-// Returns 0 (room: the message is applied) or the PG_NEED_* capacities it could outgrow.
-TD int pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
+TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const bool range = op.kind == MT_OP_REMOVE || op.kind == MT_OP_ANNOTATE;
     const int span = range ? min(max(op.pos2 - op.pos1, 0), 1 << 20) : 0;
     const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
-    int need = 0;
     // a narrow tier holds overlap slots 1..32 only
-    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) need |= PG_NEED_NARROW;
-    if (pd.ut_n + pd.wgrow + ut_b > pd.UT) need |= PG_NEED_TABLE;
-    if (pd.w.heap_n + hp_b > pd.PH) need |= PG_NEED_HEAP;
-    if (nbr(pd.up, 1) + 8 > pd.PP) need |= PG_NEED_PAGES;
+    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
+    if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
+    if (pd.w.heap_n + hp_b > pd.PH) return false;
+    if (nbr(pd.up, 1) + 8 > pd.PP) return false;
     for (int l = 2; l < pd.up.depth; l++)
-        if (nbr(pd.up, l) + 4 > bcap(pd.up, l)) need |= PG_NEED_PAGES;
-    if (need) return need;
+        if (nbr(pd.up, l) + 4 > bcap(pd.up, l)) return false;
     pd.opbound = ut_b;
     pd.wgrow += ut_b;
-    return 0;
+    return true;
 }
-// pg_load's capacity checks as PG_NEED_* bits (0: it fits this launch)
-TD int pg_load_need(PagedDoc<T> &pd, const DevState &st) {
-    const DocHdr h = *pd.w.hp;
-    int need = 0;
-    if (h.n_blk[1] > pd.PP) need |= PG_NEED_PAGES;
-    if (h.pad[HDR_UTN] > pd.UT) need |= PG_NEED_TABLE;
-    if (h.heap_n > pd.PH) need |= PG_NEED_HEAP;
-    if (T::kOvlBits < 64 && pd.w.wide) need |= PG_NEED_NARROW;
-    return need ? need : PG_NEED_PAGES;   // otherwise a page id above this launch's capacity
-}
-
 // Client.applyMsg (MT/client.ts:797-819) for a paged document; mirrors apply_op.
 TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin);
 TD void pg_apply_op(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
@@ -1179,7 +1160,7 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
 // Per-document HBM bases of the paged arrays the op path uses (pages, uid map).
 // (the main arrays, or the document's slot in the big region after a growth step)
 TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
-    const PagedBase b = doc_paged(st, doc);
+    const PagedBase b = tier_paged<T::kBig>(st, doc);
     pd.gA = (GLB_AS v4i *)b.A;
     pd.gO = (GLB_AS u64 *)b.O;
     pd.gB = (GLB_AS v4u *)b.B;
@@ -1199,8 +1180,8 @@ struct PgCold {
     GLB_AS v4i *guA;
     GLB_AS u64 *guO;
 };
-__device__ __forceinline__ PgCold pg_cold(const DevState &st, int doc) {
-    const PagedBase b = doc_paged(st, doc);
+template <class T> __device__ __forceinline__ PgCold pg_cold(const DevState &st, int doc) {
+    const PagedBase b = tier_paged<T::kBig>(st, doc);
     PgCold c;
     c.gmeta = (GLB_AS PageMeta *)b.meta;
     c.gdir = (GLB_AS uint16_t *)b.dir;
@@ -1321,7 +1302,7 @@ TD void pg_mark_free(PagedDoc<T> &pd) {
 // Loads a paged document's directory, meta, upper counts, heap and table into LDS.  Returns
 // false (nothing staged) when the document does not fit this launch's LDS capacities.
 TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
-    const PgCold g = pg_cold(st, pd.doc);
+    const PgCold g = pg_cold<T>(st, pd.doc);
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     const DocHdr h = *w.hp;
@@ -1356,7 +1337,7 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
 }
 
 TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
-    const PgCold g = pg_cold(st, pd.doc);
+    const PgCold g = pg_cold<T>(st, pd.doc);
     DocT<T> &w = pd.w;
     DocT<T> &up = pd.up;
     // a document that failed keeps the state it had at the failure (the reference's state at

@@ -54,6 +54,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     oslot_reset(st, doc);
+    if (st.bslot && lane() == 0) st.bslot[doc] = -1;   // back to the main arrays
     const int64_t s0 = seed_off ? seed_off[doc] : 0, s1 = seed_off ? seed_off[doc + 1] : 0;
     const int len = (int)(s1 - s0);
     uint16_t *text = st.text + (size_t)doc * 2 * st.T;
@@ -98,6 +99,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
     const int r = blockIdx.x, doc = lo + r;
     if (doc >= st.n_docs) return;
     oslot_reset(st, doc);
+    if (st.bslot && lane() == 0) st.bslot[doc] = -1;   // back to the main arrays
     const int n = nh[r];
     const mt_seg_rec *rs = segs + off[r];
     const bool big = sc.off && sc.off[2 * r] >= 0;
@@ -616,18 +618,13 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 // message resume[doc] -- when it does not fit its LDS capacities at load, or before a message
 // that could outgrow them (pg_room); stats[12] counts those hand-overs.
 // A last tier with PagedCaps.grow hands a document to the growth step the same way (retry[doc]
-// = 3; stats[13] counts them, stats[14] ORs the PG_NEED_* capacities they ran out of).
+// = 3, stats[13] counts them).
 template <class T>
-__device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t k, const PagedCaps &pc, int need) {
+__device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t k, const PagedCaps &pc) {
     if (lane() == 0) {
         st.retry[doc] = pc.tight ? 2 : 3;
         st.resume[doc] = k;
-        if (pc.tight) {
-            atomicAdd(st.stats + 12, 1u);
-        } else {
-            atomicAdd(st.stats + 13, 1u);
-            atomicOr(st.stats + 14, (uint32_t)need);
-        }
+        atomicAdd(st.stats + (pc.tight ? 12 : 13), 1u);
     }
 }
 // One launch of a sliced paged replay (mt_options.paged_slices): documents in [skip_lo,
@@ -664,7 +661,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     if (st.hdr[doc].pad[HDR_PAGED]) {
         if (!pg_load(pd, st)) {
             if (pc.tight || pc.grow) {
-                pg_handover<T>(st, doc, k0, pc, pg_load_need(pd, st));
+                pg_handover<T>(st, doc, k0, pc);
             } else if (lane() == 0) {   // cannot happen: the last tier has the document's capacities
                 st.hdr[doc].status = MT_DOC_CAPACITY;
                 st.retry[doc] = 0;
@@ -675,13 +672,9 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
         // stays flat (the pages written so far are unreferenced): the next tier converts it
         // again (the growth step: at larger page / heap / table capacities), or only the
         // status changes
-        const int cc = w.cap_cause;
-        const int need = cc == 7 ? PG_NEED_PAGES : (cc == 3 ? PG_NEED_HEAP : (cc == 8 ? PG_NEED_TABLE : 0));
-        if (pc.tight && w.status == MT_DOC_CAPACITY) {
-            pg_handover<T>(st, doc, k0, pc, need);
-        } else if (pc.grow && w.status == MT_DOC_CAPACITY && need) {
-            w.status = 0;   // the header is untouched: only the pages are rewritten there
-            pg_handover<T>(st, doc, k0, pc, need);
+        const int cc = w.cap_cause;   // pages 7, heap 3, table 8: capacities the growth step raises
+        if ((pc.tight || (pc.grow && (cc == 7 || cc == 3 || cc == 8))) && w.status == MT_DOC_CAPACITY) {
+            pg_handover<T>(st, doc, k0, pc);
         } else if (lane() == 0) {
             st.hdr[doc].status = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
             st.retry[doc] = 0;
@@ -693,7 +686,6 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
     int pk_ut = 0, pk_heap = 0;
     int64_t spill_at = -1;
-    int need = 0;
     for (int64_t kb = k0; kb < k1 && w.status == 0 && spill_at < 0; kb += MT_WAVE) {
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
@@ -739,12 +731,9 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
             in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
-            if (pc.tight || pc.grow) {
-                need = pg_room(pd, in.op);
-                if (need) {
-                    spill_at = kb + j;
-                    break;
-                }
+            if ((pc.tight || pc.grow) && !pg_room(pd, in.op)) {
+                spill_at = kb + j;
+                break;
             }
             pg_apply_op(pd, in, gt, gp);
             pk_ut = max(pk_ut, pd.ut_n);
@@ -756,7 +745,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     pg_store(pd, st);
     pg_peaks(st, pd, pk_ut, pk_heap);
     if (spill_at >= 0 && w.status == 0)
-        pg_handover<T>(st, doc, spill_at, pc, need);
+        pg_handover<T>(st, doc, spill_at, pc);
     else if (k1 < kend && w.status == 0) {   // slice done: the next launch of this stage resumes
         if (lane() == 0) st.resume[doc] = k1;
     } else if (lane() == 0)
@@ -816,7 +805,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
         }
         OpIn in;
         gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
-        if (pc.tight && pg_room(pd, in.op)) {
+        if (pc.tight && !pg_room(pd, in.op)) {
             if (lane() == 0) {
                 st.retry[doc] = 2;
                 atomicAdd(st.stats + 12, 1u);
@@ -1266,6 +1255,7 @@ struct mt_handle {
     struct mt_batch *pending = nullptr;
     PagedCaps big_caps{0, 0, 0, 0, 3, 0, 1};
     std::vector<int32_t> bslot_h;           // host mirror of st.bslot
+    uint32_t n_big = 0;                     // documents with a slot in the big region
     uint32_t grown_last = 0, grow_rounds_last = 0;
 };
 struct mt_batch {
@@ -1602,6 +1592,13 @@ int mt_reset(mt_handle *h) {
     if (!h) return MT_E_INVALID;
     if (h->pending) SETTLE(h);
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->n_big > 0) {   // every document starts over in the main arrays (k_init clears bslot)
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        free_region(h->st.big);
+        h->big_caps = PagedCaps{0, 0, 0, 0, 3, 0, 1};
+        h->bslot_h.assign(h->n_docs, -1);
+        h->n_big = 0;
+    }
     if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
     hipLaunchKernelGGL(k_init, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, h->d_seed_off, h->d_seed);
     HIPCHK(h, hipGetLastError());
@@ -1648,11 +1645,28 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
     return b;
 }
 
-// One paged launch over every document (those not at stage pc.stage exit at once).
-static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl) {
+// documents in the big region that this batch's LDS tier flagged (retry 1) skip the tight and
+// full launches: the growth step replays them at the big region's capacities (retry 3)
+__global__ void k_mark_big(DevState st, const int64_t *off, int resume_set) {
+    const int doc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (doc >= st.n_docs || st.bslot[doc] < 0 || st.retry[doc] != 1) return;
+    st.retry[doc] = 3;
+    if (!resume_set) st.resume[doc] = off[doc];
+    atomicAdd(st.stats + 13, 1u);
+}
+// One paged launch over every document (those not at stage pc.stage exit at once); big: the
+// documents of the big region (the growth step's launches).
+static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl,
+                        bool big = false) {
     const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8).total;
     const dim3 g(h->n_docs), blk(MT_WAVE);
-    if (h->st.DL && pc.narrow)
+    if (big && h->st.DL)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+                           b->off, b->text, b->props, res, pc, sl);
+    else if (big)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+                           b->off, b->text, b->props, res, pc, sl);
+    else if (h->st.DL && pc.narrow)
         hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
                            b->text, b->props, res, pc, sl);
     else if (h->st.DL)
@@ -1698,6 +1712,11 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         // documents that outgrew the LDS tier continue in the paged layout: the tight tier
         // first (when configured), then the full capacities for the documents it handed over
         const int use_resume = h->lds.S > 0 ? 1 : 0;
+        if (h->n_big > 0) {   // documents of the big region go straight to the growth step's launch
+            hipLaunchKernelGGL(k_mark_big, dim3((h->n_docs + 255) / 256), dim3(256), 0, h->stream, h->st, b->off,
+                               use_resume);
+            HIPCHK(h, hipGetLastError());
+        }
         const PagedCaps *tiers[2] = {h->pg_tight.PP ? &h->pg_tight : nullptr, &h->pg_full};
         const int n = (int)h->n_docs;
         for (const PagedCaps *pc : tiers) {
@@ -1731,7 +1750,7 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
                 res_k = 1;
             }
             for (const PagedSlice &sl : sls) {
-                const int rc = launch_paged(h, b, *pc, res_k, sl);
+                const int rc = launch_paged(h, b, *pc, res_k, sl, false);
                 if (rc) return rc;
             }
         }
@@ -1828,7 +1847,6 @@ static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c) {
     return ok;
 }
 
-static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl);
 
 // Moves the documents of `moving` (and every document already there) into a new big region at
 // capacities c; synchronous.
@@ -1872,10 +1890,12 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
     free_region(st.big);
     st.big = R;
     h->bslot_h = nb;
+    h->n_big = (uint32_t)slots;
     h->big_caps = PagedCaps{c.PP, c.PH, c.UT, 0, 3, 0, 1};
     const size_t lb = paged_layout(c.PP, c.PH, c.UT, 0, 8).total;
     if (lb > 64 * 1024) {
-        const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true>>, (const void *)k_replay_paged<TierPagedT<false>>};
+        const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true, false, true>>,
+                            (const void *)k_replay_paged<TierPagedT<false, false, true>>};
         for (const void *k : ks) HIPCHK(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
     }
     return 0;
@@ -1889,17 +1909,36 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
     h->grown_last = 0;
     h->grow_rounds_last = 0;
     PagedCaps launched = h->pg_full;   // the capacities of the launch that handed them over
+    bool launched_big = false;         // ... and whether it was the big region's launch
+    std::vector<int32_t> retry(n);
+    std::vector<DocHdr> hdr(n);
     for (int round = 0; round < 32; round++) {
-        uint32_t g[2] = {0, 0};
-        HIPCHK(h, hipMemcpy(g, st.stats + 13, sizeof(g), hipMemcpyDeviceToHost));
-        if (g[0] == 0) return 0;
+        uint32_t g = 0;
+        HIPCHK(h, hipMemcpy(&g, st.stats + 13, sizeof(g), hipMemcpyDeviceToHost));
+        if (g == 0) return 0;
         HIPCHK(h, hipMemset(st.stats + 13, 0, sizeof(g)));
-        std::vector<int32_t> retry(n);
         HIPCHK(h, hipMemcpy(retry.data(), st.retry, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(hdr.data(), st.hdr, (size_t)n * sizeof(DocHdr), hipMemcpyDeviceToHost));
         std::vector<uint32_t> moving;
-        for (uint32_t d = 0; d < n; d++)
-            if (retry[d] == 3) moving.push_back(d);
+        // what ran out, read from the handed-over documents' state: a capacity they fill to
+        // more than half is doubled (the kernel's bound is per message, pg_room); documents
+        // of the big region marked for this batch (k_mark_big) only need its capacities
+        bool t = false, hp = false, pg = false;
+        int judged = 0;
+        for (uint32_t d = 0; d < n; d++) {
+            if (retry[d] != 3) continue;
+            moving.push_back(d);
+            const bool in_big = !h->bslot_h.empty() && h->bslot_h[d] >= 0;
+            if (in_big && !launched_big) continue;
+            judged++;
+            const DocHdr &x = hdr[d];
+            const int np = x.pad[HDR_PAGED] ? x.pad[HDR_NPAGES] : (x.depth > 1 ? x.n_blk[1] : 1);
+            t = t || 2 * x.pad[HDR_UTN] > launched.UT;
+            hp = hp || 2 * x.heap_n > launched.PH;
+            pg = pg || 2 * (np + 8) > launched.PP;
+        }
         if (moving.empty()) return 0;
+        if (!t && !hp && !pg) t = hp = true;   // a single message's bound (a long range): its table / heap terms
         h->grown_last += (uint32_t)moving.size();
         h->grow_rounds_last++;
         // the new capacities: doubled where the documents ran out, never below the big
@@ -1908,18 +1947,18 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
         auto fits = [](const PagedCaps &c) { return paged_layout(c.PP, c.PH, c.UT, 0, 8).total <= 160 * 1024; };
         auto same = [](const PagedCaps &a, const PagedCaps &b) { return a.PP == b.PP && a.PH == b.PH && a.UT == b.UT; };
         auto doubled = [&](const PagedCaps &c) {   // c doubled where needed, one capacity at a time while it fits
-            PagedCaps r = c, t = c;
-            if (g[1] & PG_NEED_TABLE) t.UT = std::min(2 * t.UT, 1 << 20);
-            if (fits(t)) r = t;
-            t = r;
-            if (g[1] & PG_NEED_HEAP) t.PH = std::min(2 * t.PH, 1 << 20);
-            if (fits(t)) r = t;
-            t = r;
-            if (g[1] & PG_NEED_PAGES) t.PP = std::min(2 * t.PP, 65535);
-            if (fits(t)) r = t;
+            PagedCaps r = c, x = c;
+            if (t) x.UT = std::min(2 * x.UT, 1 << 20);
+            if (fits(x)) r = x;
+            x = r;
+            if (hp) x.PH = std::min(2 * x.PH, 1 << 20);
+            if (fits(x)) r = x;
+            x = r;
+            if (pg) x.PP = std::min(2 * x.PP, 65535);
+            if (fits(x)) r = x;
             return r;
         };
-        PagedCaps nc = doubled(launched);
+        PagedCaps nc = judged ? doubled(launched) : h->big_caps;   // (judged == 0: only marked documents)
         if (have) {
             nc.PP = std::max(nc.PP, h->big_caps.PP);
             nc.PH = std::max(nc.PH, h->big_caps.PH);
@@ -1927,13 +1966,14 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
         }
         int rc = 0;
         PagedCaps pc = nc;
-        pc.grow = 0;
+        bool big = true;
         if (same(nc, launched)) {
             // nothing can grow: the documents run to their end at the capacities they were
             // handed over at (in their own region) and fail as before the step existed only
             // if they do outgrow them
             pc = launched;
             pc.grow = 0;
+            big = launched_big;
         } else {
             bool all_big = have;
             for (uint32_t d : moving) all_big = all_big && !h->bslot_h.empty() && h->bslot_h[d] >= 0;
@@ -1948,10 +1988,11 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
         pc.tight = 0;
         pc.stage = 3;
         pc.narrow = 0;
-        rc = launch_paged(h, b, pc, 1, PagedSlice{0, 0, 0, 0, 0});
+        rc = launch_paged(h, b, pc, 1, PagedSlice{0, 0, 0, 0, 0}, big);
         if (rc) return rc;
         HIPCHK(h, hipStreamSynchronize(h->stream));
         launched = pc;
+        launched_big = big;
     }
     h->err = "growth step: no progress after 32 rounds";
     return MT_E_HIP;
@@ -2236,6 +2277,12 @@ int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
     if (!h || !s || s->doc_lo > h->n_docs || s->n_docs > h->n_docs - s->doc_lo) return MT_E_INVALID;
     if (h->pending) SETTLE(h);
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->n_big > 0) {   // loaded documents start over in the main arrays (k_load_header clears bslot)
+        for (uint32_t d = s->doc_lo; d < s->doc_lo + s->n_docs; d++) {
+            h->n_big -= h->bslot_h[d] >= 0;
+            h->bslot_h[d] = -1;
+        }
+    }
     if (h->st.DL)
         HIPCHK(h, hipMemsetAsync(h->st.dlog + (size_t)s->doc_lo * h->st.DL, 0, (size_t)s->n_docs * h->st.DL * 4,
                                  h->stream));
