@@ -176,8 +176,9 @@ def capacities(cfg, tight=True):
                     uid_capacity=1 << 16)
         if tight and deep and cfg["ops"] <= 10000 and cfg["writers"] <= 64:
             # C4 peaks over 4096 documents: 208 pages, 1810 table entries, 841 heap entries;
-            # 99 KB per document at the full capacities (1 per CU) vs 70.6 KB here (2 per CU)
-            caps.update(lds_page_capacity=256, lds_unsettled_capacity=2048, lds_page_heap_capacity=1024)
+            # 99 KB per document at the full capacities (1 per CU); the tight tier packs its
+            # table (12-byte entries: every client id fits 8 bits): 52.8 KB here, 3 per CU
+            caps.update(lds_page_capacity=224, lds_unsettled_capacity=1900, lds_page_heap_capacity=900)
         if tight and not deep and cfg["ops"] <= 10000:
             # the paged layout's LDS footprint sets documents per CU: 27 KB at the full
             # capacities (6 per CU), 14.9 KB here (11 per CU; the kernel is compiled for 3

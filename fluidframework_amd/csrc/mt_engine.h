@@ -74,8 +74,11 @@ template <bool kLogT> struct TierLiveT {
 // kBigT: the instantiation the growth step launches for documents in the big region (their
 // paged arrays at DevState.big[bslot[doc]], mt_replay.hip "growth step"); every other
 // launch reads the main arrays and never sees such a document.
-template <bool kLogT, bool kNarrowT = false, bool kBigT = false> struct TierPagedT {
+// kPackedT: 12-byte unsettled-table entries in LDS (mt_paged.h "packed table"; a tight tier
+// whose table dominates its LDS footprint, e.g. C4: 64 writers, minSeq ~1k messages behind).
+template <bool kLogT, bool kNarrowT = false, bool kBigT = false, bool kPackedT = false> struct TierPagedT {
     static constexpr bool kBig = kBigT;
+    static constexpr bool kPacked = kPackedT;
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;

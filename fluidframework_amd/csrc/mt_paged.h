@@ -41,6 +41,8 @@ template <class T> struct PagedDoc {
     LDS_AS uint16_t *upage;   // [UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
     LDS_AS v4i *uA;
     LDS_AS typename T::O_v *uO;
+    LDS_AS uint32_t *uL, *uS, *uP;   // T::kPacked: len | seq, rseq (16 bits each, from sbase) |
+    int sbase;                       // page, cli, rcli (16 / 8 / 8 bits) -- tab_get / tab_put
     GLB_AS v4i *gA;           // this document's pages (slot 0 of page 0)
     GLB_AS u64 *gO;
     GLB_AS v4u *gB;
@@ -74,6 +76,7 @@ struct PagedCaps {
     int grow;    // last tier: a document that does not fit at load, or whose next message could
                  // outgrow these capacities, is handed to the host's growth step (retry = 3)
                  // instead of failing -- re-tiered to a larger HBM region, it continues there
+    int packed;  // TierPagedT<., ., ., true>: 12-byte unsettled-table entries (tight tier only)
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
@@ -84,17 +87,19 @@ struct PagedLayout {
         total;
 };
 // ob: bytes per overlap mask in LDS (8, or 4 for a narrow tier)
-static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words, int ob) {
+// packed: the table's entries are 12 bytes (three u32 arrays at offUA) and carry their page
+static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words, int ob,
+                                                           bool packed = false) {
     PagedLayout L;
     uint32_t o = 0;
     L.offWA = o; o += 16u * MT_PG_SLOTS;
     L.offWB = o; o += 16u * MT_PG_SLOTS;
     L.offWO = o; o += (uint32_t)ob * MT_PG_SLOTS;
-    L.offUA = o; o += 16u * UT;
+    L.offUA = o; o += (packed ? 12u : 16u) * UT;
     L.offUO = o; o += (((uint32_t)ob * UT) + 7u) & ~7u;
     L.offHeap = o; o += 8u * (PH + 1);
     L.offMeta = o; o += (uint32_t)sizeof(PageMeta) * PP;
-    L.offUpage = o; o += (2u * UT + 3u) & ~3u;
+    L.offUpage = o; o += packed ? 0u : (2u * UT + 3u) & ~3u;
     L.offPvl = o; o += 4u * PP;
     L.offWscr = o; o += 64u * 4;
     L.offWnb = o; o += MT_LV * 4;
@@ -231,6 +236,42 @@ TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const 
     wsync<T>();
 }
 
+// ------------------------------------------------------------------ table entries
+// Packed table (T::kPacked): seq / removedSeq as 16-bit offsets from sbase = the document's
+// currentSeq at load - 32000 (0xFFFF: not removed).  A value below sbase is stored as sbase:
+// the tier only takes documents whose collab window is under 30000 messages (pg_load), so
+// such a segment's value is below minSeq and compares the same way in every view (refSeq >=
+// minSeq) and in unsettled(); messages more than 65000 above sbase go to the next tier
+// (pg_room).  Short client ids are 8-bit signed (the host packs only when every id of the
+// handle fits).
+__device__ __forceinline__ uint32_t sq_enc(int v, int sbase) {
+    return v == MT_RSEQ_NONE ? 0xFFFFu : (uint32_t)min(max(v - sbase, 0), 0xFFFE);
+}
+__device__ __forceinline__ int sq_dec(uint32_t v, int sbase) { return v == 0xFFFFu ? MT_RSEQ_NONE : (int)v + sbase; }
+TD void tab_get(PagedDoc<T> &pd, int e, int &pg, v4i &a, u64 &o) {
+    if constexpr (T::kPacked) {
+        const uint32_t l = pd.uL[e], sq = pd.uS[e], pc = pd.uP[e];
+        pg = (int)(pc & 0xFFFFu);
+        a = v4i{(int)l, sq_dec(sq & 0xFFFFu, pd.sbase), sq_dec(sq >> 16, pd.sbase),
+                pack_cli((int)(int8_t)(pc >> 16), (int)(int8_t)(pc >> 24))};
+    } else {
+        pg = pd.upage[e];
+        a = pd.uA[e];
+    }
+    o = pd.uO[e];
+}
+TD void tab_put(PagedDoc<T> &pd, int e, int pg, const v4i &a, u64 o) {
+    if constexpr (T::kPacked) {
+        pd.uL[e] = (uint32_t)a.x;
+        pd.uS[e] = sq_enc(a.y, pd.sbase) | (sq_enc(a.z, pd.sbase) << 16);
+        pd.uP[e] = (uint32_t)(pg & 0xFFFF) | ((uint32_t)(seg_cli(a) & 0xFF) << 16) | ((uint32_t)(seg_rcli(a) & 0xFF) << 24);
+    } else {
+        pd.upage[e] = (uint16_t)pg;
+        pd.uA[e] = a;
+    }
+    pd.uO[e] = (typename T::O_v)o;
+}
+
 // Removes the table entries of page pg (and every settled entry), then appends the
 // unsettled segments of window slots [lo, hi) under page pg2.
 TD void pg_table_purge(PagedDoc<T> &pd, int pg) {
@@ -242,20 +283,12 @@ TD void pg_table_purge(PagedDoc<T> &pd, int pg) {
         int p = -1;
         v4i a = v4i{0, 0, MT_RSEQ_NONE, 0};
         u64 o = 0;
-        if (v) {
-            p = pd.upage[e];
-            a = pd.uA[e];
-            o = pd.uO[e];
-        }
+        if (v) tab_get(pd, e, p, a, o);
         const bool keep = v && p != pg && unsettled<T>(a, ms);
         const u64 km = ballot(keep);
         const int at = dst + __popcll(km & ((1ull << lane()) - 1ull));
         wsync<T>();
-        if (keep) {
-            pd.upage[at] = p;
-            pd.uA[at] = a;
-            pd.uO[at] = o;
-        }
+        if (keep) tab_put(pd, at, p, a, o);
         wsync<T>();
         dst += __popcll(km);
     }
@@ -275,11 +308,7 @@ TD void pg_table_add(PagedDoc<T> &pd, int lo, int hi, int pg2) {
         return;
     }
     const int at = pd.ut_n + __popcll(m & ((1ull << lane()) - 1ull));
-    if (add) {
-        pd.upage[at] = pg2;
-        pd.uA[at] = a;
-        pd.uO[at] = o;
-    }
+    if (add) tab_put(pd, at, pg2, a, o);
     pd.ut_n += __popcll(m);
     wsync<T>();
 }
@@ -484,9 +513,11 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
     for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
         const int e = base + lane();
         if (e < pd.ut_n) {
-            const int pg = pd.upage[e];
-            const v4i a = pd.uA[e];
-            const int dlt = view_len(a, pd.uO[e], r, c, pd.w.ocs) - obs_len(a);
+            int pg;
+            v4i a;
+            u64 o;
+            tab_get(pd, e, pg, a, o);
+            const int dlt = view_len(a, o, r, c, pd.w.ocs) - obs_len(a);
             if (dlt && pg != cur) atomicAdd((int *)(pd.pvl + pg), dlt);
         }
     }
@@ -665,12 +696,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
             pg_fail_cap(w, 8);
             return;
         }
-        if (add) {
-            const int at = pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull));
-            pd.upage[at] = npg;
-            pd.uA[at] = a;
-            pd.uO[at] = o;
-        }
+        if (add) tab_put(pd, pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull)), npg, a, o);
         pd.ut_n += __popcll(am);
         const int obs = wave_sum(ol);
         // meta of the new page: blocks blo..bhi of the concatenation
@@ -945,6 +971,7 @@ TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
     // a narrow tier holds overlap slots 1..32 only
     if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
+    if (T::kPacked && op.seq - pd.sbase > 65000) return false;   // the packed table's seq offsets
     if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
     if (pd.w.heap_n + hp_b > pd.PH) return false;
     if (nbr(pd.up, 1) + 8 > pd.PP) return false;
@@ -1270,6 +1297,12 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.upage = (LDS_AS uint16_t *)(smem + L.offUpage);
     pd.uA = (LDS_AS v4i *)(smem + L.offUA);
     pd.uO = (LDS_AS typename T::O_v *)(smem + L.offUO);
+    if constexpr (T::kPacked) {
+        pd.uL = (LDS_AS uint32_t *)(smem + L.offUA);
+        pd.uS = pd.uL + pc.UT;
+        pd.uP = pd.uS + pc.UT;
+        pd.sbase = h.cur_seq - 32000;
+    }
     pd.cur = -1;
     pd.cur_pos = -1;
     pd.dirty = 0;
@@ -1309,6 +1342,7 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     const int np = h.n_blk[1];
     if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
     if (T::kOvlBits < 64 && w.wide) return false;
+    if (T::kPacked && w.cur_seq - w.min_seq > 30000) return false;   // the packed table's seq offsets
     int mx = 0;
     for (int q = lane(); q < np; q += MT_WAVE) mx = max(mx, (int)g.gdir[q]);
     if (wave_max(mx) >= pd.PP) return false;   // a page id allocated by a wider launch
@@ -1327,9 +1361,10 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = g.gheap[i];
     pd.ut_n = h.pad[HDR_UTN];
     for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
-        pd.upage[e] = (uint16_t)g.gupage[e];
-        pd.uA[e] = g.guA[e];
-        pd.uO[e] = g.guO[e];
+        const int p = g.gupage[e];
+        const v4i a = g.guA[e];
+        const u64 o = g.guO[e];
+        tab_put(pd, e, p, a, o);
     }
     wsync<T>();
     pg_mark_free(pd);
@@ -1361,9 +1396,13 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) g.gheap[i] = w.heap[i];
     for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
-        g.gupage[e] = pd.upage[e];
-        g.guA[e] = pd.uA[e];
-        g.guO[e] = pd.uO[e];
+        int p;
+        v4i a;
+        u64 o;
+        tab_get(pd, e, p, a, o);
+        g.gupage[e] = p;
+        g.guA[e] = a;
+        g.guO[e] = o;
     }
     int nbl[MT_LV];
 #pragma unroll

@@ -647,7 +647,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     if (doc >= sl.skip_lo && doc < sl.skip_hi) return;
     if (st.retry[doc] != pc.stage) return;
     if (lane() == 0 && doc >= sl.cnt_lo && doc < sl.cnt_hi) atomicAdd(st.stats, 1u);
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v));
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v), T::kPacked);
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
     const int64_t kend = off[doc + 1];
     const int64_t k1 = sl.ops > 0 ? min(kend, k0 + sl.ops) : kend;   // this launch's last message + 1
@@ -1256,6 +1256,8 @@ struct mt_handle {
     PagedCaps big_caps{0, 0, 0, 0, 3, 0, 1};
     std::vector<int32_t> bslot_h;           // host mirror of st.bslot
     uint32_t n_big = 0;                     // documents with a slot in the big region
+    int max_cli = 0;                        // largest |short client id| any batch / load / generation used
+                                            // (<= 127: the tight tier may pack its table, PagedCaps.packed)
     uint32_t grown_last = 0, grow_rounds_last = 0;
 };
 struct mt_batch {
@@ -1408,7 +1410,9 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
                                 (const void *)k_replay_paged<TierPagedT<true, true>>,
                                 (const void *)k_replay_paged<TierPagedT<false, true>>,
                                 (const void *)k_generate_paged<TierPagedT<false, true>>,
-                                (const void *)k_load_convert<TierPagedT<false>>};
+                                (const void *)k_load_convert<TierPagedT<false>>,
+                                (const void *)k_replay_paged<TierPagedT<true, false, false, true>>,
+                                (const void *)k_replay_paged<TierPagedT<false, false, false, true>>};
             for (const void *k : ks)
                 if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess) {
                     delete h;
@@ -1620,6 +1624,7 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
         h->err = "mt_batch_upload: " + bad;
         return nullptr;
     }
+    for (uint64_t i = 0; i < n_ops; i++) h->max_cli = std::max(h->max_cli, std::abs((int)(int16_t)ops[i].client));
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *b = new mt_batch();
     b->device = h->device;
@@ -1658,9 +1663,15 @@ __global__ void k_mark_big(DevState st, const int64_t *off, int resume_set) {
 // documents of the big region (the growth step's launches).
 static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl,
                         bool big = false) {
-    const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8).total;
+    const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8, pc.packed != 0).total;
     const dim3 g(h->n_docs), blk(MT_WAVE);
-    if (big && h->st.DL)
+    if (pc.packed && h->st.DL)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+                           b->off, b->text, b->props, res, pc, sl);
+    else if (pc.packed)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, false, false, true>>), g, blk, lb, h->stream, h->st,
+                           b->ops, b->off, b->text, b->props, res, pc, sl);
+    else if (big && h->st.DL)
         hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
     else if (big)
@@ -1749,8 +1760,10 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
                                          h->stream));
                 res_k = 1;
             }
+            PagedCaps pcx = *pc;   // a wide tight tier packs its table when every client id fits 8 bits
+            pcx.packed = pc->tight && !pc->narrow && h->max_cli <= 127 ? 1 : 0;
             for (const PagedSlice &sl : sls) {
-                const int rc = launch_paged(h, b, *pc, res_k, sl, false);
+                const int rc = launch_paged(h, b, pcx, res_k, sl, false);
                 if (rc) return rc;
             }
         }
@@ -2123,6 +2136,7 @@ mt_snapshots *mt_snapshots_upload_range(mt_handle *h, uint32_t doc_lo, uint32_t 
         }
     for (uint64_t i = 0; i < (uint64_t)doc_seg_off[N]; i++) {
         const mt_seg_rec &r = segs[i];
+        h->max_cli = std::max({h->max_cli, std::abs((int)r.client), std::abs((int)r.removed_client)});
         const bool marker = (r.flags & MT_F_MARKER) != 0;
         if (r.len < 0 || (!marker && (uint64_t)r.payload + (uint64_t)r.len > text_len) ||
             !props_rec_ok(props, props_len, r.props)) {
@@ -2404,6 +2418,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
                       int32_t *view_len_trace) {
     if (!h || !cfg || cfg->writers < 1 || cfg->ops < 0) return nullptr;
     if (h->pending && mt_settle(h) != 0) return nullptr;
+    h->max_cli = std::max(h->max_cli, cfg->writers);
     if (h->ordinals) {   // the generator's kernels keep no ordinals
         h->err = "mt_generate: not on a segment_ordinals handle";
         return nullptr;

@@ -91,8 +91,10 @@ class SummaryDecoder:
             off.append(len(paths))
         return paths, blobs, off
 
-    def decode_packed(self, paths, blobs, off):
-        """mt_snapdec_decode + fetch: the arrays with the decoder's own property ids."""
+    def decode_packed(self, paths, blobs, off, alloc=None):
+        """mt_snapdec_decode + fetch: the arrays with the decoder's own property ids.  alloc(n,
+        dtype) -> array supplies the three arenas (segs, text, props), e.g. page-locked memory
+        for a fast upload; numpy's allocator otherwise."""
         n = len(off) - 1
         nb = len(paths)
         offa = np.asarray(off, dtype=np.int64)
@@ -106,8 +108,13 @@ class SummaryDecoder:
         ns, nt, npr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self.lib.mt_snapdec_sizes(self.h, ctypes.byref(ns), ctypes.byref(nt), ctypes.byref(npr))
         def arena(m, dt):   # filled whole by fetch; an empty arena is one zero
+            if alloc is not None:
+                a = alloc(max(m, 1), dt)
+                if not m:
+                    a[:] = 0
+                return a
             return np.empty(m, dtype=dt) if m else np.zeros(1, dtype=dt)
-        out = dict(segs=np.empty(ns.value, dtype=SEG_DTYPE), doc_off=np.zeros(n + 1, dtype=np.int64),
+        out = dict(segs=arena(ns.value, SEG_DTYPE)[:ns.value], doc_off=np.zeros(n + 1, dtype=np.int64),
                    n_header=np.zeros(n, dtype=np.int32), text=arena(nt.value, np.uint16),
                    props=arena(npr.value, np.uint32), min_seq=np.zeros(n, dtype=np.int32),
                    cur_seq=np.zeros(n, dtype=np.int32))
@@ -145,9 +152,9 @@ class SummaryDecoder:
     def decode(self, summaries):
         return self.decode_packed_full(*self.pack(summaries))
 
-    def decode_packed_full(self, paths, blobs, off):
+    def decode_packed_full(self, paths, blobs, off, alloc=None):
         """decode() of already packed blob tables (pack())."""
-        out, cu = self.decode_packed(paths, blobs, off)
+        out, cu = self.decode_packed(paths, blobs, off, alloc)
         if not self.interner.synthetic:
             self._remap(out)
         catchup = [None if c < 0 else blobs[c].decode("utf-8", errors="surrogatepass") for c in cu]
