@@ -187,7 +187,8 @@ class MergeTreeBatch:
 
         t = threading.Thread(target=produce, daemon=True)
         t.start()
-        catchup_all, clients_all, held = [], [], []
+        from .snapdec import ClientMaps
+        catchup_all, clients_all, held = [], ClientMaps([]), []
         while True:
             item = q.get()
             if item is None:
@@ -200,8 +201,12 @@ class MergeTreeBatch:
             free_sets.put(pset)
             snaps.load_async()
             held.append(snaps)   # device copies stay alive until the loads have run
-            catchup_all += [_json.loads(c) if c is not None else [] for c in catchup]
-            clients_all += clients
+            cu_msgs = [[] for _ in catchup]
+            for i, c in enumerate(catchup):
+                if c is not None:
+                    cu_msgs[i] = _json.loads(c)
+            catchup_all += cu_msgs
+            clients_all = clients_all + clients
         t.join()
         self.sync()
         for s_ in held:

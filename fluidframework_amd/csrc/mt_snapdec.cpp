@@ -977,6 +977,19 @@ int64_t mt_snapdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint6
     if (!s || d >= s->n_docs) return -1;
     return copy_out(s->docs[d].clients, out, cap);
 }
+int64_t mt_snapdec_all_clients(const mt_snapdec *s, char *out, uint64_t cap) {
+    if (!s) return -1;
+    uint64_t n = 0;
+    for (uint32_t d = 0; d < s->n_docs; d++) {
+        const std::string &c = s->docs[d].clients;
+        if (out && n + c.size() + 1 <= cap) {
+            memcpy(out + n, c.data(), c.size());
+            out[n + c.size()] = '\n';
+        }
+        n += c.size() + 1;
+    }
+    return (int64_t)n;
+}
 uint32_t mt_snapdec_num_keys(const mt_snapdec *s) { return s ? (uint32_t)s->keys.size() : 0; }
 uint32_t mt_snapdec_num_values(const mt_snapdec *s) { return s ? (uint32_t)s->vals.size() : 0; }
 

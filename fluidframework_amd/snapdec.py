@@ -10,6 +10,7 @@ step).
 import ctypes
 import json
 import os
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -32,6 +33,7 @@ SIGNATURES = [
     ("mt_snapdec_num_keys", _U32, [_P]),
     ("mt_snapdec_num_values", _U32, [_P]),
     ("mt_snapdec_doc_clients", _I64, [_P, _U32, _P, _U64]),
+    ("mt_snapdec_all_clients", _I64, [_P, _P, _U64]),
 ]
 _lib = None
 
@@ -59,6 +61,28 @@ def _text(fn, h, i):
     buf = ctypes.create_string_buffer(max(n, 1))
     fn(h, i, buf, n)
     return buf.raw[:n].decode("utf-8", errors="surrogatepass")
+
+
+class ClientMaps(Sequence):
+    """Per document the short client id map to continue with ({long id: short id}), parsed
+    on access from the decoder's one-call dump (mt_snapdec_all_clients)."""
+
+    def __init__(self, lines):
+        self._lines = lines
+
+    def __len__(self):
+        return len(self._lines)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        return {c: k + 1 for k, c in enumerate(json.loads(self._lines[i]))}
+
+    def __add__(self, other):
+        return ClientMaps(self._lines + list(other._lines))
+
+    def __eq__(self, other):
+        return list(self) == list(other)
 
 
 class SummaryDecoder:
@@ -157,9 +181,11 @@ class SummaryDecoder:
         out, cu = self.decode_packed(paths, blobs, off, alloc)
         if not self.interner.synthetic:
             self._remap(out)
-        catchup = [None if c < 0 else blobs[c].decode("utf-8", errors="surrogatepass") for c in cu]
-        clients = []
-        for d in range(len(off) - 1):
-            names = json.loads(_text(self.lib.mt_snapdec_doc_clients, self.h, d))
-            clients.append({c: i + 1 for i, c in enumerate(names)})
-        return out, catchup, clients
+        catchup = [None] * len(cu)
+        for d in np.flatnonzero(cu >= 0).tolist():   # legacy summaries only
+            catchup[d] = blobs[cu[d]].decode("utf-8", errors="surrogatepass")
+        size = self.lib.mt_snapdec_all_clients(self.h, None, 0)
+        buf = ctypes.create_string_buffer(max(size, 1))
+        self.lib.mt_snapdec_all_clients(self.h, buf, size)
+        lines = buf.raw[:size].decode("utf-8", errors="surrogatepass").split("\n")[:-1] if size else []
+        return out, catchup, ClientMaps(lines)

@@ -54,6 +54,8 @@ uint32_t mt_snapdec_num_keys(const mt_snapdec *s);
 /* document d's writers as a JSON array of long client ids, short id 1..n in order
    (specToSegment's getOrAddShortClientId first-seen order; the catch-up ops continue it) */
 int64_t mt_snapdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint64_t cap);
+/* every document's array, in order, each followed by '\n' (one call for a whole batch) */
+int64_t mt_snapdec_all_clients(const mt_snapdec *s, char *out, uint64_t cap);
 uint32_t mt_snapdec_num_values(const mt_snapdec *s);
 
 #ifdef __cplusplus
