@@ -1149,6 +1149,34 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
     const int g = d.g_head;
     const int gw = lane() < MT_GRP_WORDS ? d.grp[g * MT_GRP_WORDS + lane()] : 0;   // the entry, lane j = word j
     const int ls = bcast(gw, 0), kind = bcast(gw, 1) & 0xFF;
+    {   // sizing pass (reads only): output buffers too small leave the document untouched --
+        // the caller retries with the sizes in io[1..3]
+        int need_n = 0, need_t = 0, need_p = 0;
+        for (int base = 0; base < d.n; base += MT_WAVE) {
+            const int i = base + lane();
+            const bool v = i < d.n;
+            v4i a;
+            u64 o;
+            load_ao(d, i, v, a, o);
+            const v4u b = d.Bv[v ? i : 0];
+            const bool mem = v && pq_first(pq_get(d, v ? i : 0)) == g;
+            const bool emit = mem && (kind != MT_OP_REMOVE || is_local_seq(a.z));
+            const bool mk = (b.z & MT_MARKER_BIT) != 0;
+            const int np = emit && kind == MT_OP_INSERT && b.y ? (int)prec(d, d.props_half, b.y)[0] : -1;
+            need_n += __popcll(ballot(emit));
+            need_t += wave_sum(emit && kind == MT_OP_INSERT && !mk ? a.x : 0);
+            need_p += wave_sum(np >= 0 ? 1 + 2 * np : 0);
+        }
+        if (need_n > cap || need_t > tcap || need_p > pcap) {
+            if (lane() == 0) {
+                io[0] = -4;
+                io[1] = need_n;
+                io[2] = need_t;
+                io[3] = need_p;
+            }
+            return;
+        }
+    }
     d.g_head = g % d.LG + 1;   // dequeue first: the new groups may reuse its table slot
     d.g_n--;
     int carry = 0, nout = 0, tu = 0, pw = 0;
@@ -1216,7 +1244,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
         }
         carry += bcast(inc, MT_WAVE - 1);
     }
-    if (over) {   // the group table / a segment's FIFO / the caller's buffers are full
+    if (over) {   // the group table / a segment's FIFO is full (the buffers were sized above)
         d.status = MT_DOC_CAPACITY;
         d.cap_cause = 15;
     }
@@ -3131,8 +3159,14 @@ int mt_regenerate_pending(mt_handle *h, uint32_t doc, mt_regen_rec *out, uint32_
         return MT_E_INVALID;
     }
     if (io[0] == -2) {
-        h->err = "mt_regenerate_pending: capacity (group table, segment groups or output buffers); document failed";
+        h->err = "mt_regenerate_pending: capacity (group table or a segment's group FIFO); document failed";
         return MT_E_INVALID;
+    }
+    if (io[0] == -4) {   // nothing changed: retry with buffers of these sizes
+        h->err = "mt_regenerate_pending: output buffers too small: need " + std::to_string(io[1]) + " records, " +
+                 std::to_string(io[2]) + " text units, " + std::to_string(io[3]) + " props words";
+        *n_out = -2;
+        return MT_E_OVERFLOW;
     }
     *n_out = io[0];
     return 0;

@@ -323,7 +323,9 @@ int mt_checksums(mt_handle *h, mt_checksum *out);
    localSeq at the tail of the queue (a remove whose segment a remote remove has replaced
    yields none).  Insert ops carry the segment's text (out_text) and property set (out_props:
    [n, (key, value) x n] or MT_NO_PROPS when it has none); annotate ops carry positions only
-   (their props / combiningOp are the pending op's own).  *n_out = -1: no pending group. */
+   (their props / combiningOp are the pending op's own).  *n_out = -1: no pending group.
+   Output buffers too small for the group: MT_E_OVERFLOW with *n_out = -2 and the document
+   unchanged (mt_last_error names the sizes needed); retry with larger buffers. */
 typedef struct mt_regen_rec {
     int32_t kind;        /* MT_OP_INSERT / MT_OP_REMOVE / MT_OP_ANNOTATE */
     int32_t pos1, pos2;  /* remove / annotate: [pos1, pos2); insert: pos1 */

@@ -204,3 +204,24 @@ def test_live_local_ops_and_invalid_ranges():
                      type="op", contents=grp))
     assert lc.pendingCounts() == (4, 0) and lc.getText() == "ablo world"
     lc.close()
+
+
+@pytest.mark.gpu
+def test_regenerate_with_small_buffers_leaves_the_document():
+    """mt_regenerate_pending with output buffers too small for the oldest group fails with
+    MT_E_OVERFLOW before touching anything: the group is still pending and a second call with
+    room regenerates it."""
+    from fluidframework_amd import MergeTreeBatch
+    mt = MergeTreeBatch(1, seg_capacity=256, lds_seg_capacity=-1, live_client=1)
+    b = Batch(Interner(synthetic=True))
+    b.add_live_doc("abc", [("local", {"pos1": 1, "seg": "xyz", "type": 0})], {"me": 0})
+    a = b.arrays()
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    before = mt.pending_counts().tolist()
+    with pytest.raises(RuntimeError, match="too small"):
+        mt.regenerate_pending(0, cap=4, text_cap=2, props_cap=16)
+    assert mt.pending_counts().tolist() == before and int(mt.status()[0]) == 0
+    recs, text, _ = mt.regenerate_pending(0)
+    assert len(recs) == 1 and int(recs[0]["pos1"]) == 1 and text[:3].tobytes().decode("utf-16-le") == "xyz"
+    mt.close()
