@@ -76,7 +76,13 @@ template <bool kLogT> struct TierLiveT {
 // launch reads the main arrays and never sees such a document.
 // kPackedT: 12-byte unsettled-table entries in LDS (mt_paged.h "packed table"; a tight tier
 // whose table dominates its LDS footprint, e.g. C4: 64 writers, minSeq ~1k messages behind).
-template <bool kLogT, bool kNarrowT = false, bool kBigT = false, bool kPackedT = false> struct TierPagedT {
+// kPPT / kPHT / kUTT (0: from PagedCaps at run time): LDS capacities fixed at compile time --
+// the launch's LDS layout becomes constant offsets and the capacities immediates, so the
+// kernel keeps none of them in registers (the bench's C3 tight tier, mt_replay.hip launch_paged).
+template <bool kLogT, bool kNarrowT = false, bool kBigT = false, bool kPackedT = false, int kPPT = 0, int kPHT = 0,
+          int kUTT = 0>
+struct TierPagedT {
+    static constexpr int kPP = kPPT, kPH = kPHT, kUT = kUTT;
     static constexpr bool kBig = kBigT;
     static constexpr bool kPacked = kPackedT;
     static constexpr bool kLds = true;

@@ -123,6 +123,13 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
 // the window is PagedDoc's first member (standard layout: pointer-interconvertible); no
 // pointer to the PagedDoc is stored, so the whole struct stays in registers
 TD PagedDoc<T> &pdoc(DocT<T> &w) { return *reinterpret_cast<PagedDoc<T> *>(&w); }
+// the launch's capacities with those the tier fixes at compile time (T::kPP ...) substituted
+template <class T> __device__ __forceinline__ PagedCaps eff_caps(PagedCaps pc) {
+    if constexpr (T::kPP > 0) pc.PP = T::kPP;
+    if constexpr (T::kPH > 0) pc.PH = T::kPH;
+    if constexpr (T::kUT > 0) pc.UT = T::kUT;
+    return pc;
+}
 // a paged-layout capacity (cause: 4 text, 5 property records, 7 pages, 8 unsettled table,
 // 9 uid map, 3 heap; kept in the header's HDR_DIAG word)
 TD void pg_fail_cap(DocT<T> &w, int cause) {

@@ -638,10 +638,11 @@ struct PagedSlice {
 template <class T>
 __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState st, const mt_op_rec *ops,
                                                           const int64_t *off, const uint16_t *tin,
-                                                          const uint32_t *pin, int use_resume, PagedCaps pc,
+                                                          const uint32_t *pin, int use_resume, PagedCaps pc_arg,
                                                           PagedSlice sl) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
+    const PagedCaps pc = eff_caps<T>(pc_arg);
     const int doc = blockIdx.x;
     if (doc >= st.n_docs) return;
     if (doc >= sl.skip_lo && doc < sl.skip_hi) return;
@@ -1693,7 +1694,12 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
                         bool big = false) {
     const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8, pc.packed != 0).total;
     const dim3 g(h->n_docs), blk(MT_WAVE);
-    if (pc.packed && h->st.DL)
+    // the bench's C3 tight tier with its capacities fixed at compile time (same code, constant
+    // LDS layout: bench.capacities)
+    if (!big && !pc.packed && pc.narrow && !h->st.DL && pc.PP == 192 && pc.PH == 192 && pc.UT == 220)
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true, false, false, 192, 192, 220>>), g, blk, lb, h->stream,
+                           h->st, b->ops, b->off, b->text, b->props, res, pc, sl);
+    else if (pc.packed && h->st.DL)
         hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
     else if (pc.packed)
