@@ -445,6 +445,30 @@ def _bench_caps(fx):
 
 
 @pytest.mark.parametrize("name", gu.FULL_FIXTURES)
+def test_gpu_full_streams_fast_path(oracle_lib, name):
+    """The replay fast path the bench times -- no delta log, the bench's own capacities (C3:
+    the tight tier with its capacities fixed at compile time) -- on the reference's full
+    10k-message streams: text, segments, leaf partition and properties equal the reference's,
+    and every checksum (delta hash included) equals the C restatement's."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=0, **_bench_caps(fx))
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    osums, ost = oracle_lib.replay_batch(a, threads=2)
+    assert (ost == 0).all() and np.array_equal(mt.checksums(), osums)
+    for i, doc in enumerate(fx["docs"]):
+        exp = dict(gu.expected(doc, interner), deltas=None)   # no delta log: its hash is checked above
+        rows, leaves = mt.get_segments(i)
+        got = dict(text=mt.get_text(i), length=mt.get_length(i), leaves=leaves, segs=rows,
+                   seg_props=[mt.get_segment_props(i, j) for j in range(len(rows))], deltas=None,
+                   status=int(mt.status()[i]))
+        assert not gu.compare_oracle(got, exp), i
+
+
+@pytest.mark.parametrize("name", gu.FULL_FIXTURES)
 def test_gpu_full_streams_at_bench_capacities(name):
     """The configs' full stream lengths (10k messages per document, made by the reference)
     replayed with exactly the capacities bench.py runs (C3: paged LDS capacities 192/220/192,
