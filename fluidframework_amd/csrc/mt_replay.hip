@@ -1699,6 +1699,9 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     if (!big && !pc.packed && pc.narrow && !h->st.DL && pc.PP == 192 && pc.PH == 192 && pc.UT == 220)
         hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true, false, false, 192, 192, 220>>), g, blk, lb, h->stream,
                            h->st, b->ops, b->off, b->text, b->props, res, pc, sl);
+    else if (!big && pc.packed && !h->st.DL && pc.PP == 224 && pc.PH == 900 && pc.UT == 1900)   // the bench's C4 tier
+        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, false, false, true, 224, 900, 1900>>), g, blk, lb, h->stream,
+                           h->st, b->ops, b->off, b->text, b->props, res, pc, sl);
     else if (pc.packed && h->st.DL)
         hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
