@@ -432,8 +432,9 @@ def run_live(args, rank, world, local_rank, dist):
     streams are the reference's own (tests/golden/ref_live_bench.json.gz: 8 participant
     streams of 4000 steps, made by oracle/ref_harness.mjs live), each replicated over the
     documents; one step = reset + one batch of every document's whole stream, resident in
-    HBM.  No CPU baseline: the C restatement models the observer only, and the reference
-    cannot travel."""
+    HBM.  CPU baseline: the C restatement as the same participant (oracle/mt_oracle.c, pinned
+    to these streams by tests/test_oracle.py) replaying rank 0's documents on the host's
+    cores; its checksums are compared with the GPU's document by document."""
     import gzip
     import numpy as np
     from fluidframework_amd import MergeTreeBatch
@@ -464,6 +465,7 @@ def run_live(args, rank, world, local_rank, dist):
              text=e["text"], props=e["props"], seed=e["seed"][sidx] if len(sidx) else e["seed"][:1],
              seed_off=np.concatenate([[0], np.cumsum(slen)]).astype(np.int64))
     n_events = int(lens.sum())
+    threads = args.cpu_threads or host_cores()
     mt = MergeTreeBatch(docs, device=local_rank, seg_capacity=4096, text_capacity=1 << 15, props_capacity=4096,
                         heap_capacity=4096, lds_seg_capacity=-1, live_client=1)
     mt.load_initial_text(a["seed_off"], a["seed"])
@@ -504,6 +506,25 @@ def run_live(args, rank, world, local_rank, dist):
                    tuple(counts[d]) != (st["out"]["localSeq"], st["out"]["pending"]))
     if rank != 0:
         return
+    cpu = oracle_sample = None
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import pyoracle                            # the checker, timed as the CPU baseline
+        # bounded sample: at most ~24M events of CPU work (all of rank 0's 4096 documents)
+        n_sample = args.cpu_sample_docs or min(docs, max(1, 24_000_000 // max(int(lens.max()), 1)))
+        sel_end = int(a["doc_off"][n_sample])
+        sub = dict(a, ops=a["ops"][:sel_end], doc_off=a["doc_off"][: n_sample + 1],
+                   seed_off=a["seed_off"][: n_sample + 1])
+        t_c = time.perf_counter()
+        osums, ost = pyoracle.replay_batch(sub, threads=threads)
+        t_c = time.perf_counter() - t_c
+        cpu = dict(value=round(sel_end / t_c, 1), unit="events/s", cores=threads, kind="port",
+                   host_cpus=os.cpu_count(),
+                   sample=f"oracle/mt_oracle.c participant replay of rank-0 docs [0,{n_sample}) of the same "
+                          f"batch ({sel_end} events) on {threads} host threads, {t_c:.2f} s")
+        sums = mt.checksums()
+        oracle_sample = dict(docs_checked=n_sample,
+                             mismatches=int((osums != sums[:n_sample]).sum() + (ost != status[:n_sample]).sum()))
     print(json.dumps({
         "metric": "live-client merge-tree events applied/sec (local ops + acks + remote ops)",
         "value": round(n_events * world * args.steps / elapsed, 1), "unit": "events/s", "n_gpus": world,
@@ -515,9 +536,10 @@ def run_live(args, rank, world, local_rank, dist):
                                f"(local ops 0.3, acks, remote ops from 8 writers, lag 48)",
                    "docs_total": docs * world, "events_per_step": n_events * world,
                    "parallelism": f"doc-shard x{world}"},
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
         "reference_calibration": _live_calibration(),
-        "parity": {"status_nonzero": int((status != 0).sum()), "docs_checked": len(sample), "mismatches": bad},
+        "parity": {"status_nonzero": int((status != 0).sum()), "docs_checked": len(sample), "mismatches": bad,
+                   "oracle_sample": oracle_sample},
     }))
 
 

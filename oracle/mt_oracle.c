@@ -12,8 +12,11 @@
  * oracle/build_ref.py) and tests/golden/ holds its outputs; tests/test_oracle.py checks
  * this file against them.
  *
- * Scope: the observer replica of SURVEY.md Appendix A -- every message is remote, no local
- * ops, all branch ids 0, no local references, no tracking groups.
+ * Scope: the replica of SURVEY.md Appendix A as a participant whose own short id is 0 --
+ * remote messages, and (live-client path) the local client's own unsequenced
+ * ops (MT_F_LOCAL records) and their acks (MT_F_ACK); an observer is the participant that
+ * submits nothing.  All branch ids 0, no local references, no tracking groups, no reconnect
+ * regeneration (the GPU's k_regen is pinned to the reference's fixtures alone).
  */
 #include "mt_oracle.h"
 
@@ -42,6 +45,7 @@ typedef struct Node {
     int index;
 } Node;
 
+struct Group;
 typedef struct Seg {
     Node n;
     int32_t len, seq, client, rseq, rclient;
@@ -51,7 +55,24 @@ typedef struct Seg {
     uint16_t *text;
     int tcap;
     Props *props;          /* NULL == properties undefined */
+    /* SegmentPropertiesManager (MT/segmentPropertiesManager.ts:12-14): pendingKeyUpdateCount
+       (key -> count) and pendingRewriteCount; allocated with the property set */
+    Props *pk;
+    int32_t prw;
+    /* segmentGroups (SegmentGroupCollection, MT/segmentGroupCollection.ts): FIFO of the
+       pending local-op groups the segment belongs to, oldest at ghead */
+    struct Group **grp;
+    int ghead, gn, gcap;
 } Seg;
+
+/* SegmentGroup {segments, localSeq} (MT/mergeTree.ts:96-99); pendingSegments is a FIFO of
+   them (the doc's pend_head .. pend_tail) */
+typedef struct Group {
+    Seg **segs;
+    int n, cap;
+    int32_t local_seq;
+    struct Group *next;
+} Group;
 
 typedef struct Block {
     Node n;
@@ -86,6 +107,9 @@ struct orc_doc {
     IVec dlog;             /* optional flattened delta records */
     uint64_t delta_hash;
     uint32_t maint[3];     /* mergeTreeMaintenanceCallback events: SPLIT, APPEND, UNLINK */
+    int32_t local_seq;     /* collabWindow.localSeq */
+    Group *pend_head, *pend_tail;   /* pendingSegments */
+    int32_t n_pend;
 };
 
 /* ------------------------------------------------------------------ utilities */
@@ -226,6 +250,44 @@ static void ovl_push(orc_doc *d, Seg *s, int32_t c) {   /* addOverlappingClient 
     s->ovl[s->novl++] = c;
 }
 
+/* SegmentGroupCollection.enqueue MT/segmentGroupCollection.ts:26-29: the group joins the
+   segment's FIFO and the segment the group's list */
+static void group_enqueue(orc_doc *d, Seg *s, Group *g) {
+    if (s->ghead + s->gn == s->gcap) {
+        int nc = s->gcap ? s->gcap * 2 : 4;
+        Group **p = (Group **)dalloc(d, sizeof(Group *) * nc);
+        if (s->gn) memcpy(p, s->grp + s->ghead, sizeof(Group *) * s->gn);
+        s->grp = p;
+        s->gcap = nc;
+        s->ghead = 0;
+    }
+    s->grp[s->ghead + s->gn++] = g;
+    if (g->n == g->cap) {
+        int nc = g->cap ? g->cap * 2 : 8;
+        Seg **p = (Seg **)dalloc(d, sizeof(Seg *) * nc);
+        if (g->n) memcpy(p, g->segs, sizeof(Seg *) * g->n);
+        g->segs = p;
+        g->cap = nc;
+    }
+    g->segs[g->n++] = s;
+}
+
+/* addToPendingList :1955-1962: the op's first segment opens its group at the queue's tail */
+static void add_to_pending(orc_doc *d, Seg *s, Group **g, int32_t local_seq) {
+    if (!*g) {
+        Group *ng = (Group *)dalloc(d, sizeof(Group));
+        ng->local_seq = local_seq;
+        if (d->pend_tail)
+            d->pend_tail->next = ng;
+        else
+            d->pend_head = ng;
+        d->pend_tail = ng;
+        d->n_pend++;
+        *g = ng;
+    }
+    group_enqueue(d, s, *g);
+}
+
 /* localNetLength :1195-1206 */
 static inline int32_t local_net_length(const Seg *s) {
     return s->rseq != RSEQ_NONE ? 0 : s->len;
@@ -340,7 +402,10 @@ static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
         Node *child = node->ch[k];
         if (child->leaf) {
             Seg *s = (Seg *)child;
-            if (s->rseq != RSEQ_NONE) {
+            if (s->gn) {                           /* a pending segment stays :1328 */
+                hold[(*nhold)++] = child;
+                prev = NULL;
+            } else if (s->rseq != RSEQ_NONE) {
                 if (s->rseq > d->min_seq) {
                     hold[(*nhold)++] = child;
                 } else {
@@ -423,6 +488,9 @@ static void zamboni(orc_doc *d) {
     }
 }
 
+static Block theUnfinishedNode;   /* MergeTree.theUnfinishedNode */
+#define UNFINISHED (&theUnfinishedNode)
+
 /* split :2509-2522 */
 static Block *split_block(orc_doc *d, Block *node) {
     int half = MAXN / 2;
@@ -436,7 +504,7 @@ static Block *split_block(orc_doc *d, Block *node) {
 }
 /* updateRoot :1909-1920 */
 static void update_root(orc_doc *d, Block *split_node) {
-    if (split_node) {
+    if (split_node && split_node != UNFINISHED) {
         Block *nr = make_block(d, 2);
         assign_child(nr, &d->root->n, 0);
         assign_child(nr, &split_node->n, 1);
@@ -452,12 +520,18 @@ static Seg *split_at(orc_doc *d, Seg *s, int32_t pos) {
     Seg *r = make_text_seg(d, s->text + pos, s->len - pos);
     s->len = pos;
     r->props = props_clone(d, s->props);
+    if (s->props) {                                  /* copyTo: the pending counts too */
+        r->pk = props_clone(d, s->pk);
+        r->prw = s->prw;
+    }
     r->n.parent = s->n.parent;
     r->rclient = s->rclient;
     r->rseq = s->rseq;
     r->seq = s->seq;
     r->client = s->client;
     for (int i = 0; i < s->novl; i++) ovl_push(d, r, s->ovl[i]);
+    /* segmentGroups.copyTo :26-38: the right half joins every group of the left one */
+    for (int i = 0; i < s->gn; i++) group_enqueue(d, r, s->grp[s->ghead + i]);
     return r;
 }
 
@@ -478,11 +552,49 @@ static int break_tie(int32_t pos, const Node *node, int32_t ref_seq, int32_t cli
 
 enum { WALK_SPLIT = 0, WALK_INSERT = 1 };
 
+/* the first segment the local client sees inside a block: nodeMap(block, 0,
+   UniversalSequenceNumber, collab client) stopping at its first leaf action (:2936-2998) */
+static Seg *first_visible(Block *b) {
+    for (int i = 0; i < b->count; i++) {
+        Node *c = b->ch[i];
+        if (node_len(c, 0, OBSERVER) <= 0) continue;
+        if (c->leaf) return (Seg *)c;
+        Seg *s = first_visible((Block *)c);
+        if (s) return s;
+    }
+    return NULL;
+}
+/* blockInsert's continuePredicate continueFrom (:2176-2194) = rightExcursion (:2346-2376)
+   with checkSegmentIsLocal: the first segment after `node` -- a following sibling leaf
+   whatever its length, else the first one the local client sees in a following block,
+   climbing the parents -- is an unacked local insert */
+static int continue_from(Block *node) {
+    Node *start = &node->n;
+    Block *parent = node->n.parent;
+    while (parent) {
+        int matched = 0;
+        for (int i = 0; i < parent->count; i++) {
+            Node *c = parent->ch[i];
+            if (matched) {
+                if (c->leaf) return ((Seg *)c)->seq == UNASSIGNED;
+                Seg *s = first_visible((Block *)c);
+                if (s) return s->seq == UNASSIGNED;
+            } else {
+                matched = c == start;
+            }
+        }
+        start = &parent->n;
+        parent = parent->n.parent;
+    }
+    return 0;
+}
+
+
 /* insertingWalk :2378-2507 with leaf = splitLeafSegment (:2258-2272) or onLeaf
-   (:2213-2223).  continuePredicate never fires for remote-only replay (no unacked local
-   segments, :2176-2194). */
+   (:2213-2223); a sequenced insert that reaches a block's end at pos 0 continues past it
+   when the next segment is an unacked local insert (continuePredicate). */
 static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_seq,
-                             int32_t client, int mode, Seg *cand) {
+                             int32_t client, int mode, Seg *cand, int32_t seq) {
     int ci;
     Node *new_node = NULL;
     for (ci = 0; ci < block->count; ci++) {
@@ -490,7 +602,11 @@ static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_
         int32_t len = node_len(child, ref_seq, client);
         if (pos < len || (pos == len && break_tie(pos, child, ref_seq, client))) {
             if (!child->leaf) {
-                Block *sn = inserting_walk(d, (Block *)child, pos, ref_seq, client, mode, cand);
+                Block *sn = inserting_walk(d, (Block *)child, pos, ref_seq, client, mode, cand, seq);
+                if (sn == UNFINISHED) {   /* act as if shifted past the child */
+                    pos -= len;
+                    continue;
+                }
                 if (!sn) return NULL;
                 new_node = &sn->n;
                 ci++;
@@ -513,7 +629,10 @@ static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_
             pos -= len;
         }
     }
-    if (!new_node && pos == 0 && mode == WALK_INSERT) new_node = &cand->n;
+    if (!new_node && pos == 0 && mode == WALK_INSERT) {
+        if (seq != UNASSIGNED && continue_from(block)) return UNFINISHED;
+        new_node = &cand->n;
+    }
     if (new_node) {
         for (int i = block->count; i > ci; i--) {
             block->ch[i] = block->ch[i - 1];
@@ -529,7 +648,7 @@ static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_
 
 /* ensureIntervalBoundary :2274-2278 */
 static void ensure_boundary(orc_doc *d, int32_t pos, int32_t ref_seq, int32_t client) {
-    Block *sn = inserting_walk(d, d->root, pos, ref_seq, client, WALK_SPLIT, NULL);
+    Block *sn = inserting_walk(d, d->root, pos, ref_seq, client, WALK_SPLIT, NULL, 0);
     update_root(d, sn);
 }
 
@@ -568,7 +687,11 @@ static void emit_deltas(orc_doc *d, int32_t seq, int kind, DeltaSeg *ds, int n) 
             ivec_push(&d->dlog, pos);
             ivec_push(&d->dlog, s->len);
         }
-        if (kind == MT_OP_ANNOTATE) {
+        if (kind == MT_OP_ANNOTATE && ds[i].npd < 0) {
+            /* propertyDeltas undefined (a pending local rewrite blocked the op) */
+            if (d->record) ivec_push(&d->dlog, -1);
+            sh = fnv_u32(sh, 0xFFFFFFFFu);
+        } else if (kind == MT_OP_ANNOTATE) {
             if (d->record) ivec_push(&d->dlog, ds[i].npd);
             for (int j = 0; j < ds[i].npd; j++) {
                 sh = fnv_u32(sh, ds[i].pd[2 * j]);
@@ -589,7 +712,8 @@ static void emit_deltas(orc_doc *d, int32_t seq, int kind, DeltaSeg *ds, int n) 
 /* ------------------------------------------------------------------ nodeMap */
 typedef struct MapCtx {
     int kind;
-    int32_t seq, client;
+    int32_t seq, client, local_seq;
+    Group *group;          /* the local op's segment group, opened by its first segment */
     const uint32_t *props_rec;
     DeltaSeg *ds;
     int nds, cap;
@@ -607,12 +731,25 @@ static void ds_push(MapCtx *m, Seg *s, int npd, uint32_t *pd) {
     m->nds++;
 }
 
-/* SegmentPropertiesManager.addProperties MT/segmentPropertiesManager.ts:35-111 for a
-   sequenced remote op (seq != Unassigned, collaborating, no pending local keys). */
-static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, uint32_t **pd_out) {
+/* pendingKeyUpdateCount[key] !== undefined */
+static int key_pending(const Seg *s, uint32_t key) { return s->pk && props_find(s->pk, key) >= 0; }
+
+/* SegmentPropertiesManager.addProperties MT/segmentPropertiesManager.ts:35-111 while
+   collaborating: seq UNASSIGNED is the local client's own annotate (every key modified, its
+   keys counted pending), otherwise a sequenced op, which an outstanding local rewrite blocks
+   (returns -1: propertyDeltas undefined) and which skips keys with a pending local update
+   unless it carries a combining op (shouldModifyKey :56-63). */
+static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, int32_t seq, uint32_t **pd_out) {
     uint32_t count = rec[0] & 0xFFFF, combine = rec[0] >> 16;
     if (!s->props) s->props = props_new(d);
     Props *p = s->props;
+    const int local = seq == UNASSIGNED;
+    *pd_out = NULL;
+    if (s->prw > 0 && !local) return -1;
+    if (!s->pk) s->pk = props_new(d);
+    const int combining = combine == MT_COMBINE_TABLE;
+#define MODIFY(k) (local || combining || !key_pending(s, (k)))
+    if (combine == MT_COMBINE_REWRITE && local) s->prw++;
     /* deltas: ordered map key -> previous value (insertion order, overwrite in place) */
     uint32_t *pd = (uint32_t *)dalloc(d, sizeof(uint32_t) * 2 * (p->n + count + 1));
     int npd = 0;
@@ -639,7 +776,7 @@ static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, uint32_t **pd
                     truthy = (v != MT_VAL_NULL) && !(v & MT_VAL_FALSY_BIT);
                 }
             }
-            if (!truthy) {
+            if (!truthy && MODIFY(key)) {
                 PD_SET(key, p->val[i]);
                 props_del(p, key);
             } else {
@@ -649,6 +786,12 @@ static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, uint32_t **pd
     }
     for (uint32_t j = 0; j < count; j++) {
         uint32_t key = rec[1 + 2 * j], val = rec[2 + 2 * j];
+        if (local) {
+            int q = props_find(s->pk, key);
+            props_set(d, s->pk, key, q >= 0 ? s->pk->val[q] + 1 : 1);
+        } else if (!MODIFY(key)) {
+            continue;
+        }
         int i = props_find(p, key);
         /* deltas[key] = previousValue === undefined ? null : previousValue */
         const int absent = i < 0 || p->val[i] == MT_VAL_UNDEF;
@@ -677,27 +820,48 @@ static int add_properties(orc_doc *d, Seg *s, const uint32_t *rec, uint32_t **pd
             props_set(d, p, key, val);
     }
 #undef PD_SET
+#undef MODIFY
     *pd_out = pd;
     return npd;
+}
+
+/* ackPendingProperties MT/segmentPropertiesManager.ts:19-33 */
+static void ack_pending_properties(Seg *s, const uint32_t *rec) {
+    uint32_t count = rec[0] & 0xFFFF, combine = rec[0] >> 16;
+    if (combine == MT_COMBINE_REWRITE) s->prw--;
+    for (uint32_t j = 0; j < count && s->pk; j++) {
+        int q = props_find(s->pk, rec[1 + 2 * j]);
+        if (q < 0) continue;
+        if (--s->pk->val[q] == 0) props_del(s->pk, rec[1 + 2 * j]);
+    }
 }
 
 /* markRemoved / annotateSegment leaf actions :2647-2693, :2607-2620 */
 static void map_leaf(MapCtx *m, Seg *s) {
     orc_doc *d = m->d;
     if (m->kind == MT_OP_REMOVE) {
-        if (s->rseq != RSEQ_NONE) {
+        if (s->rseq == UNASSIGNED) {          /* a pending local removal: replaced :2657-2662 */
+            s->rclient = m->client;
+            s->rseq = m->seq;
+        } else if (s->rseq != RSEQ_NONE) {
             ovl_push(d, s, m->client);
         } else {
             s->rclient = m->client;
             s->rseq = m->seq;
             ds_push(m, s, 0, NULL);
         }
-        add_to_lru(d, s, m->seq);
+        if (s->rseq == UNASSIGNED && m->client == OBSERVER)
+            add_to_pending(d, s, &m->group, m->local_seq);
+        else
+            add_to_lru(d, s, m->seq);
     } else {
         uint32_t *pd;
-        int npd = add_properties(d, s, m->props_rec, &pd);
+        int npd = add_properties(d, s, m->props_rec, m->seq, &pd);
         ds_push(m, s, npd, pd);
-        add_to_lru(d, s, m->seq);
+        if (m->seq == UNASSIGNED)
+            add_to_pending(d, s, &m->group, m->local_seq);
+        else
+            add_to_lru(d, s, m->seq);
     }
 }
 
@@ -754,28 +918,92 @@ static int update_seq_numbers(orc_doc *d, int32_t msn, int32_t seq) {
     return MT_DOC_OK;
 }
 
+/* ackPendingSegment MT/client.ts:589-626 (one GROUP member) -> MergeTree.ackPendingSegment
+   :1926-1953 with ISegment.ack :486-521 */
+static void ack_pending(orc_doc *d, const mt_op_rec *op, const uint32_t *props_arena) {
+    Group *g = d->pend_head;
+    const int32_t seq = op->seq;
+    if (g) {
+        d->pend_head = g->next;
+        if (!d->pend_head) d->pend_tail = NULL;
+        d->n_pend--;
+        for (int i = 0; i < g->n; i++) {
+            Seg *s = g->segs[i];
+            if (s->gn == 0 || s->grp[s->ghead] != g) {   /* assert.equal(currentSegmentGroup, ..) */
+                d->status = MT_DOC_INTERNAL;
+                return;
+            }
+            s->ghead++;
+            s->gn--;
+            if (op->kind == MT_OP_ANNOTATE) {
+                static const uint32_t empty_rec[1] = {0};
+                ack_pending_properties(s, op->props != MT_NO_PROPS ? props_arena + op->props : empty_rec);
+            } else if (op->kind == MT_OP_INSERT) {
+                s->seq = seq;
+            } else if (op->kind == MT_OP_REMOVE) {
+                if (s->rseq == UNASSIGNED) s->rseq = seq;   /* else a remote removal replaced it */
+            }
+            add_to_lru(d, s, seq);
+        }
+    }
+    zamboni(d);
+}
+
+/* getValidOpRange MT/client.ts:486-548 for the local client's own op (its length view) */
+static int local_range_ok(orc_doc *d, const mt_op_rec *op) {
+    const int32_t len = orc_length(d), start = op->pos1;
+    if (start < 0 || start > len || (start == len && op->kind != MT_OP_INSERT)) return 0;
+    if (op->kind != MT_OP_INSERT && op->pos2 <= start) return 0;
+    return 1;
+}
+
 int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
                   const uint32_t *props_arena) {
     if (d->status) return d->status;
     int32_t r = op->ref_seq, c = op->client, seq = op->seq;
+    if (op->flags & MT_F_ACK) {             /* applyMsg of our own op's echo :805-813 */
+        if (op->kind != MT_OP_NOOP) ack_pending(d, op, props_arena);
+        if (!d->status && !(op->flags & MT_F_GROUP_MORE)) {
+            int st = update_seq_numbers(d, op->min_seq, seq);
+            if (st) d->status = st;
+        }
+        return d->status;
+    }
+    int32_t local_seq = 0;
+    if (op->flags & MT_F_LOCAL) {
+        /* insertSegmentLocal / removeRangeLocal / annotateRangeLocal MT/client.ts:164-211:
+           getClientSequenceArgs (:559-575) -- the collab client at refSeq = currentSeq,
+           UnassignedSequenceNumber; an invalid range applies nothing */
+        if (op->kind == MT_OP_NOOP || !local_range_ok(d, op)) return d->status;
+        if (op->kind == MT_OP_INSERT && !(op->flags & MT_F_MARKER) && op->pos2 <= 0) return d->status;
+        r = d->current_seq;
+        c = OBSERVER;
+        seq = UNASSIGNED;
+    }
     if (op->kind == MT_OP_INSERT) {
         /* Client.applyInsertOp MT/client.ts:394-442 -> MergeTree.insertSegments :2001-2031 */
         Seg *s = segment_from_op(d, op, text_arena, props_arena);
         ensure_boundary(d, op->pos1, r, c);
+        if (seq == UNASSIGNED) local_seq = ++d->local_seq;
         if (s->len > 0) {                   /* blockInsert :2227-2256 */
             s->seq = seq;
             s->client = c;
-            Block *sn = inserting_walk(d, d->root, op->pos1, r, c, WALK_INSERT, s);
+            Block *sn = inserting_walk(d, d->root, op->pos1, r, c, WALK_INSERT, s, seq);
             if (s->n.parent == NULL) {
                 d->status = MT_DOC_INSERT_FAILED;
                 return d->status;
             }
             update_root(d, sn);
-            if (seq > d->min_seq) add_to_lru(d, s, seq);   /* saveIfLocal :2197-2212 */
+            if (seq == UNASSIGNED && c == OBSERVER) {   /* saveIfLocal :2197-2212 */
+                Group *g = NULL;
+                add_to_pending(d, s, &g, local_seq);
+            } else if (seq > d->min_seq) {
+                add_to_lru(d, s, seq);
+            }
         }
         DeltaSeg ds = {s, 0, NULL};
         emit_deltas(d, seq, MT_OP_INSERT, &ds, 1);
-        zamboni(d);
+        if (seq != UNASSIGNED) zamboni(d);
     } else if (op->kind == MT_OP_REMOVE || op->kind == MT_OP_ANNOTATE) {
         /* markRangeRemoved :2640-2752 / annotateRange :2598-2638 */
         if (op->kind == MT_OP_ANNOTATE && op->props != MT_NO_PROPS &&
@@ -791,14 +1019,16 @@ int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
         m.seq = seq;
         m.client = c;
         m.d = d;
+        if (seq == UNASSIGNED) m.local_seq = ++d->local_seq;
         m.props_rec = op->props != MT_NO_PROPS ? props_arena + op->props : NULL;
         static const uint32_t empty_rec[1] = {0};
         if (!m.props_rec) m.props_rec = empty_rec;
         node_map(&m, d->root, r, c, op->pos1, op->pos2);
         emit_deltas(d, seq, op->kind, m.ds, m.nds);
         free(m.ds);
-        zamboni(d);
+        if (seq != UNASSIGNED) zamboni(d);
     }
+    if (seq == UNASSIGNED) return d->status;   /* local: no completeAndLogOp asserts, no seq update */
     if (op->kind != MT_OP_NOOP) {
         /* completeAndLogOp asserts MT/client.ts:451-479 */
         if (!(d->current_seq < seq)) return d->status = MT_DOC_SEQ_ORDER;
@@ -868,7 +1098,7 @@ static int load_append(orc_doc *d, Seg **segs, int n, int32_t cli, int32_t seq) 
         if (s->len <= 0) continue;
         s->seq = seq;
         s->client = cli;
-        Block *sn = inserting_walk(d, d->root, ins, 0, cli, WALK_INSERT, s);
+        Block *sn = inserting_walk(d, d->root, ins, 0, cli, WALK_INSERT, s, seq);
         if (s->n.parent == NULL) return d->status = MT_DOC_INSERT_FAILED;
         update_root(d, sn);
         if (seq > d->min_seq) add_to_lru(d, s, seq);   /* saveIfLocal :2197-2212 */
@@ -948,6 +1178,10 @@ void orc_free(orc_doc *d) {
     free(d);
 }
 int32_t orc_status(const orc_doc *d) { return d->status; }
+void orc_pending_counts(const orc_doc *d, int32_t *out) {
+    out[0] = d->local_seq;   /* collabWindow.localSeq */
+    out[1] = d->n_pend;      /* pendingSegments.count() */
+}
 void orc_set_record_deltas(orc_doc *d, int32_t on) { d->record = on; }
 int32_t orc_view_length(orc_doc *d, int32_t ref_seq, int32_t client) {
     return node_len(&d->root->n, ref_seq, client);

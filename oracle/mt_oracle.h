@@ -32,6 +32,8 @@ orc_doc *orc_load(const mt_seg_rec *recs, int32_t n_header, int32_t n_total, con
 int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
                   const uint32_t *props_arena);
 int32_t orc_status(const orc_doc *d);
+/* live participant: out[0] = collabWindow.localSeq, out[1] = pending segment groups */
+void orc_pending_counts(const orc_doc *d, int32_t *out);
 int32_t orc_view_length(orc_doc *d, int32_t ref_seq, int32_t client);
 int32_t orc_length(orc_doc *d);
 int32_t orc_text(orc_doc *d, uint16_t *out, int32_t cap);

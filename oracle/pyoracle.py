@@ -43,6 +43,7 @@ def lib():
         L.orc_apply.restype = i32
         L.orc_status.argtypes = [P]
         L.orc_status.restype = i32
+        L.orc_pending_counts.argtypes = [P, P]
         L.orc_view_length.argtypes = [P, i32, i32]
         L.orc_view_length.restype = i32
         L.orc_length.argtypes = [P]
@@ -120,6 +121,12 @@ class OracleDoc:
             if st:
                 return st
         return 0
+
+    def pending_counts(self):
+        """(collabWindow.localSeq, pending segment groups) of a live participant."""
+        o = np.zeros(2, dtype=np.int32)
+        lib().orc_pending_counts(self.h, _p(o))
+        return int(o[0]), int(o[1])
 
     def maintenance(self):
         """[SPLIT, APPEND, UNLINK] mergeTreeMaintenanceCallback counts (orc_maintenance)."""

@@ -89,6 +89,39 @@ def expected(doc, interner):
                 seg_props=seg_props, deltas=flat)
 
 
+def expected_live(doc, interner):
+    """expected() of a live-participant fixture (ref_live*): propertyDeltas undefined -> -1."""
+    exp = expected(dict(doc, out=dict(doc["out"], deltas=[])), interner)
+    flat = []
+    for seq, kind, n, dsegs in doc["out"]["deltas"]:
+        flat += [seq, kind, n]
+        for s in dsegs:
+            flat += [s[0], s[1]]
+            if kind == 2:
+                if len(s) < 3:          # propertyDeltas undefined: an outstanding local rewrite
+                    flat.append(-1)
+                    continue
+                flat.append(len(s[2]))
+                for k, v in s[2].items():
+                    flat += [interner.key(k), _sid(interner.val(v))]
+    exp["deltas"] = flat
+    return exp
+
+
+def live_entries(doc, local="local-0"):
+    """A live fixture document without reconnects -> Batch.add_live_doc entries."""
+    ent = []
+    for ev in doc["events"]:
+        if ev[0] == "L":
+            ent.append(("local", ev[1]))
+        else:
+            _, cid, seq, ref, msn, op = ev
+            m = dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
+                     type="op", contents=op)
+            ent.append(("ack" if cid == local else "msg", m))
+    return ent
+
+
 def compare_oracle(o, exp, status=0):
     errs = []
     if o["status"] != status:

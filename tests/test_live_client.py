@@ -1,9 +1,9 @@
 """Live-client path: a participant Client's own unsequenced ops, their acks,
 remote ops resolved around unacked segments and reconnect regeneration, on the GPU
 (live_client handles) against streams the reference itself produced
-(tests/golden/ref_live*.json.gz, oracle/ref_harness.mjs "live").  The C restatement
-(oracle/mt_oracle.c) models the observer only, so these tests are pinned to the reference's
-fixtures alone.  Checked per document: every local op the facade returns, every op
+(tests/golden/ref_live*.json.gz, oracle/ref_harness.mjs "live"), and on reconnect-free
+streams against the C restatement's participant replay (oracle/mt_oracle.c, itself pinned to
+the same fixtures by tests/test_oracle.py).  Checked per document: every local op the facade returns, every op
 regeneratePendingOp rebuilds, the final text / length / leaf partition / segment table (unacked
 seq and removedSeq = -1) / property sets, every delta-callback record, localSeq and the
 pending segment groups."""
@@ -20,24 +20,6 @@ def _msg(ev):
     _, cid, seq, ref, msn, op = ev
     return dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref, minimumSequenceNumber=msn,
                 type="op", contents=op)
-
-
-def expected_live(doc, interner):
-    exp = gu.expected(dict(doc, out=dict(doc["out"], deltas=[])), interner)
-    flat = []
-    for seq, kind, n, dsegs in doc["out"]["deltas"]:
-        flat += [seq, kind, n]
-        for s in dsegs:
-            flat += [s[0], s[1]]
-            if kind == 2:
-                if len(s) < 3:          # propertyDeltas undefined: an outstanding local rewrite
-                    flat.append(-1)
-                    continue
-                flat.append(len(s[2]))
-                for k, v in s[2].items():
-                    flat += [interner.key(k), gu._sid(interner.val(v))]
-    exp["deltas"] = flat
-    return exp
 
 
 # ---------------------------------------------------------------- CPU: encoding
@@ -122,7 +104,7 @@ def test_live_client_matches_reference(name):
         o = dict(text=mt.get_text(0), length=mt.get_length(0), leaves=leaves, segs=rows,
                  seg_props=[mt.get_segment_props(0, i) for i in range(len(rows))],
                  deltas=mt.get_delta_log(0), status=int(mt.status()[0]))
-        errs += gu.compare_oracle(o, expected_live(doc, interner))
+        errs += gu.compare_oracle(o, gu.expected_live(doc, interner))
         ls, ng = lc.pendingCounts()
         if (ls, ng) != (doc["out"]["localSeq"], doc["out"]["pending"]):
             errs.append(f"localSeq/pending {(ls, ng)} != {(doc['out']['localSeq'], doc['out']['pending'])}")
@@ -224,4 +206,33 @@ def test_regenerate_with_small_buffers_leaves_the_document():
     assert mt.pending_counts().tolist() == before and int(mt.status()[0]) == 0
     recs, text, _ = mt.regenerate_pending(0)
     assert len(recs) == 1 and int(recs[0]["pos1"]) == 1 and text[:3].tobytes().decode("utf-16-le") == "xyz"
+    mt.close()
+
+
+@pytest.mark.gpu
+def test_live_checksums_match_oracle_participant():
+    """Device checksums of live documents (text, property runs, every delta callback) equal
+    the C restatement's participant replay (oracle/mt_oracle.c, pinned to the reference by
+    tests/test_oracle.py) on the reference's participant streams without reconnects."""
+    import os
+    import sys
+    from fluidframework_amd import MergeTreeBatch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyoracle
+    docs = [d for name in ["ref_live_bench", "ref_live_deep"] for d in gu.load(name)["docs"]
+            if not any(e[0] == "R" for e in d["events"])]
+    b = Batch(Interner(synthetic=True))
+    for d in docs:
+        b.add_live_doc(d["seed_text"], gu.live_entries(d), {"local-0": 0})
+    a = b.arrays()
+    mt = MergeTreeBatch(len(docs), seg_capacity=16384, text_capacity=1 << 17, props_capacity=1 << 16,
+                        heap_capacity=4096, lds_seg_capacity=-1, live_client=1)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    osums, ost = pyoracle.replay_batch(a)
+    assert ost.tolist() == [0] * len(docs)
+    assert mt.status().tolist() == [0] * len(docs)
+    sums = mt.checksums()
+    for f in sums.dtype.names:
+        assert sums[f].tolist() == osums[f].tolist(), f
     mt.close()

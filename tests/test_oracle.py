@@ -130,3 +130,42 @@ def test_snapshot_encoder_round_trip(name):
         names = {v: k for k, v in short.items()}
         specs, lengths = record_specs(a["segs"], a["text"], a["props"], interner, names)
         assert encode_chunks(specs, lengths, snap.min_seq, snap.cur_seq, cs) == doc["chunks"], doc["doc"]
+
+
+def _live_docs():
+    """Live-participant fixture documents without reconnects (the oracle does not model
+    regeneratePendingOp): all 8 ref_live_bench streams (4000 steps each) and the others'."""
+    out = []
+    for name in ["ref_live_bench", "ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep"]:
+        out += [(name, d) for d in gu.load(name)["docs"] if not any(e[0] == "R" for e in d["events"])]
+    return out
+
+
+def test_oracle_live_participant_matches_reference(oracle_lib):
+    """The restatement as a participant (MT_F_LOCAL ops, MT_F_ACK echoes, remote ops around
+    unacked segments) equals the reference Client on its own streams: text, length, leaf
+    partition, segment table, property sets, every delta record, localSeq and pending groups;
+    then, after the fixture's drain acks every pending op, the drained replica."""
+    from fluidframework_amd.wire import Batch, Interner
+    docs = _live_docs()
+    assert len(docs) >= 9
+    for name, doc in docs:
+        it = Interner(synthetic=True)
+        b = Batch(it)
+        b.add_live_doc(doc["seed_text"], gu.live_entries(doc), {"local-0": 0})
+        n_run = len(b.recs)
+        b = Batch(it)   # the same stream + the drain (same interner: the same records first)
+        b.add_live_doc(doc["seed_text"], gu.live_entries(doc) + gu.live_entries(dict(events=doc["drain"])),
+                       {"local-0": 0})
+        a = b.arrays()
+        d = oracle_lib.OracleDoc.new(a["seed"][:a["seed_off"][1]])
+        assert d.apply_all(a["ops"][:n_run], a["text"], a["props"]) == 0
+        errs = gu.compare_oracle(d.outputs(), gu.expected_live(doc, it))
+        assert d.pending_counts() == (doc["out"]["localSeq"], doc["out"]["pending"]), (name, doc["doc"])
+        assert not errs, (name, doc["doc"], errs)
+        assert d.apply_all(a["ops"][n_run:], a["text"], a["props"]) == 0
+        o = d.outputs()
+        exp = gu.expected(dict(doc, out=dict(doc["drained"], deltas=[])), it)
+        assert d.pending_counts()[1] == doc["drained"]["pending"] == 0
+        assert (o["text"], o["leaves"], o["segs"].tolist(), o["seg_props"]) == \
+            (exp["text"], exp["leaves"], exp["segs"], exp["seg_props"]), (name, doc["doc"])
