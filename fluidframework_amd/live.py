@@ -21,6 +21,34 @@ OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_GROUP = 0, 1, 2, 3
 F_MARKER = 2
 
 
+def regen_op(interner, reset, rec, text, props):
+    """One mt_regen_rec (include/mt_replay.h) -> the op regeneratePendingOp returns
+    (OpBuilder.createInsertSegmentOp / createRemoveRangeOp / createAnnotateRangeOp)."""
+    kind = int(rec["kind"])
+    if kind == OP_INSERT:
+        pset = None
+        if int(rec["props_off"]) != MT_NO_PROPS_U32:
+            o = int(rec["props_off"])
+            n = int(props[o])
+            pset = {interner.key_name(int(props[o + 1 + 2 * j])):
+                    interner.val_value(int(props[o + 2 + 2 * j])) for j in range(n)}
+        if int(rec["flags"]) & F_MARKER:
+            seg = {"marker": {"refType": int(rec["text_off"])}}
+        else:
+            t0, tl = int(rec["text_off"]), int(rec["text_len"])
+            s = text[t0:t0 + tl].tobytes().decode("utf-16-le")
+            seg = {"text": s} if pset is not None else s
+        if pset is not None:
+            seg["props"] = pset
+        return {"pos1": int(rec["pos1"]), "seg": seg, "type": OP_INSERT}
+    if kind == OP_REMOVE:
+        return {"pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "type": OP_REMOVE}
+    op = {"pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "props": reset["props"], "type": OP_ANNOTATE}
+    if reset.get("combiningOp") is not None:
+        op["combiningOp"] = reset["combiningOp"]
+    return op
+
+
 class LiveClient:
     """One GPU document replica owned by a participant client (short id 0)."""
 
@@ -135,29 +163,7 @@ class LiveClient:
         return ops[0] if len(ops) == 1 else {"ops": ops, "type": OP_GROUP}
 
     def _regen_op(self, reset, rec, text, props):
-        kind = int(rec["kind"])
-        if kind == OP_INSERT:
-            pset = None
-            if int(rec["props_off"]) != MT_NO_PROPS_U32:
-                o = int(rec["props_off"])
-                n = int(props[o])
-                pset = {self.interner.key_name(int(props[o + 1 + 2 * j])):
-                        self.interner.val_value(int(props[o + 2 + 2 * j])) for j in range(n)}
-            if int(rec["flags"]) & F_MARKER:
-                seg = {"marker": {"refType": int(rec["text_off"])}}
-            else:
-                t0, tl = int(rec["text_off"]), int(rec["text_len"])
-                s = text[t0:t0 + tl].tobytes().decode("utf-16-le")
-                seg = {"text": s} if pset is not None else s
-            if pset is not None:
-                seg["props"] = pset
-            return {"pos1": int(rec["pos1"]), "seg": seg, "type": OP_INSERT}
-        if kind == OP_REMOVE:
-            return {"pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "type": OP_REMOVE}
-        op = {"pos1": int(rec["pos1"]), "pos2": int(rec["pos2"]), "props": reset["props"], "type": OP_ANNOTATE}
-        if reset.get("combiningOp") is not None:
-            op["combiningOp"] = reset["combiningOp"]
-        return op
+        return regen_op(self.interner, reset, rec, text, props)
 
     # -------------------------------------------------------------- read-outs (local view)
     def getLength(self):

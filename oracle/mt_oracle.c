@@ -15,8 +15,8 @@
  * Scope: the replica of SURVEY.md Appendix A as a participant whose own short id is 0 --
  * remote messages, and (live-client path) the local client's own unsequenced
  * ops (MT_F_LOCAL records) and their acks (MT_F_ACK); an observer is the participant that
- * submits nothing.  All branch ids 0, no local references, no tracking groups, no reconnect
- * regeneration (the GPU's k_regen is pinned to the reference's fixtures alone).
+ * submits nothing; reconnects regenerate the pending ops (orc_regenerate).  All branch ids
+ * 0, no local references, no tracking groups.
  */
 #include "mt_oracle.h"
 
@@ -63,6 +63,8 @@ typedef struct Seg {
        pending local-op groups the segment belongs to, oldest at ghead */
     struct Group **grp;
     int ghead, gn, gcap;
+    int32_t lseq, lrseq;   /* localSeq / localRemovedSeq (RSEQ_NONE: undefined) */
+    int32_t ord;           /* document order (regeneration's ordinal sort) */
 } Seg;
 
 /* SegmentGroup {segments, localSeq} (MT/mergeTree.ts:96-99); pendingSegments is a FIFO of
@@ -111,6 +113,9 @@ struct orc_doc {
     Group *pend_head, *pend_tail;   /* pendingSegments */
     int32_t n_pend;
 };
+
+typedef void (*seg_fn)(Seg *, void *);
+static void walk_segs(Node *n, seg_fn fn, void *arg);
 
 /* ------------------------------------------------------------------ utilities */
 static void vec_push(Vec *v, void *x) {
@@ -222,6 +227,7 @@ static Seg *make_text_seg(orc_doc *d, const uint16_t *text, int32_t len) {
     s->seq = 0;               /* UniversalSequenceNumber  MT/mergeTree.ts:433 */
     s->client = -1;           /* LocalClientId            MT/mergeTree.ts:432 */
     s->rseq = RSEQ_NONE;
+    s->lseq = s->lrseq = RSEQ_NONE;
     s->marker = -1;
     s->tcap = len > 0 ? len : 1;
     s->text = (uint16_t *)malloc(sizeof(uint16_t) * s->tcap);
@@ -529,6 +535,8 @@ static Seg *split_at(orc_doc *d, Seg *s, int32_t pos) {
     r->rseq = s->rseq;
     r->seq = s->seq;
     r->client = s->client;
+    r->lseq = s->lseq;
+    r->lrseq = s->lrseq;
     for (int i = 0; i < s->novl; i++) ovl_push(d, r, s->ovl[i]);
     /* segmentGroups.copyTo :26-38: the right half joins every group of the left one */
     for (int i = 0; i < s->gn; i++) group_enqueue(d, r, s->grp[s->ghead + i]);
@@ -843,11 +851,13 @@ static void map_leaf(MapCtx *m, Seg *s) {
         if (s->rseq == UNASSIGNED) {          /* a pending local removal: replaced :2657-2662 */
             s->rclient = m->client;
             s->rseq = m->seq;
+            s->lrseq = RSEQ_NONE;
         } else if (s->rseq != RSEQ_NONE) {
             ovl_push(d, s, m->client);
         } else {
             s->rclient = m->client;
             s->rseq = m->seq;
+            s->lrseq = m->seq == UNASSIGNED ? m->local_seq : RSEQ_NONE;
             ds_push(m, s, 0, NULL);
         }
         if (s->rseq == UNASSIGNED && m->client == OBSERVER)
@@ -940,13 +950,37 @@ static void ack_pending(orc_doc *d, const mt_op_rec *op, const uint32_t *props_a
                 ack_pending_properties(s, op->props != MT_NO_PROPS ? props_arena + op->props : empty_rec);
             } else if (op->kind == MT_OP_INSERT) {
                 s->seq = seq;
+                s->lseq = RSEQ_NONE;
             } else if (op->kind == MT_OP_REMOVE) {
+                s->lrseq = RSEQ_NONE;
                 if (s->rseq == UNASSIGNED) s->rseq = seq;   /* else a remote removal replaced it */
             }
             add_to_lru(d, s, seq);
         }
     }
     zamboni(d);
+}
+
+static void ord_fn(Seg *s, void *arg) { s->ord = (*(int32_t *)arg)++; }
+typedef struct ReconAcc {
+    const Seg *target;
+    int32_t local_seq, pos, done;
+} ReconAcc;
+/* findReconnectionPostition MT/client.ts:675-707: the segments before `target` that are
+   inserted and not removed as of the group's localSeq */
+static void recon_fn(Seg *s, void *arg) {
+    ReconAcc *a = (ReconAcc *)arg;
+    if (a->done || s == a->target) {
+        a->done = 1;
+        return;
+    }
+    if ((s->lseq == RSEQ_NONE || s->lseq <= a->local_seq) &&
+        (s->rseq == RSEQ_NONE || (s->lrseq != RSEQ_NONE && s->lrseq > a->local_seq)))
+        a->pos += s->len;
+}
+static int cmp_ord(const void *a, const void *b) {
+    const Seg *x = *(Seg *const *)a, *y = *(Seg *const *)b;
+    return x->ord < y->ord ? -1 : x->ord > y->ord;
 }
 
 /* getValidOpRange MT/client.ts:486-548 for the local client's own op (its length view) */
@@ -988,6 +1022,7 @@ int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
         if (s->len > 0) {                   /* blockInsert :2227-2256 */
             s->seq = seq;
             s->client = c;
+            s->lseq = seq == UNASSIGNED ? local_seq : RSEQ_NONE;
             Block *sn = inserting_walk(d, d->root, op->pos1, r, c, WALK_INSERT, s, seq);
             if (s->n.parent == NULL) {
                 d->status = MT_DOC_INSERT_FAILED;
@@ -1178,6 +1213,82 @@ void orc_free(orc_doc *d) {
     free(d);
 }
 int32_t orc_status(const orc_doc *d) { return d->status; }
+/* regeneratePendingOp MT/client.ts:855-893 for one (non-GROUP) pending op of kind `kind`:
+   resetPendingDeltaToOps (:709-767) on the oldest segment group -- its segments in document
+   order (the ordinal sort), each at findReconnectionPostition, one op each (a remove whose
+   removal a remote replaced: none), each joining a new group at the queue's tail.  Outputs
+   mt_regen_rec records (include/mt_replay.h); returns their count, -1 without a pending
+   group, -2 when an output buffer is too small (the document is then left unusable). */
+int32_t orc_regenerate(orc_doc *d, int32_t kind, orc_regen_rec *out, int32_t cap, uint16_t *text,
+                       int32_t text_cap, uint32_t *props, int32_t props_cap) {
+    Group *g = d->pend_head;
+    if (!g) return -1;
+    d->pend_head = g->next;
+    if (!d->pend_head) d->pend_tail = NULL;
+    d->n_pend--;
+    int32_t ord = 0;
+    walk_segs(&d->root->n, ord_fn, &ord);
+    Seg **segs = (Seg **)malloc(sizeof(Seg *) * (g->n > 0 ? g->n : 1));
+    memcpy(segs, g->segs, sizeof(Seg *) * g->n);
+    qsort(segs, g->n, sizeof(Seg *), cmp_ord);
+    int32_t n = 0, tu = 0, pu = 0;
+    for (int i = 0; i < g->n; i++) {
+        Seg *s = segs[i];
+        if (s->gn == 0 || s->grp[s->ghead] != g) {
+            d->status = MT_DOC_INTERNAL;
+            break;
+        }
+        s->ghead++;
+        s->gn--;
+        ReconAcc ra = {s, g->local_seq, 0, 0};
+        walk_segs(&d->root->n, recon_fn, &ra);
+        if (kind == MT_OP_REMOVE && s->lrseq == RSEQ_NONE) continue;
+        if (n >= cap) {
+            n = -2;
+            break;
+        }
+        orc_regen_rec *r = &out[n++];
+        memset(r, 0, sizeof(*r));
+        r->kind = kind;
+        r->pos1 = ra.pos;
+        r->pos2 = kind == MT_OP_INSERT ? 0 : ra.pos + s->len;
+        r->local_seq = g->local_seq;
+        r->props_off = MT_NO_PROPS;
+        if (kind == MT_OP_INSERT) {   /* createInsertSegmentOp: the segment's JSON as it is now */
+            if (s->marker >= 0) {
+                r->flags = MT_F_MARKER;
+                r->text_off = (uint32_t)s->marker;
+                r->text_len = 1;
+            } else {
+                if (tu + s->len > text_cap) {
+                    n = -2;
+                    break;
+                }
+                memcpy(text + tu, s->text, sizeof(uint16_t) * s->len);
+                r->text_off = (uint32_t)tu;
+                r->text_len = (uint32_t)s->len;
+                tu += s->len;
+            }
+            if (s->props) {
+                if (pu + 1 + 2 * s->props->n > props_cap) {
+                    n = -2;
+                    break;
+                }
+                r->props_off = (uint32_t)pu;
+                props[pu++] = (uint32_t)s->props->n;
+                for (int k = 0; k < s->props->n; k++) {
+                    props[pu++] = s->props->key[k];
+                    props[pu++] = s->props->val[k];
+                }
+            }
+        }
+        Group *ng = NULL;
+        add_to_pending(d, s, &ng, g->local_seq);
+    }
+    free(segs);
+    return d->status ? -3 : n;
+}
+
 void orc_pending_counts(const orc_doc *d, int32_t *out) {
     out[0] = d->local_seq;   /* collabWindow.localSeq */
     out[1] = d->n_pend;      /* pendingSegments.count() */

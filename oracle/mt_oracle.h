@@ -34,6 +34,15 @@ int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
 int32_t orc_status(const orc_doc *d);
 /* live participant: out[0] = collabWindow.localSeq, out[1] = pending segment groups */
 void orc_pending_counts(const orc_doc *d, int32_t *out);
+/* one regenerated op; the layout of mt_regen_rec (include/mt_replay.h) */
+typedef struct orc_regen_rec {
+    int32_t kind, pos1, pos2, local_seq;
+    uint32_t text_off, text_len, props_off, flags;
+} orc_regen_rec;
+/* regeneratePendingOp of the oldest pending group (one non-GROUP op of kind `kind`); records; returns their count, -1: no pending group, -2: a
+   buffer too small, -3: an internal inconsistency */
+int32_t orc_regenerate(orc_doc *d, int32_t kind, orc_regen_rec *out, int32_t cap, uint16_t *text,
+                       int32_t text_cap, uint32_t *props, int32_t props_cap);
 int32_t orc_view_length(orc_doc *d, int32_t ref_seq, int32_t client);
 int32_t orc_length(orc_doc *d);
 int32_t orc_text(orc_doc *d, uint16_t *out, int32_t cap);

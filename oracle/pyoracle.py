@@ -44,6 +44,8 @@ def lib():
         L.orc_status.argtypes = [P]
         L.orc_status.restype = i32
         L.orc_pending_counts.argtypes = [P, P]
+        L.orc_regenerate.argtypes = [P, i32, P, i32, P, i32, P, i32]
+        L.orc_regenerate.restype = i32
         L.orc_view_length.argtypes = [P, i32, i32]
         L.orc_view_length.restype = i32
         L.orc_length.argtypes = [P]
@@ -127,6 +129,19 @@ class OracleDoc:
         o = np.zeros(2, dtype=np.int32)
         lib().orc_pending_counts(self.h, _p(o))
         return int(o[0]), int(o[1])
+
+    def regenerate(self, kind, cap=4096):
+        """orc_regenerate: (records as REGEN_DTYPE, text, props) or None without a group."""
+        from fluidframework_amd._native import REGEN_DTYPE
+        recs = np.zeros(cap, dtype=REGEN_DTYPE)
+        text = np.zeros(1 << 16, dtype=np.uint16)
+        props = np.zeros(1 << 16, dtype=np.uint32)
+        n = lib().orc_regenerate(self.h, int(kind), _p(recs), cap, _p(text), len(text), _p(props), len(props))
+        if n == -1:
+            return None
+        if n < 0:
+            raise RuntimeError(f"orc_regenerate failed ({n})")
+        return recs[:n], text, props
 
     def maintenance(self):
         """[SPLIT, APPEND, UNLINK] mergeTreeMaintenanceCallback counts (orc_maintenance)."""

@@ -169,3 +169,87 @@ def test_oracle_live_participant_matches_reference(oracle_lib):
         assert d.pending_counts()[1] == doc["drained"]["pending"] == 0
         assert (o["text"], o["leaves"], o["segs"].tolist(), o["seg_props"]) == \
             (exp["text"], exp["leaves"], exp["segs"], exp["seg_props"]), (name, doc["doc"])
+
+
+def _replay_live_with_reconnects(oracle_lib, doc, interner):
+    """Replay one live fixture document on the restatement event by event, reconnects
+    included: at each "R" every pending op is regenerated (orc_regenerate) and compared with
+    the reference's regeneratePendingOp output.  Returns (doc, errors)."""
+    from fluidframework_amd.live import OP_GROUP, regen_op
+    from fluidframework_amd.wire import F_ACK, F_LOCAL, Batch, DocEncoder
+    ids = {"local-0": 0}
+    ids.update({e[1]: 0 for e in doc["events"] if e[0] == "R"})
+    b = Batch(interner)
+    enc = DocEncoder(b, ids)
+    steps = []
+    me = "local-0"
+    for ev in doc["events"] + doc["drain"]:
+        lo = len(b.recs)
+        if ev[0] == "L":
+            b._msg(enc, dict(clientId="local-0", sequenceNumber=-1, referenceSequenceNumber=0,
+                             minimumSequenceNumber=0, contents=ev[1]), F_LOCAL)
+            steps.append(("L", lo, len(b.recs), ev[1]))
+        elif ev[0] == "M":
+            _, cid, seq, ref, msn, op = ev
+            b._msg(enc, dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=ref,
+                             minimumSequenceNumber=msn, type="op", contents=op), F_ACK if cid == me else 0)
+            steps.append(("M", lo, len(b.recs), cid == me))
+        else:
+            me = ev[1]
+            steps.append(("R", ev[2]))
+    b.doc_off.append(len(b.recs))
+    steps.insert(len(doc["events"]), ("X",))   # the end of the stream: the fixture's "out" state
+    a = b.arrays()
+    d = oracle_lib.OracleDoc.new(np.frombuffer(doc["seed_text"].encode("utf-16-le"), dtype="<u2"))
+    unseq, errs = [], []
+    for i, st in enumerate(steps):
+        if st[0] == "X":
+            yield d, errs
+        elif st[0] in ("L", "M"):
+            if d.apply_all(a["ops"][st[1]:st[2]], a["text"], a["props"]):
+                errs.append(f"status {d.outputs()['status']} at event {i}")
+                break
+            if st[0] == "L":
+                unseq.append(st[3])
+            elif st[3]:
+                unseq.pop(0)
+        else:
+            got = []
+            for op in unseq:
+                members = op["ops"] if op["type"] == OP_GROUP else [op]
+                out = []
+                for m in members:
+                    r = d.regenerate(m["type"])
+                    assert r is not None, "no pending group to regenerate"
+                    recs, text, props = r
+                    out += [regen_op(interner, m, rec, text, props) for rec in recs]
+                got.append(out[0] if len(out) == 1 else {"ops": out, "type": OP_GROUP})
+            if got != st[1]:
+                errs.append(f"regenerated ops differ at event {i}")
+            unseq = list(st[1])
+        if errs:
+            break
+    yield d, errs
+
+
+@pytest.mark.parametrize("name", ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep"])
+def test_oracle_live_reconnects_match_reference(oracle_lib, name):
+    """Every live fixture document, reconnects included: each regenerated op list equals the
+    reference's, and the final state (text, length, leaves, segment table, property sets,
+    delta records, localSeq, pending groups) and the drained replica equal the reference's."""
+    from fluidframework_amd.wire import Interner
+    for doc in gu.load(name)["docs"]:
+        it = Interner(synthetic=True)
+        run = _replay_live_with_reconnects(oracle_lib, doc, it)
+        d, errs = next(run)
+        assert not errs, (name, doc["doc"], errs)
+        errs = gu.compare_oracle(d.outputs(), gu.expected_live(doc, it))
+        assert d.pending_counts() == (doc["out"]["localSeq"], doc["out"]["pending"]), (name, doc["doc"])
+        assert not errs, (name, doc["doc"], errs)
+        d, errs = next(run)
+        assert not errs, (name, doc["doc"], errs)
+        o = d.outputs()
+        exp = gu.expected(dict(doc, out=dict(doc["drained"], deltas=[])), it)
+        assert d.pending_counts()[1] == doc["drained"]["pending"] == 0
+        assert (o["text"], o["leaves"], o["segs"].tolist(), o["seg_props"]) == \
+            (exp["text"], exp["leaves"], exp["segs"], exp["seg_props"]), (name, doc["doc"])
