@@ -35,7 +35,7 @@ SEG_BYTES = 40             # segA 16 + segO 8 + segB 16
 OP_BYTES = 32              # mt_op_rec
 RESULT_BYTES = 16          # per-op result record (position, length) in B_op
 PROFILE_PMC = os.path.join(REPO, "profiles", "pmc_summary.json")
-CALIBRATION = os.path.join(REPO, "profiles", "r2", "cpu_calibration.json")
+CALIBRATION = os.path.join(REPO, "profiles", "r3", "cpu_calibration.json")
 
 
 def parse():

@@ -64,7 +64,7 @@ def calibrate(name, ndocs, nops, configs):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r2", "cpu_calibration.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r3", "cpu_calibration.json")
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
     res = {"note": "one thread each, same op streams: the transpiled reference MergeTree (Client.applyMsg, "
                    "observer with the position-recording delta callback / with no callback) under Node vs "
