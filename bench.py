@@ -522,6 +522,13 @@ def run_live(args, rank, world, local_rank, dist):
                    host_cpus=os.cpu_count(),
                    sample=f"oracle/mt_oracle.c participant replay of rank-0 docs [0,{n_sample}) of the same "
                           f"batch ({sel_end} events) on {threads} host threads, {t_c:.2f} s")
+        cal = _live_calibration()
+        if cal and cal.get("ratio_port_over_reference"):
+            r = cal["ratio_port_over_reference"]
+            cpu["reference_estimate"] = dict(
+                value=round(cpu["value"] / r, 1), unit="events/s", cores=threads,
+                how=f"port value / {r} (port vs the transpiled reference participant on the same streams, one "
+                    f"thread each, in the build container; {cal['sample']})")
         sums = mt.checksums()
         oracle_sample = dict(docs_checked=n_sample,
                              mismatches=int((osums != sums[:n_sample]).sum() + (ost != status[:n_sample]).sum()))
@@ -546,12 +553,13 @@ def run_live(args, rank, world, local_rank, dist):
 def _live_calibration():
     """The reference participant's own speed on the same streams (one thread, measured in the
     build container: the reference cannot travel to the GPU box)."""
-    p = os.path.join(REPO, "profiles", "r2", "live_calibration.json")
+    p = os.path.join(REPO, "profiles", "r3", "live_calibration.json")
     if not os.path.exists(p):
         return None
     c = json.load(open(p))
     return dict(value=round(c["events_per_s"], 1), unit="events/s", cores=1, kind="reference",
-                sample=f"{c['events']} events, {os.path.relpath(p, REPO)}")
+                sample=f"{c['events']} events, {os.path.relpath(p, REPO)}",
+                ratio_port_over_reference=c.get("ratio_port_over_reference"))
 
 
 def main():
