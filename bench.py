@@ -467,7 +467,7 @@ def run_live(args, rank, world, local_rank, dist):
     n_events = int(lens.sum())
     threads = args.cpu_threads or host_cores()
     mt = MergeTreeBatch(docs, device=local_rank, seg_capacity=4096, text_capacity=1 << 15, props_capacity=4096,
-                        heap_capacity=4096, lds_seg_capacity=-1, live_client=1)
+                        heap_capacity=4096, lds_seg_capacity=args.lds_cap if args.lds_cap > 0 else -1, live_client=1)
     mt.load_initial_text(a["seed_off"], a["seed"])
     batch = mt.upload(a)
 

@@ -66,6 +66,23 @@ template <bool kLogT> struct TierLiveT {
     typedef GLB_AS v2i *H_t;
 };
 
+// Live-client documents staged in LDS: the LDS tier's storage with the live semantics; the
+// segment-group FIFOs (DocT.P), the group table and the queue stay in HBM at the same
+// segment indices, so a document that outgrows the LDS capacities spills and continues in
+// TierLiveT exactly as an observer continues in TierGlbT.
+template <bool kLogT> struct TierLiveLdsT {
+    static constexpr bool kLds = true;
+    static constexpr bool kLog = kLogT;
+    static constexpr bool kPaged = false;
+    static constexpr bool kLive = true;
+    static constexpr int kOvlBits = 32;
+    typedef uint32_t O_v;
+    typedef LDS_AS v4i *A_t;
+    typedef LDS_AS uint32_t *O_t;
+    typedef LDS_AS v4u *B_t;
+    typedef LDS_AS v2i *H_t;
+};
+
 // The paged layout (mt_paged.h): LDS-staged window and upper levels.  kPaged compiles the
 // page bookkeeping in; the flat tiers carry none of it.  kNarrow: removedClientOverlap masks
 // of short ids 1..32 in LDS (window and unsettled table: 4 bytes per segment instead of 8) --
@@ -114,7 +131,7 @@ __device__ __forceinline__ void gsync_rd() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 }
 template <class T> __device__ __forceinline__ void wsync() {
-    if constexpr (T::kLds)
+    if constexpr (T::kLds && !T::kLive)   // live: the HBM-resident group FIFOs move too
         asm volatile("" ::: "memory");
     else
         gsync();

@@ -1400,7 +1400,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         delete h;
         return nullptr;
     }
-    if (o.lds_seg_capacity >= 0 && !h->live) {
+    if (o.lds_seg_capacity >= 0) {   // live handles: TierLiveLdsT, then TierLiveT
         int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 192;
         S_l = std::min(S_l, st.S);
         h->lds.S = S_l;
@@ -1742,7 +1742,15 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     if (h->lds.S > 0) {
         // LDS tier for every document; the ones that outgrow it are flagged and replayed
         // from HBM by the second launch (whose other workgroups exit at once)
-        if (h->st.DL)
+        if (h->live && h->st.DL)
+            hipLaunchKernelGGL((k_replay<TierLiveLdsT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE),
+                               tier_lds_bytes(true, h->lds, 0), h->stream, h->st, b->ops, b->off, b->text, b->props,
+                               h->lds);
+        else if (h->live)
+            hipLaunchKernelGGL((k_replay<TierLiveLdsT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE),
+                               tier_lds_bytes(true, h->lds, 0), h->stream, h->st, b->ops, b->off, b->text, b->props,
+                               h->lds);
+        else if (h->st.DL)
             hipLaunchKernelGGL((k_replay<TierLdsT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
                                h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
         else if (h->wpg == 2)

@@ -53,9 +53,12 @@ class LiveClient:
     """One GPU document replica owned by a participant client (short id 0)."""
 
     def __init__(self, seed_text="", device=0, seg_capacity=4096, text_capacity=1 << 16, delta_log_capacity=0,
-                 interner=None):
+                 interner=None, lds_seg_capacity=-1):
+        # lds_seg_capacity >= 0: each flush stages the document in LDS (TierLiveLdsT) while it
+        # fits, continuing in the HBM tier when it outgrows it
         self.mt = MergeTreeBatch(1, device=device, seg_capacity=seg_capacity, text_capacity=text_capacity,
-                                 lds_seg_capacity=-1, delta_log_capacity=delta_log_capacity, live_client=1)
+                                 lds_seg_capacity=lds_seg_capacity, delta_log_capacity=delta_log_capacity,
+                                 live_client=1)
         units = np.frombuffer(seed_text.encode("utf-16-le"), dtype="<u2")
         self.mt.load_initial_text(np.array([0, len(units)], dtype=np.int64),
                                   units if len(units) else np.zeros(1, dtype=np.uint16))

@@ -55,11 +55,11 @@ def test_live_fixtures_are_reference_made():
 
 
 # ---------------------------------------------------------------- GPU
-def _run_doc(doc, log=True):
+def _run_doc(doc, log=True, lds=-1):
     from fluidframework_amd.live import LiveClient
     interner = Interner(synthetic=True)
     lc = LiveClient(doc["seed_text"], seg_capacity=16384, text_capacity=1 << 17,
-                    delta_log_capacity=(1 << 20) if log else 0, interner=interner)
+                    delta_log_capacity=(1 << 20) if log else 0, interner=interner, lds_seg_capacity=lds)
     lc.startOrUpdateCollaboration("local-0")
     unseq = []
     errs = []
@@ -93,12 +93,15 @@ def _run_doc(doc, log=True):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lds", [-1, 64, 192], ids=["hbm", "lds64", "lds192"])
 @pytest.mark.parametrize("name", LIVE_FIXTURES)
-def test_live_client_matches_reference(name):
+def test_live_client_matches_reference(name, lds):
+    """hbm: the flat HBM tier only; lds64 / lds192: each flush staged in LDS (TierLiveLdsT)
+    while the document fits 64 / 192 segments, continuing in the HBM tier beyond."""
     fx = gu.load(name)
     bad = []
     for doc in fx["docs"]:
-        lc, interner, errs = _run_doc(doc)
+        lc, interner, errs = _run_doc(doc, lds=lds)
         mt = lc.mt
         rows, leaves = mt.get_segments(0)
         o = dict(text=mt.get_text(0), length=mt.get_length(0), leaves=leaves, segs=rows,
@@ -225,14 +228,15 @@ def test_live_checksums_match_oracle_participant():
     for d in docs:
         b.add_live_doc(d["seed_text"], gu.live_entries(d), {"local-0": 0})
     a = b.arrays()
-    mt = MergeTreeBatch(len(docs), seg_capacity=16384, text_capacity=1 << 17, props_capacity=1 << 16,
-                        heap_capacity=4096, lds_seg_capacity=-1, live_client=1)
-    mt.load_initial_text(a["seed_off"], a["seed"])
-    mt.apply_arrays(a)
     osums, ost = pyoracle.replay_batch(a)
     assert ost.tolist() == [0] * len(docs)
-    assert mt.status().tolist() == [0] * len(docs)
-    sums = mt.checksums()
-    for f in sums.dtype.names:
-        assert sums[f].tolist() == osums[f].tolist(), f
-    mt.close()
+    for lds in (-1, 192):   # the HBM tier; LDS-staged (TierLiveLdsT) with hand-over
+        mt = MergeTreeBatch(len(docs), seg_capacity=16384, text_capacity=1 << 17, props_capacity=1 << 16,
+                            heap_capacity=4096, lds_seg_capacity=lds, live_client=1)
+        mt.load_initial_text(a["seed_off"], a["seed"])
+        mt.apply_arrays(a)
+        assert mt.status().tolist() == [0] * len(docs)
+        sums = mt.checksums()
+        for f in sums.dtype.names:
+            assert sums[f].tolist() == osums[f].tolist(), (lds, f)
+        mt.close()
