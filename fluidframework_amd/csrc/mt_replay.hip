@@ -1400,7 +1400,8 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         delete h;
         return nullptr;
     }
-    if (o.lds_seg_capacity >= 0) {   // live handles: TierLiveLdsT, then TierLiveT
+    // live handles stage in LDS (TierLiveLdsT, then TierLiveT) only when asked for explicitly
+    if (o.lds_seg_capacity > 0 || (o.lds_seg_capacity == 0 && !h->live)) {
         int S_l = o.lds_seg_capacity > 0 ? o.lds_seg_capacity : 192;
         S_l = std::min(S_l, st.S);
         h->lds.S = S_l;

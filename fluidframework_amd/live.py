@@ -54,7 +54,7 @@ class LiveClient:
 
     def __init__(self, seed_text="", device=0, seg_capacity=4096, text_capacity=1 << 16, delta_log_capacity=0,
                  interner=None, lds_seg_capacity=-1):
-        # lds_seg_capacity >= 0: each flush stages the document in LDS (TierLiveLdsT) while it
+        # lds_seg_capacity > 0: each flush stages the document in LDS (TierLiveLdsT) while it
         # fits, continuing in the HBM tier when it outgrows it
         self.mt = MergeTreeBatch(1, device=device, seg_capacity=seg_capacity, text_capacity=text_capacity,
                                  lds_seg_capacity=lds_seg_capacity, delta_log_capacity=delta_log_capacity,

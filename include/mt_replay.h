@@ -49,7 +49,8 @@ typedef struct mt_options {
     int32_t delta_log_capacity; /* int32 words of per-document delta log; 0 = hash only */
     int32_t lds_seg_capacity;   /* segments a document may hold while staged in LDS
                                    (default 192; -1 = always replay from HBM).  A document
-                                   that outgrows it is replayed from HBM transparently. */
+                                   that outgrows it is replayed from HBM transparently.
+                                   Live handles: staged only for a value > 0 (default: HBM). */
     int32_t page_capacity;      /* paged layout for documents that outgrow the LDS tier:
                                    pages (level-1 B-tree nodes, <= 64 segments each) per
                                    document; 0 = off (such documents replay from the flat
@@ -82,8 +83,9 @@ typedef struct mt_options {
        the local client (startOrUpdateCollaboration's own id, MT/client.ts:1053-1064):
        records flagged MT_F_LOCAL are its own unsequenced ops, MT_F_ACK records the sequenced
        echoes of them (ackPendingSegment), and mt_regenerate_pending rebuilds the oldest
-       pending op after a reconnect.  Live handles replay from HBM (no LDS / paged tiers); a
-       segment can be in 16 pending segment groups at once (MT_DOC_CAPACITY beyond). */
+       pending op after a reconnect.  Live handles replay from HBM, or staged in LDS while
+       they fit lds_seg_capacity > 0 (no paged tier); a segment can be in 16 pending segment
+       groups at once (MT_DOC_CAPACITY beyond). */
     int32_t live_client;
     /* live handles: segment groups (unacked ops, one per regenerated segment after a
        reconnect) a document may have outstanding (default 1024, at most 65535) */
