@@ -65,6 +65,7 @@ static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { retu
 #define MT_OSLOTS 64
 #define MT_OSLOT_FREE 0x7FFFFFFF
 #define MT_PG_SLOTS 64
+#define MT_PG_OLB 32          // ordinal characters kept per page for its leaf blocks (16 + scratch)
 // DocHdr.pad[] words used by paged documents
 #define HDR_PAGED 0           // 1: the document lives in the paged layout
 #define HDR_NPAGES 1          // pages in the directory
@@ -91,6 +92,12 @@ struct PagedRegion {
     int32_t *upage;           // [slots][UT]
     v4i *uA;
     u64 *uO;
+    // segment ordinals (segment_ordinals handles; null otherwise): each node's own ordinal
+    // character -- per page slot, per leaf block of a page (16 + 16 scratch), and per node of
+    // the upper levels by level position (level 1 = pages in directory order)
+    uint16_t *oS;             // [slots][PP][64]
+    uint16_t *oL;             // [slots][PP][32]
+    uint16_t *oU;             // [slots][MT_LV][PP]
     int32_t PP, PH, UT, slots;
 };
 // document doc's paged arrays (bslot: its slot in the big region, -1: the main set); the
@@ -106,6 +113,7 @@ struct PagedBase {
     int32_t *upage;
     v4i *uA;
     u64 *uO;
+    uint16_t *oS, *oL, *oU;   // ordinal characters (null: none)
     int32_t PP, PH, UT;
 };
 __host__ __device__ inline PagedBase paged_base(const PagedRegion &R, size_t i) {
@@ -121,6 +129,9 @@ __host__ __device__ inline PagedBase paged_base(const PagedRegion &R, size_t i) 
     b.upage = R.upage + i * (size_t)R.UT;
     b.uA = R.uA + i * (size_t)R.UT;
     b.uO = R.uO + i * (size_t)R.UT;
+    b.oS = R.oS ? R.oS + i * PP * MT_PG_SLOTS : nullptr;
+    b.oL = R.oL ? R.oL + i * PP * MT_PG_OLB : nullptr;
+    b.oU = R.oU ? R.oU + i * MT_LV * PP : nullptr;
     b.PP = R.PP;
     b.PH = R.PH;
     b.UT = R.UT;
@@ -154,12 +165,13 @@ struct DevState {
     v4i *pgUtA;
     u64 *pgUtO;
     uint16_t *pgUmap;         // [n_docs][UM] uid -> page
+    uint16_t *pgOS, *pgOL, *pgOU;   // ordinal characters of the paged layout (PagedRegion oS / oL / oU)
     int32_t PP, PH, UT, UM;
     int32_t *bslot;           // [n_docs] slot in the big region (-1: main arrays); null: no big region
     PagedRegion big;          // documents re-tiered by the growth step (larger PP / PH / UT)
     int32_t S, B, H, T, P, DL;
     int32_t DLR;              // rich delta log: segment text / properties + maintenance events
-    // segment ordinals (mt_options.segment_ordinals, flat tiers; null otherwise): every
+    // segment ordinals (mt_options.segment_ordinals; null otherwise) of flat documents: every
     // node's own ordinal character (MergeBlock.setOrdinal, MT/mergeTree.ts:347-372); a
     // node's ordinal is its ancestors' characters then its own (mt_engine.h "ordinals")
     uint16_t *ordS;           // [n_docs][S] per segment
@@ -173,8 +185,9 @@ struct DevState {
 };
 
 __host__ __device__ inline PagedRegion main_region(const DevState &st) {
-    return PagedRegion{st.pgA, st.pgO, st.pgB, st.pgMeta, st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA,
-                       st.pgUtO, st.PP, st.PH, st.UT, st.n_docs};
+    return PagedRegion{st.pgA,   st.pgO,    st.pgB,   st.pgMeta, st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage,
+                       st.pgUtA, st.pgUtO, st.pgOS, st.pgOL,   st.pgOU,  st.PP,    st.PH,    st.UT,
+                       st.n_docs};
 }
 // the paged arrays of document doc (device side: its slot from st.bslot; readers outside the
 // replay kernels, which are instantiated per region)

@@ -170,8 +170,14 @@ template <class T> struct DocT {
     int m_split, m_append, m_unlink;   // maintenance events (kept only when T::kLog)
     int dlog_rec, dlog_ovf;            // open log record header (-1: none), log overflowed
     int rich;                          // rich delta log (segments' state, maintenance events)
-    // segment ordinals (DevState.ordS / ordB; flat tiers of logging handles only): each
-    // segment's and each block's own ordinal character, in HBM
+    // paged windows (segment_ordinals): the insert callback's [uid, position, ordinal] entry
+    // is written after the op's page split (pg_op_insert), as the reference reads it once the
+    // whole insertingWalk is done; dfr_rec = its record's first word (-1: none pending)
+    int dfr_rec, dfr_uid, dfr_pos;
+    // segment ordinals (logging handles with segment_ordinals): each segment's and each
+    // block's own ordinal character, in HBM -- DevState.ordS / ordB for flat documents; for a
+    // paged window the current page's slot / leaf-block characters, for the paged upper
+    // instance the characters of levels >= 1 by level position (mt_paged.h "ordinals")
     int ord;
     int obst;                          // per-level stride of ob (st.B)
     GLB_AS uint16_t *os;               // [S]
@@ -191,6 +197,8 @@ template <class T> struct DocT {
     int pend_split;         // the page reached MaxNodesInBlock leaf blocks: split it after the op
     int pend_second;        // leaf block split while a page split was pending (-1: none)
     LDS_AS uint16_t *dir;   // upper instance: page ids in level-1 order (moved with level 1)
+    int sp_pg, sp_l, sp_r;  // upper instance, segment ordinals: the page split blk_split_up links in
+                            // at level 1 (new page id, blocks of the two halves; pg_split_page)
     // live-client documents (T::kLive): collabWindow.localSeq, the segment-group queue
     // (head id, length; MT/mergeTree.ts pendingSegments) and the current message's group
     int local_seq, g_head, g_n;
@@ -616,14 +624,18 @@ TD void mark_dirty(DocT<T> &d, int i) {
 #endif
 }
 
-// Segment ordinals are kept by the logging instantiations of the flat tiers only (the
-// replay fast path and the paged layout compile them out).
+// Segment ordinals are kept by the logging instantiations only (the replay fast path
+// compiles them out).
 TD bool ordon(DocT<T> &d) {
-    if constexpr (T::kLog && !T::kPaged)
+    if constexpr (T::kLog)
         return d.ord != 0;
     else
         return false;
 }
+// paged layout (mt_paged.h): nodeUpdateOrdinals below the upper instance's block b of level l
+// (its pages' leaf blocks and segments are in HBM), and the ordinal of a window segment
+TD void pg_ord_canon_up(DocT<T> &up, int l, int b);
+TD int pg_ord_of_win(DocT<T> &w, int i, int *codes);
 // setOrdinal's width for a block of c children (mt_engine.h "segment ordinals")
 __device__ __forceinline__ int ord_w(int c) { return 1 << (7 - min(max(c, 1), 7)); }
 // lane 0 writes one ordinal character (a global store other lanes read after gsync)
@@ -847,6 +859,13 @@ TD void blk_split_up(DocT<T> &d, int l, int b) {
             lvl(d, l)[b] = MT_HALF;
             lvl(d, l)[b + 1] = MT_HALF;
             if (l == 0) d.flg[b + 1] = MT_SCOUR_UNDEF;
+            // the paged upper instance's page split: its halves' real leaf-block counts and the
+            // new page id are in place before any re-derivation reads them (pg_ord_canon_up)
+            if (T::kPaged && ordon(d) && d.dir && l == 1) {
+                lvl(d, 1)[b] = (uint8_t)d.sp_l;
+                lvl(d, 1)[b + 1] = (uint8_t)d.sp_r;
+                d.dir[b + 1] = (uint16_t)d.sp_pg;
+            }
         }
         wsync<T>();
         if (!has_parent) {
@@ -951,6 +970,12 @@ TD GLB_AS uint16_t *ordl(DocT<T> &d, int l) { return d.ob + (size_t)l * d.obst; 
 
 // nodeUpdateOrdinals(block b of level l): every node below it gets its canonical character
 TD void ord_canon(DocT<T> &d, int l, int b) {
+    if constexpr (T::kPaged) {
+        if (d.dir) {   // the paged upper instance: levels 1 and 0 are pages in HBM
+            pg_ord_canon_up(d, l, b);
+            return;
+        }
+    }
     int lo = b, hi = b + 1;
     for (int j = l; j >= 0; j--) {
         const int c0 = blk_prefix(d, j, lo);
@@ -977,6 +1002,7 @@ TD void ord_canon_all(DocT<T> &d) { ord_canon(d, d.depth - 1, 0); }
 // the ordinal of segment i: its ancestors' characters below the root, then its own
 // (codes[0 .. depth)); returns the length
 TD int ord_of(DocT<T> &d, int i, int *codes) {
+    if constexpr (T::kPaged) return pg_ord_of_win(d, i, codes);
     const int dep = d.depth;
     gsync();
     codes[dep - 1] = uni((int)d.os[i]);
@@ -1405,8 +1431,9 @@ TD void split_seg(DocT<T> &d, int i, int q) {
     MaintExt ex{0u, 0u, 0, 0, i, i, true};
     if (ordon(d) && d.rich) {
         const v4i ai = uni4(d.A[i]);
-        ex.pos0 = obs_prefix(d, i);
-        ex.pos1 = obs_prefix(d, bstart + cntr(d, 0, b)) - (ai.z == MT_RSEQ_NONE ? ai.x - q : 0);
+        const int ob = T::kPaged ? d.obs_base : 0;   // a paged window's observer start
+        ex.pos0 = ob + obs_prefix(d, i);
+        ex.pos1 = ob + obs_prefix(d, bstart + cntr(d, 0, b)) - (ai.z == MT_RSEQ_NONE ? ai.x - q : 0);
         ex.uid0 = uni((int)(d.Bv[i].z & ~MT_MARKER_BIT));
         ex.uid1 = (uint32_t)d.next_uid;
     }
@@ -1540,7 +1567,7 @@ TD void scour_events(DocT<T> &d, v4i a, v4u b, u64 m_unlink, u64 m_app, u64 m_ke
             const int val = base_k * (((m_app >> k) & 1ull) ? 2 : 1);
             const int dex = wave_scan_incl(val) - val;
             const int bex = wave_scan_incl(base_k) - base_k;
-            const int s0 = obs_prefix(d, s);
+            const int s0 = (T::kPaged ? d.obs_base : 0) + obs_prefix(d, s);
             pos_k = s0 + __shfl(bex, start, MT_WAVE) + dex - __shfl(dex, start, MT_WAVE);
         }
         for (u64 ev = m_unlink | m_app; ev; ev &= ev - 1) {
@@ -2051,8 +2078,9 @@ TD void pack(DocT<T> &d, int l, int b) {
     }
 }
 
-// pack :1401-1453 above the leaf level only (no scour): the paged upper instance
-TD void pack_counts(DocT<T> &d, int l, int b) {
+// pack :1401-1453 above the leaf level only (no scour): the paged upper instance.  top_l /
+// top_b: the block whose subtree nodeUpdateOrdinals re-derives at the end (:1449-1450).
+TD void pack_counts(DocT<T> &d, int l, int b, int &top_l, int &top_b) {
     while (true) {
         int c0;
         const int P = blk_find(d, l + 1, b, true, c0);
@@ -2075,6 +2103,8 @@ TD void pack_counts(DocT<T> &d, int l, int b) {
             b = P;
             continue;
         }
+        top_l = l + 1;
+        top_b = P;
         return;
     }
 }
@@ -2408,7 +2438,13 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         if (d.rich) {
             wsync<T>();
             cb_log_seg(d, uni4(d.A[x]), uni4(d.Bv[x]));
-            cb_log_ext(d, uid, pos, x, false);
+            if (T::kPaged && ordon(d)) {   // after the page split (pg_op_insert)
+                d.dfr_rec = d.dlog_rec;
+                d.dfr_uid = (int)uid;
+                d.dfr_pos = pos;
+            } else {
+                cb_log_ext(d, uid, pos, x, false);
+            }
         }
     }
     cb.h = fnv_u64(cb.h, fnv_u32(fnv_u32(MT_FNV_OFF, (uint32_t)pos), (uint32_t)slen));

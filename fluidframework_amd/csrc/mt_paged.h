@@ -47,6 +47,8 @@ template <class T> struct PagedDoc {
     GLB_AS u64 *gO;
     GLB_AS v4u *gB;
     GLB_AS uint16_t *gumap;   // (the bases used only at load / store are PgCold's: fewer live SGPRs)
+    GLB_AS uint16_t *goS;     // segment ordinals (T::kLog handles with them): page slot / leaf-block
+    GLB_AS uint16_t *goL;     // characters by page id (the window's os / ob point into them)
     int doc;
     int PP, PH, UT, UM;       // LDS capacities of this launch (pages, heap, table); uid map size
     int PPh;                  // page capacity of the HBM arrays (stride; >= PP)
@@ -136,6 +138,15 @@ TD void pg_fail_cap(DocT<T> &w, int cause) {
     if (w.status == 0) w.cap_cause = cause;
     fail(w, MT_DOC_CAPACITY);
 }
+__device__ __forceinline__ PageMeta pm_load(const LDS_AS PageMeta *m) {
+    PageMeta r;
+    r.nseg = m->nseg;
+    r.nblk = m->nblk;
+    r.flg2 = m->flg2;
+    r.bc = m->bc;
+    r.obs = m->obs;
+    return r;
+}
 __device__ __forceinline__ int pm_bcnt_l(const LDS_AS PageMeta *m, int q) { return (int)((m->bc >> (4 * q)) & 15u); }
 __device__ __forceinline__ int8_t pm_flg_l(const LDS_AS PageMeta *m, int q) {
     return (int8_t)((int)((m->flg2 >> (2 * q)) & 3u) - 1);
@@ -185,6 +196,153 @@ TD int pg_cur_pos(PagedDoc<T> &pd) {
     if (pd.cur_pos < 0) pd.cur_pos = pg_pos(pd, pd.cur);
     return pd.cur_pos;
 }
+// observer position of the window page's first segment (the pages before it in the directory)
+TD int pg_obs_start(PagedDoc<T> &pd) {
+    const int pos = pg_cur_pos(pd);
+    int s = 0;
+    for (int base = 0; base < pos; base += MT_WAVE) {
+        const int q = base + lane();
+        s += q < pos ? pd.meta[pd.up.dir[q]].obs : 0;
+    }
+    return wave_sum(s);
+}
+
+// ------------------------------------------------------------------ segment ordinals
+// The flat engine's representation (mt_engine.h "segment ordinals": one character per node,
+// an ordinal is the ancestors' characters below the root then the node's own) over the paged
+// layout, in HBM: each page keeps its slots' characters (PagedDoc.goS, 64 per page) and its
+// leaf blocks' (goL), and the upper instance keeps levels >= 1 by level position (DocT.ob,
+// level 1 = pages in directory order, moved with the directory by blk_shift).  The window's
+// os / ob point at its page's arrays, so every engine step inside a page (inserts, splits,
+// leaf-block splits, scours, pack of the page's leaf blocks) writes them as for a flat
+// document; the steps that cross pages re-derive from the upper instance (pg_ord_canon_up):
+// a page split (blk_split_up of the upper instance, whose page-level link is pg_split_page's
+// sp_*), pack at level 1 (pg_pack1: the topmost parent, :1444-1450), a new root (updateRoot
+// :1909-1920) and a converted document without characters (reloadFromSegments).
+// The PagedDoc of its upper instance (the second member)
+TD PagedDoc<T> &updoc(DocT<T> &up) {
+    return *reinterpret_cast<PagedDoc<T> *>(reinterpret_cast<char *>(&up) - offsetof(PagedDoc<T>, up));
+}
+// canonical characters of page pg's leaf blocks and slots (nodeUpdateOrdinals of the page):
+// leaf block q of nb gets (q + 1) * width(nb) - 1, slot k of block q's c_q the same in c_q
+TD void pg_ord_canon_page(PagedDoc<T> &pd, int pg, bool root_leaf) {
+    const PageMeta m = pm_load(pd.meta + pg);
+    const int nb = root_leaf ? 1 : (int)m.nblk;
+    const int t = lane();
+    int q = 0, st = 0, c = root_leaf ? (int)m.nseg : pm_bcnt(m, 0);
+    while (q + 1 < nb && t >= st + c) {
+        st += c;
+        q++;
+        c = pm_bcnt(m, q);
+    }
+    if (t < (int)m.nseg) pd.goS[(size_t)pg * MT_PG_SLOTS + t] = (uint16_t)((t - st + 1) * ord_w(c) - 1);
+    if (!root_leaf && t < nb) pd.goL[(size_t)pg * MT_PG_OLB + t] = (uint16_t)((t + 1) * ord_w(nb) - 1);
+}
+TD void pg_ord_canon_up(DocT<T> &up, int l, int b) {
+    PagedDoc<T> &pd = updoc(up);
+    if (l == 0) {   // a one-level tree: the root is page dir[0]'s only leaf block
+        pg_ord_canon_page(pd, uni((int)up.dir[0]), true);
+        gsync();
+        return;
+    }
+    int lo = b, hi = b + 1;
+    for (int j = l; j >= 2; j--) {   // children of [lo, hi) at level j: nodes of level j - 1
+        const int c0 = blk_prefix(up, j, lo);
+        int carry = c0;
+        GLB_AS uint16_t *dst = up.ob + (size_t)(j - 1) * up.obst;
+        const LDS_AS uint8_t *cnt = lvl(up, j);
+        for (int base = lo; base < hi; base += MT_WAVE) {
+            const int p = base + lane();
+            const int c = p < hi ? (int)cnt[p] : 0;
+            const int inc = wave_scan_incl(c);
+            const int first = carry + inc - c;
+            const int w = ord_w(c);
+            for (int q = 0; q < c; q++) dst[first + q] = (uint16_t)((q + 1) * w - 1);
+            carry += bcast(inc, MT_WAVE - 1);
+        }
+        lo = c0;
+        hi = carry;
+    }
+    for (int q = lo; q < hi; q++) pg_ord_canon_page(pd, uni((int)up.dir[q]), false);   // level-1 nodes
+    gsync();
+}
+// The ordinal of slot i of page pg (codes[0 .. depth)): window counts for the current page,
+// the page metadata otherwise.
+TD int pg_ord_of_page(PagedDoc<T> &pd, int pg, int i, int *codes) {
+    DocT<T> &w = pd.w;
+    DocT<T> &up = pd.up;
+    gsync();
+    // a root leaf block split inside this step: the page is the root (pg_win_sync sets up.depth)
+    const int D = (up.depth == 1 && pg == pd.cur && w.depth == 2) ? 2 : up.depth;
+    codes[D - 1] = uni((int)pd.goS[(size_t)pg * MT_PG_SLOTS + i]);
+    if (D == 1) return 1;
+    int q;
+    if (pg == pd.cur) {
+        int st;
+        q = blk_find(w, 0, i, true, st);
+    } else {
+        const PageMeta m = pm_load(pd.meta + pg);
+        int st = 0;
+        q = 0;
+        while (q + 1 < (int)m.nblk && i >= st + pm_bcnt(m, q)) st += pm_bcnt(m, q++);
+        q = uni(q);
+    }
+    if (q < 0) return -1;
+    codes[D - 2] = uni((int)pd.goL[(size_t)pg * MT_PG_OLB + q]);
+    if (D == 2) return 2;
+    int x = pg == pd.cur ? pg_cur_pos(pd) : pg_pos(pd, pg);
+    if (x < 0) return -1;
+    codes[D - 3] = uni((int)up.ob[(size_t)up.obst + x]);
+    for (int l = 2; l + 1 < D; l++) {
+        int st;
+        const int b = blk_find(up, l, x, true, st);
+        if (b < 0) return -1;
+        codes[D - 2 - l] = uni((int)up.ob[(size_t)l * up.obst + b]);
+        x = b;
+    }
+    return D;
+}
+TD int pg_ord_of_win(DocT<T> &w, int i, int *codes) { return pg_ord_of_page(pdoc(w), pdoc(w).cur, i, codes); }
+// The insert callback's [uid, position, ordinal] entry once the op's page split is done
+// (op_insert deferred it: DocT.dfr_*); the segment is in the window or in the new page.
+TD void pg_log_deferred(PagedDoc<T> &pd) {
+    if constexpr (T::kLog) {
+        DocT<T> &w = pd.w;
+        const int rec = w.dfr_rec;
+        w.dfr_rec = -1;
+        const uint32_t uid = (uint32_t)w.dfr_uid;
+        int pg = pd.cur, i = find_uid(w, uid);
+        if (i < 0 && uid < (uint32_t)pd.UM) {
+            gsync();
+            pg = uni((int)pd.gumap[uid]);
+            const bool hit = lane() < (int)pd.meta[pg].nseg &&
+                             (pd.gB[(size_t)pg * MT_PG_SLOTS + lane()].z & ~MT_MARKER_BIT) == uid;
+            const u64 m = ballot(hit);
+            i = m ? first_lane(m) : -1;
+        }
+        int codes[MT_LV + 1];
+        const int olen = i >= 0 ? pg_ord_of_page(pd, pg, i, codes) : -1;
+        if (olen < 0) {
+            FAIL_INTERNAL(w);
+            return;
+        }
+        if (!w.dlog || w.dlog_n + 3 + olen > w.DL_cap) {   // the whole record goes (cb_room)
+            if (w.dlog) {
+                w.dlog_n = rec;
+                w.dlog_ovf = 1;
+            }
+            return;
+        }
+        GLB_AS int32_t *o = w.dlog + w.dlog_n;
+        if (lane() == 0) {
+            o[0] = (int32_t)uid;
+            o[1] = w.dfr_pos;
+            o[2] = olen;
+            for (int q = 0; q < olen; q++) o[3 + q] = codes[q];
+        }
+        w.dlog_n += 3 + olen;
+    }
+}
 
 // ------------------------------------------------------------------ window load / store
 TD void pg_win_load_impl(PagedDoc<T> &pd, int pg);
@@ -231,6 +389,10 @@ TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const 
     }
     w.n = n;
     w.depth = pd.up.depth == 1 ? 1 : 2;
+    if (ordon(w)) {   // the page's own ordinal characters (its slots, its leaf blocks)
+        w.os = pd.goS + (size_t)pg * MT_PG_SLOTS;
+        w.ob = pd.goL + (size_t)pg * MT_PG_OLB;
+    }
     w.pend_split = 0;
     w.pend_second = -1;
     w.dlo = MT_PG_SLOTS;
@@ -390,6 +552,21 @@ TD void pg_split_page(PagedDoc<T> &pd) {
             pd.pvl[np] = dl;
             pd.pvl[pd.cur] -= dl;
         }
+        wsync<T>();
+    }
+    if (ordon(w)) {
+        // segment ordinals: blk_split_up re-derives the split halves' subtrees from the page
+        // metadata, so this page's holds its first sp blocks already, and level 1 links the
+        // new page in with the real counts (blk_split_up: sp_*)
+        const bool vb = lane() < sp;
+        pm_set_blocks(pd, pd.cur, lane(), vb, vb ? lvl(w, 0)[lane()] : 0, vb ? w.flg[lane()] : 0);
+        if (lane() == 0) {
+            pd.meta[pd.cur].nseg = (uint8_t)s0;
+            pd.meta[pd.cur].nblk = (uint8_t)sp;
+        }
+        up.sp_pg = np;
+        up.sp_l = sp;
+        up.sp_r = nbk - sp;
         wsync<T>();
     }
     // level 1: new node after cur (blk_split_up grows the parents / the root)
@@ -735,11 +912,14 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
         if (lane() == 0) up.dir[c0 + m] = (uint16_t)newp[m];
     if (lane() == 0) lvl(up, 2)[P] = (uint8_t)k;
     wsync<T>();
-    if (k < MT_HALF && 3 < up.depth) pack_counts(up, 2, P);   // counts only above level 1
+    int top_l = 2, top_b = P;
+    if (k < MT_HALF && 3 < up.depth) pack_counts(up, 2, P, top_l, top_b);   // counts only above level 1
     if (up.status) {
         if (w.status == 0) w.cap_cause = up.cap_cause;
         fail(w, MT_DOC_INTERNAL);
+        return;
     }
+    if (ordon(w)) ord_canon(up, top_l, top_b);   // nodeUpdateOrdinals(the topmost parent) :1449-1450
 }
 
 // ------------------------------------------------------------------ zamboni (paged)
@@ -791,6 +971,7 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         const int f = flgr(w, b);
         const int old = cntr(w, 0, b);
         if (f == 0) continue;
+        if (ordon(w) && w.rich) w.obs_base = pg_obs_start(pd);   // scour event positions
         PG_T0(2)
         const int kept = scour_range(w, bstart, b, 1);
         PG_T1(2)
@@ -803,6 +984,8 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
             pack(w, 0, b);   // regroups this page's leaf blocks (stops at the window top)
             if (w.status) return;
             pk = nbr(w, 0) < MT_HALF && pd.up.depth > 2;
+        } else if (kept < old && ordon(w)) {
+            ord_canon(w, 0, b);   // nodeUpdateOrdinals(block) :1500-1501
         }
         pg_win_sync(pd);
         if (w.status) return;
@@ -814,14 +997,34 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
 }
 
 // ------------------------------------------------------------------ ops (paged)
+TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c);
+TD void pg_log_deferred(PagedDoc<T> &pd);
 TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin, const GLB_AS uint32_t *pin) {
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
     const int slen = (op.flags & MT_F_MARKER) ? 1 : op.pos2;
+    if (ordon(w)) {
+        // insertSegments splits at the position in a walk of its own first
+        // (ensureIntervalBoundary, MT/mergeTree.ts:2004): a page split it causes re-derives
+        // ordinals before the new segment takes its character
+        pg_boundary(pd, op.pos1, op.ref_seq, op_cli(op));
+        if (w.status) return;
+    }
     pg_views_cached(pd, op.ref_seq, op_cli(op));
     int start;
     int ostart;
-    const int pos = pg_find(pd, op.pos1, false, start, ostart);
+    int pos = pg_find(pd, op.pos1, false, start, ostart);
+    if constexpr (T::kLog) {
+        // a zero-length insert past the end logs its (never linked) segment like the flat
+        // engine: the last page's window runs it
+        const int np = nbr(pd.up, 1);
+        if (pos < 0 && slen == 0 && np > 0 && !(op.flags & MT_F_LOAD)) {
+            pos = np - 1;
+            const int lp = uni((int)pd.up.dir[pos]);
+            start -= uni(pd.pvl[lp]);
+            ostart -= uni(pd.meta[lp].obs);
+        }
+    }
     if (pos < 0) {
         if (slen == 0) {   // boundary only; nothing splits past the end
             if (op.flags & MT_F_LOAD) return;
@@ -844,6 +1047,7 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     op_insert(w, rel, tin, pin);
     if (w.status) return;
     pg_win_sync(pd);
+    if (T::kLog && w.dfr_rec >= 0) pg_log_deferred(pd);
 }
 
 TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
@@ -1199,6 +1403,8 @@ TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
     pd.gO = (GLB_AS u64 *)b.O;
     pd.gB = (GLB_AS v4u *)b.B;
     pd.gumap = (GLB_AS uint16_t *)(st.pgUmap + (size_t)doc * st.UM);
+    pd.goS = (GLB_AS uint16_t *)b.oS;
+    pd.goL = (GLB_AS uint16_t *)b.oL;
     pd.PPh = b.PP;
     pd.UM = st.UM;
     pd.doc = doc;
@@ -1286,6 +1492,17 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
         w.dlog_rec = -1;
     }
     w.text_gcs = w.props_gcs = w.cap_cause = 0;
+    w.ord = 0;
+    w.obst = 0;
+    w.os = nullptr;
+    w.ob = nullptr;
+    w.dfr_rec = -1;
+    if constexpr (T::kLog) {
+        if (pd.goS) {   // segment ordinals: the window's pointers follow its page (pg_win_place)
+            w.ord = 1;
+            w.obst = 16;   // level 1 of a window (the page itself) lands in the scratch half of goL
+        }
+    }
     w.dlo = MT_PG_SLOTS;
     w.paged = 1;
     w.obs_base = 0;
@@ -1299,6 +1516,10 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     up.dir = (LDS_AS uint16_t *)(smem + L.offDir);
     up.B_cap = pc.PP;
     up.status = 0;
+    if (ordon(w)) {   // levels >= 1 by level position (PagedBase.oU)
+        up.ob = (GLB_AS uint16_t *)tier_paged<T::kBig>(st, doc).oU;
+        up.obst = pd.PPh;
+    }
     pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
     pd.pvl = (LDS_AS int *)(smem + L.offPvl);
     pd.upage = (LDS_AS uint16_t *)(smem + L.offUpage);
@@ -1461,6 +1682,7 @@ struct FlatSrc {
     GLB_AS const int8_t *flg;
     GLB_AS const v2i *heap;
     size_t B;
+    GLB_AS const uint16_t *os, *ob;   // ordinal characters (DevState.ordS / ordB; null: none kept)
 };
 __device__ __forceinline__ FlatSrc flat_src(const DevState &st, int doc) {
     const size_t S = st.S, B = st.B;
@@ -1472,6 +1694,8 @@ __device__ __forceinline__ FlatSrc flat_src(const DevState &st, int doc) {
     f.flg = (GLB_AS const int8_t *)(st.flg + doc * B);
     f.heap = (GLB_AS const v2i *)(st.heap + doc * (size_t)(st.H + 1));
     f.B = B;
+    f.os = st.ordS ? (GLB_AS const uint16_t *)(st.ordS + doc * S) : nullptr;
+    f.ob = st.ordS ? (GLB_AS const uint16_t *)(st.ordB + doc * (size_t)MT_LV * B) : nullptr;
     return f;
 }
 
@@ -1494,6 +1718,12 @@ TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
     const int np = depth == 1 ? 1 : h.n_blk[1];
     if (np + 8 > pd.PP || h.heap_n > pd.PH) {
         pg_fail_cap(w, np + 8 > pd.PP ? 7 : 3);
+        return false;
+    }
+    // the packed table stores seq / removedSeq as 16-bit offsets from currentSeq - 32000: a
+    // wider collab window goes to the next tier (as pg_load refuses it)
+    if (T::kPacked && w.cur_seq - w.min_seq > 30000) {
+        pg_fail_cap(w, 8);
         return false;
     }
     up.depth = depth;
@@ -1542,6 +1772,11 @@ TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
             lvl(up, 1)[j] = (uint8_t)nbk;
         }
         w.n = ns;
+        if (ordon(w) && src.os) {   // the flat document's characters: slots, leaf blocks, the page
+            if (i < ns) pd.goS[(size_t)j * MT_PG_SLOTS + i] = src.os[s + i];
+            if (i < nbk) pd.goL[(size_t)j * MT_PG_OLB + i] = src.ob[lb + i];
+            if (i == 0) up.ob[(size_t)up.obst + j] = src.ob[B + j];
+        }
         wsync<T>();
         pg_table_add(pd, 0, ns, j);
         if (w.status) return false;
@@ -1552,6 +1787,15 @@ TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
     pg_mark_free(pd);
     pd.cur = -1;
     pd.wgrow = pd.opbound = 0;
+    if (ordon(w)) {
+        if (src.os) {   // levels >= 2 keep their positions
+            for (int l = 2; l < depth; l++)
+                for (int b = lane(); b < h.n_blk[l]; b += MT_WAVE) up.ob[(size_t)l * up.obst + b] = src.ob[l * B + b];
+            gsync();
+        } else {   // a loaded summary: reloadFromSegments ends with nodeUpdateOrdinals(root) (:1273-1276)
+            ord_canon_all(up);
+        }
+    }
     // the flat tiers number ids without bound: compact them for the uid -> page map
     if (w.next_uid + 4 > pd.UM) pg_renumber(pd);
     return w.status == 0;

@@ -848,6 +848,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_convert(DevState st, LoadScrat
     src.flg = (GLB_AS const int8_t *)(sc.flg + sc.off[2 * r + 1]);
     src.heap = nullptr;   // a fresh collaboration: heap_n == 0
     src.B = (size_t)w.hp->n_blk[0];
+    src.os = src.ob = nullptr;   // canonical ordinals (pg_convert re-derives them)
     if (w.status == 0 && pg_convert(pd, src)) {
         pg_store(pd, st);
     } else if (lane() == 0) {
@@ -1288,6 +1289,11 @@ struct mt_handle {
     int max_cli = 0;                        // largest |short client id| any batch / load / generation used
                                             // (<= 127: the tight tier may pack its table, PagedCaps.packed)
     uint32_t grown_last = 0, grow_rounds_last = 0;
+    // remote views a client can still hold (segment read-outs): per document, the largest refSeq
+    // of each short client's applied messages, {client, refSeq} sorted by client; a generated
+    // batch's documents are untracked (their writers' views are refused)
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> lastref;
+    std::vector<uint8_t> untracked;
 };
 struct mt_batch {
     mt_handle *owner = nullptr;   // the handle whose growth step still needs this batch
@@ -1298,6 +1304,11 @@ struct mt_batch {
     mt_op_rec *ops = nullptr;
     uint16_t *text = nullptr;
     uint32_t *props = nullptr;
+    // per document, the largest refSeq of each client's messages ({client, refSeq} sorted by
+    // client, [lr_off[d], lr_off[d + 1])); generated: the batch came from mt_generate
+    std::vector<int64_t> lr_off;
+    std::vector<std::pair<int32_t, int32_t>> lr;
+    bool generated = false;
 };
 
 #define HIPCHK(h, x)                                                               \
@@ -1390,7 +1401,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     st.DL = o.delta_log_capacity > 0 ? o.delta_log_capacity : 0;
     st.DLR = st.DL > 0 && o.delta_log_mode == 1 ? 1 : 0;
     h->ordinals = o.segment_ordinals != 0;
-    if (h->ordinals && (!st.DLR || o.page_capacity > 0)) {   // needs the rich log and the flat tiers
+    if (h->ordinals && !st.DLR) {   // ordinals ride on the rich log
         delete h;
         return nullptr;
     }
@@ -1441,6 +1452,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
                                 (const void *)k_replay_paged<TierPagedT<false, true>>,
                                 (const void *)k_generate_paged<TierPagedT<false, true>>,
                                 (const void *)k_load_convert<TierPagedT<false>>,
+                                (const void *)k_load_convert<TierPagedT<true>>,
                                 (const void *)k_replay_paged<TierPagedT<true, false, false, true>>,
                                 (const void *)k_replay_paged<TierPagedT<false, false, false, true>>};
             for (const void *k : ks)
@@ -1510,6 +1522,11 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         alloc((void **)&st.pgUtA, N * (size_t)st.UT * sizeof(int4));
         alloc((void **)&st.pgUtO, N * (size_t)st.UT * sizeof(u64));
         alloc((void **)&st.pgUmap, N * (size_t)st.UM * sizeof(uint16_t));
+        if (h->ordinals) {
+            alloc((void **)&st.pgOS, slots * sizeof(uint16_t));
+            alloc((void **)&st.pgOL, N * (size_t)st.PP * MT_PG_OLB * sizeof(uint16_t));
+            alloc((void **)&st.pgOU, N * (size_t)MT_LV * st.PP * sizeof(uint16_t));
+        }
     }
     if (!ok || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
@@ -1525,7 +1542,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
 }
 
 static void free_region(PagedRegion &R) {
-    void *ps[] = {R.A, R.O, R.B, R.meta, R.dir, R.cnt, R.heap, R.upage, R.uA, R.uO};
+    void *ps[] = {R.A, R.O, R.B, R.meta, R.dir, R.cnt, R.heap, R.upage, R.uA, R.uO, R.oS, R.oL, R.oU};
     for (void *p : ps)
         if (p) hipFree(p);
     R = PagedRegion{};
@@ -1541,7 +1558,7 @@ void mt_destroy(mt_handle *h) {
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
                   st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot,
-                  st.live, st.grp, st.segP, st.ordS, st.ordB};
+                  st.live, st.grp, st.segP, st.ordS, st.ordB, st.pgOS, st.pgOL, st.pgOU};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -1634,6 +1651,7 @@ int mt_reset(mt_handle *h) {
         h->n_big = 0;
     }
     if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
+    untrack_views(h, 0, h->n_docs);
     hipLaunchKernelGGL(k_init, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, h->d_seed_off, h->d_seed);
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -1657,6 +1675,20 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
     for (uint64_t i = 0; i < n_ops; i++) h->max_cli = std::max(h->max_cli, std::abs((int)(int16_t)ops[i].client));
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *b = new mt_batch();
+    // each client's latest refSeq per document (summary-load records are no client's messages)
+    b->lr_off.assign(h->n_docs + 1, 0);
+    {
+        std::vector<std::pair<int32_t, int32_t>> tmp;
+        for (uint32_t d = 0; d < h->n_docs; d++) {
+            tmp.clear();
+            for (int64_t k = doc_op_off[d]; k < doc_op_off[d + 1]; k++)
+                if (!(ops[k].flags & MT_F_LOAD)) tmp.emplace_back((int32_t)(int16_t)ops[k].client, ops[k].ref_seq);
+            std::sort(tmp.begin(), tmp.end());
+            for (size_t i = 0; i < tmp.size(); i++)
+                if (i + 1 == tmp.size() || tmp[i + 1].first != tmp[i].first) b->lr.push_back(tmp[i]);
+            b->lr_off[d + 1] = (int64_t)b->lr.size();
+        }
+    }
     b->device = h->device;
     b->n_docs = h->n_docs;
     b->n_ops = n_ops;
@@ -1731,12 +1763,41 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     return 0;
 }
 
+// folds a batch's latest refSeq per client into the handle's (segment read-outs)
+static void track_views(mt_handle *h, const mt_batch *b) {
+    if (h->lastref.size() != h->n_docs) h->lastref.assign(h->n_docs, {});
+    if (h->untracked.size() != h->n_docs) h->untracked.assign(h->n_docs, 0);
+    if (b->generated) {
+        std::fill(h->untracked.begin(), h->untracked.end(), 1);
+        return;
+    }
+    if (b->lr_off.size() != (size_t)h->n_docs + 1) return;
+    for (uint32_t d = 0; d < h->n_docs; d++) {
+        auto &v = h->lastref[d];
+        for (int64_t i = b->lr_off[d]; i < b->lr_off[d + 1]; i++) {
+            const auto &e = b->lr[i];
+            auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(e.first, INT32_MIN));
+            if (it != v.end() && it->first == e.first)
+                it->second = std::max(it->second, e.second);
+            else
+                v.insert(it, e);
+        }
+    }
+}
+static void untrack_views(mt_handle *h, uint32_t lo, uint32_t n) {
+    if (h->lastref.size() == h->n_docs)
+        for (uint32_t d = lo; d < lo + n; d++) h->lastref[d].clear();
+    if (h->untracked.size() == h->n_docs)
+        for (uint32_t d = lo; d < lo + n; d++) h->untracked[d] = 0;
+}
+
 int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     if (!h || !b || b->n_docs != h->n_docs) return MT_E_INVALID;
     if (h->pending) {   // the previous batch's growth step runs before anything else
         const int rc = mt_settle(h);
         if (rc) return rc;
     }
+    track_views(h, b);
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
@@ -1873,6 +1934,12 @@ __global__ void __launch_bounds__(MT_WAVE) k_migrate_paged(DevState st, PagedReg
         d.uA[i] = s.uA[i];
         d.uO[i] = s.uO[i];
     }
+    if (s.oS && d.oS) {   // segment ordinals: per page (same page ids), levels by position
+        for (size_t i = lane(); i < ns; i += MT_WAVE) d.oS[i] = s.oS[i];
+        for (size_t i = lane(); i < (size_t)s.PP * MT_PG_OLB; i += MT_WAVE) d.oL[i] = s.oL[i];
+        for (int l = 0; l < MT_LV; l++)
+            for (int b = lane(); b < s.PP; b += MT_WAVE) d.oU[(size_t)l * d.PP + b] = s.oU[(size_t)l * s.PP + b];
+    }
 }
 // documents the growth step cannot serve (out of device memory) fail as before the step existed
 __global__ void k_fail_grow(DevState st) {
@@ -1885,7 +1952,7 @@ __global__ void k_fail_grow(DevState st) {
     }
 }
 
-static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c) {
+static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c, bool ordinals) {
     R = PagedRegion{};
     R.PP = c.PP;
     R.PH = c.PH;
@@ -1902,6 +1969,10 @@ static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c) {
               hipMalloc(&R.upage, n * (size_t)c.UT * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&R.uA, n * (size_t)c.UT * sizeof(int4)) == hipSuccess &&
               hipMalloc(&R.uO, n * (size_t)c.UT * sizeof(u64)) == hipSuccess;
+    if (ok && ordinals)
+        ok = hipMalloc(&R.oS, pages * MT_PG_SLOTS * sizeof(uint16_t)) == hipSuccess &&
+             hipMalloc(&R.oL, pages * MT_PG_OLB * sizeof(uint16_t)) == hipSuccess &&
+             hipMalloc(&R.oU, pages * MT_LV * sizeof(uint16_t)) == hipSuccess;
     if (!ok) free_region(R);
     return ok;
 }
@@ -1929,7 +2000,7 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
             slots++;
         }
     PagedRegion R;
-    if (!alloc_region(R, std::max(slots, 1), c)) {
+    if (!alloc_region(R, std::max(slots, 1), c, h->ordinals)) {
         (void)hipGetLastError();
         h->err = "growth step: device allocation of the big region failed";
         return MT_E_NOMEM;
@@ -2347,14 +2418,19 @@ int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
         HIPCHK(h, hipMemsetAsync(h->st.dlog + (size_t)s->doc_lo * h->st.DL, 0, (size_t)s->n_docs * h->st.DL * 4,
                                  h->stream));
     HIPCHK(h, hipEventRecord(h->ev_load, h->stream));
+    untrack_views(h, s->doc_lo, s->n_docs);
     hipLaunchKernelGGL(k_load_header, dim3(s->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, s->off, s->nh, s->segs,
                        s->text, s->props, s->min_seq, s->cur_seq, s->sc, (int)s->doc_lo);
     HIPCHK(h, hipGetLastError());
     if (s->any_big) {
         const PagedCaps &pc = h->pg_full;
         const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, 8).total;
-        hipLaunchKernelGGL(k_load_convert<TierPagedT<false>>, dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
-                           s->sc, pc, (int)s->doc_lo);
+        if (h->ordinals)   // canonical ordinals for the paged documents (reloadFromSegments)
+            hipLaunchKernelGGL(k_load_convert<TierPagedT<true>>, dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                               s->sc, pc, (int)s->doc_lo);
+        else
+            hipLaunchKernelGGL(k_load_convert<TierPagedT<false>>, dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+                               s->sc, pc, (int)s->doc_lo);
         HIPCHK(h, hipGetLastError());
     }
     if (s->body) return mt_batch_apply_async(h, s->body);
@@ -2642,6 +2718,10 @@ struct HostDoc {
     std::vector<uint8_t> cnt;
     std::vector<uint16_t> text;
     std::vector<uint32_t> props;
+    // paged documents: each row's page id, slot and directory position, and the page metadata
+    std::vector<int32_t> rpage, rslot, rpos;
+    std::vector<PageMeta> pmeta;
+    int32_t oslot[2 * MT_OSLOTS];   // overlap slots {client, last seq}
 };
 // document doc's paged arrays, host side (the growth step's slot mirror)
 static PagedBase host_paged(const mt_handle *h, uint32_t doc) {
@@ -2654,6 +2734,7 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
     SETTLE(h);
     const DevState &st = h->st;
     HIPCHK(h, hipMemcpy(&hd.hdr, st.hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(hd.oslot, st.oslot + (size_t)doc * 2 * MT_OSLOTS, sizeof(hd.oslot), hipMemcpyDeviceToHost));
     if (hd.hdr.pad[HDR_PAGED]) {
         // paged layout: concatenate the pages in directory order; leaf-block counts from
         // the page metadata
@@ -2674,6 +2755,9 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
         hd.O.clear();
         hd.B.clear();
         hd.cnt.clear();
+        hd.rpage.clear();
+        hd.rslot.clear();
+        hd.rpos.clear();
         for (int q = 0; q < np; q++) {
             const PageMeta &m = meta[dir[q]];
             const size_t b0 = (size_t)dir[q] * MT_PG_SLOTS;
@@ -2681,9 +2765,13 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
                 hd.A.push_back(pA[b0 + i]);
                 hd.O.push_back(pO[b0 + i]);
                 hd.B.push_back(pB[b0 + i]);
+                hd.rpage.push_back(dir[q]);
+                hd.rslot.push_back(i);
+                hd.rpos.push_back(q);
             }
             for (int k = 0; k < m.nblk; k++) hd.cnt.push_back((uint8_t)pm_bcnt(m, k));
         }
+        hd.pmeta = std::move(meta);
         hd.hdr.n_seg = (int)hd.A.size();
         hd.hdr.n_blk[0] = (int)hd.cnt.size();
         hd.A.resize(std::max<size_t>(hd.A.size(), 1));
@@ -2857,10 +2945,23 @@ static int host_view_setup(mt_handle *h, uint32_t doc, const HostDoc &hd, int32_
         h->err = "remote view: refSeq outside the collab window [minSeq, currentSeq]";
         return MT_E_INVALID;
     }
-    int32_t os[2 * MT_OSLOTS];
-    HIPCHK(h, hipMemcpy(os, h->st.oslot + (size_t)doc * 2 * MT_OSLOTS, sizeof(os), hipMemcpyDeviceToHost));
+    // a view below the client's latest refSeq: the reference answers from partial lengths
+    // that need not add up to its leaves' lengths (MT/partialLengths.ts:455-486) -- refused
+    if (doc < h->untracked.size() && h->untracked[doc]) {
+        h->err = "remote view: the document replayed a generated batch (its clients' refSeqs are not tracked)";
+        return MT_E_STALE_VIEW;
+    }
+    if (doc < h->lastref.size()) {
+        const auto &v = h->lastref[doc];
+        auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(client, INT32_MIN));
+        if (it != v.end() && it->first == client && ref_seq < it->second) {
+            h->err = "remote view: refSeq " + std::to_string(ref_seq) + " is below client " + std::to_string(client) +
+                     "'s latest refSeq " + std::to_string(it->second) + " (a stale view)";
+            return MT_E_STALE_VIEW;
+        }
+    }
     for (int i = 0; i < MT_OSLOTS; i++)
-        if (os[2 * i] == client) {
+        if (hd.oslot[2 * i] == client) {
             v.cs = i + 1;
             break;
         }
@@ -2918,6 +3019,41 @@ static int host_seg_info(mt_handle *h, uint32_t doc, const HostDoc &hd, int i, m
             x = b_;
         }
         out->ordinal_len = dep;
+    } else if (h->ordinals && h->st.pgOS) {
+        // paged: the slot's character, its leaf block's (page metadata), then the upper levels'
+        // by position (level 1: the page's directory position; mt_paged.h "segment ordinals")
+        const PagedBase pb = host_paged(h, doc);
+        const size_t PP = pb.PP;
+        const int pg = hd.rpage[i], slot = hd.rslot[i], dep = hd.hdr.depth;
+        uint16_t code = 0;
+        HIPCHK(h, hipMemcpy(&code, pb.oS + (size_t)pg * MT_PG_SLOTS + slot, 2, hipMemcpyDeviceToHost));
+        out->ordinal[dep - 1] = code;
+        if (dep >= 2) {
+            const PageMeta &m = hd.pmeta[pg];
+            int q = 0, st = 0;
+            while (q + 1 < m.nblk && slot >= st + pm_bcnt(m, q)) st += pm_bcnt(m, q++);
+            HIPCHK(h, hipMemcpy(&code, pb.oL + (size_t)pg * MT_PG_OLB + q, 2, hipMemcpyDeviceToHost));
+            out->ordinal[dep - 2] = code;
+        }
+        if (dep >= 3) {
+            std::vector<uint16_t> ou((size_t)MT_LV * PP);
+            std::vector<uint8_t> cn((size_t)MT_LV * PP);
+            HIPCHK(h, hipMemcpy(ou.data(), pb.oU, ou.size() * 2, hipMemcpyDeviceToHost));
+            HIPCHK(h, hipMemcpy(cn.data(), pb.cnt, cn.size(), hipMemcpyDeviceToHost));
+            int x = hd.rpos[i];
+            out->ordinal[dep - 3] = ou[PP + x];
+            for (int l = 2; l + 1 < dep; l++) {
+                int b_ = 0, end = 0;
+                while (b_ < hd.hdr.n_blk[l]) {
+                    end += cn[(size_t)l * PP + b_];
+                    if (end > x) break;
+                    b_++;
+                }
+                out->ordinal[dep - 2 - l] = ou[(size_t)l * PP + b_];
+                x = b_;
+            }
+        }
+        out->ordinal_len = dep;
     }
     return 0;
 }
@@ -2971,15 +3107,30 @@ int mt_get_segment_by_uid(mt_handle *h, uint32_t doc, uint32_t uid, int32_t ref_
 int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const int32_t *ref_seq,
                         const int32_t *client, int32_t *out) {
     if (!h || (n && (!docs || !ref_seq || !client || !out))) return MT_E_INVALID;
+    HostDoc hd;
+    int64_t have = -1;   // the document fetched last (queries of one document fetch it once)
+    int stale = 0;
+    std::string stale_err;
     for (uint32_t q = 0; q < n; q++) {
-        HostDoc hd;
-        int rc = fetch_doc(h, docs[q], hd, false, false);
-        if (rc) return rc;
+        int rc;
+        if ((int64_t)docs[q] != have) {
+            if ((rc = fetch_doc(h, docs[q], hd, false, false))) return rc;
+            have = docs[q];
+        }
         HostView v;
-        if ((rc = host_view_setup(h, docs[q], hd, ref_seq[q], client[q], v))) return rc;
+        if ((rc = host_view_setup(h, docs[q], hd, ref_seq[q], client[q], v))) {
+            if (rc != MT_E_STALE_VIEW) return rc;
+            out[q] = -1;   // refused; the others are answered
+            if (!stale++) stale_err = h->err;
+            continue;
+        }
         int len = 0;
         for (int i = 0; i < hd.hdr.n_seg; i++) len += host_view_len(hd, v, i);
         out[q] = len;
+    }
+    if (stale) {
+        h->err = std::to_string(stale) + " stale view(s) refused (length -1), first: " + stale_err;
+        return MT_E_STALE_VIEW;
     }
     return 0;
 }

@@ -101,9 +101,9 @@ class GpuMergeTreeBatch {
             options = Object.assign({}, options, { deltaLogMode: 1 });
         }
         this.rich = !!options.deltaLogCapacity && options.deltaLogMode === 1;
-        // event handles keep segment ordinals (SequenceDeltaEvent orders ranges by them); the
-        // paged layout keeps none
-        if (this.rich && !options.pageCapacity && options.segmentOrdinals === undefined) {
+        // event handles keep segment ordinals (SequenceDeltaEvent orders ranges by them), in
+        // the flat tiers and the paged layout alike
+        if (this.rich && options.segmentOrdinals === undefined) {
             options = Object.assign({}, options, { segmentOrdinals: 1 });
         }
         this.ordinals = !!options.segmentOrdinals;

@@ -458,12 +458,13 @@ function replayEventsDoc(log) {
 }
 
 // Read-outs of the final replica (MT/mergeTree.ts:1610-1667): MergeTree.getLength(refSeq,
-// clientId) and getContainingSegment(pos, refSeq, clientId) for the observer's view and for
-// writers' views, and getPosition of the found segment in that view.  A writer's view is one
-// it can still hold: refSeq at or above the refSeq of its latest message (below it the
-// reference's partial lengths no longer add up to its segments' lengths -- measured: every
-// mismatch between getLength and the sum of nodeLength over the leaves was such a view).
-// Segments are identified by their observer position and contents.
+// clientId) and getContainingSegment(pos, refSeq, clientId) in the observer's view and in every
+// writer's view the collab window holds (refSeq in [minSeq, currentSeq], every writer), and
+// getPosition of the found segment in that view.  A writer's view below the refSeq of its
+// latest message is one the client can no longer hold ("stale", flag 1): there the reference
+// answers from partial lengths that need not add up to its own leaves' nodeLength (each length
+// entry also records that sum), and the replay backend refuses the query.  Segments are
+// identified by their observer position and contents.
 function readoutsDoc(log) {
     const { c } = makeObserver(log.seed_text);
     c.mergeTreeDeltaCallback = undefined;
@@ -474,30 +475,55 @@ function readoutsDoc(log) {
         const msg = makeMsg(k, t, r, msn, cseq[k], op);
         if (type) { msg.type = type; }
         c.applyMsg(msg);
-        lastRef[c.getShortClientId(msg.clientId)] = r;
+        const cli = c.getShortClientId(msg.clientId);
+        lastRef[cli] = Math.max(lastRef[cli] === undefined ? r : lastRef[cli], r);
     }
     const mt = c.mergeTree;
     const cw = mt.getCollabWindow();
     const rng = new Rng(777, log.doc.length);
-    const views = [[cw.currentSeq, cw.clientId]];
-    for (let cli = 1; cli < 12; cli++) {
-        if (c.getLongClientId(cli) === undefined || lastRef[cli] === undefined) { break; }
-        const r0 = Math.max(lastRef[cli], cw.minSeq);
-        for (const ref of [r0, Math.floor((r0 + cw.currentSeq) / 2), cw.currentSeq]) { views.push([ref, cli]); }
+    const leafSum = (ref, cli) => {
+        let s = 0;
+        const walk = (b) => {
+            for (let i = 0; i < b.childCount; i++) {
+                const x = b.children[i];
+                if (x.isLeaf()) { s += mt.nodeLength(x, ref, cli) || 0; } else { walk(x); }
+            }
+        };
+        walk(mt.root);
+        return s;
+    };
+    const views = [[cw.currentSeq, cw.clientId, 0]];
+    for (let cli = 1; c.getLongClientId(cli) !== undefined; cli++) {
+        if (lastRef[cli] === undefined) { continue; }
+        for (let ref = cw.minSeq; ref <= cw.currentSeq; ref++) { views.push([ref, cli, ref < lastRef[cli] ? 1 : 0]); }
     }
-    const lengths = views.map(([ref, cli]) => [ref, cli, mt.getLength(ref, cli)]);
+    const lengths = views.map(([ref, cli, stale]) => [ref, cli, mt.getLength(ref, cli), stale, leafSum(ref, cli)]);
+    // getContainingSegment / getPosition on a sample of the views: the observer's, and per
+    // writer its oldest and latest views, the one at its latest refSeq, the one just below it
+    // (stale) and two more drawn from the window
+    const sample = [views[0]];
+    const byCli = {};
+    for (const v of views.slice(1)) { (byCli[v[1]] = byCli[v[1]] || []).push(v); }
+    for (const cli of Object.keys(byCli)) {
+        const vs = byCli[cli];
+        const at = vs.findIndex((v) => v[2] === 0);
+        const pick = new Set([0, vs.length - 1, rng.uniform(vs.length), rng.uniform(vs.length)]);
+        if (at >= 0) { pick.add(at); }
+        if (at > 0) { pick.add(at - 1); }
+        for (const i of [...pick].sort((x, y) => x - y)) { sample.push(vs[i]); }
+    }
     const containing = [];
-    for (const [ref, cli] of views) {
+    for (const [ref, cli, stale] of sample) {
         const len = mt.getLength(ref, cli);
-        for (let q = 0; q < 12; q++) {
-            const pos = q === 11 ? len : rng.uniform(len + 1);
+        for (let q = 0; q < 2; q++) {
+            const pos = q === 1 ? len : rng.uniform(len + 1);
             const { segment, offset } = mt.getContainingSegment(pos, ref, cli);
             if (segment === undefined) {
-                containing.push([pos, ref, cli, null]);
+                containing.push([pos, ref, cli, null, stale]);
                 continue;
             }
             containing.push([pos, ref, cli, [offset, mt.getPosition(segment, ref, cli),
-                c.getPosition(segment), segment.cachedLength, ordCodes(segment), segState(segment)]]);
+                c.getPosition(segment), segment.cachedLength, ordCodes(segment), segState(segment)], stale]);
         }
     }
     return { doc: log.doc, minSeq: cw.minSeq, currentSeq: cw.currentSeq, lengths, containing };

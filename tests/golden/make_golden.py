@@ -213,23 +213,28 @@ def make_rich_fixture():
 EVENTS_FROM = RICH_FROM + [("ref_c4", 1), ("ref_wide", 1), ("ref_ext_long", 1)]
 
 
-def make_events_fixture():
+# The configs' full-length streams (C3 / C4 at 10k messages, paged-size documents: thousands of
+# live segments, page splits and repacks) for the paged layout's ordinals.
+EVENTS_FULL_FROM = [("ref_c3_full", 1), ("ref_c4_full", 1)]
+
+
+def make_events_fixture(name="ref_events", sources=EVENTS_FROM):
     out = []
     with tempfile.TemporaryDirectory() as td:
-        for name, n in EVENTS_FROM:
-            with gzip.open(os.path.join(HERE, name + ".json.gz"), "rt") as fh:
+        for name_src, n in sources:
+            with gzip.open(os.path.join(HERE, name_src + ".json.gz"), "rt") as fh:
                 fx = json.load(fh)
-            docs = [dict(doc=f"{name}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in fx["docs"][:n]]
+            docs = [dict(doc=f"{name_src}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in fx["docs"][:n]]
             lp, op = os.path.join(td, "logs.json"), os.path.join(td, "out.json")
             json.dump({"docs": docs}, open(lp, "w"))
             subprocess.check_call(["node", os.path.join(REPO, "oracle", "ref_harness.mjs"), "events", lp, op])
             ev = json.load(open(op))["docs"]
             for d, e in zip(docs, ev):
                 d["events"] = e["events"]
-                d["source"] = name
+                d["source"] = name_src
                 out.append(d)
-    _dump("ref_events", dict(config={"ext": True, "sources": EVENTS_FROM}, docs=out))
-    print("ref_events", len(out), "docs", sum(len(d["events"]) for d in out), "events")
+    _dump(name, dict(config={"ext": True, "sources": sources}, docs=out))
+    print(name, len(out), "docs", sum(len(d["events"]) for d in out), "events")
 
 
 # Read-outs of the final replicas (harness "readouts"): MergeTree.getLength(refSeq, clientId),
@@ -310,6 +315,7 @@ def main():
         return
     if "--events" in sys.argv[1:]:
         make_events_fixture()
+        make_events_fixture("ref_events_full", EVENTS_FULL_FROM)
         make_readouts_fixture()
         return
     only = None
@@ -341,6 +347,7 @@ def main():
     make_error_fixture()
     make_rich_fixture()
     make_events_fixture()
+    make_events_fixture("ref_events_full", EVENTS_FULL_FROM)
     make_readouts_fixture()
     make_live_fixtures()
 

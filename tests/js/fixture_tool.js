@@ -189,12 +189,15 @@ if (mode === "encode") {
     // events <ref_events fixture> <flushEvery>: a listener's view of every event, built the
     // way SharedSegmentSequence does (sequence_event.js restates SequenceEvent.ranges) over
     // the facade's callbacks -> per event [segs: [getPosition, ordinal codes, cachedLength],
-    // ranges: [[index into deltaSegments, position]]], the harness's format
+    // ranges: [[index into deltaSegments, position]]], the harness's format; "paged": the
+    // documents live in the paged layout (a 16-segment LDS tier, then pages)
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js"));
     const { sequenceEventRanges } = require(path.join(__dirname, "sequence_event.js"));
     const every = parseInt(extra[0], 10);
+    const paged = extra[1] === "paged" ? { ldsSegCapacity: 16, pageCapacity: 256, unsettledCapacity: 2048,
+        pageHeapCapacity: 2048 } : {};
     const batch = new GpuMergeTreeBatch(fx.docs.length,
-        { segCapacity: 8192, textCapacity: 1 << 17, deltaLogCapacity: 1 << 22 });
+        Object.assign({ segCapacity: 8192, textCapacity: 1 << 18, deltaLogCapacity: 1 << 23 }, paged));
     batch.loadInitialText(fx.docs.map((d) => d.seed_text));
     const events = fx.docs.map(() => []);
     const codes = (seg) => (seg.ordinal === undefined ? null : Array.from(seg.ordinal, (ch) => ch.charCodeAt(0)));
@@ -250,19 +253,29 @@ if (mode === "encode") {
         for (const m of msgs(d)) { c.applyMsg(m); }
         return c;
     });
+    // a stale view (below the writer's latest refSeq) must throw (MT_E_STALE_VIEW, -6)
+    const refused = (f) => {
+        try { return f(); } catch (e) {
+            if (/failed \(-6\)/.test(e.message)) { return "refused"; }
+            throw e;
+        }
+    };
     const out = fx.docs.map((d, i) => {
         const c = views[i];
         const mt = c.mergeTree;
-        const lengths = d.lengths.map(([ref, cli]) => [ref, cli, cli === 0 ? c.getLength() : mt.getLength(ref, cli)]);
-        const containing = d.containing.map(([pos, ref, cli]) => {
+        // lengths: every view of a document with few, every 97th of the others (fetches are per call)
+        const stride = d.lengths.length > 2000 ? 97 : 1;
+        const lengths = d.lengths.filter((x, k) => k % stride === 0).map(([ref, cli]) =>
+            [ref, cli, cli === 0 ? c.getLength() : refused(() => mt.getLength(ref, cli))]);
+        const containing = d.containing.map(([pos, ref, cli]) => refused(() => {
             const { segment, offset } = cli === 0 ? c.getContainingSegment(pos) : mt.getContainingSegment(pos, ref, cli);
             if (segment === undefined) { return [pos, ref, cli, null]; }
             const st = Object.assign(segment.type === "Marker" ? { m: segment.refType } : { t: segment.text },
                 { p: segment.properties === undefined ? null : segment.properties });
             return [pos, ref, cli, [offset, mt.getPosition(segment, ref, cli), c.getPosition(segment), segment.cachedLength,
                 segment.ordinal === undefined ? null : Array.from(segment.ordinal, (ch) => ch.charCodeAt(0)), st]];
-        });
-        return { lengths, containing };
+        }));
+        return { lengths, containing, stride };
     });
     process.stdout.write(JSON.stringify({ docs: out }, jsReplacer));
 } else if (mode === "snapemit") {

@@ -45,22 +45,21 @@ def test_sorted_segment_set_collisions_and_undefined():
     assert gu.sorted_segment_ranges([((5,), "a"), (None, "x")]) == ["a"]
 
 
-# the flat tiers keep ordinals (mt_options.segment_ordinals; the paged layout does not)
-ORD_TIERS = {"lds": dict(lds_seg_capacity=0), "hbm": dict(lds_seg_capacity=-1), "tiny": dict(lds_seg_capacity=16)}
+# every storage tier keeps ordinals (mt_options.segment_ordinals): the flat ones and the paged
+# layout -- its page splits, level-1 packs and new roots, a tight tier handing documents over,
+# a narrow one, and the growth step moving documents to larger regions mid-batch
+ORD_TIERS = {"lds": dict(lds_seg_capacity=0), "hbm": dict(lds_seg_capacity=-1), "tiny": dict(lds_seg_capacity=16),
+             "paged": dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048),
+             "tight": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
+                           lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40),
+             "narrow": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048,
+                            page_heap_capacity=2048, lds_page_capacity=200, lds_unsettled_capacity=600,
+                            lds_page_heap_capacity=600, lds_narrow_overlap=1),
+             "grow": dict(lds_seg_capacity=16, page_capacity=12, unsettled_capacity=16, page_heap_capacity=16)}
+PAGED_TIERS = ("paged", "tight", "narrow", "grow")
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("tier", list(ORD_TIERS))
-def test_gpu_event_positions_and_ordinals_match_reference(tier):
-    from fluidframework_amd import MergeTreeBatch
-    fx = _fixture()
-    interner = gu.Interner()
-    a = gu.encode_docs(fx, interner)
-    mt = MergeTreeBatch(len(fx["docs"]), delta_log_mode=1, delta_log_capacity=1 << 22, segment_ordinals=1,
-                        seg_capacity=8192, text_capacity=1 << 17, **ORD_TIERS[tier])
-    mt.load_initial_text(a["seed_off"], a["seed"])
-    mt.apply_arrays(a)
-    assert (mt.status() == 0).all()
+def _check_events(mt, fx):
     for i, doc in enumerate(fx["docs"]):
         ext = []
         gu.parse_rich_log(mt.get_delta_log(i), ext)
@@ -74,19 +73,52 @@ def test_gpu_event_positions_and_ordinals_match_reference(tier):
 
 
 @pytest.mark.gpu
-def test_gpu_segment_ordinals_need_flat_tiers():
+@pytest.mark.parametrize("tier", list(ORD_TIERS))
+@pytest.mark.parametrize("name", ["ref_events", "ref_events_full"])
+def test_gpu_event_positions_and_ordinals_match_reference(name, tier):
+    """Every callback segment's position and ordinal, and so the ranges the reference's own
+    SequenceDeltaEvent / SequenceMaintenanceEvent keep, on every tier; ref_events_full holds
+    the configs' 10k-message C3 / C4 documents (paged-size: thousands of live segments)."""
     from fluidframework_amd import MergeTreeBatch
-    with pytest.raises(RuntimeError):
-        MergeTreeBatch(2, delta_log_mode=1, delta_log_capacity=1024, segment_ordinals=1, page_capacity=64)
+    fx = gu.load(name)
+    interner = gu.Interner()
+    a = gu.encode_docs(fx, interner)
+    mt = MergeTreeBatch(len(fx["docs"]), delta_log_mode=1, delta_log_capacity=1 << 23, segment_ordinals=1,
+                        seg_capacity=8192, text_capacity=1 << 18, **ORD_TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all()
+    _check_events(mt, fx)
+    if tier in PAGED_TIERS and name == "ref_events_full":
+        assert all(mt.is_paged(i) for i in range(len(fx["docs"])))
+
+
+@pytest.mark.gpu
+def test_gpu_segment_ordinals_need_the_rich_log():
+    from fluidframework_amd import MergeTreeBatch
     with pytest.raises(RuntimeError):   # ordinals ride on the rich log
         MergeTreeBatch(2, segment_ordinals=1)
 
 
 # ---------------------------------------------------------------- read-outs
-READ_TIERS = dict(ORD_TIERS, paged=dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=2048,
-                                        page_heap_capacity=2048),
-                  tight=dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
-                             lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40))
+READ_TIERS = dict(ORD_TIERS, paged_noord=ORD_TIERS["paged"])
+
+
+def test_reference_readouts_differ_from_leaves_only_in_stale_views():
+    """Pins the refusal rule on the reference itself (CPU): over every writer view of the
+    read-out fixture's collab windows, the reference's MergeTree.getLength (partial lengths)
+    differs from the sum of its own leaves' nodeLength only in views below the writer's latest
+    refSeq -- and does in many of those."""
+    fx = gu.load("ref_readouts")
+    stale = differ = differ_live = views = 0
+    for d in fx["docs"]:
+        for ref, cli, n, st, leaves in d["lengths"]:
+            views += 1
+            stale += st
+            differ += n != leaves
+            differ_live += n != leaves and not st
+    assert views > 270000 and stale > 200000
+    assert differ > 50000 and differ_live == 0
 
 
 @pytest.mark.gpu
@@ -94,24 +126,41 @@ READ_TIERS = dict(ORD_TIERS, paged=dict(lds_seg_capacity=-1, page_capacity=256, 
 def test_gpu_readouts_match_reference(tier):
     """MergeTree.getLength(refSeq, clientId), getContainingSegment(pos, refSeq, clientId) and
     getPosition (MT/mergeTree.ts:1610-1667, Client.getPosition / getContainingSegment) of the
-    final replicas equal the reference's in the observer's and every writer's views
-    (tests/golden/ref_readouts.json.gz); ordinals too on the flat tiers."""
-    from fluidframework_amd import MergeTreeBatch
+    final replicas equal the reference's in the observer's view and in every writer's view of
+    the collab window (tests/golden/ref_readouts.json.gz: getLength in all of them,
+    getContainingSegment in a sample of each writer's) -- except the views below the writer's
+    latest refSeq, which the reference answers from partial lengths that need not add up to its
+    leaves (51 239 of 211 951 differ) and which are refused (StaleViewError); ordinals too on
+    every tier that keeps them."""
+    from fluidframework_amd import MergeTreeBatch, StaleViewError
     fx = gu.load("ref_readouts")
     interner = gu.Interner()
     a = gu.encode_docs(fx, interner)
-    ords = tier in ORD_TIERS
+    ords = tier in ORD_TIERS   # (paged_noord: the read-outs without the rich log)
     kw = dict(delta_log_mode=1, delta_log_capacity=1 << 22, segment_ordinals=1) if ords else {}
     mt = MergeTreeBatch(len(fx["docs"]), seg_capacity=8192, text_capacity=1 << 17, **kw, **READ_TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     assert (mt.status() == 0).all()
+    n_stale = n_views = 0
     for i, doc in enumerate(fx["docs"]):
-        refs, clis, want = zip(*doc["lengths"])
-        assert list(mt.get_view_lengths([i] * len(refs), refs, clis)) == list(want), doc["doc"]
-        for pos, ref, cli, exp in doc["containing"]:
-            got = mt.get_containing_segment(i, pos, ref, cli)
+        refs, clis, want, stale, _ = zip(*doc["lengths"])
+        got = mt.get_view_lengths([i] * len(refs), refs, clis, refuse_stale=False)
+        # every view of the collab window: equal to the reference, or refused when stale
+        assert list(got) == [-1 if s else w for w, s in zip(want, stale)], doc["doc"]
+        n_stale += sum(stale)
+        n_views += len(refs)
+        if 1 in stale:
+            k = stale.index(1)
+            with pytest.raises(StaleViewError):
+                mt.get_view_lengths([i], [refs[k]], [clis[k]])
+        for pos, ref, cli, exp, st in doc["containing"]:
             where = (doc["doc"], pos, ref, cli)
+            if st:
+                with pytest.raises(StaleViewError):
+                    mt.get_containing_segment(i, pos, ref, cli)
+                continue
+            got = mt.get_containing_segment(i, pos, ref, cli)
             if exp is None:
                 assert got is None, where
                 continue
@@ -128,6 +177,7 @@ def test_gpu_readouts_match_reference(tier):
             assert mt.get_segment_by_uid(i, got["uid"], ref, cli)["position"] == vpos, where
     # a segment that left the tree reads as gone (the reference's getPosition walks no parent)
     assert mt.get_segment_by_uid(0, 0xFFFFFFF) is None
+    assert n_stale > 200000 and n_views > 270000
 
 
 def test_reference_ordinal_invariant_holds_on_fixture_streams(tmp_path):

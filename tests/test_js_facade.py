@@ -295,16 +295,18 @@ def test_js_sequence_event_restatement_matches_reference_events():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("every", [100000, 37])
-def test_js_facade_sequence_events_match_reference(every):
+@pytest.mark.parametrize("name,every,layout", [("ref_events", 100000, "flat"), ("ref_events", 37, "flat"),
+                                               ("ref_events_full", 100000, "paged"), ("ref_events", 37, "paged")])
+def test_js_facade_sequence_events_match_reference(name, every, layout):
     """A listener builds SharedSegmentSequence's event objects over GpuClient callbacks
     (getPosition + segment ordinals, SEQ/sequence.ts:139-149): every event's positions,
     ordinals and ranges equal those of the reference's own SequenceDeltaEvent /
     SequenceMaintenanceEvent (tests/golden/ref_events), in one flush or in flushes of 37
-    messages (segment objects keep their identity across flushes)."""
+    messages (segment objects keep their identity across flushes), on flat documents and on
+    a paged batch (ref_events_full: the configs' 10k-message C3 / C4 documents)."""
     _addon()
-    fx = gu.load("ref_events")
-    got = _node("events", os.path.join(gu.GOLDEN, "ref_events.json.gz"), str(every), timeout=600)["events"]
+    fx = gu.load(name)
+    got = _node("events", os.path.join(gu.GOLDEN, name + ".json.gz"), str(every), layout, timeout=600)["events"]
     for d, evs in zip(fx["docs"], got):
         assert len(evs) == len(d["events"]), d["doc"]
         for k, (g, w) in enumerate(zip(evs, d["events"])):
@@ -320,9 +322,10 @@ def test_js_facade_readouts_match_reference():
     fx = gu.load("ref_readouts")
     got = _node("readouts", os.path.join(gu.GOLDEN, "ref_readouts.json.gz"), timeout=600)["docs"]
     for d, g in zip(fx["docs"], got):
-        assert g["lengths"] == d["lengths"], d["doc"]
+        want = [[r, c, "refused" if st else n] for r, c, n, st, _ in d["lengths"][::g["stride"]]]
+        assert g["lengths"] == want, d["doc"]
         for q, (x, y) in enumerate(zip(g["containing"], d["containing"])):
-            assert x == y, (d["doc"], q, x, y)
+            assert x == ("refused" if y[4] else y[:4]), (d["doc"], q, x, y)
 
 
 @pytest.mark.gpu
