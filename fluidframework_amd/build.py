@@ -2,13 +2,17 @@
 host summary decoder (libmtsnapdec.so).
 hipcc cross-compiles here without a GPU; the .so travels to the GPU box with the repo."""
 import os
+import re
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "mt_replay.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", "mt_device.h", "mt_paged.h")] + [
+VARIANTS_H = os.path.join(HERE, "csrc", "mt_variants.h")
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("mt_replay.hip", "mt_engine.h", "mt_device.h", "mt_paged.h",
+                                                 "mt_kernels.h", "mt_variants.h")] + [
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mt_replay.h", "mt_types.h")]
+OBJ_DIR = os.path.join(HERE, "_build")
 OUT = os.environ.get("MT_OUT") or os.path.join(HERE, "libmtreplay.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -amdgpu-use-amdgpu-trackers: the scheduler's AMDGPU register-pressure trackers (A/B on the
@@ -24,10 +28,56 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in DEPS)
 
 
+def variants():
+    """(name, kernel expression) of every kernel instantiation in csrc/mt_variants.h."""
+    text = open(VARIANTS_H).read()
+    return re.findall(r"X\((\w+), \((.*?)\)\)\s*\\?\n", text)
+
+
 def build(force=False, verbose=False):
+    """One translation unit per kernel instantiation (csrc/mt_variants.h) plus the host side,
+    compiled in parallel and linked into one shared library (MT_SINGLE_TU=1: the whole library
+    as one translation unit, e.g. for -DMT_PROF builds)."""
     if not force and not needs_build():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC]
+    single = os.environ.get("MT_SINGLE_TU") == "1" or "-DMT_PROF" in FLAGS
+    if single:
+        cmd = [HIPCC] + FLAGS + ["-DMT_SINGLE_TU", "-o", OUT + ".tmp", SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        os.replace(OUT + ".tmp", OUT)
+        return OUT
+    tag = os.path.splitext(os.path.basename(OUT))[0]   # variant libraries (MT_OUT) build apart
+    obj_dir = os.path.join(OBJ_DIR, tag)
+    os.makedirs(obj_dir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
+    jobs = [(SRC, os.path.join(obj_dir, "mt_replay.o"))]
+    for name, expr in variants():
+        src = os.path.join(obj_dir, f"mtk_{name}.hip")
+        body = (f'#include "{os.path.join(HERE, "csrc", "mt_kernels.h")}"\n'
+                f"const void *mtk_{name}() {{ return (const void *)({expr}); }}\n")
+        if not os.path.exists(src) or open(src).read() != body:
+            with open(src, "w") as fh:
+                fh.write(body)
+        jobs.append((src, os.path.join(obj_dir, f"mtk_{name}.o")))
+    par = int(os.environ.get("MT_BUILD_JOBS") or min(8, os.cpu_count() or 1))
+    running, done = [], []
+    pending = list(jobs)
+    while pending or running:
+        while pending and len(running) < par:
+            src, obj = pending.pop(0)
+            cmd = [HIPCC] + cflags + ["-o", obj, src]
+            if verbose:
+                print(" ".join(cmd))
+            running.append((subprocess.Popen(cmd), src))
+        p, src = running.pop(0)
+        if p.wait() != 0:
+            for q, _ in running:
+                q.wait()
+            raise subprocess.CalledProcessError(p.returncode, src)
+        done.append(src)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + [o for _, o in jobs]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -10,44 +10,12 @@
 #include <vector>
 
 #include "../../include/mt_replay.h"
-#include "mt_paged.h"
-
-// ============================================================================ kernels
-// Initial document contents (Client.insertSegmentLocal before collaboration: seq 0,
-// client LocalClientId -1; MT/client.ts:202-215) and collaboration start
-// (MT/mergeTree.ts:1287-1304): one leaf block under the root.
-__device__ static void init_doc_hdr(const DevState &st, int doc, int len) {
-    DocHdr h;
-    memset(&h, 0, sizeof(h));
-    h.depth = 1;
-    h.n_blk[0] = 1;
-    h.text_top = len;
-    h.props_top = 1;
-    h.next_uid = 2;   // segment ids start at 1 (0 marks a heap entry whose segment is gone)
-    h.delta_hash = MT_FNV_OFF;
-    h.status = len > st.T ? MT_DOC_CAPACITY : 0;
-    const size_t S = st.S;
-    if (len > 0) {
-        h.n_seg = 1;
-        st.segA[doc * S] = v4i{len, 0, MT_RSEQ_NONE, pack_cli(-1, 0)};
-        st.segO[doc * S] = 0ull;
-        st.segB[doc * S] = v4u{0u, 0u, 1u, 0u};
-        if (st.segP) {
-            u64 *w = (u64 *)(st.segP + doc * S);
-            w[0] = w[1] = w[2] = w[3] = 0ull;
-        }
-    }
-    st.cnt[(size_t)doc * MT_LV * st.B] = len > 0 ? 1 : 0;
-    st.flg[(size_t)doc * st.B] = MT_SCOUR_UNDEF;
-    st.hdr[doc] = h;
-}
-
-// every overlap slot free (one wave: lane i clears slot i)
-__device__ static void oslot_reset(const DevState &st, int doc) {
-    int32_t *o = st.oslot + (size_t)doc * 2 * MT_OSLOTS;
-    o[2 * lane()] = MT_OSLOT_FREE;
-    o[2 * lane() + 1] = 0;
-}
+#include "mt_kernels.h"
+#include "mt_variants.h"
+#ifdef MT_SINGLE_TU
+#define MT_VARIANT_DEF(n, k) const void *mtk_##n() { return (const void *)k; }
+MT_VARIANTS(MT_VARIANT_DEF)
+#endif
 
 __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *seed_off,
                                                   const uint16_t *seed) {
@@ -79,18 +47,6 @@ __global__ void __launch_bounds__(MT_WAVE) k_init(DevState st, const int64_t *se
 // (reloadFromSegments MT/mergeTree.ts:1229-1284; new blocks: needsScour undefined), then
 // startOrUpdateCollaboration(minSeq, seq) (MT/mergeTree.ts:1287-1304: fresh zamboni heap).
 // Body segments are appended afterwards by replaying MT_F_LOAD records (mt_load_snapshots).
-#define MT_LOAD_FANOUT (MT_MAXN - 1)
-// Staging for summary headers larger than the flat capacities on a paged handle: the flat
-// tree is built here (off[2d] = first segment, off[2d+1] = first leaf block of document d;
-// -1: the document uses the flat HBM arrays), then k_load_convert pages it.
-struct LoadScratch {
-    v4i *A;
-    u64 *O;
-    v4u *B;
-    uint8_t *cnt;   // [MT_LV][nb0] per document
-    int8_t *flg;
-    const int64_t *off;
-};
 __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int64_t *off, const int32_t *nh,
                                                          const mt_seg_rec *segs, const uint16_t *tin,
                                                          const uint32_t *pin, const int32_t *min_seq,
@@ -226,634 +182,6 @@ __global__ void __launch_bounds__(MT_WAVE) k_load_header(DevState st, const int6
         for (int l = 0; l < MT_LV; l++) h.n_blk[l] = status ? (l == 0) : nbl[l];
         st.hdr[doc] = h;
         st.retry[doc] = 0;
-    }
-}
-
-// Per-launch LDS capacities of the tier (the HBM tier keeps only the B-tree counts in LDS).
-struct TierCaps {
-    int S, B, H;
-    int resume;   // TierGlb: start from resume[doc] (documents handed over by the LDS tier)
-};
-
-// Client.applyMsg for every record of this document (one wavefront per document).  The
-// records are prefetched 64 at a time (lane l holds record k+l plus up to 8 payload units)
-// and broadcast with readlane, so no op waits on HBM latency.
-//
-// TierLds: the document is staged in LDS; before each message lds_room() checks that the
-// LDS capacities cannot overflow while applying it.  If they could, the LDS state is
-// spilled to HBM and the document continues from that message in the TierGlb launch
-// (retry[doc] = 1, resume[doc] = message index).
-//
-// WPG documents per workgroup, one per wave, each with its own LDS slice; the waves never
-// synchronise (more documents per CU than its workgroup limit of 16 would allow).
-template <class T, int WPG>
-__global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_op_rec *ops,
-                                                          const int64_t *off, const uint16_t *tin,
-                                                          const uint32_t *pin, TierCaps caps) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 0);
-    // wave-uniform (SGPR) document index and LDS slice
-    const int wv = WPG == 1 ? 0 : uni((int)(threadIdx.x >> 6));
-    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw + (uint32_t)(wv * (int)L.total);
-    const int doc = (int)blockIdx.x * WPG + wv;
-    if (doc >= st.n_docs) return;
-    if (!T::kLds && !st.retry[doc]) return;
-    if (!T::kLds && lane() == 0) atomicAdd(st.stats, 1u);
-    const int64_t k1 = off[doc + 1];
-    const int64_t k0 = (T::kLds || !caps.resume) ? off[doc] : st.resume[doc];
-    DocT<T> d;
-    if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
-        if (lane() == 0) {
-            st.retry[doc] = 1;
-            st.resume[doc] = k0;
-            atomicAdd(st.stats + 1 + d.cap_cause, 1u);
-        }
-        return;
-    }
-    if (d.status) {
-        if (!T::kLds && lane() == 0) st.retry[doc] = 0;
-        return;
-    }
-    const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
-    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
-    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
-    int64_t spill_at = -1;
-    for (int64_t kb = k0; kb < k1 && d.status == 0 && spill_at < 0; kb += MT_WAVE) {
-        const int64_t k = kb + lane();
-        v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        int nl = 0, pok = 0;
-        if (k < k1) {
-            r0 = o4[2 * k];
-            r1 = o4[2 * k + 1];
-            const int kind = (r1.w >> 16) & 0xFF, flags = ((uint32_t)r1.w >> 24) & 0xFF;
-            const int len = r1.x;
-            if (kind == MT_OP_INSERT && !(flags & MT_F_MARKER) && len > 0) {
-                const GLB_AS uint16_t *src = gt + (uint32_t)r1.y;
-                nl = src[len - 1] == '\n';
-                if (len <= 8) {
-                    pok = 1;
-                    uint32_t u[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) u[j] = j < len ? src[j] : 0u;
-                    w0 = u[0] | (u[1] << 16);
-                    w1 = u[2] | (u[3] << 16);
-                    w2 = u[4] | (u[5] << 16);
-                    w3 = u[6] | (u[7] << 16);
-                }
-            }
-        }
-        const int cnt = (int)min((int64_t)MT_WAVE, k1 - kb);
-        for (int j = 0; j < cnt && d.status == 0; j++) {
-            OpIn in;
-            in.op.seq = __builtin_amdgcn_readlane(r0.x, j);
-            in.op.ref_seq = __builtin_amdgcn_readlane(r0.y, j);
-            in.op.min_seq = __builtin_amdgcn_readlane(r0.z, j);
-            in.op.pos1 = __builtin_amdgcn_readlane(r0.w, j);
-            in.op.pos2 = __builtin_amdgcn_readlane(r1.x, j);
-            in.op.payload = (uint32_t)__builtin_amdgcn_readlane(r1.y, j);
-            in.op.props = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
-            const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane(r1.w, j);
-            in.op.client = (uint16_t)(cw & 0xFFFF);
-            in.op.kind = (uint8_t)((cw >> 16) & 0xFF);
-            in.op.flags = (uint8_t)(cw >> 24);
-            if (T::kLds && !lds_room(d, in.op)) {
-                spill_at = kb + j;
-                break;
-            }
-            in.pay_lo = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w0, j) |
-                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w1, j) << 32);
-            in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
-                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
-            in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
-            in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
-            opaque(d);
-
-            apply_op(d, in, gt, gp);
-        }
-    }
-    if (T::kLds && d.status == MT_DOC_RETRY) {
-        // an LDS capacity overflowed mid-message despite lds_room(): not resumable
-        d.status = MT_DOC_CAPACITY;
-        if (lane() == 0) atomicAdd(st.stats + 1 + d.cap_cause, 1u);
-    }
-    if (T::kLds && spill_at >= 0) {
-        if (lane() == 0) {
-            st.retry[doc] = 1;
-            st.resume[doc] = spill_at;
-            atomicAdd(st.stats + 1, 1u);
-        }
-    }
-    if (!T::kLds && lane() == 0) st.retry[doc] = 0;
-#ifdef MT_PROF
-    if (lane() < 32) atomicAdd(&g_prof[lane()], d.prof[lane()]);
-#endif
-    store_doc(d, st, doc);
-}
-
-// ---------------------------------------------------------------- synthetic generator
-struct Rng {
-    uint32_t s[4];
-};
-__host__ __device__ static inline uint32_t sm32(uint32_t &x) {
-    x += 0x9E3779B9u;
-    uint32_t z = x;
-    z = (z ^ (z >> 16)) * 0x85EBCA6Bu;
-    z = (z ^ (z >> 13)) * 0xC2B2AE35u;
-    return z ^ (z >> 16);
-}
-__host__ __device__ static inline void rng_init(Rng &r, uint32_t seed, int doc) {
-    uint32_t x = seed ^ ((uint32_t)(doc + 1) * 0x9E3779B9u);
-    for (int i = 0; i < 4; i++) r.s[i] = sm32(x);
-}
-__host__ __device__ static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
-__host__ __device__ static inline uint32_t rng_next(Rng &r) {   // xoshiro128**
-    uint32_t result = rotl32(r.s[1] * 5u, 7) * 9u;
-    uint32_t t = r.s[1] << 9;
-    r.s[2] ^= r.s[0];
-    r.s[3] ^= r.s[1];
-    r.s[1] ^= r.s[2];
-    r.s[0] ^= r.s[3];
-    r.s[2] ^= t;
-    r.s[3] = rotl32(r.s[3], 11);
-    return result;
-}
-__host__ __device__ static inline uint32_t rng_uniform(Rng &r, uint32_t n) {
-    return (uint32_t)(((uint64_t)rng_next(r) * n) >> 32);
-}
-__device__ static __forceinline__ uint32_t gen_props(Rng &r, const mt_gen_cfg &cfg, uint32_t *out) {
-    const uint32_t nk = 1 + rng_uniform(r, (uint32_t)cfg.max_keys_per_op);
-    uint32_t count = 0;
-    for (uint32_t j = 0; j < nk; j++) {
-        const uint32_t key = rng_uniform(r, (uint32_t)cfg.n_keys);
-        const bool is_null = (uint64_t)rng_next(r) < cfg.p_null;
-        const uint32_t val = rng_uniform(r, (uint32_t)cfg.n_values);
-        bool dup = false;
-        gsync();
-        for (uint32_t q = 0; q < count; q++)
-            if (out[1 + 2 * q] == key) dup = true;   // lane 0 wrote these
-        if (dup) continue;
-        if (lane() == 0) {
-            out[1 + 2 * count] = key;
-            out[2 + 2 * count] = is_null ? MT_VAL_NULL : (val | (val == 0 ? MT_VAL_FALSY_BIT : 0u));
-        }
-        count++;
-    }
-    if (lane() == 0) out[0] = count;
-    gsync();
-    return 1 + 2 * count;
-}
-
-// Per-document generator state (DESIGN.md "Synthetic op streams"), shared by the flat and
-// the paged generators.  Every lane draws the same numbers (uniform state).
-struct GenCtx {
-    Rng rng;
-    LDS_AS int32_t *last_ref;
-    LDS_AS int32_t *short_id;
-    int next_short;
-    int64_t tu, pu, tb, pb;
-};
-__device__ static __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
-__device__ static void gen_begin(GenCtx &g, const DevState &st, const mt_gen_cfg &cfg, int gdoc, int doc,
-                                 LDS_AS uint8_t *gen_lds, int64_t tstride, int64_t pstride) {
-    const int W = cfg.writers;
-    g.last_ref = (LDS_AS int32_t *)gen_lds;
-    g.short_id = g.last_ref + (W + 1);
-    rng_init(g.rng, cfg.seed, gdoc);
-    // seed text (drawn exactly like the oracle / reference harness)
-    uint16_t *arena = st.text + (size_t)doc * 2 * st.T;
-    for (int i = 0; i < cfg.seed_len; i++) {
-        (void)rng_next(g.rng);
-        const uint16_t ch = (uint16_t)(97 + rng_uniform(g.rng, 26));
-        if (lane() == 0) arena[i] = ch;
-    }
-    if (lane() == 0) init_doc_hdr(st, doc, cfg.seed_len);
-    oslot_reset(st, doc);
-    for (int j = lane(); j <= W; j += MT_WAVE) {
-        g.last_ref[j] = 0;
-        g.short_id[j] = 0;
-    }
-    gsync();
-    g.next_short = 1;
-    g.tu = g.pu = 0;
-    g.tb = (int64_t)doc * tstride;
-    g.pb = (int64_t)doc * pstride;
-}
-// Writer, reference sequence number and minSeq of message t.
-__device__ static void gen_pick(GenCtx &g, const mt_gen_cfg &cfg, int t, int &r, int &c, int &msn) {
-    const int W = cfg.writers;
-    const int k = 1 + (int)rng_uniform(g.rng, (uint32_t)W);
-    int lo = max(g.last_ref[k], t - 1 - cfg.lag);
-    if (lo < 0) lo = 0;
-    r = lo + (int)rng_uniform(g.rng, (uint32_t)(t - 1 - lo + 1));
-    lds_fence();
-    if (lane() == 0) g.last_ref[k] = r;
-    lds_fence();
-    int m = 0x7fffffff;
-    for (int j = 1 + lane(); j <= W; j += MT_WAVE) m = min(m, g.last_ref[j]);
-    msn = -wave_max(-m);
-    c = g.short_id[k];
-    if (!c) {
-        c = g.next_short++;
-        lds_fence();
-        if (lane() == 0) g.short_id[k] = c;
-        lds_fence();
-    }
-}
-// The op of message t given the writer's view length (drawn like the oracle's generator).
-__device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, int c, int msn, int len,
-                              OpIn &in, mt_op_rec *ops_out, uint16_t *text_out, uint32_t *props_out,
-                              int64_t doc) {
-    const uint32_t u = rng_next(g.rng);
-    mt_op_rec &op = in.op;
-    op.seq = t;
-    op.ref_seq = r;
-    op.min_seq = msn;
-    op.client = (uint16_t)c;
-    op.flags = 0;
-    op.props = MT_NO_PROPS;
-    op.payload = 0;
-    in.pay_ok = true;
-    in.nl = false;
-    u64 plo = 0, phi = 0;
-    if (len == 0 || (uint64_t)u < cfg.p_insert) {
-        op.kind = MT_OP_INSERT;
-        op.pos1 = (int)rng_uniform(g.rng, (uint32_t)(len + 1));
-        const int tl = 1 + (int)rng_uniform(g.rng, (uint32_t)cfg.text_max);
-        op.pos2 = tl;
-        op.payload = (uint32_t)g.tu;   // local to the document's region (rebased by k_gen_compact)
-        uint16_t ch = 0;
-        for (int j = 0; j < tl; j++) {
-            const uint32_t v = rng_next(g.rng);
-            ch = (uint16_t)'\n';
-            if ((uint64_t)v >= cfg.p_newline) ch = (uint16_t)(97 + rng_uniform(g.rng, 26));
-            if (lane() == 0) text_out[g.tb + g.tu + j] = ch;
-            if (j < 4)
-                plo |= (u64)ch << (16 * j);
-            else if (j < 8)
-                phi |= (u64)ch << (16 * (j - 4));
-        }
-        in.nl = ch == '\n';
-        in.pay_ok = tl <= 8;
-        g.tu += tl;
-        if (cfg.p_insert_props > 0 && (uint64_t)rng_next(g.rng) < cfg.p_insert_props) {
-            op.props = (uint32_t)g.pu;
-            g.pu += gen_props(g.rng, cfg, props_out + g.pb + g.pu);
-        }
-    } else {
-        const int p1 = (int)rng_uniform(g.rng, (uint32_t)len);
-        int m = 1;
-        while (m < 64 && (uint64_t)rng_next(g.rng) < cfg.p_len_continue) m++;
-        op.pos1 = p1;
-        op.pos2 = min(p1 + m, len);
-        if ((uint64_t)u < cfg.p_insert_remove) {
-            op.kind = MT_OP_REMOVE;
-        } else {
-            op.kind = MT_OP_ANNOTATE;
-            op.props = (uint32_t)g.pu;
-            g.pu += gen_props(g.rng, cfg, props_out + g.pb + g.pu);
-        }
-    }
-    in.pay_lo = plo;
-    in.pay_hi = phi;
-    if (lane() == 0) ops_out[doc * cfg.ops + (t - 1)] = op;
-    gsync();
-}
-// The document's text / property words used so far (k_gen_compact packs the regions).
-__device__ static void gen_end(const GenCtx &g, int64_t *used_out, int doc) {
-    if (lane() == 0) {
-        used_out[2 * doc] = g.tu;
-        used_out[2 * doc + 1] = g.pu;
-    }
-}
-
-// Generates and applies cfg.ops messages per document; the view length each writer draws
-// positions from is read off the live replica.
-template <class T>
-__global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cfg, uint32_t doc_base,
-                                                      mt_op_rec *ops_out, uint16_t *text_out,
-                                                      uint32_t *props_out, int64_t tstride,
-                                                      int64_t pstride, int32_t *fail_out,
-                                                      int32_t *dbg_len, int64_t *used_out, TierCaps caps) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
-    const int doc = blockIdx.x;
-    if (doc >= st.n_docs) return;
-    if (!T::kLds && !st.retry[doc]) return;
-    const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 2 * (cfg.writers + 1));
-    GenCtx g;
-    gen_begin(g, st, cfg, (int)(doc_base + doc), doc, smem + L.offGen, tstride, pstride);
-    DocT<T> d;
-    if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
-        if (lane() == 0) st.retry[doc] = 1;
-        return;
-    }
-    // op records carry offsets local to the document's region of the arenas
-    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)(text_out + g.tb);
-    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)(props_out + g.pb);
-    for (int t = 1; t <= cfg.ops && d.status == 0; t++) {
-        int r, c, msn;
-        gen_pick(g, cfg, t, r, c, msn);
-        d.ocs = oslot_of(d, c);
-        int vsum = 0;
-        for (int base = 0; base < d.n; base += MT_WAVE) {
-            const int i = base + lane();
-            v4i a;
-            u64 o;
-            load_ao(d, i, i < d.n, a, o);
-            vsum += i < d.n ? view_len(a, o, r, c, d.ocs) : 0;
-        }
-        const int len = wave_sum(vsum);
-        if (dbg_len && lane() == 0) {
-            int32_t *q = dbg_len + ((int64_t)doc * cfg.ops + (t - 1)) * 4;
-            q[0] = len;
-            q[1] = d.n;
-            q[2] = r;
-            q[3] = c;
-        }
-        OpIn in;
-        gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
-        apply_op(d, in, gt, gp);
-    }
-    gen_end(g, used_out, doc);
-    if (T::kLds && d.status == MT_DOC_RETRY) {
-        if (lane() == 0) st.retry[doc] = 1;
-        return;
-    }
-    if (lane() == 0) {
-        if (d.status) fail_out[doc] = d.status;
-        if (!T::kLds) st.retry[doc] = 0;
-    }
-    store_doc(d, st, doc);
-}
-
-// ---------------------------------------------------------------- paged kernels
-// high-water marks -> stats[8..11] (mt_last_paged_peaks)
-template <class T>
-__device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, int pk_ut, int pk_heap) {
-    const int np = nbr(pd.up, 1);
-    int ns = 0;
-    for (int q = lane(); q < np; q += MT_WAVE) ns += pd.meta[pd.up.dir[q]].nseg;
-    ns = wave_sum(ns);
-    if (lane() == 0) {
-        atomicMax(st.stats + 8, (uint32_t)np);
-        atomicMax(st.stats + 9, (uint32_t)pk_ut);
-        atomicMax(st.stats + 10, (uint32_t)pk_heap);
-        atomicMax(st.stats + 11, (uint32_t)ns);
-    }
-}
-// Replay of the documents flagged by the LDS tier (retry[doc]) in the paged layout: a
-// document seen for the first time is converted from its flat state (initial contents, or
-// what the LDS tier spilled) and stays paged until the next reset.
-// waves per SIMD the paged kernel is compiled for (VGPR budget 512 / n); 0 = compiler choice
-#ifndef MT_PAGED_WAVES
-#define MT_PAGED_WAVES 3
-#endif
-#if MT_PAGED_WAVES > 0
-#define MT_PAGED_WPE __attribute__((amdgpu_waves_per_eu(MT_PAGED_WAVES)))
-#else
-#define MT_PAGED_WPE
-#endif
-// A tight launch (pc.tight) hands a document to the next launch -- retry[doc] = 2 from
-// message resume[doc] -- when it does not fit its LDS capacities at load, or before a message
-// that could outgrow them (pg_room); stats[12] counts those hand-overs.
-// A last tier with PagedCaps.grow hands a document to the growth step the same way (retry[doc]
-// = 3, stats[13] counts them).
-template <class T>
-__device__ __forceinline__ void pg_handover(const DevState &st, int doc, int64_t k, const PagedCaps &pc) {
-    if (lane() == 0) {
-        st.retry[doc] = pc.tight ? 2 : 3;
-        st.resume[doc] = k;
-        atomicAdd(st.stats + (pc.tight ? 12 : 13), 1u);
-    }
-}
-// One launch of a sliced paged replay (mt_options.paged_slices): documents in [skip_lo,
-// skip_hi) sit this launch out, the others replay at most `ops` messages (0: all) and keep
-// their stage with resume[doc] at the next one; stats[0] counts documents in [cnt_lo, cnt_hi).
-struct PagedSlice {
-    int64_t ops;
-    int skip_lo, skip_hi, cnt_lo, cnt_hi;
-};
-
-template <class T>
-__global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState st, const mt_op_rec *ops,
-                                                          const int64_t *off, const uint16_t *tin,
-                                                          const uint32_t *pin, int use_resume, PagedCaps pc_arg,
-                                                          PagedSlice sl) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
-    const PagedCaps pc = eff_caps<T>(pc_arg);
-    const int doc = blockIdx.x;
-    if (doc >= st.n_docs) return;
-    if (doc >= sl.skip_lo && doc < sl.skip_hi) return;
-    if (st.retry[doc] != pc.stage) return;
-    if (lane() == 0 && doc >= sl.cnt_lo && doc < sl.cnt_hi) atomicAdd(st.stats, 1u);
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v), T::kPacked);
-    const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
-    const int64_t kend = off[doc + 1];
-    const int64_t k1 = sl.ops > 0 ? min(kend, k0 + sl.ops) : kend;   // this launch's last message + 1
-    PagedDoc<T> pd;
-    pg_setup(pd, st, doc, smem, L, pc);
-    DocT<T> &w = pd.w;
-    if (w.status) {
-        if (lane() == 0) st.retry[doc] = 0;
-        return;
-    }
-    if (st.hdr[doc].pad[HDR_PAGED]) {
-        if (!pg_load(pd, st)) {
-            if (pc.tight || pc.grow) {
-                pg_handover<T>(st, doc, k0, pc);
-            } else if (lane() == 0) {   // cannot happen: the last tier has the document's capacities
-                st.hdr[doc].status = MT_DOC_CAPACITY;
-                st.retry[doc] = 0;
-            }
-            return;
-        }
-    } else if (!pg_convert(pd, flat_src(st, doc))) {
-        // stays flat (the pages written so far are unreferenced): the next tier converts it
-        // again (the growth step: at larger page / heap / table capacities), or only the
-        // status changes
-        const int cc = w.cap_cause;   // pages 7, heap 3, table 8: capacities the growth step raises
-        if ((pc.tight || (pc.grow && (cc == 7 || cc == 3 || cc == 8))) && w.status == MT_DOC_CAPACITY) {
-            pg_handover<T>(st, doc, k0, pc);
-        } else if (lane() == 0) {
-            st.hdr[doc].status = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
-            st.retry[doc] = 0;
-        }
-        return;
-    }
-    const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
-    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
-    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
-    int pk_ut = 0, pk_heap = 0;
-    int64_t spill_at = -1;
-    for (int64_t kb = k0; kb < k1 && w.status == 0 && spill_at < 0; kb += MT_WAVE) {
-        const int64_t k = kb + lane();
-        v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        int nl = 0, pok = 0;
-        if (k < k1) {
-            r0 = o4[2 * k];
-            r1 = o4[2 * k + 1];
-            const int kind = (r1.w >> 16) & 0xFF, flags = ((uint32_t)r1.w >> 24) & 0xFF;
-            const int len = r1.x;
-            if (kind == MT_OP_INSERT && !(flags & MT_F_MARKER) && len > 0) {
-                const GLB_AS uint16_t *src = gt + (uint32_t)r1.y;
-                nl = src[len - 1] == '\n';
-                if (len <= 8) {
-                    pok = 1;
-                    uint32_t u[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) u[j] = j < len ? src[j] : 0u;
-                    w0 = u[0] | (u[1] << 16);
-                    w1 = u[2] | (u[3] << 16);
-                    w2 = u[4] | (u[5] << 16);
-                    w3 = u[6] | (u[7] << 16);
-                }
-            }
-        }
-        const int cnt = (int)min((int64_t)MT_WAVE, k1 - kb);
-        for (int j = 0; j < cnt && w.status == 0; j++) {
-            OpIn in;
-            in.op.seq = __builtin_amdgcn_readlane(r0.x, j);
-            in.op.ref_seq = __builtin_amdgcn_readlane(r0.y, j);
-            in.op.min_seq = __builtin_amdgcn_readlane(r0.z, j);
-            in.op.pos1 = __builtin_amdgcn_readlane(r0.w, j);
-            in.op.pos2 = __builtin_amdgcn_readlane(r1.x, j);
-            in.op.payload = (uint32_t)__builtin_amdgcn_readlane(r1.y, j);
-            in.op.props = (uint32_t)__builtin_amdgcn_readlane(r1.z, j);
-            const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane(r1.w, j);
-            in.op.client = (uint16_t)(cw & 0xFFFF);
-            in.op.kind = (uint8_t)((cw >> 16) & 0xFF);
-            in.op.flags = (uint8_t)(cw >> 24);
-            in.pay_lo = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w0, j) |
-                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w1, j) << 32);
-            in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
-                        ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
-            in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
-            in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
-            if ((pc.tight || pc.grow) && !pg_room(pd, in.op)) {
-                spill_at = kb + j;
-                break;
-            }
-            pg_apply_op(pd, in, gt, gp);
-            pk_ut = max(pk_ut, pd.ut_n);
-            pk_heap = max(pk_heap, w.heap_n);
-        }
-    }
-    // a window capacity is a paged-layout capacity: there is no further tier
-    if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
-    pg_store(pd, st);
-    pg_peaks(st, pd, pk_ut, pk_heap);
-    if (spill_at >= 0 && w.status == 0)
-        pg_handover<T>(st, doc, spill_at, pc);
-    else if (k1 < kend && w.status == 0) {   // slice done: the next launch of this stage resumes
-        if (lane() == 0) st.resume[doc] = k1;
-    } else if (lane() == 0)
-        st.retry[doc] = 0;
-#ifdef MT_PROF
-    if (lane() < 32) atomicAdd(&g_prof[lane()], w.prof[lane()]);
-#endif
-}
-
-// Generator for documents that outgrew the LDS tier: regenerated from the start in the
-// paged layout (the draws are identical, so the op stream is the same).
-// A tight launch hands a document that could outgrow its LDS capacities to the next launch,
-// which regenerates it from the start (the draws are identical).
-template <class T>
-__global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_cfg cfg, uint32_t doc_base,
-                                                            mt_op_rec *ops_out, uint16_t *text_out,
-                                                            uint32_t *props_out, int64_t tstride,
-                                                            int64_t pstride, int32_t *fail_out,
-                                                            int32_t *dbg_len, int64_t *used_out, PagedCaps pc) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
-    const int doc = blockIdx.x;
-    if (doc >= st.n_docs) return;
-    if (st.retry[doc] != pc.stage) return;
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 2 * (cfg.writers + 1), (int)sizeof(typename T::O_v));
-    GenCtx g;
-    gen_begin(g, st, cfg, (int)(doc_base + doc), doc, smem + L.offGen, tstride, pstride);
-    PagedDoc<T> pd;
-    pg_setup(pd, st, doc, smem, L, pc);
-    DocT<T> &w = pd.w;
-    if (w.status || !pg_convert(pd, flat_src(st, doc))) {
-        if (lane() == 0) {
-            if (pc.tight && w.status == MT_DOC_CAPACITY) {
-                st.retry[doc] = 2;
-                atomicAdd(st.stats + 12, 1u);
-            } else {
-                fail_out[doc] = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
-                st.retry[doc] = 0;
-            }
-        }
-        return;
-    }
-    const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)(text_out + g.tb);
-    const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)(props_out + g.pb);
-    int pk_ut = 0, pk_heap = 0;
-    for (int t = 1; t <= cfg.ops && w.status == 0; t++) {
-        int r, c, msn;
-        gen_pick(g, cfg, t, r, c, msn);
-        w.ocs = oslot_of(w, c);
-        const int len = pg_views(pd, r, c);
-        if (dbg_len && lane() == 0) {
-            int32_t *q = dbg_len + ((int64_t)doc * cfg.ops + (t - 1)) * 4;
-            q[0] = len;
-            q[1] = -1;
-            q[2] = r;
-            q[3] = c;
-        }
-        OpIn in;
-        gen_op(g, cfg, t, r, c, msn, len, in, ops_out, text_out, props_out, doc);
-        if (pc.tight && !pg_room(pd, in.op)) {
-            if (lane() == 0) {
-                st.retry[doc] = 2;
-                atomicAdd(st.stats + 12, 1u);
-            }
-            return;
-        }
-        pg_apply_op(pd, in, gt, gp);
-        pk_ut = max(pk_ut, pd.ut_n);
-        pk_heap = max(pk_heap, w.heap_n);
-    }
-    gen_end(g, used_out, doc);
-    if (w.status == MT_DOC_RETRY) w.status = MT_DOC_CAPACITY;
-    if (lane() == 0) {
-        if (w.status) fail_out[doc] = w.status;
-        st.retry[doc] = 0;
-    }
-    pg_store(pd, st);
-    pg_peaks(st, pd, pk_ut, pk_heap);
-}
-
-// A summary header staged by k_load_header (LoadScratch) becomes a paged document at the
-// handle's full paged capacities (pg_convert from the staging buffers); the body appends
-// then replay like any paged document's messages.
-template <class T>
-__global__ void __launch_bounds__(MT_WAVE) k_load_convert(DevState st, LoadScratch sc, PagedCaps pc, int lo) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
-    const int r = blockIdx.x, doc = lo + r;   // summary r of the set -> document lo + r
-    if (doc >= st.n_docs || sc.off[2 * r] < 0 || st.hdr[doc].status) return;
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v));
-    PagedDoc<T> pd;
-    pg_setup(pd, st, doc, smem, L, pc);
-    DocT<T> &w = pd.w;
-    FlatSrc src;
-    src.A = (GLB_AS const v4i *)(sc.A + sc.off[2 * r]);
-    src.O = (GLB_AS const u64 *)(sc.O + sc.off[2 * r]);
-    src.Bv = (GLB_AS const v4u *)(sc.B + sc.off[2 * r]);
-    src.cnt = (GLB_AS const uint8_t *)(sc.cnt + MT_LV * sc.off[2 * r + 1]);
-    src.flg = (GLB_AS const int8_t *)(sc.flg + sc.off[2 * r + 1]);
-    src.heap = nullptr;   // a fresh collaboration: heap_n == 0
-    src.B = (size_t)w.hp->n_blk[0];
-    src.os = src.ob = nullptr;   // canonical ordinals (pg_convert re-derives them)
-    if (w.status == 0 && pg_convert(pd, src)) {
-        pg_store(pd, st);
-    } else if (lane() == 0) {
-        st.hdr[doc].status = w.status == MT_DOC_RETRY || w.status == 0 ? MT_DOC_CAPACITY : w.status;
-        st.hdr[doc].pad[HDR_DIAG] = w.cap_cause;
     }
 }
 
@@ -1320,6 +648,69 @@ struct mt_batch {
         }                                                                          \
     } while (0)
 
+// Launches through the kernel pointers of mt_variants.h (hipLaunchKernel with the kernels'
+// exact parameter types; errors are read with hipGetLastError as for hipLaunchKernelGGL)
+static void launch_replay(const void *k, dim3 g, dim3 b, size_t lds, hipStream_t s, DevState st, const mt_op_rec *ops,
+                          const int64_t *off, const uint16_t *tin, const uint32_t *pin, TierCaps caps) {
+    void *a[] = {&st, &ops, &off, &tin, &pin, &caps};
+    (void)hipLaunchKernel(k, g, b, a, lds, s);
+}
+static void launch_replay_paged(const void *k, dim3 g, dim3 b, size_t lds, hipStream_t s, DevState st,
+                                const mt_op_rec *ops, const int64_t *off, const uint16_t *tin, const uint32_t *pin,
+                                int use_resume, PagedCaps pc, PagedSlice sl) {
+    void *a[] = {&st, &ops, &off, &tin, &pin, &use_resume, &pc, &sl};
+    (void)hipLaunchKernel(k, g, b, a, lds, s);
+}
+static void launch_generate(const void *k, dim3 g, dim3 b, size_t lds, hipStream_t s, DevState st, mt_gen_cfg cfg,
+                            uint32_t doc_base, mt_op_rec *ops_out, uint16_t *text_out, uint32_t *props_out,
+                            int64_t tstride, int64_t pstride, int32_t *fail_out, int32_t *dbg_len, int64_t *used_out,
+                            TierCaps caps) {
+    void *a[] = {&st, &cfg, &doc_base, &ops_out, &text_out, &props_out, &tstride, &pstride, &fail_out, &dbg_len,
+                 &used_out, &caps};
+    (void)hipLaunchKernel(k, g, b, a, lds, s);
+}
+static void launch_generate_paged(const void *k, dim3 g, dim3 b, size_t lds, hipStream_t s, DevState st,
+                                  mt_gen_cfg cfg, uint32_t doc_base, mt_op_rec *ops_out, uint16_t *text_out,
+                                  uint32_t *props_out, int64_t tstride, int64_t pstride, int32_t *fail_out,
+                                  int32_t *dbg_len, int64_t *used_out, PagedCaps pc) {
+    void *a[] = {&st, &cfg, &doc_base, &ops_out, &text_out, &props_out, &tstride, &pstride, &fail_out, &dbg_len,
+                 &used_out, &pc};
+    (void)hipLaunchKernel(k, g, b, a, lds, s);
+}
+static void launch_load_convert(const void *k, dim3 g, dim3 b, size_t lds, hipStream_t s, DevState st, LoadScratch sc,
+                                PagedCaps pc, int lo) {
+    void *a[] = {&st, &sc, &pc, &lo};
+    (void)hipLaunchKernel(k, g, b, a, lds, s);
+}
+
+// folds a batch's latest refSeq per client into the handle's (segment read-outs)
+static void track_views(mt_handle *h, const mt_batch *b) {
+    if (h->lastref.size() != h->n_docs) h->lastref.assign(h->n_docs, {});
+    if (h->untracked.size() != h->n_docs) h->untracked.assign(h->n_docs, 0);
+    if (b->generated) {
+        std::fill(h->untracked.begin(), h->untracked.end(), 1);
+        return;
+    }
+    if (b->lr_off.size() != (size_t)h->n_docs + 1) return;
+    for (uint32_t d = 0; d < h->n_docs; d++) {
+        auto &v = h->lastref[d];
+        for (int64_t i = b->lr_off[d]; i < b->lr_off[d + 1]; i++) {
+            const auto &e = b->lr[i];
+            auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(e.first, INT32_MIN));
+            if (it != v.end() && it->first == e.first)
+                it->second = std::max(it->second, e.second);
+            else
+                v.insert(it, e);
+        }
+    }
+}
+static void untrack_views(mt_handle *h, uint32_t lo, uint32_t n) {
+    if (h->lastref.size() == h->n_docs)
+        for (uint32_t d = lo; d < lo + n; d++) h->lastref[d].clear();
+    if (h->untracked.size() == h->n_docs)
+        for (uint32_t d = lo; d < lo + n; d++) h->untracked[d] = 0;
+}
+
 static int mt_settle(mt_handle *h);
 // waits for the stream and finishes a pending growth step (API entry points that read state or
 // enqueue work: a growth step's launches must come before anything else)
@@ -1446,15 +837,15 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
             return nullptr;
         }
         if (lb > 64 * 1024) {
-            const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true>>, (const void *)k_replay_paged<TierPagedT<false>>,
-                                (const void *)k_generate_paged<TierPagedT<false>>,
-                                (const void *)k_replay_paged<TierPagedT<true, true>>,
-                                (const void *)k_replay_paged<TierPagedT<false, true>>,
-                                (const void *)k_generate_paged<TierPagedT<false, true>>,
-                                (const void *)k_load_convert<TierPagedT<false>>,
-                                (const void *)k_load_convert<TierPagedT<true>>,
-                                (const void *)k_replay_paged<TierPagedT<true, false, false, true>>,
-                                (const void *)k_replay_paged<TierPagedT<false, false, false, true>>};
+            const void *ks[] = {MTK(P_LOG), MTK(P_FULL),
+                                MTK(GP_FULL),
+                                MTK(P_NARROW_LOG),
+                                MTK(P_NARROW),
+                                MTK(GP_NARROW),
+                                MTK(LC_FAST),
+                                MTK(LC_LOG),
+                                MTK(P_PACKED_LOG),
+                                MTK(P_PACKED)};
             for (const void *k : ks)
                 if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb) != hipSuccess) {
                     delete h;
@@ -1466,10 +857,10 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         if (h->paged_slices > 1) {
             const PagedCaps &c = h->pg_tight.PP ? h->pg_tight : h->pg_full;
             const size_t lt = paged_layout(c.PP, c.PH, c.UT, 0, c.narrow ? 4 : 8).total;
-            const void *k = st.DL ? (c.narrow ? (const void *)k_replay_paged<TierPagedT<true, true>>
-                                              : (const void *)k_replay_paged<TierPagedT<true>>)
-                                  : (c.narrow ? (const void *)k_replay_paged<TierPagedT<false, true>>
-                                              : (const void *)k_replay_paged<TierPagedT<false>>);
+            const void *k = st.DL ? (c.narrow ? MTK(P_NARROW_LOG)
+                                              : MTK(P_LOG))
+                                  : (c.narrow ? MTK(P_NARROW)
+                                              : MTK(P_FULL));
             int per_cu = 0, cus = 0;
             hipDeviceProp_t prop;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, MT_WAVE, lt) == hipSuccess &&
@@ -1730,65 +1121,37 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     // the bench's C3 tight tier with its capacities fixed at compile time (same code, constant
     // LDS layout: bench.capacities)
     if (!big && !pc.packed && pc.narrow && !h->st.DL && pc.PP == 192 && pc.PH == 192 && pc.UT == 220)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true, false, false, 192, 192, 220>>), g, blk, lb, h->stream,
+        launch_replay_paged(MTK(P_C3), g, blk, lb, h->stream,
                            h->st, b->ops, b->off, b->text, b->props, res, pc, sl);
     else if (!big && pc.packed && !h->st.DL && pc.PP == 224 && pc.PH == 900 && pc.UT == 1900)   // the bench's C4 tier
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, false, false, true, 224, 900, 1900>>), g, blk, lb, h->stream,
+        launch_replay_paged(MTK(P_C4), g, blk, lb, h->stream,
                            h->st, b->ops, b->off, b->text, b->props, res, pc, sl);
     else if (pc.packed && h->st.DL)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+        launch_replay_paged(MTK(P_PACKED_LOG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
     else if (pc.packed)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, false, false, true>>), g, blk, lb, h->stream, h->st,
+        launch_replay_paged(MTK(P_PACKED), g, blk, lb, h->stream, h->st,
                            b->ops, b->off, b->text, b->props, res, pc, sl);
     else if (big && h->st.DL)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+        launch_replay_paged(MTK(P_BIG_LOG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
     else if (big)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, false, true>>), g, blk, lb, h->stream, h->st, b->ops,
+        launch_replay_paged(MTK(P_BIG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
     else if (h->st.DL && pc.narrow)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+        launch_replay_paged(MTK(P_NARROW_LOG), g, blk, lb, h->stream, h->st, b->ops, b->off,
                            b->text, b->props, res, pc, sl);
     else if (h->st.DL)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<true>>), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
+        launch_replay_paged(MTK(P_LOG), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
                            b->props, res, pc, sl);
     else if (pc.narrow)
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false, true>>), g, blk, lb, h->stream, h->st, b->ops, b->off,
+        launch_replay_paged(MTK(P_NARROW), g, blk, lb, h->stream, h->st, b->ops, b->off,
                            b->text, b->props, res, pc, sl);
     else
-        hipLaunchKernelGGL((k_replay_paged<TierPagedT<false>>), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
+        launch_replay_paged(MTK(P_FULL), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
                            b->props, res, pc, sl);
     HIPCHK(h, hipGetLastError());
     return 0;
-}
-
-// folds a batch's latest refSeq per client into the handle's (segment read-outs)
-static void track_views(mt_handle *h, const mt_batch *b) {
-    if (h->lastref.size() != h->n_docs) h->lastref.assign(h->n_docs, {});
-    if (h->untracked.size() != h->n_docs) h->untracked.assign(h->n_docs, 0);
-    if (b->generated) {
-        std::fill(h->untracked.begin(), h->untracked.end(), 1);
-        return;
-    }
-    if (b->lr_off.size() != (size_t)h->n_docs + 1) return;
-    for (uint32_t d = 0; d < h->n_docs; d++) {
-        auto &v = h->lastref[d];
-        for (int64_t i = b->lr_off[d]; i < b->lr_off[d + 1]; i++) {
-            const auto &e = b->lr[i];
-            auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(e.first, INT32_MIN));
-            if (it != v.end() && it->first == e.first)
-                it->second = std::max(it->second, e.second);
-            else
-                v.insert(it, e);
-        }
-    }
-}
-static void untrack_views(mt_handle *h, uint32_t lo, uint32_t n) {
-    if (h->lastref.size() == h->n_docs)
-        for (uint32_t d = lo; d < lo + n; d++) h->lastref[d].clear();
-    if (h->untracked.size() == h->n_docs)
-        for (uint32_t d = lo; d < lo + n; d++) h->untracked[d] = 0;
 }
 
 int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
@@ -1805,22 +1168,22 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         // LDS tier for every document; the ones that outgrow it are flagged and replayed
         // from HBM by the second launch (whose other workgroups exit at once)
         if (h->live && h->st.DL)
-            hipLaunchKernelGGL((k_replay<TierLiveLdsT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE),
+            launch_replay(MTK(R_LIVELDS_LOG), dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(true, h->lds, 0), h->stream, h->st, b->ops, b->off, b->text, b->props,
                                h->lds);
         else if (h->live)
-            hipLaunchKernelGGL((k_replay<TierLiveLdsT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE),
+            launch_replay(MTK(R_LIVELDS), dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(true, h->lds, 0), h->stream, h->st, b->ops, b->off, b->text, b->props,
                                h->lds);
         else if (h->st.DL)
-            hipLaunchKernelGGL((k_replay<TierLdsT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+            launch_replay(MTK(R_LDS_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
                                h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
         else if (h->wpg == 2)
-            hipLaunchKernelGGL((k_replay<TierLdsT<false>, 2>), dim3((h->n_docs + 1) / 2), dim3(2 * MT_WAVE),
+            launch_replay(MTK(R_LDS2), dim3((h->n_docs + 1) / 2), dim3(2 * MT_WAVE),
                                2 * tier_lds_bytes(true, h->lds, 0), h->stream, h->st, b->ops, b->off, b->text, b->props,
                                h->lds);
         else
-            hipLaunchKernelGGL((k_replay<TierLdsT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
+            launch_replay(MTK(R_LDS), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, 0),
                                h->stream, h->st, b->ops, b->off, b->text, b->props, h->lds);
         HIPCHK(h, hipGetLastError());
     } else {
@@ -1875,16 +1238,16 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
             }
         }
     } else if (h->live && h->st.DL)
-        hipLaunchKernelGGL((k_replay<TierLiveT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+        launch_replay(MTK(R_LIVE_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     else if (h->live)
-        hipLaunchKernelGGL((k_replay<TierLiveT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+        launch_replay(MTK(R_LIVE), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     else if (h->st.DL)
-        hipLaunchKernelGGL((k_replay<TierGlbT<true>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+        launch_replay(MTK(R_GLB_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     else
-        hipLaunchKernelGGL((k_replay<TierGlbT<false>, 1>), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
+        launch_replay(MTK(R_GLB), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
@@ -2024,8 +1387,8 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
     h->big_caps = PagedCaps{c.PP, c.PH, c.UT, 0, 3, 0, 1};
     const size_t lb = paged_layout(c.PP, c.PH, c.UT, 0, 8).total;
     if (lb > 64 * 1024) {
-        const void *ks[] = {(const void *)k_replay_paged<TierPagedT<true, false, true>>,
-                            (const void *)k_replay_paged<TierPagedT<false, false, true>>};
+        const void *ks[] = {MTK(P_BIG_LOG),
+                            MTK(P_BIG)};
         for (const void *k : ks) HIPCHK(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
     }
     return 0;
@@ -2426,10 +1789,10 @@ int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
         const PagedCaps &pc = h->pg_full;
         const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, 8).total;
         if (h->ordinals)   // canonical ordinals for the paged documents (reloadFromSegments)
-            hipLaunchKernelGGL(k_load_convert<TierPagedT<true>>, dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+            launch_load_convert(MTK(LC_LOG), dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
                                s->sc, pc, (int)s->doc_lo);
         else
-            hipLaunchKernelGGL(k_load_convert<TierPagedT<false>>, dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
+            launch_load_convert(MTK(LC_FAST), dim3(s->n_docs), dim3(MT_WAVE), lb, h->stream, h->st,
                                s->sc, pc, (int)s->doc_lo);
         HIPCHK(h, hipGetLastError());
     }
@@ -2576,7 +1939,7 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
     if (ok) {
         const int gw = 2 * (cfg->writers + 1);
         if (h->lds.S > 0) {
-            hipLaunchKernelGGL(k_generate<TierLdsT<false>>, dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, gw),
+            launch_generate(MTK(G_LDS), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(true, h->lds, gw),
                                h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
                                pstride, d_fail, d_trace, d_used, h->lds);
             ok = hipGetLastError() == hipSuccess;
@@ -2589,18 +1952,18 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
                 if (!pc || !ok) continue;
                 const size_t lb = paged_layout(pc->PP, pc->PH, pc->UT, gw, pc->narrow ? 4 : 8).total;
                 if (pc->narrow)
-                    hipLaunchKernelGGL((k_generate_paged<TierPagedT<false, true>>), dim3(h->n_docs), dim3(MT_WAVE), lb,
+                    launch_generate_paged(MTK(GP_NARROW), dim3(h->n_docs), dim3(MT_WAVE), lb,
                                        h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
                                        pstride, d_fail, d_trace, d_used, *pc);
                 else
-                    hipLaunchKernelGGL((k_generate_paged<TierPagedT<false>>), dim3(h->n_docs), dim3(MT_WAVE), lb,
+                    launch_generate_paged(MTK(GP_FULL), dim3(h->n_docs), dim3(MT_WAVE), lb,
                                        h->stream, h->st, *cfg, doc_index_base, b->ops, b->text, b->props, tstride,
                                        pstride, d_fail, d_trace, d_used, *pc);
                 ok = hipGetLastError() == hipSuccess;
             }
             ok = ok && hipStreamSynchronize(h->stream) == hipSuccess;
         } else if (ok) {
-            hipLaunchKernelGGL(k_generate<TierGlbT<false>>, dim3(h->n_docs), dim3(MT_WAVE),
+            launch_generate(MTK(G_GLB), dim3(h->n_docs), dim3(MT_WAVE),
                                tier_lds_bytes(false, glb_caps(h), gw), h->stream, h->st, *cfg, doc_index_base,
                                b->ops, b->text, b->props, tstride, pstride, d_fail, d_trace, d_used, glb_caps(h));
             ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
