@@ -182,6 +182,7 @@ struct DevState {
     int32_t *grp;             // [n_docs][LG + 1][MT_GRP_WORDS] segment-group table (index = id)
     struct PendQ *segP;       // [n_docs][S] per segment: its pending segment groups
     int32_t LG;               // group ids per document (outstanding segment groups)
+    unsigned long long *prof; // [128] section timers of a -DMT_PROF build (null otherwise)
 };
 
 __host__ __device__ inline PagedRegion main_region(const DevState &st) {

@@ -208,7 +208,7 @@ template <class T> struct DocT {
     GLB_AS u64 *P;          // [S][4] each segment's pending segment groups (mt_device.h PendQ)
     int LG;                 // group ids 1..LG
 #ifdef MT_PROF
-    LDS_AS u64 *prof;       // [32] section timers
+    LDS_AS u64 *prof;       // [128] section timers: ticks [0, 64), calls / counts [64, 128)
 #endif
 };
 
@@ -227,24 +227,23 @@ TD void pq_put(DocT<T> &d, int i, const PendQ &q) {
 }
 
 #ifdef MT_PROF
-__device__ unsigned long long g_prof[32];
 // per-wave accumulators live in LDS (no global atomics inside the timed sections: they
-// would be waited for by the engine's s_waitcnt vmcnt(0))
+// would be waited for by the engine's s_waitcnt vmcnt(0)); added to DevState.prof at the end
 #define PROF_WRAP_BEGIN const unsigned long long _t0 = __builtin_amdgcn_s_memtime();
 #define PROF_WRAP_END(k)                                                              \
     if (lane() == 0) {                                                                \
         d.prof[k] += __builtin_amdgcn_s_memtime() - _t0;                              \
-        d.prof[16 + k] += 1ull;                                                       \
+        d.prof[64 + k] += 1ull;                                                       \
     }
 #endif
 
-// MT_PROF2 (with MT_PROF, flat documents only): finer timers in paged slots 9..15
+// MT_PROF2 (with MT_PROF): finer timers, P2 slot k (9..15) in slot k + 17
 #if defined(MT_PROF) && defined(MT_PROF2)
 #define P2_T0(k) const unsigned long long _p2##k = __builtin_amdgcn_s_memtime();
 #define P2_T1(k)                                                         \
     if (lane() == 0) {                                                   \
-        d.prof[k] += __builtin_amdgcn_s_memtime() - _p2##k;              \
-        d.prof[16 + k] += 1ull;                                          \
+        d.prof[k + 17] += __builtin_amdgcn_s_memtime() - _p2##k;         \
+        d.prof[64 + k + 17] += 1ull;                                     \
     }
 #else
 #define P2_T0(k)
@@ -313,7 +312,7 @@ static __host__ __device__ inline LdsLayout lds_layout(bool seg_in_lds, int S, i
     L.offFlg = o; o += (uint32_t)B;
 #ifdef MT_PROF
     o = (o + 7u) & ~7u;
-    L.offProf = o; o += 32u * 8;
+    L.offProf = o; o += 128u * 8;
 #else
     L.offProf = 0;
 #endif
@@ -439,7 +438,8 @@ TD bool load_doc(DocT<T> &d, const DevState &st, int doc, LDS_AS uint8_t *smem, 
     d.flg = (LDS_AS int8_t *)(smem + L.offFlg);
 #ifdef MT_PROF
     d.prof = (LDS_AS u64 *)(smem + L.offProf);
-    if (lane() < 32) d.prof[lane()] = 0;
+    d.prof[lane()] = 0;
+    d.prof[64 + lane()] = 0;
 #endif
     GLB_AS const uint8_t *gcnt = (GLB_AS const uint8_t *)(st.cnt + doc * (size_t)MT_LV * B);
     GLB_AS const int8_t *gflg = (GLB_AS const int8_t *)(st.flg + doc * B);

@@ -174,7 +174,10 @@ __global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_
     }
     if (!T::kLds && lane() == 0) st.retry[doc] = 0;
 #ifdef MT_PROF
-    if (lane() < 32) atomicAdd(&g_prof[lane()], d.prof[lane()]);
+    if (st.prof) {
+        atomicAdd(&st.prof[lane()], d.prof[lane()]);
+        atomicAdd(&st.prof[64 + lane()], d.prof[64 + lane()]);
+    }
 #endif
     store_doc(d, st, doc);
 }
@@ -580,7 +583,10 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     } else if (lane() == 0)
         st.retry[doc] = 0;
 #ifdef MT_PROF
-    if (lane() < 32) atomicAdd(&g_prof[lane()], w.prof[lane()]);
+    if (st.prof) {
+        atomicAdd(&st.prof[lane()], w.prof[lane()]);
+        atomicAdd(&st.prof[64 + lane()], w.prof[64 + lane()]);
+    }
 #endif
 }
 

@@ -26,11 +26,14 @@
 #define PG_T1(k)                                                         \
     if (lane() == 0) {                                                   \
         pd.w.prof[k] += __builtin_amdgcn_s_memtime() - _pt##k;           \
-        pd.w.prof[16 + k] += 1ull;                                       \
+        pd.w.prof[64 + k] += 1ull;                                       \
     }
+#define PG_CNT(k)                                                        \
+    if (lane() == 0) pd.w.prof[64 + k] += 1ull;
 #else
 #define PG_T0(k)
 #define PG_T1(k)
+#define PG_CNT(k)
 #endif
 
 template <class T> struct PagedDoc {
@@ -114,7 +117,7 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     L.offUcnt = o; o += (uint32_t)(pcnt_bytes(PP) - PP);   // levels >= 1 (level 0 is the window's)
 #ifdef MT_PROF
     o = (o + 7u) & ~7u;
-    L.offProf = o; o += 32u * 8;
+    L.offProf = o; o += 128u * 8;
 #else
     L.offProf = 0;
 #endif
@@ -532,6 +535,7 @@ TD void pg_split_page(PagedDoc<T> &pd) {
         pg_fail_cap(w, 7);
         return;
     }
+    PG_CNT(25)
     const int pos = pg_cur_pos(pd);
     // table: the window's entries are rebuilt now (first half under this page, second half
     // under the new one), so it never holds both a stale and a fresh copy of a segment
@@ -641,10 +645,17 @@ TD void pg_win_flush_impl(PagedDoc<T> &pd) {
     w.dlo = 0;
 #endif
     if (w.dlo < w.n) {   // some slot changed: its table entries and the slots from dlo on
+        PG_CNT(23)
+        PG_T0(33)
         pg_table_purge(pd, pd.cur);
+        PG_T1(33)
+        PG_T0(34)
         pg_table_add(pd, 0, w.n, pd.cur);
+        PG_T1(34)
         if (w.status) return;
+        PG_T0(35)
         pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0), w.dlo);
+        PG_T1(35)
     }
     w.dlo = MT_PG_SLOTS;
     pd.dirty = 0;
@@ -694,6 +705,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
     }
     wsync<T>();
     const int cur = pd.cur;
+    PG_T0(36)
     for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
         const int e = base + lane();
         if (e < pd.ut_n) {
@@ -705,6 +717,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
             if (dlt && pg != cur) atomicAdd((int *)(pd.pvl + pg), dlt);
         }
     }
+    PG_T1(36)
     if (cur >= 0) {   // the window's page: its own slots are authoritative
         DocT<T> &w = pd.w;
         const int i = lane();
@@ -765,7 +778,10 @@ TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart
 // the window onto level-1 position pos, whose observer start is obs_base
 TD void pg_load_pos(PagedDoc<T> &pd, int pos, int obs_base) {
     const int pg = uni(pd.up.dir[pos]);
-    if (pd.cur != pg) pg_win_switch(pd, pg);
+    if (pd.cur != pg) {
+        PG_CNT(24)
+        pg_win_switch(pd, pg);
+    }
     pd.cur_pos = pos;
     pd.w.obs_base = obs_base;
 }
@@ -949,17 +965,28 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         heap_pop(w);
         wsync<T>();
         PG_T1(5)
+        PG_CNT(16)
         PG_T0(4)
-        if (uid == 0) continue;   // its segment was merged or unlinked before a renumbering
+        if (uid == 0) {   // its segment was merged or unlinked before a renumbering
+            PG_CNT(17)
+            continue;
+        }
         // the window first (its uid map entries are written when it is flushed)
         int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
         if (i < 0) {
             const int pg = uni(gpg);
-            if (pg == pd.cur || pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) continue;
+            if (pg == pd.cur || pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) {
+                PG_CNT(19)
+                continue;
+            }
+            PG_CNT(18)
             pg_win_switch(pd, pg);
             if (w.status) return;
             i = find_uid(w, uid);
-            if (i < 0) continue;
+            if (i < 0) {
+                PG_CNT(19)
+                continue;
+            }
         }
         PG_T1(4)
         int bstart;
@@ -970,7 +997,11 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         }
         const int f = flgr(w, b);
         const int old = cntr(w, 0, b);
-        if (f == 0) continue;
+        if (f == 0) {
+            PG_CNT(20)
+            continue;
+        }
+        PG_CNT(21)
         if (ordon(w) && w.rich) w.obs_base = pg_obs_start(pd);   // scour event positions
         PG_T0(2)
         const int kept = scour_range(w, bstart, b, 1);
@@ -990,6 +1021,7 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         pg_win_sync(pd);
         if (w.status) return;
         if (pk) {
+            PG_CNT(22)
             pg_pack1(pd, pg_cur_pos(pd));
             if (w.status) return;
         }
@@ -1467,7 +1499,8 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     w.nb = (LDS_AS int32_t *)(smem + L.offWnb);
 #ifdef MT_PROF
     w.prof = (LDS_AS u64 *)(smem + L.offProf);
-    if (lane() < 32) w.prof[lane()] = 0;
+    w.prof[lane()] = 0;
+    w.prof[64 + lane()] = 0;
 #endif
     const DocHdr h = *w.hp;
     w.n = 0;

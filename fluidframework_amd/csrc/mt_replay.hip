@@ -890,6 +890,10 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     alloc((void **)&st.retry, N * sizeof(int32_t));
     alloc((void **)&st.resume, N * sizeof(int64_t));
     alloc((void **)&st.stats, 16 * sizeof(uint32_t));
+#ifdef MT_PROF
+    alloc((void **)&st.prof, 128 * sizeof(unsigned long long));
+    if (ok) ok = hipMemset(st.prof, 0, 128 * sizeof(unsigned long long)) == hipSuccess;
+#endif
     if (h->ordinals) {
         alloc((void **)&st.ordS, N * (size_t)st.S * sizeof(uint16_t));
         alloc((void **)&st.ordB, N * (size_t)MT_LV * st.B * sizeof(uint16_t));
@@ -949,7 +953,7 @@ void mt_destroy(mt_handle *h) {
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
                   st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot,
-                  st.live, st.grp, st.segP, st.ordS, st.ordB, st.pgOS, st.pgOL, st.pgOU};
+                  st.live, st.grp, st.segP, st.ordS, st.ordB, st.pgOS, st.pgOL, st.pgOU, st.prof};
     for (void *p : ps)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -2601,17 +2605,15 @@ int mt_delta_log_reset(mt_handle *h) {
     return 0;
 }
 
-// Debug: section timers of an MT_PROF build (s_memtime ticks and call counts, 16 + 16).
+// Debug: section timers of an MT_PROF build (s_memtime ticks [0, 64) and call / event counts
+// [64, 128)).
 int mt_debug_prof(mt_handle *h, uint64_t *out, int reset) {
 #ifdef MT_PROF
-    if (!h) return MT_E_INVALID;
+    if (!h || !h->st.prof) return MT_E_INVALID;
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipDeviceSynchronize());
-    if (out) HIPCHK(h, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), 32 * sizeof(uint64_t)));
-    if (reset) {
-        uint64_t z[32] = {0};
-        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
-    }
+    if (out) HIPCHK(h, hipMemcpy(out, h->st.prof, 128 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(h, hipMemset(h->st.prof, 0, 128 * sizeof(uint64_t)));
     return 0;
 #else
     (void)h; (void)out; (void)reset;

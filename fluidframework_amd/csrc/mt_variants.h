@@ -2,8 +2,8 @@
 // X(name, kernel).  fluidframework_amd/build.py compiles each into a translation unit of its
 // own that defines `const void *mtk_<name>()` (the kernel's host pointer); the host side
 // (mt_replay.hip) launches through those pointers with hipLaunchKernel, so the ~25 large
-// kernels compile in parallel.  -DMT_SINGLE_TU (the MT_PROF section-timer builds, whose
-// g_prof symbol must be one) defines them in mt_replay.hip instead.
+// kernels compile in parallel.  -DMT_SINGLE_TU (build.py MT_SINGLE_TU=1) defines them in
+// mt_replay.hip instead.
 #pragma once
 #define MT_VARIANTS(X)                                                               \
     X(R_LDS_LOG, (k_replay<TierLdsT<true>, 1>))                                      \

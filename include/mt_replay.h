@@ -295,7 +295,7 @@ int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const in
 int mt_debug_raw(mt_handle *h, uint32_t doc, uint32_t *rows, uint32_t cap_rows, uint32_t *n_rows,
                  int32_t *hdr_words);
 /* Debug: section timers of a build with -DMT_PROF (MT_E_INVALID otherwise). */
-int mt_debug_prof(mt_handle *h, uint64_t *out /* [32] */, int reset);
+int mt_debug_prof(mt_handle *h, uint64_t *out /* [128] */, int reset);
 /* Debug (flat documents): the zamboni heap in array order ({maxSeq, leaf index of its segment
    or -1} pairs) and every leaf block's needsScour flag (-1 undefined, 0, 1). */
 int mt_debug_heap(mt_handle *h, uint32_t doc, int32_t *heap, uint32_t cap, uint32_t *n_heap, int32_t *flags,
