@@ -171,9 +171,13 @@ class MergeTreeBatch:
         for ps in pool:
             free_sets.put(ps)
 
+        stop = threading.Event()   # the consumer failed: the producer stops at its next slice
+
         def produce():
             try:
                 for d0 in range(0, self.n_docs, slice_docs):
+                    if stop.is_set():
+                        return
                     d1 = min(self.n_docs, d0 + slice_docs)
                     b0, b1 = off[d0], off[d1]
                     sub = (paths[b0:b1], blobs[b0:b1], [o - b0 for o in off[d0:d1 + 1]])
@@ -196,28 +200,42 @@ class MergeTreeBatch:
         t.start()
         from .snapdec import ClientMaps
         catchup_all, clients_all, held = [], ClientMaps([]), []
-        while True:
-            item = q.get()
-            if item is None:
-                break
-            if isinstance(item, BaseException):
-                t.join()
-                raise item
-            d0, out, catchup, clients, pset = item
-            snaps = self.upload_snapshots(out, doc_lo=d0)   # synchronous copies: the set is free again
-            free_sets.put(pset)
-            snaps.load_async()
-            held.append(snaps)   # device copies stay alive until the loads have run
-            cu_msgs = [[] for _ in catchup]
-            for i, c in enumerate(catchup):
-                if c is not None:
-                    cu_msgs[i] = _json.loads(c)
-            catchup_all += cu_msgs
-            clients_all = clients_all + clients
-        t.join()
-        self.sync()
-        for s_ in held:
-            s_.free()
+        try:
+            while True:
+                item = q.get()
+                if item is None:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                d0, out, catchup, clients, pset = item
+                snaps = self.upload_snapshots(out, doc_lo=d0)   # synchronous copies: the set is free again
+                free_sets.put(pset)
+                snaps.load_async()
+                held.append(snaps)   # device copies stay alive until the loads have run
+                cu_msgs = [[] for _ in catchup]
+                for i, c in enumerate(catchup):
+                    if c is not None:
+                        cu_msgs[i] = _json.loads(c)
+                catchup_all += cu_msgs
+                clients_all = clients_all + clients
+        finally:
+            # on any exit: unblock and join the producer (it may wait for a free arena set or
+            # on the queue), finish the enqueued loads, free every uploaded snapshot set
+            stop.set()
+            while t.is_alive():
+                try:
+                    item = q.get(timeout=0.05)
+                    if isinstance(item, tuple):
+                        free_sets.put(item[4])
+                except queue.Empty:
+                    pass
+                free_sets.put({})
+            t.join()
+            try:
+                self.sync()
+            finally:
+                for s_ in held:
+                    s_.free()
         return catchup_all, clients_all
 
     def extract_snapshots_raw(self):

@@ -3,6 +3,7 @@ host summary decoder (libmtsnapdec.so).
 hipcc cross-compiles here without a GPU; the .so travels to the GPU box with the repo."""
 import os
 import re
+import shutil
 import subprocess
 import sys
 
@@ -37,10 +38,10 @@ def variants():
 def build(force=False, verbose=False):
     """One translation unit per kernel instantiation (csrc/mt_variants.h) plus the host side,
     compiled in parallel and linked into one shared library (MT_SINGLE_TU=1: the whole library
-    as one translation unit, e.g. for -DMT_PROF builds)."""
+    as one translation unit)."""
     if not force and not needs_build():
         return OUT
-    single = os.environ.get("MT_SINGLE_TU") == "1" or "-DMT_PROF" in FLAGS
+    single = os.environ.get("MT_SINGLE_TU") == "1"
     if single:
         cmd = [HIPCC] + FLAGS + ["-DMT_SINGLE_TU", "-o", OUT + ".tmp", SRC]
         if verbose:
@@ -51,8 +52,12 @@ def build(force=False, verbose=False):
     tag = os.path.splitext(os.path.basename(OUT))[0]   # variant libraries (MT_OUT) build apart
     obj_dir = os.path.join(OBJ_DIR, tag)
     os.makedirs(obj_dir, exist_ok=True)
+    # MT_ONLY=P_C3,P_C4: an A/B variant that recompiles only those kernels; the other objects
+    # come from the product build (_build/libmtreplay)
+    only = [x for x in os.environ.get("MT_ONLY", "").split(",") if x]
     cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
     jobs = [(SRC, os.path.join(obj_dir, "mt_replay.o"))]
+    link_only = []
     for name, expr in variants():
         src = os.path.join(obj_dir, f"mtk_{name}.hip")
         body = (f'#include "{os.path.join(HERE, "csrc", "mt_kernels.h")}"\n'
@@ -60,7 +65,13 @@ def build(force=False, verbose=False):
         if not os.path.exists(src) or open(src).read() != body:
             with open(src, "w") as fh:
                 fh.write(body)
-        jobs.append((src, os.path.join(obj_dir, f"mtk_{name}.o")))
+        obj = os.path.join(obj_dir, f"mtk_{name}.o")
+        if only and name not in only:
+            base_obj = os.path.join(OBJ_DIR, "libmtreplay", f"mtk_{name}.o")
+            shutil.copyfile(base_obj, obj)
+            link_only.append(obj)
+            continue
+        jobs.append((src, obj))
     par = int(os.environ.get("MT_BUILD_JOBS") or min(8, os.cpu_count() or 1))
     running, done = [], []
     pending = list(jobs)
@@ -77,7 +88,7 @@ def build(force=False, verbose=False):
                 q.wait()
             raise subprocess.CalledProcessError(p.returncode, src)
         done.append(src)
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + [o for _, o in jobs]
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + [o for _, o in jobs] + link_only
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

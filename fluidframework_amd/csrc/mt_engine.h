@@ -142,6 +142,8 @@ template <class T> __device__ __forceinline__ void wsync() {
 #define SEGF_NL 2u         // the segment's text ends with '\n' (TextSegment.canAppend :63-68)
 #define SEGF_NOMATCH 4u    // its property set holds a value matchProperties never finds equal
                            // (MT_VAL_NOMATCH_BIT: NaN / undefined from a combining op, Q4)
+#define SEGF_NONL 8u       // its text holds no '\n' at all: every piece a split makes ends
+                           // without one (the trailing-'\n' flag is known without a text read)
 #define SEGF_SLACK_SHIFT 16 // bits 16..31: arena units reserved after the text for appends
 __device__ __forceinline__ int text_slack(int len) { return min((len >> 1) + 8, 4096); }
 
@@ -1463,6 +1465,9 @@ TD void split_seg(DocT<T> &d, int i, int q) {
         rb.x = bb.x + (uint32_t)q;
         rb.z = (uint32_t)d.next_uid | (bb.z & MT_MARKER_BIT);
         bb.w &= ~(SEGF_NL_KNOWN | SEGF_NL | (0xFFFFu << SEGF_SLACK_SHIFT));
+#ifndef MT_NO_NONL
+        if (bb.w & SEGF_NONL) bb.w |= SEGF_NL_KNOWN;   // a newline-free text's left part ends without one
+#endif
         d.A[i] = a;
         d.Bv[i] = bb;
         d.A[i + 1] = r;
@@ -1717,7 +1722,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
             const uint32_t kslack = bk.w >> SEGF_SLACK_SHIFT;
             bool contig = true;
             int endp = (int)bk.x + ak, add = 0;
-            uint32_t lastw = 0;
+            uint32_t lastw = 0, nonl = bk.w & SEGF_NONL;
             for (int j = kk + 1; j < cntb && ((owners >> (4 * j)) & 0xFu) == (uint32_t)kk; j++) {
                 const v4u bj = uni4(d.Bv[s + j]);
                 const int lj = bcast(a.x, j);
@@ -1725,6 +1730,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
                 endp += lj;
                 add += lj;
                 lastw = bj.w;
+                nonl &= bj.w;
             }
             uint32_t newoff = bk.x, newslack = lastw >> SEGF_SLACK_SHIFT;
             if (!contig) {
@@ -1776,7 +1782,7 @@ TD int scour_block(DocT<T> &d, int s, int e) {
                 d.A[s + kk].x = gk;
                 v4u nb = bk;
                 nb.x = newoff;
-                nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | (newslack << SEGF_SLACK_SHIFT);
+                nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | nonl | (newslack << SEGF_SLACK_SHIFT);
                 d.Bv[s + kk] = nb;
             }
             wsync<T>();
@@ -1937,6 +1943,8 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
             const bool contig = !ballot(!contig_lane);
             const int add = gk - ak;
             const uint32_t lastw = (uint32_t)bcast((int)bm.w, ge);
+            // the merged text is newline-free when the keeper's and every member's are
+            const uint32_t nonl = (bk.w & SEGF_NONL) && !ballot(mem && !(bm.w & SEGF_NONL)) ? SEGF_NONL : 0u;
             uint32_t newoff = bk.x, newslack = lastw >> SEGF_SLACK_SHIFT;
             if (!contig) {
                 int dst;
@@ -1979,7 +1987,7 @@ TD int scour_range(DocT<T> &d, int s, int b0, int nbk) {
                 d.A[s + kk].x = gk;
                 v4u nb = bk;
                 nb.x = newoff;
-                nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | (newslack << SEGF_SLACK_SHIFT);
+                nb.w = (lastw & (SEGF_NL_KNOWN | SEGF_NL)) | nonl | (newslack << SEGF_SLACK_SHIFT);
                 d.Bv[s + kk] = nb;
             }
             wsync<T>();
@@ -2181,6 +2189,8 @@ struct OpIn {
     u64 pay_lo, pay_hi;   // units 0..3 / 4..7 when pay_ok
     bool pay_ok;
     bool nl;
+    bool pay_lane = false;   // pay_ok, with lane j's unit in pay_v (a load issued with the message)
+    uint32_t pay_v = 0;
 };
 
 __device__ __forceinline__ uint16_t pay_unit(const OpIn &in, int j) {
@@ -2375,13 +2385,29 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
     } else {
         toff = (uint32_t)d.text_top;
         GLB_AS uint16_t *dst = text_base(d, d.text_half) + d.text_top;
+        // the payload (<= 8 units prefetched with the record, else read from the batch); its last
+        // unit decides TextSegment.canAppend's trailing-'\n' rule
+        bool anynl = false, lastnl = false;
         if (in.pay_ok) {
-            if (lane() < slen) dst[lane()] = pay_unit(in, lane());
+            const uint16_t u = lane() < slen ? (in.pay_lane ? (uint16_t)in.pay_v : pay_unit(in, lane())) : (uint16_t)0;
+            if (lane() < slen) dst[lane()] = u;
+            anynl = ballot(lane() < slen && u == (uint16_t)'\n') != 0ull;
+            lastnl = ballot(lane() == slen - 1 && u == (uint16_t)'\n') != 0ull;
         } else {
-            copy_text<T>(dst, tin + op.payload, slen);
+            for (int j = lane(); j < slen; j += MT_WAVE) {
+                const uint16_t u = tin[op.payload + j];
+                dst[j] = u;
+                anynl = anynl || u == (uint16_t)'\n';
+                lastnl = lastnl || (j == slen - 1 && u == (uint16_t)'\n');
+            }
+            anynl = ballot(anynl) != 0ull;
+            lastnl = ballot(lastnl) != 0ull;
         }
+#ifdef MT_NO_NONL
+        anynl = true;
+#endif
         d.text_top += slen;
-        segw = SEGF_NL_KNOWN | (in.nl ? SEGF_NL : 0u);
+        segw = SEGF_NL_KNOWN | (lastnl ? SEGF_NL : 0u) | (anynl ? 0u : SEGF_NONL);
     }
     P2_T0(15)
     seg_move_right(d, x, 1);

@@ -86,9 +86,13 @@ __global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_
     const int doc = (int)blockIdx.x * WPG + wv;
     if (doc >= st.n_docs) return;
     if (!T::kLds && !st.retry[doc]) return;
-    if (!T::kLds && lane() == 0) atomicAdd(st.stats, 1u);
     const int64_t k1 = off[doc + 1];
     const int64_t k0 = (T::kLds || !caps.resume) ? off[doc] : st.resume[doc];
+    if (k0 >= k1) {   // no message for this document in the batch: its state stays as it is
+        if (!T::kLds && lane() == 0) st.retry[doc] = 0;
+        return;
+    }
+    if (!T::kLds && lane() == 0) atomicAdd(st.stats, 1u);
     DocT<T> d;
     if (!load_doc(d, st, doc, smem, L, caps.S, caps.B, caps.H)) {
         if (lane() == 0) {
@@ -482,6 +486,10 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v), T::kPacked);
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
     const int64_t kend = off[doc + 1];
+    if (k0 >= kend) {   // no message left for this document in the batch (no load / store)
+        if (lane() == 0) st.retry[doc] = 0;
+        return;
+    }
     const int64_t k1 = sl.ops > 0 ? min(kend, k0 + sl.ops) : kend;   // this launch's last message + 1
     PagedDoc<T> pd;
     pg_setup(pd, st, doc, smem, L, pc);
@@ -522,15 +530,18 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
         uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        int nl = 0, pok = 0;
+        int pok = 0;
         if (k < k1) {
             r0 = o4[2 * k];
             r1 = o4[2 * k + 1];
             const int kind = (r1.w >> 16) & 0xFF, flags = ((uint32_t)r1.w >> 24) & 0xFF;
             const int len = r1.x;
+            // (the payload units are not prefetched with the records here: six more VGPRs live
+            // through the op loop cost more in spills than op_insert's own read of them --
+            // A/B on the C3 shard: 851 -> 843 ms, 18 -> 5 spilled VGPRs)
+#ifdef MT_PAYPF
             if (kind == MT_OP_INSERT && !(flags & MT_F_MARKER) && len > 0) {
                 const GLB_AS uint16_t *src = gt + (uint32_t)r1.y;
-                nl = src[len - 1] == '\n';
                 if (len <= 8) {
                     pok = 1;
                     uint32_t u[8];
@@ -542,6 +553,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
                     w3 = u[6] | (u[7] << 16);
                 }
             }
+#endif
         }
         const int cnt = (int)min((int64_t)MT_WAVE, k1 - kb);
         for (int j = 0; j < cnt && w.status == 0; j++) {
@@ -562,7 +574,21 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
             in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w3, j) << 32);
             in.pay_ok = __builtin_amdgcn_readlane(pok, j) != 0;
-            in.nl = __builtin_amdgcn_readlane(nl, j) != 0;
+            in.nl = false;   // op_insert derives it from the payload's last unit
+            in.pay_lane = false;
+            in.pay_v = 0;
+#ifndef MT_NO_PAYMSG
+            {   // a short insert's payload: one load per message, used by op_insert after the page
+                // lookup (its latency hides behind the views and the window switch); A/B on the
+                // 12.5k-document C3 shard: 844 -> 840 ms (profiles/r4/ab_paymsg.log)
+                const int len = in.op.pos2;
+                if (in.op.kind == MT_OP_INSERT && !(in.op.flags & MT_F_MARKER) && len > 0 && len <= 8) {
+                    in.pay_ok = true;
+                    in.pay_lane = true;
+                    if (lane() < len) in.pay_v = gt[in.op.payload + lane()];
+                }
+            }
+#endif
             if ((pc.tight || pc.grow) && !pg_room(pd, in.op)) {
                 spill_at = kb + j;
                 break;

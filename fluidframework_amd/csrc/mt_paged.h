@@ -59,10 +59,16 @@ template <class T> struct PagedDoc {
     int cur;                  // page id staged in the window (-1: none)
     int cur_pos;              // its level-1 position (-1: not known yet)
     int dirty;                // the window differs from the page in HBM (slots, uid map, table)
+    int tdirty;               // an op changed the window since it was loaded: its unsettled-table
+                              // entries are rebuilt at the flush (zamboni's scours / packs change
+                              // settled segments only, whose entries contribute nothing to a view)
     int uid_lo;               // next_uid when the window was loaded: older segments of the
                               // window are already mapped to its page
     int vvalid, vr, vc;       // pvl holds the page view lengths of view (vr, vc): boundary
                               // splits keep them (lengths are preserved), any other change drops them
+    int zuid, zpv;            // zamboni's first pop of the current message (known before the op:
+                              // the op only adds heap entries above minSeq) and its page from the
+                              // uid map, loaded at the message's start (zuid 0: none)
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
                               // window's entries since they were last rebuilt); the current
                               // message's bound (pg_room)
@@ -402,6 +408,7 @@ TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const 
     pd.cur = pg;
     pd.cur_pos = -1;
     pd.dirty = 0;
+    pd.tdirty = 0;
     pd.uid_lo = w.next_uid;
     // the table holds >= as many entries for this page as it has unsettled segments now
     pd.wgrow = max(pd.wgrow, pd.opbound);
@@ -536,6 +543,7 @@ TD void pg_split_page(PagedDoc<T> &pd) {
         return;
     }
     PG_CNT(25)
+    pd.zuid = 0;   // zamboni's prefetched page may be the moved half's
     const int pos = pg_cur_pos(pd);
     // table: the window's entries are rebuilt now (first half under this page, second half
     // under the new one), so it never holds both a stale and a fresh copy of a segment
@@ -646,13 +654,19 @@ TD void pg_win_flush_impl(PagedDoc<T> &pd) {
 #endif
     if (w.dlo < w.n) {   // some slot changed: its table entries and the slots from dlo on
         PG_CNT(23)
-        PG_T0(33)
-        pg_table_purge(pd, pd.cur);
-        PG_T1(33)
-        PG_T0(34)
-        pg_table_add(pd, 0, w.n, pd.cur);
-        PG_T1(34)
-        if (w.status) return;
+#ifndef MT_FLUSH_TABLE_ALWAYS
+        if (pd.tdirty) {
+#endif
+            PG_T0(33)
+            pg_table_purge(pd, pd.cur);
+            PG_T1(33)
+            PG_T0(34)
+            pg_table_add(pd, 0, w.n, pd.cur);
+            PG_T1(34)
+            if (w.status) return;
+#ifndef MT_FLUSH_TABLE_ALWAYS
+        }
+#endif
         PG_T0(35)
         pg_write_page(pd, pd.cur, 0, w.n, 0, nbr(w, 0), w.dlo);
         PG_T1(35)
@@ -776,11 +790,41 @@ TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart
     return -1;
 }
 // the window onto level-1 position pos, whose observer start is obs_base
+// L2 warm-up of zamboni's page (the message's first pop, pd.zuid / zpv): one dword load per
+// 128-byte line of its slots, lanes 0-7 / 8-15 / 16-19 -> A / B / O.  Issued between the op
+// page's fetch and the flush: the place step waits for the fetch, and so (in-order vmcnt) for
+// this load too, before `touch` dies -- its register is never reused while the load is out.
+__device__ __forceinline__ int pg_touch_lines(const GLB_AS void *a, const GLB_AS void *b, const GLB_AS void *o) {
+    const int l = lane();
+    const GLB_AS char *p = l < 8 ? (const GLB_AS char *)a + 128 * l
+                                 : (l < 16 ? (const GLB_AS char *)b + 128 * (l - 8)
+                                           : (const GLB_AS char *)o + 128 * (l < 20 ? l - 16 : 0));
+    int x;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(x) : "v"(p) : "memory");
+    return x;
+}
 TD void pg_load_pos(PagedDoc<T> &pd, int pos, int obs_base) {
     const int pg = uni(pd.up.dir[pos]);
     if (pd.cur != pg) {
         PG_CNT(24)
+#ifdef MT_ZPF
+        v4i a = v4i{0, 0, 0, 0};
+        u64 o = 0;
+        v4u b = v4u{0, 0, 0, 0};
+        pg_win_fetch(pd, pg, a, o, b);
+        int touch = 0;
+        const int zp = pd.zuid ? uni(pd.zpv) : -1;
+        if (pd.zuid) pd.zpv = zp;   // uniform from here on
+        if (zp >= 0 && zp != pg && zp < pd.PP)
+            touch = pg_touch_lines(pd.gA + (size_t)zp * MT_PG_SLOTS, pd.gB + (size_t)zp * MT_PG_SLOTS,
+                                   pd.gO + (size_t)zp * MT_PG_SLOTS);
+        pg_win_flush(pd);
+        if (pd.w.status) return;
+        pg_win_place(pd, pg, a, o, b);
+        asm volatile("" ::"v"(touch));
+#else
         pg_win_switch(pd, pg);
+#endif
     }
     pd.cur_pos = pos;
     pd.w.obs_base = obs_base;
@@ -959,8 +1003,14 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
             return;
         }
         // the segment's page from the uid map: issued before the heap pop so that its
-        // latency hides behind it; needed only if the segment is not in the window
+        // latency hides behind it; needed only if the segment is not in the window (the
+        // message's first pop: loaded at the message's start)
+#ifdef MT_ZPF
+        const int gpg = uid == (uint32_t)pd.zuid ? pd.zpv : (int)pd.gumap[uid];
+        pd.zuid = 0;
+#else
         const int gpg = pd.gumap[uid];
+#endif
         PG_T0(5)
         heap_pop(w);
         wsync<T>();
@@ -1076,6 +1126,7 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
     OpIn rel = in;
     rel.op.pos1 = op.pos1 - start;
     pd.vvalid = 0;
+    pd.tdirty = 1;
     op_insert(w, rel, tin, pin);
     if (w.status) return;
     pg_win_sync(pd);
@@ -1090,6 +1141,7 @@ TD void pg_boundary(PagedDoc<T> &pd, int p, int r, int c) {
     if (pos < 0 || start >= p) return;   // p is at a page boundary or past the end
     pg_load_pos(pd, pos, ostart);
     if (pd.w.status) return;
+    pd.tdirty = 1;
     boundary(pd.w, p - start, r, c);
     if (pd.w.status) return;
     pg_win_sync(pd);
@@ -1121,6 +1173,7 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
         while (pos < np && carry < p2) {
             pg_load_pos(pd, pos, ocarry);
             if (w.status) return;
+            pd.tdirty = 1;
             const bool done = range_mark(w, op, rec, carry, ocarry, cb);
             if (w.status) return;
             pg_win_sync(pd);
@@ -1252,6 +1305,7 @@ TD void pg_load_removed(PagedDoc<T> &pd, const mt_op_rec &op) {
             return;
         }
     }
+    pd.tdirty = 1;
     load_removed(w, op);
     if (w.status) return;
     pg_win_sync(pd);
@@ -1266,6 +1320,18 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
         pg_renumber(pd);
         if (w.status) return;
     }
+#ifdef MT_ZPF
+    {   // zamboni's first pop of this message and its page (the op adds entries above minSeq only)
+        pd.zuid = 0;
+        if (w.heap_n > 0 && op.kind != MT_OP_NOOP) {
+            const v2i top = heap_top(w);
+            if (top.x <= max(w.min_seq, op.min_seq) && top.y > 0 && top.y < pd.UM) {
+                pd.zuid = top.y;
+                pd.zpv = pd.gumap[top.y];
+            }
+        }
+    }
+#endif
     if (op.flags & MT_F_LOAD) {   // summary body append (apply_op); no events
         const int rich = w.rich;
         w.rich = 0;
@@ -1330,7 +1396,7 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
 // Compacts the live text of every page into the other arena half, page by page.
 TD bool paged_text_ensure(DocT<T> &w, int need) {
     PagedDoc<T> &pd = pdoc(w);
-    const int keep = pd.cur, keep_pos = pd.cur_pos;
+    const int keep = pd.cur, keep_pos = pd.cur_pos, keep_td = pd.tdirty;
     if (keep >= 0) pd.dirty = 1;   // a scour may have updated flags in the window since its sync
     pg_win_flush(pd);
     if (w.status) return false;
@@ -1374,9 +1440,10 @@ TD bool paged_text_ensure(DocT<T> &w, int need) {
     w.text_half = dh;
     w.text_top = carry;
     pd.cur = -1;
-    if (keep >= 0) {
+    if (keep >= 0) {   // the step that asked for room goes on in the same page
         pg_win_load(pd, keep);
         pd.cur_pos = keep_pos;
+        pd.tdirty = keep_td;
     }
     if (w.text_top + need <= w.T_cap) return true;
     pg_fail_cap(w, 4);
@@ -1385,7 +1452,7 @@ TD bool paged_text_ensure(DocT<T> &w, int need) {
 
 TD bool paged_props_ensure(DocT<T> &w, int need) {
     PagedDoc<T> &pd = pdoc(w);
-    const int keep = pd.cur, keep_pos = pd.cur_pos;
+    const int keep = pd.cur, keep_pos = pd.cur_pos, keep_td = pd.tdirty;
     if (keep >= 0) pd.dirty = 1;   // a scour may have updated flags in the window since its sync
     pg_win_flush(pd);
     if (w.status) return false;
@@ -1417,9 +1484,10 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
     w.props_top = carry;
     pd.cur = -1;
     gsync_rd();
-    if (keep >= 0) {
+    if (keep >= 0) {   // the step that asked for room goes on in the same page
         pg_win_load(pd, keep);
         pd.cur_pos = keep_pos;
+        pd.tdirty = keep_td;
     }
     if (w.props_top + need <= w.P_cap) return true;
     pg_fail_cap(w, 5);
@@ -1567,9 +1635,12 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.cur = -1;
     pd.cur_pos = -1;
     pd.dirty = 0;
+    pd.tdirty = 0;
     pd.vvalid = 0;
     pd.wgrow = 0;
     pd.opbound = 0;
+    pd.zuid = 0;
+    pd.zpv = 0;
 }
 
 // Pages not in the directory are free (meta cleared; pvl as scratch marks): the HBM meta of

@@ -1504,6 +1504,12 @@ static int mt_settle(mt_handle *h) {
     h->pending = nullptr;
     const int rc = grow_loop(h, b);
     b->owner = nullptr;
+    // the growth step's launches belong to the batch: the batch's timing (mt_last_kernel_ms)
+    // ends after them
+    if (h->grown_last > 0 && h->timed) {
+        HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+        HIPCHK(h, hipEventSynchronize(h->ev1));
+    }
     return rc;
 }
 
