@@ -285,9 +285,17 @@ class MergeTreeBatch:
     def upload(self, a):
         return DeviceBatch(self, a)
 
-    def generate(self, cfg, doc_base=0, trace=None):
+    def generate(self, cfg, doc_base=0, trace=None, ops_per_doc=None):
+        """Device-generated batch (mt_generate); ops_per_doc: a length per document
+        (mt_generate_docs), else cfg["ops"] each."""
         c = _native.gen_cfg(cfg)
-        b = self.lib.mt_generate(self.h, ctypes.byref(c), doc_base, _native.ptr(trace))
+        if ops_per_doc is not None:
+            lens = np.ascontiguousarray(ops_per_doc, dtype=np.int32)
+            if lens.shape != (self.n_docs,):
+                raise ValueError("ops_per_doc: one length per document")
+            b = self.lib.mt_generate_docs(self.h, ctypes.byref(c), doc_base, _native.ptr(lens), _native.ptr(trace))
+        else:
+            b = self.lib.mt_generate(self.h, ctypes.byref(c), doc_base, _native.ptr(trace))
         if not b:
             raise RuntimeError(f"mt_generate failed: {self.lib.mt_last_error(self.h).decode()}")
         return DeviceBatch(self, None, handle=b)

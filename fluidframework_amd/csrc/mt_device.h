@@ -63,6 +63,15 @@ static_assert(sizeof(PageMeta) == 12, "PageMeta size");
 static __host__ __device__ inline int pm_bcnt(const PageMeta &m, int q) { return (int)((m.bc >> (4 * q)) & 15u); }
 static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { return (int8_t)((int)((m.flg2 >> (2 * q)) & 3u) - 1); }
 #define MT_OSLOTS 64
+// Overlap masks use slots 1..63; bit 63 marks an *overflow set* (the last-tier paged
+// instantiations, TierPagedT::kMayGrow, once every slot is taken): the mask's low 32 bits are
+// then the offset of the segment's whole removedClientOverlap list in the document's overflow
+// arena ([count, short ids...], u16), which starts with a 4-unit header {top (u32), last seq
+// that made a set (u32)}
+#define MT_OSLOT_USE 63
+#define MT_OVF_BIT (1ull << 63)
+#define MT_OVF_HDR 4
+#define MT_OVF_ARENA 1024      // overflow-arena units per document in the main arrays (the growth step raises it)
 #define MT_OSLOT_FREE 0x7FFFFFFF
 #define MT_PG_SLOTS 64
 #define MT_PG_OLB 32          // ordinal characters kept per page for its leaf blocks (16 + scratch)
@@ -99,9 +108,16 @@ struct PagedRegion {
     uint16_t *oL;             // [slots][PP][32]
     uint16_t *oU;             // [slots][MT_LV][PP]
     int32_t PP, PH, UT, slots;
+    // text / property arenas (two halves each, DocT text_base / prec): the main set's are the
+    // handle's (DevState.text / props); the big region's are sized by the growth step too
+    uint16_t *text;           // [slots][2][T]
+    uint32_t *props;          // [slots][2][P][MT_PREC]
+    uint16_t *umap;           // [slots][UM] uid -> page (pg_renumber keeps ids below UM)
+    uint16_t *ovf;            // [slots][OA] overflow overlap sets (MT_OVF_BIT masks)
+    int32_t T, P, UM, OA;
 };
-// document doc's paged arrays (bslot: its slot in the big region, -1: the main set); the
-// uid -> page map always stays in the main set (DevState.pgUmap)
+// document doc's paged arrays, arenas and uid map (bslot: its slot in the big region, -1: the
+// main set)
 struct PagedBase {
     v4i *A;
     u64 *O;
@@ -115,6 +131,11 @@ struct PagedBase {
     u64 *uO;
     uint16_t *oS, *oL, *oU;   // ordinal characters (null: none)
     int32_t PP, PH, UT;
+    uint16_t *text;           // [2][T]
+    uint32_t *props;          // [2][P][MT_PREC]
+    uint16_t *umap;           // [UM]
+    uint16_t *ovf;            // [OA]
+    int32_t T, P, UM, OA;
 };
 __host__ __device__ inline PagedBase paged_base(const PagedRegion &R, size_t i) {
     PagedBase b;
@@ -135,6 +156,14 @@ __host__ __device__ inline PagedBase paged_base(const PagedRegion &R, size_t i) 
     b.PP = R.PP;
     b.PH = R.PH;
     b.UT = R.UT;
+    b.text = R.text + i * 2 * (size_t)R.T;
+    b.props = R.props + i * 2 * (size_t)R.P * MT_PREC;
+    b.umap = R.umap + i * (size_t)R.UM;
+    b.ovf = R.ovf ? R.ovf + i * (size_t)R.OA : nullptr;
+    b.T = R.T;
+    b.P = R.P;
+    b.UM = R.UM;
+    b.OA = R.OA;
     return b;
 }
 
@@ -165,8 +194,9 @@ struct DevState {
     v4i *pgUtA;
     u64 *pgUtO;
     uint16_t *pgUmap;         // [n_docs][UM] uid -> page
+    uint16_t *pgOvf;          // [n_docs][OA] overflow overlap sets (MT_OVF_BIT)
     uint16_t *pgOS, *pgOL, *pgOU;   // ordinal characters of the paged layout (PagedRegion oS / oL / oU)
-    int32_t PP, PH, UT, UM;
+    int32_t PP, PH, UT, UM, OA;
     int32_t *bslot;           // [n_docs] slot in the big region (-1: main arrays); null: no big region
     PagedRegion big;          // documents re-tiered by the growth step (larger PP / PH / UT)
     int32_t S, B, H, T, P, DL;
@@ -183,12 +213,20 @@ struct DevState {
     struct PendQ *segP;       // [n_docs][S] per segment: its pending segment groups
     int32_t LG;               // group ids per document (outstanding segment groups)
     unsigned long long *prof; // [128] section timers of a -DMT_PROF build (null otherwise)
+    const int64_t *gen_off;   // mt_generate_docs: [n_docs + 1] op offsets (per-document lengths);
+                              // null: cfg.ops messages every document
+    const int32_t *order;     // the applied batch's dispatch order (documents by message count,
+                              // longest first); null: index order (equal lengths)
 };
+// The document replay workgroup i serves: the hardware dispatches workgroups in index order as
+// slots free up, so a longest-first order is LPT scheduling of a skewed batch's documents
+// (its serial tail is the longest document, not whichever came last).
+__device__ __forceinline__ int doc_at(const DevState &st, int i) { return st.order ? st.order[i] : i; }
 
 __host__ __device__ inline PagedRegion main_region(const DevState &st) {
     return PagedRegion{st.pgA,   st.pgO,    st.pgB,   st.pgMeta, st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage,
                        st.pgUtA, st.pgUtO, st.pgOS, st.pgOL,   st.pgOU,  st.PP,    st.PH,    st.UT,
-                       st.n_docs};
+                       st.n_docs, st.text, st.props, st.pgUmap, st.pgOvf, st.T, st.P, st.UM, st.OA};
 }
 // the paged arrays of document doc (device side: its slot from st.bslot; readers outside the
 // replay kernels, which are instantiated per region)
@@ -273,7 +311,7 @@ __device__ __forceinline__ int pack_cli(int cli, int rcli) {
     return (int)(((uint32_t)(uint16_t)cli) | (((uint32_t)(uint16_t)rcli) << 16));
 }
 // removedClientOverlap (MT/mergeTree.ts:2577-2585) as a bit mask over the document's overlap
-// *slots*: a client that removes an already-removed segment takes a slot (1..64) for as long
+// *slots*: a client that removes an already-removed segment takes a slot (1..63) for as long
 // as a segment it marked is unsettled (DocT.ocli, mt_engine.h oslot_alloc); s = 0: no slot
 __device__ __forceinline__ bool ovl_has(u64 o, int s) {
     const uint32_t sh = (uint32_t)(s - 1) & 63u;

@@ -32,6 +32,7 @@ template <bool kLogT> struct TierLdsT {
     // removedClientOverlap masks of short ids 1..32 (4 bytes per segment in LDS); a
     // document that needs ids 33..64 continues in the next tier (lds_room / load_doc)
     static constexpr int kOvlBits = 32;
+    static constexpr bool kMayGrow = false;
     typedef uint32_t O_v;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS uint32_t *O_t;
@@ -44,6 +45,7 @@ template <bool kLogT> struct TierGlbT {
     static constexpr bool kPaged = false;
     static constexpr bool kLive = false;
     static constexpr int kOvlBits = 64;
+    static constexpr bool kMayGrow = false;
     typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
@@ -59,6 +61,7 @@ template <bool kLogT> struct TierLiveT {
     static constexpr bool kPaged = false;
     static constexpr bool kLive = true;
     static constexpr int kOvlBits = 64;
+    static constexpr bool kMayGrow = false;
     typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
@@ -76,6 +79,7 @@ template <bool kLogT> struct TierLiveLdsT {
     static constexpr bool kPaged = false;
     static constexpr bool kLive = true;
     static constexpr int kOvlBits = 32;
+    static constexpr bool kMayGrow = false;
     typedef uint32_t O_v;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS uint32_t *O_t;
@@ -102,6 +106,9 @@ struct TierPagedT {
     static constexpr int kPP = kPPT, kPH = kPHT, kUT = kUTT;
     static constexpr bool kBig = kBigT;
     static constexpr bool kPacked = kPackedT;
+    // a last-tier instantiation (runtime capacities, wide masks, full table entries): the
+    // launches the growth step may serve (PagedCaps.grow)
+    static constexpr bool kMayGrow = !kNarrowT && !kPackedT && kPPT == 0;
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;
@@ -345,7 +352,12 @@ TD void fail_cap(DocT<T> &d, int cause) {
 // minSeq sees a segment removed at <= minSeq as removed anyway).  So the masks index slots,
 // not ids: a client takes a slot at its first overlapping remove and keeps it while a segment
 // it marked may be unsettled (the slot's last use > minSeq); after that the slot is reused.
-// Bits a reused slot left on settled segments are never consulted.
+// Bits a reused slot left on settled segments are never consulted.  Slots 1..63: bit 63 marks
+// an overflow set (MT_OVF_BIT): when every slot is taken, a last-tier paged document keeps the
+// segment's whole list in its overflow arena instead (ovf_member / ovf_mark, mt_paged.h), so
+// the number of clients overlapping at once is bounded only by that arena, which the growth
+// step raises; the other tiers hand such a document on (pg_room, pg_load).
+#define MT_SLOTS_OF(T) (T::kOvlBits < MT_OSLOT_USE ? T::kOvlBits : MT_OSLOT_USE)
 TD int oslot_of(DocT<T> &d, int c) {
     const u64 m = ballot(d.ocli == c);
     return m ? first_lane(m) + 1 : 0;
@@ -353,7 +365,7 @@ TD int oslot_of(DocT<T> &d, int c) {
 // A slot for client c (the current message's remover) within T::kOvlBits; 0: none free.
 TD int oslot_take(DocT<T> &d, int c) {
     const int last = d.oslot[2 * lane() + 1];
-    const u64 m = ballot(lane() < T::kOvlBits && (d.ocli == MT_OSLOT_FREE || last <= d.min_seq));
+    const u64 m = ballot(lane() < MT_SLOTS_OF(T) && (d.ocli == MT_OSLOT_FREE || last <= d.min_seq));
     if (!m) return 0;
     const int s = first_lane(m);
     if (lane() == s) d.ocli = c;
@@ -363,9 +375,21 @@ TD int oslot_take(DocT<T> &d, int c) {
 // Would a remove by client c need a slot none of the first T::kOvlBits can give?
 TD bool oslot_short(DocT<T> &d, int c) {
     if (oslot_of(d, c)) return false;
-    if (ballot(lane() < T::kOvlBits && d.ocli == MT_OSLOT_FREE)) return false;
+    if (ballot(lane() < MT_SLOTS_OF(T) && d.ocli == MT_OSLOT_FREE)) return false;
     const int last = d.oslot[2 * lane() + 1];
-    return !ballot(lane() < T::kOvlBits && last <= d.min_seq);
+    return !ballot(lane() < MT_SLOTS_OF(T) && last <= d.min_seq);
+}
+// overflow overlap sets of paged documents (mt_paged.h)
+TD bool ovf_member(DocT<T> &d, u64 o, int c);
+TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq);
+// nodeLength of a leaf in the remote view (c, r) of document d: view_len, with the segment's
+// overflow set consulted instead of the slot bits when its mask carries MT_OVF_BIT (last-tier
+// paged instantiations only; the others never load such a document)
+TD int vlen(DocT<T> &d, v4i a, u64 o, int r, int c) {
+    if constexpr (T::kPaged && T::kMayGrow) {
+        if (o & MT_OVF_BIT) return ovf_member(d, o, c) ? 0 : view_len(a, 0, r, c, 0);
+    }
+    return view_len(a, o, r, c, d.ocs);
 }
 
 // paged instances (window: levels 0-1; upper levels: 1.. with level 1 = pages): B entries
@@ -1506,7 +1530,7 @@ TD void boundary(DocT<T> &d, int p, int r, int c) {
         v4i a;
         u64 o;
         load_ao(d, i, v, a, o);
-        const int vl = v ? view_len(a, o, r, c, d.ocs) : 0;
+        const int vl = v ? vlen(d, a, o, r, c) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin = carry + inc;
         const u64 m = ballot(v && pex < p && p < pin);
@@ -2247,7 +2271,7 @@ TD void op_insert(DocT<T> &d, const OpIn &in, const GLB_AS uint16_t *tin, const 
         v4i a;
         u64 o;
         load_ao(d, i, v, a, o);
-        const int vl = v ? view_len(a, o, r, c, d.ocs) : 0;
+        const int vl = v ? vlen(d, a, o, r, c) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin_ = carry + inc;
         const u64 ms = ballot(v && pex < p && p < pin_);
@@ -2665,7 +2689,7 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         u64 o;
         load_ao(d, i, v, a, o);
         const v4u bv = d.Bv[v ? i : 0];
-        const int vl = v ? view_len(a, o, r, c, d.ocs) : 0;
+        const int vl = v ? vlen(d, a, o, r, c) : 0;
         const int inc = wave_scan_incl(vl);
         const int pex = carry + inc - vl, pin_ = carry + inc;
         const bool sel = v && vl > 0 && pex < p2 && pin_ > p1;
@@ -2688,7 +2712,11 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                 a.w = pack_cli(seg_cli(a), c);
                 d.A[i] = a;
             } else if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
-                if (d.ocs == 0) {
+                bool ovf = false;
+                if constexpr (T::kPaged && T::kMayGrow) ovf = d.ocs == 0 || (o & MT_OVF_BIT);
+                if (ovf) {
+                    // (ovf_mark below)
+                } else if (d.ocs == 0) {
                     if (T::kOvlBits < 64)
                         spill = true;
                     else
@@ -2711,6 +2739,10 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                     }
                 }
             }
+        }
+        if constexpr (T::kPaged && T::kMayGrow) {   // overflow sets: the whole list, in the arena
+            const bool need = rem && sel && !lrem && a.z != MT_RSEQ_NONE && (d.ocs == 0 || (o & MT_OVF_BIT));
+            if (ballot(need) && !ovf_mark(d, need, i, o, c, seq)) bad = true;
         }
         uint32_t nh = 0;
         if (!rem && sel) nh = (uint32_t)(d.props_top + __popcll(sel_m & ((1ull << L) - 1ull)));
@@ -2742,7 +2774,8 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
             d.Bv[i] = nb;
         }
         if (ballot(bad)) {
-            // diagnostic 11: more than 64 clients' overlapping removes unsettled at once
+            // diagnostic 11: more than 63 clients' overlapping removes unsettled at once (or a
+            // full overflow arena)
             if (ovl_any && d.ocs == 0 && d.status == 0) d.cap_cause = 11;
             fail(d, MT_DOC_CAPACITY);
             return true;

@@ -42,6 +42,7 @@ __device__ static void oslot_reset(const DevState &st, int doc) {
     int32_t *o = st.oslot + (size_t)doc * 2 * MT_OSLOTS;
     o[2 * lane()] = MT_OSLOT_FREE;
     o[2 * lane() + 1] = 0;
+    if (st.pgOvf && lane() < 2) ((uint32_t *)(st.pgOvf + (size_t)doc * st.OA))[lane()] = lane() ? 0u : (uint32_t)MT_OVF_HDR;
 }
 
 #define MT_LOAD_FANOUT (MT_MAXN - 1)
@@ -83,8 +84,9 @@ __global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_
     // wave-uniform (SGPR) document index and LDS slice
     const int wv = WPG == 1 ? 0 : uni((int)(threadIdx.x >> 6));
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw + (uint32_t)(wv * (int)L.total);
-    const int doc = (int)blockIdx.x * WPG + wv;
-    if (doc >= st.n_docs) return;
+    const int di = (int)blockIdx.x * WPG + wv;
+    if (di >= st.n_docs) return;
+    const int doc = doc_at(st, di);
     if (!T::kLds && !st.retry[doc]) return;
     const int64_t k1 = off[doc + 1];
     const int64_t k0 = (T::kLds || !caps.resume) ? off[doc] : st.resume[doc];
@@ -247,6 +249,8 @@ struct GenCtx {
     LDS_AS int32_t *short_id;
     int next_short;
     int64_t tu, pu, tb, pb;
+    int64_t ob;   // the document's first op record in the batch
+    int n;        // its messages
 };
 __device__ static __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
 __device__ static void gen_begin(GenCtx &g, const DevState &st, const mt_gen_cfg &cfg, int gdoc, int doc,
@@ -271,8 +275,18 @@ __device__ static void gen_begin(GenCtx &g, const DevState &st, const mt_gen_cfg
     gsync();
     g.next_short = 1;
     g.tu = g.pu = 0;
-    g.tb = (int64_t)doc * tstride;
-    g.pb = (int64_t)doc * pstride;
+    // regions at fixed strides per message (mt_generate: tstride = ops * text_max + 1, ...)
+    if (st.gen_off) {
+        g.ob = st.gen_off[doc];
+        g.n = (int)(st.gen_off[doc + 1] - g.ob);
+    } else {
+        g.ob = (int64_t)doc * cfg.ops;
+        g.n = cfg.ops;
+    }
+    g.tb = g.ob * cfg.text_max + doc;
+    g.pb = g.ob * (1 + 2 * (int64_t)cfg.max_keys_per_op) + doc;
+    (void)tstride;
+    (void)pstride;
 }
 // Writer, reference sequence number and minSeq of message t.
 __device__ static void gen_pick(GenCtx &g, const mt_gen_cfg &cfg, int t, int &r, int &c, int &msn) {
@@ -351,7 +365,7 @@ __device__ static void gen_op(GenCtx &g, const mt_gen_cfg &cfg, int t, int r, in
     }
     in.pay_lo = plo;
     in.pay_hi = phi;
-    if (lane() == 0) ops_out[doc * cfg.ops + (t - 1)] = op;
+    if (lane() == 0) ops_out[g.ob + (t - 1)] = op;
     gsync();
 }
 // The document's text / property words used so far (k_gen_compact packs the regions).
@@ -386,7 +400,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
     // op records carry offsets local to the document's region of the arenas
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)(text_out + g.tb);
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)(props_out + g.pb);
-    for (int t = 1; t <= cfg.ops && d.status == 0; t++) {
+    for (int t = 1; t <= g.n && d.status == 0; t++) {
         int r, c, msn;
         gen_pick(g, cfg, t, r, c, msn);
         d.ocs = oslot_of(d, c);
@@ -400,7 +414,7 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate(DevState st, mt_gen_cfg cf
         }
         const int len = wave_sum(vsum);
         if (dbg_len && lane() == 0) {
-            int32_t *q = dbg_len + ((int64_t)doc * cfg.ops + (t - 1)) * 4;
+            int32_t *q = dbg_len + (g.ob + (t - 1)) * 4;
             q[0] = len;
             q[1] = d.n;
             q[2] = r;
@@ -478,11 +492,12 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     LDS_AS uint8_t *smem = (LDS_AS uint8_t *)smem_raw;
     const PagedCaps pc = eff_caps<T>(pc_arg);
-    const int doc = blockIdx.x;
-    if (doc >= st.n_docs) return;
-    if (doc >= sl.skip_lo && doc < sl.skip_hi) return;
+    const int di = blockIdx.x;   // dispatch position (slices count positions: hardware rounds)
+    if (di >= st.n_docs) return;
+    if (di >= sl.skip_lo && di < sl.skip_hi) return;
+    const int doc = doc_at(st, di);
     if (st.retry[doc] != pc.stage) return;
-    if (lane() == 0 && doc >= sl.cnt_lo && doc < sl.cnt_hi) atomicAdd(st.stats, 1u);
+    if (lane() == 0 && di >= sl.cnt_lo && di < sl.cnt_hi) atomicAdd(st.stats, 1u);
     const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v), T::kPacked);
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
     const int64_t kend = off[doc + 1];
@@ -500,7 +515,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     }
     if (st.hdr[doc].pad[HDR_PAGED]) {
         if (!pg_load(pd, st)) {
-            if (pc.tight || pc.grow) {
+            if (pc.tight || pc.grow == 1) {
                 pg_handover<T>(st, doc, k0, pc);
             } else if (lane() == 0) {   // cannot happen: the last tier has the document's capacities
                 st.hdr[doc].status = MT_DOC_CAPACITY;
@@ -512,8 +527,11 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
         // stays flat (the pages written so far are unreferenced): the next tier converts it
         // again (the growth step: at larger page / heap / table capacities), or only the
         // status changes
-        const int cc = w.cap_cause;   // pages 7, heap 3, table 8: capacities the growth step raises
-        if ((pc.tight || (pc.grow && (cc == 7 || cc == 3 || cc == 8))) && w.status == MT_DOC_CAPACITY) {
+        // pages 7, heap 3, table 8, uid map 9 (pg_renumber): capacities the growth step raises
+        const int cc = w.cap_cause;
+        if ((pc.tight || (pc.grow == 1 && (cc == 7 || cc == 3 || cc == 8)) || (pc.grow && cc == 9)) &&
+            w.status == MT_DOC_CAPACITY) {
+            if (!pc.tight && cc == 9 && lane() == 0) st.hdr[doc].pad[HDR_DIAG] = 9;   // (for the growth step)
             pg_handover<T>(st, doc, k0, pc);
         } else if (lane() == 0) {
             st.hdr[doc].status = w.status == MT_DOC_RETRY ? MT_DOC_CAPACITY : w.status;
@@ -589,10 +607,11 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
                 }
             }
 #endif
-            if ((pc.tight || pc.grow) && !pg_room(pd, in.op)) {
+            if ((pc.tight || pc.grow) && !((pc.grow == 2 || pg_room(pd, in.op)) && pg_arena_room(pd, in.op, pc))) {
                 spill_at = kb + j;
                 break;
             }
+            if (w.status) break;   // (an arena compaction failed)
             pg_apply_op(pd, in, gt, gp);
             pk_ut = max(pk_ut, pd.ut_n);
             pk_heap = max(pk_heap, w.heap_n);
@@ -652,13 +671,13 @@ __global__ void __launch_bounds__(MT_WAVE) k_generate_paged(DevState st, mt_gen_
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)(text_out + g.tb);
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)(props_out + g.pb);
     int pk_ut = 0, pk_heap = 0;
-    for (int t = 1; t <= cfg.ops && w.status == 0; t++) {
+    for (int t = 1; t <= g.n && w.status == 0; t++) {
         int r, c, msn;
         gen_pick(g, cfg, t, r, c, msn);
         w.ocs = oslot_of(w, c);
         const int len = pg_views(pd, r, c);
         if (dbg_len && lane() == 0) {
-            int32_t *q = dbg_len + ((int64_t)doc * cfg.ops + (t - 1)) * 4;
+            int32_t *q = dbg_len + (g.ob + (t - 1)) * 4;
             q[0] = len;
             q[1] = -1;
             q[2] = r;

@@ -69,6 +69,8 @@ template <class T> struct PagedDoc {
     int zuid, zpv;            // zamboni's first pop of the current message (known before the op:
                               // the op only adds heap entries above minSeq) and its page from the
                               // uid map, loaded at the message's start (zuid 0: none)
+    GLB_AS uint16_t *govf;    // overflow overlap sets (MT_OVF_BIT; last-tier instantiations)
+    int ovf_top, ovf_last, OA;   // its fill, the last message that made a set, its capacity
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
                               // window's entries since they were last rebuilt); the current
                               // message's bound (pg_room)
@@ -86,7 +88,8 @@ struct PagedCaps {
     int narrow;  // TierPagedT<., true>: 32-bit overlap masks in LDS (tight tier only)
     int grow;    // last tier: a document that does not fit at load, or whose next message could
                  // outgrow these capacities, is handed to the host's growth step (retry = 3)
-                 // instead of failing -- re-tiered to a larger HBM region, it continues there
+                 // instead of failing -- re-tiered to a larger HBM region, it continues there;
+                 // 2: only the HBM arenas and the uid map can still grow (pg_arena_room)
     int packed;  // TierPagedT<., ., ., true>: 12-byte unsettled-table entries (tight tier only)
 };
 
@@ -559,7 +562,7 @@ TD void pg_split_page(PagedDoc<T> &pd) {
         v4i a;
         u64 o;
         load_ao(w, i, i < w.n, a, o);
-        const int dl = wave_sum(i < w.n ? view_len(a, o, pd.vr, pd.vc, pd.w.ocs) : 0);
+        const int dl = wave_sum(i < w.n ? vlen(pd.w, a, o, pd.vr, pd.vc) : 0);
         if (lane() == 0) {
             pd.pvl[np] = dl;
             pd.pvl[pd.cur] -= dl;
@@ -727,7 +730,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
             v4i a;
             u64 o;
             tab_get(pd, e, pg, a, o);
-            const int dlt = view_len(a, o, r, c, pd.w.ocs) - obs_len(a);
+            const int dlt = vlen(pd.w, a, o, r, c) - obs_len(a);
             if (dlt && pg != cur) atomicAdd((int *)(pd.pvl + pg), dlt);
         }
     }
@@ -738,7 +741,7 @@ TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
         v4i a;
         u64 o;
         load_ao(w, i, i < w.n, a, o);
-        const int dlt = wave_sum(i < w.n ? view_len(a, o, r, c, w.ocs) - obs_len(a) : 0);
+        const int dlt = wave_sum(i < w.n ? vlen(w, a, o, r, c) - obs_len(a) : 0);
         if (i == 0) pd.pvl[cur] += dlt;
     }
     wsync<T>();
@@ -1192,7 +1195,7 @@ TD void pg_op_range(PagedDoc<T> &pd, const mt_op_rec &op, const GLB_AS uint32_t 
 // compacted when they run out.  Zamboni heap entries follow their segments; an entry whose
 // segment is gone (merged or unlinked: the reference skips it, its parent is undefined)
 // gets id 0, which matches nothing.  Runs between messages, from the pages in HBM.
-TD void pg_renumber(PagedDoc<T> &pd) {
+TD void pg_renumber(PagedDoc<T> &pd, bool soft = false) {
     DocT<T> &w = pd.w;
     pg_win_flush(pd);
     if (w.status) return;
@@ -1248,7 +1251,8 @@ TD void pg_renumber(PagedDoc<T> &pd) {
         }
     }
     w.next_uid = carry;
-    if (w.next_uid + 8 > pd.UM) pg_fail_cap(w, 9);   // more live segments than map entries
+    // more live segments than map entries (soft: the caller hands the document to the growth step)
+    if (w.next_uid + 8 > pd.UM && !soft) pg_fail_cap(w, 9);
     gsync();
     wsync<T>();
 }
@@ -1266,7 +1270,8 @@ TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
     // a narrow tier holds overlap slots 1..32 only
-    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
+    // (and a 64-bit tight tier, whose documents keep no overflow sets, at slots 1..63)
+    if ((T::kOvlBits < 64 || !T::kMayGrow) && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
     if (T::kPacked && op.seq - pd.sbase > 65000) return false;   // the packed table's seq offsets
     if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
     if (pd.w.heap_n + hp_b > pd.PH) return false;
@@ -1315,6 +1320,9 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
     w.ocs = oslot_of(w, op_cli(op));
+    if constexpr (T::kMayGrow) {   // no unsettled segment holds an overflow set: start over
+        if (pd.ovf_top > MT_OVF_HDR && pd.ovf_last <= w.min_seq) pd.ovf_top = MT_OVF_HDR;
+    }
     // a message creates <= 3 ids (load_removed finds the id its insert just created)
     if (w.next_uid + 4 > pd.UM && op.kind != MT_OP_LOAD_REMOVED) {
         pg_renumber(pd);
@@ -1394,12 +1402,12 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
 
 // ------------------------------------------------------------------ text / props gc (paged)
 // Compacts the live text of every page into the other arena half, page by page.
-TD bool paged_text_ensure(DocT<T> &w, int need) {
+TD void paged_text_compact(DocT<T> &w) {
     PagedDoc<T> &pd = pdoc(w);
     const int keep = pd.cur, keep_pos = pd.cur_pos, keep_td = pd.tdirty;
     if (keep >= 0) pd.dirty = 1;   // a scour may have updated flags in the window since its sync
     pg_win_flush(pd);
-    if (w.status) return false;
+    if (w.status) return;
     gsync_rd();
     const int dh = 1 - w.text_half;
     GLB_AS uint16_t *dst = text_base(w, dh);
@@ -1445,17 +1453,21 @@ TD bool paged_text_ensure(DocT<T> &w, int need) {
         pd.cur_pos = keep_pos;
         pd.tdirty = keep_td;
     }
+}
+TD bool paged_text_ensure(DocT<T> &w, int need) {
+    paged_text_compact(w);
+    if (w.status) return false;
     if (w.text_top + need <= w.T_cap) return true;
     pg_fail_cap(w, 4);
     return false;
 }
 
-TD bool paged_props_ensure(DocT<T> &w, int need) {
+TD void paged_props_compact(DocT<T> &w) {
     PagedDoc<T> &pd = pdoc(w);
     const int keep = pd.cur, keep_pos = pd.cur_pos, keep_td = pd.tdirty;
     if (keep >= 0) pd.dirty = 1;   // a scour may have updated flags in the window since its sync
     pg_win_flush(pd);
-    if (w.status) return false;
+    if (w.status) return;
     gsync_rd();
     const int dh = 1 - w.props_half;
     int carry = 1;
@@ -1489,8 +1501,121 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
         pd.cur_pos = keep_pos;
         pd.tdirty = keep_td;
     }
+}
+TD bool paged_props_ensure(DocT<T> &w, int need) {
+    paged_props_compact(w);
+    if (w.status) return false;
     if (w.props_top + need <= w.P_cap) return true;
     pg_fail_cap(w, 5);
+    return false;
+}
+
+// ------------------------------------------------------------------ overflow overlap sets
+// removedClientOverlap beyond the 63 slots (MT/mergeTree.ts:2577-2585, read at :1717): a
+// segment's mask MT_OVF_BIT | off points at [n, client...] in the document's overflow arena.
+// Sets are written once; a segment that gains a client gets a new set (copy + the client), so
+// the halves of a split share theirs.  The arena starts over once minSeq passes the last
+// message that made a set (pg_arena_room) -- every segment holding one is then settled and no
+// view consults it (vlen reads a set only for a removal the view has not seen).
+TD bool ovf_member(DocT<T> &d, u64 o, int c) {
+    PagedDoc<T> &pd = pdoc(d);
+    const GLB_AS uint16_t *s = pd.govf + (uint32_t)o;
+    const int n = s[0];
+    bool in = false;
+    for (int k = 1; k <= n; k++) in = in || s[k] == (uint16_t)c;
+    return in;
+}
+// Adds client c to the overlap list of the window's segment i (lanes with need; wave-uniform
+// call): its overflow set, or the clients of its slot bits, copied with c into a new set.
+// false: the arena is full (the caller fails the document, diagnostic 11).
+TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
+    PagedDoc<T> &pd = pdoc(d);
+    const bool isset = (o & MT_OVF_BIT) != 0;
+    const int n_old = !need ? 0 : (isset ? (int)pd.govf[(uint32_t)o] : __popcll(o));
+    const int sz = need ? n_old + 2 : 0;
+    const int inc = wave_scan_incl(sz);
+    const int tot = bcast(inc, MT_WAVE - 1), top = pd.ovf_top;
+    if (!pd.govf || top + tot > pd.OA) return false;
+    if (need) {
+        const int off = top + inc - sz;
+        GLB_AS uint16_t *t = pd.govf + off;
+        t[0] = (uint16_t)(n_old + 1);
+        if (isset) {
+            const GLB_AS uint16_t *s = pd.govf + (uint32_t)o;
+            for (int k = 1; k <= n_old; k++) t[k] = s[k];
+        } else {
+            u64 m = o;
+            for (int k = 1; m; k++) {
+                const int b = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                t[k] = (uint16_t)d.oslot[2 * b];   // slot b + 1's client (unsettled: not reused)
+            }
+        }
+        t[n_old + 1] = (uint16_t)c;
+        d.O[i] = (typename T::O_v)(MT_OVF_BIT | (u64)(uint32_t)off);
+    }
+    pd.ovf_top = top + tot;
+    pd.ovf_last = seq;
+    d.wide = 1;
+    gsync_rd();   // the new sets are read by other lanes
+    return true;
+}
+
+// Can this message's text / property records be placed without running out of the arenas?
+// (TextSegment.append and property sets are unbounded in the reference, MT/textSegment.ts:74-85.)
+// A tight launch hands the document on when the arena's free tail is short (the next tier
+// compacts it); a growing launch compacts here, between messages, and hands the document to the
+// growth step (cause 4 text / 5 records / 9 uid map / 11 overflow overlap sets, kept in
+// HDR_DIAG with status 0) when the live text / records / segments / sets then fill more than
+// half of it -- so a message never fails half applied.  The
+// bound covers an insert's own text and one range step's records (props_ensure(d, MT_WAVE));
+// a zamboni merge's copy is served by the half kept free.
+TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc) {
+    DocT<T> &w = pd.w;
+    const int nt = op.kind == MT_OP_INSERT && !(op.flags & MT_F_MARKER) ? max(op.pos2, 0) : 0;
+    const int np = MT_WAVE + 1;
+    const bool t_ok = w.text_top + nt <= w.T_cap, p_ok = w.props_top + np <= w.P_cap;
+    const bool u_ok = w.next_uid + 4 <= pd.UM || op.kind == MT_OP_LOAD_REMOVED;
+    if constexpr (T::kMayGrow) {
+        if (pd.govf) {   // the overflow overlap arena (cause 11; a tight launch hands the document on)
+            // no unsettled segment holds a set made at or below minSeq: the arena starts over
+            if (pd.ovf_top > MT_OVF_HDR && pd.ovf_last <= w.min_seq) pd.ovf_top = MT_OVF_HDR;
+            if (2 * pd.ovf_top > pd.OA) {
+                w.cap_cause = 11;
+                return false;
+            }
+        }
+    }
+    if (t_ok && p_ok && u_ok) return true;
+    if constexpr (T::kMayGrow) {
+        if (!pc.tight) {
+            if (!u_ok) {   // (the renumbering pg_apply_op would do, done here; cause 9)
+                pg_renumber(pd, true);
+                if (w.status) return true;
+                if (2 * (w.next_uid + 8) > pd.UM) {
+                    w.cap_cause = 9;
+                    return false;
+                }
+            }
+            if (!t_ok) {
+                paged_text_compact(w);
+                if (w.status) return true;   // (failed: the loop stops)
+                if (2 * (w.text_top + nt) > w.T_cap) {
+                    w.cap_cause = 4;
+                    return false;
+                }
+            }
+            if (!p_ok) {
+                paged_props_compact(w);
+                if (w.status) return true;
+                if (2 * (w.props_top + np) > w.P_cap) {
+                    w.cap_cause = 5;
+                    return false;
+                }
+            }
+            return true;
+        }
+    }
     return false;
 }
 
@@ -1502,11 +1627,13 @@ TD void pg_bases(PagedDoc<T> &pd, const DevState &st, int doc) {
     pd.gA = (GLB_AS v4i *)b.A;
     pd.gO = (GLB_AS u64 *)b.O;
     pd.gB = (GLB_AS v4u *)b.B;
-    pd.gumap = (GLB_AS uint16_t *)(st.pgUmap + (size_t)doc * st.UM);
+    pd.gumap = (GLB_AS uint16_t *)b.umap;
+    pd.govf = (GLB_AS uint16_t *)b.ovf;
+    pd.OA = b.OA;
     pd.goS = (GLB_AS uint16_t *)b.oS;
     pd.goL = (GLB_AS uint16_t *)b.oL;
     pd.PPh = b.PP;
-    pd.UM = st.UM;
+    pd.UM = b.UM;
     pd.doc = doc;
 }
 
@@ -1543,11 +1670,14 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.PH = pc.PH;
     pd.UT = pc.UT;
     w.hp = st.hdr + doc;
-    w.text = (GLB_AS uint16_t *)(st.text + doc * (size_t)2 * st.T);
-    w.props = (GLB_AS uint32_t *)(st.props + doc * (size_t)2 * st.P * MT_PREC);
+    {   // the arenas of the document's region (the big region's grow with the growth step)
+        const PagedBase b = tier_paged<T::kBig>(st, doc);
+        w.text = (GLB_AS uint16_t *)b.text;
+        w.props = (GLB_AS uint32_t *)b.props;
+        w.T_cap = b.T;
+        w.P_cap = b.P;
+    }
     w.dlog = st.DL ? (GLB_AS int32_t *)(st.dlog + doc * (size_t)st.DL) : nullptr;
-    w.T_cap = st.T;
-    w.P_cap = st.P;
     w.DL_cap = st.DL;
     w.rich = st.DLR;
     w.oslot = (GLB_AS int32_t *)(st.oslot + doc * (size_t)(2 * MT_OSLOTS));
@@ -1641,6 +1771,15 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.opbound = 0;
     pd.zuid = 0;
     pd.zpv = 0;
+    pd.ovf_top = MT_OVF_HDR;
+    pd.ovf_last = 0;
+    if constexpr (T::kMayGrow) {
+        if (pd.govf) {
+            const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
+            pd.ovf_top = max((int)hw[0], MT_OVF_HDR);
+            pd.ovf_last = (int)hw[1];
+        }
+    }
 }
 
 // Pages not in the directory are free (meta cleared; pvl as scratch marks): the HBM meta of
@@ -1674,6 +1813,12 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     const int np = h.n_blk[1];
     if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
     if (T::kOvlBits < 64 && w.wide) return false;
+    if constexpr (!T::kMayGrow) {   // overflow overlap sets still consulted: the last tier's
+        if (pd.govf) {
+            const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
+            if ((int)hw[0] > MT_OVF_HDR && (int)hw[1] > w.min_seq) return false;
+        }
+    }
     if (T::kPacked && w.cur_seq - w.min_seq > 30000) return false;   // the packed table's seq offsets
     int mx = 0;
     for (int q = lane(); q < np; q += MT_WAVE) mx = max(mx, (int)g.gdir[q]);
@@ -1714,6 +1859,9 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
     pg_win_flush(pd);
     if (failed) w.status = failed;
     w.oslot[2 * lane()] = w.ocli;
+    if constexpr (T::kMayGrow) {
+        if (pd.govf && lane() < 2) ((GLB_AS uint32_t *)pd.govf)[lane()] = (uint32_t)(lane() ? pd.ovf_last : pd.ovf_top);
+    }
     wsync<T>();
     const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) g.gdir[q] = up.dir[q];
@@ -1765,7 +1913,9 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
         h.pad[HDR_PAGED] = 1;
         h.pad[HDR_NPAGES] = np;
         h.pad[HDR_UTN] = pd.ut_n;
-        h.pad[HDR_DIAG] = w.status ? w.cap_cause : 0;
+        // (status 0: an arena hand-over's cause for the growth step, pg_arena_room)
+        h.pad[HDR_DIAG] =
+            w.status || w.cap_cause == 4 || w.cap_cause == 5 || w.cap_cause == 9 || w.cap_cause == 11 ? w.cap_cause : 0;
         if (T::kLog) {
             h.pad[HDR_MSPLIT] = w.m_split;
             h.pad[HDR_MAPPEND] = w.m_append;

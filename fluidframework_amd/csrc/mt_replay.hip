@@ -285,8 +285,9 @@ __global__ void __launch_bounds__(MT_WAVE) k_extract(DevState st, int mode, int6
     if (doc >= st.n_docs) return;
     const DocHdr h = st.hdr[doc];
     const SegRanges R = seg_ranges(st, doc, h);
-    const uint16_t *tb = st.text + ((size_t)doc * 2 + h.text_half) * st.T;
-    const uint32_t *pr = st.props + ((size_t)doc * 2 + h.props_half) * st.P * MT_PREC;
+    const PagedBase ar = doc_paged(st, doc);   // (the arenas of the document's region)
+    const uint16_t *tb = ar.text + (size_t)h.text_half * ar.T;
+    const uint32_t *pr = ar.props + (size_t)h.props_half * ar.P * MT_PREC;
     const int ms = h.min_seq;
     int64_t nrec = 0, ntext = 0, nprop = 0;
     const int64_t rbase = mode ? io[3 * doc] : 0, tbase = mode ? io[3 * doc + 1] : 0, pbase = mode ? io[3 * doc + 2] : 0;
@@ -384,8 +385,9 @@ __global__ void __launch_bounds__(MT_WAVE) k_checksum(DevState st, mt_checksum *
     if (doc >= st.n_docs) return;
     const DocHdr h = st.hdr[doc];
     const SegRanges R = seg_ranges(st, doc, h);
-    const uint16_t *tb = st.text + ((size_t)doc * 2 + h.text_half) * st.T;
-    const uint32_t *pr = st.props + ((size_t)doc * 2 + h.props_half) * st.P * MT_PREC;
+    const PagedBase ar = doc_paged(st, doc);   // (the arenas of the document's region)
+    const uint16_t *tb = ar.text + (size_t)h.text_half * ar.T;
+    const uint32_t *pr = ar.props + (size_t)h.props_half * ar.P * MT_PREC;
     int len = 0, ntext = 0, nseg = 0;
     for (int r = 0; r < R.count(); r++) {
         const v4i *A;
@@ -637,7 +639,22 @@ struct mt_batch {
     std::vector<int64_t> lr_off;
     std::vector<std::pair<int32_t, int32_t>> lr;
     bool generated = false;
+    int32_t *order = nullptr;     // dispatch order (DevState.order), null when lengths are equal
 };
+// Longest-first dispatch order of a batch whose documents differ in length (stable: equal
+// lengths keep index order); none when every document has the same number of messages.
+static bool set_order(mt_batch *b, const int64_t *off) {
+    const uint32_t n = b->n_docs;
+    bool equal = true;
+    for (uint32_t d = 1; d < n && equal; d++) equal = off[d + 1] - off[d] == off[1] - off[0];
+    if (equal) return true;
+    std::vector<int32_t> ord(n);
+    for (uint32_t d = 0; d < n; d++) ord[d] = (int32_t)d;
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](int32_t x, int32_t y) { return off[x + 1] - off[x] > off[y + 1] - off[y]; });
+    return hipMalloc(&b->order, (size_t)n * 4) == hipSuccess &&
+           hipMemcpy(b->order, ord.data(), (size_t)n * 4, hipMemcpyHostToDevice) == hipSuccess;
+}
 
 #define HIPCHK(h, x)                                                               \
     do {                                                                           \
@@ -917,6 +934,9 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         alloc((void **)&st.pgUtA, N * (size_t)st.UT * sizeof(int4));
         alloc((void **)&st.pgUtO, N * (size_t)st.UT * sizeof(u64));
         alloc((void **)&st.pgUmap, N * (size_t)st.UM * sizeof(uint16_t));
+        st.OA = MT_OVF_ARENA;
+        alloc((void **)&st.pgOvf, N * (size_t)st.OA * sizeof(uint16_t));
+        if (st.pgOvf) hipMemset(st.pgOvf, 0, N * (size_t)st.OA * sizeof(uint16_t));
         if (h->ordinals) {
             alloc((void **)&st.pgOS, slots * sizeof(uint16_t));
             alloc((void **)&st.pgOL, N * (size_t)st.PP * MT_PG_OLB * sizeof(uint16_t));
@@ -937,7 +957,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
 }
 
 static void free_region(PagedRegion &R) {
-    void *ps[] = {R.A, R.O, R.B, R.meta, R.dir, R.cnt, R.heap, R.upage, R.uA, R.uO, R.oS, R.oL, R.oU};
+    void *ps[] = {R.A, R.O, R.B, R.meta, R.dir, R.cnt, R.heap, R.upage, R.uA, R.uO, R.oS, R.oL, R.oU, R.text, R.props, R.umap, R.ovf};
     for (void *p : ps)
         if (p) hipFree(p);
     R = PagedRegion{};
@@ -952,7 +972,7 @@ void mt_destroy(mt_handle *h) {
     DevState &st = h->st;
     void *ps[] = {st.hdr, st.segA, st.segO, st.segB, st.cnt, st.flg, st.heap, st.text, st.props, st.dlog, h->d_sums,
                   h->d_seed_off, h->d_seed, st.retry, st.stats, st.resume, st.pgA, st.pgO, st.pgB, st.pgMeta,
-                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.oslot,
+                  st.pgDir, st.pgCnt, st.pgHeap, st.pgUtPage, st.pgUtA, st.pgUtO, st.pgUmap, st.pgOvf, st.oslot,
                   st.live, st.grp, st.segP, st.ordS, st.ordB, st.pgOS, st.pgOL, st.pgOU, st.prof};
     for (void *p : ps)
         if (p) hipFree(p);
@@ -1098,6 +1118,7 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
         if (ok && n_ops) ok = hipMemcpy(b->ops, ops, n_ops * sizeof(mt_op_rec), hipMemcpyHostToDevice) == hipSuccess;
         if (ok && text_len) ok = hipMemcpy(b->text, text, text_len * 2, hipMemcpyHostToDevice) == hipSuccess;
         if (ok && props_len) ok = hipMemcpy(b->props, props, props_len * 4, hipMemcpyHostToDevice) == hipSuccess;
+        if (ok) ok = set_order(b, doc_op_off);
     }
     if (!ok) {
         h->err = "mt_batch_upload: device allocation/copy failed";
@@ -1165,6 +1186,7 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         if (rc) return rc;
     }
     track_views(h, b);
+    h->st.order = b->order;   // (its launches and its growth step's)
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
@@ -1280,9 +1302,27 @@ struct MigItem {
 __global__ void __launch_bounds__(MT_WAVE) k_migrate_paged(DevState st, PagedRegion old_big, PagedRegion dst_r,
                                                            const MigItem *items) {
     const MigItem it = items[blockIdx.x];
-    if (!st.hdr[it.doc].pad[HDR_PAGED]) return;   // still flat: pg_convert pages it at the new capacities
+    const DocHdr h = st.hdr[it.doc];
     const PagedBase s = it.src < 0 ? paged_base(main_region(st), (size_t)it.doc) : paged_base(old_big, (size_t)it.src);
     const PagedBase d = paged_base(dst_r, (size_t)it.dst);
+    {   // the live half of the text / property arenas (same half, same offsets): every record
+        // below text_top / props_top
+        const uint16_t *ts = s.text + (size_t)h.text_half * s.T;
+        uint16_t *td = d.text + (size_t)h.text_half * d.T;
+        for (int i = lane(); i < h.text_top; i += MT_WAVE) td[i] = ts[i];
+        const uint32_t *ps = s.props + (size_t)h.props_half * s.P * MT_PREC;
+        uint32_t *pd = d.props + (size_t)h.props_half * d.P * MT_PREC;
+        for (size_t i = lane(); i < (size_t)h.props_top * MT_PREC; i += MT_WAVE) pd[i] = ps[i];
+        // the uid map's entries below next_uid (a flat document has none yet)
+        if (h.pad[HDR_PAGED])
+            for (int i = lane(); i < min(h.next_uid, s.UM); i += MT_WAVE) d.umap[i] = s.umap[i];
+        // the overflow overlap arena up to its fill (sets keep their offsets)
+        if (s.ovf && d.ovf) {
+            const int top = min(max((int)((const uint32_t *)s.ovf)[0], MT_OVF_HDR), s.OA);
+            for (int i = lane(); i < top; i += MT_WAVE) d.ovf[i] = s.ovf[i];
+        }
+    }
+    if (!h.pad[HDR_PAGED]) return;   // still flat: pg_convert pages it at the new capacities
     const size_t ns = (size_t)s.PP * MT_PG_SLOTS;   // page p slot k sits at p * 64 + k in both
     for (size_t i = lane(); i < ns; i += MT_WAVE) {
         d.A[i] = s.A[i];
@@ -1319,11 +1359,15 @@ __global__ void k_fail_grow(DevState st) {
     }
 }
 
-static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c, bool ordinals) {
+static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c, bool ordinals, int T, int P, int UM, int OA) {
     R = PagedRegion{};
     R.PP = c.PP;
     R.PH = c.PH;
     R.UT = c.UT;
+    R.T = T;
+    R.P = P;
+    R.UM = UM;
+    R.OA = OA;
     R.slots = slots;
     const size_t n = (size_t)slots, pages = n * c.PP;
     bool ok = hipMalloc(&R.A, pages * MT_PG_SLOTS * sizeof(int4)) == hipSuccess &&
@@ -1335,7 +1379,12 @@ static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c, bool ord
               hipMalloc(&R.heap, n * (size_t)(c.PH + 1) * sizeof(int2)) == hipSuccess &&
               hipMalloc(&R.upage, n * (size_t)c.UT * sizeof(int32_t)) == hipSuccess &&
               hipMalloc(&R.uA, n * (size_t)c.UT * sizeof(int4)) == hipSuccess &&
-              hipMalloc(&R.uO, n * (size_t)c.UT * sizeof(u64)) == hipSuccess;
+              hipMalloc(&R.uO, n * (size_t)c.UT * sizeof(u64)) == hipSuccess &&
+              hipMalloc(&R.text, n * 2 * (size_t)T * sizeof(uint16_t)) == hipSuccess &&
+              hipMalloc(&R.props, n * 2 * (size_t)P * MT_PREC * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&R.umap, n * (size_t)UM * sizeof(uint16_t)) == hipSuccess &&
+              hipMalloc(&R.ovf, n * (size_t)OA * sizeof(uint16_t)) == hipSuccess &&
+              hipMemset(R.ovf, 0, n * (size_t)OA * sizeof(uint16_t)) == hipSuccess;
     if (ok && ordinals)
         ok = hipMalloc(&R.oS, pages * MT_PG_SLOTS * sizeof(uint16_t)) == hipSuccess &&
              hipMalloc(&R.oL, pages * MT_PG_OLB * sizeof(uint16_t)) == hipSuccess &&
@@ -1346,8 +1395,10 @@ static bool alloc_region(PagedRegion &R, int slots, const PagedCaps &c, bool ord
 
 
 // Moves the documents of `moving` (and every document already there) into a new big region at
-// capacities c; synchronous.
-static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const PagedCaps &c) {
+// capacities c, text / property arenas of T units / P records per half, UM uid-map entries
+// and OA overflow-arena units; synchronous.
+static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const PagedCaps &c, int T, int P, int UM,
+                  int OA) {
     DevState &st = h->st;
     const uint32_t n = h->n_docs;
     if (!st.bslot) {
@@ -1367,7 +1418,7 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
             slots++;
         }
     PagedRegion R;
-    if (!alloc_region(R, std::max(slots, 1), c, h->ordinals)) {
+    if (!alloc_region(R, std::max(slots, 1), c, h->ordinals, T, P, UM, OA)) {
         (void)hipGetLastError();
         h->err = "growth step: device allocation of the big region failed";
         return MT_E_NOMEM;
@@ -1402,6 +1453,7 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
 // growth step until none is left (synchronous).
 static int grow_loop(mt_handle *h, const mt_batch *b) {
     DevState &st = h->st;
+    st.order = b->order;
     const uint32_t n = h->n_docs;
     h->grown_last = 0;
     h->grow_rounds_last = 0;
@@ -1420,7 +1472,7 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
         // what ran out, read from the handed-over documents' state: a capacity they fill to
         // more than half is doubled (the kernel's bound is per message, pg_room); documents
         // of the big region marked for this batch (k_mark_big) only need its capacities
-        bool t = false, hp = false, pg = false;
+        bool t = false, hp = false, pg = false, tx = false, pr = false, um = false, ov = false;
         int judged = 0;
         for (uint32_t d = 0; d < n; d++) {
             if (retry[d] != 3) continue;
@@ -1433,9 +1485,14 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
             t = t || 2 * x.pad[HDR_UTN] > launched.UT;
             hp = hp || 2 * x.heap_n > launched.PH;
             pg = pg || 2 * (np + 8) > launched.PP;
+            const int cause = x.status == 0 ? x.pad[HDR_DIAG] : 0;   // an arena hand-over (pg_arena_room)
+            tx = tx || cause == 4;
+            pr = pr || cause == 5;
+            um = um || cause == 9;
+            ov = ov || cause == 11;
         }
         if (moving.empty()) return 0;
-        if (!t && !hp && !pg) t = hp = true;   // a single message's bound (a long range): its table / heap terms
+        if (!t && !hp && !pg && !tx && !pr && !um && !ov) t = hp = true;   // a single message's bound (a long range): its table / heap terms
         h->grown_last += (uint32_t)moving.size();
         h->grow_rounds_last++;
         // the new capacities: doubled where the documents ran out, never below the big
@@ -1461,21 +1518,37 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
             nc.PH = std::max(nc.PH, h->big_caps.PH);
             nc.UT = std::max(nc.UT, h->big_caps.UT);
         }
+        // the text / property arenas and the uid map (HBM only): doubled when a document's live
+        // text / records / segments fill more than half of them after a compaction
+        const int lT = launched_big ? st.big.T : st.T, lP = launched_big ? st.big.P : st.P;
+        const int lU = launched_big ? st.big.UM : st.UM, lO = launched_big ? st.big.OA : st.OA;
+        int nT = judged && tx ? (int)std::min<int64_t>(2LL * lT, 1 << 28) : lT;
+        int nP = judged && pr ? (int)std::min<int64_t>(2LL * lP, 1 << 26) : lP;
+        int nU = judged && um ? (int)std::min<int64_t>(2LL * lU, 1 << 24) : lU;
+        int nO = judged && ov ? (int)std::min<int64_t>(2LL * lO, 1 << 30) : lO;
+        if (have) {
+            nT = std::max(nT, st.big.T);
+            nP = std::max(nP, st.big.P);
+            nU = std::max(nU, st.big.UM);
+            nO = std::max(nO, st.big.OA);
+        }
         int rc = 0;
         PagedCaps pc = nc;
         bool big = true;
-        if (same(nc, launched)) {
-            // nothing can grow: the documents run to their end at the capacities they were
-            // handed over at (in their own region) and fail as before the step existed only
-            // if they do outgrow them
+        if (same(nc, launched) && nT == lT && nP == lP && nU == lU && nO == lO) {
+            // no LDS capacity can grow: the documents run to their end at the capacities they
+            // were handed over at (in their own region) and fail as before the step existed
+            // only if they do outgrow them -- the arenas and the uid map still grow
             pc = launched;
-            pc.grow = 0;
+            pc.grow = 2;
             big = launched_big;
         } else {
             bool all_big = have;
             for (uint32_t d : moving) all_big = all_big && !h->bslot_h.empty() && h->bslot_h[d] >= 0;
-            if (!(all_big && same(nc, h->big_caps))) rc = regrow(h, moving, nc);
-            pc.grow = same(doubled(nc), nc) ? 0 : 1;
+            if (!(all_big && same(nc, h->big_caps) && nT == st.big.T && nP == st.big.P && nU == st.big.UM &&
+                  nO == st.big.OA))
+                rc = regrow(h, moving, nc, nT, nP, nU, nO);
+            pc.grow = 1;   // (the arenas can always grow; a round that raises nothing runs with grow 0)
         }
         if (rc) {
             hipLaunchKernelGGL(k_fail_grow, dim3((n + 255) / 256), dim3(256), 0, h->stream, st);
@@ -1521,6 +1594,7 @@ void mt_batch_free(mt_batch *b) {
     if (b->ops) hipFree(b->ops);
     if (b->text) hipFree(b->text);
     if (b->props) hipFree(b->props);
+    if (b->order) hipFree(b->order);
     delete b;
 }
 
@@ -1889,19 +1963,20 @@ int mt_extract_snapshots(mt_handle *h, int64_t *io, mt_seg_rec *recs, uint16_t *
 // to back and rebases their op records, whose offsets the generator wrote local to the
 // document's region: the wire format's u32 offsets address the whole batch, and the strided
 // layout would pass 2^32 units (C3: at document ~53.7k).
-__global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, int64_t ops_per_doc, const uint16_t *text_in,
-                                                     const uint32_t *props_in, int64_t tstride, int64_t pstride,
+__global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, const int64_t *off, const uint16_t *text_in,
+                                                     const uint32_t *props_in, int64_t text_max, int64_t prec_words,
                                                      const int64_t *used, const int64_t *base, uint16_t *text_out,
                                                      uint32_t *props_out, int n_docs) {
     const int doc = blockIdx.x;
     if (doc >= n_docs) return;
     const int64_t tu = used[2 * doc], pu = used[2 * doc + 1], tb = base[2 * doc], pb = base[2 * doc + 1];
-    const uint16_t *ts = text_in + doc * tstride;
-    const uint32_t *ps = props_in + doc * pstride;
+    const int64_t o0 = off[doc], n = off[doc + 1] - o0;
+    const uint16_t *ts = text_in + o0 * text_max + doc;   // the generator's region (gen_begin)
+    const uint32_t *ps = props_in + o0 * prec_words + doc;
     for (int64_t i = threadIdx.x; i < tu; i += blockDim.x) text_out[tb + i] = ts[i];
     for (int64_t i = threadIdx.x; i < pu; i += blockDim.x) props_out[pb + i] = ps[i];
-    mt_op_rec *o = ops + doc * ops_per_doc;
-    for (int64_t k = threadIdx.x; k < ops_per_doc; k += blockDim.x) {
+    mt_op_rec *o = ops + o0;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
         mt_op_rec op = o[k];
         if (op.kind == MT_OP_INSERT && !(op.flags & MT_F_MARKER)) op.payload += (uint32_t)tb;
         if (op.props != MT_NO_PROPS) op.props += (uint32_t)pb;
@@ -1911,7 +1986,15 @@ __global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, int64_t ops
 
 mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                       int32_t *view_len_trace) {
+    return mt_generate_docs(h, cfg, doc_index_base, nullptr, view_len_trace);
+}
+
+mt_batch *mt_generate_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
+                           const int32_t *ops_per_doc, int32_t *view_len_trace) {
     if (!h || !cfg || cfg->writers < 1 || cfg->ops < 0) return nullptr;
+    if (ops_per_doc)
+        for (uint32_t d = 0; d < h->n_docs; d++)
+            if (ops_per_doc[d] < 0) return nullptr;
     if (h->pending && mt_settle(h) != 0) return nullptr;
     h->max_cli = std::max(h->max_cli, cfg->writers);
     if (h->ordinals) {   // the generator's kernels keep no ordinals
@@ -1923,14 +2006,17 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
     b->device = h->device;
     b->n_docs = h->n_docs;
     const int64_t N = h->n_docs, ops = cfg->ops;
+    // every document's region at fixed strides per message (gen_begin)
     const int64_t tstride = ops * cfg->text_max + 1;
     const int64_t pstride = ops * (1 + 2 * (int64_t)cfg->max_keys_per_op) + 1;
-    b->n_ops = N * ops;
-    b->text_len = N * tstride;
-    b->props_len = N * pstride;
+    std::vector<int64_t> off(N + 1);
+    for (int64_t i = 0; i <= N; i++) off[i] = ops_per_doc ? (i ? off[i - 1] + ops_per_doc[i - 1] : 0) : i * ops;
+    b->n_ops = off[N];
+    b->text_len = off[N] * cfg->text_max + N;
+    b->props_len = off[N] * (1 + 2 * (int64_t)cfg->max_keys_per_op) + N;
     int32_t *d_fail = nullptr, *d_trace = nullptr;
     int64_t *d_used = nullptr;
-    if (view_len_trace && hipMalloc(&d_trace, std::max<int64_t>(N * ops, 1) * 16) != hipSuccess) {
+    if (view_len_trace && hipMalloc(&d_trace, std::max<int64_t>(b->n_ops, 1) * 16) != hipSuccess) {
         delete b;
         return nullptr;
     }
@@ -1940,10 +2026,9 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
               hipMalloc(&b->props, b->props_len * 4) == hipSuccess &&
               hipMalloc(&d_fail, N * 4) == hipSuccess && hipMalloc(&d_used, N * 16) == hipSuccess;
     if (ok) {
-        std::vector<int64_t> off(N + 1);
-        for (int64_t i = 0; i <= N; i++) off[i] = i * ops;
         ok = hipMemcpy(b->off, off.data(), (N + 1) * 8, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemset(d_fail, 0, N * 4) == hipSuccess;
+             hipMemset(d_fail, 0, N * 4) == hipSuccess && set_order(b, off.data());
+        h->st.gen_off = ops_per_doc ? b->off : nullptr;   // (the generator kernels' lengths)
     }
     if (ok) ok = hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream) == hipSuccess;
     if (ok) {
@@ -2014,8 +2099,9 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
         if (ok) ok = hipMalloc(&d_base, N * 16) == hipSuccess &&
                      hipMemcpy(d_base, base.data(), N * 16, hipMemcpyHostToDevice) == hipSuccess;
         if (ok) {
-            hipLaunchKernelGGL(k_gen_compact, dim3(h->n_docs), dim3(256), 0, h->stream, b->ops, ops, b->text,
-                               b->props, tstride, pstride, d_used, d_base, nt, np, h->n_docs);
+            hipLaunchKernelGGL(k_gen_compact, dim3(h->n_docs), dim3(256), 0, h->stream, b->ops, b->off, b->text,
+                               b->props, (int64_t)cfg->text_max, 1 + 2 * (int64_t)cfg->max_keys_per_op, d_used,
+                               d_base, nt, np, h->n_docs);
             ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess;
         }
         if (d_base) hipFree(d_base);
@@ -2031,8 +2117,9 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
             if (np) hipFree(np);
         }
     }
+    h->st.gen_off = nullptr;
     if (ok && d_trace)
-        ok = hipMemcpy(view_len_trace, d_trace, N * ops * 16, hipMemcpyDeviceToHost) == hipSuccess;
+        ok = hipMemcpy(view_len_trace, d_trace, b->n_ops * 16, hipMemcpyDeviceToHost) == hipSuccess;
     if (d_trace) hipFree(d_trace);
     if (d_fail) hipFree(d_fail);
     if (d_used) hipFree(d_used);
@@ -2095,6 +2182,7 @@ struct HostDoc {
     std::vector<int32_t> rpage, rslot, rpos;
     std::vector<PageMeta> pmeta;
     int32_t oslot[2 * MT_OSLOTS];   // overlap slots {client, last seq}
+    std::vector<uint16_t> ovf;      // paged: the overflow overlap arena (MT_OVF_BIT masks)
 };
 // document doc's paged arrays, host side (the growth step's slot mirror)
 static PagedBase host_paged(const mt_handle *h, uint32_t doc) {
@@ -2124,6 +2212,8 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
         HIPCHK(h, hipMemcpy(pA.data(), pb.A, slots * sizeof(int4), hipMemcpyDeviceToHost));
         HIPCHK(h, hipMemcpy(pO.data(), pb.O, slots * sizeof(u64), hipMemcpyDeviceToHost));
         HIPCHK(h, hipMemcpy(pB.data(), pb.B, slots * sizeof(uint4), hipMemcpyDeviceToHost));
+        hd.ovf.assign(pb.ovf ? pb.OA : 0, 0);
+        if (pb.ovf) HIPCHK(h, hipMemcpy(hd.ovf.data(), pb.ovf, (size_t)pb.OA * 2, hipMemcpyDeviceToHost));
         hd.A.clear();
         hd.O.clear();
         hd.B.clear();
@@ -2164,15 +2254,16 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
     hd.cnt.resize((size_t)MT_LV * st.B);
     HIPCHK(h, hipMemcpy(hd.cnt.data(), st.cnt + (size_t)doc * MT_LV * st.B, MT_LV * st.B, hipMemcpyDeviceToHost));
     }
+    const PagedBase ar = host_paged(h, doc);   // (the arenas of the document's region)
     if (with_text) {
-        hd.text.resize(st.T);
-        HIPCHK(h, hipMemcpy(hd.text.data(), st.text + ((size_t)doc * 2 + hd.hdr.text_half) * st.T, st.T * 2,
+        hd.text.resize(ar.T);
+        HIPCHK(h, hipMemcpy(hd.text.data(), ar.text + (size_t)hd.hdr.text_half * ar.T, (size_t)ar.T * 2,
                             hipMemcpyDeviceToHost));
     }
     if (with_props) {
-        const size_t words = (size_t)st.P * MT_PREC;
+        const size_t words = (size_t)ar.P * MT_PREC;
         hd.props.resize(words);
-        HIPCHK(h, hipMemcpy(hd.props.data(), st.props + ((size_t)doc * 2 + hd.hdr.props_half) * words, words * 4,
+        HIPCHK(h, hipMemcpy(hd.props.data(), ar.props + (size_t)hd.hdr.props_half * words, words * 4,
                             hipMemcpyDeviceToHost));
     }
     return 0;
@@ -2345,7 +2436,13 @@ static int host_view_len(const HostDoc &hd, const HostView &v, int i) {
     if (v.local) return a.z == MT_RSEQ_NONE ? a.x : 0;
     const int cli = (int)(short)(a.w & 0xFFFF), rcli = (int)(short)((uint32_t)a.w >> 16);
     const u64 o = hd.O[i];
-    const bool ovl = v.cs >= 1 && ((o >> (v.cs - 1)) & 1ull);
+    bool ovl = v.cs >= 1 && ((o >> (v.cs - 1)) & 1ull);
+    if (o & MT_OVF_BIT) {   // an overflow set: the segment's whole overlap list
+        ovl = false;
+        const size_t off = (uint32_t)o;
+        const size_t n = off < hd.ovf.size() ? hd.ovf[off] : 0;
+        for (size_t k = 1; k <= n && off + k < hd.ovf.size(); k++) ovl = ovl || hd.ovf[off + k] == (uint16_t)v.c;
+    }
     const bool ins = cli == v.c || (a.y != -1 && a.y <= v.r);
     const bool gone = a.z != MT_RSEQ_NONE && (rcli == v.c || ovl || (a.z != -1 && a.z <= v.r));
     return ins && !gone ? a.x : 0;

@@ -38,6 +38,9 @@ FIXTURES = {
     # 200 writers, lag 100: overlapping removes by short ids far above 64 (removedClientOverlap
     # is an unbounded list; the device masks index reusable overlap slots)
     "ref_wide": ("c4", {"ops": 4000, "writers": 200, "lag": 100, "seed": 7171}, 2),
+    # 200 writers, lag 400: ~80 clients' overlapping removes unsettled at once -- more than the
+    # 63 overlap slots, so the device keeps overflow sets (MT_OVF_BIT)
+    "ref_wide400": ("c4", {"ops": 3000, "writers": 200, "lag": 400, "seed": 7272}, 2),
     # a long-lived document: 30k messages (~45k segment ids created, ~12k live segments)
     "ref_c3_long": ("c3", {"ops": 30000}, 2),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),

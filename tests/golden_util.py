@@ -20,6 +20,9 @@ ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_l
 FULL_FIXTURES = ["ref_c3_full", "ref_c4_full"]
 # long-lived documents (30k messages)
 LONG_FIXTURES = ["ref_c3_long"]
+# more clients' overlapping removes unsettled at once than the 63 overlap slots (paged tiers:
+# overflow sets)
+WIDE_FIXTURES = ["ref_wide400"]
 SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
 # error model (tests/golden/make_golden.py --errors): the reference's throw -> mt_doc_status
 ERROR_STATUS = {
