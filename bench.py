@@ -583,7 +583,14 @@ def main():
     if args.config == "live":
         return run_live(args, rank, world, local_rank, dist)
     cfg = dict(configs[args.config])
-    if args.config == "c5":
+    if args.config == "c3skew":   # skewed document lengths (bench_skew.py)
+        import bench_skew
+        line = bench_skew.run_skew(args, cfg, rank, world, local_rank, dist, sys.modules[__name__])
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
         run_c5(args, cfg, rank, world, local_rank, dist)
         if dist is not None:
             dist.destroy_process_group()

@@ -1,0 +1,130 @@
+"""bench.py --config c3skew: the C3 job (10^9 messages over 100k documents) with Zipf-skewed
+document lengths (fluidframework_amd/skew.py; SURVEY.md section 7 hard part 5, 8e).
+
+Documents are sharded by message count (skew.shard_range_ops), grouped into size classes on
+every rank, and each class is replayed by its own handle -- capacities sized for its longest
+document, its own HIP stream -- with the class of the longest documents launched first; inside
+each batch the library dispatches documents longest first (mt_batch order).  The step is the
+whole rank's job: every class reset + applied, then every class synchronised.  Inputs are
+generated on the GPU (untimed, mt_generate_docs) and stay resident in HBM.
+"""
+import time
+
+import numpy as np
+
+
+def class_caps(bench, cfg, max_ops):
+    """Capacities of the handle of a size class: the C3 bench sizing at <= 10k messages (its
+    tight tier, fixed at compile time), else the full paged tier sized from the C3 high-water
+    marks (183 pages, 208 table entries, 173 heap entries at 10k messages: pages grow with the
+    length, table and heap with the collaboration window), text arenas by length."""
+    caps = bench.capacities(dict(cfg, ops=min(max_ops, 10000)))
+    if max_ops <= 10000:
+        return caps
+    text = 1 << 16
+    while text < 4 * max_ops:
+        text *= 2
+    segs = int(max_ops * 0.5) + 512
+    caps.update(page_capacity=int(max_ops * 0.0183 * 1.12) + 16, text_capacity=text, props_capacity=segs + 256,
+                uid_capacity=min(1 << 20, max(1 << 16, 2 * segs)))
+    for k in ("lds_page_capacity", "lds_unsettled_capacity", "lds_page_heap_capacity", "lds_narrow_overlap"):
+        caps.pop(k, None)
+    return caps
+
+
+def run_skew(args, cfg, rank, world, local_rank, dist, bench):
+    from fluidframework_amd import MergeTreeBatch
+    from fluidframework_amd.skew import shard_range_ops, size_classes, zipf_lengths
+    total_docs = cfg["docs"]
+    lens_all = zipf_lengths(total_docs, total_docs * cfg["ops"], cfg["zipf_s"], cfg["max_ops"], cfg["lens_seed"])
+    lo, hi = shard_range_ops(lens_all, world, rank)
+    ids = np.arange(lo, hi, dtype=np.int32)
+    lens = lens_all[lo:hi]
+    classes = size_classes(lens, cfg["classes"])
+    t_gen = time.time()
+    runs = []
+    for max_ops, idx in classes:        # longest class first
+        mt = MergeTreeBatch(len(idx), device=local_rank, **class_caps(bench, cfg, max_ops))
+        ccfg = dict(cfg, ops=int(max_ops))
+        batch = mt.generate(ccfg, ops_per_doc=lens[idx], doc_ids=ids[idx])
+        gsum = mt.checksums()
+        so, sd = mt.generated_seeds(ccfg, doc_ids=ids[idx])
+        mt.load_initial_text(so, sd)
+        runs.append(dict(max_ops=max_ops, idx=idx, mt=mt, batch=batch, gen=gsum, ops=int(lens[idx].sum()),
+                         cfg=ccfg))
+    t_gen = time.time() - t_gen
+
+    def step():
+        for r in runs:
+            r["mt"].reset()
+            r["batch"].apply_async()
+        for r in runs:
+            r["mt"].sync()
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    n_ops = int(lens.sum())
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        t = torch.tensor([n_ops], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        total_ops = int(t.item())
+    else:
+        total_ops = n_ops
+    ok = True
+    per_class = []
+    for r in runs:
+        st = r["mt"].status()
+        same = bool(np.array_equal(r["mt"].checksums(), r["gen"])) and int((st != 0).sum()) == 0
+        ok = ok and same
+        per_class.append(dict(max_ops=r["max_ops"], docs=int(len(r["idx"])), ops=r["ops"],
+                              replay_equals_generation=same, grown=r["mt"].last_grown()["grown"]))
+    # oracle sample: the longest and a middle document of every class (rank 0)
+    mism, sampled = 0, 0
+    if rank == 0 and not args.no_cpu:
+        import os
+        import sys
+        sys.path.insert(0, os.path.join(bench.REPO, "oracle"))
+        import pyoracle
+        for r in runs:
+            order = np.argsort(-lens[r["idx"]], kind="stable")
+            for j in sorted({int(order[0]), int(order[len(order) // 2])}):
+                d = int(r["idx"][j])
+                g = pyoracle.generate(dict(cfg, ops=int(lens[d])), int(ids[d]), keep=True)
+                osum = g["doc"].outputs()["checksum"]
+                got = r["mt"].checksums()[j]
+                sampled += 1
+                mism += int(any(got[f] != osum[f] for f in ("length", "text_hash", "props_hash", "delta_hash")))
+    if dist is not None:
+        import torch
+        t = torch.tensor([1 if ok else 0], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    if rank != 0:
+        return None
+    value = total_ops * args.steps / elapsed
+    line = {"metric": "sequenced merge-tree ops applied per second", "value": round(value, 1), "unit": "ops/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1000.0 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "int32", "data": "synthetic (device generator, Zipf lengths)",
+            "config": {"workload": "c3skew", "docs_total": total_docs, "ops_total": int(lens_all.sum()),
+                       "zipf_s": cfg["zipf_s"], "max_ops": cfg["max_ops"], "classes": cfg["classes"],
+                       "median_ops": int(np.median(lens_all)), "docs_at_max": int((lens_all == cfg["max_ops"]).sum()),
+                       "parallelism": f"dp{world} (op-balanced shards)"},
+            "parity": {"replay_equals_generation": ok, "oracle_docs": sampled, "oracle_mismatches": mism},
+            "per_class": per_class, "gen_s": round(t_gen, 1)}
+    return line

@@ -285,29 +285,33 @@ class MergeTreeBatch:
     def upload(self, a):
         return DeviceBatch(self, a)
 
-    def generate(self, cfg, doc_base=0, trace=None, ops_per_doc=None):
-        """Device-generated batch (mt_generate); ops_per_doc: a length per document
-        (mt_generate_docs), else cfg["ops"] each."""
+    def generate(self, cfg, doc_base=0, trace=None, ops_per_doc=None, doc_ids=None):
+        """Device-generated batch (mt_generate); ops_per_doc: a length per document, doc_ids:
+        their global indices (mt_generate_docs), else cfg["ops"] each and doc_base + d."""
         c = _native.gen_cfg(cfg)
-        if ops_per_doc is not None:
-            lens = np.ascontiguousarray(ops_per_doc, dtype=np.int32)
-            if lens.shape != (self.n_docs,):
-                raise ValueError("ops_per_doc: one length per document")
-            b = self.lib.mt_generate_docs(self.h, ctypes.byref(c), doc_base, _native.ptr(lens), _native.ptr(trace))
+        if ops_per_doc is not None or doc_ids is not None:
+            lens = None if ops_per_doc is None else np.ascontiguousarray(ops_per_doc, dtype=np.int32)
+            ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.int32)
+            for x in (lens, ids):
+                if x is not None and x.shape != (self.n_docs,):
+                    raise ValueError("ops_per_doc / doc_ids: one per document")
+            b = self.lib.mt_generate_docs(self.h, ctypes.byref(c), doc_base, _native.ptr(lens), _native.ptr(ids),
+                                          _native.ptr(trace))
         else:
             b = self.lib.mt_generate(self.h, ctypes.byref(c), doc_base, _native.ptr(trace))
         if not b:
             raise RuntimeError(f"mt_generate failed: {self.lib.mt_last_error(self.h).decode()}")
         return DeviceBatch(self, None, handle=b)
 
-    def generated_seeds(self, cfg, doc_base=0):
+    def generated_seeds(self, cfg, doc_base=0, doc_ids=None):
         c = _native.gen_cfg(cfg)
+        ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.int32)
         off = np.zeros(self.n_docs + 1, dtype=np.int64)
-        self._check(self.lib.mt_generated_seeds(self.h, ctypes.byref(c), doc_base, _native.ptr(off), None),
-                    "mt_generated_seeds")
+        self._check(self.lib.mt_generated_seeds_docs(self.h, ctypes.byref(c), doc_base, _native.ptr(ids),
+                                                     _native.ptr(off), None), "mt_generated_seeds")
         seed = np.zeros(max(int(off[-1]), 1), dtype=np.uint16)
-        self._check(self.lib.mt_generated_seeds(self.h, ctypes.byref(c), doc_base, _native.ptr(off),
-                                                _native.ptr(seed)), "mt_generated_seeds")
+        self._check(self.lib.mt_generated_seeds_docs(self.h, ctypes.byref(c), doc_base, _native.ptr(ids),
+                                                     _native.ptr(off), _native.ptr(seed)), "mt_generated_seeds")
         return off, seed
 
     def sync(self):

@@ -81,7 +81,8 @@ SIGNATURES = [
     ("mt_last_paged_peaks", _I, [_P, _P]),
     ("mt_last_grown", _I, [_P, _P]),
     ("mt_generate", _P, [_P, _P, _U32, _P]),
-    ("mt_generate_docs", _P, [_P, _P, _U32, _P, _P]),
+    ("mt_generate_docs", _P, [_P, _P, _U32, _P, _P, _P]),
+    ("mt_generated_seeds_docs", _I, [_P, _P, _U32, _P, _P, _P]),
     ("mt_generated_seeds", _I, [_P, _P, _U32, _P, _P]),
     ("mt_batch_sizes", _I, [_P, _P, _P, _P]),
     ("mt_batch_download", _I, [_P, _P, _P, _P, _P]),

@@ -215,6 +215,8 @@ struct DevState {
     unsigned long long *prof; // [128] section timers of a -DMT_PROF build (null otherwise)
     const int64_t *gen_off;   // mt_generate_docs: [n_docs + 1] op offsets (per-document lengths);
                               // null: cfg.ops messages every document
+    const int32_t *gen_ids;   // mt_generate_docs: [n_docs] global document indices (draws); null:
+                              // doc_index_base + doc
     const int32_t *order;     // the applied batch's dispatch order (documents by message count,
                               // longest first); null: index order (equal lengths)
 };

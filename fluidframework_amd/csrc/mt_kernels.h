@@ -258,7 +258,7 @@ __device__ static void gen_begin(GenCtx &g, const DevState &st, const mt_gen_cfg
     const int W = cfg.writers;
     g.last_ref = (LDS_AS int32_t *)gen_lds;
     g.short_id = g.last_ref + (W + 1);
-    rng_init(g.rng, cfg.seed, gdoc);
+    rng_init(g.rng, cfg.seed, st.gen_ids ? st.gen_ids[doc] : gdoc);
     // seed text (drawn exactly like the oracle / reference harness)
     uint16_t *arena = st.text + (size_t)doc * 2 * st.T;
     for (int i = 0; i < cfg.seed_len; i++) {

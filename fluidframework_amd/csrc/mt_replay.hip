@@ -1986,11 +1986,11 @@ __global__ void __launch_bounds__(256) k_gen_compact(mt_op_rec *ops, const int64
 
 mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                       int32_t *view_len_trace) {
-    return mt_generate_docs(h, cfg, doc_index_base, nullptr, view_len_trace);
+    return mt_generate_docs(h, cfg, doc_index_base, nullptr, nullptr, view_len_trace);
 }
 
 mt_batch *mt_generate_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
-                           const int32_t *ops_per_doc, int32_t *view_len_trace) {
+                           const int32_t *ops_per_doc, const int32_t *doc_ids, int32_t *view_len_trace) {
     if (!h || !cfg || cfg->writers < 1 || cfg->ops < 0) return nullptr;
     if (ops_per_doc)
         for (uint32_t d = 0; d < h->n_docs; d++)
@@ -2030,6 +2030,10 @@ mt_batch *mt_generate_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_ind
              hipMemset(d_fail, 0, N * 4) == hipSuccess && set_order(b, off.data());
         h->st.gen_off = ops_per_doc ? b->off : nullptr;   // (the generator kernels' lengths)
     }
+    int32_t *d_ids = nullptr;   // the documents' global indices (their draws)
+    if (ok && doc_ids)
+        ok = hipMalloc(&d_ids, N * 4) == hipSuccess && hipMemcpy(d_ids, doc_ids, N * 4, hipMemcpyHostToDevice) == hipSuccess;
+    h->st.gen_ids = d_ids;
     if (ok) ok = hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream) == hipSuccess;
     if (ok) {
         const int gw = 2 * (cfg->writers + 1);
@@ -2118,6 +2122,8 @@ mt_batch *mt_generate_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_ind
         }
     }
     h->st.gen_off = nullptr;
+    h->st.gen_ids = nullptr;
+    if (d_ids) hipFree(d_ids);
     if (ok && d_trace)
         ok = hipMemcpy(view_len_trace, d_trace, b->n_ops * 16, hipMemcpyDeviceToHost) == hipSuccess;
     if (d_trace) hipFree(d_trace);
@@ -2133,12 +2139,16 @@ mt_batch *mt_generate_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_ind
 
 int mt_generated_seeds(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                        int64_t *seed_off, uint16_t *seed_text) {
+    return mt_generated_seeds_docs(h, cfg, doc_index_base, nullptr, seed_off, seed_text);
+}
+int mt_generated_seeds_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base, const int32_t *doc_ids,
+                            int64_t *seed_off, uint16_t *seed_text) {
     if (!h || !cfg) return MT_E_INVALID;
     int64_t pos = 0;
     for (uint32_t doc = 0; doc < h->n_docs; doc++) {
         seed_off[doc] = pos;
         Rng r;
-        rng_init(r, cfg->seed, (int)(doc_index_base + doc));
+        rng_init(r, cfg->seed, doc_ids ? doc_ids[doc] : (int)(doc_index_base + doc));
         for (int i = 0; i < cfg->seed_len; i++) {
             (void)rng_next(r);
             const uint16_t ch = (uint16_t)(97 + rng_uniform(r, 26));

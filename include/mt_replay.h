@@ -227,12 +227,16 @@ mt_batch *mt_generate(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_ba
                                                  per op {view length, n_seg, refSeq,
                                                  client} */);
 /* mt_generate with a length per document: ops_per_doc[n_docs] messages (nullable: cfg->ops
-   each).  Document d's stream is the first ops_per_doc[d] messages of the stream mt_generate
-   draws for it (the draws do not depend on the length), so skewed batches (bench c3skew)
-   reuse the oracle's generator for parity. */
+   each), and global document indices doc_ids[n_docs] (nullable: doc_index_base + d).
+   Document d's stream is the first ops_per_doc[d] messages of the stream mt_generate draws
+   for its global index (the draws do not depend on the length), so skewed batches (bench
+   c3skew) reuse the oracle's generator for parity. */
 mt_batch *mt_generate_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
-                           const int32_t *ops_per_doc, int32_t *view_len_trace);
-/* Initial seed texts as the generator draws them (seed_off[n_docs+1], seed_text). */
+                           const int32_t *ops_per_doc, const int32_t *doc_ids, int32_t *view_len_trace);
+/* Initial seed texts as the generator draws them (seed_off[n_docs+1], seed_text); _docs:
+   for the global indices doc_ids[n_docs] (nullable: doc_index_base + d). */
+int mt_generated_seeds_docs(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base, const int32_t *doc_ids,
+                            int64_t *seed_off, uint16_t *seed_text);
 int mt_generated_seeds(mt_handle *h, const mt_gen_cfg *cfg, uint32_t doc_index_base,
                        int64_t *seed_off, uint16_t *seed_text);
 /* Copies a batch back to the host (arrays sized by mt_batch_sizes). */

@@ -97,27 +97,28 @@ def test_gpu_skewed_batch_longest_first(tier):
 
 
 def test_gpu_generator_per_document_lengths(oracle_lib):
-    """mt_generate_docs: document d's stream is the first ops_per_doc[d] messages of its
-    mt_generate stream (the C restatement's generator at that length), and the skewed batch
-    replays, longest first, to the generated state."""
+    """mt_generate_docs: document d's stream is the first ops_per_doc[d] messages of the
+    mt_generate stream of its global index doc_ids[d] (the C restatement's generator at that
+    length and index), and the skewed batch replays, longest first, to the generated state."""
     import json
     import os
     cfg = dict(json.load(open(os.path.join(gu.GOLDEN, "..", "..", "bench", "configs.json")))["c3"], ops=3000)
     lens = np.array([40, 3000, 700, 1, 0, 2200, 150, 1200], dtype=np.int32)
+    ids = np.array([9, 3, 40, 7, 1, 12, 2, 100], dtype=np.int32)   # global indices (the draws)
     mt = _gpu_batch(len(lens), **TIERS["tight"])
-    b = mt.generate(cfg, ops_per_doc=lens)
+    b = mt.generate(cfg, ops_per_doc=lens, doc_ids=ids)
     got = b.download()
     assert np.array_equal(np.diff(got["doc_off"]), lens)
     gsums = mt.checksums()
     for d, n in enumerate(lens):
-        g = oracle_lib.generate(dict(cfg, ops=int(n)), d, keep=True)
+        g = oracle_lib.generate(dict(cfg, ops=int(n)), int(ids[d]), keep=True)
         lo, hi = got["doc_off"][d], got["doc_off"][d + 1]
         f = ["seq", "ref_seq", "min_seq", "pos1", "pos2", "client", "kind"]
         assert np.array_equal(got["ops"][lo:hi][f], g["ops"][f]), d
         osum = g["doc"].outputs()["checksum"]
         for k in ("length", "text_hash", "props_hash", "delta_hash"):
             assert gsums[d][k] == osum[k], (d, k)
-    seed_off, seed = mt.generated_seeds(cfg)
+    seed_off, seed = mt.generated_seeds(cfg, doc_ids=ids)
     mt.load_initial_text(seed_off, seed)
     b.apply_async()
     mt.sync()
