@@ -8,27 +8,32 @@ each batch the library dispatches documents longest first (mt_batch order).  The
 whole rank's job: every class reset + applied, then every class synchronised.  Inputs are
 generated on the GPU (untimed, mt_generate_docs) and stay resident in HBM.
 """
+import os
+import sys
 import time
 
 import numpy as np
 
 
 def class_caps(bench, cfg, max_ops):
-    """Capacities of the handle of a size class: the C3 bench sizing at <= 10k messages (its
-    tight tier, fixed at compile time), else the full paged tier sized from the C3 high-water
-    marks (183 pages, 208 table entries, 173 heap entries at 10k messages: pages grow with the
-    length, table and heap with the collaboration window), text arenas by length."""
-    caps = bench.capacities(dict(cfg, ops=min(max_ops, 10000)))
-    if max_ops <= 10000:
-        return caps
-    text = 1 << 16
-    while text < 4 * max_ops:
+    """Capacities of the handle of a size class, sized for its longest document from the C3
+    high-water marks (183 pages, ~3.5k live segments, ~11k live text units at 10k messages:
+    pages and segments grow with the length, the unsettled table and the heap with the
+    collaboration window).  Classes up to 10k messages keep the C3 bench's tight tier (its LDS
+    capacities fixed at compile time; the HBM pages must hold its 192); longer ones run the
+    full-capacity paged tier at their own capacities."""
+    caps = bench.capacities(dict(cfg, ops=10000))
+    text = 4096
+    while text < 2.5 * max_ops:
         text *= 2
-    segs = int(max_ops * 0.5) + 512
-    caps.update(page_capacity=int(max_ops * 0.0183 * 1.12) + 16, text_capacity=text, props_capacity=segs + 256,
-                uid_capacity=min(1 << 20, max(1 << 16, 2 * segs)))
-    for k in ("lds_page_capacity", "lds_unsettled_capacity", "lds_page_heap_capacity", "lds_narrow_overlap"):
-        caps.pop(k, None)
+    uid = 1 << 15
+    while uid < 4 * max_ops:
+        uid *= 2
+    caps.update(page_capacity=max(192, int(max_ops * 0.0183 * 1.12) + 16), text_capacity=text,
+                props_capacity=int(0.3 * max_ops) + 512, uid_capacity=min(uid, 1 << 20))
+    if max_ops > 10000:
+        for k in ("lds_page_capacity", "lds_unsettled_capacity", "lds_page_heap_capacity", "lds_narrow_overlap"):
+            caps.pop(k, None)
     return caps
 
 
@@ -52,6 +57,8 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
         mt.load_initial_text(so, sd)
         runs.append(dict(max_ops=max_ops, idx=idx, mt=mt, batch=batch, gen=gsum, ops=int(lens[idx].sum()),
                          cfg=ccfg))
+        print(f"c3skew: class <= {max_ops}: {len(idx)} documents, {runs[-1]['ops']} messages generated "
+              f"({time.time() - t_gen:.1f} s)", file=sys.stderr, flush=True)
     t_gen = time.time() - t_gen
 
     def step():
@@ -70,8 +77,9 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
 
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         step()
+        print(f"c3skew: step {k + 1}: {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     barrier()
     elapsed = time.perf_counter() - t0
     n_ops = int(lens.sum())
@@ -96,8 +104,6 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     # oracle sample: the longest and a middle document of every class (rank 0)
     mism, sampled = 0, 0
     if rank == 0 and not args.no_cpu:
-        import os
-        import sys
         sys.path.insert(0, os.path.join(bench.REPO, "oracle"))
         import pyoracle
         for r in runs:
@@ -117,7 +123,7 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     if rank != 0:
         return None
     value = total_ops * args.steps / elapsed
-    line = {"metric": "sequenced merge-tree ops applied per second", "value": round(value, 1), "unit": "ops/s",
+    line = {"metric": "sequenced merge-tree ops applied/sec (node) at 100k docs; bit-exact text+props", "value": round(value, 1), "unit": "ops/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1000.0 / args.steps, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "int32", "data": "synthetic (device generator, Zipf lengths)",

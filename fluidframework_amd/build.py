@@ -68,7 +68,8 @@ def build(force=False, verbose=False):
         obj = os.path.join(obj_dir, f"mtk_{name}.o")
         if only and name not in only:
             base_obj = os.path.join(OBJ_DIR, "libmtreplay", f"mtk_{name}.o")
-            shutil.copyfile(base_obj, obj)
+            if os.path.abspath(base_obj) != os.path.abspath(obj):
+                shutil.copyfile(base_obj, obj)
             link_only.append(obj)
             continue
         jobs.append((src, obj))

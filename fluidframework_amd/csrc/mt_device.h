@@ -64,14 +64,14 @@ static __host__ __device__ inline int pm_bcnt(const PageMeta &m, int q) { return
 static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { return (int8_t)((int)((m.flg2 >> (2 * q)) & 3u) - 1); }
 #define MT_OSLOTS 64
 // Overlap masks use slots 1..63; bit 63 marks an *overflow set* (the last-tier paged
-// instantiations, TierPagedT::kMayGrow, once every slot is taken): the mask's low 32 bits are
+// instantiations with 64-bit masks, TierPagedT::kOvf, once every slot is taken): the mask's low 32 bits are
 // then the offset of the segment's whole removedClientOverlap list in the document's overflow
 // arena ([count, short ids...], u16), which starts with a 4-unit header {top (u32), last seq
 // that made a set (u32)}
 #define MT_OSLOT_USE 63
 #define MT_OVF_BIT (1ull << 63)
 #define MT_OVF_HDR 4
-#define MT_OVF_ARENA 1024      // overflow-arena units per document in the main arrays (the growth step raises it)
+#define MT_OVF_ARENA 8192      // overflow-arena units per document in the main arrays (the growth step raises it)
 #define MT_OSLOT_FREE 0x7FFFFFFF
 #define MT_PG_SLOTS 64
 #define MT_PG_OLB 32          // ordinal characters kept per page for its leaf blocks (16 + scratch)

@@ -33,6 +33,7 @@ template <bool kLogT> struct TierLdsT {
     // document that needs ids 33..64 continues in the next tier (lds_room / load_doc)
     static constexpr int kOvlBits = 32;
     static constexpr bool kMayGrow = false;
+    static constexpr bool kOvf = false;
     typedef uint32_t O_v;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS uint32_t *O_t;
@@ -46,6 +47,7 @@ template <bool kLogT> struct TierGlbT {
     static constexpr bool kLive = false;
     static constexpr int kOvlBits = 64;
     static constexpr bool kMayGrow = false;
+    static constexpr bool kOvf = false;
     typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
@@ -62,6 +64,7 @@ template <bool kLogT> struct TierLiveT {
     static constexpr bool kLive = true;
     static constexpr int kOvlBits = 64;
     static constexpr bool kMayGrow = false;
+    static constexpr bool kOvf = false;
     typedef u64 O_v;
     typedef GLB_AS v4i *A_t;
     typedef GLB_AS u64 *O_t;
@@ -80,6 +83,7 @@ template <bool kLogT> struct TierLiveLdsT {
     static constexpr bool kLive = true;
     static constexpr int kOvlBits = 32;
     static constexpr bool kMayGrow = false;
+    static constexpr bool kOvf = false;
     typedef uint32_t O_v;
     typedef LDS_AS v4i *A_t;
     typedef LDS_AS uint32_t *O_t;
@@ -109,6 +113,8 @@ struct TierPagedT {
     // a last-tier instantiation (runtime capacities, wide masks, full table entries): the
     // launches the growth step may serve (PagedCaps.grow)
     static constexpr bool kMayGrow = !kNarrowT && !kPackedT && kPPT == 0;
+    // 64-bit overlap masks: the tier keeps overflow overlap sets (MT_OVF_BIT)
+    static constexpr bool kOvf = !kNarrowT;
     static constexpr bool kLds = true;
     static constexpr bool kLog = kLogT;
     static constexpr bool kPaged = true;
@@ -384,9 +390,9 @@ TD bool ovf_member(DocT<T> &d, u64 o, int c);
 TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq);
 // nodeLength of a leaf in the remote view (c, r) of document d: view_len, with the segment's
 // overflow set consulted instead of the slot bits when its mask carries MT_OVF_BIT (last-tier
-// paged instantiations only; the others never load such a document)
+// paged instantiations with 64-bit masks; the narrow tier never loads such a document)
 TD int vlen(DocT<T> &d, v4i a, u64 o, int r, int c) {
-    if constexpr (T::kPaged && T::kMayGrow) {
+    if constexpr (T::kPaged && T::kOvf) {
         if (o & MT_OVF_BIT) return ovf_member(d, o, c) ? 0 : view_len(a, 0, r, c, 0);
     }
     return view_len(a, o, r, c, d.ocs);
@@ -2695,7 +2701,7 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
         const bool sel = v && vl > 0 && pex < p2 && pin_ > p1;
         const u64 sel_m = ballot(sel);
         if (sel_m) mark_dirty(d, base + first_lane(sel_m));
-        bool newly = false, bad = false, spill = false;
+        bool newly = false, bad = false, spill = false, want_ovf = false;
         // live documents: a remote remove of a segment the local client removed (unacked)
         // replaces that removal (:2657-2662): no overlap slot, no callback entry
         bool lrem = false;
@@ -2713,9 +2719,9 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                 d.A[i] = a;
             } else if (a.z != MT_RSEQ_NONE) {          // addOverlappingClient :2577-2585
                 bool ovf = false;
-                if constexpr (T::kPaged && T::kMayGrow) ovf = d.ocs == 0 || (o & MT_OVF_BIT);
+                if constexpr (T::kPaged && T::kOvf) ovf = d.ocs == 0 || (o & MT_OVF_BIT);
                 if (ovf) {
-                    // (ovf_mark below)
+                    want_ovf = true;   // (ovf_mark below)
                 } else if (d.ocs == 0) {
                     if (T::kOvlBits < 64)
                         spill = true;
@@ -2740,9 +2746,9 @@ TD bool range_mark(DocT<T> &d, const mt_op_rec &op, const GLB_AS uint32_t *rec, 
                 }
             }
         }
-        if constexpr (T::kPaged && T::kMayGrow) {   // overflow sets: the whole list, in the arena
-            const bool need = rem && sel && !lrem && a.z != MT_RSEQ_NONE && (d.ocs == 0 || (o & MT_OVF_BIT));
-            if (ballot(need) && !ovf_mark(d, need, i, o, c, seq)) bad = true;
+        if constexpr (T::kPaged && T::kOvf) {   // overflow sets: the whole list, in the arena
+            // (want_ovf: decided on the segment's removal state before this message marked it)
+            if (ballot(want_ovf) && !ovf_mark(d, want_ovf, i, o, c, seq)) bad = true;
         }
         uint32_t nh = 0;
         if (!rem && sel) nh = (uint32_t)(d.props_top + __popcll(sel_m & ((1ull << L) - 1ull)));

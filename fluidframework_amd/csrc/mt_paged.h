@@ -45,7 +45,9 @@ template <class T> struct PagedDoc {
     LDS_AS v4i *uA;
     LDS_AS typename T::O_v *uO;
     LDS_AS uint32_t *uL, *uS, *uP;   // T::kPacked: len | seq, rseq (16 bits each, from sbase) |
-    int sbase;                       // page, cli, rcli (16 / 8 / 8 bits) -- tab_get / tab_put
+    int sbase;                       // page, mask index, cli, rcli (8 bits each) -- tab_get / tab_put
+    LDS_AS u64 *uM;                  // T::kPacked: the overlap masks of the entries that have one
+    LDS_AS uint32_t *mbm;            // [MT_PK_MASKS] by index (0: none), and their use bitmap
     GLB_AS v4i *gA;           // this document's pages (slot 0 of page 0)
     GLB_AS u64 *gO;
     GLB_AS v4u *gB;
@@ -71,6 +73,8 @@ template <class T> struct PagedDoc {
                               // uid map, loaded at the message's start (zuid 0: none)
     GLB_AS uint16_t *govf;    // overflow overlap sets (MT_OVF_BIT; last-tier instantiations)
     int ovf_top, ovf_last, OA;   // its fill, the last message that made a set, its capacity
+    int press;                // a compaction left the text (4) / record (5) arena more than 7/8
+                              // full: a tight launch hands the document on (pg_arena_room)
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
                               // window's entries since they were last rebuilt); the current
                               // message's bound (pg_room)
@@ -94,6 +98,7 @@ struct PagedCaps {
 };
 
 #define PW_B 16   // window leaf-block capacity (a page holds <= 9 transiently)
+#define MT_PK_MASKS 256   // packed table: overlap-mask slots (index 0: no mask)
 
 struct PagedLayout {
     uint32_t offWA, offWB, offWO, offWcnt, offWflg, offWends, offWscr, offWnb;
@@ -110,7 +115,10 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     L.offWB = o; o += 16u * MT_PG_SLOTS;
     L.offWO = o; o += (uint32_t)ob * MT_PG_SLOTS;
     L.offUA = o; o += (packed ? 12u : 16u) * UT;
-    L.offUO = o; o += (((uint32_t)ob * UT) + 7u) & ~7u;
+    // packed: a sparse mask table instead of one mask per entry (few unsettled segments carry
+    // an overlap: C4 peaks at ~70 of ~1000)
+    o = (o + 7u) & ~7u;
+    L.offUO = o; o += packed ? 8u * MT_PK_MASKS + MT_PK_MASKS / 8 : ((((uint32_t)ob * UT) + 7u) & ~7u);
     L.offHeap = o; o += 8u * (PH + 1);
     L.offMeta = o; o += (uint32_t)sizeof(PageMeta) * PP;
     L.offUpage = o; o += packed ? 0u : (2u * UT + 3u) & ~3u;
@@ -433,25 +441,84 @@ __device__ __forceinline__ int sq_dec(uint32_t v, int sbase) { return v == 0xFFF
 TD void tab_get(PagedDoc<T> &pd, int e, int &pg, v4i &a, u64 &o) {
     if constexpr (T::kPacked) {
         const uint32_t l = pd.uL[e], sq = pd.uS[e], pc = pd.uP[e];
-        pg = (int)(pc & 0xFFFFu);
+        pg = (int)(pc & 0xFFu);
         a = v4i{(int)l, sq_dec(sq & 0xFFFFu, pd.sbase), sq_dec(sq >> 16, pd.sbase),
                 pack_cli((int)(int8_t)(pc >> 16), (int)(int8_t)(pc >> 24))};
+        const uint32_t mi = (pc >> 8) & 0xFFu;
+        o = pd.uM[mi];   // (slot 0 holds 0: an unconditional load, see pg_load)
     } else {
         pg = pd.upage[e];
         a = pd.uA[e];
+        o = pd.uO[e];
     }
-    o = pd.uO[e];
 }
-TD void tab_put(PagedDoc<T> &pd, int e, int pg, const v4i &a, u64 o) {
+// mi: the entry's mask slot (tab_midx; packed tables only)
+TD void tab_put(PagedDoc<T> &pd, int e, int pg, const v4i &a, u64 o, int mi = 0) {
     if constexpr (T::kPacked) {
         pd.uL[e] = (uint32_t)a.x;
         pd.uS[e] = sq_enc(a.y, pd.sbase) | (sq_enc(a.z, pd.sbase) << 16);
-        pd.uP[e] = (uint32_t)(pg & 0xFFFF) | ((uint32_t)(seg_cli(a) & 0xFF) << 16) | ((uint32_t)(seg_rcli(a) & 0xFF) << 24);
+        pd.uP[e] = (uint32_t)(pg & 0xFF) | ((uint32_t)mi << 8) | ((uint32_t)(seg_cli(a) & 0xFF) << 16) |
+                   ((uint32_t)(seg_rcli(a) & 0xFF) << 24);
+        if (mi) pd.uM[mi] = o;
     } else {
         pd.upage[e] = (uint16_t)pg;
         pd.uA[e] = a;
+        pd.uO[e] = (typename T::O_v)o;
     }
-    pd.uO[e] = (typename T::O_v)o;
+}
+// Packed tables move an entry as it is (its mask slot goes with it).
+TD v4i tab_raw(PagedDoc<T> &pd, int e) { return v4i{(int)pd.uL[e], (int)pd.uS[e], (int)pd.uP[e], 0}; }
+TD void tab_raw_put(PagedDoc<T> &pd, int e, const v4i &r) {
+    pd.uL[e] = (uint32_t)r.x;
+    pd.uS[e] = (uint32_t)r.y;
+    pd.uP[e] = (uint32_t)r.z;
+}
+// Mask slots of a packed table: lanes with `need` get distinct free slots (1..255), marked used
+// in the bitmap; a slot dropped with its entry stays marked until a collection (tab_mgc) when
+// too few are free.  -1 (every lane): not enough slots even after one.  Wave-uniform call.
+TD void tab_mgc(PagedDoc<T> &pd) {
+    if (lane() < MT_PK_MASKS / 32) pd.mbm[lane()] = lane() == 0 ? 1u : 0u;   // (slot 0: no mask)
+    wsync<T>();
+    for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
+        const uint32_t mi = (pd.uP[e] >> 8) & 0xFFu;
+        if (mi) atomicOr((uint32_t *)&pd.mbm[mi >> 5], 1u << (mi & 31));
+    }
+    wsync<T>();
+}
+TD int tab_mfree(PagedDoc<T> &pd) {
+    const int f = lane() < MT_PK_MASKS / 32 ? __popc(~pd.mbm[lane()]) : 0;
+    return wave_sum(f);
+}
+TD int tab_midx(PagedDoc<T> &pd, bool need) {
+    if constexpr (!T::kPacked) {
+        return 0;
+    } else {
+        const u64 m = ballot(need);
+        if (!m) return 0;
+        const int k = __popcll(m);
+        if (tab_mfree(pd) < k) {
+            tab_mgc(pd);
+            if (tab_mfree(pd) < k) return -1;
+        }
+        int mi = 0;
+        if (need) {
+            int r = __popcll(m & ((1ull << lane()) - 1ull));
+            for (int wd = 0; wd < MT_PK_MASKS / 32; wd++) {
+                uint32_t f = ~pd.mbm[wd];
+                const int c = __popc(f);
+                if (r < c) {
+                    for (; r > 0; r--) f &= f - 1;
+                    mi = wd * 32 + __ffs(f) - 1;
+                    break;
+                }
+                r -= c;
+            }
+        }
+        wsync<T>();
+        if (need) atomicOr((uint32_t *)&pd.mbm[mi >> 5], 1u << (mi & 31));
+        wsync<T>();
+        return mi;
+    }
 }
 
 // Removes the table entries of page pg (and every settled entry), then appends the
@@ -465,12 +532,21 @@ TD void pg_table_purge(PagedDoc<T> &pd, int pg) {
         int p = -1;
         v4i a = v4i{0, 0, MT_RSEQ_NONE, 0};
         u64 o = 0;
-        if (v) tab_get(pd, e, p, a, o);
+        v4i raw = v4i{0, 0, 0, 0};
+        if (v) {
+            tab_get(pd, e, p, a, o);
+            if constexpr (T::kPacked) raw = tab_raw(pd, e);
+        }
         const bool keep = v && p != pg && unsettled<T>(a, ms);
         const u64 km = ballot(keep);
         const int at = dst + __popcll(km & ((1ull << lane()) - 1ull));
         wsync<T>();
-        if (keep) tab_put(pd, at, p, a, o);
+        if (keep) {
+            if constexpr (T::kPacked)
+                tab_raw_put(pd, at, raw);
+            else
+                tab_put(pd, at, p, a, o);
+        }
         wsync<T>();
         dst += __popcll(km);
     }
@@ -489,8 +565,13 @@ TD void pg_table_add(PagedDoc<T> &pd, int lo, int hi, int pg2) {
         pg_fail_cap(w, 8);
         return;
     }
+    const int mi = tab_midx(pd, add && o != 0);
+    if (mi < 0) {
+        pg_fail_cap(w, 8);
+        return;
+    }
     const int at = pd.ut_n + __popcll(m & ((1ull << lane()) - 1ull));
-    if (add) tab_put(pd, at, pg2, a, o);
+    if (add) tab_put(pd, at, pg2, a, o, mi);
     pd.ut_n += __popcll(m);
     wsync<T>();
 }
@@ -943,7 +1024,12 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
             pg_fail_cap(w, 8);
             return;
         }
-        if (add) tab_put(pd, pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull)), npg, a, o);
+        const int mi = tab_midx(pd, add && o != 0);
+        if (mi < 0) {
+            pg_fail_cap(w, 8);
+            return;
+        }
+        if (add) tab_put(pd, pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull)), npg, a, o, mi);
         pd.ut_n += __popcll(am);
         const int obs = wave_sum(ol);
         // meta of the new page: blocks blo..bhi of the concatenation
@@ -1270,8 +1356,7 @@ TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     const int ut_b = op.kind == MT_OP_INSERT ? 3 : (range ? 2 + span : (op.kind == MT_OP_LOAD_REMOVED ? 1 : 0));
     const int hp_b = op.kind == MT_OP_INSERT ? 1 : (range ? 1 + span : 0);
     // a narrow tier holds overlap slots 1..32 only
-    // (and a 64-bit tight tier, whose documents keep no overflow sets, at slots 1..63)
-    if ((T::kOvlBits < 64 || !T::kMayGrow) && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
+    if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
     if (T::kPacked && op.seq - pd.sbase > 65000) return false;   // the packed table's seq offsets
     if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
     if (pd.w.heap_n + hp_b > pd.PH) return false;
@@ -1320,9 +1405,6 @@ TD void pg_apply_op_impl(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t 
     DocT<T> &w = pd.w;
     const mt_op_rec &op = in.op;
     w.ocs = oslot_of(w, op_cli(op));
-    if constexpr (T::kMayGrow) {   // no unsettled segment holds an overflow set: start over
-        if (pd.ovf_top > MT_OVF_HDR && pd.ovf_last <= w.min_seq) pd.ovf_top = MT_OVF_HDR;
-    }
     // a message creates <= 3 ids (load_removed finds the id its insert just created)
     if (w.next_uid + 4 > pd.UM && op.kind != MT_OP_LOAD_REMOVED) {
         pg_renumber(pd);
@@ -1457,6 +1539,7 @@ TD void paged_text_compact(DocT<T> &w) {
 TD bool paged_text_ensure(DocT<T> &w, int need) {
     paged_text_compact(w);
     if (w.status) return false;
+    if (8 * (w.text_top + need) > 7 * w.T_cap) pdoc(w).press = 4;
     if (w.text_top + need <= w.T_cap) return true;
     pg_fail_cap(w, 4);
     return false;
@@ -1505,6 +1588,7 @@ TD void paged_props_compact(DocT<T> &w) {
 TD bool paged_props_ensure(DocT<T> &w, int need) {
     paged_props_compact(w);
     if (w.status) return false;
+    if (8 * (w.props_top + need) > 7 * w.P_cap) pdoc(w).press = 5;
     if (w.props_top + need <= w.P_cap) return true;
     pg_fail_cap(w, 5);
     return false;
@@ -1514,9 +1598,8 @@ TD bool paged_props_ensure(DocT<T> &w, int need) {
 // removedClientOverlap beyond the 63 slots (MT/mergeTree.ts:2577-2585, read at :1717): a
 // segment's mask MT_OVF_BIT | off points at [n, client...] in the document's overflow arena.
 // Sets are written once; a segment that gains a client gets a new set (copy + the client), so
-// the halves of a split share theirs.  The arena starts over once minSeq passes the last
-// message that made a set (pg_arena_room) -- every segment holding one is then settled and no
-// view consults it (vlen reads a set only for a removal the view has not seen).
+// the halves of a split share theirs.  vlen reads a set only for a removal the view has not
+// seen; the sets of settled segments stay for their rows (mt_get_segments: n_overlap).
 TD bool ovf_member(DocT<T> &d, u64 o, int c) {
     PagedDoc<T> &pd = pdoc(d);
     const GLB_AS uint16_t *s = pd.govf + (uint32_t)o;
@@ -1563,8 +1646,9 @@ TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
 
 // Can this message's text / property records be placed without running out of the arenas?
 // (TextSegment.append and property sets are unbounded in the reference, MT/textSegment.ts:74-85.)
-// A tight launch hands the document on when the arena's free tail is short (the next tier
-// compacts it); a growing launch compacts here, between messages, and hands the document to the
+// A tight launch compacts inside messages, as every tier does, and hands the document on when a
+// compaction left an arena nearly full (press); a growing launch compacts here, between
+// messages, and hands the document to the
 // growth step (cause 4 text / 5 records / 9 uid map / 11 overflow overlap sets, kept in
 // HDR_DIAG with status 0) when the live text / records / segments / sets then fill more than
 // half of it -- so a message never fails half applied.  The
@@ -1576,19 +1660,23 @@ TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc)
     const int np = MT_WAVE + 1;
     const bool t_ok = w.text_top + nt <= w.T_cap, p_ok = w.props_top + np <= w.P_cap;
     const bool u_ok = w.next_uid + 4 <= pd.UM || op.kind == MT_OP_LOAD_REMOVED;
-    if constexpr (T::kMayGrow) {
+    if constexpr (T::kOvf) {
         if (pd.govf) {   // the overflow overlap arena (cause 11; a tight launch hands the document on)
-            // no unsettled segment holds a set made at or below minSeq: the arena starts over
-            if (pd.ovf_top > MT_OVF_HDR && pd.ovf_last <= w.min_seq) pd.ovf_top = MT_OVF_HDR;
+            // (sets are never reclaimed: a removed segment that zamboni has not unlinked yet
+            // keeps its list, which the segment rows report; the growth step raises the arena)
             if (2 * pd.ovf_top > pd.OA) {
                 w.cap_cause = 11;
                 return false;
             }
         }
     }
+    // a tight launch compacts inside the message (text_ensure) and hands the document on once
+    // a compaction leaves an arena nearly full (press); the uid map is renumbered at the next
+    // tier's message start
+    if (pc.tight) return u_ok && !pd.press;
     if (t_ok && p_ok && u_ok) return true;
     if constexpr (T::kMayGrow) {
-        if (!pc.tight) {
+        {
             if (!u_ok) {   // (the renumbering pg_apply_op would do, done here; cause 9)
                 pg_renumber(pd, true);
                 if (w.status) return true;
@@ -1761,6 +1849,10 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
         pd.uS = pd.uL + pc.UT;
         pd.uP = pd.uS + pc.UT;
         pd.sbase = h.cur_seq - 32000;
+        pd.uM = (LDS_AS u64 *)(smem + L.offUO);
+        pd.mbm = (LDS_AS uint32_t *)(smem + L.offUO + 8u * MT_PK_MASKS);
+        if (lane() < MT_PK_MASKS / 32) pd.mbm[lane()] = lane() == 0 ? 1u : 0u;
+        if (lane() == 0) pd.uM[0] = 0;
     }
     pd.cur = -1;
     pd.cur_pos = -1;
@@ -1771,9 +1863,10 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.opbound = 0;
     pd.zuid = 0;
     pd.zpv = 0;
+    pd.press = 0;
     pd.ovf_top = MT_OVF_HDR;
     pd.ovf_last = 0;
-    if constexpr (T::kMayGrow) {
+    if constexpr (T::kOvf) {
         if (pd.govf) {
             const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
             pd.ovf_top = max((int)hw[0], MT_OVF_HDR);
@@ -1813,7 +1906,7 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     const int np = h.n_blk[1];
     if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
     if (T::kOvlBits < 64 && w.wide) return false;
-    if constexpr (!T::kMayGrow) {   // overflow overlap sets still consulted: the last tier's
+    if constexpr (!T::kOvf) {   // overflow overlap sets still consulted: a 64-bit tier's
         if (pd.govf) {
             const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
             if ((int)hw[0] > MT_OVF_HDR && (int)hw[1] > w.min_seq) return false;
@@ -1837,11 +1930,18 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = g.gheap[i];
     pd.ut_n = h.pad[HDR_UTN];
-    for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
-        const int p = g.gupage[e];
-        const v4i a = g.guA[e];
-        const u64 o = g.guO[e];
-        tab_put(pd, e, p, a, o);
+    for (int base = 0; base < pd.ut_n; base += MT_WAVE) {   // (uniform: tab_midx is collective)
+        const int e = base + lane();
+        const bool v = e < pd.ut_n;
+        // unconditional loads (a 64-bit load under a per-lane select miscompiles: DESIGN.md
+        // section 10); entry 0 exists whenever the loop runs
+        const int ec = v ? e : 0;
+        const int p = g.gupage[ec];
+        const v4i a = g.guA[ec];
+        const u64 o = g.guO[ec];
+        const int mi = tab_midx(pd, v && o != 0);
+        if (mi < 0) return false;   // (more masked entries than the packed table keeps)
+        if (v) tab_put(pd, e, p, a, o, mi);
     }
     wsync<T>();
     pg_mark_free(pd);
@@ -1859,7 +1959,7 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
     pg_win_flush(pd);
     if (failed) w.status = failed;
     w.oslot[2 * lane()] = w.ocli;
-    if constexpr (T::kMayGrow) {
+    if constexpr (T::kOvf) {
         if (pd.govf && lane() < 2) ((GLB_AS uint32_t *)pd.govf)[lane()] = (uint32_t)(lane() ? pd.ovf_last : pd.ovf_top);
     }
     wsync<T>();

@@ -1257,7 +1257,7 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
                 res_k = 1;
             }
             PagedCaps pcx = *pc;   // a wide tight tier packs its table when every client id fits 8 bits
-            pcx.packed = pc->tight && !pc->narrow && h->max_cli <= 127 ? 1 : 0;
+            pcx.packed = pc->tight && !pc->narrow && h->max_cli <= 127 && pc->PP <= 255 ? 1 : 0;   // (8-bit pages)
             for (const PagedSlice &sl : sls) {
                 const int rc = launch_paged(h, b, pcx, res_k, sl, false);
                 if (rc) return rc;
@@ -2389,7 +2389,11 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
         r[2] = (int)(short)(a.w & 0xFFFF);
         r[3] = lrem ? -1 : a.z;
         r[4] = a.z == MT_RSEQ_NONE ? MT_RSEQ_NONE : (int)(short)((uint32_t)a.w >> 16);
-        r[5] = __builtin_popcountll(hd.O[i]);
+        {   // removedClientOverlap's length: the slot bits, or an overflow set's count
+            const u64 o = hd.O[i];
+            const size_t off = (uint32_t)o;
+            r[5] = !(o & MT_OVF_BIT) ? __builtin_popcountll(o) : (off < hd.ovf.size() ? (int)hd.ovf[off] : -1);
+        }
         r[6] = (b.z & MT_MARKER_BIT) ? (int32_t)b.x : -1;
         r[7] = b.y ? 1 : 0;
     }
