@@ -690,12 +690,13 @@ def main():
     alg_bytes = n_ops * (OP_BYTES + RESULT_BYTES) + 2 * payload_chars + final_bytes
     k_ms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (k_ms / 1000.0)
-    traffic = None
+    traffic = traffic_raw = None
     if os.path.exists(PROFILE_PMC):
         try:
             pm = json.load(open(PROFILE_PMC)).get(args.config, {})
             if pm.get("docs") == docs and pm.get("ops") == cfg["ops"] and pm.get("seed_base", 0) == doc_base:
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_raw = pm.get("hbm_bytes_per_launch_raw")
         except Exception:
             traffic = None
 
@@ -759,6 +760,11 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
+            "traffic_raw": traffic_raw,
+            "traffic_correction": ("2 x FETCH_SIZE + WRITE_SIZE: on gfx950 FETCH_SIZE counts 64 B per 128-byte read "
+                                   "request; measured 1/2 on this kernel's page-window, uid-map and text read "
+                                   "patterns (profiles/r4/fetch_calibration.json) and cross-checked by the L2 "
+                                   "request counts (profiles/pmc_summary.json)") if traffic is not None else None,
             "kernel": ("k_replay<TierLdsT<false>> (first ops) + k_replay_paged<TierPagedT<false>> (rest)"
                        if "page_capacity" in caps else
                        "k_replay<TierLdsT<false>> + k_replay<TierGlbT<false>> (HBM-tier hand-over)"),

@@ -39,16 +39,30 @@ def main():
     per_op = {k: v / ops for k, v in counters.items() if k.startswith("SQ_INSTS") or k.startswith("SQ_WAIT")
               or k in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT",
                        "SQ_LDS_IDX_ACTIVE", "SQ_ACTIVE_INST_VALU")}
-    hbm = None
+    hbm = raw = req = None
     if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+        # FETCH_SIZE doubled: on gfx950 it tallies TCC_EA0_RDREQ x 64 B while the requests are
+        # 128 B (MI355X_MICROARCH.md 'HBM'); profiles/tools/fetch_probe.hip measured the same 1/2
+        # on this kernel's own page-window read pattern (profiles/r4/fetch_calibration.json)
         hbm = 2 * counters["FETCH_SIZE"] * 1024 + counters["WRITE_SIZE"] * 1024
+        raw = counters["FETCH_SIZE"] * 1024 + counters["WRITE_SIZE"] * 1024
+    if "TCC_EA0_RDREQ_sum" in counters:
+        # cross-check from the request counts: 128 B per read request (32 B ones counted apart),
+        # 64 B per 64-byte write request, 32 B per other write request
+        rd = counters["TCC_EA0_RDREQ_sum"]
+        rd32 = counters.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+        wr = counters.get("TCC_EA0_WRREQ_sum", 0.0)
+        wr64 = counters.get("TCC_EA0_WRREQ_64B_sum", 0.0)
+        req = (rd - rd32) * 128 + rd32 * 32 + wr64 * 64 + (wr - wr64) * 32
     out = dict(bench=bench, kernels=stats, replay_counters_per_step=counters, replay_per_op=per_op,
-               hbm_bytes_per_step=hbm,
+               hbm_bytes_per_step=hbm, hbm_bytes_per_step_raw=raw, hbm_bytes_per_step_from_requests=req,
                note="counters of every k_replay* dispatch summed per step (LDS-tier launch + hand-over launch);"
-                    " FETCH_SIZE doubled per the gfx950 correction; KB = 1024 B")
+                    " hbm_bytes_per_step = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction, measured on the"
+                    " kernel's read pattern: profiles/r4/fetch_calibration.json); _raw = FETCH_SIZE + WRITE_SIZE;"
+                    " _from_requests = TCC_EA0 read / write request counts x their sizes; KB = 1024 B")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
-    print(json.dumps(dict(kernels=stats, per_op=per_op, hbm=hbm), indent=1))
+    print(json.dumps(dict(kernels=stats, per_op=per_op, hbm=hbm, hbm_raw=raw, hbm_req=req), indent=1))
 
 
 if __name__ == "__main__":
