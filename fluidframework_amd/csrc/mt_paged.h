@@ -848,17 +848,45 @@ TD int pg_find(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart) {
 TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart) {
     const int np = nbr(pd.up, 1);
     int carry = 0, ocarry = 0;
-    for (int base = 0; base < np; base += MT_WAVE) {
+    int b0 = 0, b1 = np;
+    if constexpr (T::kPP == 0 || T::kPP > 4 * MT_WAVE) {
+        if (np > 4 * MT_WAVE) {
+            // a long directory: each lane first sums a contiguous run of ceil(np / 64) pages
+            // (plain adds), one pair of wave scans picks the run holding p, and only that run
+            // is scanned page by page below -- O(np / 64) adds instead of O(np / 64) scans
+            const int chunk = (np + MT_WAVE - 1) / MT_WAVE;
+            const int lo = min(lane() * chunk, np), hi = min(lo + chunk, np);
+            int v = 0, ov = 0;
+            for (int q = lo; q < hi; q++) {
+                const int pg = pd.up.dir[q];
+                v += pd.pvl[pg];
+                ov += pd.meta[pg].obs;
+            }
+            const int inc = wave_scan_incl(v), oinc = wave_scan_incl(ov);
+            const u64 m = ballot(hi > lo && (strict ? inc > p : inc >= p));
+            if (!m) {
+                start = bcast(inc, MT_WAVE - 1);
+                ostart = bcast(oinc, MT_WAVE - 1);
+                return -1;
+            }
+            const int fl = first_lane(m);
+            carry = bcast(inc - v, fl);
+            ocarry = bcast(oinc - ov, fl);
+            b0 = bcast(lo, fl);
+            b1 = bcast(hi, fl);
+        }
+    }
+    for (int base = b0; base < b1; base += MT_WAVE) {
         const int q = base + lane();
         int v = 0, ov = 0;
-        if (q < np) {
+        if (q < b1) {
             const int pg = pd.up.dir[q];
             v = pd.pvl[pg];
             ov = pd.meta[pg].obs;
         }
         const int inc = wave_scan_incl(v);
         const int end = carry + inc;
-        const u64 m = ballot(q < np && (strict ? end > p : end >= p));
+        const u64 m = ballot(q < b1 && (strict ? end > p : end >= p));
         const int oinc = wave_scan_incl(ov);
         if (m) {
             const int fl = first_lane(m);
@@ -1649,9 +1677,11 @@ TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
 // A tight launch compacts inside messages, as every tier does, and hands the document on when a
 // compaction left an arena nearly full (press); a growing launch compacts here, between
 // messages, and hands the document to the
-// growth step (cause 4 text / 5 records / 9 uid map / 11 overflow overlap sets, kept in
-// HDR_DIAG with status 0) when the live text / records / segments / sets then fill more than
-// half of it -- so a message never fails half applied.  The
+// growth step (cause 4 text / 5 records / 9 uid map, kept in HDR_DIAG with status 0) when the
+// live text / records / segments then leave less than 1/8 of it free (and at least 4096 text
+// units / 128 records / 64 ids, for a message's merges; 11: the overflow overlap
+// sets, never reclaimed, half of it) -- so a message never fails half applied, and a document
+// whose live data fits is compacted, not moved.  The
 // bound covers an insert's own text and one range step's records (props_ensure(d, MT_WAVE));
 // a zamboni merge's copy is served by the half kept free.
 TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc) {
@@ -1680,7 +1710,7 @@ TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc)
             if (!u_ok) {   // (the renumbering pg_apply_op would do, done here; cause 9)
                 pg_renumber(pd, true);
                 if (w.status) return true;
-                if (2 * (w.next_uid + 8) > pd.UM) {
+                if (w.next_uid + 8 > pd.UM - max(pd.UM / 8, 64)) {
                     w.cap_cause = 9;
                     return false;
                 }
@@ -1688,7 +1718,7 @@ TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc)
             if (!t_ok) {
                 paged_text_compact(w);
                 if (w.status) return true;   // (failed: the loop stops)
-                if (2 * (w.text_top + nt) > w.T_cap) {
+                if (w.text_top + nt > w.T_cap - max(w.T_cap / 8, 4096)) {   // (slack: merges' copies)
                     w.cap_cause = 4;
                     return false;
                 }
@@ -1696,7 +1726,7 @@ TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc)
             if (!p_ok) {
                 paged_props_compact(w);
                 if (w.status) return true;
-                if (2 * (w.props_top + np) > w.P_cap) {
+                if (w.props_top + np > w.P_cap - max(w.P_cap / 8, 2 * MT_WAVE)) {
                     w.cap_cause = 5;
                     return false;
                 }
