@@ -29,7 +29,11 @@ def class_caps(bench, cfg, max_ops):
     uid = 1 << 15
     while uid < 4 * max_ops:
         uid *= 2
-    caps.update(page_capacity=max(192, int(max_ops * 0.0183 * 1.12) + 16), text_capacity=text,
+    # pages: the measured peaks are 0.0154-0.0161 per message above 10k (c3skew: 3080 at 200k,
+    # 1496 at 100k, 629 at 40k, 323 at 20k); 200k -> 3200 pages keeps a document at 78 KB of LDS,
+    # 2 per CU (a document that still outgrows it moves to the growth step's region by itself)
+    pages = max(192, int(max_ops * 0.0155) + 100)
+    caps.update(page_capacity=pages, text_capacity=text,
                 props_capacity=int(0.3 * max_ops) + 512, uid_capacity=min(uid, 1 << 20))
     if max_ops > 10000:
         for k in ("lds_page_capacity", "lds_unsettled_capacity", "lds_page_heap_capacity", "lds_narrow_overlap"):
