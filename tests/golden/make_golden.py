@@ -219,6 +219,8 @@ EVENTS_FROM = RICH_FROM + [("ref_c4", 1), ("ref_wide", 1), ("ref_ext_long", 1)]
 # The configs' full-length streams (C3 / C4 at 10k messages, paged-size documents: thousands of
 # live segments, page splits and repacks) for the paged layout's ordinals.
 EVENTS_FULL_FROM = [("ref_c3_full", 1), ("ref_c4_full", 1)]
+# more clients overlapping at once than the 63 overlap slots: the paged layout's overflow sets
+EVENTS_WIDE_FROM = [("ref_wide400", 2)]
 
 
 def make_events_fixture(name="ref_events", sources=EVENTS_FROM):
@@ -243,10 +245,10 @@ def make_events_fixture(name="ref_events", sources=EVENTS_FROM):
 # Read-outs of the final replicas (harness "readouts"): MergeTree.getLength(refSeq, clientId),
 # getContainingSegment(pos, refSeq, clientId) and getPosition in the observer's and the
 # writers' views, on the events fixture's streams.
-def make_readouts_fixture():
+def make_readouts_fixture(out_name="ref_readouts", sources=EVENTS_FROM):
     out = []
     with tempfile.TemporaryDirectory() as td:
-        for name, n in EVENTS_FROM:
+        for name, n in sources:
             with gzip.open(os.path.join(HERE, name + ".json.gz"), "rt") as fh:
                 fx = json.load(fh)
             docs = [dict(doc=f"{name}/{d['doc']}", seed_text=d["seed_text"], msgs=d["msgs"]) for d in fx["docs"][:n]]
@@ -257,8 +259,8 @@ def make_readouts_fixture():
                 d.update(r)
                 d["source"] = name
                 out.append(d)
-    _dump("ref_readouts", dict(config={"ext": True, "sources": EVENTS_FROM}, docs=out))
-    print("ref_readouts", len(out), "docs", sum(len(d["containing"]) for d in out), "queries")
+    _dump(out_name, dict(config={"ext": True, "sources": sources}, docs=out))
+    print(out_name, len(out), "docs", sum(len(d["containing"]) for d in out), "queries")
 
 
 # Live-client path (harness "live"): a participant client's own unsequenced
@@ -319,7 +321,13 @@ def main():
     if "--events" in sys.argv[1:]:
         make_events_fixture()
         make_events_fixture("ref_events_full", EVENTS_FULL_FROM)
+        make_events_fixture("ref_events_wide", EVENTS_WIDE_FROM)
         make_readouts_fixture()
+        make_readouts_fixture("ref_readouts_wide", EVENTS_WIDE_FROM)
+        return
+    if "--wide" in sys.argv[1:]:   # (only the overflow-set fixtures)
+        make_events_fixture("ref_events_wide", EVENTS_WIDE_FROM)
+        make_readouts_fixture("ref_readouts_wide", EVENTS_WIDE_FROM)
         return
     only = None
     if "--only" in sys.argv[1:]:
@@ -351,7 +359,9 @@ def main():
     make_rich_fixture()
     make_events_fixture()
     make_events_fixture("ref_events_full", EVENTS_FULL_FROM)
+    make_events_fixture("ref_events_wide", EVENTS_WIDE_FROM)
     make_readouts_fixture()
+    make_readouts_fixture("ref_readouts_wide", EVENTS_WIDE_FROM)
     make_live_fixtures()
 
 
