@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="0 = all docs of rank 0")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
+    ap.add_argument("--seg-cap", type=int, default=0, help="flat HBM segments per document (0 = default; sweeps)")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
     ap.add_argument("--shard", type=int, default=-1,
                     help="replay shard r of the 8-way split of the config's job on this one GPU")
@@ -602,6 +603,8 @@ def main():
     caps = capacities(cfg)
     if args.lds_cap:
         caps["lds_seg_capacity"] = args.lds_cap
+    if args.seg_cap:
+        caps["seg_capacity"] = args.seg_cap
     if args.heap_cap:
         caps["heap_capacity"] = args.heap_cap
     if args.page_caps:
