@@ -41,7 +41,8 @@ class MergeTreeBatch:
                  text_capacity=0, props_capacity=0, delta_log_capacity=0, lds_seg_capacity=0,
                  page_capacity=0, page_heap_capacity=0, unsettled_capacity=0, uid_capacity=0,
                  lds_page_capacity=0, lds_unsettled_capacity=0, lds_page_heap_capacity=0, lds_narrow_overlap=0,
-                 delta_log_mode=0, live_client=0, live_group_capacity=0, paged_slices=0, segment_ordinals=0):
+                 delta_log_mode=0, live_client=0, live_group_capacity=0, paged_slices=0, segment_ordinals=0,
+                 overlap_arena_capacity=0):
         self.lib = _native.load()
         opt = _native.MtOptions(device, seg_capacity, block_capacity, heap_capacity,
                                 text_capacity, props_capacity, delta_log_capacity,
@@ -49,7 +50,7 @@ class MergeTreeBatch:
                                 unsettled_capacity, uid_capacity, lds_page_capacity,
                                 lds_unsettled_capacity, lds_page_heap_capacity, lds_narrow_overlap,
                                 delta_log_mode, live_client, live_group_capacity, paged_slices,
-                                segment_ordinals)
+                                segment_ordinals, overlap_arena_capacity)
         self.h = self.lib.mt_create(n_docs, ctypes.byref(opt))
         if not self.h:
             raise RuntimeError("mt_create failed (no HIP device visible, or out of device memory)")

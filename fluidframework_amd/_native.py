@@ -27,7 +27,7 @@ class MtOptions(ctypes.Structure):
                 ("lds_page_heap_capacity", ctypes.c_int32), ("lds_narrow_overlap", ctypes.c_int32),
                 ("delta_log_mode", ctypes.c_int32), ("live_client", ctypes.c_int32),
                 ("live_group_capacity", ctypes.c_int32), ("paged_slices", ctypes.c_int32),
-                ("segment_ordinals", ctypes.c_int32)]
+                ("segment_ordinals", ctypes.c_int32), ("overlap_arena_capacity", ctypes.c_int32)]
 
 
 class MtSegInfo(ctypes.Structure):

@@ -934,7 +934,8 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
         alloc((void **)&st.pgUtA, N * (size_t)st.UT * sizeof(int4));
         alloc((void **)&st.pgUtO, N * (size_t)st.UT * sizeof(u64));
         alloc((void **)&st.pgUmap, N * (size_t)st.UM * sizeof(uint16_t));
-        st.OA = MT_OVF_ARENA;
+        st.OA = o.overlap_arena_capacity > 0 ? std::min(std::max(o.overlap_arena_capacity, 64), 1 << 30) & ~7
+                                              : MT_OVF_ARENA;
         alloc((void **)&st.pgOvf, N * (size_t)st.OA * sizeof(uint16_t));
         if (st.pgOvf) hipMemset(st.pgOvf, 0, N * (size_t)st.OA * sizeof(uint16_t));
         if (h->ordinals) {

@@ -106,14 +106,15 @@ napi_value Create(napi_env env, napi_callback_info info) {
                            "propsCapacity", "deltaLogCapacity", "ldsSegCapacity", "pageCapacity",
                            "pageHeapCapacity", "unsettledCapacity", "uidCapacity", "ldsPageCapacity",
                            "ldsUnsettledCapacity", "ldsPageHeapCapacity", "ldsNarrowOverlap", "deltaLogMode",
-                           "liveClient", "liveGroupCapacity", "pagedSlices", "segmentOrdinals"};
+                           "liveClient", "liveGroupCapacity", "pagedSlices", "segmentOrdinals",
+                           "overlapArenaCapacity"};
     int32_t *fields[] = {&o.device, &o.seg_capacity, &o.block_capacity, &o.heap_capacity, &o.text_capacity,
                          &o.props_capacity, &o.delta_log_capacity, &o.lds_seg_capacity, &o.page_capacity,
                          &o.page_heap_capacity, &o.unsettled_capacity, &o.uid_capacity, &o.lds_page_capacity,
                          &o.lds_unsettled_capacity, &o.lds_page_heap_capacity, &o.lds_narrow_overlap,
                          &o.delta_log_mode, &o.live_client, &o.live_group_capacity, &o.paged_slices,
-                         &o.segment_ordinals};
-    for (int i = 0; i < 21; i++) {
+                         &o.segment_ordinals, &o.overlap_arena_capacity};
+    for (int i = 0; i < 22; i++) {
         bool has = false;
         napi_has_named_property(env, argv[1], names[i], &has);
         if (has) {

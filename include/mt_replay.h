@@ -101,10 +101,14 @@ typedef struct mt_options {
        nodeUpdateOrdinals, MT/mergeTree.ts:347-372, 2553-2575) -- the strings
        SortedSegmentSet and SequenceDeltaEvent order and dedup ranges by (Q8).  Each rich log
        entry then also carries the segment's id, its position as Client.getPosition reads it
-       inside the callback, and its ordinal; mt_get_segment_info reads the current ones.  The
-       documents stay in the flat tiers (with page_capacity set, mt_create fails); the
-       replay fast path and the synthetic generator keep no ordinals. */
+       inside the callback, and its ordinal; mt_get_segment_info reads the current ones.  Every
+       tier keeps them, the paged layout included; the replay fast path and the synthetic
+       generator keep none. */
     int32_t segment_ordinals;
+    /* u16 units of a paged document's overflow overlap arena: the removedClientOverlap lists of
+       segments whose overlapping removers outnumber the 63 mask slots (default 8192; the
+       growth step doubles it for a document that fills half of it) */
+    int32_t overlap_arena_capacity;
 } mt_options;
 
 /* Synthetic op-stream generator parameters (DESIGN.md "Synthetic op streams"); the

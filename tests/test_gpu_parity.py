@@ -451,7 +451,13 @@ def test_gpu_start_collaboration_window(tier):
         mt2.start_collaboration(np.full(n, 5, np.int32), np.full(n, 4, np.int32))
 
 
-@pytest.mark.parametrize("tier", ["paged", "tiny_paged", "tight", "narrow", "grow"])
+OVF_TIERS = dict({t: TIERS[t] for t in ("paged", "tiny_paged", "tight", "narrow", "grow")},
+                 # a 64-unit overflow arena: handed to the growth step (cause 11) again and again
+                 grow_arena64=dict(TIERS["grow"], overlap_arena_capacity=64),
+                 tight_arena64=dict(TIERS["tight"], overlap_arena_capacity=64))
+
+
+@pytest.mark.parametrize("tier", list(OVF_TIERS))
 def test_gpu_overlap_beyond_the_slots_matches_reference(tier):
     """More clients whose overlapping removes are unsettled at once than the 63 overlap slots
     (200 writers, lag 400: ~80; removedClientOverlap is an unbounded list, MT/mergeTree.ts:
@@ -461,10 +467,12 @@ def test_gpu_overlap_beyond_the_slots_matches_reference(tier):
     fx = gu.load("ref_wide400")
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
-    mt = _gpu_batch(len(fx["docs"]), **TIERS[tier])
+    mt = _gpu_batch(len(fx["docs"]), **OVF_TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     assert (mt.status() == 0).all(), mt.status()
+    if tier.endswith("arena64"):
+        assert mt.last_grown()["in_big_region"] == len(fx["docs"])
     bad = []
     for i, doc in enumerate(fx["docs"]):
         errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner))
