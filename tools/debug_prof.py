@@ -1,6 +1,6 @@
 """Debug aid (GPU box, MT_PROF build): section time breakdown of one replay step.
     MT_EXTRA_FLAGS=-DMT_PROF MT_OUT=fluidframework_amd/libmtreplay_prof.so python fluidframework_amd/build.py --force
-    MT_LIB_PATH=fluidframework_amd/libmtreplay_prof.so python tools/debug_prof.py c3 10000 12500
+    MT_LIB_PATH=fluidframework_amd/libmtreplay_prof.so python tools/debug_prof.py c3 10000 12500 [skew]
 """
 import json
 import sys
@@ -14,7 +14,11 @@ cfg = json.load(open("bench/configs.json"))[sys.argv[1]]
 cfg = dict(cfg, ops=int(sys.argv[2]))
 docs = int(sys.argv[3])
 import bench  # noqa: E402
-mt = MergeTreeBatch(docs, **bench.capacities(cfg))
+caps = bench.capacities(cfg)
+if len(sys.argv) > 4 and sys.argv[4] == "skew":   # the c3skew class capacities for this length
+    import bench_skew  # noqa: E402
+    caps = bench_skew.class_caps(bench, cfg, cfg["ops"])
+mt = MergeTreeBatch(docs, **caps)
 b = mt.generate(cfg)
 print("generation peaks", mt.last_paged_peaks())
 seed_off, seed = mt.generated_seeds(cfg)
