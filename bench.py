@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
     ap.add_argument("--seg-cap", type=int, default=0, help="flat HBM segments per document (0 = default; sweeps)")
+    ap.add_argument("--skew-classes", default="",
+                    help="c3skew: replay only these size classes (comma-separated bounds; diagnostics)")
+    ap.add_argument("--skew-serial", action="store_true",
+                    help="c3skew: run the size classes one after another instead of concurrently")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")
     ap.add_argument("--shard", type=int, default=-1,
                     help="replay shard r of the 8-way split of the config's job on this one GPU")

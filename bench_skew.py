@@ -50,6 +50,9 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     ids = np.arange(lo, hi, dtype=np.int32)
     lens = lens_all[lo:hi]
     classes = size_classes(lens, cfg["classes"])
+    if args.skew_classes:
+        keep = {int(x) for x in args.skew_classes.split(",")}
+        classes = [(b, i) for b, i in classes if b in keep]
     t_gen = time.time()
     runs = []
     for max_ops, idx in classes:        # longest class first
@@ -69,6 +72,8 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
         for r in runs:
             r["mt"].reset()
             r["batch"].apply_async()
+            if args.skew_serial:
+                r["mt"].sync()
         for r in runs:
             r["mt"].sync()
 
@@ -86,7 +91,7 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
         print(f"c3skew: step {k + 1}: {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     barrier()
     elapsed = time.perf_counter() - t0
-    n_ops = int(lens.sum())
+    n_ops = int(sum(r["ops"] for r in runs))
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
