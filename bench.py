@@ -583,23 +583,40 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from fluidframework_amd import MergeTreeBatch
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
+    runner = dispatch(args)
     if args.config == "live":
-        return run_live(args, rank, world, local_rank, dist)
-    cfg = dict(configs[args.config])
-    if args.config == "c3skew":   # skewed document lengths (bench_skew.py)
+        runner(args, rank, world, local_rank, dist)
+    else:
+        runner(args, dict(configs[args.config]), rank, world, local_rank, dist)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def dispatch(args):
+    """The runner of `--config`: c5 (cold catch-up), live (participant replicas), c3skew
+    (skewed lengths, bench_skew.py) or the uniform replay (c2 / c3 / c4)."""
+    if args.config == "live":
+        return run_live
+    if args.config == "c5":
+        return run_c5
+    if args.config == "c3skew":
         import bench_skew
-        line = bench_skew.run_skew(args, cfg, rank, world, local_rank, dist, sys.modules[__name__])
-        if line is not None:
-            print(json.dumps(line), flush=True)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-        run_c5(args, cfg, rank, world, local_rank, dist)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+        mod = sys.modules[__name__]
+
+        def skew(args, cfg, rank, world, local_rank, dist):
+            line = bench_skew.run_skew(args, cfg, rank, world, local_rank, dist, mod)
+            if line is not None:
+                print(json.dumps(line), flush=True)
+        return skew
+    if args.config in ("c2", "c3", "c4"):
+        return run_replay
+    raise SystemExit(f"bench.py: unknown --config {args.config}")
+
+
+def run_replay(args, cfg, rank, world, local_rank, dist):
+    """Uniform replay (c2 / c3 / c4): the default line, BASELINE configs[2]."""
+    from fluidframework_amd import MergeTreeBatch
     docs, doc_base, docs_total, scaling = shard_plan(args, cfg, world, rank)
     if args.ops:
         cfg["ops"] = args.ops
@@ -682,8 +699,6 @@ def main():
             replay_consistent = False
 
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
         return
 
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -789,8 +804,6 @@ def main():
         "gen_s": round(t_gen, 2),
     }
     print(json.dumps(out))
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ from .wire import CHECKSUM_DTYPE, OP_DTYPE
 HERE = os.path.dirname(os.path.abspath(__file__))
 MT_E_INVALID, MT_E_HIP, MT_E_NOMEM, MT_E_NODEVICE, MT_E_OVERFLOW, MT_E_STALE_VIEW = -1, -2, -3, -4, -5, -6
 # MT_LIB_PATH: an instrumented build of the same sources (e.g. the -DMT_PROF section timers,
-# tools/debug_prof.py); the product library otherwise
+# profiles/tools/sections.py); the product library otherwise
 LIB_PATH = os.environ.get("MT_LIB_PATH") or os.path.join(HERE, "libmtreplay.so")
 
 

@@ -1,6 +1,6 @@
 """LDS bytes per document of a paged launch (mirror of csrc/mt_paged.h paged_layout) and the
 documents per CU they allow (160 KB LDS per CU on gfx950).
-    python tools/paged_lds.py PP UT PH [overlap_bytes]"""
+    python profiles/tools/lds_footprint.py PP UT PH [overlap_bytes]"""
 import sys
 
 MT_PG_SLOTS, MT_LV, META, LDS_CU = 64, 8, 12, 160 * 1024

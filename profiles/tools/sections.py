@@ -1,6 +1,6 @@
 """Debug aid (GPU box, MT_PROF build): section time breakdown of one replay step.
     MT_EXTRA_FLAGS=-DMT_PROF MT_OUT=fluidframework_amd/libmtreplay_prof.so python fluidframework_amd/build.py --force
-    MT_LIB_PATH=fluidframework_amd/libmtreplay_prof.so python tools/debug_prof.py c3 10000 12500 [skew]
+    MT_LIB_PATH=fluidframework_amd/libmtreplay_prof.so python profiles/tools/sections.py c3 10000 12500 [skew]
 """
 import json
 import sys

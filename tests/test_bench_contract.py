@@ -88,3 +88,27 @@ def test_cpu_calibration_recorded():
             assert r > 0 and abs(c["port_ops_per_s"] / c["reference" + sfx + "_ops_per_s"] - r) < 0.01 * r
         # the reference without a callback is at least as fast as with the position-recording one
         assert c["reference_nocb_ops_per_s"] >= 0.95 * c["reference_ops_per_s"]
+
+
+@pytest.mark.parametrize("config,runner", [("c2", "run_replay"), ("c3", "run_replay"), ("c4", "run_replay"),
+                                           ("c5", "run_c5"), ("live", "run_live"), ("c3skew", "run_skew")])
+def test_every_config_reaches_its_runner(bench, monkeypatch, config, runner):
+    """`bench.py --config X` calls X's own runner (round 4 lost the C5 branch behind the
+    c3skew one: `--config c5` replayed C3 streams under a C5 label)."""
+    import bench_skew
+    calls = []
+    for name in ("run_replay", "run_c5", "run_live"):
+        monkeypatch.setattr(bench, name, lambda *a, _n=name, **k: calls.append((_n, a)))
+    monkeypatch.setattr(bench_skew, "run_skew", lambda *a, **k: calls.append(("run_skew", a)))
+    monkeypatch.setattr("sys.argv", ["bench.py", "--config", config])
+    bench.main()
+    assert [c[0] for c in calls] == [runner]
+    if runner in ("run_replay", "run_c5", "run_skew"):
+        cfg = calls[0][1][1]
+        assert cfg == _configs()[config]
+
+
+def test_unknown_config_is_refused(bench, monkeypatch):
+    monkeypatch.setattr("sys.argv", ["bench.py", "--config", "c9"])
+    with pytest.raises(SystemExit):
+        bench.main()
