@@ -191,7 +191,9 @@ def capacities(cfg, tight=True):
             caps.update(lds_page_capacity=192, lds_unsettled_capacity=220, lds_page_heap_capacity=192,
                         lds_narrow_overlap=1 if cfg["writers"] <= 32 else 0)
         return caps
-    return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128)
+    # C2: documents stay in the LDS tier (<= ~100 live segments): a flat-only handle
+    return dict(seg_capacity=512, text_capacity=1 << 15, heap_capacity=1024, props_capacity=512 + 128,
+                page_capacity=-1)
 
 
 def _decode_slice(chunk_list):
@@ -345,7 +347,7 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
     docs = args.docs or cfg["docs"] // 8          # the 1M summaries shard over 8 GPUs
     K, tail = cfg["ops"], cfg["tail"]
     caps = dict(seg_capacity=1024, text_capacity=1 << 14, heap_capacity=1024, props_capacity=1024,
-                lds_seg_capacity=args.lds_cap or 256)
+                lds_seg_capacity=args.lds_cap or 256, page_capacity=-1)
     mt = MergeTreeBatch(docs, device=local_rank, **caps)
     base = rank * docs
     t_prep = time.time()
@@ -631,12 +633,12 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
     if args.page_caps:
         pp, ut, ph = (int(x) for x in args.page_caps.split(","))
         caps.update(lds_page_capacity=pp, lds_unsettled_capacity=ut, lds_page_heap_capacity=ph)
-    if args.paged_slices and "page_capacity" in caps:
+    if args.paged_slices and caps.get("page_capacity", 0) > 0:
         caps["paged_slices"] = args.paged_slices
     t_gen = time.time()
     mt = MergeTreeBatch(docs, device=local_rank, **caps)
     batch = mt.generate(cfg, doc_base)          # untimed: inputs resident in HBM
-    gen_peaks = mt.last_paged_peaks() if "page_capacity" in caps else None
+    gen_peaks = mt.last_paged_peaks() if caps.get("page_capacity", 0) > 0 else None
     gen_sums = mt.checksums()
     t_gen = time.time() - t_gen
     seed_off, seed = mt.generated_seeds(cfg, doc_base)
@@ -678,7 +680,7 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
         total_ops = n_ops
 
     hbm_docs = mt.last_hbm_docs()
-    peaks = mt.last_paged_peaks() if "page_capacity" in caps else None
+    peaks = mt.last_paged_peaks() if caps.get("page_capacity", 0) > 0 else None
     status = mt.status()
     sums = mt.checksums()
     replay_consistent = bool(np.array_equal(sums, gen_sums)) and int((status != 0).sum()) == 0
@@ -788,7 +790,7 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
                                    "patterns (profiles/r4/fetch_calibration.json) and cross-checked by the L2 "
                                    "request counts (profiles/pmc_summary.json)") if traffic is not None else None,
             "kernel": ("k_replay<TierLdsT<false>> (first ops) + k_replay_paged<TierPagedT<false>> (rest)"
-                       if "page_capacity" in caps else
+                       if caps.get("page_capacity", 0) > 0 else
                        "k_replay<TierLdsT<false>> + k_replay<TierGlbT<false>> (HBM-tier hand-over)"),
             "kernel_ms": round(k_ms, 3), "alg_bytes_per_launch": alg_bytes,
             "docs_replayed_from_hbm": hbm_docs,

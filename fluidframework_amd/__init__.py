@@ -11,7 +11,7 @@ import numpy as np
 from . import _native
 from .wire import CHECKSUM_DTYPE, OP_DTYPE, Batch, Interner  # noqa: F401
 
-__all__ = ["MergeTreeBatch", "DeviceBatch", "Batch", "Interner", "DeltaLogOverflow", "StaleViewError"]
+__all__ = ["MergeTreeBatch", "DeviceBatch", "Batch", "Interner", "DeltaLogOverflow"]
 
 
 class DeltaLogOverflow(RuntimeError):
@@ -21,12 +21,6 @@ class DeltaLogOverflow(RuntimeError):
     def __init__(self, msg, records):
         super().__init__(msg)
         self.records = records
-
-
-class StaleViewError(RuntimeError):
-    """A segment read-out in a remote view below the refSeq of the client's latest message
-    (MT_E_STALE_VIEW): the reference answers such a view from partial lengths that need not add
-    up to its segments' lengths (MT/partialLengths.ts:455-486), so the replay backend refuses it."""
 
 
 class MergeTreeBatch:
@@ -70,7 +64,7 @@ class MergeTreeBatch:
     def _check(self, rc, what):
         if rc != 0:
             msg = f"{what} failed ({rc}): {self.lib.mt_last_error(self.h).decode()}"
-            raise (StaleViewError if rc == _native.MT_E_STALE_VIEW else RuntimeError)(msg)
+            raise RuntimeError(msg)
 
     # -------------------------------------------------------------- input
     def load_initial_text(self, seed_off, seed):
@@ -412,18 +406,16 @@ class MergeTreeBatch:
                                                    _native.ptr(text), text_cap), "mt_get_segment_by_uid")
         return self._seg_info(info, text)
 
-    def get_view_lengths(self, docs, ref_seq, client, refuse_stale=True):
-        """MergeTree.getLength(refSeq, clientId) (:1610-1612) for each (doc, refSeq, client).  A
-        view below the client's latest refSeq raises StaleViewError (refuse_stale=False: its
-        length is -1 and the others are returned)."""
+    def get_view_lengths(self, docs, ref_seq, client):
+        """MergeTree.getLength(refSeq, clientId) (:1610-1612) for each (doc, refSeq, client):
+        the root's partial length in a remote view (every refSeq of the collab window,
+        MT/partialLengths.ts:455-486), the local length for client 0."""
         docs = np.ascontiguousarray(docs, dtype=np.uint32)
         ref = np.ascontiguousarray(ref_seq, dtype=np.int32)
         cli = np.ascontiguousarray(client, dtype=np.int32)
         out = np.zeros(len(docs), dtype=np.int32)
-        rc = self.lib.mt_get_view_lengths(self.h, len(docs), _native.ptr(docs), _native.ptr(ref), _native.ptr(cli),
-                                          _native.ptr(out))
-        if not (rc == _native.MT_E_STALE_VIEW and not refuse_stale):
-            self._check(rc, "mt_get_view_lengths")
+        self._check(self.lib.mt_get_view_lengths(self.h, len(docs), _native.ptr(docs), _native.ptr(ref),
+                                                 _native.ptr(cli), _native.ptr(out)), "mt_get_view_lengths")
         return out
 
     def get_prop_runs(self, doc):

@@ -22,6 +22,18 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno
          "-Wno-unused-value", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"] + os.environ.get("MT_EXTRA_FLAGS", "").split()
 
 
+# what the kernel instantiations (mtk_*.o) compile from: not mt_replay.hip's host code
+KERNEL_DEPS = [p for p in DEPS if not p.endswith("mt_replay.hip")]
+
+
+def _fresh(obj, deps):
+    """obj exists and is newer than every dependency (and than this build script's flags)."""
+    if not os.path.exists(obj):
+        return False
+    t = os.path.getmtime(obj)
+    return all(os.path.getmtime(d) <= t for d in deps + [os.path.abspath(__file__)])
+
+
 def needs_build():
     if not os.path.exists(OUT):
         return True
@@ -52,12 +64,19 @@ def build(force=False, verbose=False):
     tag = os.path.splitext(os.path.basename(OUT))[0]   # variant libraries (MT_OUT) build apart
     obj_dir = os.path.join(OBJ_DIR, tag)
     os.makedirs(obj_dir, exist_ok=True)
+    stamp = os.path.join(obj_dir, "flags.txt")   # objects built with other flags are rebuilt
+    if not os.path.exists(stamp) or open(stamp).read() != " ".join(FLAGS):
+        force = True
+        with open(stamp, "w") as fh:
+            fh.write(" ".join(FLAGS))
     # MT_ONLY=P_C3,P_C4: an A/B variant that recompiles only those kernels; the other objects
     # come from the product build (_build/libmtreplay)
     only = [x for x in os.environ.get("MT_ONLY", "").split(",") if x]
     cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
     jobs = [(SRC, os.path.join(obj_dir, "mt_replay.o"))]
     link_only = []
+    if not force and not os.environ.get("MT_ONLY") and _fresh(jobs[0][1], DEPS):
+        link_only.append(jobs.pop()[1])
     for name, expr in variants():
         src = os.path.join(obj_dir, f"mtk_{name}.hip")
         body = (f'#include "{os.path.join(HERE, "csrc", "mt_kernels.h")}"\n'
@@ -66,6 +85,9 @@ def build(force=False, verbose=False):
             with open(src, "w") as fh:
                 fh.write(body)
         obj = os.path.join(obj_dir, f"mtk_{name}.o")
+        if not force and not only and _fresh(obj, [src] + KERNEL_DEPS):   # (mt_replay.hip is host code)
+            link_only.append(obj)
+            continue
         if only and name not in only:
             base_obj = os.path.join(OBJ_DIR, "libmtreplay", f"mtk_{name}.o")
             if os.path.abspath(base_obj) != os.path.abspath(obj):

@@ -1387,6 +1387,16 @@ TD bool pg_room(PagedDoc<T> &pd, const mt_op_rec &op) {
     if (T::kOvlBits < 64 && op.kind == MT_OP_REMOVE && oslot_short(pd.w, op_cli(op))) return false;
     if (T::kPacked && op.seq - pd.sbase > 65000) return false;   // the packed table's seq offsets
     if (pd.ut_n + pd.wgrow + ut_b > pd.UT) return false;
+    if constexpr (T::kPacked) {
+        // the sparse mask table: every entry this message (and the window's rebuild) may add
+        // could carry a mask; a shortage hands the document on here instead of failing a
+        // table add mid-message (a collection runs only when the bound is not met outright)
+        const int need = pd.wgrow + ut_b;
+        if (tab_mfree(pd) < need) {
+            tab_mgc(pd);
+            if (tab_mfree(pd) < need) return false;
+        }
+    }
     if (pd.w.heap_n + hp_b > pd.PH) return false;
     if (nbr(pd.up, 1) + 8 > pd.PP) return false;
     for (int l = 2; l < pd.up.depth; l++)
@@ -1959,10 +1969,13 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = g.gcnt[l * pd.PPh + b];
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = g.gheap[i];
-    pd.ut_n = h.pad[HDR_UTN];
-    for (int base = 0; base < pd.ut_n; base += MT_WAVE) {   // (uniform: tab_midx is collective)
+    // ut_n follows the fill, so that a mask collection inside tab_midx (tab_mgc) scans only
+    // the entries written so far, not stale LDS of an earlier workgroup
+    const int utn = h.pad[HDR_UTN];
+    pd.ut_n = 0;
+    for (int base = 0; base < utn; base += MT_WAVE) {   // (uniform: tab_midx is collective)
         const int e = base + lane();
-        const bool v = e < pd.ut_n;
+        const bool v = e < utn;
         // unconditional loads (a 64-bit load under a per-lane select miscompiles: DESIGN.md
         // section 10); entry 0 exists whenever the loop runs
         const int ec = v ? e : 0;
@@ -1972,6 +1985,7 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         const int mi = tab_midx(pd, v && o != 0);
         if (mi < 0) return false;   // (more masked entries than the packed table keeps)
         if (v) tab_put(pd, e, p, a, o, mi);
+        pd.ut_n = min(base + MT_WAVE, utn);
     }
     wsync<T>();
     pg_mark_free(pd);

@@ -619,11 +619,6 @@ struct mt_handle {
     int max_cli = 0;                        // largest |short client id| any batch / load / generation used
                                             // (<= 127: the tight tier may pack its table, PagedCaps.packed)
     uint32_t grown_last = 0, grow_rounds_last = 0;
-    // remote views a client can still hold (segment read-outs): per document, the largest refSeq
-    // of each short client's applied messages, {client, refSeq} sorted by client; a generated
-    // batch's documents are untracked (their writers' views are refused)
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> lastref;
-    std::vector<uint8_t> untracked;
 };
 struct mt_batch {
     mt_handle *owner = nullptr;   // the handle whose growth step still needs this batch
@@ -634,11 +629,6 @@ struct mt_batch {
     mt_op_rec *ops = nullptr;
     uint16_t *text = nullptr;
     uint32_t *props = nullptr;
-    // per document, the largest refSeq of each client's messages ({client, refSeq} sorted by
-    // client, [lr_off[d], lr_off[d + 1])); generated: the batch came from mt_generate
-    std::vector<int64_t> lr_off;
-    std::vector<std::pair<int32_t, int32_t>> lr;
-    bool generated = false;
     int32_t *order = nullptr;     // dispatch order (DevState.order), null when lengths are equal
 };
 // Longest-first dispatch order of a batch whose documents differ in length (stable: equal
@@ -698,34 +688,6 @@ static void launch_load_convert(const void *k, dim3 g, dim3 b, size_t lds, hipSt
                                 PagedCaps pc, int lo) {
     void *a[] = {&st, &sc, &pc, &lo};
     (void)hipLaunchKernel(k, g, b, a, lds, s);
-}
-
-// folds a batch's latest refSeq per client into the handle's (segment read-outs)
-static void track_views(mt_handle *h, const mt_batch *b) {
-    if (h->lastref.size() != h->n_docs) h->lastref.assign(h->n_docs, {});
-    if (h->untracked.size() != h->n_docs) h->untracked.assign(h->n_docs, 0);
-    if (b->generated) {
-        std::fill(h->untracked.begin(), h->untracked.end(), 1);
-        return;
-    }
-    if (b->lr_off.size() != (size_t)h->n_docs + 1) return;
-    for (uint32_t d = 0; d < h->n_docs; d++) {
-        auto &v = h->lastref[d];
-        for (int64_t i = b->lr_off[d]; i < b->lr_off[d + 1]; i++) {
-            const auto &e = b->lr[i];
-            auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(e.first, INT32_MIN));
-            if (it != v.end() && it->first == e.first)
-                it->second = std::max(it->second, e.second);
-            else
-                v.insert(it, e);
-        }
-    }
-}
-static void untrack_views(mt_handle *h, uint32_t lo, uint32_t n) {
-    if (h->lastref.size() == h->n_docs)
-        for (uint32_t d = lo; d < lo + n; d++) h->lastref[d].clear();
-    if (h->untracked.size() == h->n_docs)
-        for (uint32_t d = lo; d < lo + n; d++) h->untracked[d] = 0;
 }
 
 static int mt_settle(mt_handle *h);
@@ -791,6 +753,18 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return nullptr;
     mt_options o{};
     if (opt) o = *opt;
+    // the default handle is unbounded: the paged layout with the growth step behind it, at
+    // small starting capacities (a flat-only handle is opt-in: page_capacity < 0); live
+    // handles stay flat
+    const bool dflt_paged = o.page_capacity == 0 && o.live_client == 0;
+    if (dflt_paged) {
+        o.page_capacity = 64;
+        if (o.page_heap_capacity <= 0) o.page_heap_capacity = 256;
+        if (o.unsettled_capacity <= 0) o.unsettled_capacity = 256;
+        if (o.uid_capacity <= 0) o.uid_capacity = 8192;
+        if (o.seg_capacity <= 0) o.seg_capacity = 512;
+    }
+    if (o.page_capacity < 0) o.page_capacity = 0;
     auto *h = new mt_handle();
     h->device = o.device;
     h->n_docs = n_docs;
@@ -1067,7 +1041,6 @@ int mt_reset(mt_handle *h) {
         h->n_big = 0;
     }
     if (h->st.DL) HIPCHK(h, hipMemsetAsync(h->st.dlog, 0, (size_t)h->n_docs * h->st.DL * 4, h->stream));
-    untrack_views(h, 0, h->n_docs);
     hipLaunchKernelGGL(k_init, dim3(h->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, h->d_seed_off, h->d_seed);
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -1091,20 +1064,6 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
     for (uint64_t i = 0; i < n_ops; i++) h->max_cli = std::max(h->max_cli, std::abs((int)(int16_t)ops[i].client));
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *b = new mt_batch();
-    // each client's latest refSeq per document (summary-load records are no client's messages)
-    b->lr_off.assign(h->n_docs + 1, 0);
-    {
-        std::vector<std::pair<int32_t, int32_t>> tmp;
-        for (uint32_t d = 0; d < h->n_docs; d++) {
-            tmp.clear();
-            for (int64_t k = doc_op_off[d]; k < doc_op_off[d + 1]; k++)
-                if (!(ops[k].flags & MT_F_LOAD)) tmp.emplace_back((int32_t)(int16_t)ops[k].client, ops[k].ref_seq);
-            std::sort(tmp.begin(), tmp.end());
-            for (size_t i = 0; i < tmp.size(); i++)
-                if (i + 1 == tmp.size() || tmp[i + 1].first != tmp[i].first) b->lr.push_back(tmp[i]);
-            b->lr_off[d + 1] = (int64_t)b->lr.size();
-        }
-    }
     b->device = h->device;
     b->n_docs = h->n_docs;
     b->n_ops = n_ops;
@@ -1186,7 +1145,6 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
         const int rc = mt_settle(h);
         if (rc) return rc;
     }
-    track_views(h, b);
     h->st.order = b->order;   // (its launches and its growth step's)
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipMemsetAsync(h->st.stats, 0, 16 * sizeof(uint32_t), h->stream));
@@ -1866,7 +1824,6 @@ int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
         HIPCHK(h, hipMemsetAsync(h->st.dlog + (size_t)s->doc_lo * h->st.DL, 0, (size_t)s->n_docs * h->st.DL * 4,
                                  h->stream));
     HIPCHK(h, hipEventRecord(h->ev_load, h->stream));
-    untrack_views(h, s->doc_lo, s->n_docs);
     hipLaunchKernelGGL(k_load_header, dim3(s->n_docs), dim3(MT_WAVE), 0, h->stream, h->st, s->off, s->nh, s->segs,
                        s->text, s->props, s->min_seq, s->cur_seq, s->sc, (int)s->doc_lo);
     HIPCHK(h, hipGetLastError());
@@ -2194,6 +2151,9 @@ struct HostDoc {
     std::vector<PageMeta> pmeta;
     int32_t oslot[2 * MT_OSLOTS];   // overlap slots {client, last seq}
     std::vector<uint16_t> ovf;      // paged: the overflow overlap arena (MT_OVF_BIT masks)
+    // the B-tree's child counts by level (lv[0]: segments per leaf block, lv[depth - 1]: the
+    // root's children), in order -- the shape the remote views' partial lengths follow
+    std::vector<std::vector<int>> lv;
 };
 // document doc's paged arrays, host side (the growth step's slot mirror)
 static PagedBase host_paged(const mt_handle *h, uint32_t doc) {
@@ -2245,6 +2205,20 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
             }
             for (int k = 0; k < m.nblk; k++) hd.cnt.push_back((uint8_t)pm_bcnt(m, k));
         }
+        {   // the levels: leaf blocks from the pages, level 1 = the pages in directory order,
+            // levels >= 2 from the upper count arrays
+            const int D = std::max(hd.hdr.depth, 1);
+            hd.lv.assign(D, {});
+            hd.lv[0].assign(hd.cnt.begin(), hd.cnt.end());
+            if (D >= 2)
+                for (int q = 0; q < np; q++) hd.lv[1].push_back(meta[dir[q]].nblk);
+            if (D >= 3) {
+                std::vector<uint8_t> cn((size_t)MT_LV * PP);
+                HIPCHK(h, hipMemcpy(cn.data(), pb.cnt, cn.size(), hipMemcpyDeviceToHost));
+                for (int l = 2; l < D; l++)
+                    for (int b = 0; b < hd.hdr.n_blk[l]; b++) hd.lv[l].push_back(cn[(size_t)l * PP + b]);
+            }
+        }
         hd.pmeta = std::move(meta);
         hd.hdr.n_seg = (int)hd.A.size();
         hd.hdr.n_blk[0] = (int)hd.cnt.size();
@@ -2264,6 +2238,10 @@ static int fetch_doc(mt_handle *h, uint32_t doc, HostDoc &hd, bool with_text, bo
     }
     hd.cnt.resize((size_t)MT_LV * st.B);
     HIPCHK(h, hipMemcpy(hd.cnt.data(), st.cnt + (size_t)doc * MT_LV * st.B, MT_LV * st.B, hipMemcpyDeviceToHost));
+    const int D = std::max(hd.hdr.depth, 1);
+    hd.lv.assign(D, {});
+    for (int l = 0; l < D; l++)
+        for (int b = 0; b < hd.hdr.n_blk[l]; b++) hd.lv[l].push_back(hd.cnt[(size_t)l * st.B + b]);
     }
     const PagedBase ar = host_paged(h, doc);   // (the arenas of the document's region)
     if (with_text) {
@@ -2415,6 +2393,7 @@ struct HostView {
 };
 static int host_view_setup(mt_handle *h, uint32_t doc, const HostDoc &hd, int32_t ref_seq, int32_t client,
                            HostView &v) {
+    (void)doc;
     v.r = ref_seq;
     v.c = client;
     v.cs = 0;
@@ -2424,21 +2403,6 @@ static int host_view_setup(mt_handle *h, uint32_t doc, const HostDoc &hd, int32_
         h->err = "remote view: refSeq outside the collab window [minSeq, currentSeq]";
         return MT_E_INVALID;
     }
-    // a view below the client's latest refSeq: the reference answers from partial lengths
-    // that need not add up to its leaves' lengths (MT/partialLengths.ts:455-486) -- refused
-    if (doc < h->untracked.size() && h->untracked[doc]) {
-        h->err = "remote view: the document replayed a generated batch (its clients' refSeqs are not tracked)";
-        return MT_E_STALE_VIEW;
-    }
-    if (doc < h->lastref.size()) {
-        const auto &v = h->lastref[doc];
-        auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(client, INT32_MIN));
-        if (it != v.end() && it->first == client && ref_seq < it->second) {
-            h->err = "remote view: refSeq " + std::to_string(ref_seq) + " is below client " + std::to_string(client) +
-                     "'s latest refSeq " + std::to_string(it->second) + " (a stale view)";
-            return MT_E_STALE_VIEW;
-        }
-    }
     for (int i = 0; i < MT_OSLOTS; i++)
         if (hd.oslot[2 * i] == client) {
             v.cs = i + 1;
@@ -2446,9 +2410,9 @@ static int host_view_setup(mt_handle *h, uint32_t doc, const HostDoc &hd, int32_
         }
     return 0;
 }
-static int host_view_len(const HostDoc &hd, const HostView &v, int i) {
+// row i in view v: {inserted in the view, removed in the view} (nodeLength's two tests)
+static void host_view_vis(const HostDoc &hd, const HostView &v, int i, bool &ins, bool &gone) {
     const int4 a = hd.A[i];
-    if (v.local) return a.z == MT_RSEQ_NONE ? a.x : 0;
     const int cli = (int)(short)(a.w & 0xFFFF), rcli = (int)(short)((uint32_t)a.w >> 16);
     const u64 o = hd.O[i];
     bool ovl = v.cs >= 1 && ((o >> (v.cs - 1)) & 1ull);
@@ -2458,9 +2422,67 @@ static int host_view_len(const HostDoc &hd, const HostView &v, int i) {
         const size_t n = off < hd.ovf.size() ? hd.ovf[off] : 0;
         for (size_t k = 1; k <= n && off + k < hd.ovf.size(); k++) ovl = ovl || hd.ovf[off + k] == (uint16_t)v.c;
     }
-    const bool ins = cli == v.c || (a.y != -1 && a.y <= v.r);
-    const bool gone = a.z != MT_RSEQ_NONE && (rcli == v.c || ovl || (a.z != -1 && a.z <= v.r));
+    ins = cli == v.c || (a.y != -1 && a.y <= v.r);
+    gone = a.z != MT_RSEQ_NONE && (rcli == v.c || ovl || (a.z != -1 && a.z <= v.r));
+}
+// a leaf's nodeLength in the view
+static int host_view_len(const HostDoc &hd, const HostView &v, int i) {
+    const int4 a = hd.A[i];
+    if (v.local) return a.z == MT_RSEQ_NONE ? a.x : 0;
+    bool ins, gone;
+    host_view_vis(hd, v, i, ins, gone);
     return ins && !gone ? a.x : 0;
+}
+// The leaf's term in its ancestors' PartialSequenceLengths (MT/partialLengths.ts): +len at its
+// insert, -len at its removal, each counted when the view holds it (getBranchPartialLength
+// :455-486 adds every entry at or below refSeq and the client's own later ones, overlap
+// removes included via clientSeqNumbers :581-590).  The two are independent: a view below the
+// client's latest refSeq can see a segment removed (by the client) but not inserted, and then
+// the segment counts -len -- the reference's interior node lengths there differ from the sum
+// of their leaves' nodeLength (oracle/mt_oracle.c seg_partial; pinned on every view of
+// tests/golden/ref_readouts*).  In any other view it equals the leaf's nodeLength.
+static int host_seg_partial(const HostDoc &hd, const HostView &v, int i) {
+    const int4 a = hd.A[i];
+    if (v.local) return a.z == MT_RSEQ_NONE ? a.x : 0;   // blockLength: cachedLength
+    bool ins, gone;
+    host_view_vis(hd, v, i, ins, gone);
+    return a.x * ((int)ins - (int)gone);
+}
+// The tree's node lengths in view v: P[l][b] = node b of level l's length (partial lengths),
+// first[l][b] = its first child (a segment row at level 0, a node of level l - 1 above).
+struct HostTree {
+    std::vector<std::vector<int>> P, first;
+};
+static void host_tree(const HostDoc &hd, const HostView &v, HostTree &t) {
+    const int D = (int)hd.lv.size();
+    t.P.assign(D, {});
+    t.first.assign(D, {});
+    for (int l = 0; l < D; l++) {
+        int f = 0;
+        for (int b = 0; b < (int)hd.lv[l].size(); b++) {
+            t.first[l].push_back(f);
+            int sum = 0;
+            for (int k = f; k < f + hd.lv[l][b]; k++)
+                sum += l == 0 ? (k < hd.hdr.n_seg ? host_seg_partial(hd, v, k) : 0)
+                              : (k < (int)t.P[l - 1].size() ? t.P[l - 1][k] : 0);
+            t.P[l].push_back(sum);
+            f += hd.lv[l][b];
+        }
+    }
+}
+// MergeTree.getPosition(node, refSeq, clientId) (:1619-1636) of row i: the nodeLength of its
+// earlier siblings and of each ancestor's earlier siblings (interior ones: partial lengths)
+static int host_position(const HostDoc &hd, const HostView &v, const HostTree &t, int i) {
+    const int D = (int)hd.lv.size();
+    int x = i, p = 0;
+    for (int l = 0; l < D; l++) {
+        int b = 0;   // x's parent at level l
+        while (b + 1 < (int)t.first[l].size() && t.first[l][b + 1] <= x) b++;
+        for (int k = t.first[l].empty() ? x : t.first[l][b]; k < x; k++)
+            p += l == 0 ? host_view_len(hd, v, k) : t.P[l - 1][k];
+        x = b;
+    }
+    return p;
 }
 // the fields of row i (and, on a segment_ordinals handle, its ordinal from the per-node
 // characters: ancestors below the root, then its own)
@@ -2553,16 +2575,35 @@ int mt_get_containing_segment(mt_handle *h, uint32_t doc, int32_t pos, int32_t r
     if ((rc = host_view_setup(h, doc, hd, ref_seq, client, v))) return rc;
     memset(out, 0, sizeof(*out));
     out->row = -1;
-    int p = 0;
-    for (int i = 0; i < hd.hdr.n_seg; i++) {   // searchBlock's leaf test: pos < len (:1830-1862)
+    if (hd.hdr.n_seg == 0 || hd.lv.empty()) return 0;
+    // searchBlock (:1830-1862): at every level the first child with pos < nodeLength(child),
+    // interior children by their partial lengths; no backtracking (a block whose leaves do not
+    // hold pos yields no segment)
+    HostTree t;
+    host_tree(hd, v, t);
+    const int D = (int)hd.lv.size();
+    int b = 0;
+    for (int l = D - 1; l >= 1; l--) {
+        int hit = -1;
+        for (int k = t.first[l][b]; k < t.first[l][b] + hd.lv[l][b]; k++) {
+            if (pos < t.P[l - 1][k]) {
+                hit = k;
+                break;
+            }
+            pos -= t.P[l - 1][k];
+        }
+        if (hit < 0) return 0;
+        b = hit;
+    }
+    for (int i = t.first[0][b]; i < t.first[0][b] + hd.lv[0][b] && i < hd.hdr.n_seg; i++) {
         const int l = host_view_len(hd, v, i);
-        if (l > 0 && pos >= p && pos < p + l) {
+        if (pos < l) {
             host_seg_info(h, doc, hd, i, out, text, text_cap);
-            out->position = p;
-            out->offset = pos - p;
+            out->position = host_position(hd, v, t, i);
+            out->offset = pos;
             return 0;
         }
-        p += l;
+        pos -= l;
     }
     return 0;
 }
@@ -2577,14 +2618,14 @@ int mt_get_segment_by_uid(mt_handle *h, uint32_t doc, uint32_t uid, int32_t ref_
     if ((rc = host_view_setup(h, doc, hd, ref_seq, client, v))) return rc;
     memset(out, 0, sizeof(*out));
     out->row = -1;
-    int p = 0;
     for (int i = 0; i < hd.hdr.n_seg; i++) {
         if ((hd.B[i].z & ~MT_MARKER_BIT) == uid) {
+            HostTree t;
+            host_tree(hd, v, t);
             host_seg_info(h, doc, hd, i, out, text, text_cap);
-            out->position = p;
+            out->position = host_position(hd, v, t, i);
             return 0;
         }
-        p += host_view_len(hd, v, i);
     }
     return 0;
 }
@@ -2594,8 +2635,6 @@ int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const in
     if (!h || (n && (!docs || !ref_seq || !client || !out))) return MT_E_INVALID;
     HostDoc hd;
     int64_t have = -1;   // the document fetched last (queries of one document fetch it once)
-    int stale = 0;
-    std::string stale_err;
     for (uint32_t q = 0; q < n; q++) {
         int rc;
         if ((int64_t)docs[q] != have) {
@@ -2603,19 +2642,11 @@ int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const in
             have = docs[q];
         }
         HostView v;
-        if ((rc = host_view_setup(h, docs[q], hd, ref_seq[q], client[q], v))) {
-            if (rc != MT_E_STALE_VIEW) return rc;
-            out[q] = -1;   // refused; the others are answered
-            if (!stale++) stale_err = h->err;
-            continue;
-        }
+        if ((rc = host_view_setup(h, docs[q], hd, ref_seq[q], client[q], v))) return rc;
+        // blockLength(root) (:1664-1670): the root's partial length in a remote view
         int len = 0;
-        for (int i = 0; i < hd.hdr.n_seg; i++) len += host_view_len(hd, v, i);
+        for (int i = 0; i < hd.hdr.n_seg; i++) len += host_seg_partial(hd, v, i);
         out[q] = len;
-    }
-    if (stale) {
-        h->err = std::to_string(stale) + " stale view(s) refused (length -1), first: " + stale_err;
-        return MT_E_STALE_VIEW;
     }
     return 0;
 }

@@ -17,6 +17,8 @@ import numpy as np
 def zipf_lengths(n_docs, total_ops, s, cap, seed):
     """int32[n_docs] message counts summing to total_ops: min(c r^-s, cap) for the document of
     rank r (c solved for the total), at least 1 each, ranks assigned by a seeded permutation."""
+    if not n_docs <= total_ops <= n_docs * cap:
+        raise ValueError(f"zipf_lengths: {total_ops} messages do not fit {n_docs} documents of 1..{cap}")
     r = np.arange(1, n_docs + 1, dtype=np.float64)
     lo, hi = 1.0, 1e18
     for _ in range(300):
@@ -26,12 +28,18 @@ def zipf_lengths(n_docs, total_ops, s, cap, seed):
         else:
             hi = m
     lens = np.maximum(np.floor(np.minimum(lo * r ** -s, cap)), 1).astype(np.int64)
-    resid = int(total_ops - lens.sum())
-    free = np.flatnonzero(lens < cap)          # the residual of the rounding, one message each
-    if resid > 0:
-        lens[free[:resid]] += 1
-    elif resid < 0:
-        lens[np.flatnonzero(lens > 1)[resid:]] -= 1
+    # the residual of the rounding, one message per document per pass (several passes when it
+    # exceeds the documents still below the cap / above 1)
+    while True:
+        resid = int(total_ops - lens.sum())
+        if resid > 0:
+            free = np.flatnonzero(lens < cap)
+            lens[free[:resid]] += 1
+        elif resid < 0:
+            lens[np.flatnonzero(lens > 1)[resid:]] -= 1
+        else:
+            break
+    assert lens.sum() == total_ops
     perm = np.random.default_rng(seed).permutation(n_docs)
     out = np.empty(n_docs, dtype=np.int32)
     out[perm] = lens

@@ -32,17 +32,23 @@ extern "C" {
 #define MT_E_NOMEM (-3)      /* device allocation failed */
 #define MT_E_NODEVICE (-4)   /* no HIP device visible: the product has no CPU fallback */
 #define MT_E_OVERFLOW (-5)   /* a document's delta log overflowed (mt_get_delta_log) */
-#define MT_E_STALE_VIEW (-6) /* a remote view below the refSeq of the client's latest message */
+#define MT_E_STALE_VIEW (-6) /* reserved (round 4 refused remote views below a client's latest refSeq;
+                                 they are answered since round 5) */
 
 typedef struct mt_handle mt_handle;
 typedef struct mt_batch mt_batch;
 
-/* Per-document capacities (0 = default).  The paged ones (page / unsettled / page heap) are
-   starting points that the growth step raises per document (mt_last_grown); exceeding any
-   other marks that document MT_DOC_CAPACITY. */
+/* Per-document capacities (0 = default).  By default (page_capacity 0) a handle has the
+   paged layout and no capacity is a limit: the paged ones (page / unsettled / page heap), the
+   text / property arenas, the uid map and the overflow overlap arena are starting points that
+   the growth step raises per document (mt_last_grown), as the reference's documents grow
+   without bound (MT/mergeTree.ts:2577-2585, MT/textSegment.ts:74-85).  page_capacity < 0
+   opts into a flat-only handle, whose capacities are hard (MT_DOC_CAPACITY beyond them). */
 typedef struct mt_options {
     int32_t device;          /* HIP device ordinal (one process per GPU) */
-    int32_t seg_capacity;    /* leaf segments per document          (default 2048) */
+    int32_t seg_capacity;    /* leaf segments per document in the flat tiers (default 2048;
+                                512 on a paged handle, where it only receives what the LDS
+                                tier hands to the paged layout) */
     int32_t block_capacity;  /* blocks per tree level per document  (default seg/2) */
     int32_t heap_capacity;   /* zamboni LRU heap entries            (default 2*seg) */
     int32_t text_capacity;   /* UTF-16 units per document text arena half (default 32768) */
@@ -54,14 +60,18 @@ typedef struct mt_options {
                                    Live handles: staged only for a value > 0 (default: HBM). */
     int32_t page_capacity;      /* paged layout for documents that outgrow the LDS tier:
                                    pages (level-1 B-tree nodes, <= 64 segments each) per
-                                   document; 0 = off (such documents replay from the flat
-                                   HBM tier, O(segments) per op) */
-    int32_t page_heap_capacity; /* zamboni heap entries of a paged document (default 1024) */
+                                   document to start with (default 64; the growth step raises
+                                   it); < 0 = a flat-only handle (such documents replay from
+                                   the flat HBM tier, O(segments) per op, within its hard
+                                   capacities).  Live handles are flat-only. */
+    int32_t page_heap_capacity; /* zamboni heap entries of a paged document (default 1024;
+                                   256 with the default page_capacity) */
     int32_t unsettled_capacity; /* segments of a paged document inserted or removed above
                                    minSeq (default 256) */
     int32_t uid_capacity;       /* entries of a paged document's segment-id -> page map
-                                   (default 65536): ids are renumbered when they run out, so
-                                   this bounds the live segments, not the segments created */
+                                   (default 65536; 8192 with the default page_capacity): ids
+                                   are renumbered when they run out, and the growth step
+                                   raises it when live segments fill it */
     /* Tight paged tier (0 = off): LDS capacities below the three above.  Documents are
        replayed at these first (a smaller LDS footprint: more documents per CU); one that
        does not fit, or whose next message could outgrow them, continues -- from that
@@ -268,13 +278,13 @@ int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_
         (SEQ/sequence.ts:240, 251; MT/mergeTree.ts:1610-1667; MT/client.ts getPosition /
         getContainingSegment).  A view is (ref_seq, client): client is a short client id as
         the encoder numbered it, 0 = this replica (its view is the observer view whatever the
-        ref_seq, MT/mergeTree.ts:1692-1698).  A remote view is one the client can still hold:
-        ref_seq at or above the refSeq of its latest message (>= minSeq; MT_E_INVALID below
-        minSeq or above currentSeq).  Below its latest refSeq the reference answers from
-        partial lengths that need not add up to its segments' view lengths (measured on the
-        read-out fixture: 51 239 of 211 951 such views differ, none of the 59 558 others), so
-        such a view is refused with MT_E_STALE_VIEW, as is any remote view of a document a
-        generated batch (mt_generate) replayed. ---- */
+        ref_seq, MT/mergeTree.ts:1692-1698).  A remote view takes any ref_seq of the collab
+        window [minSeq, currentSeq] (MT_E_INVALID outside it).  Interior nodes answer a remote
+        view from their partial lengths (nodeLength / blockLength, MT/partialLengths.ts:455-486),
+        leaves by visibility: every segment adds its length when the view holds its insert and
+        subtracts it when the view holds its removal, so in a view below the client's latest
+        refSeq a node can count a segment the client removed but had not seen inserted as
+        negative, as the reference does (pinned on every view of tests/golden/ref_readouts*). ---- */
 typedef struct mt_seg_info {
     int32_t row;             /* index in document order (-1: no such segment) */
     uint32_t uid;            /* segment id: stable for the segment's life (a split's left half
@@ -290,8 +300,11 @@ typedef struct mt_seg_info {
     int32_t ordinal_len;     /* -1: no ordinals on this handle (mt_options.segment_ordinals) */
     uint16_t ordinal[16];    /* MergeNode.ordinal's characters (MT/mergeTree.ts:347-372) */
 } mt_seg_info;
-/* MergeTree.getContainingSegment(pos, refSeq, clientId) (MT/mergeTree.ts:1656-1667): the
-   first segment visible in the view whose span holds pos; row -1 when pos is past the end. */
+/* MergeTree.getContainingSegment(pos, refSeq, clientId) (MT/mergeTree.ts:1656-1667):
+   searchBlock's descent (:1830-1862) -- at every level the first child whose length in the
+   view (partial lengths for interior nodes) exceeds pos; row -1 when it finds no segment
+   (past the end, or, in a view below the client's latest refSeq, a block whose leaves do not
+   hold the position: the reference does not backtrack). */
 int mt_get_containing_segment(mt_handle *h, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
                               mt_seg_info *out, uint16_t *text, uint32_t text_cap);
 /* MergeTree.getPosition(segment, refSeq, clientId) (MT/mergeTree.ts:1619-1636) of the segment
@@ -301,8 +314,7 @@ int mt_get_containing_segment(mt_handle *h, uint32_t doc, int32_t pos, int32_t r
 int mt_get_segment_by_uid(mt_handle *h, uint32_t doc, uint32_t uid, int32_t ref_seq, int32_t client,
                           mt_seg_info *out, uint16_t *text, uint32_t text_cap);
 /* MergeTree.getLength(refSeq, clientId) (MT/mergeTree.ts:1610-1612) for n (doc, ref_seq,
-   client) queries.  Stale views get out[q] = -1 and the call returns MT_E_STALE_VIEW after
-   answering every other query. */
+   client) queries: the root's partial length in each view. */
 int mt_get_view_lengths(mt_handle *h, uint32_t n, const uint32_t *docs, const int32_t *ref_seq,
                         const int32_t *client, int32_t *out);
 /* Debug: raw segment records (8 u32 per segment: segA then segB) and the 32-word header. */

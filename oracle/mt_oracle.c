@@ -299,12 +299,39 @@ static inline int32_t local_net_length(const Seg *s) {
     return s->rseq != RSEQ_NONE ? 0 : s->len;
 }
 
-/* nodeLength :1692-1732.  Interior nodes: the reference reads PartialSequenceLengths
-   (MT/partialLengths.ts:432-486) whose contract is the sum of the leaves' lengths. */
+/* A leaf's term in its ancestors' PartialSequenceLengths for a remote view (client, refSeq).
+   The partials (MT/partialLengths.ts fromLeaves :208-259 / insertSegment :286-336 / combine
+   :88-207) record +len at the segment's seq and -len at its removedSeq under the remover, and
+   under every overlapping remover in clientSeqNumbers (addClientSeqNumberFromPartial
+   :581-590); getBranchPartialLength (:455-486) takes every entry at or below refSeq (latestLEQ
+   :31-47) plus the client's own entries above it.  So a segment adds len when it is inserted
+   in the view (seq <= refSeq or its own client) and subtracts len when it is removed in the
+   view (removedSeq <= refSeq, or removed / overlap-removed by the client) -- independently:
+   a segment the view sees removed but not inserted counts -len.  That happens only in views
+   below the client's latest refSeq ("stale"); elsewhere a removal implies the insert, and the
+   term equals the leaf's nodeLength. */
+static int32_t seg_partial(const Seg *s, int32_t ref_seq, int32_t client) {
+    const int ins = s->client == client || (s->seq != UNASSIGNED && s->seq <= ref_seq);
+    const int rem = s->rseq != RSEQ_NONE && (s->rclient == client || ovl_has(s, client) ||
+                                             (s->rseq != UNASSIGNED && s->rseq <= ref_seq));
+    return s->len * (ins - rem);
+}
+static int32_t block_partial(const Block *b, int32_t ref_seq, int32_t client) {
+    int32_t sum = 0;
+    for (int i = 0; i < b->count; i++)
+        sum += b->ch[i]->leaf ? seg_partial((const Seg *)b->ch[i], ref_seq, client)
+                              : block_partial((const Block *)b->ch[i], ref_seq, client);
+    return sum;
+}
+
+/* nodeLength :1692-1732.  Interior nodes read PartialSequenceLengths.getPartialLength
+   (blockLength :1664-1670): the sum of their leaves' partial terms (seg_partial); leaves
+   their visibility in the view. */
 static int32_t node_len(const Node *n, int32_t ref_seq, int32_t client) {
     if (!n->leaf) {
         const Block *b = (const Block *)n;
         int32_t sum = 0;
+        if (client != OBSERVER) return block_partial(b, ref_seq, client);
         for (int i = 0; i < b->count; i++) sum += node_len(b->ch[i], ref_seq, client);
         return sum;
     }
@@ -1298,6 +1325,80 @@ int32_t orc_view_length(orc_doc *d, int32_t ref_seq, int32_t client) {
     return node_len(&d->root->n, ref_seq, client);
 }
 int32_t orc_length(orc_doc *d) { return node_len(&d->root->n, 0, OBSERVER); }
+
+/* getPosition :1619-1636 in view (client, refSeq): the nodeLength of every earlier sibling of
+   the node and of each of its ancestors */
+static int32_t get_position_view(const Node *node, int32_t ref_seq, int32_t client) {
+    int32_t total = 0;
+    const Block *parent = node->parent;
+    const Node *prev = node;
+    while (parent) {
+        for (int i = 0; i < parent->count; i++) {
+            const Node *c = parent->ch[i];
+            if (c == prev) break;
+            total += node_len(c, ref_seq, client);
+        }
+        prev = &parent->n;
+        parent = parent->n.parent;
+    }
+    return total;
+}
+typedef struct IdxAcc {
+    const Seg *want;
+    int32_t idx, hit;
+} IdxAcc;
+static void idx_fn(Seg *s, void *arg) {
+    IdxAcc *a = (IdxAcc *)arg;
+    if (s == a->want) a->hit = a->idx;
+    a->idx++;
+}
+/* getContainingSegment :1656-1667 -> searchBlock :1830-1862 in view (client, refSeq): at
+   every level the first child with pos < nodeLength(child) (interior children by their partial
+   lengths), descending without backtracking -- a block whose leaves do not hold pos yields no
+   segment.  out = {document-order index, offset, getPosition in the view, observer position}
+   (index -1: undefined). */
+void orc_containing(orc_doc *d, int32_t pos, int32_t ref_seq, int32_t client, int32_t *out) {
+    const Block *b = d->root;
+    out[0] = -1;
+    out[1] = out[2] = out[3] = 0;
+    for (;;) {
+        const Node *hit = NULL;
+        for (int i = 0; i < b->count; i++) {
+            const int32_t len = node_len(b->ch[i], ref_seq, client);
+            if (pos < len) {
+                hit = b->ch[i];
+                break;
+            }
+            pos -= len;
+        }
+        if (!hit) return;
+        if (!hit->leaf) {
+            b = (const Block *)hit;
+            continue;
+        }
+        IdxAcc a = {(const Seg *)hit, 0, -1};
+        walk_segs(&d->root->n, idx_fn, &a);
+        out[0] = a.hit;
+        out[1] = pos;
+        out[2] = get_position_view(hit, ref_seq, client);
+        out[3] = get_position_view(hit, 0, OBSERVER);
+        return;
+    }
+}
+typedef struct NthAcc {
+    int32_t want, idx;
+    Seg *hit;
+} NthAcc;
+static void nth_fn(Seg *s, void *arg) {
+    NthAcc *a = (NthAcc *)arg;
+    if (a->idx++ == a->want) a->hit = s;
+}
+/* getPosition of the seg_index-th segment (document order) in view (client, refSeq); -1: none */
+int32_t orc_position(orc_doc *d, int32_t seg_index, int32_t ref_seq, int32_t client) {
+    NthAcc a = {seg_index, 0, NULL};
+    walk_segs(&d->root->n, nth_fn, &a);
+    return a.hit ? get_position_view(&a.hit->n, ref_seq, client) : -1;
+}
 
 typedef void (*seg_fn)(Seg *, void *);
 static void walk_segs(Node *n, seg_fn fn, void *arg) {   /* walkAllSegments :3002-3016 */

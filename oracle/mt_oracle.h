@@ -44,6 +44,10 @@ typedef struct orc_regen_rec {
 int32_t orc_regenerate(orc_doc *d, int32_t kind, orc_regen_rec *out, int32_t cap, uint16_t *text,
                        int32_t text_cap, uint32_t *props, int32_t props_cap);
 int32_t orc_view_length(orc_doc *d, int32_t ref_seq, int32_t client);
+/* MergeTree.getContainingSegment / getPosition in a remote view (partial lengths at interior
+   nodes): out = {segment index (-1: undefined), offset, position in the view, observer position} */
+void orc_containing(orc_doc *d, int32_t pos, int32_t ref_seq, int32_t client, int32_t *out);
+int32_t orc_position(orc_doc *d, int32_t seg_index, int32_t ref_seq, int32_t client);
 int32_t orc_length(orc_doc *d);
 int32_t orc_text(orc_doc *d, uint16_t *out, int32_t cap);
 /* segment rows of 8 int32: len, seq, client, rseq(INT32_MIN=none), rclient, n_overlap,

@@ -48,6 +48,10 @@ def lib():
         L.orc_regenerate.restype = i32
         L.orc_view_length.argtypes = [P, i32, i32]
         L.orc_view_length.restype = i32
+        L.orc_containing.argtypes = [P, i32, i32, i32, P]
+        L.orc_containing.restype = None
+        L.orc_position.argtypes = [P, i32, i32, i32]
+        L.orc_position.restype = i32
         L.orc_length.argtypes = [P]
         L.orc_length.restype = i32
         L.orc_text.argtypes = [P, P, i32]
@@ -148,6 +152,17 @@ class OracleDoc:
         m = np.zeros(3, dtype=np.uint32)
         lib().orc_maintenance(self.h, _p(m))
         return m.tolist()
+
+    def view_length(self, ref_seq, client):
+        """MergeTree.getLength(refSeq, clientId) (partial lengths: stale views included)."""
+        return int(lib().orc_view_length(self.h, int(ref_seq), int(client)))
+
+    def containing(self, pos, ref_seq, client):
+        """getContainingSegment in a view: (segment index, offset, position in the view,
+        observer position), or None when the reference finds no segment."""
+        o = np.zeros(4, dtype=np.int32)
+        lib().orc_containing(self.h, int(pos), int(ref_seq), int(client), _p(o))
+        return None if o[0] < 0 else tuple(int(x) for x in o)
 
     def outputs(self):
         L = lib()

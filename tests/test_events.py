@@ -48,7 +48,8 @@ def test_sorted_segment_set_collisions_and_undefined():
 # every storage tier keeps ordinals (mt_options.segment_ordinals): the flat ones and the paged
 # layout -- its page splits, level-1 packs and new roots, a tight tier handing documents over,
 # a narrow one, and the growth step moving documents to larger regions mid-batch
-ORD_TIERS = {"lds": dict(lds_seg_capacity=0), "hbm": dict(lds_seg_capacity=-1), "tiny": dict(lds_seg_capacity=16),
+ORD_TIERS = {"lds": dict(lds_seg_capacity=0, page_capacity=-1), "hbm": dict(lds_seg_capacity=-1, page_capacity=-1),
+             "tiny": dict(lds_seg_capacity=16, page_capacity=-1),
              "paged": dict(lds_seg_capacity=-1, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048),
              "tight": dict(lds_seg_capacity=16, page_capacity=256, unsettled_capacity=2048, page_heap_capacity=2048,
                            lds_page_capacity=24, lds_unsettled_capacity=40, lds_page_heap_capacity=40),
@@ -133,12 +134,13 @@ def test_gpu_readouts_match_reference(tier, name):
     getPosition (MT/mergeTree.ts:1610-1667, Client.getPosition / getContainingSegment) of the
     final replicas equal the reference's in the observer's view and in every writer's view of
     the collab window (tests/golden/ref_readouts.json.gz: getLength in all of them,
-    getContainingSegment in a sample of each writer's) -- except the views below the writer's
-    latest refSeq, which the reference answers from partial lengths that need not add up to its
-    leaves (51 239 of 211 951 differ) and which are refused (StaleViewError); ordinals too on
-    every tier that keeps them.  ref_readouts_wide: the same on the paged tiers for the
-    200-writer / lag-400 streams (views through overflow overlap sets)."""
-    from fluidframework_amd import MergeTreeBatch, StaleViewError
+    getContainingSegment in a sample of each writer's) -- the views below the writer's latest
+    refSeq included, where the reference's interior nodes answer from partial lengths that
+    need not add up to their leaves (51 239 of 211 951 differ; 1 079 containing queries find
+    no segment); ordinals too on every tier that keeps them.  ref_readouts_wide: the same on
+    the paged tiers for the 200-writer / lag-400 streams (views through overflow overlap
+    sets)."""
+    from fluidframework_amd import MergeTreeBatch
     if name == "ref_readouts_wide" and tier not in PAGED_TIERS + ("paged_noord",):
         pytest.skip("more than 63 concurrent overlapping removers: paged layout only")
     fx = gu.load(name)
@@ -150,24 +152,16 @@ def test_gpu_readouts_match_reference(tier, name):
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     assert (mt.status() == 0).all()
-    n_stale = n_views = 0
+    n_stale = n_views = n_stale_cont = 0
     for i, doc in enumerate(fx["docs"]):
         refs, clis, want, stale, _ = zip(*doc["lengths"])
-        got = mt.get_view_lengths([i] * len(refs), refs, clis, refuse_stale=False)
-        # every view of the collab window: equal to the reference, or refused when stale
-        assert list(got) == [-1 if s else w for w, s in zip(want, stale)], doc["doc"]
+        got = mt.get_view_lengths([i] * len(refs), refs, clis)
+        assert list(got) == list(want), doc["doc"]
         n_stale += sum(stale)
         n_views += len(refs)
-        if 1 in stale:
-            k = stale.index(1)
-            with pytest.raises(StaleViewError):
-                mt.get_view_lengths([i], [refs[k]], [clis[k]])
         for pos, ref, cli, exp, st in doc["containing"]:
-            where = (doc["doc"], pos, ref, cli)
-            if st:
-                with pytest.raises(StaleViewError):
-                    mt.get_containing_segment(i, pos, ref, cli)
-                continue
+            where = (doc["doc"], pos, ref, cli, st)
+            n_stale_cont += st
             got = mt.get_containing_segment(i, pos, ref, cli)
             if exp is None:
                 assert got is None, where
@@ -186,7 +180,10 @@ def test_gpu_readouts_match_reference(tier, name):
     # a segment that left the tree reads as gone (the reference's getPosition walks no parent)
     assert mt.get_segment_by_uid(0, 0xFFFFFFF) is None
     if name == "ref_readouts":
-        assert n_stale > 200000 and n_views > 270000
+        assert n_stale > 200000 and n_views > 270000 and n_stale_cont > 2000
+    # outside the collab window a remote view is invalid
+    with pytest.raises(RuntimeError):
+        mt.get_view_lengths([0], [int(fx["docs"][0]["minSeq"]) - 1], [1])
 
 
 def test_reference_ordinal_invariant_holds_on_fixture_streams(tmp_path):

@@ -10,10 +10,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _gpu_batch(n_docs, **kw):
+    """A handle for one storage tier: without paged capacities, a flat-only one (page_capacity
+    -1: the library's default handle is paged, see test_gpu_default_handle_is_unbounded)."""
     from fluidframework_amd import MergeTreeBatch
     kw.setdefault("delta_log_capacity", 1 << 18)
     kw.setdefault("seg_capacity", 8192)       # flat tiers: the 10k-op fixtures hold ~4.5k segments
     kw.setdefault("text_capacity", 1 << 17)
+    kw.setdefault("page_capacity", -1)
     return MergeTreeBatch(n_docs, **kw)
 
 
@@ -744,3 +747,28 @@ def test_gpu_rich_callback_stream_matches_reference(tier):
     plain.load_initial_text(a["seed_off"], a["seed"])
     plain.apply_arrays(a)
     assert np.array_equal(plain.checksums(), mt.checksums())
+
+
+@pytest.mark.parametrize("name", ["ref_c3_full", "ref_c4_full", "ref_wide400", "ref_c3_long"])
+def test_gpu_default_handle_is_unbounded(name):
+    """A handle built with no capacity options (the drop-in default) takes documents of any
+    size: the reference's MergeTree has no per-document ceiling (removedClientOverlap and
+    TextSegment.append are unbounded, MT/mergeTree.ts:2577-2585, MT/textSegment.ts:74-85).  The
+    10k-message C3 / C4 documents (~4k live segments), the 200-writer lag-400 streams (~80
+    concurrent overlapping removers) and the 30k-message documents replay equal to the
+    reference, the growth step raising whatever the small default starting capacities lack."""
+    from fluidframework_amd import MergeTreeBatch
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = MergeTreeBatch(len(fx["docs"]), delta_log_capacity=1 << 21)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all(), mt.status()
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, bad[:4]
+    assert all(mt.is_paged(i) for i in range(len(fx["docs"])))

@@ -253,3 +253,35 @@ def test_oracle_live_reconnects_match_reference(oracle_lib, name):
         assert d.pending_counts()[1] == doc["drained"]["pending"] == 0
         assert (o["text"], o["leaves"], o["segs"].tolist(), o["seg_props"]) == \
             (exp["text"], exp["leaves"], exp["segs"], exp["seg_props"]), (name, doc["doc"])
+
+
+@pytest.mark.parametrize("name", ["ref_readouts", "ref_readouts_wide"])
+def test_oracle_readouts_match_reference_in_every_view(oracle_lib, name):
+    """MergeTree.getLength(refSeq, clientId), getContainingSegment and getPosition in every
+    writer view of the collab window -- including the views below the writer's latest refSeq,
+    which the reference answers from partial lengths (MT/partialLengths.ts:455-486) rather than
+    from its leaves' nodeLength -- equal the reference's (the oracle restates the partial
+    lengths as each leaf's +len at its insert and -len at its removal, oracle/mt_oracle.c
+    seg_partial)."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    n_stale = n_stale_cont = 0
+    for doc in fx["docs"]:
+        a = gu.encode_docs(fx, interner, [doc])
+        od = oracle_lib.OracleDoc.new(a["seed"][: a["seed_off"][1]])
+        assert od.apply_all(a["ops"], a["text"], a["props"]) == 0
+        rows = od.outputs()["segs"]
+        for ref, cli, want, stale, _ in doc["lengths"]:
+            assert od.view_length(ref, cli) == want, (doc["doc"], ref, cli, stale)
+            n_stale += stale
+        for pos, ref, cli, exp, stale in doc["containing"]:
+            got = od.containing(pos, ref, cli)
+            where = (doc["doc"], pos, ref, cli, stale)
+            n_stale_cont += stale
+            if exp is None:
+                assert got is None, where
+                continue
+            offset, vpos, lpos, clen = exp[:4]
+            assert got is not None and got[1:] == (offset, vpos, lpos), (where, got, exp)
+            assert rows[got[0]][0] == clen, where
+    assert n_stale > 200000 and n_stale_cont > 1000
