@@ -106,28 +106,88 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     per_class = []
     for r in runs:
         st = r["mt"].status()
-        same = bool(np.array_equal(r["mt"].checksums(), r["gen"])) and int((st != 0).sum()) == 0
+        sums = r["mt"].checksums()
+        same = bool(np.array_equal(sums, r["gen"])) and int((st != 0).sum()) == 0
         ok = ok and same
+        # algorithmic bytes of the class's replay (SURVEY 8d B_op, as bench.run_replay): op
+        # records + result records + inserted UTF-16 units (a generated batch's text arena holds
+        # exactly the insert payloads) + the final state write-back
+        n, t, p = r["batch"].sizes()
+        alg = (n * (bench.OP_BYTES + bench.RESULT_BYTES) + 2 * t +
+               int(sums["n_segments"].astype(np.int64).sum()) * bench.SEG_BYTES +
+               2 * int(sums["length"].astype(np.int64).sum()))
         per_class.append(dict(max_ops=r["max_ops"], docs=int(len(r["idx"])), ops=r["ops"],
-                              kernel_ms=round(float(r["mt"].last_kernel_ms()), 1),
+                              kernel_ms=round(float(r["mt"].last_kernel_ms()), 1), alg_bytes=alg,
                               replay_equals_generation=same, grown=r["mt"].last_grown(),
                               peaks=r["mt"].last_paged_peaks()))
-    # oracle sample: the longest and a middle document of every class (rank 0)
-    mism, sampled = 0, 0
+    # the dominant class (longest kernel time) bounds the step: its roofline
+    dom = max(per_class, key=lambda c: c["kernel_ms"])
+    achieved = dom["alg_bytes"] / (dom["kernel_ms"] / 1000.0) if dom["kernel_ms"] > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": bench.HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / bench.HBM_PEAK, "traffic": None,
+                "kernel": f"k_replay_paged (class <= {dom['max_ops']} messages, its own stream)",
+                "kernel_ms": dom["kernel_ms"], "alg_bytes_per_launch": dom["alg_bytes"]}
+    # oracle sample and CPU baseline: the longest and a middle document of every class (rank 0),
+    # generated by the CPU restatement on parallel host threads (its generator replays them:
+    # their checksums are the check), then replayed again from their op records, timed
+    mism, sampled, cpu = 0, 0, None
     if rank == 0 and not args.no_cpu:
+        from concurrent.futures import ThreadPoolExecutor
         sys.path.insert(0, os.path.join(bench.REPO, "oracle"))
         import pyoracle
-        for r in runs:   # (the CPU restatement takes ~1 s per 10k messages: classes <= 20k only)
-            if r["max_ops"] > 20000:
-                continue
+        picks = []
+        for ri, r in enumerate(runs):
             order = np.argsort(-lens[r["idx"]], kind="stable")
             for j in sorted({int(order[0]), int(order[len(order) // 2])}):
-                d = int(r["idx"][j])
-                g = pyoracle.generate(dict(cfg, ops=int(lens[d])), int(ids[d]), keep=True)
-                osum = g["doc"].outputs()["checksum"]
-                got = r["mt"].checksums()[j]
-                sampled += 1
-                mism += int(any(got[f] != osum[f] for f in ("length", "text_hash", "props_hash", "delta_hash")))
+                picks.append((ri, j, int(r["idx"][j])))
+        threads = args.cpu_threads or bench.host_cores()
+
+        def gen(pk):
+            _, _, d = pk
+            g = pyoracle.generate(dict(cfg, ops=int(lens[d])), int(ids[d]), keep=True)
+            g["sum"] = g.pop("doc").outputs()["checksum"]
+            return g
+
+        # longest first, so the 200k documents do not start last
+        order = sorted(range(len(picks)), key=lambda k: -int(lens[picks[k][2]]))
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            gens = dict(zip(order, ex.map(gen, [picks[k] for k in order])))
+        for k, (ri, j, d) in enumerate(picks):
+            got = runs[ri]["mt"].checksums()[j]
+            osum = gens[k]["sum"]
+            sampled += 1
+            mism += int(any(got[f] != osum[f] for f in ("length", "text_hash", "props_hash", "delta_hash")))
+        # the CPU baseline: the same documents' streams replayed by the restatement
+        ops, text, props, seed, doc_off, seed_off = [], [], [], [], [0], [0]
+        tb = pb = 0
+        for k in order:
+            g = gens[k]
+            o = g["ops"].copy()
+            ins = o["kind"] == 0
+            o["payload"][ins] += tb
+            hp = o["props"] != 0xFFFFFFFF
+            o["props"][hp] += pb
+            ops.append(o)
+            text.append(g["text"])
+            props.append(g["props"])
+            seed.append(g["seed"])
+            tb += len(g["text"])
+            pb += len(g["props"])
+            doc_off.append(doc_off[-1] + len(o))
+            seed_off.append(seed_off[-1] + len(g["seed"]))
+        arrays = dict(ops=np.concatenate(ops), text=np.concatenate(text), props=np.concatenate(props),
+                      seed=np.concatenate(seed), doc_off=np.asarray(doc_off, dtype=np.int64),
+                      seed_off=np.asarray(seed_off, dtype=np.int64))
+        used = min(threads, len(picks))
+        t_c = time.perf_counter()
+        osums, ost = pyoracle.replay_batch(arrays, threads=used)
+        t_c = time.perf_counter() - t_c
+        n_c = int(doc_off[-1])
+        cpu = dict(value=round(n_c / t_c, 1), unit="ops/s", cores=used, kind="port", host_cpus=os.cpu_count(),
+                   sample=f"oracle/mt_oracle.c replay of {len(picks)} documents (the longest and a middle one of "
+                          f"every size class, {n_c} messages; the 200k-message ones bound the wall time) on "
+                          f"{used} host threads, {t_c:.2f} s")
+        mism += int(sum(osums[q] != gens[k]["sum"] for q, k in enumerate(order)) + (ost != 0).sum())
     if dist is not None:
         import torch
         t = torch.tensor([1 if ok else 0], device="cuda")
@@ -144,6 +204,7 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
                        "zipf_s": cfg["zipf_s"], "max_ops": cfg["max_ops"], "classes": cfg["classes"],
                        "median_ops": int(np.median(lens_all)), "docs_at_max": int((lens_all == cfg["max_ops"]).sum()),
                        "parallelism": f"dp{world} (op-balanced shards)"},
+            "roofline": roofline, "cpu_baseline": cpu,
             "parity": {"replay_equals_generation": ok, "oracle_docs": sampled, "oracle_mismatches": mism},
             "per_class": per_class, "gen_s": round(t_gen, 1)}
     return line

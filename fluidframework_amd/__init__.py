@@ -533,6 +533,12 @@ class DeviceBatch:
     def apply_async(self):
         self.owner._check(self.owner.lib.mt_batch_apply_async(self.owner.h, self.b), "mt_batch_apply_async")
 
+    def sizes(self):
+        """(op records, text units, property words) of the batch."""
+        n, t, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self.owner.lib.mt_batch_sizes(self.b, ctypes.byref(n), ctypes.byref(t), ctypes.byref(p))
+        return int(n.value), int(t.value), int(p.value)
+
     def download(self):
         lib = self.owner.lib
         n, t, p = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()

@@ -43,6 +43,10 @@ FIXTURES = {
     "ref_wide400": ("c4", {"ops": 3000, "writers": 200, "lag": 400, "seed": 7272}, 2),
     # a long-lived document: 30k messages (~45k segment ids created, ~12k live segments)
     "ref_c3_long": ("c3", {"ops": 30000}, 2),
+    # the long classes of the skewed bench (c3skew: 40k-200k messages; 1.5k-3.2k pages): one
+    # C3-mix document of 60k and one of 100k messages
+    "ref_c3_60k": ("c3", {"ops": 60000, "seed": 6060}, 1),
+    "ref_c3_xl": ("c3", {"ops": 100000, "seed": 10100}, 1),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),
     "ref_ext": (None, {"ext": True, "seed": 77, "ops": 700, "writers": 5, "lag": 40, "seed_len": 40,
                        "p_insert": 0.5, "p_remove": 0.3, "text_max": 12, "p_newline": 0.08,

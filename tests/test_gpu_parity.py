@@ -772,3 +772,39 @@ def test_gpu_default_handle_is_unbounded(name):
             bad.append((doc["doc"], errs))
     assert not bad, bad[:4]
     assert all(mt.is_paged(i) for i in range(len(fx["docs"])))
+
+
+@pytest.mark.parametrize("caps", ["c3_bench", "class_100k", "class_200k", "grow"])
+@pytest.mark.parametrize("name", gu.XL_FIXTURES)
+def test_gpu_xl_documents_match_reference(name, caps):
+    """The skewed bench's long classes (c3skew: 40k-200k messages per document) pinned to the
+    reference: a 60k- and a 100k-message C3 document (tests/golden/ref_c3_60k / ref_c3_xl, made
+    by the reference) replayed at the capacities of the bench's 100k and 200k classes
+    (bench_skew.class_caps: 1.6k / 3.2k pages, the two-level page search), at the uniform C3
+    bench's (the tight tier hands them to the full tier, which hands them to the growth step
+    as they pass 275 pages) and at the grow tier's (12 pages: growth round after round) --
+    text, leaf partition, segment table, property sets and every delta record equal."""
+    import json
+    import os
+    import bench
+    import bench_skew
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    cfg = json.load(open(os.path.join(bench.REPO, "bench", "configs.json")))["c3skew"]
+    kw = {"c3_bench": bench.capacities(dict(fx["config"], ops=10000)),
+          "class_100k": bench_skew.class_caps(bench, cfg, 100000),
+          "class_200k": bench_skew.class_caps(bench, cfg, 200000),
+          "grow": TIERS["grow"]}[caps]
+    mt = _gpu_batch(len(fx["docs"]), **dict(kw, delta_log_capacity=1 << 22))
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all(), mt.status()
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        errs = gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, bad
+    if caps in ("c3_bench", "grow"):
+        assert mt.last_grown()["grown"] >= 1

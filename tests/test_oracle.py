@@ -7,7 +7,7 @@ import pytest
 import golden_util as gu
 
 
-@pytest.mark.parametrize("name", gu.ALL_FIXTURES + gu.LONG_FIXTURES + gu.WIDE_FIXTURES)
+@pytest.mark.parametrize("name", gu.ALL_FIXTURES + gu.LONG_FIXTURES + gu.WIDE_FIXTURES + gu.XL_FIXTURES)
 def test_oracle_matches_reference(oracle_lib, name):
     fx = gu.load(name)
     interner = gu.interner_for(fx)
