@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = every core this process may use)")
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="0 = all docs of rank 0")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the encode / H2D upload rates")
     ap.add_argument("--lds-cap", type=int, default=0, help="segments per document in the LDS tier (0 = default)")
     ap.add_argument("--seg-cap", type=int, default=0, help="flat HBM segments per document (0 = default; sweeps)")
     ap.add_argument("--skew-classes", default="",
@@ -616,6 +617,40 @@ def dispatch(args):
     raise SystemExit(f"bench.py: unknown --config {args.config}")
 
 
+def ingest_rates(mt, host, step_s):
+    """What the timed region leaves out, reported beside it: the host encode of
+    sequenced messages into op records (the reference's own C3 message logs, ref_c3_full,
+    through wire.Batch -- the encoder encode.js mirrors) and the H2D upload of this step's op
+    records and arenas from pageable host memory (mt_batch_upload), so that a log ingested
+    from the host would replay at value_with_upload."""
+    import gzip
+    from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts
+    fx = json.load(gzip.open(os.path.join(REPO, "tests", "golden", "ref_c3_full.json.gz"), "rt"))
+    msgs = [compact_msgs_to_dicts(d["msgs"]) for d in fx["docs"]]
+    t = time.perf_counter()
+    b = Batch(Interner(synthetic=True))
+    for d, m in zip(fx["docs"], msgs):
+        b.add_doc(d["seed_text"], m)
+    b.arrays()
+    t_enc = time.perf_counter() - t
+    n_msgs = sum(len(m) for m in msgs)
+    nbytes = host["ops"].nbytes + host["text"].nbytes + host["props"].nbytes + host["doc_off"].nbytes
+    mt.sync()
+    t = time.perf_counter()
+    up = mt.upload(host)
+    mt.sync()
+    t_up = time.perf_counter() - t
+    up.free()
+    n_ops = len(host["ops"])
+    return {"encode": {"value": round(n_msgs / t_enc, 1), "unit": "messages/s", "cores": 1,
+                       "sample": f"{n_msgs} messages of tests/golden/ref_c3_full (JSON message objects -> op records "
+                                 f"+ arenas, fluidframework_amd/wire.py Batch), {t_enc:.2f} s"},
+            "h2d_upload": {"bytes": int(nbytes), "s": round(t_up, 3), "GB_per_s": round(nbytes / t_up / 1e9, 2),
+                           "how": "mt_batch_upload of this step's op records, text and property arenas from pageable "
+                                  "host memory (validation + hipMemcpy)"},
+            "value_with_upload": round(n_ops / (step_s + t_up), 1)}
+
+
 def run_replay(args, cfg, rank, world, local_rank, dist):
     """Uniform replay (c2 / c3 / c4): the default line, BASELINE configs[2]."""
     from fluidframework_amd import MergeTreeBatch
@@ -714,6 +749,7 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
     alg_bytes = n_ops * (OP_BYTES + RESULT_BYTES) + 2 * payload_chars + final_bytes
     k_ms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (k_ms / 1000.0)
+    ingest = None if args.no_ingest else ingest_rates(mt, host, ms_per_step / 1000.0)
     traffic = traffic_raw = None
     if os.path.exists(PROFILE_PMC):
         try:
@@ -801,6 +837,7 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
                                    caps.get("page_heap_capacity")]},
         },
         "cpu_baseline": cpu,
+        "ingest": ingest,
         "parity": {"replay_equals_generation": replay_consistent, "oracle_sample": parity,
                    "shards": shards},
         "gen_s": round(t_gen, 2),

@@ -42,7 +42,7 @@ __device__ static void oslot_reset(const DevState &st, int doc) {
     int32_t *o = st.oslot + (size_t)doc * 2 * MT_OSLOTS;
     o[2 * lane()] = MT_OSLOT_FREE;
     o[2 * lane() + 1] = 0;
-    if (st.pgOvf && lane() < 2) ((uint32_t *)(st.pgOvf + (size_t)doc * st.OA))[lane()] = lane() ? 0u : (uint32_t)MT_OVF_HDR;
+    if (st.pgOvf && lane() < 4) ((uint32_t *)(st.pgOvf + (size_t)doc * st.OA))[lane()] = lane() ? 0u : (uint32_t)MT_OVF_HDR;
 }
 
 #define MT_LOAD_FANOUT (MT_MAXN - 1)

@@ -73,6 +73,8 @@ template <class T> struct PagedDoc {
                               // uid map, loaded at the message's start (zuid 0: none)
     GLB_AS uint16_t *govf;    // overflow overlap sets (MT_OVF_BIT; last-tier instantiations)
     int ovf_top, ovf_last, OA;   // its fill, the last message that made a set, its capacity
+    int ovf_maxn, ovf_half;      // the largest set made; the half sets are appended in (the
+                                 // other one receives the live sets at a compaction)
     int press;                // a compaction left the text (4) / record (5) arena more than 7/8
                               // full: a tight launch hands the document on (pg_arena_room)
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
@@ -1646,6 +1648,12 @@ TD bool ovf_member(DocT<T> &d, u64 o, int c) {
     for (int k = 1; k <= n; k++) in = in || s[k] == (uint16_t)c;
     return in;
 }
+// The arena is used in two halves, [MT_OVF_HDR, OA/2) and [OA/2, OA): sets are appended in
+// one, and a compaction (pg_ovf_compact) copies the live ones -- those a segment row still
+// names -- into the other, as the text arena's halves are compacted.  Masks hold offsets from
+// the arena's start, so a set is read the same wherever it lies.
+TD int ovf_half_lo(const PagedDoc<T> &pd, int half) { return half ? (pd.OA / 2) & ~7 : MT_OVF_HDR; }
+TD int ovf_half_end(const PagedDoc<T> &pd) { return pd.ovf_half ? pd.OA : (pd.OA / 2) & ~7; }
 // Adds client c to the overlap list of the window's segment i (lanes with need; wave-uniform
 // call): its overflow set, or the clients of its slot bits, copied with c into a new set.
 // false: the arena is full (the caller fails the document, diagnostic 11).
@@ -1656,7 +1664,8 @@ TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
     const int sz = need ? n_old + 2 : 0;
     const int inc = wave_scan_incl(sz);
     const int tot = bcast(inc, MT_WAVE - 1), top = pd.ovf_top;
-    if (!pd.govf || top + tot > pd.OA) return false;
+    if (!pd.govf || top + tot > ovf_half_end(pd)) return false;
+    pd.ovf_maxn = max(pd.ovf_maxn, wave_max(need ? n_old + 1 : 0));
     if (need) {
         const int off = top + inc - sz;
         GLB_AS uint16_t *t = pd.govf + off;
@@ -1682,6 +1691,72 @@ TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
     return true;
 }
 
+// Reclaims the overflow sets no segment names any more (removedClientOverlap lists go with
+// their segments: the reference drops them when zamboni unlinks or merges the segment,
+// MT/mergeTree.ts:1322-1398): every page's sets are copied into the other half of the arena,
+// each row's mask re-pointed, and the pages' unsettled-table entries (which copy the masks)
+// rebuilt.  Runs between messages, page by page from HBM, like paged_text_compact.
+TD void pg_ovf_compact(PagedDoc<T> &pd) {
+    DocT<T> &w = pd.w;
+    const int keep = pd.cur, keep_pos = pd.cur_pos;
+    if (keep >= 0) pd.dirty = 1;
+    pg_win_flush(pd);
+    if (w.status) return;
+    gsync_rd();
+    const int nh = 1 - pd.ovf_half;
+    const int lo = ovf_half_lo(pd, nh), hi = nh ? pd.OA : (pd.OA / 2) & ~7;
+    int top = lo;
+    const int np = nbr(pd.up, 1);
+    for (int q = 0; q < np; q++) {
+        pg_win_load(pd, uni(pd.up.dir[q]));
+        const int i = lane();
+        const u64 o = i < w.n ? (u64)w.O[i] : 0ull;
+        const bool isset = (o & MT_OVF_BIT) != 0;
+        const int n = isset ? (int)pd.govf[(uint32_t)o] : 0;
+        const int sz = isset ? n + 1 : 0;
+        const int inc = wave_scan_incl(sz);
+        const int tot = bcast(inc, MT_WAVE - 1);
+        if (!ballot(isset)) continue;
+        if (top + tot > hi) {   // (cannot happen: the live sets fit the half they came from)
+            FAIL_INTERNAL(w);
+            return;
+        }
+        if (isset) {
+            const int off = top + inc - sz;
+            const GLB_AS uint16_t *src = pd.govf + (uint32_t)o;
+            GLB_AS uint16_t *dst = pd.govf + off;
+            for (int k = 0; k <= n; k++) dst[k] = src[k];
+            w.O[i] = (typename T::O_v)(MT_OVF_BIT | (u64)(uint32_t)off);
+        }
+        top += tot;
+        wsync<T>();
+        pd.dirty = 1;
+        pd.tdirty = 1;   // the table's copies of the masks are rebuilt at the flush
+        w.dlo = 0;
+        pg_win_flush(pd);
+        if (w.status) return;
+    }
+    gsync_rd();
+    pd.ovf_half = nh;
+    pd.ovf_top = top;
+    pd.cur = -1;
+    if (keep >= 0) {
+        pg_win_load(pd, keep);
+        pd.cur_pos = keep_pos;
+    }
+}
+// Arena units one message may take for new overflow sets: a remove makes at most one set per
+// segment it marks (<= its span), each the largest set so far (or the 63 slots' clients) plus
+// the remover and the count.  0 when no set can be made (no set exists yet and the remover has
+// or can take an overlap slot).
+TD int pg_ovf_need(PagedDoc<T> &pd, const mt_op_rec &op) {
+    if (op.kind != MT_OP_REMOVE) return 0;
+    DocT<T> &w = pd.w;
+    if (!w.wide && !oslot_short(w, op_cli(op))) return 0;
+    const int span = min(max(op.pos2 - op.pos1, 0), 1 << 16);
+    return (int)min((int64_t)span * (max(pd.ovf_maxn, 63) + 2), (int64_t)1 << 30);
+}
+
 // Can this message's text / property records be placed without running out of the arenas?
 // (TextSegment.append and property sets are unbounded in the reference, MT/textSegment.ts:74-85.)
 // A tight launch compacts inside messages, as every tier does, and hands the document on when a
@@ -1702,11 +1777,18 @@ TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc)
     const bool u_ok = w.next_uid + 4 <= pd.UM || op.kind == MT_OP_LOAD_REMOVED;
     if constexpr (T::kOvf) {
         if (pd.govf) {   // the overflow overlap arena (cause 11; a tight launch hands the document on)
-            // (sets are never reclaimed: a removed segment that zamboni has not unlinked yet
-            // keeps its list, which the segment rows report; the growth step raises the arena)
-            if (2 * pd.ovf_top > pd.OA) {
-                w.cap_cause = 11;
-                return false;
+            // this message's new sets must fit the current half: the live sets are compacted
+            // into the other half first when they would not, and the document is handed to
+            // the growth step (which doubles the arena) when even that leaves too little room
+            // -- so ovf_mark never runs out in the middle of a message
+            const int need = pg_ovf_need(pd, op);
+            if (need > 0 && pd.ovf_top + need > ovf_half_end(pd)) {
+                pg_ovf_compact(pd);
+                if (w.status) return true;   // (failed: the loop stops)
+                if (pd.ovf_top + need > ovf_half_end(pd)) {
+                    w.cap_cause = 11;
+                    return false;
+                }
             }
         }
     }
@@ -1906,11 +1988,18 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.press = 0;
     pd.ovf_top = MT_OVF_HDR;
     pd.ovf_last = 0;
+    pd.ovf_maxn = 0;
+    pd.ovf_half = 0;
     if constexpr (T::kOvf) {
         if (pd.govf) {
             const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
             pd.ovf_top = max((int)hw[0], MT_OVF_HDR);
             pd.ovf_last = (int)hw[1];
+            pd.ovf_maxn = (int)hw[2];
+            // the upper half only while the fill is above the midpoint: after a growth step
+            // (the arena doubled, its contents copied at the same offsets) the sets lie in the
+            // new lower half
+            pd.ovf_half = ((int)hw[3] & 1) && pd.ovf_top > ((pd.OA / 2) & ~7) ? 1 : 0;
         }
     }
 }
@@ -2004,7 +2093,9 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
     if (failed) w.status = failed;
     w.oslot[2 * lane()] = w.ocli;
     if constexpr (T::kOvf) {
-        if (pd.govf && lane() < 2) ((GLB_AS uint32_t *)pd.govf)[lane()] = (uint32_t)(lane() ? pd.ovf_last : pd.ovf_top);
+        if (pd.govf && lane() < 4)
+            ((GLB_AS uint32_t *)pd.govf)[lane()] =
+                (uint32_t)(lane() == 0 ? pd.ovf_top : (lane() == 1 ? pd.ovf_last : (lane() == 2 ? pd.ovf_maxn : pd.ovf_half)));
     }
     wsync<T>();
     const int np = nbr(up, 1);

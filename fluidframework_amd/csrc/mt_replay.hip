@@ -2694,6 +2694,30 @@ int mt_debug_heap(mt_handle *h, uint32_t doc, int32_t *heap, uint32_t cap, uint3
     return 0;
 }
 
+int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out) {
+    if (!out) return MT_E_INVALID;
+    HostDoc hd;
+    int rc = fetch_doc(h, doc, hd, false, false);
+    if (rc) return rc;
+    for (int k = 0; k < 5; k++) out[k] = 0;
+    if (hd.ovf.size() < MT_OVF_HDR) return 0;
+    uint32_t w[4];
+    memcpy(w, hd.ovf.data(), sizeof(w));
+    const int OA = (int)hd.ovf.size(), mid = (OA / 2) & ~7;
+    const int half = (w[3] & 1) && (int)w[0] > mid ? 1 : 0;
+    out[0] = OA;
+    out[1] = (int)w[0] - (half ? mid : MT_OVF_HDR);
+    out[2] = half;
+    out[3] = (int)w[2];
+    std::vector<uint32_t> offs;
+    for (int i = 0; i < hd.hdr.n_seg; i++)
+        if (hd.O[i] & MT_OVF_BIT) offs.push_back((uint32_t)hd.O[i]);
+    std::sort(offs.begin(), offs.end());
+    offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+    for (uint32_t off : offs) out[4] += off < hd.ovf.size() ? (int)hd.ovf[off] + 1 : 0;
+    return 0;
+}
+
 int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_t *pairs,
                          uint32_t cap_pairs, int32_t *n_pairs) {
     HostDoc hd;

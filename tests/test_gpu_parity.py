@@ -484,6 +484,30 @@ def test_gpu_overlap_beyond_the_slots_matches_reference(tier):
     assert not bad, bad[:4]
 
 
+@pytest.mark.parametrize("tier", ["paged", "tight", "grow"])
+def test_gpu_overflow_sets_are_reclaimed(tier):
+    """removedClientOverlap lists leave with their segments (zamboni unlinks or merges them,
+    MT/mergeTree.ts:1322-1398).  Over a 30k-message 200-writer lag-400 document
+    (tests/golden/ref_wide_long, made by the reference) thousands of overflow sets are made,
+    few live at once: the arena's halves are compacted (pg_ovf_compact) so that a 2048-unit
+    arena serves the whole document -- its fill stays bounded by the live sets, not by every
+    set made -- and the document equals the reference's."""
+    fx = gu.load("ref_wide_long")
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 21, overlap_arena_capacity=2048,
+                    **OVF_TIERS[tier])
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all(), mt.status()
+    for i, doc in enumerate(fx["docs"]):
+        assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), doc["doc"]
+        ar = mt.get_overlap_arena(i)
+        print(tier, ar, mt.last_grown())
+        assert ar["largest_set"] > 63          # sets were made (more than the 63 slots)
+        assert ar["capacity"] <= 8192, ar       # compacted: at most two doublings of 2048
+        assert ar["live_units"] <= ar["fill"]
+
 
 # ---------------------------------------------------------------- error model
 @pytest.mark.parametrize("tier", list(TIERS))
