@@ -38,6 +38,11 @@ def class_caps(bench, cfg, max_ops):
     if max_ops > 10000:
         for k in ("lds_page_capacity", "lds_unsettled_capacity", "lds_page_heap_capacity", "lds_narrow_overlap"):
             caps.pop(k, None)
+        # unsettled table / heap at the measured peaks plus a margin (c3skew: <= 203 / 183 in
+        # every class; the growth step takes a document past them): 26 + 8 fewer LDS bytes per
+        # entry over the C3 full tier's 320 / 512 -- with the leaf-block words in HBM (>= 512
+        # pages, mt_replay.hip use_hm) a 200k-message document takes 43.9 KB: 3 per CU
+        caps.update(unsettled_capacity=240, page_heap_capacity=224)
     return caps
 
 

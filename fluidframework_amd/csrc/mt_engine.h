@@ -104,10 +104,15 @@ template <bool kLogT> struct TierLiveLdsT {
 // kPPT / kPHT / kUTT (0: from PagedCaps at run time): LDS capacities fixed at compile time --
 // the launch's LDS layout becomes constant offsets and the capacities immediates, so the
 // kernel keeps none of them in registers (the bench's C3 tight tier, mt_replay.hip launch_paged).
+// kHMT: the leaf-block counts and needsScour flags of the pages stay in HBM (mt_paged.h "page
+// metadata accessors"): 6 instead of 12 LDS bytes per page, for documents of thousands of pages
+// (the skewed bench's long classes); replay only (no delta log, no ordinals).
 template <bool kLogT, bool kNarrowT = false, bool kBigT = false, bool kPackedT = false, int kPPT = 0, int kPHT = 0,
-          int kUTT = 0>
+          int kUTT = 0, bool kHMT = false>
 struct TierPagedT {
+    static_assert(!(kHMT && kLogT), "HBM page metadata: replay tiers only");
     static constexpr int kPP = kPPT, kPH = kPHT, kUT = kUTT;
+    static constexpr bool kHM = kHMT;
     static constexpr bool kBig = kBigT;
     static constexpr bool kPacked = kPackedT;
     // a last-tier instantiation (runtime capacities, wide masks, full table entries): the

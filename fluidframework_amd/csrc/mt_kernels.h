@@ -42,7 +42,7 @@ __device__ static void oslot_reset(const DevState &st, int doc) {
     int32_t *o = st.oslot + (size_t)doc * 2 * MT_OSLOTS;
     o[2 * lane()] = MT_OSLOT_FREE;
     o[2 * lane() + 1] = 0;
-    if (st.pgOvf && lane() < 4) ((uint32_t *)(st.pgOvf + (size_t)doc * st.OA))[lane()] = lane() ? 0u : (uint32_t)MT_OVF_HDR;
+    if (st.pgOvf && lane() < MT_OVF_HDR / 2) ((uint32_t *)(st.pgOvf + (size_t)doc * st.OA))[lane()] = lane() ? 0u : (uint32_t)MT_OVF_HDR;
 }
 
 #define MT_LOAD_FANOUT (MT_MAXN - 1)
@@ -442,7 +442,7 @@ template <class T>
 __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, int pk_ut, int pk_heap) {
     const int np = nbr(pd.up, 1);
     int ns = 0;
-    for (int q = lane(); q < np; q += MT_WAVE) ns += pd.meta[pd.up.dir[q]].nseg;
+    for (int q = lane(); q < np; q += MT_WAVE) ns += pm_nseg(pd, pd.up.dir[q]);
     ns = wave_sum(ns);
     if (lane() == 0) {
         atomicMax(st.stats + 8, (uint32_t)np);
@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(MT_WAVE) MT_PAGED_WPE k_replay_paged(DevState 
     const int doc = doc_at(st, di);
     if (st.retry[doc] != pc.stage) return;
     if (lane() == 0 && di >= sl.cnt_lo && di < sl.cnt_hi) atomicAdd(st.stats, 1u);
-    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v), T::kPacked);
+    const PagedLayout L = paged_layout(pc.PP, pc.PH, pc.UT, 0, (int)sizeof(typename T::O_v), T::kPacked, T::kHM);
     const int64_t k0 = use_resume ? st.resume[doc] : off[doc];
     const int64_t kend = off[doc + 1];
     if (k0 >= kend) {   // no message left for this document in the batch (no load / store)

@@ -11,7 +11,10 @@
 //  * page view lengths for a remote view (c, r): settled segments (seq <= minSeq and not
 //    removed after minSeq) look the same in every view (refSeq >= minSeq), so a page's view
 //    length is its observer length plus the (view - observer) difference of its unsettled
-//    segments, kept in a per-document table (<= 56 entries on C3);
+//    segments, kept in a per-document table (~200 entries on C3, each naming its page's
+//    level-1 position).  Positions are grouped in chunks of 64: the chunks' observer lengths
+//    are kept up to date, so a search sums the table's differences per chunk, picks the chunk
+//    and then the page inside it -- O(table / 64 + pages / 4096) per op, not O(pages);
 //  * the page is staged in a "window" DocT and the flat engine's own functions (op_insert,
 //    boundary, range_mark, scour_range, pack at level 0) run on it unchanged; a page that
 //    reaches MaxNodesInBlock leaf blocks is split 4|4 after the op (blk_split_up records it),
@@ -39,9 +42,17 @@
 template <class T> struct PagedDoc {
     DocT<T> w;    // window: one page staged in LDS (first member: see pdoc)
     DocT<T> up;   // levels >= 1 of the tree (level 1 = pages, counted in leaf blocks)
-    LDS_AS PageMeta *meta;    // [PP] by page id
-    LDS_AS int *pvl;          // [PP] by page id: view length of the current view
-    LDS_AS uint16_t *upage;   // [UT] unsettled-segment table: page, {len, seq, rseq, cli}, overlap
+    LDS_AS PageMeta *meta;    // [PP] by page id (T::kHM: null -- pobs / pnsb / gmeta instead)
+    LDS_AS int *pobs;         // T::kHM: [PP] observer length by page id
+    LDS_AS uint16_t *pnsb;    // T::kHM: [PP] segments | leaf blocks << 8 by page id
+    GLB_AS PageMeta *gmeta;   // T::kHM: the page metadata in HBM, where the leaf-block counts
+                              // and needsScour flags live for the launch
+    LDS_AS int *pvl;          // [PP] by level-1 position: view length in the cached view (vr, vc)
+    LDS_AS int *cob;          // T::kHM (no pvl): [PP / 64] observer length of each chunk of 64
+    LDS_AS int *cdl;          //   level-1 positions, and its (view - observer) in the cached view
+    int vgen, scr_ch;         // T::kHM: views computed so far; the chunk whose per-position
+                              //   differences w.scr holds for view number vgen (-1: none)
+    LDS_AS uint16_t *upage;   // [UT] unsettled-segment table: level-1 position, {len, seq, rseq, cli}, overlap
     LDS_AS v4i *uA;
     LDS_AS typename T::O_v *uO;
     LDS_AS uint32_t *uL, *uS, *uP;   // T::kPacked: len | seq, rseq (16 bits each, from sbase) |
@@ -66,7 +77,7 @@ template <class T> struct PagedDoc {
                               // settled segments only, whose entries contribute nothing to a view)
     int uid_lo;               // next_uid when the window was loaded: older segments of the
                               // window are already mapped to its page
-    int vvalid, vr, vc;       // pvl holds the page view lengths of view (vr, vc): boundary
+    int vvalid, vr, vc;       // cdl holds the chunk view differences of view (vr, vc): boundary
                               // splits keep them (lengths are preserved), any other change drops them
     int zuid, zpv;            // zamboni's first pop of the current message (known before the op:
                               // the op only adds heap entries above minSeq) and its page from the
@@ -75,6 +86,7 @@ template <class T> struct PagedDoc {
     int ovf_top, ovf_last, OA;   // its fill, the last message that made a set, its capacity
     int ovf_maxn, ovf_half;      // the largest set made; the half sets are appended in (the
                                  // other one receives the live sets at a compaction)
+    uint32_t ovf_made;           // units of every set made (diagnostic: reclamation)
     int press;                // a compaction left the text (4) / record (5) arena more than 7/8
                               // full: a tight launch hands the document on (pg_arena_room)
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
@@ -104,13 +116,14 @@ struct PagedCaps {
 
 struct PagedLayout {
     uint32_t offWA, offWB, offWO, offWcnt, offWflg, offWends, offWscr, offWnb;
-    uint32_t offUcnt, offUnb, offDir, offMeta, offPvl, offHeap, offUpage, offUA, offUO, offGen, offProf,
+    uint32_t offUcnt, offUnb, offDir, offMeta, offCob, offHeap, offUpage, offUA, offUO, offGen, offProf,
         total;
 };
 // ob: bytes per overlap mask in LDS (8, or 4 for a narrow tier)
 // packed: the table's entries are 12 bytes (three u32 arrays at offUA) and carry their page
+// hm: T::kHM (per page in LDS only the observer length and the segment / leaf-block counts)
 static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words, int ob,
-                                                           bool packed = false) {
+                                                           bool packed = false, bool hm = false) {
     PagedLayout L;
     uint32_t o = 0;
     L.offWA = o; o += 16u * MT_PG_SLOTS;
@@ -122,9 +135,9 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     o = (o + 7u) & ~7u;
     L.offUO = o; o += packed ? 8u * MT_PK_MASKS + MT_PK_MASKS / 8 : ((((uint32_t)ob * UT) + 7u) & ~7u);
     L.offHeap = o; o += 8u * (PH + 1);
-    L.offMeta = o; o += (uint32_t)sizeof(PageMeta) * PP;
+    L.offMeta = o; o += hm ? 6u * PP : (uint32_t)sizeof(PageMeta) * PP;
     L.offUpage = o; o += packed ? 0u : (2u * UT + 3u) & ~3u;
-    L.offPvl = o; o += 4u * PP;
+    L.offCob = o; o += hm ? 8u * (uint32_t)((PP + 63) / 64) : 4u * PP;   // cob + cdl, or pvl
     L.offWscr = o; o += 64u * 4;
     L.offWnb = o; o += MT_LV * 4;
     L.offUnb = o; o += MT_LV * 4;
@@ -173,14 +186,76 @@ __device__ __forceinline__ int pm_bcnt_l(const LDS_AS PageMeta *m, int q) { retu
 __device__ __forceinline__ int8_t pm_flg_l(const LDS_AS PageMeta *m, int q) {
     return (int8_t)((int)((m->flg2 >> (2 * q)) & 3u) - 1);
 }
+// Page metadata accessors.  A tier with T::kHM (documents of thousands of pages: LDS per page
+// sets how many share a CU) keeps only each page's segment / leaf-block counts and observer
+// length in LDS; its leaf-block counts and needsScour flags stay in HBM (read when the page is
+// staged, written back when it changes -- once per window move, not per op).
+TD int pm_nseg(const PagedDoc<T> &pd, int pg) {
+    if constexpr (T::kHM) return pd.pnsb[pg] & 0xFF;
+    else return pd.meta[pg].nseg;
+}
+TD int pm_nblk(const PagedDoc<T> &pd, int pg) {
+    if constexpr (T::kHM) return pd.pnsb[pg] >> 8;
+    else return pd.meta[pg].nblk;
+}
+TD int pm_obs(const PagedDoc<T> &pd, int pg) {
+    if constexpr (T::kHM) return pd.pobs[pg];
+    else return pd.meta[pg].obs;
+}
+TD void pm_set_ns(PagedDoc<T> &pd, int pg, int ns, int nb) {
+    if constexpr (T::kHM) {
+        pd.pnsb[pg] = (uint16_t)((ns & 0xFF) | (nb << 8));
+    } else {
+        pd.meta[pg].nseg = (uint8_t)ns;
+        pd.meta[pg].nblk = (uint8_t)nb;
+    }
+}
+TD void pm_set_nblk(PagedDoc<T> &pd, int pg, int nb) {
+    if constexpr (T::kHM) pd.pnsb[pg] = (uint16_t)((pd.pnsb[pg] & 0xFF) | (nb << 8));
+    else pd.meta[pg].nblk = (uint8_t)nb;
+}
+TD void pm_set_obs(PagedDoc<T> &pd, int pg, int obs) {
+    if constexpr (T::kHM) pd.pobs[pg] = obs;
+    else pd.meta[pg].obs = obs;
+}
+// page pg's leaf-block counts and needsScour flags (any lane; T::kHM: a global load -- after
+// gsync() + gsync_rd() when another lane may have written them)
+TD void pm_blocks(const PagedDoc<T> &pd, int pg, uint32_t &bc, uint32_t &f2) {
+    if constexpr (T::kHM) {
+        bc = pd.gmeta[pg].bc;
+        f2 = pd.gmeta[pg].flg2;
+    } else {
+        bc = pd.meta[pg].bc;
+        f2 = pd.meta[pg].flg2;
+    }
+}
+// the whole PageMeta of page pg (ordinal code paths)
+TD PageMeta pm_page(const PagedDoc<T> &pd, int pg) {
+    PageMeta m;
+    m.nseg = (uint8_t)pm_nseg(pd, pg);
+    m.nblk = (uint8_t)pm_nblk(pd, pg);
+    uint32_t bc, f2;
+    pm_blocks(pd, pg, bc, f2);
+    m.bc = bc;
+    m.flg2 = (uint16_t)f2;
+    m.obs = pm_obs(pd, pg);
+    return m;
+}
+__device__ __forceinline__ int pm_bc_of(uint32_t bc, int q) { return (int)((bc >> (4 * q)) & 15u); }
+__device__ __forceinline__ int8_t pm_fl_of(uint32_t f2, int q) { return (int8_t)((int)((f2 >> (2 * q)) & 3u) - 1); }
 // Packs the leaf-block counts / needsScour flags of page pg from lanes holding block q (v):
 // all lanes call it (wave-uniform control flow); fields are disjoint, so the sum is an OR.
 TD void pm_set_blocks(PagedDoc<T> &pd, int pg, int q, bool v, int cnt, int flg) {
     const uint32_t bc = (uint32_t)wave_sum(v ? (int)((uint32_t)cnt << (4 * q)) : 0);
     const uint32_t f2 = (uint32_t)wave_sum(v ? (flg + 1) << (2 * q) : 0);
     if (lane() == 0) {
-        pd.meta[pg].bc = bc;
-        pd.meta[pg].flg2 = (uint16_t)f2;
+        if constexpr (T::kHM) {
+            pd.gmeta[pg].bc = bc;
+            pd.gmeta[pg].flg2 = (uint16_t)f2;
+        } else {
+            pd.meta[pg].bc = bc;
+            pd.meta[pg].flg2 = (uint16_t)f2;
+        }
     }
 }
 TD bool unsettled(const v4i a, int min_seq) {
@@ -192,10 +267,10 @@ TD bool unsettled(const v4i a, int min_seq) {
 TD int pg_alloc(PagedDoc<T> &pd) {
     for (int base = 0; base < pd.PP; base += MT_WAVE) {
         const int pg = base + lane();
-        const u64 m = ballot(pg < pd.PP && pd.meta[pg].nblk == 0);
+        const u64 m = ballot(pg < pd.PP && pm_nblk(pd, pg) == 0);
         if (m) {
             const int r = base + first_lane(m);
-            if (lane() == 0) pd.meta[r].nblk = 1;
+            if (lane() == 0) pm_set_nblk(pd, r, 1);
             wsync<T>();
             return r;
         }
@@ -218,15 +293,51 @@ TD int pg_cur_pos(PagedDoc<T> &pd) {
     if (pd.cur_pos < 0) pd.cur_pos = pg_pos(pd, pd.cur);
     return pd.cur_pos;
 }
-// observer position of the window page's first segment (the pages before it in the directory)
+// observer position of the window page's first segment (the pages before it in the directory:
+// whole chunks, then the chunk's pages before it)
 TD int pg_obs_start(PagedDoc<T> &pd) {
     const int pos = pg_cur_pos(pd);
     int s = 0;
-    for (int base = 0; base < pos; base += MT_WAVE) {
-        const int q = base + lane();
-        s += q < pos ? pd.meta[pd.up.dir[q]].obs : 0;
+    if constexpr (T::kHM) {
+        const int c = pos >> 6;
+        for (int base = 0; base < c; base += MT_WAVE) s += base + lane() < c ? pd.cob[base + lane()] : 0;
+        const int q = (c << 6) + lane();
+        s += q < pos ? pm_obs(pd, pd.up.dir[q]) : 0;
+    } else {
+        for (int base = 0; base < pos; base += MT_WAVE) {
+            const int q = base + lane();
+            s += q < pos ? pm_obs(pd, pd.up.dir[q]) : 0;
+        }
     }
     return wave_sum(s);
+}
+// Chunk observer lengths from the pages (after the directory changed: page split, pack at
+// level 1, load, conversion): one wave sum per chunk of 64 positions.
+TD void pg_cob_rebuild(PagedDoc<T> &pd) {
+    pd.vvalid = 0;
+    if constexpr (!T::kHM) return;
+    const int np = nbr(pd.up, 1);
+    for (int base = 0; base < np; base += MT_WAVE) {
+        const int q = base + lane();
+        const int s = wave_sum(q < np ? pm_obs(pd, pd.up.dir[q]) : 0);
+        if (lane() == 0) pd.cob[base >> 6] = s;
+    }
+    pd.vvalid = 0;
+    wsync<T>();
+}
+// Table positions at or after `from` move by delta (a page inserted / pages replaced there).
+TD void pg_table_shift(PagedDoc<T> &pd, int from, int delta) {
+    for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
+        if constexpr (T::kPacked) {
+            const uint32_t pc = pd.uP[e];
+            const int pos = (int)(pc & 0xFFu);
+            if (pos >= from) pd.uP[e] = (pc & ~0xFFu) | (uint32_t)((pos + delta) & 0xFF);
+        } else {
+            const int pos = pd.upage[e];
+            if (pos >= from) pd.upage[e] = (uint16_t)(pos + delta);
+        }
+    }
+    wsync<T>();
 }
 
 // ------------------------------------------------------------------ segment ordinals
@@ -248,7 +359,7 @@ TD PagedDoc<T> &updoc(DocT<T> &up) {
 // canonical characters of page pg's leaf blocks and slots (nodeUpdateOrdinals of the page):
 // leaf block q of nb gets (q + 1) * width(nb) - 1, slot k of block q's c_q the same in c_q
 TD void pg_ord_canon_page(PagedDoc<T> &pd, int pg, bool root_leaf) {
-    const PageMeta m = pm_load(pd.meta + pg);
+    const PageMeta m = pm_page(pd, pg);
     const int nb = root_leaf ? 1 : (int)m.nblk;
     const int t = lane();
     int q = 0, st = 0, c = root_leaf ? (int)m.nseg : pm_bcnt(m, 0);
@@ -303,7 +414,7 @@ TD int pg_ord_of_page(PagedDoc<T> &pd, int pg, int i, int *codes) {
         int st;
         q = blk_find(w, 0, i, true, st);
     } else {
-        const PageMeta m = pm_load(pd.meta + pg);
+        const PageMeta m = pm_page(pd, pg);
         int st = 0;
         q = 0;
         while (q + 1 < (int)m.nblk && i >= st + pm_bcnt(m, q)) st += pm_bcnt(m, q++);
@@ -337,7 +448,7 @@ TD void pg_log_deferred(PagedDoc<T> &pd) {
         if (i < 0 && uid < (uint32_t)pd.UM) {
             gsync();
             pg = uni((int)pd.gumap[uid]);
-            const bool hit = lane() < (int)pd.meta[pg].nseg &&
+            const bool hit = lane() < pm_nseg(pd, pg) &&
                              (pd.gB[(size_t)pg * MT_PG_SLOTS + lane()].z & ~MT_MARKER_BIT) == uid;
             const u64 m = ballot(hit);
             i = m ? first_lane(m) : -1;
@@ -375,7 +486,7 @@ TD void pg_win_load(PagedDoc<T> &pd, int pg) {
 }
 // page pg's slots into registers (lane i: slot i)
 TD void pg_win_fetch(PagedDoc<T> &pd, int pg, v4i &a, u64 &o, v4u &b) {
-    const int n = uni(pd.meta[pg].nseg);
+    const int n = uni(pm_nseg(pd, pg));
     const int i = lane();
     if (i < n) {
         a = pd.gA[(size_t)pg * MT_PG_SLOTS + i];
@@ -383,17 +494,32 @@ TD void pg_win_fetch(PagedDoc<T> &pd, int pg, v4i &a, u64 &o, v4u &b) {
         b = pd.gB[(size_t)pg * MT_PG_SLOTS + i];
     }
 }
-TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b);
+// the page's leaf-block words: from LDS, or (T::kHM) loaded beside its slots
+TD void pg_win_fetch_blocks(PagedDoc<T> &pd, int pg, uint32_t &bc, uint32_t &f2) {
+    if constexpr (T::kHM) {
+        bc = f2 = 0;
+        if (lane() == 0) pm_blocks(pd, pg, bc, f2);
+    }
+}
+TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2);
 TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
     v4i a = v4i{0, 0, 0, 0};
     u64 o = 0;
     v4u b = v4u{0, 0, 0, 0};
+    uint32_t bc = 0, f2 = 0;
     pg_win_fetch(pd, pg, a, o, b);
-    pg_win_place(pd, pg, a, o, b);
+    pg_win_fetch_blocks(pd, pg, bc, f2);
+    pg_win_place(pd, pg, a, o, b, bc, f2);
 }
-TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b) {
+TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2) {
     DocT<T> &w = pd.w;
-    const int n = uni(pd.meta[pg].nseg), nb = uni(pd.meta[pg].nblk);
+    const int n = uni(pm_nseg(pd, pg)), nb = uni(pm_nblk(pd, pg));
+    if constexpr (T::kHM) {
+        bc = (uint32_t)bcast((int)bc, 0);
+        f2 = (uint32_t)bcast((int)f2, 0);
+    } else {
+        pm_blocks(pd, pg, bc, f2);
+    }
     const int i = lane();
     if (i < n) {
         w.A[i] = a;
@@ -401,8 +527,8 @@ TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const 
         w.Bv[i] = b;
     }
     if (i < PW_B) {
-        lvl(w, 0)[i] = i < nb ? (uint8_t)pm_bcnt_l(pd.meta + pg, i & 7) : 0;
-        w.flg[i] = i < nb ? pm_flg_l(pd.meta + pg, i & 7) : (int8_t)0;
+        lvl(w, 0)[i] = i < nb ? (uint8_t)pm_bc_of(bc, i & 7) : 0;
+        w.flg[i] = i < nb ? pm_fl_of(f2, i & 7) : (int8_t)0;
     }
     if (i == 0) {
         w.nb[0] = nb;
@@ -523,8 +649,8 @@ TD int tab_midx(PagedDoc<T> &pd, bool need) {
     }
 }
 
-// Removes the table entries of page pg (and every settled entry), then appends the
-// unsettled segments of window slots [lo, hi) under page pg2.
+// Removes the table entries of level-1 position pg (and every settled entry); pg_table_add
+// appends the unsettled segments of window slots [lo, hi) under position pg2.
 TD void pg_table_purge(PagedDoc<T> &pd, int pg) {
     const int ms = pd.w.min_seq;
     int dst = 0;
@@ -606,9 +732,8 @@ TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1, i
     const bool vb = i < 8 && b0 + i < b1;
     pm_set_blocks(pd, pg, i, vb, vb ? lvl(w, 0)[b0 + i] : 0, vb ? w.flg[b0 + i] : 0);
     if (i == 0) {
-        pd.meta[pg].nseg = (uint8_t)(hi - lo);
-        pd.meta[pg].nblk = (uint8_t)(b1 - b0);
-        pd.meta[pg].obs = obs;
+        pm_set_ns(pd, pg, hi - lo, b1 - b0);
+        pm_set_obs(pd, pg, obs);
     }
     wsync<T>();
 }
@@ -631,37 +756,25 @@ TD void pg_split_page(PagedDoc<T> &pd) {
     PG_CNT(25)
     pd.zuid = 0;   // zamboni's prefetched page may be the moved half's
     const int pos = pg_cur_pos(pd);
-    // table: the window's entries are rebuilt now (first half under this page, second half
-    // under the new one), so it never holds both a stale and a fresh copy of a segment
-    pg_table_purge(pd, pd.cur);
-    pg_table_add(pd, 0, s0, pd.cur);
+    // table: the window's entries are rebuilt now (first half at this position, second half
+    // at the new page's, pos + 1, after the later positions moved up), so it never holds both
+    // a stale and a fresh copy of a segment
+    pg_table_purge(pd, pos);
+    pg_table_shift(pd, pos + 1, 1);
+    pg_table_add(pd, 0, s0, pos);
     if (w.status) return;
-    pg_table_add(pd, s0, w.n, np);
+    pg_table_add(pd, s0, w.n, pos + 1);
     if (w.status) return;
     pd.wgrow = pd.opbound;
     pg_write_page(pd, np, s0, w.n, sp, nbk);
-    if (pd.vvalid) {   // the moved half's view length goes with it
-        const int i = lane() + s0;
-        v4i a;
-        u64 o;
-        load_ao(w, i, i < w.n, a, o);
-        const int dl = wave_sum(i < w.n ? vlen(pd.w, a, o, pd.vr, pd.vc) : 0);
-        if (lane() == 0) {
-            pd.pvl[np] = dl;
-            pd.pvl[pd.cur] -= dl;
-        }
-        wsync<T>();
-    }
+    pd.vvalid = 0;   // (the chunks are rebuilt once the directory holds the new page)
     if (ordon(w)) {
         // segment ordinals: blk_split_up re-derives the split halves' subtrees from the page
         // metadata, so this page's holds its first sp blocks already, and level 1 links the
         // new page in with the real counts (blk_split_up: sp_*)
         const bool vb = lane() < sp;
         pm_set_blocks(pd, pd.cur, lane(), vb, vb ? lvl(w, 0)[lane()] : 0, vb ? w.flg[lane()] : 0);
-        if (lane() == 0) {
-            pd.meta[pd.cur].nseg = (uint8_t)s0;
-            pd.meta[pd.cur].nblk = (uint8_t)sp;
-        }
+        if (lane() == 0) pm_set_ns(pd, pd.cur, s0, sp);
         up.sp_pg = np;
         up.sp_l = sp;
         up.sp_r = nbk - sp;
@@ -699,7 +812,8 @@ TD void pg_win_sync(PagedDoc<T> &pd) {
         up.depth = 2;
         if (lane() == 0) up.nb[2] = 0;
     }
-    if (w.pend_split) {
+    const bool split = w.pend_split != 0;
+    if (split) {
         pg_split_page(pd);
         if (w.status) return;
     }
@@ -709,20 +823,22 @@ TD void pg_win_sync(PagedDoc<T> &pd) {
     if (i < w.n) ol = obs_len(w.A[i]);
     const int obs = wave_sum(ol);
     const int pg = pd.cur;
-    // the level-1 count (== meta nblk) changes only with the page's leaf-block count: its
-    // directory position is looked up only then
-    const int old_nb = uni(pd.meta[pg].nblk);
+    // the level-1 count (== meta nblk) changes only with the page's leaf-block count, the
+    // chunk's observer length only with the page's: its directory position is looked up only
+    // then (an op's window knows it)
+    const int old_nb = uni(pm_nblk(pd, pg)), old_obs = uni(pm_obs(pd, pg));
     const bool vb = i < 8 && i < nbk;
     pm_set_blocks(pd, pg, i, vb, vb ? lvl(w, 0)[i] : 0, vb ? w.flg[i] : 0);
-    const int pos = nbk != old_nb ? pg_cur_pos(pd) : -1;
+    const int pos = (nbk != old_nb || (T::kHM && obs != old_obs)) ? pg_cur_pos(pd) : -1;
     if (i == 0) {
-        pd.meta[pg].nseg = (uint8_t)w.n;
-        pd.meta[pg].nblk = (uint8_t)nbk;
-        pd.meta[pg].obs = obs;
+        pm_set_ns(pd, pg, w.n, nbk);
+        pm_set_obs(pd, pg, obs);
         if (pos >= 0) lvl(up, 1)[pos] = (uint8_t)nbk;
+        if (T::kHM && pos >= 0 && !split) pd.cob[pos >> 6] += obs - old_obs;
     }
     pd.dirty = 1;
     wsync<T>();
+    if (split) pg_cob_rebuild(pd);
 }
 
 // Writes a dirty window back: slots and uid map to HBM, its unsettled-table entries rebuilt.
@@ -743,11 +859,12 @@ TD void pg_win_flush_impl(PagedDoc<T> &pd) {
 #ifndef MT_FLUSH_TABLE_ALWAYS
         if (pd.tdirty) {
 #endif
+            const int pos = pg_cur_pos(pd);   // (an op's window: known)
             PG_T0(33)
-            pg_table_purge(pd, pd.cur);
+            pg_table_purge(pd, pos);
             PG_T1(33)
             PG_T0(34)
-            pg_table_add(pd, 0, w.n, pd.cur);
+            pg_table_add(pd, 0, w.n, pos);
             PG_T1(34)
             if (w.status) return;
 #ifndef MT_FLUSH_TABLE_ALWAYS
@@ -768,17 +885,34 @@ TD void pg_win_switch(PagedDoc<T> &pd, int pg) {
     v4i a = v4i{0, 0, 0, 0};
     u64 o = 0;
     v4u b = v4u{0, 0, 0, 0};
+    uint32_t bc = 0, f2 = 0;
     pg_win_fetch(pd, pg, a, o, b);
+    pg_win_fetch_blocks(pd, pg, bc, f2);
     pg_win_flush(pd);
     if (pd.w.status) return;
     PG_T0(10)
-    pg_win_place(pd, pg, a, o, b);
+    pg_win_place(pd, pg, a, o, b, bc, f2);
     PG_T1(10)
 }
 
 // ------------------------------------------------------------------ page view lengths
-// pvl[page] = view length of every page for (c, r); returns the total when asked (the
-// generator draws positions from it; replay only needs pvl).
+// A page's length in view (c, r) is its observer length (PageMeta.obs) plus the (view -
+// observer) difference of its unsettled segments: their table entries, or -- when an op has
+// changed the window since it was loaded (tdirty) -- the window's own slots for its page (its
+// entries are rebuilt only at the flush; zamboni's scours change settled segments only, so a
+// window they alone touched keeps exact entries).  Level-1 positions are grouped in chunks of
+// 64 whose observer lengths (cob) are kept up to date; a view sums the differences per chunk
+// (cdl, O(table / 64)), and a search picks the chunk, then the page inside it.
+TD int pg_win_delta(PagedDoc<T> &pd, int r, int c) {
+    DocT<T> &w = pd.w;
+    const int i = lane();
+    v4i a;
+    u64 o;
+    load_ao(w, i, i < w.n, a, o);
+    return wave_sum(i < w.n ? vlen(w, a, o, r, c) - obs_len(a) : 0);
+}
+// cdl for view (r, c); returns the total length when asked (the generator draws positions
+// from it; replay only needs cdl).
 TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total);
 TD int pg_views(PagedDoc<T> &pd, int r, int c, bool total = true) {
     PG_T0(9)
@@ -789,53 +923,78 @@ TD int pg_views(PagedDoc<T> &pd, int r, int c, bool total = true) {
     pd.vc = c;
     return r_;
 }
-// pvl for view (r, c): recomputed only if a change other than a boundary split happened
+// cdl for view (r, c): recomputed only if a change other than a boundary split happened
 TD void pg_views_cached(PagedDoc<T> &pd, int r, int c) {
     if (!(pd.vvalid && pd.vr == r && pd.vc == c)) pg_views(pd, r, c, false);
 }
 TD int pg_views_impl(PagedDoc<T> &pd, int r, int c, bool total) {
     const int np = nbr(pd.up, 1);
-    int tot = 0;
-    for (int base = 0; base < np; base += MT_WAVE) {
-        const int q = base + lane();
-        if (q < np) {
-            const int pg = pd.up.dir[q];
-            pd.pvl[pg] = pd.meta[pg].obs;
+    const bool win = pd.cur >= 0 && pd.tdirty;
+    const int wpos = win ? pg_cur_pos(pd) : -1;
+    if constexpr (!T::kHM) {   // pvl[position] = observer length + differences
+        for (int base = 0; base < np; base += MT_WAVE) {
+            const int q = base + lane();
+            if (q < np) pd.pvl[q] = pm_obs(pd, pd.up.dir[q]);
         }
-    }
-    wsync<T>();
-    const int cur = pd.cur;
-    PG_T0(36)
-    for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
-        const int e = base + lane();
-        if (e < pd.ut_n) {
-            int pg;
-            v4i a;
-            u64 o;
-            tab_get(pd, e, pg, a, o);
-            const int dlt = vlen(pd.w, a, o, r, c) - obs_len(a);
-            if (dlt && pg != cur) atomicAdd((int *)(pd.pvl + pg), dlt);
+        wsync<T>();
+        PG_T0(36)
+        for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
+            const int e = base + lane();
+            if (e < pd.ut_n) {
+                int pos;
+                v4i a;
+                u64 o;
+                tab_get(pd, e, pos, a, o);
+                const int dlt = vlen(pd.w, a, o, r, c) - obs_len(a);
+                if (dlt && pos != wpos) atomicAdd((int *)(pd.pvl + pos), dlt);
+            }
         }
-    }
-    PG_T1(36)
-    if (cur >= 0) {   // the window's page: its own slots are authoritative
-        DocT<T> &w = pd.w;
-        const int i = lane();
-        v4i a;
-        u64 o;
-        load_ao(w, i, i < w.n, a, o);
-        const int dlt = wave_sum(i < w.n ? vlen(w, a, o, r, c) - obs_len(a) : 0);
-        if (i == 0) pd.pvl[cur] += dlt;
-    }
-    wsync<T>();
+        PG_T1(36)
+        if (win) {
+            const int dlt = pg_win_delta(pd, r, c);
+            if (lane() == 0) pd.pvl[wpos] += dlt;
+        }
+        wsync<T>();
 #ifndef MT_VIEWS_TOTAL
-    if (!total) return 0;
+        if (!total) return 0;
 #endif
-    for (int base = 0; base < np; base += MT_WAVE) {
-        const int q = base + lane();
-        tot += q < np ? pd.pvl[pd.up.dir[q]] : 0;
+        int tot = 0;
+        for (int base = 0; base < np; base += MT_WAVE) tot += base + lane() < np ? pd.pvl[base + lane()] : 0;
+        return wave_sum(tot);
+    } else {   // cdl[chunk] = differences
+        const int nch = (np + 63) >> 6;
+        pd.vgen = (pd.vgen + 1) & 0x7FFF;
+        for (int base = 0; base < nch; base += MT_WAVE)
+            if (base + lane() < nch) pd.cdl[base + lane()] = 0;
+        wsync<T>();
+        PG_T0(36)
+        for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
+            const int e = base + lane();
+            if (e < pd.ut_n) {
+                int pos;
+                v4i a;
+                u64 o;
+                tab_get(pd, e, pos, a, o);
+                const int dlt = vlen(pd.w, a, o, r, c) - obs_len(a);
+                if (dlt && pos != wpos) atomicAdd((int *)(pd.cdl + (pos >> 6)), dlt);
+            }
+        }
+        PG_T1(36)
+        if (win) {
+            const int dlt = pg_win_delta(pd, r, c);
+            if (lane() == 0) pd.cdl[wpos >> 6] += dlt;
+        }
+        wsync<T>();
+#ifndef MT_VIEWS_TOTAL
+        if (!total) return 0;
+#endif
+        int tot = 0;
+        for (int base = 0; base < nch; base += MT_WAVE) {
+            const int ch = base + lane();
+            tot += ch < nch ? pd.cob[ch] + pd.cdl[ch] : 0;
+        }
+        return wave_sum(tot);
     }
-    return wave_sum(tot);
 }
 // First level-1 position whose cumulative view end is >= p (strict: > p); start = its
 // view start.  -1 (start = total) if none.
@@ -846,62 +1005,163 @@ TD int pg_find(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart) {
     PG_T1(13)
     return r_;
 }
-// ... and ostart = its observer start (the same pass over the directory)
+// ... and ostart = its observer start.  The chunk first (cob + cdl), then the chunk's pages:
+// their differences from the table entries at those positions (and the window), summed in the
+// window's scratch.  Views are never negative here (a writer's view at its op's refSeq), so
+// the cumulative lengths grow with the position and the page lies in the chunk found.
 TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart) {
+    DocT<T> &w = pd.w;
     const int np = nbr(pd.up, 1);
-    int carry = 0, ocarry = 0;
-    int b0 = 0, b1 = np;
-    if constexpr (T::kPP == 0 || T::kPP > 4 * MT_WAVE) {
-        if (np > 4 * MT_WAVE) {
-            // a long directory: each lane first sums a contiguous run of ceil(np / 64) pages
-            // (plain adds), one pair of wave scans picks the run holding p, and only that run
-            // is scanned page by page below -- O(np / 64) adds instead of O(np / 64) scans
-            const int chunk = (np + MT_WAVE - 1) / MT_WAVE;
-            const int lo = min(lane() * chunk, np), hi = min(lo + chunk, np);
+    if constexpr (!T::kHM) {   // pvl by position
+        int carry = 0, ocarry = 0;
+        int b0 = 0, b1 = np;
+        if constexpr (T::kPP == 0 || T::kPP > 4 * MT_WAVE) {
+            if (np > 4 * MT_WAVE) {
+                // a long directory: each lane first sums a contiguous run of ceil(np / 64) pages
+                // (plain adds), one pair of wave scans picks the run holding p, and only that run
+                // is scanned page by page below
+                const int chunk = (np + MT_WAVE - 1) / MT_WAVE;
+                const int lo = min(lane() * chunk, np), hi = min(lo + chunk, np);
+                int v = 0, ov = 0;
+                for (int q = lo; q < hi; q++) {
+                    v += pd.pvl[q];
+                    ov += pm_obs(pd, pd.up.dir[q]);
+                }
+                const int inc = wave_scan_incl(v), oinc = wave_scan_incl(ov);
+                const u64 m = ballot(hi > lo && (strict ? inc > p : inc >= p));
+                if (!m) {
+                    start = bcast(inc, MT_WAVE - 1);
+                    ostart = bcast(oinc, MT_WAVE - 1);
+                    return -1;
+                }
+                const int fl = first_lane(m);
+                carry = bcast(inc - v, fl);
+                ocarry = bcast(oinc - ov, fl);
+                b0 = bcast(lo, fl);
+                b1 = bcast(hi, fl);
+            }
+        }
+        for (int base = b0; base < b1; base += MT_WAVE) {
+            const int q = base + lane();
             int v = 0, ov = 0;
-            for (int q = lo; q < hi; q++) {
-                const int pg = pd.up.dir[q];
-                v += pd.pvl[pg];
-                ov += pd.meta[pg].obs;
+            if (q < b1) {
+                v = pd.pvl[q];
+                ov = pm_obs(pd, pd.up.dir[q]);
+            }
+            const int inc = wave_scan_incl(v);
+            const int end = carry + inc;
+            const u64 m = ballot(q < b1 && (strict ? end > p : end >= p));
+            const int oinc = wave_scan_incl(ov);
+            if (m) {
+                const int fl = first_lane(m);
+                start = bcast(end - v, fl);
+                ostart = ocarry + bcast(oinc - ov, fl);
+                return base + fl;
+            }
+            carry += bcast(inc, MT_WAVE - 1);
+            ocarry += bcast(oinc, MT_WAVE - 1);
+        }
+        start = carry;
+        ostart = ocarry;
+        return -1;
+    } else {   // chunks, then the chunk's pages
+        const int nch = (np + 63) >> 6;
+        int carry = 0, ocarry = 0, cf = -1;
+        for (int base = 0; base < nch; base += MT_WAVE) {
+            const int ch = base + lane();
+            int v = 0, ov = 0;
+            if (ch < nch) {
+                ov = pd.cob[ch];
+                v = ov + pd.cdl[ch];
             }
             const int inc = wave_scan_incl(v), oinc = wave_scan_incl(ov);
-            const u64 m = ballot(hi > lo && (strict ? inc > p : inc >= p));
-            if (!m) {
-                start = bcast(inc, MT_WAVE - 1);
-                ostart = bcast(oinc, MT_WAVE - 1);
-                return -1;
+            const int end = carry + inc;
+            const u64 m = ballot(ch < nch && (strict ? end > p : end >= p));
+            if (m) {
+                const int fl = first_lane(m);
+                cf = base + fl;
+                carry += bcast(inc - v, fl);
+                ocarry += bcast(oinc - ov, fl);
+                break;
             }
-            const int fl = first_lane(m);
-            carry = bcast(inc - v, fl);
-            ocarry = bcast(oinc - ov, fl);
-            b0 = bcast(lo, fl);
-            b1 = bcast(hi, fl);
+            carry += bcast(inc, MT_WAVE - 1);
+            ocarry += bcast(oinc, MT_WAVE - 1);
         }
-    }
-    for (int base = b0; base < b1; base += MT_WAVE) {
-        const int q = base + lane();
+        if (cf < 0) {
+            start = carry;
+            ostart = ocarry;
+            return -1;
+        }
+        // the chunk's pages: differences per position in w.scr (64 entries), kept for the
+        // view's next search in the same chunk (boundary splits preserve them)
+        const int key = cf | ((pd.vgen & 0x7FFF) << 16);
+        if (pd.scr_ch != key) {
+            const int r = pd.vr, c = pd.vc;
+            w.scr[lane()] = 0;
+            wsync<T>();
+            const bool win = pd.cur >= 0 && pd.tdirty;
+            const int wpos = win ? pg_cur_pos(pd) : -1;
+            for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
+                const int e = base + lane();
+                if (e < pd.ut_n) {
+                    int pos;
+                    v4i a;
+                    u64 o;
+                    tab_get(pd, e, pos, a, o);
+                    if ((pos >> 6) == cf && pos != wpos) {
+                        const int dlt = vlen(pd.w, a, o, r, c) - obs_len(a);
+                        if (dlt) atomicAdd((int *)(w.scr + (pos & 63)), dlt);
+                    }
+                }
+            }
+            if (win && (wpos >> 6) == cf) {
+                const int dlt = pg_win_delta(pd, r, c);
+                if (lane() == 0) w.scr[wpos & 63] += dlt;
+            }
+            wsync<T>();
+            pd.scr_ch = key;
+        }
+        const int q = (cf << 6) + lane();
         int v = 0, ov = 0;
-        if (q < b1) {
-            const int pg = pd.up.dir[q];
-            v = pd.pvl[pg];
-            ov = pd.meta[pg].obs;
+        if (q < np) {
+            ov = pm_obs(pd, pd.up.dir[q]);
+            v = ov + w.scr[lane()];
         }
-        const int inc = wave_scan_incl(v);
+        const int inc = wave_scan_incl(v), oinc = wave_scan_incl(ov);
         const int end = carry + inc;
-        const u64 m = ballot(q < b1 && (strict ? end > p : end >= p));
-        const int oinc = wave_scan_incl(ov);
-        if (m) {
-            const int fl = first_lane(m);
-            start = bcast(end - v, fl);
-            ostart = ocarry + bcast(oinc - ov, fl);
-            return base + fl;
+        const u64 m = ballot(q < np && (strict ? end > p : end >= p));
+        if (!m) {   // (the chunk's sum and its pages' disagree: cannot happen)
+            FAIL_INTERNAL(w);
+            start = carry;
+            ostart = ocarry;
+            return -1;
         }
-        carry += bcast(inc, MT_WAVE - 1);
-        ocarry += bcast(oinc, MT_WAVE - 1);
+        const int fl = first_lane(m);
+        start = carry + bcast(inc - v, fl);
+        ostart = ocarry + bcast(oinc - ov, fl);
+        return (cf << 6) + fl;
     }
-    start = carry;
-    ostart = ocarry;
-    return -1;
+}
+// The length of level-1 position pos in the cached view (pg_views first).
+TD int pg_page_view(PagedDoc<T> &pd, int pos) {
+    if constexpr (!T::kHM) return uni(pd.pvl[pos]);
+    const int pg = uni((int)pd.up.dir[pos]);
+    const bool win = pd.cur >= 0 && pd.tdirty;
+    const int wpos = win ? pg_cur_pos(pd) : -1;
+    int d = 0;
+    for (int base = 0; base < pd.ut_n; base += MT_WAVE) {
+        const int e = base + lane();
+        if (e < pd.ut_n) {
+            int ep;
+            v4i a;
+            u64 o;
+            tab_get(pd, e, ep, a, o);
+            if (ep == pos && pos != wpos) d += vlen(pd.w, a, o, pd.vr, pd.vc) - obs_len(a);
+        }
+    }
+    d = wave_sum(d);
+    if (pos == wpos) d = pg_win_delta(pd, pd.vr, pd.vc);
+    return uni(pm_obs(pd, pg)) + d;
 }
 // the window onto level-1 position pos, whose observer start is obs_base
 // L2 warm-up of zamboni's page (the message's first pop, pd.zuid / zpv): one dword load per
@@ -932,9 +1192,11 @@ TD void pg_load_pos(PagedDoc<T> &pd, int pos, int obs_base) {
         if (zp >= 0 && zp != pg && zp < pd.PP)
             touch = pg_touch_lines(pd.gA + (size_t)zp * MT_PG_SLOTS, pd.gB + (size_t)zp * MT_PG_SLOTS,
                                    pd.gO + (size_t)zp * MT_PG_SLOTS);
+        uint32_t bc = 0, f2 = 0;
+        pg_win_fetch_blocks(pd, pg, bc, f2);
         pg_win_flush(pd);
         if (pd.w.status) return;
-        pg_win_place(pd, pg, a, o, b);
+        pg_win_place(pd, pg, a, o, b, bc, f2);
         asm volatile("" ::"v"(touch));
 #else
         pg_win_switch(pd, pg);
@@ -969,7 +1231,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
     int TB = 0, TS = 0;
     for (int j = 0; j < nch; j++) {
         TB += cntr(up, 1, c0 + j);
-        TS += uni(pd.meta[up.dir[c0 + j]].nseg);
+        TS += uni(pm_nseg(pd, up.dir[c0 + j]));
     }
     int k = TB / MT_HALF;
     if (k > MT_MAXN - 1) k = MT_MAXN - 1;
@@ -980,26 +1242,32 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
         return;
     }
     // per lane: one leaf block of the concatenation (TB <= 49): its old page / index
+    if constexpr (T::kHM) {   // the block words lane 0 wrote to HBM are read by every lane
+        gsync();
+        gsync_rd();
+    }
     const int bl = lane();
     int opg = -1, ob = 0, bseg0 = 0;   // old page, block index in it, first segment (concat)
+    uint32_t obc = 0, of2 = 0;         // its block words
     {
         int acc_b = 0, acc_s = 0;
         for (int j = 0; j < nch; j++) {
             const int pg = uni(up.dir[c0 + j]);
-            const int nb = uni(pd.meta[pg].nblk);
+            const int nb = uni(pm_nblk(pd, pg));
             if (bl >= acc_b && bl < acc_b + nb) {
                 opg = pg;
                 ob = bl - acc_b;
+                pm_blocks(pd, pg, obc, of2);
                 int s = acc_s;
-                for (int q = 0; q < ob; q++) s += pm_bcnt_l(pd.meta + pg, q);
+                for (int q = 0; q < ob; q++) s += pm_bc_of(obc, q);
                 bseg0 = s;
             }
             acc_b += nb;
-            acc_s += uni(pd.meta[pg].nseg);
+            acc_s += uni(pm_nseg(pd, pg));
         }
     }
-    const int bcnt = opg >= 0 ? pm_bcnt_l(pd.meta + opg, ob) : 0;
-    const int8_t bflg = opg >= 0 ? pm_flg_l(pd.meta + opg, ob) : (int8_t)0;
+    const int bcnt = opg >= 0 ? pm_bc_of(obc, ob) : 0;
+    const int8_t bflg = opg >= 0 ? pm_fl_of(of2, ob) : (int8_t)0;
     // new page m gets blocks [nb0(m), nb0(m) + base + (m < extra))
     auto nb0 = [&](int m) { return m * base + min(m, extra); };
     LDS_AS int32_t *newp = w.scr;   // scratch: the new page ids
@@ -1012,8 +1280,10 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
         if (lane() == 0) newp[m] = pg;
     }
     wsync<T>();
-    // table entries of the old pages go; the copy pass re-adds the unsettled ones
-    for (int j = 0; j < nch; j++) pg_table_purge(pd, uni(up.dir[c0 + j]));
+    // table entries of the old pages go (and the later positions move by k - nch); the copy
+    // pass re-adds the unsettled ones at the new pages' positions c0 .. c0 + k - 1
+    for (int j = 0; j < nch; j++) pg_table_purge(pd, c0 + j);
+    if (k != nch) pg_table_shift(pd, c0 + nch, k - nch);
     // copy, one new page at a time (<= 7 * 8 segments each)
     for (int m = 0; m < k; m++) {
         const int npg = uni(newp[m]);
@@ -1031,7 +1301,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
             int acc = 0, spg = 0, slot = 0;
             for (int j = 0; j < nch; j++) {
                 const int pg = uni(up.dir[c0 + j]);
-                const int ns = uni(pd.meta[pg].nseg);
+                const int ns = uni(pm_nseg(pd, pg));
                 if (g >= acc && g < acc + ns) {
                     spg = pg;
                     slot = g - acc;
@@ -1059,26 +1329,22 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
             pg_fail_cap(w, 8);
             return;
         }
-        if (add) tab_put(pd, pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull)), npg, a, o, mi);
+        if (add) tab_put(pd, pd.ut_n + __popcll(am & ((1ull << lane()) - 1ull)), c0 + m, a, o, mi);
         pd.ut_n += __popcll(am);
         const int obs = wave_sum(ol);
         // meta of the new page: blocks blo..bhi of the concatenation
         const bool vb = lane() >= blo && lane() < bhi;
         pm_set_blocks(pd, npg, lane() - blo, vb, bcnt, bflg);
         if (lane() == 0) {
-            pd.meta[npg].nseg = (uint8_t)(s_hi - s_lo);
-            pd.meta[npg].nblk = (uint8_t)(bhi - blo);
-            pd.meta[npg].obs = obs;
+            pm_set_ns(pd, npg, s_hi - s_lo, bhi - blo);
+            pm_set_obs(pd, npg, obs);
         }
         wsync<T>();
     }
     // free the old pages (their meta marks them empty)
     for (int j = 0; j < nch; j++) {
         const int pg = uni(up.dir[c0 + j]);
-        if (lane() == 0) {
-            pd.meta[pg].nseg = 0;
-            pd.meta[pg].nblk = 0;
-        }
+        if (lane() == 0) pm_set_ns(pd, pg, 0, 0);
         wsync<T>();
     }
     // level 1: nch entries -> k entries of base (+1) blocks; then the page ids
@@ -1091,6 +1357,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
         if (lane() == 0) up.dir[c0 + m] = (uint16_t)newp[m];
     if (lane() == 0) lvl(up, 2)[P] = (uint8_t)k;
     wsync<T>();
+    pg_cob_rebuild(pd);
     int top_l = 2, top_b = P;
     if (k < MT_HALF && 3 < up.depth) pack_counts(up, 2, P, top_l, top_b);   // counts only above level 1
     if (up.status) {
@@ -1144,7 +1411,7 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
         if (i < 0) {
             const int pg = uni(gpg);
-            if (pg == pd.cur || pg >= pd.PP || uni(pd.meta[pg].nseg) == 0) {
+            if (pg == pd.cur || pg >= pd.PP || uni(pm_nseg(pd, pg)) == 0) {
                 PG_CNT(19)
                 continue;
             }
@@ -1222,8 +1489,8 @@ TD void pg_op_insert(PagedDoc<T> &pd, const OpIn &in, const GLB_AS uint16_t *tin
         if (pos < 0 && slen == 0 && np > 0 && !(op.flags & MT_F_LOAD)) {
             pos = np - 1;
             const int lp = uni((int)pd.up.dir[pos]);
-            start -= uni(pd.pvl[lp]);
-            ostart -= uni(pd.meta[lp].obs);
+            start -= pg_page_view(pd, pos);
+            ostart -= uni(pm_obs(pd, lp));
         }
     }
     if (pos < 0) {
@@ -1320,17 +1587,24 @@ TD void pg_renumber(PagedDoc<T> &pd, bool soft = false) {
     pd.vvalid = 0;
     gsync();
     const int np = nbr(pd.up, 1);
-    // first new id of every page (pvl as scratch, by page id): segments before it + 1
+    // first new id of every page (segments before it + 1), by page id, in the text arena's
+    // idle half (scratch: only a compaction writes it, and none runs here)
+    if (2 * pd.PP > w.T_cap) {
+        pg_fail_cap(w, 4);
+        return;
+    }
+    GLB_AS int32_t *first = (GLB_AS int32_t *)text_base(w, 1 - w.text_half);
     int carry = 1;
     for (int base = 0; base < np; base += MT_WAVE) {
         const int q = base + lane();
         const int pg = q < np ? (int)pd.up.dir[q] : 0;
-        const int ns = q < np ? (int)pd.meta[pg].nseg : 0;
+        const int ns = q < np ? pm_nseg(pd, pg) : 0;
         const int inc = wave_scan_incl(ns);
-        if (q < np) pd.pvl[pg] = carry + inc - ns;
+        if (q < np) first[pg] = carry + inc - ns;
         carry += bcast(inc, MT_WAVE - 1);
     }
-    wsync<T>();
+    gsync();
+    gsync_rd();
     // heap entries: old id -> page (map) -> slot -> new id.  Ids at or above the map size
     // (a document converted from the flat tiers after many creations) are searched for.
     const int i = lane();
@@ -1342,11 +1616,11 @@ TD void pg_renumber(PagedDoc<T> &pd, bool soft = false) {
             for (int q = (mp >= 0 ? -1 : 0); q < (mp >= 0 ? 0 : np); q++) {
                 const int pg = q < 0 ? mp : uni((int)pd.up.dir[q]);
                 if (pg >= pd.PP) continue;
-                const int ns = uni((int)pd.meta[pg].nseg);
+                const int ns = uni(pm_nseg(pd, pg));
                 const bool hit = i < ns && (pd.gB[(size_t)pg * MT_PG_SLOTS + i].z & ~MT_MARKER_BIT) == uid;
                 const u64 m = ballot(hit);
                 if (m) {
-                    nid = uni(pd.pvl[pg]) + first_lane(m);
+                    nid = uni((int)first[pg]) + first_lane(m);
                     break;
                 }
             }
@@ -1356,10 +1630,10 @@ TD void pg_renumber(PagedDoc<T> &pd, bool soft = false) {
     // every slot gets its new id; the map follows
     for (int q = 0; q < np; q++) {
         const int pg = uni((int)pd.up.dir[q]);
-        const int ns = uni((int)pd.meta[pg].nseg);
+        const int ns = uni(pm_nseg(pd, pg));
         if (i < ns) {
             GLB_AS v4u *b = pd.gB + (size_t)pg * MT_PG_SLOTS + i;
-            const uint32_t nid = (uint32_t)(uni(pd.pvl[pg]) + i);
+            const uint32_t nid = (uint32_t)(uni((int)first[pg]) + i);
             v4u bv = *b;
             bv.z = nid | (bv.z & MT_MARKER_BIT);
             *b = bv;
@@ -1685,6 +1959,7 @@ TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
         d.O[i] = (typename T::O_v)(MT_OVF_BIT | (u64)(uint32_t)off);
     }
     pd.ovf_top = top + tot;
+    pd.ovf_made = (uint32_t)min((u64)pd.ovf_made + (u64)tot, (u64)0xFFFFFFFFu);
     pd.ovf_last = seq;
     d.wide = 1;
     gsync_rd();   // the new sets are read by other lanes
@@ -1746,15 +2021,17 @@ TD void pg_ovf_compact(PagedDoc<T> &pd) {
     }
 }
 // Arena units one message may take for new overflow sets: a remove makes at most one set per
-// segment it marks (<= its span), each the largest set so far (or the 63 slots' clients) plus
-// the remover and the count.  0 when no set can be made (no set exists yet and the remover has
-// or can take an overlap slot).
+// segment it marks (<= its span), each a copy of the segment's list -- an existing set (<= the
+// largest made) or the clients of its slot bits (<= the slots in use) -- plus the remover and
+// the count.  0 when no set can be made (no set exists yet and the remover has or can take an
+// overlap slot).
 TD int pg_ovf_need(PagedDoc<T> &pd, const mt_op_rec &op) {
     if (op.kind != MT_OP_REMOVE) return 0;
     DocT<T> &w = pd.w;
     if (!w.wide && !oslot_short(w, op_cli(op))) return 0;
+    const int used = __popcll(ballot(lane() < MT_OSLOT_USE && w.ocli != MT_OSLOT_FREE));
     const int span = min(max(op.pos2 - op.pos1, 0), 1 << 16);
-    return (int)min((int64_t)span * (max(pd.ovf_maxn, 63) + 2), (int64_t)1 << 30);
+    return (int)min((int64_t)span * (max(pd.ovf_maxn, used) + 2), (int64_t)1 << 30);
 }
 
 // Can this message's text / property records be placed without running out of the arenas?
@@ -1961,8 +2238,19 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
         up.ob = (GLB_AS uint16_t *)tier_paged<T::kBig>(st, doc).oU;
         up.obst = pd.PPh;
     }
-    pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
-    pd.pvl = (LDS_AS int *)(smem + L.offPvl);
+    if constexpr (T::kHM) {
+        pd.meta = nullptr;
+        pd.pobs = (LDS_AS int *)(smem + L.offMeta);
+        pd.pnsb = (LDS_AS uint16_t *)(smem + L.offMeta + 4u * pc.PP);
+        pd.gmeta = (GLB_AS PageMeta *)tier_paged<T::kBig>(st, doc).meta;
+    } else {
+        pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
+    }
+    pd.pvl = (LDS_AS int *)(smem + L.offCob);
+    pd.cob = pd.pvl;
+    pd.cdl = pd.cob + (pc.PP + 63) / 64;
+    pd.vgen = 0;
+    pd.scr_ch = -1;
     pd.upage = (LDS_AS uint16_t *)(smem + L.offUpage);
     pd.uA = (LDS_AS v4i *)(smem + L.offUA);
     pd.uO = (LDS_AS typename T::O_v *)(smem + L.offUO);
@@ -1990,12 +2278,14 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.ovf_last = 0;
     pd.ovf_maxn = 0;
     pd.ovf_half = 0;
+    pd.ovf_made = 0;
     if constexpr (T::kOvf) {
         if (pd.govf) {
             const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
             pd.ovf_top = max((int)hw[0], MT_OVF_HDR);
             pd.ovf_last = (int)hw[1];
             pd.ovf_maxn = (int)hw[2];
+            pd.ovf_made = hw[4];
             // the upper half only while the fill is above the midpoint: after a growth step
             // (the arena doubled, its contents copied at the same offsets) the sets lie in the
             // new lower half
@@ -2004,23 +2294,23 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     }
 }
 
-// Pages not in the directory are free (meta cleared; pvl as scratch marks): the HBM meta of
-// ids above a narrower launch's capacity may never have been written.
+// Pages not in the directory are free (meta cleared; a tag bit in nblk marks them first): the
+// HBM meta of ids above a narrower launch's capacity may never have been written.
 TD void pg_mark_free(PagedDoc<T> &pd) {
     const int np = nbr(pd.up, 1);
     pd.vvalid = 0;
     for (int base = 0; base < pd.PP; base += MT_WAVE)
-        if (base + lane() < pd.PP) pd.pvl[base + lane()] = 0;
+        if (base + lane() < pd.PP) pm_set_nblk(pd, base + lane(), pm_nblk(pd, base + lane()) | 0x80);
     wsync<T>();
     for (int base = 0; base < np; base += MT_WAVE)
-        if (base + lane() < np) pd.pvl[pd.up.dir[base + lane()]] = 1;
+        if (base + lane() < np) {
+            const int pg = pd.up.dir[base + lane()];
+            pm_set_nblk(pd, pg, pm_nblk(pd, pg) & 0x7F);
+        }
     wsync<T>();
     for (int base = 0; base < pd.PP; base += MT_WAVE) {
         const int pg = base + lane();
-        if (pg < pd.PP && pd.pvl[pg] == 0) {
-            pd.meta[pg].nseg = 0;
-            pd.meta[pg].nblk = 0;
-        }
+        if (pg < pd.PP && (pm_nblk(pd, pg) & 0x80)) pm_set_ns(pd, pg, 0, 0);
     }
     wsync<T>();
 }
@@ -2048,7 +2338,13 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     if (lane() < MT_LV) up.nb[lane()] = w.hp->n_blk[lane()];
     wsync<T>();
     for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = g.gdir[q];
-    {
+    if constexpr (T::kHM) {   // (the block words stay in HBM)
+        for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) {
+            const GLB_AS PageMeta *m = g.gmeta + pg;
+            pm_set_ns(pd, pg, m->nseg, m->nblk);
+            pm_set_obs(pd, pg, m->obs);
+        }
+    } else {
         GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)g.gmeta;
         LDS_AS uint32_t *lm = (LDS_AS uint32_t *)pd.meta;
         for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) lm[i] = gm[i];
@@ -2058,6 +2354,11 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = g.gcnt[l * pd.PPh + b];
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = g.gheap[i];
+    // the HBM table names page ids; LDS entries name level-1 positions: each page's position
+    // in its meta obs word for the conversion (restored from HBM below)
+    wsync<T>();
+    for (int q = lane(); q < np; q += MT_WAVE) pm_set_obs(pd, up.dir[q], q);
+    wsync<T>();
     // ut_n follows the fill, so that a mask collection inside tab_midx (tab_mgc) scans only
     // the entries written so far, not stale LDS of an earlier workgroup
     const int utn = h.pad[HDR_UTN];
@@ -2068,7 +2369,7 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         // unconditional loads (a 64-bit load under a per-lane select miscompiles: DESIGN.md
         // section 10); entry 0 exists whenever the loop runs
         const int ec = v ? e : 0;
-        const int p = g.gupage[ec];
+        const int p = pm_obs(pd, g.gupage[ec]);   // (its position)
         const v4i a = g.guA[ec];
         const u64 o = g.guO[ec];
         const int mi = tab_midx(pd, v && o != 0);
@@ -2077,7 +2378,10 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         pd.ut_n = min(base + MT_WAVE, utn);
     }
     wsync<T>();
+    for (int q = lane(); q < np; q += MT_WAVE) pm_set_obs(pd, up.dir[q], g.gmeta[up.dir[q]].obs);
+    wsync<T>();
     pg_mark_free(pd);
+    pg_cob_rebuild(pd);
     return true;
 }
 
@@ -2093,14 +2397,24 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
     if (failed) w.status = failed;
     w.oslot[2 * lane()] = w.ocli;
     if constexpr (T::kOvf) {
-        if (pd.govf && lane() < 4)
+        if (pd.govf && lane() < MT_OVF_HDR / 2)
             ((GLB_AS uint32_t *)pd.govf)[lane()] =
-                (uint32_t)(lane() == 0 ? pd.ovf_top : (lane() == 1 ? pd.ovf_last : (lane() == 2 ? pd.ovf_maxn : pd.ovf_half)));
+                lane() == 0 ? (uint32_t)pd.ovf_top
+                            : (lane() == 1 ? (uint32_t)pd.ovf_last
+                                           : (lane() == 2 ? (uint32_t)pd.ovf_maxn
+                                                          : (lane() == 3 ? (uint32_t)pd.ovf_half : pd.ovf_made)));
     }
     wsync<T>();
     const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) g.gdir[q] = up.dir[q];
-    {
+    if constexpr (T::kHM) {   // (the block words are in HBM already)
+        for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) {
+            GLB_AS PageMeta *m = g.gmeta + pg;
+            m->nseg = (uint8_t)pm_nseg(pd, pg);
+            m->nblk = (uint8_t)pm_nblk(pd, pg);
+            m->obs = pm_obs(pd, pg);
+        }
+    } else {
         GLB_AS uint32_t *gm = (GLB_AS uint32_t *)g.gmeta;
         LDS_AS const uint32_t *lm = (LDS_AS const uint32_t *)pd.meta;
         for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) gm[i] = lm[i];
@@ -2115,7 +2429,7 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
         v4i a;
         u64 o;
         tab_get(pd, e, p, a, o);
-        g.gupage[e] = p;
+        g.gupage[e] = up.dir[p];   // (LDS entries name positions; HBM ones page ids)
         g.guA[e] = a;
         g.guO[e] = o;
     }
@@ -2123,7 +2437,7 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
 #pragma unroll
     for (int l = 0; l < MT_LV; l++) nbl[l] = nbr(up, l);
     int nseg = 0;
-    for (int q = lane(); q < np; q += MT_WAVE) nseg += pd.meta[up.dir[q]].nseg;
+    for (int q = lane(); q < np; q += MT_WAVE) nseg += pm_nseg(pd, up.dir[q]);
     nseg = wave_sum(nseg);
     if (lane() == 0) {
         DocHdr h;
@@ -2223,10 +2537,7 @@ TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
         for (int b = lane(); b < nl; b += MT_WAVE) lvl(up, l)[b] = fc[l * B + b];
     }
     for (int i = 1 + lane(); i <= h.heap_n; i += MT_WAVE) w.heap[i] = fH[i];
-    for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) {
-        pd.meta[pg].nseg = 0;
-        pd.meta[pg].nblk = 0;
-    }
+    for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) pm_set_ns(pd, pg, 0, 0);
     pd.ut_n = 0;
     wsync<T>();
     int lb = 0, s = 0;
@@ -2274,6 +2585,7 @@ TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
         s += ns;
     }
     pg_mark_free(pd);
+    pg_cob_rebuild(pd);
     pd.cur = -1;
     pd.wgrow = pd.opbound = 0;
     if (ordon(w)) {

@@ -828,7 +828,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
             return nullptr;
         }
         if (lb > 64 * 1024) {
-            const void *ks[] = {MTK(P_LOG), MTK(P_FULL),
+            const void *ks[] = {MTK(P_LOG), MTK(P_FULL), MTK(P_HM),
                                 MTK(GP_FULL),
                                 MTK(P_NARROW_LOG),
                                 MTK(P_NARROW),
@@ -1099,9 +1099,17 @@ __global__ void k_mark_big(DevState st, const int64_t *off, int resume_set) {
 }
 // One paged launch over every document (those not at stage pc.stage exit at once); big: the
 // documents of the big region (the growth step's launches).
+// Documents of many pages replay with their leaf-block words in HBM (TierPagedT kHM: 6 LDS
+// bytes per page instead of 12, so more of them share a CU); the bench's C3 / C4 documents
+// (< 300 pages) keep them in LDS.
+#define MT_HM_PAGES 512
+static bool use_hm(const mt_handle *h, const PagedCaps &pc) {
+    return !pc.packed && !pc.narrow && !h->st.DL && pc.PP >= MT_HM_PAGES;
+}
 static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl,
                         bool big = false) {
-    const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8, pc.packed != 0).total;
+    const bool hm = use_hm(h, pc);
+    const size_t lb = paged_layout(pc.PP, pc.PH, pc.UT, 0, pc.narrow ? 4 : 8, pc.packed != 0, hm).total;
     const dim3 g(h->n_docs), blk(MT_WAVE);
     // the bench's C3 tight tier with its capacities fixed at compile time (same code, constant
     // LDS layout: bench.capacities)
@@ -1120,6 +1128,9 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     else if (big && h->st.DL)
         launch_replay_paged(MTK(P_BIG_LOG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
+    else if (big && hm)
+        launch_replay_paged(MTK(P_BIG_HM), g, blk, lb, h->stream, h->st, b->ops,
+                           b->off, b->text, b->props, res, pc, sl);
     else if (big)
         launch_replay_paged(MTK(P_BIG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
@@ -1132,6 +1143,9 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     else if (pc.narrow)
         launch_replay_paged(MTK(P_NARROW), g, blk, lb, h->stream, h->st, b->ops, b->off,
                            b->text, b->props, res, pc, sl);
+    else if (hm)
+        launch_replay_paged(MTK(P_HM), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
+                           b->props, res, pc, sl);
     else
         launch_replay_paged(MTK(P_FULL), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
                            b->props, res, pc, sl);
@@ -1402,7 +1416,7 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
     const size_t lb = paged_layout(c.PP, c.PH, c.UT, 0, 8).total;
     if (lb > 64 * 1024) {
         const void *ks[] = {MTK(P_BIG_LOG),
-                            MTK(P_BIG)};
+                            MTK(P_BIG), MTK(P_BIG_HM)};
         for (const void *k : ks) HIPCHK(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
     }
     return 0;
@@ -2699,9 +2713,9 @@ int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out) {
     HostDoc hd;
     int rc = fetch_doc(h, doc, hd, false, false);
     if (rc) return rc;
-    for (int k = 0; k < 5; k++) out[k] = 0;
+    for (int k = 0; k < 6; k++) out[k] = 0;
     if (hd.ovf.size() < MT_OVF_HDR) return 0;
-    uint32_t w[4];
+    uint32_t w[MT_OVF_HDR / 2];
     memcpy(w, hd.ovf.data(), sizeof(w));
     const int OA = (int)hd.ovf.size(), mid = (OA / 2) & ~7;
     const int half = (w[3] & 1) && (int)w[0] > mid ? 1 : 0;
@@ -2715,6 +2729,7 @@ int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out) {
     std::sort(offs.begin(), offs.end());
     offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
     for (uint32_t off : offs) out[4] += off < hd.ovf.size() ? (int)hd.ovf[off] + 1 : 0;
+    out[5] = (int)std::min<uint32_t>(w[4], INT32_MAX);
     return 0;
 }
 

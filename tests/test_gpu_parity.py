@@ -487,15 +487,15 @@ def test_gpu_overlap_beyond_the_slots_matches_reference(tier):
 @pytest.mark.parametrize("tier", ["paged", "tight", "grow"])
 def test_gpu_overflow_sets_are_reclaimed(tier):
     """removedClientOverlap lists leave with their segments (zamboni unlinks or merges them,
-    MT/mergeTree.ts:1322-1398).  Over a 30k-message 200-writer lag-400 document
-    (tests/golden/ref_wide_long, made by the reference) thousands of overflow sets are made,
-    few live at once: the arena's halves are compacted (pg_ovf_compact) so that a 2048-unit
-    arena serves the whole document -- its fill stays bounded by the live sets, not by every
-    set made -- and the document equals the reference's."""
+    MT/mergeTree.ts:1322-1398).  Over a 30k-message document with 400 writers at lag 800
+    (tests/golden/ref_wide_long, made by the reference) overflow sets are made all along, few
+    live at once: the arena's halves are compacted (pg_ovf_compact), so it ends far smaller than
+    the sets made over the document's life -- its fill bounded by the live sets -- and the
+    document equals the reference's."""
     fx = gu.load("ref_wide_long")
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
-    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 21, overlap_arena_capacity=2048,
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 21, overlap_arena_capacity=512,
                     **OVF_TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
@@ -504,8 +504,8 @@ def test_gpu_overflow_sets_are_reclaimed(tier):
         assert not gu.compare_oracle(_gpu_outputs(mt, i), gu.expected(doc, interner)), doc["doc"]
         ar = mt.get_overlap_arena(i)
         print(tier, ar, mt.last_grown())
-        assert ar["largest_set"] > 63          # sets were made (more than the 63 slots)
-        assert ar["capacity"] <= 8192, ar       # compacted: at most two doublings of 2048
+        assert ar["largest_set"] >= 2                 # sets were made (clients beyond the 63 slots)
+        assert ar["made"] > 2 * ar["capacity"], ar    # far more than the arena ever held: reclaimed
         assert ar["live_units"] <= ar["fill"]
 
 
