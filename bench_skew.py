@@ -147,10 +147,14 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
                 picks.append((ri, j, int(r["idx"][j])))
         threads = args.cpu_threads or bench.host_cores()
 
+        t_o = time.time()
+
         def gen(pk):
             _, _, d = pk
             g = pyoracle.generate(dict(cfg, ops=int(lens[d])), int(ids[d]), keep=True)
             g["sum"] = g.pop("doc").outputs()["checksum"]
+            print(f"c3skew: oracle document {int(ids[d])} ({int(lens[d])} messages) done ({time.time() - t_o:.1f} s)",
+                  file=sys.stderr, flush=True)
             return g
 
         # longest first, so the 200k documents do not start last
@@ -184,6 +188,7 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
                       seed=np.concatenate(seed), doc_off=np.asarray(doc_off, dtype=np.int64),
                       seed_off=np.asarray(seed_off, dtype=np.int64))
         used = min(threads, len(picks))
+        print(f"c3skew: CPU baseline replay of {len(picks)} documents on {used} threads", file=sys.stderr, flush=True)
         t_c = time.perf_counter()
         osums, ost = pyoracle.replay_batch(arrays, threads=used)
         t_c = time.perf_counter() - t_c

@@ -2033,6 +2033,45 @@ TD int pg_ovf_need(PagedDoc<T> &pd, const mt_op_rec &op) {
     const int span = min(max(op.pos2 - op.pos1, 0), 1 << 16);
     return (int)min((int64_t)span * (max(pd.ovf_maxn, used) + 2), (int64_t)1 << 30);
 }
+// The same bound counted instead of assumed, for when the first would not fit: a set is made
+// only for a segment some concurrent remover already removed (removedSeq above the remover's
+// refSeq >= minSeq, so an unsettled segment: an unsettled-table entry, or a row of the page in
+// the window when that page changed since its entries were written) that the remover still
+// sees (its view length > 0), so on a page its view [pos1, pos2) reaches; at most one per
+// segment (a split segment's set goes to the piece inside the range), of its list's size + 2.
+TD int ovf_units_of(PagedDoc<T> &pd, const v4i &a, u64 o, int r, int c) {
+    if (a.z == MT_RSEQ_NONE || vlen(pd.w, a, o, r, c) <= 0) return 0;
+    return ((o & MT_OVF_BIT) ? (int)pd.govf[(uint32_t)o] : __popcll(o)) + 2;
+}
+TD int pg_ovf_need_counted(PagedDoc<T> &pd, const mt_op_rec &op) {
+    DocT<T> &w = pd.w;
+    const int r = op.ref_seq, c = op_cli(op);
+    w.ocs = oslot_of(w, c);   // (as pg_apply_op_impl sets it: the view's own slot)
+    pg_views_cached(pd, r, c);
+    int start, ostart;
+    const int np = nbr(pd.up, 1);
+    const int p1 = pg_find(pd, op.pos1, true, start, ostart);
+    int p2 = pg_find(pd, op.pos2, false, start, ostart);
+    if (w.status) return 1 << 30;
+    if (p1 < 0) return 0;   // (the range starts past the end: nothing to mark)
+    if (p2 < 0) p2 = np - 1;
+    const int wpos = pd.cur >= 0 && pd.tdirty ? pg_cur_pos(pd) : -1;   // (as pg_views_impl)
+    int s = 0;
+    for (int e = lane(); e < pd.ut_n; e += MT_WAVE) {
+        int pos;
+        v4i a;
+        u64 o;
+        tab_get(pd, e, pos, a, o);
+        if (pos >= p1 && pos <= p2 && pos != wpos) s += ovf_units_of(pd, a, o, r, c);
+    }
+    if (wpos >= p1 && wpos <= p2) {
+        v4i a;
+        u64 o;
+        load_ao(w, lane(), lane() < w.n, a, o);
+        if (lane() < w.n) s += ovf_units_of(pd, a, o, r, c);
+    }
+    return wave_sum(s);
+}
 
 // Can this message's text / property records be placed without running out of the arenas?
 // (TextSegment.append and property sets are unbounded in the reference, MT/textSegment.ts:74-85.)
@@ -2058,7 +2097,8 @@ TD bool pg_arena_room(PagedDoc<T> &pd, const mt_op_rec &op, const PagedCaps &pc)
             // into the other half first when they would not, and the document is handed to
             // the growth step (which doubles the arena) when even that leaves too little room
             // -- so ovf_mark never runs out in the middle of a message
-            const int need = pg_ovf_need(pd, op);
+            int need = pg_ovf_need(pd, op);
+            if (need > 0 && pd.ovf_top + need > ovf_half_end(pd)) need = min(need, pg_ovf_need_counted(pd, op));
             if (need > 0 && pd.ovf_top + need > ovf_half_end(pd)) {
                 pg_ovf_compact(pd);
                 if (w.status) return true;   // (failed: the loop stops)

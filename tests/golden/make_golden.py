@@ -41,10 +41,10 @@ FIXTURES = {
     # 200 writers, lag 400: ~80 clients' overlapping removes unsettled at once -- more than the
     # 63 overlap slots, so the device keeps overflow sets (MT_OVF_BIT)
     "ref_wide400": ("c4", {"ops": 3000, "writers": 200, "lag": 400, "seed": 7272}, 2),
-    # 400 writers, lag 800, removes 0.45, over 30k messages: overflow sets made all along the
+    # 200 writers, lag 400, removes 0.5, over 60k messages: overflow sets made all along the
     # document's life, few live at once (the arena is compacted, not grown without bound)
-    "ref_wide_long": ("c4", {"ops": 30000, "writers": 400, "lag": 800, "seed": 7373, "p_insert": 0.4,
-                             "p_remove": 0.45}, 1),
+    "ref_wide_long": ("c4", {"ops": 60000, "writers": 200, "lag": 400, "seed": 7373, "p_insert": 0.4,
+                             "p_remove": 0.5}, 1),
     # a long-lived document: 30k messages (~45k segment ids created, ~12k live segments)
     "ref_c3_long": ("c3", {"ops": 30000}, 2),
     # the long classes of the skewed bench (c3skew: 40k-200k messages; 1.5k-3.2k pages): one

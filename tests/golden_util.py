@@ -24,7 +24,7 @@ LONG_FIXTURES = ["ref_c3_long"]
 XL_FIXTURES = ["ref_c3_60k", "ref_c3_xl"]
 # more clients' overlapping removes unsettled at once than the 63 overlap slots (paged tiers:
 # overflow sets)
-WIDE_FIXTURES = ["ref_wide400"]
+WIDE_FIXTURES = ["ref_wide400", "ref_wide_long"]
 SNAP_FIXTURES = ["ref_snap", "ref_snap_body", "ref_snap_files"]
 # error model (tests/golden/make_golden.py --errors): the reference's throw -> mt_doc_status
 ERROR_STATUS = {

@@ -487,7 +487,7 @@ def test_gpu_overlap_beyond_the_slots_matches_reference(tier):
 @pytest.mark.parametrize("tier", ["paged", "tight", "grow"])
 def test_gpu_overflow_sets_are_reclaimed(tier):
     """removedClientOverlap lists leave with their segments (zamboni unlinks or merges them,
-    MT/mergeTree.ts:1322-1398).  Over a 30k-message document with 400 writers at lag 800
+    MT/mergeTree.ts:1322-1398).  Over a 60k-message document with 200 writers at lag 400
     (tests/golden/ref_wide_long, made by the reference) overflow sets are made all along, few
     live at once: the arena's halves are compacted (pg_ovf_compact), so it ends far smaller than
     the sets made over the document's life -- its fill bounded by the live sets -- and the
