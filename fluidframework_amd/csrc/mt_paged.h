@@ -42,11 +42,10 @@
 template <class T> struct PagedDoc {
     DocT<T> w;    // window: one page staged in LDS (first member: see pdoc)
     DocT<T> up;   // levels >= 1 of the tree (level 1 = pages, counted in leaf blocks)
-    LDS_AS PageMeta *meta;    // [PP] by page id (T::kHM: null -- pobs / pnsb / gmeta instead)
-    LDS_AS int *pobs;         // T::kHM: [PP] observer length by page id
-    LDS_AS uint16_t *pnsb;    // T::kHM: [PP] segments | leaf blocks << 8 by page id
-    GLB_AS PageMeta *gmeta;   // T::kHM: the page metadata in HBM, where the leaf-block counts
-                              // and needsScour flags live for the launch
+    LDS_AS PageMeta *meta;    // [PP] by page id (T::kHM: null -- pst / gmeta instead)
+    LDS_AS uint8_t *pst;      // T::kHM: [PP] by page id: segments | 0x80 while in use
+    GLB_AS PageMeta *gmeta;   // T::kHM: the page metadata in HBM, where it lives for the launch
+                              // (observer length, leaf-block counts, needsScour flags)
     LDS_AS int *pvl;          // [PP] by level-1 position: view length in the cached view (vr, vc)
     LDS_AS int *cob;          // T::kHM (no pvl): [PP / 64] observer length of each chunk of 64
     LDS_AS int *cdl;          //   level-1 positions, and its (view - observer) in the cached view
@@ -92,6 +91,10 @@ template <class T> struct PagedDoc {
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
                               // window's entries since they were last rebuilt); the current
                               // message's bound (pg_room)
+    LDS_AS int *sob;          // T::kHM: observer lengths of chunk sob_ch's 64 positions (a
+    int sob_ch;               //   cache of the HBM values, kept in step by pg_win_sync; -1: none)
+    int wnb, wobs;            // T::kHM: leaf blocks / observer length of the window's page as
+                              //   its meta in HBM holds them (uniform)
 };
 
 // LDS capacities of one paged launch.  The HBM arrays are sized for the handle's paged
@@ -121,7 +124,7 @@ struct PagedLayout {
 };
 // ob: bytes per overlap mask in LDS (8, or 4 for a narrow tier)
 // packed: the table's entries are 12 bytes (three u32 arrays at offUA) and carry their page
-// hm: T::kHM (per page in LDS only the observer length and the segment / leaf-block counts)
+// hm: T::kHM (per page in LDS only its segment count; its metadata stays in HBM)
 static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words, int ob,
                                                            bool packed = false, bool hm = false) {
     PagedLayout L;
@@ -135,9 +138,9 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     o = (o + 7u) & ~7u;
     L.offUO = o; o += packed ? 8u * MT_PK_MASKS + MT_PK_MASKS / 8 : ((((uint32_t)ob * UT) + 7u) & ~7u);
     L.offHeap = o; o += 8u * (PH + 1);
-    L.offMeta = o; o += hm ? 6u * PP : (uint32_t)sizeof(PageMeta) * PP;
+    L.offMeta = o; o += hm ? ((uint32_t)PP + 7u) & ~7u : (uint32_t)sizeof(PageMeta) * PP;
     L.offUpage = o; o += packed ? 0u : (2u * UT + 3u) & ~3u;
-    L.offCob = o; o += hm ? 8u * (uint32_t)((PP + 63) / 64) : 4u * PP;   // cob + cdl, or pvl
+    L.offCob = o; o += hm ? 8u * (uint32_t)((PP + 63) / 64) + 4u * 64 : 4u * PP;   // cob + cdl + sob, or pvl
     L.offWscr = o; o += 64u * 4;
     L.offWnb = o; o += MT_LV * 4;
     L.offUnb = o; o += MT_LV * 4;
@@ -190,32 +193,48 @@ __device__ __forceinline__ int8_t pm_flg_l(const LDS_AS PageMeta *m, int q) {
 // sets how many share a CU) keeps only each page's segment / leaf-block counts and observer
 // length in LDS; its leaf-block counts and needsScour flags stay in HBM (read when the page is
 // staged, written back when it changes -- once per window move, not per op).
+// T::kHM: only the segment count (and an in-use bit) of a page is in LDS; its observer length
+// and leaf-block count are global loads (after gsync_rd() where another lane wrote them).
 TD int pm_nseg(const PagedDoc<T> &pd, int pg) {
-    if constexpr (T::kHM) return pd.pnsb[pg] & 0xFF;
+    if constexpr (T::kHM) return pd.pst[pg] & 0x7F;
     else return pd.meta[pg].nseg;
 }
 TD int pm_nblk(const PagedDoc<T> &pd, int pg) {
-    if constexpr (T::kHM) return pd.pnsb[pg] >> 8;
-    else return pd.meta[pg].nblk;
+    if constexpr (T::kHM) {
+        gsync_rd();
+        return pd.gmeta[pg].nblk;
+    } else {
+        return pd.meta[pg].nblk;
+    }
 }
 TD int pm_obs(const PagedDoc<T> &pd, int pg) {
-    if constexpr (T::kHM) return pd.pobs[pg];
-    else return pd.meta[pg].obs;
+    if constexpr (T::kHM) {
+        gsync_rd();
+        return pd.gmeta[pg].obs;
+    } else {
+        return pd.meta[pg].obs;
+    }
 }
 TD void pm_set_ns(PagedDoc<T> &pd, int pg, int ns, int nb) {
     if constexpr (T::kHM) {
-        pd.pnsb[pg] = (uint16_t)((ns & 0xFF) | (nb << 8));
+        pd.pst[pg] = (uint8_t)(nb ? (ns & 0x7F) | 0x80 : 0);
+        pd.gmeta[pg].nseg = (uint8_t)ns;
+        pd.gmeta[pg].nblk = (uint8_t)nb;
     } else {
         pd.meta[pg].nseg = (uint8_t)ns;
         pd.meta[pg].nblk = (uint8_t)nb;
     }
 }
 TD void pm_set_nblk(PagedDoc<T> &pd, int pg, int nb) {
-    if constexpr (T::kHM) pd.pnsb[pg] = (uint16_t)((pd.pnsb[pg] & 0xFF) | (nb << 8));
-    else pd.meta[pg].nblk = (uint8_t)nb;
+    if constexpr (T::kHM) {
+        pd.pst[pg] = (uint8_t)(nb ? (pd.pst[pg] & 0x7F) | 0x80 : 0);
+        pd.gmeta[pg].nblk = (uint8_t)nb;
+    } else {
+        pd.meta[pg].nblk = (uint8_t)nb;
+    }
 }
 TD void pm_set_obs(PagedDoc<T> &pd, int pg, int obs) {
-    if constexpr (T::kHM) pd.pobs[pg] = obs;
+    if constexpr (T::kHM) pd.gmeta[pg].obs = obs;
     else pd.meta[pg].obs = obs;
 }
 // page pg's leaf-block counts and needsScour flags (any lane; T::kHM: a global load -- after
@@ -267,7 +286,10 @@ TD bool unsettled(const v4i a, int min_seq) {
 TD int pg_alloc(PagedDoc<T> &pd) {
     for (int base = 0; base < pd.PP; base += MT_WAVE) {
         const int pg = base + lane();
-        const u64 m = ballot(pg < pd.PP && pm_nblk(pd, pg) == 0);
+        bool fr;
+        if constexpr (T::kHM) fr = pg < pd.PP && pd.pst[pg] == 0;
+        else fr = pg < pd.PP && pm_nblk(pd, pg) == 0;
+        const u64 m = ballot(fr);
         if (m) {
             const int r = base + first_lane(m);
             if (lane() == 0) pm_set_nblk(pd, r, 1);
@@ -299,6 +321,7 @@ TD int pg_obs_start(PagedDoc<T> &pd) {
     const int pos = pg_cur_pos(pd);
     int s = 0;
     if constexpr (T::kHM) {
+        gsync_rd();
         const int c = pos >> 6;
         for (int base = 0; base < c; base += MT_WAVE) s += base + lane() < c ? pd.cob[base + lane()] : 0;
         const int q = (c << 6) + lane();
@@ -316,6 +339,8 @@ TD int pg_obs_start(PagedDoc<T> &pd) {
 TD void pg_cob_rebuild(PagedDoc<T> &pd) {
     pd.vvalid = 0;
     if constexpr (!T::kHM) return;
+    pd.sob_ch = -1;
+    gsync_rd();
     const int np = nbr(pd.up, 1);
     for (int base = 0; base < np; base += MT_WAVE) {
         const int q = base + lane();
@@ -494,30 +519,47 @@ TD void pg_win_fetch(PagedDoc<T> &pd, int pg, v4i &a, u64 &o, v4u &b) {
         b = pd.gB[(size_t)pg * MT_PG_SLOTS + i];
     }
 }
-// the page's leaf-block words: from LDS, or (T::kHM) loaded beside its slots
-TD void pg_win_fetch_blocks(PagedDoc<T> &pd, int pg, uint32_t &bc, uint32_t &f2) {
+// the page's leaf-block words: from LDS, or (T::kHM) loaded beside its slots with its
+// leaf-block count (f2 bits 16..23) and observer length (ob), lane 0
+TD void pg_win_fetch_blocks(PagedDoc<T> &pd, int pg, uint32_t &bc, uint32_t &f2, int &ob) {
     if constexpr (T::kHM) {
         bc = f2 = 0;
-        if (lane() == 0) pm_blocks(pd, pg, bc, f2);
+        ob = 0;
+        if (lane() == 0) {
+            gsync_rd();
+            const GLB_AS PageMeta *m = pd.gmeta + pg;
+            bc = m->bc;
+            f2 = (uint32_t)m->flg2 | ((uint32_t)m->nblk << 16);
+            ob = m->obs;
+        }
     }
 }
-TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2);
+TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2,
+                     int ob);
 TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
     v4i a = v4i{0, 0, 0, 0};
     u64 o = 0;
     v4u b = v4u{0, 0, 0, 0};
     uint32_t bc = 0, f2 = 0;
+    int ob = 0;
     pg_win_fetch(pd, pg, a, o, b);
-    pg_win_fetch_blocks(pd, pg, bc, f2);
-    pg_win_place(pd, pg, a, o, b, bc, f2);
+    pg_win_fetch_blocks(pd, pg, bc, f2, ob);
+    pg_win_place(pd, pg, a, o, b, bc, f2, ob);
 }
-TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2) {
+TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2,
+                     int ob) {
     DocT<T> &w = pd.w;
-    const int n = uni(pm_nseg(pd, pg)), nb = uni(pm_nblk(pd, pg));
+    const int n = uni(pm_nseg(pd, pg));
+    int nb;
     if constexpr (T::kHM) {
         bc = (uint32_t)bcast((int)bc, 0);
         f2 = (uint32_t)bcast((int)f2, 0);
+        nb = (int)(f2 >> 16);
+        f2 &= 0xFFFFu;
+        pd.wnb = nb;
+        pd.wobs = bcast(ob, 0);
     } else {
+        nb = uni(pm_nblk(pd, pg));
         pm_blocks(pd, pg, bc, f2);
     }
     const int i = lane();
@@ -735,6 +777,15 @@ TD void pg_write_page(PagedDoc<T> &pd, int pg, int lo, int hi, int b0, int b1, i
         pm_set_ns(pd, pg, hi - lo, b1 - b0);
         pm_set_obs(pd, pg, obs);
     }
+    if constexpr (T::kHM) {
+        if (pg == pd.cur) {
+            if (obs != pd.wobs) pd.sob_ch = -1;   // (pg_win_sync keeps the cache otherwise)
+            pd.wnb = b1 - b0;
+            pd.wobs = obs;
+        } else {
+            pd.sob_ch = -1;
+        }
+    }
     wsync<T>();
 }
 
@@ -826,7 +877,14 @@ TD void pg_win_sync(PagedDoc<T> &pd) {
     // the level-1 count (== meta nblk) changes only with the page's leaf-block count, the
     // chunk's observer length only with the page's: its directory position is looked up only
     // then (an op's window knows it)
-    const int old_nb = uni(pm_nblk(pd, pg)), old_obs = uni(pm_obs(pd, pg));
+    int old_nb, old_obs;
+    if constexpr (T::kHM) {
+        old_nb = pd.wnb;
+        old_obs = pd.wobs;
+    } else {
+        old_nb = uni(pm_nblk(pd, pg));
+        old_obs = uni(pm_obs(pd, pg));
+    }
     const bool vb = i < 8 && i < nbk;
     pm_set_blocks(pd, pg, i, vb, vb ? lvl(w, 0)[i] : 0, vb ? w.flg[i] : 0);
     const int pos = (nbk != old_nb || (T::kHM && obs != old_obs)) ? pg_cur_pos(pd) : -1;
@@ -834,7 +892,14 @@ TD void pg_win_sync(PagedDoc<T> &pd) {
         pm_set_ns(pd, pg, w.n, nbk);
         pm_set_obs(pd, pg, obs);
         if (pos >= 0) lvl(up, 1)[pos] = (uint8_t)nbk;
-        if (T::kHM && pos >= 0 && !split) pd.cob[pos >> 6] += obs - old_obs;
+        if (T::kHM && pos >= 0 && !split) {
+            pd.cob[pos >> 6] += obs - old_obs;
+            if ((pos >> 6) == pd.sob_ch) pd.sob[pos & 63] = obs;
+        }
+    }
+    if constexpr (T::kHM) {
+        pd.wnb = nbk;
+        pd.wobs = obs;
     }
     pd.dirty = 1;
     wsync<T>();
@@ -886,12 +951,13 @@ TD void pg_win_switch(PagedDoc<T> &pd, int pg) {
     u64 o = 0;
     v4u b = v4u{0, 0, 0, 0};
     uint32_t bc = 0, f2 = 0;
+    int ob = 0;
     pg_win_fetch(pd, pg, a, o, b);
-    pg_win_fetch_blocks(pd, pg, bc, f2);
+    pg_win_fetch_blocks(pd, pg, bc, f2, ob);
     pg_win_flush(pd);
     if (pd.w.status) return;
     PG_T0(10)
-    pg_win_place(pd, pg, a, o, b, bc, f2);
+    pg_win_place(pd, pg, a, o, b, bc, f2, ob);
     PG_T1(10)
 }
 
@@ -1122,9 +1188,14 @@ TD int pg_find_impl(PagedDoc<T> &pd, int p, bool strict, int &start, int &ostart
             pd.scr_ch = key;
         }
         const int q = (cf << 6) + lane();
+        if (pd.sob_ch != cf) {   // the chunk's observer lengths from HBM, kept for its next search
+            pd.sob[lane()] = q < np ? pm_obs(pd, pd.up.dir[q]) : 0;
+            pd.sob_ch = cf;
+            wsync<T>();
+        }
         int v = 0, ov = 0;
         if (q < np) {
-            ov = pm_obs(pd, pd.up.dir[q]);
+            ov = pd.sob[lane()];
             v = ov + w.scr[lane()];
         }
         const int inc = wave_scan_incl(v), oinc = wave_scan_incl(ov);
@@ -1161,6 +1232,7 @@ TD int pg_page_view(PagedDoc<T> &pd, int pos) {
     }
     d = wave_sum(d);
     if (pos == wpos) d = pg_win_delta(pd, pd.vr, pd.vc);
+    if ((pos >> 6) == pd.sob_ch) return uni(pd.sob[pos & 63]) + d;
     return uni(pm_obs(pd, pg)) + d;
 }
 // the window onto level-1 position pos, whose observer start is obs_base
@@ -1193,10 +1265,11 @@ TD void pg_load_pos(PagedDoc<T> &pd, int pos, int obs_base) {
             touch = pg_touch_lines(pd.gA + (size_t)zp * MT_PG_SLOTS, pd.gB + (size_t)zp * MT_PG_SLOTS,
                                    pd.gO + (size_t)zp * MT_PG_SLOTS);
         uint32_t bc = 0, f2 = 0;
-        pg_win_fetch_blocks(pd, pg, bc, f2);
+        int ob = 0;
+        pg_win_fetch_blocks(pd, pg, bc, f2, ob);
         pg_win_flush(pd);
         if (pd.w.status) return;
-        pg_win_place(pd, pg, a, o, b, bc, f2);
+        pg_win_place(pd, pg, a, o, b, bc, f2, ob);
         asm volatile("" ::"v"(touch));
 #else
         pg_win_switch(pd, pg);
@@ -2278,17 +2351,19 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
         up.ob = (GLB_AS uint16_t *)tier_paged<T::kBig>(st, doc).oU;
         up.obst = pd.PPh;
     }
-    if constexpr (T::kHM) {
-        pd.meta = nullptr;
-        pd.pobs = (LDS_AS int *)(smem + L.offMeta);
-        pd.pnsb = (LDS_AS uint16_t *)(smem + L.offMeta + 4u * pc.PP);
-        pd.gmeta = (GLB_AS PageMeta *)tier_paged<T::kBig>(st, doc).meta;
-    } else {
-        pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
-    }
     pd.pvl = (LDS_AS int *)(smem + L.offCob);
     pd.cob = pd.pvl;
     pd.cdl = pd.cob + (pc.PP + 63) / 64;
+    if constexpr (T::kHM) {
+        pd.meta = nullptr;
+        pd.pst = (LDS_AS uint8_t *)(smem + L.offMeta);
+        pd.gmeta = (GLB_AS PageMeta *)tier_paged<T::kBig>(st, doc).meta;
+        pd.sob = pd.cdl + (pc.PP + 63) / 64;
+        pd.sob_ch = -1;
+        pd.wnb = pd.wobs = 0;
+    } else {
+        pd.meta = (LDS_AS PageMeta *)(smem + L.offMeta);
+    }
     pd.vgen = 0;
     pd.scr_ch = -1;
     pd.upage = (LDS_AS uint16_t *)(smem + L.offUpage);
@@ -2339,6 +2414,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
 TD void pg_mark_free(PagedDoc<T> &pd) {
     const int np = nbr(pd.up, 1);
     pd.vvalid = 0;
+    if constexpr (T::kHM) return;   // (pst marks the pages in use; a free page's HBM meta is unread)
     for (int base = 0; base < pd.PP; base += MT_WAVE)
         if (base + lane() < pd.PP) pm_set_nblk(pd, base + lane(), pm_nblk(pd, base + lane()) | 0x80);
     wsync<T>();
@@ -2378,11 +2454,12 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     if (lane() < MT_LV) up.nb[lane()] = w.hp->n_blk[lane()];
     wsync<T>();
     for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = g.gdir[q];
-    if constexpr (T::kHM) {   // (the block words stay in HBM)
-        for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) {
-            const GLB_AS PageMeta *m = g.gmeta + pg;
-            pm_set_ns(pd, pg, m->nseg, m->nblk);
-            pm_set_obs(pd, pg, m->obs);
+    if constexpr (T::kHM) {   // (the metadata stays in HBM: only the directory's pages are in use)
+        for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) pd.pst[pg] = 0;
+        wsync<T>();
+        for (int q = lane(); q < np; q += MT_WAVE) {
+            const int pg = up.dir[q];
+            pd.pst[pg] = (uint8_t)((g.gmeta[pg].nseg & 0x7F) | 0x80);
         }
     } else {
         GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)g.gmeta;
@@ -2395,9 +2472,19 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     }
     for (int i = 1 + lane(); i <= w.heap_n; i += MT_WAVE) w.heap[i] = g.gheap[i];
     // the HBM table names page ids; LDS entries name level-1 positions: each page's position
-    // in its meta obs word for the conversion (restored from HBM below)
+    // in its meta obs word for the conversion (restored from HBM below) -- T::kHM: in the text
+    // arena's idle half (scratch, as pg_renumber), or found in the directory when it is short
     wsync<T>();
-    for (int q = lane(); q < np; q += MT_WAVE) pm_set_obs(pd, up.dir[q], q);
+    GLB_AS int32_t *posof = T::kHM ? (GLB_AS int32_t *)text_base(w, 1 - w.text_half) : nullptr;
+    const bool pscr = T::kHM && 2 * pd.PP <= w.T_cap;
+    if constexpr (T::kHM) {
+        if (pscr)
+            for (int q = lane(); q < np; q += MT_WAVE) posof[up.dir[q]] = q;
+        gsync();
+        gsync_rd();
+    } else {
+        for (int q = lane(); q < np; q += MT_WAVE) pm_set_obs(pd, up.dir[q], q);
+    }
     wsync<T>();
     // ut_n follows the fill, so that a mask collection inside tab_midx (tab_mgc) scans only
     // the entries written so far, not stale LDS of an earlier workgroup
@@ -2409,7 +2496,22 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         // unconditional loads (a 64-bit load under a per-lane select miscompiles: DESIGN.md
         // section 10); entry 0 exists whenever the loop runs
         const int ec = v ? e : 0;
-        const int p = pm_obs(pd, g.gupage[ec]);   // (its position)
+        int p;   // (its position)
+        if constexpr (T::kHM) {
+            const int pg = g.gupage[ec];
+            if (pscr) {
+                p = posof[pg];
+            } else {
+                p = 0;
+                for (int q = 0; q < np; q++)
+                    if (up.dir[q] == pg) {
+                        p = q;
+                        break;
+                    }
+            }
+        } else {
+            p = pm_obs(pd, g.gupage[ec]);
+        }
         const v4i a = g.guA[ec];
         const u64 o = g.guO[ec];
         const int mi = tab_midx(pd, v && o != 0);
@@ -2418,8 +2520,10 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
         pd.ut_n = min(base + MT_WAVE, utn);
     }
     wsync<T>();
-    for (int q = lane(); q < np; q += MT_WAVE) pm_set_obs(pd, up.dir[q], g.gmeta[up.dir[q]].obs);
-    wsync<T>();
+    if constexpr (!T::kHM) {
+        for (int q = lane(); q < np; q += MT_WAVE) pm_set_obs(pd, up.dir[q], g.gmeta[up.dir[q]].obs);
+        wsync<T>();
+    }
     pg_mark_free(pd);
     pg_cob_rebuild(pd);
     return true;
@@ -2447,14 +2551,7 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
     wsync<T>();
     const int np = nbr(up, 1);
     for (int q = lane(); q < np; q += MT_WAVE) g.gdir[q] = up.dir[q];
-    if constexpr (T::kHM) {   // (the block words are in HBM already)
-        for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) {
-            GLB_AS PageMeta *m = g.gmeta + pg;
-            m->nseg = (uint8_t)pm_nseg(pd, pg);
-            m->nblk = (uint8_t)pm_nblk(pd, pg);
-            m->obs = pm_obs(pd, pg);
-        }
-    } else {
+    if constexpr (!T::kHM) {   // (T::kHM: the metadata is in HBM already)
         GLB_AS uint32_t *gm = (GLB_AS uint32_t *)g.gmeta;
         LDS_AS const uint32_t *lm = (LDS_AS const uint32_t *)pd.meta;
         for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) gm[i] = lm[i];

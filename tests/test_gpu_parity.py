@@ -832,3 +832,55 @@ def test_gpu_xl_documents_match_reference(name, caps):
     assert not bad, bad
     if caps in ("c3_bench", "grow"):
         assert mt.last_grown()["grown"] >= 1
+
+
+# ---------------------------------------------------------------- HBM page metadata (kHM)
+HM_CASES = {
+    # the skewed bench's long classes: 1.6k / 3.2k pages from the start
+    "class_100k": ("ref_c3_xl", lambda b, bs, cfg: bs.class_caps(b, cfg, 100000)),
+    "class_200k": ("ref_c3_60k", lambda b, bs, cfg: bs.class_caps(b, cfg, 200000)),
+    # 12 pages at first: growth rounds until the big region passes 512 pages (P_BIG_HM)
+    "grow_xl": ("ref_c3_xl", lambda b, bs, cfg: TIERS["grow"]),
+    # more concurrent overlapping removers than the 63 slots: overflow sets on the kHM tier
+    "wide_long": ("ref_wide_long", lambda b, bs, cfg: dict(TIERS["paged"], page_capacity=600)),
+    "wide400": ("ref_wide400", lambda b, bs, cfg: dict(TIERS["paged"], page_capacity=512)),
+}
+
+
+@pytest.mark.parametrize("case", list(HM_CASES))
+def test_gpu_hbm_page_metadata_matches_reference(case):
+    """Documents of >= 512 pages without a delta log replay on the kHM tiers (mt_replay.hip
+    use_hm: P_HM, P_BIG_HM), whose page metadata stays in HBM (LDS keeps one byte per page):
+    text, leaf partition, segment table and property sets equal the reference's."""
+    import json
+    import os
+    import bench
+    import bench_skew
+    name, kw_of = HM_CASES[case]
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    cfg = json.load(open(os.path.join(bench.REPO, "bench", "configs.json")))["c3skew"]
+    kw = dict(kw_of(bench, bench_skew, cfg))
+    kw["delta_log_capacity"] = 0
+    mt = _gpu_batch(len(fx["docs"]), **kw)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    assert (mt.status() == 0).all(), mt.status()
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        o = _gpu_outputs_nolog(mt, i)
+        exp = dict(gu.expected(doc, interner))
+        o["deltas"] = exp["deltas"]
+        errs = gu.compare_oracle(o, exp)
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, bad
+    if case == "grow_xl":
+        assert mt.last_grown()["grown"] >= 1
+
+
+def _gpu_outputs_nolog(mt, doc):
+    rows, leaves = mt.get_segments(doc)
+    return dict(text=mt.get_text(doc), length=mt.get_length(doc), leaves=leaves, segs=rows,
+                seg_props=[mt.get_segment_props(doc, i) for i in range(len(rows))], status=int(mt.status()[doc]))
