@@ -335,6 +335,29 @@ def c5_end_to_end(mt, counts, recs, text, props, mn, cu, chunk, tail_arr, tail, 
                        f"{el:.3f} s (best of 2 after a warm-up run)")
 
 
+def c5_roofline(load, counts, tail_arr, sums, n_tail, load_ms, tail_ms):
+    """Roofline of C5's dominant kernel: the summary load (k_load_header:
+    reads every 32-byte mt_seg_rec, its text and property words; writes the segment rows and
+    the text) or the tail replay (the C3 accounting: op records, results, payload, final state)."""
+    import numpy as np
+    n_segs = int(len(load["segs"]))
+    text_units = int(counts[:, 1].sum())
+    props_words = int(counts[:, 2].sum())
+    load_bytes = n_segs * (32 + SEG_BYTES) + 4 * text_units + 4 * props_words
+    ops = tail_arr["ops"]
+    ins = ops["kind"] == 0
+    final_bytes = int(sums["n_segments"].astype(np.int64).sum()) * SEG_BYTES + 2 * int(sums["length"].astype(np.int64).sum())
+    tail_bytes = n_tail * (OP_BYTES + RESULT_BYTES) + 2 * int(ops["pos2"][ins].sum()) + final_bytes
+    load_dom = load_ms >= tail_ms
+    ms, alg = (load_ms, load_bytes) if load_dom else (tail_ms, tail_bytes)
+    achieved = alg / (ms / 1000.0) / 1e9 if ms > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / (HBM_PEAK / 1e9), "traffic": None,
+            "kernel": "k_load_header (summary load)" if load_dom else "k_replay (64-op tails)",
+            "kernel_ms": round(ms, 3), "alg_bytes_per_launch": alg,
+            "other_kernel_ms": round(tail_ms if load_dom else load_ms, 3)}
+
+
 def run_c5(args, cfg, rank, world, local_rank, dist):
     """Config C5 (cold catch-up): every document's SnapshotV1 summary is loaded
     (mt_snapshots_load_async: reloadFromSegments + loadBody) and its tail of `tail` sequenced
@@ -388,11 +411,13 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    load_ms, tail_ms = mt.last_load_ms(), mt.last_kernel_ms()   # (the last step's, HIP events)
     status = mt.status()
     sums = mt.checksums()
     if rank != 0:
         return
     n_tail = int(len(idx))
+    roofline = c5_roofline(load, counts, tail_arr, sums, n_tail, load_ms, tail_ms)
     cpu = parity = decode = e2e = None
     if not args.no_cpu:
         threads = args.cpu_threads or host_cores()
@@ -426,6 +451,7 @@ def run_c5(args, cfg, rank, world, local_rank, dist):
                    "summary_text_units": int(counts[:, 1].sum()), "body_docs": int((load["n_header"] <
                                                                                      np.diff(load["doc_off"])).sum()),
                    "parallelism": f"doc-shard x{world}"},
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "summary_decode": decode,
         "end_to_end": e2e,

@@ -336,6 +336,10 @@ class MergeTreeBatch:
     def last_kernel_ms(self):
         return float(self.lib.mt_last_kernel_ms(self.h))
 
+    def last_load_ms(self):
+        """Device time of the most recent snapshot load's kernels (mt_last_load_ms)."""
+        return float(self.lib.mt_last_load_ms(self.h))
+
     # -------------------------------------------------------------- read-out
     def status(self):
         out = np.zeros(self.n_docs, dtype=np.int32)

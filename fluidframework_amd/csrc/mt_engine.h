@@ -404,12 +404,19 @@ TD int vlen(DocT<T> &d, v4i a, u64 o, int r, int c) {
 }
 
 // paged instances (window: levels 0-1; upper levels: 1.. with level 1 = pages): B entries
-// for levels 0 and 1, B/2 for level 2, B/8 above -- a node holds >= 4 children after a split
-// or a repack, so level l + 1 has about a quarter of level l (growth is checked against bcap)
-static __host__ __device__ inline int pcnt_cap3(int B) { return B / 8 > 2 ? B / 8 : 2; }
-static __host__ __device__ inline int pcnt_cap(int B, int l) { return l <= 1 ? B : (l == 2 ? B / 2 : pcnt_cap3(B)); }
+// for levels 0 and 1, B / 4^(l-1) + 8 above (growth is checked against bcap)
+// paged instances: a node above level 1 holds >= 4 children once split or repacked (pack
+// regroups a parent's children max(1, min(7, n/4)) to a node), so level l >= 2 has at most
+// B / 4^(l-1) nodes -- plus 8 for the few a repack leaves short (pg_room keeps 4 free per level;
+// a document that needs more is handed to the growth step, which doubles B)
+static __host__ __device__ inline int pcnt_cap(int B, int l) { return l <= 1 ? B : (B >> (2 * (l - 1))) + 8; }
 static __host__ __device__ inline int pcnt_off(int B, int l) {
-    return l <= 1 ? l * B : (l == 2 ? 2 * B : 2 * B + B / 2 + (l - 3) * pcnt_cap3(B));
+    if (l <= 1) return l * B;
+    int o = 2 * B;
+#pragma unroll
+    for (int j = 2; j < MT_LV; j++)
+        if (j < l) o += pcnt_cap(B, j);
+    return o;
 }
 static __host__ __device__ inline int pcnt_bytes(int B) { return pcnt_off(B, MT_LV); }
 TD LDS_AS uint8_t *lvl(DocT<T> &d, int l) {

@@ -2440,6 +2440,8 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     const DocHdr h = *w.hp;
     const int np = h.n_blk[1];
     if (np > pd.PP || h.pad[HDR_UTN] > pd.UT || h.heap_n > pd.PH) return false;
+    for (int l = 2; l < h.depth; l++)
+        if (h.n_blk[l] + 4 > pcnt_cap(pd.PP, l)) return false;   // (the upper levels' room, pg_room)
     if (T::kOvlBits < 64 && w.wide) return false;
     if constexpr (!T::kOvf) {   // overflow overlap sets still consulted: a 64-bit tier's
         if (pd.govf) {
@@ -2656,8 +2658,10 @@ TD bool pg_convert(PagedDoc<T> &pd, const FlatSrc &src) {
     GLB_AS const v2i *fH = src.heap;
     const int depth = h.depth;
     const int np = depth == 1 ? 1 : h.n_blk[1];
-    if (np + 8 > pd.PP || h.heap_n > pd.PH) {
-        pg_fail_cap(w, np + 8 > pd.PP ? 7 : 3);
+    bool up_ok = true;
+    for (int l = 2; l < depth; l++) up_ok = up_ok && h.n_blk[l] + 4 <= pcnt_cap(pd.PP, l);
+    if (np + 8 > pd.PP || !up_ok || h.heap_n > pd.PH) {
+        pg_fail_cap(w, np + 8 > pd.PP || !up_ok ? 7 : 3);
         return false;
     }
     // the packed table stores seq / removedSeq as 16-bit offsets from currentSeq - 32000: a

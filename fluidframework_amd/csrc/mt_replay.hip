@@ -595,7 +595,8 @@ struct mt_handle {
     uint32_t n_docs = 0;
     DevState st{};
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_load = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_load = nullptr, ev_load1 = nullptr;
+    bool load_timed = false;   // ev_load / ev_load1 bracket the last snapshot load's kernels
     // documents per workgroup of the LDS-tier replay (env MT_WPG=2 for two): measured on C2
     // the CU saturates at 16 resident documents (16 -> 18 per CU: 61.8 -> 64.6 ms)
     int wpg = 1;
@@ -920,7 +921,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
     }
     if (!ok || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-        hipEventCreate(&h->ev_load) != hipSuccess) {
+        hipEventCreate(&h->ev_load) != hipSuccess || hipEventCreate(&h->ev_load1) != hipSuccess) {
         mt_destroy(h);
         return nullptr;
     }
@@ -954,6 +955,7 @@ void mt_destroy(mt_handle *h) {
     if (h->ev0) hipEventDestroy(h->ev0);
     if (h->ev1) hipEventDestroy(h->ev1);
     if (h->ev_load) hipEventDestroy(h->ev_load);
+    if (h->ev_load1) hipEventDestroy(h->ev_load1);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1102,7 +1104,9 @@ __global__ void k_mark_big(DevState st, const int64_t *off, int resume_set) {
 // Documents of many pages replay with their leaf-block words in HBM (TierPagedT kHM: 6 LDS
 // bytes per page instead of 12, so more of them share a CU); the bench's C3 / C4 documents
 // (< 300 pages) keep them in LDS.
+#ifndef MT_HM_PAGES
 #define MT_HM_PAGES 512
+#endif
 static bool use_hm(const mt_handle *h, const PagedCaps &pc) {
     return !pc.packed && !pc.narrow && !h->st.DL && pc.PP >= MT_HM_PAGES;
 }
@@ -1458,6 +1462,8 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
             t = t || 2 * x.pad[HDR_UTN] > launched.UT;
             hp = hp || 2 * x.heap_n > launched.PH;
             pg = pg || 2 * (np + 8) > launched.PP;
+            if (x.pad[HDR_PAGED])   // an upper level near its room (pcnt_cap scales with the pages)
+                for (int l = 2; l < x.depth && l < MT_LV; l++) pg = pg || 2 * (x.n_blk[l] + 4) > pcnt_cap(launched.PP, l);
             const int cause = x.status == 0 ? x.pad[HDR_DIAG] : 0;   // an arena hand-over (pg_arena_room)
             tx = tx || cause == 4;
             pr = pr || cause == 5;
@@ -1852,8 +1858,18 @@ int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s) {
                                s->sc, pc, (int)s->doc_lo);
         HIPCHK(h, hipGetLastError());
     }
+    HIPCHK(h, hipEventRecord(h->ev_load1, h->stream));
+    h->load_timed = true;
     if (s->body) return mt_batch_apply_async(h, s->body);
     return 0;
+}
+
+float mt_last_load_ms(mt_handle *h) {
+    if (!h || !h->load_timed) return 0.f;
+    float ms = 0.f;
+    if (hipEventSynchronize(h->ev_load1) != hipSuccess || hipEventElapsedTime(&ms, h->ev_load, h->ev_load1) != hipSuccess)
+        return 0.f;
+    return ms;
 }
 
 int mt_load_snapshots(mt_handle *h, const int64_t *doc_seg_off, const int32_t *n_header, const mt_seg_rec *segs,

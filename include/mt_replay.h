@@ -192,6 +192,10 @@ mt_snapshots *mt_snapshots_upload_range(mt_handle *h, uint32_t doc_lo, uint32_t 
                                         uint64_t props_len, const int32_t *min_seq, const int32_t *cur_seq);
 int mt_snapshots_load_async(mt_handle *h, const mt_snapshots *s);
 void mt_snapshots_free(mt_snapshots *s);
+/* Device time of the most recent snapshot load's kernels (k_load_header and, for documents
+   that load straight into pages, the conversion; HIP events on the handle's stream; waits
+   for them).  0 before any load. */
+float mt_last_load_ms(mt_handle *h);
 
 /* Summary emission: SnapshotV1.extractSync (snapshotV1.ts:156-252) of every document's
    current state as mt_seg_rec records in summary order (runs below minSeq coalesced, merge

@@ -8,9 +8,8 @@ import sys
 MT_PG_SLOTS, MT_LV, META, LDS_CU = 64, 8, 12, 160 * 1024
 
 
-def pcnt_bytes(B):
-    c3 = max(B // 8, 2)
-    return 2 * B + B // 2 + (MT_LV - 3) * c3
+def pcnt_bytes(B):   # mt_engine.h pcnt_off(B, MT_LV): levels 0-1 B each, level l >= 2 B / 4^(l-1) + 8
+    return 2 * B + sum((B >> (2 * (l - 1))) + 8 for l in range(2, MT_LV))
 
 
 def paged_lds(PP, UT, PH, ob=4, hm=0, gen_words=0):
