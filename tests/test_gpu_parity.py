@@ -798,8 +798,13 @@ def test_gpu_default_handle_is_unbounded(name):
     assert all(mt.is_paged(i) for i in range(len(fx["docs"])))
 
 
-@pytest.mark.parametrize("caps", ["c3_bench", "class_100k", "class_200k", "grow"])
-@pytest.mark.parametrize("name", gu.XL_FIXTURES)
+# (each capacity set once per fixture length: the 100k document at the 200k class's
+# capacities and through growth from 12 pages, the 60k one at the uniform C3 and 100k class's)
+XL_CASES = [("ref_c3_xl", "class_200k"), ("ref_c3_xl", "grow"), ("ref_c3_60k", "c3_bench"),
+            ("ref_c3_60k", "class_100k")]
+
+
+@pytest.mark.parametrize("name,caps", XL_CASES)
 def test_gpu_xl_documents_match_reference(name, caps):
     """The skewed bench's long classes (c3skew: 40k-200k messages per document) pinned to the
     reference: a 60k- and a 100k-message C3 document (tests/golden/ref_c3_60k / ref_c3_xl, made
@@ -837,10 +842,10 @@ def test_gpu_xl_documents_match_reference(name, caps):
 # ---------------------------------------------------------------- HBM page metadata (kHM)
 HM_CASES = {
     # the skewed bench's long classes: 1.6k / 3.2k pages from the start
-    "class_100k": ("ref_c3_xl", lambda b, bs, cfg: bs.class_caps(b, cfg, 100000)),
-    "class_200k": ("ref_c3_60k", lambda b, bs, cfg: bs.class_caps(b, cfg, 200000)),
+    "class_100k": ("ref_c3_60k", lambda b, bs, cfg: bs.class_caps(b, cfg, 100000)),
+    "class_200k": ("ref_c3_xl", lambda b, bs, cfg: bs.class_caps(b, cfg, 200000)),
     # 12 pages at first: growth rounds until the big region passes 512 pages (P_BIG_HM)
-    "grow_xl": ("ref_c3_xl", lambda b, bs, cfg: TIERS["grow"]),
+    "grow_60k": ("ref_c3_60k", lambda b, bs, cfg: TIERS["grow"]),
     # more concurrent overlapping removers than the 63 slots: overflow sets on the kHM tier
     "wide_long": ("ref_wide_long", lambda b, bs, cfg: dict(TIERS["paged"], page_capacity=600)),
     "wide400": ("ref_wide400", lambda b, bs, cfg: dict(TIERS["paged"], page_capacity=512)),
@@ -876,7 +881,7 @@ def test_gpu_hbm_page_metadata_matches_reference(case):
         if errs:
             bad.append((doc["doc"], errs))
     assert not bad, bad
-    if case == "grow_xl":
+    if case == "grow_60k":
         assert mt.last_grown()["grown"] >= 1
 
 
