@@ -30,8 +30,8 @@ def class_caps(bench, cfg, max_ops):
     while uid < 4 * max_ops:
         uid *= 2
     # pages: the measured peaks are 0.0154-0.0161 per message above 10k (c3skew: 3080 at 200k,
-    # 1496 at 100k, 629 at 40k, 323 at 20k); 200k -> 3200 pages keeps a document at 78 KB of LDS,
-    # 2 per CU (a document that still outgrows it moves to the growth step's region by itself)
+    # 1496 at 100k, 629 at 40k, 323 at 20k); 200k -> 3200 pages (a document that still outgrows
+    # it moves to the growth step's region by itself)
     pages = max(192, int(max_ops * 0.0155) + 100)
     caps.update(page_capacity=pages, text_capacity=text,
                 props_capacity=int(0.3 * max_ops) + 512, uid_capacity=min(uid, 1 << 20))
@@ -40,8 +40,9 @@ def class_caps(bench, cfg, max_ops):
             caps.pop(k, None)
         # unsettled table / heap at the measured peaks plus a margin (c3skew: <= 203 / 183 in
         # every class; the growth step takes a document past them): 26 + 8 fewer LDS bytes per
-        # entry over the C3 full tier's 320 / 512 -- with the leaf-block words in HBM (>= 512
-        # pages, mt_replay.hip use_hm) a 200k-message document takes 43.9 KB: 3 per CU
+        # entry over the C3 full tier's 320 / 512 -- with the page metadata in HBM (>= 512 pages,
+        # mt_replay.hip use_hm) a 200k-message document takes 25.7 KB of LDS: 6 per CU
+        # (profiles/tools/lds_footprint.py 3200 240 224 8 1)
         caps.update(unsettled_capacity=240, page_heap_capacity=224)
     return caps
 
