@@ -668,9 +668,29 @@ def ingest_rates(mt, host, step_s):
     t_up = time.perf_counter() - t
     up.free()
     n_ops = len(host["ops"])
+    # the native encoder (mt_opdec, libmtsnapdec.so) on the same logs as JSON text, each
+    # document's log repeated to 512 documents, on the host's cores
+    from fluidframework_amd.opdec import MessageDecoder
+    blobs = MessageDecoder.pack(msgs)
+    reps = max(1, 512 // len(blobs))
+    many = blobs * reps
+    threads = host_cores()
+    dec = MessageDecoder(Interner(synthetic=True), threads=threads)
+    dec.decode_packed(many[:len(blobs)])   # (warm: thread pool buffers)
+    t = time.perf_counter()
+    dec.decode_packed(many)
+    t_nat = time.perf_counter() - t
+    nat_msgs, nat_mb = n_msgs * reps, sum(len(x) for x in many) / 1e6
+    nat_rate = nat_msgs / t_nat
     return {"encode": {"value": round(n_msgs / t_enc, 1), "unit": "messages/s", "cores": 1,
                        "sample": f"{n_msgs} messages of tests/golden/ref_c3_full (JSON message objects -> op records "
                                  f"+ arenas, fluidframework_amd/wire.py Batch), {t_enc:.2f} s"},
+            "encode_native": {"value": round(nat_rate, 1), "unit": "messages/s", "cores": threads,
+                              "MB_per_s": round(nat_mb / t_nat, 1),
+                              "sample": f"{nat_msgs} messages ({nat_mb:.0f} MB of JSON: the ref_c3_full logs x {reps}) "
+                                        f"-> op records + arenas by mt_opdec_decode + fetch (libmtsnapdec.so, equal to "
+                                        f"wire.Batch: tests/test_snapdec.py), {t_nat:.2f} s"},
+            "value_with_native_encode_and_upload": round(n_ops / (step_s + t_up + n_ops / nat_rate), 1),
             "h2d_upload": {"bytes": int(nbytes), "s": round(t_up, 3), "GB_per_s": round(nbytes / t_up / 1e9, 2),
                            "how": "mt_batch_upload of this step's op records, text and property arenas from pageable "
                                   "host memory (validation + hipMemcpy)"},

@@ -772,6 +772,243 @@ struct Worker {
     }
 };
 
+// ---------------------------------------------------------------- sequenced messages
+// ISequencedDocumentMessage JSON (PD/protocol.ts:132-172) carrying IMergeTree ops
+// (MT/ops.ts:63-110) -> mt_op_rec records, as fluidframework_amd/wire.py Batch.add_doc /
+// _msg / _op encode them (its tests compare the two on the reference's fixtures).
+struct OpDocOut {
+    std::vector<mt_op_rec> ops;       // payload (text) / props: offsets into this document's arenas
+    std::vector<uint16_t> text;
+    std::vector<uint32_t> props;      // [count | combine << 16, (key, value) x count]: local ids
+    std::vector<std::u16string> keys; // local key id -> key
+    std::vector<std::string> vals;    // local value id -> canonical JSON
+    std::string clients, err;
+    std::vector<uint32_t> kmap, vmap;
+    size_t oi = 0, ti = 0, pi = 0;
+};
+
+const char *const kMsgKeys[6] = {"clientId", "sequenceNumber", "referenceSequenceNumber", "minimumSequenceNumber",
+                                 "type", "contents"};
+
+struct OpWorker {
+    bool synthetic = false;
+    Blob B;
+    std::unordered_map<std::u16string, uint32_t> key_ids, shortid;
+    std::unordered_map<std::string, uint32_t> val_ids;
+    std::vector<std::u16string> sid;   // short id k + 1 -> long client id (k = 0: the first seen)
+    std::u16string kbuf;
+    std::string cbuf;
+    std::vector<uint32_t> mbuf;
+
+    bool bad(OpDocOut &o, const std::string &m) {
+        o.err = m;
+        return false;
+    }
+    // DocEncoder.client: first-seen order from 1 (the observer is 0); a null clientId is an
+    // id of its own (a dict key None in the Python encoder)
+    int client(uint32_t c) {
+        static const char16_t kNull = (char16_t)0xFFFF;   // (not a UTF-16 string)
+        const bool str = c != NONE && B.nodes[c].t == Node::STR;
+        const char16_t *u = str ? B.s(B.nodes[c].off) : &kNull;
+        const uint32_t n = str ? B.nodes[c].len : 1;
+        if (sid.size() <= 32) {   // few writers: a linear scan over the first-seen names
+            for (size_t k = 0; k < sid.size(); k++)
+                if (sid[k].size() == n && !memcmp(sid[k].data(), u, n * sizeof(char16_t))) return (int)k + 1;
+            sid.emplace_back(u, n);
+            if (sid.size() > 32)
+                for (size_t k = 0; k < sid.size(); k++) shortid.emplace(sid[k], (uint32_t)k + 1);
+            return (int)sid.size();
+        }
+        kbuf.assign(u, n);
+        auto it = shortid.find(kbuf);
+        if (it != shortid.end()) return (int)it->second;
+        sid.push_back(kbuf);
+        shortid.emplace(kbuf, (uint32_t)sid.size());
+        return (int)sid.size();
+    }
+    uint32_t key(OpDocOut &o, uint32_t m) {
+        const char16_t *k = B.s(B.nodes[m].koff);
+        const uint32_t n = B.nodes[m].klen;
+        if (synthetic) {
+            uint32_t v = 0;
+            for (uint32_t i = 1; i < n; i++) v = v * 10 + (uint32_t)(k[i] - u'0');
+            return v;
+        }
+        kbuf.assign(k, n);
+        auto it = key_ids.find(kbuf);
+        if (it != key_ids.end()) return it->second;
+        const uint32_t id = (uint32_t)o.keys.size();
+        key_ids.emplace(kbuf, id);
+        o.keys.push_back(kbuf);
+        return id;
+    }
+    uint32_t val(OpDocOut &o, uint32_t i) {
+        if (B.nodes[i].t == Node::NUL) return MT_VAL_NULL;
+        if (synthetic) {
+            const uint32_t x = (uint32_t)B.as_int(i);
+            return x | (x == 0 ? MT_VAL_FALSY_BIT : 0u);
+        }
+        cbuf.clear();
+        canon(cbuf, B, i);
+        uint32_t id;
+        auto it = val_ids.find(cbuf);
+        if (it != val_ids.end()) {
+            id = it->second;
+        } else {
+            id = (uint32_t)o.vals.size();
+            val_ids.emplace(cbuf, id);
+            o.vals.push_back(cbuf);
+        }
+        return id | (falsy(B, i) ? MT_VAL_FALSY_BIT : 0u);
+    }
+    // Batch._props_rec: [count | combine << 16, (key, value) x count], members in insertion order
+    bool props_rec(OpDocOut &o, uint32_t pr, uint32_t combine, uint32_t &off) {
+        if (pr == NONE || B.nodes[pr].t != Node::OBJ) return bad(o, "props is not an object");
+        off = (uint32_t)o.props.size();
+        B.members(pr, mbuf);
+        o.props.push_back((uint32_t)mbuf.size() | (combine << 16));
+        for (uint32_t kv : mbuf) {
+            o.props.push_back(key(o, kv));
+            o.props.push_back(val(o, kv));
+        }
+        return true;
+    }
+    static bool truthy_obj(const Blob &B, uint32_t i) {   // Python truthiness of a JSON value
+        if (i == NONE) return false;
+        const Node &v = B.nodes[i];
+        switch (v.t) {
+            case Node::NUL: return false;
+            case Node::BOOL: return v.b != 0;
+            case Node::NUM: return B.num(i) != 0.0;
+            default: return v.len != 0;   // STR: units; ARR / OBJ: members
+        }
+    }
+    // Batch._op for one op (member of a GROUP when `more`)
+    bool op(OpDocOut &o, const mt_op_rec &base, uint32_t op, bool more) {
+        mt_op_rec r = base;
+        r.flags = more ? MT_F_GROUP_MORE : 0;
+        if (op == NONE || B.nodes[op].t != Node::OBJ) return bad(o, "op is not an object");
+        const int64_t t = B.as_int(B.get(op, "type"));
+        if (t == MT_OP_INSERT) {
+            const uint32_t seg = B.get(op, "seg");
+            const uint32_t p1 = B.get(op, "pos1");
+            if (p1 == NONE) return bad(o, "insert without pos1");
+            r.kind = MT_OP_INSERT;
+            r.pos1 = (int32_t)B.as_int(p1);
+            const bool is_obj = seg != NONE && B.nodes[seg].t == Node::OBJ;
+            if (!truthy_obj(B, seg) && !is_obj) {   // `if (op.seg)` falsy: seq / msn only
+                r.kind = MT_OP_NOOP;
+            } else if (B.nodes[seg].t == Node::STR) {
+                r.payload = (uint32_t)o.text.size();
+                o.text.insert(o.text.end(), B.s(B.nodes[seg].off), B.s(B.nodes[seg].off) + B.nodes[seg].len);
+                r.pos2 = (int32_t)B.nodes[seg].len;
+            } else if (is_obj && B.get(seg, "text") != NONE) {
+                const uint32_t tx = B.get(seg, "text");
+                if (B.nodes[tx].t != Node::STR) return bad(o, "insert text is not a string");
+                r.payload = (uint32_t)o.text.size();
+                o.text.insert(o.text.end(), B.s(B.nodes[tx].off), B.s(B.nodes[tx].off) + B.nodes[tx].len);
+                r.pos2 = (int32_t)B.nodes[tx].len;
+                const uint32_t pr = B.get(seg, "props");
+                if (B.present(pr) && !props_rec(o, pr, MT_COMBINE_NONE, r.props)) return false;
+            } else if (is_obj && B.get(seg, "marker") != NONE) {
+                r.flags |= MT_F_MARKER;
+                const uint32_t mk = B.get(seg, "marker");
+                if (B.nodes[mk].t != Node::OBJ) return bad(o, "marker is not an object");
+                r.payload = (uint32_t)B.as_int(B.get(mk, "refType"));
+                r.pos2 = 1;
+                const uint32_t pr = B.get(seg, "props");
+                if (B.present(pr) && !props_rec(o, pr, MT_COMBINE_NONE, r.props)) return false;
+            } else {
+                return bad(o, "unsupported insert segment");
+            }
+        } else if (t == MT_OP_REMOVE || t == MT_OP_ANNOTATE) {
+            r.kind = (uint8_t)t;
+            const uint32_t p1 = B.get(op, "pos1"), p2 = B.get(op, "pos2");
+            if (p1 == NONE || p2 == NONE) return bad(o, "range op without pos1 / pos2");
+            r.pos1 = (int32_t)B.as_int(p1);
+            r.pos2 = (int32_t)B.as_int(p2);
+            if (t == MT_OP_ANNOTATE) {
+                const uint32_t comb = B.get(op, "combiningOp");
+                const bool has = truthy_obj(B, comb);
+                uint32_t cb = has ? MT_COMBINE_REWRITE : MT_COMBINE_NONE;
+                if (has && !B.is_str(B.nodes[comb].t == Node::OBJ ? B.get(comb, "name") : NONE, "rewrite")) {
+                    // Batch._combine_rec: a synthetic interner keeps COMBINE_OTHER; otherwise the
+                    // transform table needs every value the keys held so far -- wire.Batch builds it
+                    if (!synthetic) return bad(o, "combining op: encode with wire.Batch (its transform tables)");
+                    cb = MT_COMBINE_OTHER;
+                }
+                if (!props_rec(o, B.get(op, "props"), cb, r.props)) return false;
+            }
+        } else {
+            return bad(o, "unsupported op type " + std::to_string(t));
+        }
+        o.ops.push_back(r);
+        return true;
+    }
+
+    bool build(OpDocOut &o, const char *json, uint64_t len) {
+        o.ops.clear();
+        o.text.clear();
+        o.props.clear();
+        o.keys.clear();
+        o.vals.clear();
+        o.err.clear();
+        key_ids.clear();
+        val_ids.clear();
+        shortid.clear();
+        sid.clear();
+        B.src = json;
+        B.n = (size_t)len;
+        std::string e;
+        if (!parse(B, e)) return bad(o, e);
+        if (B.nodes[0].t != Node::ARR) return bad(o, "messages are not an array");
+        uint32_t m = B.first(0);
+        o.ops.reserve(B.nodes[0].len);
+        for (uint32_t k = 0; k < B.nodes[0].len; k++, m = B.nodes[m].next) {
+            if (B.nodes[m].t != Node::OBJ) return bad(o, "message " + std::to_string(k) + " is not an object");
+            uint32_t f[6] = {NONE, NONE, NONE, NONE, NONE, NONE};
+            B.fields(m, kMsgKeys, 6, f);
+            if (f[1] == NONE || f[2] == NONE || f[3] == NONE)
+                return bad(o, "message " + std::to_string(k) + " without its sequence numbers");
+            mt_op_rec base;
+            memset(&base, 0, sizeof base);
+            base.seq = (int32_t)B.as_int(f[1]);
+            base.ref_seq = (int32_t)B.as_int(f[2]);
+            base.min_seq = (int32_t)B.as_int(f[3]);
+            base.props = MT_NO_PROPS;
+            base.client = (uint16_t)client(f[0]);
+            base.kind = MT_OP_NOOP;
+            if (f[4] != NONE && !B.is_str(f[4], "op")) {   // a non-op message: seq / msn only
+                o.ops.push_back(base);
+                continue;
+            }
+            const uint32_t c = f[5];
+            if (c == NONE || B.nodes[c].t != Node::OBJ) return bad(o, "message contents are not an object");
+            if (B.as_int(B.get(c, "type")) == 3) {   // GROUP
+                const uint32_t arr = B.get(c, "ops");
+                if (arr == NONE || B.nodes[arr].t != Node::ARR) return bad(o, "group without ops");
+                if (B.nodes[arr].len == 0) {   // applies nothing; applyMsg still updates seq / msn
+                    o.ops.push_back(base);
+                    continue;
+                }
+                uint32_t g = B.first(arr);
+                for (uint32_t j = 0; j < B.nodes[arr].len; j++, g = B.nodes[g].next)
+                    if (!op(o, base, g, j + 1 < B.nodes[arr].len)) return false;
+            } else if (!op(o, base, c, false)) {
+                return false;
+            }
+        }
+        o.clients = "[";
+        for (size_t i = 0; i < sid.size(); i++) {
+            if (i) o.clients.push_back(',');
+            if (sid[i].size() == 1 && sid[i][0] == (char16_t)0xFFFF) o.clients += "null";
+            else json_str(o.clients, sid[i].data(), sid[i].size());
+        }
+        o.clients.push_back(']');
+        return true;
+    }
+};
+
 }  // namespace
 
 struct mt_snapdec {
@@ -783,6 +1020,11 @@ struct mt_snapdec {
     std::vector<std::string> vals;
     std::vector<DocOut> docs;           // reused between calls
     std::vector<Worker> workers;
+    std::vector<OpDocOut> opdocs;       // sequenced-message decoding (mt_opdec_*)
+    std::vector<OpWorker> opworkers;
+    uint32_t op_n_docs = 0;
+    int op_threads = 1;
+    size_t nops = 0, optx = 0, oppr = 0;
     uint32_t n_docs = 0;                // of the last successful decode
     int threads = 1;
     size_t ns = 0, ntx = 0, npr = 0;    // its output sizes
@@ -991,6 +1233,129 @@ int64_t mt_snapdec_all_clients(const mt_snapdec *s, char *out, uint64_t cap) {
     return (int64_t)n;
 }
 uint32_t mt_snapdec_num_keys(const mt_snapdec *s) { return s ? (uint32_t)s->keys.size() : 0; }
+
+int mt_opdec_decode(mt_snapdec *s, uint32_t n_docs, const char *const *json, const uint64_t *json_len, int threads) {
+    if (!s || (n_docs && (!json || !json_len))) return -1;
+    s->err.clear();
+    if (s->opdocs.size() < n_docs) s->opdocs.resize(n_docs);
+    s->op_n_docs = 0;
+    const int nt = std::max(1, std::min({threads, 256, (int)std::max<uint32_t>(n_docs, 1)}));
+    if ((int)s->opworkers.size() < nt) s->opworkers.resize((size_t)nt);
+    {   // phase 1: each document parsed and encoded on its own (dynamic, one at a time)
+        std::atomic<uint32_t> next{0};
+        auto work = [&](int t) {
+            OpWorker &w = s->opworkers[(size_t)t];
+            w.synthetic = s->synthetic;
+            for (;;) {
+                const uint32_t d = next.fetch_add(1);
+                if (d >= n_docs) break;
+                try {
+                    w.build(s->opdocs[d], json[d], json_len[d]);
+                } catch (const std::exception &ex) {
+                    s->opdocs[d].err = std::string("decode failed: ") + ex.what();
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
+        work(0);
+        for (auto &t : pool) t.join();
+    }
+    // phase 2: places and the batch's key / value ids, first seen in document order
+    size_t no = 0, ntx = 0, npr = 0;
+    for (uint32_t d = 0; d < n_docs; d++) {
+        OpDocOut &o = s->opdocs[d];
+        if (!o.err.empty()) {
+            s->err = "document " + std::to_string(d) + ": " + o.err;
+            return -1;
+        }
+        o.oi = no;
+        o.ti = ntx;
+        o.pi = npr;
+        no += o.ops.size();
+        ntx += o.text.size();
+        npr += o.props.size();
+        if (s->synthetic) continue;
+        o.kmap.resize(o.keys.size());
+        for (size_t k = 0; k < o.keys.size(); k++) {
+            auto it = s->key_ids.find(o.keys[k]);
+            if (it == s->key_ids.end()) {
+                it = s->key_ids.emplace(o.keys[k], (uint32_t)s->keys.size()).first;
+                s->keys.push_back(o.keys[k]);
+            }
+            o.kmap[k] = it->second;
+        }
+        o.vmap.resize(o.vals.size());
+        for (size_t k = 0; k < o.vals.size(); k++) {
+            auto it = s->val_ids.find(o.vals[k]);
+            if (it == s->val_ids.end()) {
+                it = s->val_ids.emplace(o.vals[k], (uint32_t)s->vals.size()).first;
+                s->vals.push_back(o.vals[k]);
+            }
+            o.vmap[k] = it->second;
+        }
+    }
+    if (ntx > 0xFFFFFFFFull || npr > 0xFFFFFFFFull) {   // mt_op_rec offsets are 32-bit
+        s->err = "encoded text / property arena exceeds 2^32 entries: decode fewer documents per call";
+        return -1;
+    }
+    s->op_n_docs = n_docs;
+    s->op_threads = nt;
+    s->nops = no;
+    s->optx = ntx;
+    s->oppr = npr;
+    return 0;
+}
+
+int mt_opdec_sizes(const mt_snapdec *s, uint64_t *n_ops, uint64_t *text_len, uint64_t *props_len) {
+    if (!s) return -1;
+    if (n_ops) *n_ops = s->nops;
+    if (text_len) *text_len = s->optx;
+    if (props_len) *props_len = s->oppr;
+    return 0;
+}
+
+int mt_opdec_fetch(const mt_snapdec *s, int64_t *doc_op_off, mt_op_rec *ops, uint16_t *text, uint32_t *props) {
+    if (!s) return -1;
+    const uint32_t n = s->op_n_docs;
+    parallel_docs(n, s->op_threads, 16, [&](uint32_t d) {
+        const OpDocOut &o = s->opdocs[d];
+        if (doc_op_off) doc_op_off[d] = (int64_t)o.oi;
+        if (ops) {
+            mt_op_rec *dst = ops + o.oi;
+            for (size_t k = 0; k < o.ops.size(); k++) {
+                mt_op_rec r = o.ops[k];
+                if (r.kind == MT_OP_INSERT && !(r.flags & MT_F_MARKER)) r.payload += (uint32_t)o.ti;
+                if (r.props != MT_NO_PROPS) r.props += (uint32_t)o.pi;
+                dst[k] = r;
+            }
+        }
+        if (text && !o.text.empty()) memcpy(text + o.ti, o.text.data(), o.text.size() * sizeof(uint16_t));
+        if (props && !o.props.empty()) {
+            if (s->synthetic) {
+                memcpy(props + o.pi, o.props.data(), o.props.size() * sizeof(uint32_t));
+            } else {
+                uint32_t *q = props + o.pi;
+                for (size_t i = 0; i < o.props.size();) {
+                    const uint32_t c = o.props[i++];
+                    *q++ = c;
+                    for (uint32_t j = 0; j < (c & 0xFFFFu); j++, i += 2) {
+                        const uint32_t v = o.props[i + 1];
+                        *q++ = o.kmap[o.props[i]];
+                        *q++ = v == MT_VAL_NULL ? v : (o.vmap[v & ~MT_VAL_FALSY_BIT] | (v & MT_VAL_FALSY_BIT));
+                    }
+                }
+            }
+        }
+    });
+    if (doc_op_off) doc_op_off[n] = (int64_t)s->nops;
+    return 0;
+}
+
+int64_t mt_opdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint64_t cap) {
+    if (!s || d >= s->op_n_docs) return -1;
+    return copy_out(s->opdocs[d].clients, out, cap);
+}
 uint32_t mt_snapdec_num_values(const mt_snapdec *s) { return s ? (uint32_t)s->vals.size() : 0; }
 
 }  // extern "C"

@@ -34,6 +34,10 @@ SIGNATURES = [
     ("mt_snapdec_num_values", _U32, [_P]),
     ("mt_snapdec_doc_clients", _I64, [_P, _U32, _P, _U64]),
     ("mt_snapdec_all_clients", _I64, [_P, _P, _U64]),
+    ("mt_opdec_decode", _I, [_P, _U32, _P, _P, _I]),
+    ("mt_opdec_sizes", _I, [_P, _P, _P, _P]),
+    ("mt_opdec_fetch", _I, [_P, _P, _P, _P, _P]),
+    ("mt_opdec_doc_clients", _I64, [_P, _U32, _P, _U64]),
 ]
 _lib = None
 

@@ -58,6 +58,26 @@ int64_t mt_snapdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint6
 int64_t mt_snapdec_all_clients(const mt_snapdec *s, char *out, uint64_t cap);
 uint32_t mt_snapdec_num_values(const mt_snapdec *s);
 
+/* Sequenced messages -> op records: the host encode in front of mt_batch_upload, native.
+   Document d's messages are one JSON array of ISequencedDocumentMessage objects
+   (PD/protocol.ts:132-172; clientId, sequenceNumber, referenceSequenceNumber,
+   minimumSequenceNumber, type, contents = an IMergeTree op, MT/ops.ts:63-110) in json[d]
+   (json_len[d] bytes).  Records as fluidframework_amd/wire.py Batch.add_doc makes them (the
+   encoder the JS facade mirrors, js/encode.js): one mt_op_rec per op (GROUP members with
+   MT_F_GROUP_MORE, an empty GROUP or a non-"op" message a MT_OP_NOOP record), short client
+   ids first-seen per document from 1, property keys / values interned on this decoder in
+   first-seen document order (mt_snapdec_key / mt_snapdec_value, shared with summary
+   decoding).  A non-rewrite combining op fails the decode (its transform table needs every
+   value its keys have held: wire.Batch builds it), as do malformed messages; the error names
+   the first failing document.  `threads` workers take documents dynamically. */
+int mt_opdec_decode(mt_snapdec *s, uint32_t n_docs, const char *const *json, const uint64_t *json_len, int threads);
+int mt_opdec_sizes(const mt_snapdec *s, uint64_t *n_ops, uint64_t *text_len, uint64_t *props_len);
+/* doc_op_off[n_docs + 1], ops[n_ops], text[text_len], props[props_len] (each nullable) */
+int mt_opdec_fetch(const mt_snapdec *s, int64_t *doc_op_off, mt_op_rec *ops, uint16_t *text, uint32_t *props);
+/* document d's long client ids in short-id order (id 1 first) as a JSON array; null for a
+   message without a clientId */
+int64_t mt_opdec_doc_clients(const mt_snapdec *s, uint32_t d, char *out, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

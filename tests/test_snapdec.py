@@ -46,7 +46,7 @@ def test_library_exports_header():
     import re
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                             "mt_snapshot.h")).read()
-    names = set(re.findall(r"\b(mt_snapdec_\w+)\s*\(", hdr))
+    names = set(re.findall(r"\b(mt_(?:snapdec|opdec)_\w+)\s*\(", hdr))
     lib = snapdec.load()
     assert names and all(hasattr(lib, n) for n in names), names
 
@@ -183,3 +183,81 @@ def test_native_decoder_ill_formed_utf8_as_buffer_tostring(bad):
     _check([{"header": raw}])
     text = decode_chunks({"header": raw}).header_specs[0]["text"]
     assert "\ufffd" in text and text.startswith("q") and text.endswith("z")
+
+
+# ---------------------------------------------------------------- sequenced messages (mt_opdec)
+def _messages(fx):
+    from fluidframework_amd.wire import compact_msgs_to_dicts
+    return [d for d in fx["docs"] if "observer_name" not in d], \
+        [compact_msgs_to_dicts(d["msgs"]) for d in fx["docs"] if "observer_name" not in d]
+
+
+def _check_ops(docs, msgs, synthetic=False, threads=4):
+    from fluidframework_amd.opdec import MessageDecoder
+    from fluidframework_amd.wire import Batch
+    pi, ni = Interner(synthetic), Interner(synthetic)
+    b = Batch(pi)
+    for d, m in zip(docs, msgs):
+        b.add_doc(d["seed_text"], m)
+    pa = b.arrays()
+    na, ncl = MessageDecoder(ni, threads=threads).decode(msgs, seeds=[d["seed_text"] for d in docs])
+    for k in ("doc_off", "seed_off", "seed", "text", "props"):
+        assert np.array_equal(pa[k], na[k]), k
+    assert pa["ops"].tobytes() == na["ops"].tobytes()
+    assert b.clients == ncl
+    assert pi.keys == ni.keys and pi.key_ids == ni.key_ids and pi.val_ids == ni.val_ids
+    assert pi.key_vals == ni.key_vals
+
+
+@pytest.mark.parametrize("name", ["ref_small", "ref_c3_full", "ref_c4", "ref_ext", "ref_ext_long", "ref_wide400"])
+def test_native_message_encode_matches_wire_batch(name):
+    """mt_opdec (native, 4 threads) and wire.Batch give the same op records, text and
+    property arenas, short client maps and interning on the reference's message streams
+    (inserts of text / markers with properties, removes, annotates with rewrite, GROUPs, noops)."""
+    docs, msgs = _messages(gu.load(name))
+    assert docs
+    _check_ops(docs, msgs)
+
+
+def test_native_message_encode_synthetic_and_edge_cases():
+    """Synthetic interning (k<n> keys, integer values) and the encoder's corner cases: falsy
+    insert segments (a noop record keeping pos1), empty GROUPs, non-op messages, duplicate
+    property keys (first position, last value), numbers as JS Numbers, a null clientId."""
+    m = lambda seq, op, cid="a", typ="op": dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=seq - 1,
+                                                minimumSequenceNumber=0, type=typ, contents=op)
+    msgs = [[m(1, {"type": 0, "pos1": 0, "seg": "héllo\U0001F600"}),
+             m(2, {"type": 0, "pos1": 1, "seg": ""}),
+             m(3, {"type": 3, "ops": []}, cid="b"),
+             m(4, None, cid="c", typ="join"),
+             m(5, {"type": 3, "ops": [{"type": 1, "pos1": 0, "pos2": 2},
+                                      {"type": 2, "pos1": 0, "pos2": 1, "props": {"k1": 5, "k2": None}}]}),
+             m(6, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 2}, "props": {"k3": 0}}}, cid=None),
+             m(7, {"type": 2, "pos1": 0, "pos2": 1, "props": {"k1": 1.0}, "combiningOp": {"name": "rewrite"}}),
+             m(8, {"type": 0, "pos1": 2, "seg": {"text": "x", "props": {}}})]]
+    docs = [dict(seed_text="ab")]
+    _check_ops(docs, msgs, synthetic=False)
+    _check_ops(docs, msgs, synthetic=True)
+    raw = ['[{"clientId":"a","sequenceNumber":1,"referenceSequenceNumber":0,"minimumSequenceNumber":0,'
+           '"contents":{"type":2,"pos1":0,"pos2":1,"props":{"x":1,"y":2,"x":3}}}]']
+    from fluidframework_amd.opdec import MessageDecoder
+    from fluidframework_amd.wire import Batch
+    pi = Interner()
+    b = Batch(pi)
+    b.add_doc("", json.loads(raw[0]))
+    na, _ = MessageDecoder(Interner()).decode(raw)
+    assert np.array_equal(b.arrays()["props"], na["props"])
+
+
+def test_native_message_encode_refuses_combining_tables():
+    """A non-rewrite combining op needs wire.Batch's transform table: the native decode names
+    the document and fails; with a synthetic interner it keeps COMBINE_OTHER like wire.Batch."""
+    from fluidframework_amd.opdec import EncodeError, MessageDecoder
+    docs, msgs = _messages(gu.load("ref_combine"))
+    with pytest.raises(EncodeError, match="combining op"):
+        MessageDecoder(Interner()).decode(msgs)
+    bad = [[dict(clientId="a", sequenceNumber=1, referenceSequenceNumber=0, minimumSequenceNumber=0, type="op",
+                 contents={"type": 9})]]
+    with pytest.raises(EncodeError, match="document 0: unsupported op type 9"):
+        MessageDecoder(Interner()).decode(bad)
+    with pytest.raises(EncodeError, match="document 0"):
+        MessageDecoder(Interner()).decode(["[{]"])
