@@ -680,6 +680,7 @@ def ingest_rates(mt, host, step_s):
     t = time.perf_counter()
     dec.decode_packed(many)
     t_nat = time.perf_counter() - t
+    del dec
     nat_msgs, nat_mb = n_msgs * reps, sum(len(x) for x in many) / 1e6
     nat_rate = nat_msgs / t_nat
     return {"encode": {"value": round(n_msgs / t_enc, 1), "unit": "messages/s", "cores": 1,
