@@ -53,7 +53,8 @@ class MessageDecoder:
             elif isinstance(m, str):
                 out.append(m.encode("utf-8", errors="surrogatepass"))
             else:
-                out.append(json.dumps(m, ensure_ascii=False).encode("utf-8", errors="surrogatepass"))
+                # (escaped non-ASCII: a lone surrogate is a \u escape, as JSON.stringify writes it)
+                out.append(json.dumps(m).encode("ascii"))
         return out
 
     def decode_packed(self, blobs):
@@ -113,7 +114,8 @@ class MessageDecoder:
         blobs = self.pack(docs)
         out = self.decode_packed(blobs)
         self.remap(out)
-        seed = [np.frombuffer(s.encode("utf-16-le"), dtype="<u2") for s in (seeds or [""] * len(blobs))]
+        seed = [np.frombuffer(s.encode("utf-16-le", errors="surrogatepass"), dtype="<u2")
+                for s in (seeds or [""] * len(blobs))]
         out["seed_off"] = np.concatenate([[0], np.cumsum([len(x) for x in seed])]).astype(np.int64)
         out["seed"] = np.concatenate(seed).astype(np.uint16) if out["seed_off"][-1] else np.zeros(1, dtype=np.uint16)
         return out, self.clients(len(blobs))

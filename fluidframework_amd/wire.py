@@ -303,7 +303,7 @@ class Batch:
 
     def _text(self, s):
         off = len(self.text)
-        b = s.encode("utf-16-le")
+        b = s.encode("utf-16-le", errors="surrogatepass")   # (JS strings may hold lone surrogates)
         self.text.extend(np.frombuffer(b, dtype="<u2").tolist())
         return off, len(b) // 2
 
@@ -353,7 +353,7 @@ class Batch:
         writers, snapshot.SnapshotBatch.clients); new ids continue after them."""
         enc = DocEncoder(self, clients)
         self.clients.append(enc.short)
-        s = seed_text.encode("utf-16-le")
+        s = seed_text.encode("utf-16-le", errors="surrogatepass")
         self.seed.extend(np.frombuffer(s, dtype="<u2").tolist())
         self.seed_off.append(len(self.seed))
         for msg in msgs:
@@ -387,7 +387,7 @@ class Batch:
         clients maps long ids to short ids, the local client's ids to 0."""
         enc = DocEncoder(self, clients)
         self.clients.append(enc.short)
-        s = seed_text.encode("utf-16-le")
+        s = seed_text.encode("utf-16-le", errors="surrogatepass")
         self.seed.extend(np.frombuffer(s, dtype="<u2").tolist())
         self.seed_off.append(len(self.seed))
         local_key = next((k for k, v in enc.short.items() if v == 0), None)

@@ -261,3 +261,55 @@ def test_native_message_encode_refuses_combining_tables():
         MessageDecoder(Interner()).decode(bad)
     with pytest.raises(EncodeError, match="document 0"):
         MessageDecoder(Interner()).decode(["[{]"])
+
+
+def test_native_message_encode_matches_wire_batch_on_random_streams():
+    """Seeded random message streams over the encoder's whole input space -- unicode text
+    (astral planes, lone surrogates), markers, GROUPs (empty too), property values of every
+    JSON kind (nested objects with keys in any order, -0, 1.0 vs 1, big numbers), null deletes,
+    rewrite annotates, non-op messages, many writers -- encode identically natively and in
+    wire.Batch, interning included."""
+    import random
+    rng = random.Random(20251018)
+    pool = ["", "a", "héllo", "\U0001F600x", "\ud800", "tab\there", "q\"uote", "back\\slash", "日本語", "\n"]
+    vals = [None, 0, -0.0, 1, 1.0, 2.5, 1e21, 123456789012345678901234, "", "s", True, False, [], [1, "a", None],
+            {"b": 1, "a": [2, {"z": None, "y": 0}]}, {"a": [2, {"y": 0, "z": None}], "b": 1.0}]
+    keys = ["k", "key2", "ключ", "\U0001F511", ""]
+
+    def props():
+        return {rng.choice(keys): rng.choice(vals) for _ in range(rng.randint(0, 3))}
+
+    def op():
+        t = rng.random()
+        if t < 0.45:
+            r = rng.random()
+            if r < 0.5:
+                seg = rng.choice(pool) + rng.choice(pool)
+            elif r < 0.75:
+                seg = {"text": rng.choice(pool) or "x", **({"props": props()} if rng.random() < 0.5 else {})}
+            else:
+                seg = {"marker": {"refType": rng.randint(0, 9)}, **({"props": props()} if rng.random() < 0.5 else {})}
+            return {"type": 0, "pos1": rng.randint(0, 50), "seg": seg}
+        p1 = rng.randint(0, 50)
+        if t < 0.7:
+            return {"type": 1, "pos1": p1, "pos2": p1 + rng.randint(0, 9)}
+        o = {"type": 2, "pos1": p1, "pos2": p1 + rng.randint(0, 9), "props": props()}
+        if rng.random() < 0.3:
+            o["combiningOp"] = {"name": "rewrite"}
+        return o
+
+    msgs = []
+    for d in range(6):
+        ms = []
+        for seq in range(1, 400):
+            cid = f"writer-{rng.randint(0, 40)}" if rng.random() < 0.97 else None
+            if rng.random() < 0.05:
+                ms.append(dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=seq - 1,
+                               minimumSequenceNumber=max(0, seq - 20), type="join", contents=None))
+                continue
+            c = {"type": 3, "ops": [op() for _ in range(rng.randint(0, 3))]} if rng.random() < 0.15 else op()
+            ms.append(dict(clientId=cid, sequenceNumber=seq, referenceSequenceNumber=seq - rng.randint(1, 9),
+                           minimumSequenceNumber=max(0, seq - 20), type="op", contents=c))
+        msgs.append(ms)
+    docs = [dict(seed_text=rng.choice(pool)) for _ in msgs]
+    _check_ops(docs, msgs, threads=3)
