@@ -54,7 +54,7 @@ class MessageDecoder:
                 out.append(m.encode("utf-8", errors="surrogatepass"))
             else:
                 # (escaped non-ASCII: a lone surrogate is a \u escape, as JSON.stringify writes it)
-                out.append(json.dumps(m).encode("ascii"))
+                out.append(json.dumps(m, separators=(",", ":")).encode("ascii"))   # (as JSON.stringify)
         return out
 
     def decode_packed(self, blobs):
