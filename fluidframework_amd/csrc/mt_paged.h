@@ -1294,6 +1294,7 @@ TD void pg_pack1_impl(PagedDoc<T> &pd, int pos) {
     DocT<T> &up = pd.up;
     pg_win_flush(pd);
     pd.cur = -1;
+    pd.zuid = 0;   // (zamboni's prefetched page may be one of the repacked ones)
     int c0;
     const int P = blk_find(up, 2, pos, true, c0);
     if (P < 0) {
