@@ -367,6 +367,7 @@ def test_gpu_catch_up_in_slices_matches_reference(tier, slice_docs):
     assert cu_r == cu_g and cl_r == cl_g
     assert np.array_equal(ref.status(), got.status())
     assert np.array_equal(ref.checksums(), got.checksums())
+    assert got.last_load_ms() > 0   # (HIP events around the last slice's load kernels)
     ok = [i for i, d in enumerate(docs) if gu.snap_status(d) == 0]
     b = Batch(got_i)
     for i, d in enumerate(docs):
