@@ -42,8 +42,7 @@
 template <class T> struct PagedDoc {
     DocT<T> w;    // window: one page staged in LDS (first member: see pdoc)
     DocT<T> up;   // levels >= 1 of the tree (level 1 = pages, counted in leaf blocks)
-    LDS_AS PageMeta *meta;    // [PP] by page id (T::kHM: null -- pst / gmeta instead)
-    LDS_AS uint8_t *pst;      // T::kHM: [PP] by page id: segments | 0x80 while in use
+    LDS_AS PageMeta *meta;    // [PP] by page id (T::kHM: null -- gmeta instead)
     GLB_AS PageMeta *gmeta;   // T::kHM: the page metadata in HBM, where it lives for the launch
                               // (observer length, leaf-block counts, needsScour flags)
     LDS_AS int *pvl;          // [PP] by level-1 position: view length in the cached view (vr, vc)
@@ -124,7 +123,7 @@ struct PagedLayout {
 };
 // ob: bytes per overlap mask in LDS (8, or 4 for a narrow tier)
 // packed: the table's entries are 12 bytes (three u32 arrays at offUA) and carry their page
-// hm: T::kHM (per page in LDS only its segment count; its metadata stays in HBM)
+// hm: T::kHM (no per-page metadata in LDS: it stays in HBM)
 static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int UT, int gen_words, int ob,
                                                            bool packed = false, bool hm = false) {
     PagedLayout L;
@@ -138,7 +137,7 @@ static __host__ __device__ inline PagedLayout paged_layout(int PP, int PH, int U
     o = (o + 7u) & ~7u;
     L.offUO = o; o += packed ? 8u * MT_PK_MASKS + MT_PK_MASKS / 8 : ((((uint32_t)ob * UT) + 7u) & ~7u);
     L.offHeap = o; o += 8u * (PH + 1);
-    L.offMeta = o; o += hm ? ((uint32_t)PP + 7u) & ~7u : (uint32_t)sizeof(PageMeta) * PP;
+    L.offMeta = o; o += hm ? 0u : (uint32_t)sizeof(PageMeta) * PP;
     L.offUpage = o; o += packed ? 0u : (2u * UT + 3u) & ~3u;
     L.offCob = o; o += hm ? 8u * (uint32_t)((PP + 63) / 64) + 4u * 64 : 4u * PP;   // cob + cdl + sob, or pvl
     L.offWscr = o; o += 64u * 4;
@@ -193,11 +192,15 @@ __device__ __forceinline__ int8_t pm_flg_l(const LDS_AS PageMeta *m, int q) {
 // sets how many share a CU) keeps only each page's segment / leaf-block counts and observer
 // length in LDS; its leaf-block counts and needsScour flags stay in HBM (read when the page is
 // staged, written back when it changes -- once per window move, not per op).
-// T::kHM: only the segment count (and an in-use bit) of a page is in LDS; its observer length
-// and leaf-block count are global loads (after gsync_rd() where another lane wrote them).
+// T::kHM: no per-page LDS at all; the fields are global loads (after gsync_rd() where another
+// lane wrote them) -- the window's page has them in registers (pg_win_fetch_blocks).
 TD int pm_nseg(const PagedDoc<T> &pd, int pg) {
-    if constexpr (T::kHM) return pd.pst[pg] & 0x7F;
-    else return pd.meta[pg].nseg;
+    if constexpr (T::kHM) {
+        gsync_rd();
+        return pd.gmeta[pg].nseg;
+    } else {
+        return pd.meta[pg].nseg;
+    }
 }
 TD int pm_nblk(const PagedDoc<T> &pd, int pg) {
     if constexpr (T::kHM) {
@@ -217,7 +220,6 @@ TD int pm_obs(const PagedDoc<T> &pd, int pg) {
 }
 TD void pm_set_ns(PagedDoc<T> &pd, int pg, int ns, int nb) {
     if constexpr (T::kHM) {
-        pd.pst[pg] = (uint8_t)(nb ? (ns & 0x7F) | 0x80 : 0);
         pd.gmeta[pg].nseg = (uint8_t)ns;
         pd.gmeta[pg].nblk = (uint8_t)nb;
     } else {
@@ -227,7 +229,6 @@ TD void pm_set_ns(PagedDoc<T> &pd, int pg, int ns, int nb) {
 }
 TD void pm_set_nblk(PagedDoc<T> &pd, int pg, int nb) {
     if constexpr (T::kHM) {
-        pd.pst[pg] = (uint8_t)(nb ? (pd.pst[pg] & 0x7F) | 0x80 : 0);
         pd.gmeta[pg].nblk = (uint8_t)nb;
     } else {
         pd.meta[pg].nblk = (uint8_t)nb;
@@ -286,10 +287,7 @@ TD bool unsettled(const v4i a, int min_seq) {
 TD int pg_alloc(PagedDoc<T> &pd) {
     for (int base = 0; base < pd.PP; base += MT_WAVE) {
         const int pg = base + lane();
-        bool fr;
-        if constexpr (T::kHM) fr = pg < pd.PP && pd.pst[pg] == 0;
-        else fr = pg < pd.PP && pm_nblk(pd, pg) == 0;
-        const u64 m = ballot(fr);
+        const u64 m = ballot(pg < pd.PP && pm_nblk(pd, pg) == 0);
         if (m) {
             const int r = base + first_lane(m);
             if (lane() == 0) pm_set_nblk(pd, r, 1);
@@ -511,7 +509,9 @@ TD void pg_win_load(PagedDoc<T> &pd, int pg) {
 }
 // page pg's slots into registers (lane i: slot i)
 TD void pg_win_fetch(PagedDoc<T> &pd, int pg, v4i &a, u64 &o, v4u &b) {
-    const int n = uni(pm_nseg(pd, pg));
+    // (T::kHM: every slot -- the page's count arrives with its meta, pg_win_fetch_blocks, so
+    // the rows do not wait for it; slots past the count are never placed)
+    const int n = T::kHM ? MT_PG_SLOTS : uni(pm_nseg(pd, pg));
     const int i = lane();
     if (i < n) {
         a = pd.gA[(size_t)pg * MT_PG_SLOTS + i];
@@ -520,7 +520,7 @@ TD void pg_win_fetch(PagedDoc<T> &pd, int pg, v4i &a, u64 &o, v4u &b) {
     }
 }
 // the page's leaf-block words: from LDS, or (T::kHM) loaded beside its slots with its
-// leaf-block count (f2 bits 16..23) and observer length (ob), lane 0
+// leaf-block count (f2 bits 16..23), segment count (bits 24..31) and observer length (ob), lane 0
 TD void pg_win_fetch_blocks(PagedDoc<T> &pd, int pg, uint32_t &bc, uint32_t &f2, int &ob) {
     if constexpr (T::kHM) {
         bc = f2 = 0;
@@ -529,7 +529,7 @@ TD void pg_win_fetch_blocks(PagedDoc<T> &pd, int pg, uint32_t &bc, uint32_t &f2,
             gsync_rd();
             const GLB_AS PageMeta *m = pd.gmeta + pg;
             bc = m->bc;
-            f2 = (uint32_t)m->flg2 | ((uint32_t)m->nblk << 16);
+            f2 = (uint32_t)m->flg2 | ((uint32_t)m->nblk << 16) | ((uint32_t)m->nseg << 24);
             ob = m->obs;
         }
     }
@@ -549,16 +549,17 @@ TD void pg_win_load_impl(PagedDoc<T> &pd, int pg) {
 TD void pg_win_place(PagedDoc<T> &pd, int pg, const v4i &a, const u64 &o, const v4u &b, uint32_t bc, uint32_t f2,
                      int ob) {
     DocT<T> &w = pd.w;
-    const int n = uni(pm_nseg(pd, pg));
-    int nb;
+    int n, nb;
     if constexpr (T::kHM) {
         bc = (uint32_t)bcast((int)bc, 0);
         f2 = (uint32_t)bcast((int)f2, 0);
-        nb = (int)(f2 >> 16);
+        n = (int)(f2 >> 24);
+        nb = (int)((f2 >> 16) & 0xFFu);
         f2 &= 0xFFFFu;
         pd.wnb = nb;
         pd.wobs = bcast(ob, 0);
     } else {
+        n = uni(pm_nseg(pd, pg));
         nb = uni(pm_nblk(pd, pg));
         pm_blocks(pd, pg, bc, f2);
     }
@@ -1485,13 +1486,36 @@ TD void pg_zamboni_impl(PagedDoc<T> &pd) {
         int i = pd.cur >= 0 ? find_uid(w, uid) : -1;
         if (i < 0) {
             const int pg = uni(gpg);
-            if (pg == pd.cur || pg >= pd.PP || uni(pm_nseg(pd, pg)) == 0) {
-                PG_CNT(19)
-                continue;
+            if constexpr (T::kHM) {   // the page's count arrives with its rows: an empty page is
+                                      // skipped before the window moves
+                if (pg == pd.cur || pg >= pd.PP) {
+                    PG_CNT(19)
+                    continue;
+                }
+                v4i a = v4i{0, 0, 0, 0};
+                u64 o = 0;
+                v4u b = v4u{0, 0, 0, 0};
+                uint32_t bc = 0, f2 = 0;
+                int ob = 0;
+                pg_win_fetch(pd, pg, a, o, b);
+                pg_win_fetch_blocks(pd, pg, bc, f2, ob);
+                if ((((uint32_t)bcast((int)f2, 0)) >> 24) == 0) {
+                    PG_CNT(19)
+                    continue;
+                }
+                PG_CNT(18)
+                pg_win_flush(pd);
+                if (w.status) return;
+                pg_win_place(pd, pg, a, o, b, bc, f2, ob);
+            } else {
+                if (pg == pd.cur || pg >= pd.PP || uni(pm_nseg(pd, pg)) == 0) {
+                    PG_CNT(19)
+                    continue;
+                }
+                PG_CNT(18)
+                pg_win_switch(pd, pg);
+                if (w.status) return;
             }
-            PG_CNT(18)
-            pg_win_switch(pd, pg);
-            if (w.status) return;
             i = find_uid(w, uid);
             if (i < 0) {
                 PG_CNT(19)
@@ -2357,7 +2381,6 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.cdl = pd.cob + (pc.PP + 63) / 64;
     if constexpr (T::kHM) {
         pd.meta = nullptr;
-        pd.pst = (LDS_AS uint8_t *)(smem + L.offMeta);
         pd.gmeta = (GLB_AS PageMeta *)tier_paged<T::kBig>(st, doc).meta;
         pd.sob = pd.cdl + (pc.PP + 63) / 64;
         pd.sob_ch = -1;
@@ -2415,7 +2438,6 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
 TD void pg_mark_free(PagedDoc<T> &pd) {
     const int np = nbr(pd.up, 1);
     pd.vvalid = 0;
-    if constexpr (T::kHM) return;   // (pst marks the pages in use; a free page's HBM meta is unread)
     for (int base = 0; base < pd.PP; base += MT_WAVE)
         if (base + lane() < pd.PP) pm_set_nblk(pd, base + lane(), pm_nblk(pd, base + lane()) | 0x80);
     wsync<T>();
@@ -2457,14 +2479,7 @@ TD bool pg_load(PagedDoc<T> &pd, const DevState &st) {
     if (lane() < MT_LV) up.nb[lane()] = w.hp->n_blk[lane()];
     wsync<T>();
     for (int q = lane(); q < np; q += MT_WAVE) up.dir[q] = g.gdir[q];
-    if constexpr (T::kHM) {   // (the metadata stays in HBM: only the directory's pages are in use)
-        for (int pg = lane(); pg < pd.PP; pg += MT_WAVE) pd.pst[pg] = 0;
-        wsync<T>();
-        for (int q = lane(); q < np; q += MT_WAVE) {
-            const int pg = up.dir[q];
-            pd.pst[pg] = (uint8_t)((g.gmeta[pg].nseg & 0x7F) | 0x80);
-        }
-    } else {
+    if constexpr (!T::kHM) {   // (T::kHM: the metadata stays in HBM; pg_mark_free clears the free pages')
         GLB_AS const uint32_t *gm = (GLB_AS const uint32_t *)g.gmeta;
         LDS_AS uint32_t *lm = (LDS_AS uint32_t *)pd.meta;
         for (int i = lane(); i < pd.PP * (int)(sizeof(PageMeta) / 4); i += MT_WAVE) lm[i] = gm[i];
