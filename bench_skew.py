@@ -41,7 +41,7 @@ def class_caps(bench, cfg, max_ops):
         # unsettled table / heap at the measured peaks plus a margin (c3skew: <= 203 / 183 in
         # every class; the growth step takes a document past them): 26 + 8 fewer LDS bytes per
         # entry over the C3 full tier's 320 / 512 -- with the page metadata in HBM (>= 512 pages,
-        # mt_replay.hip use_hm) a 200k-message document takes 25.7 KB of LDS: 6 per CU
+        # mt_replay.hip use_hm) a 200k-message document takes 22.5 KB of LDS: 7 per CU
         # (profiles/tools/lds_footprint.py 3200 240 224 8 1)
         caps.update(unsettled_capacity=240, page_heap_capacity=224)
     return caps

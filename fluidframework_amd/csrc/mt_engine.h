@@ -105,8 +105,8 @@ template <bool kLogT> struct TierLiveLdsT {
 // the launch's LDS layout becomes constant offsets and the capacities immediates, so the
 // kernel keeps none of them in registers (the bench's C3 tight tier, mt_replay.hip launch_paged).
 // kHMT: the page metadata (observer length, leaf-block counts, needsScour flags) stays in HBM
-// (mt_paged.h "page metadata accessors"): 1 LDS byte per page (its segment count) instead of
-// 12, for documents of thousands of pages (the skewed bench's long classes); replay only (no
+// (mt_paged.h "page metadata accessors"): no LDS per page instead of 12 bytes, for documents
+// of thousands of pages (the skewed bench's long classes); replay only (no
 // delta log, no ordinals).
 template <bool kLogT, bool kNarrowT = false, bool kBigT = false, bool kPackedT = false, int kPPT = 0, int kPHT = 0,
           int kUTT = 0, bool kHMT = false>

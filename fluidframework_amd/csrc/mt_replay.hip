@@ -1101,8 +1101,8 @@ __global__ void k_mark_big(DevState st, const int64_t *off, int resume_set) {
 }
 // One paged launch over every document (those not at stage pc.stage exit at once); big: the
 // documents of the big region (the growth step's launches).
-// Documents of many pages replay with their page metadata in HBM (TierPagedT kHM: 1 LDS byte
-// per page instead of 12, so more of them share a CU); the bench's C3 / C4 documents (< 300
+// Documents of many pages replay with their page metadata in HBM (TierPagedT kHM: no LDS per
+// page instead of 12 bytes, so more of them share a CU); the bench's C3 / C4 documents (< 300
 // pages) keep it in LDS (no global load on their page searches).
 #ifndef MT_HM_PAGES
 #define MT_HM_PAGES 512
