@@ -38,12 +38,12 @@ def class_caps(bench, cfg, max_ops):
     if max_ops > 10000:
         for k in ("lds_page_capacity", "lds_unsettled_capacity", "lds_page_heap_capacity", "lds_narrow_overlap"):
             caps.pop(k, None)
-        # unsettled table / heap at the measured peaks plus a margin (c3skew: <= 203 / 183 in
-        # every class; the growth step takes a document past them): 26 + 8 fewer LDS bytes per
-        # entry over the C3 full tier's 320 / 512 -- with the page metadata in HBM (>= 512 pages,
-        # mt_replay.hip use_hm) a 200k-message document takes 22.5 KB of LDS: 7 per CU
-        # (profiles/tools/lds_footprint.py 3200 240 224 8 1)
-        caps.update(unsettled_capacity=240, page_heap_capacity=224)
+        # unsettled table / heap at the measured peaks plus a margin (c3skew classes above 10k
+        # messages: <= 194 / 181; the growth step takes a document past them -- none on the
+        # bench's streams, profiles/r5/bench_c3skew_r5t.json): with the page metadata in HBM
+        # (>= 512 pages, mt_replay.hip use_hm) a 200k-message document takes 21.7 KB of LDS,
+        # 7 per CU, a 100k one 16.3 KB, 10 per CU (profiles/tools/lds_footprint.py 1650 216 200 8 1)
+        caps.update(unsettled_capacity=216, page_heap_capacity=200)
     return caps
 
 
