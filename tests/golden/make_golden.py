@@ -282,6 +282,9 @@ LIVE_FIXTURES = {
     # long runs: thousands of segments, many zamboni passes around pending segments
     "ref_live_long": (dict(LIVE_BASE, seed=4343, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.004,
                            p_ack=0.6, n_keys=8, n_values=16), 3),
+    # a long-lived participant: 20k events, thousands of live segments, reconnects
+    "ref_live_xl": (dict(LIVE_BASE, seed=4747, steps=20000, writers=8, lag=48, p_local=0.3, p_reconnect=0.001,
+                         p_ack=0.6, n_keys=8, n_values=16), 3),
     # bench.py --config live: long streams without reconnects, replicated across documents
     "ref_live_bench": (dict(LIVE_BASE, seed=4545, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.0,
                             p_ack=0.6, n_keys=8, n_values=16), 8),

@@ -13,7 +13,7 @@ import pytest
 import golden_util as gu
 from fluidframework_amd.wire import F_ACK, F_LOCAL, Batch, Interner
 
-LIVE_FIXTURES = ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep"]
+LIVE_FIXTURES = ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep", "ref_live_xl"]
 
 
 def _msg(ev):

@@ -232,7 +232,7 @@ def _replay_live_with_reconnects(oracle_lib, doc, interner):
     yield d, errs
 
 
-@pytest.mark.parametrize("name", ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep"])
+@pytest.mark.parametrize("name", ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep", "ref_live_xl"])
 def test_oracle_live_reconnects_match_reference(oracle_lib, name):
     """Every live fixture document, reconnects included: each regenerated op list equals the
     reference's, and the final state (text, length, leaves, segment table, property sets,
