@@ -19,7 +19,9 @@
 //    boundary, range_mark, scour_range, pack at level 0) run on it unchanged; a page that
 //    reaches MaxNodesInBlock leaf blocks is split 4|4 after the op (blk_split_up records it),
 //    a page that underflows is repacked with its siblings (pack at level 1) in HBM;
-//  * the zamboni heap is the flat one (LDS); a uid -> page map in HBM locates its segments.
+//  * the zamboni heap is the flat one (LDS); a uid -> page map in HBM locates its segments;
+//  * documents of thousands of pages (T::kHM) keep every PageMeta in HBM: the window's page
+//    has its own in registers, searches read a chunk's 64 observer lengths once (sob).
 #pragma once
 #include "mt_engine.h"
 
