@@ -68,6 +68,12 @@ def parse():
     return ap.parse_args()
 
 
+def progress(rank, msg):
+    """A progress line on stderr (rank 0): long runs write something every few seconds."""
+    if rank == 0:
+        print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+
 def host_cores():
     """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota (a GPU
     box shows the whole machine in os.cpu_count() but grants a share of it)."""
@@ -726,14 +732,16 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
     seed_off, seed = mt.generated_seeds(cfg, doc_base)
     mt.load_initial_text(seed_off, seed)
     n_ops = batch.n_ops
+    progress(rank, f"generated {docs} documents, {n_ops} messages ({t_gen:.1f} s)")
 
     def step():
         mt.reset()
         batch.apply_async()
 
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
         step()
         mt.sync()
+        progress(rank, f"warmup step {k + 1}/{args.warmup}")
 
     def barrier():
         if dist is not None:
@@ -743,10 +751,11 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
     barrier()
     mt.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         step()
         mt.sync()                     # per-step sync to read this step's kernel events
         kernel_ms.append(mt.last_kernel_ms())
+        progress(rank, f"step {k + 1}/{args.steps}: {kernel_ms[-1]:.0f} ms")   # (stderr, after the sync)
     mt.sync()
     barrier()
     elapsed = time.perf_counter() - t0
