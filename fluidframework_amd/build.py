@@ -64,11 +64,13 @@ def build(force=False, verbose=False):
     tag = os.path.splitext(os.path.basename(OUT))[0]   # variant libraries (MT_OUT) build apart
     obj_dir = os.path.join(OBJ_DIR, tag)
     os.makedirs(obj_dir, exist_ok=True)
-    stamp = os.path.join(obj_dir, "flags.txt")   # objects built with other flags are rebuilt
+    # objects built with other flags are rebuilt; the stamp names the flags only once a build
+    # with them has linked (an interrupted rebuild must not leave old-flag objects looking fresh)
+    stamp = os.path.join(obj_dir, "flags.txt")
     if not os.path.exists(stamp) or open(stamp).read() != " ".join(FLAGS):
         force = True
-        with open(stamp, "w") as fh:
-            fh.write(" ".join(FLAGS))
+        if os.path.exists(stamp):
+            os.remove(stamp)
     # MT_ONLY=P_C3,P_C4: an A/B variant that recompiles only those kernels; the other objects
     # come from the product build (_build/libmtreplay)
     only = [x for x in os.environ.get("MT_ONLY", "").split(",") if x]
@@ -116,6 +118,8 @@ def build(force=False, verbose=False):
         print(" ".join(cmd))
     subprocess.check_call(cmd)
     os.replace(OUT + ".tmp", OUT)
+    with open(stamp, "w") as fh:
+        fh.write(" ".join(FLAGS))
     return OUT
 
 

@@ -51,6 +51,8 @@ FIXTURES = {
     # C3-mix document of 60k and one of 100k messages
     "ref_c3_60k": ("c3", {"ops": 60000, "seed": 6060}, 1),
     "ref_c3_xl": ("c3", {"ops": 100000, "seed": 10100}, 1),
+    # the c3skew cap: one C3-mix document of 200k messages (~3 000 pages at its peak)
+    "ref_c3_200k": ("c3", {"ops": 200000, "seed": 20200}, 1),
     "ref_small": ("c2", {"ops": 60, "seed_len": 5, "writers": 3, "lag": 6}, 24),
     "ref_ext": (None, {"ext": True, "seed": 77, "ops": 700, "writers": 5, "lag": 40, "seed_len": 40,
                        "p_insert": 0.5, "p_remove": 0.3, "text_max": 12, "p_newline": 0.08,

@@ -20,8 +20,9 @@ ALL_FIXTURES = ["ref_small", "ref_c2", "ref_c3", "ref_c4", "ref_ext", "ref_ext_l
 FULL_FIXTURES = ["ref_c3_full", "ref_c4_full"]
 # long-lived documents (30k messages)
 LONG_FIXTURES = ["ref_c3_long"]
-# the skewed bench's long classes: one 60k- and one 100k-message C3 document (1k-1.6k pages)
-XL_FIXTURES = ["ref_c3_60k", "ref_c3_xl"]
+# the skewed bench's long classes: one 60k-, one 100k- and one 200k-message C3 document (the
+# c3skew cap; 1k-3k pages)
+XL_FIXTURES = ["ref_c3_60k", "ref_c3_xl", "ref_c3_200k"]
 # more clients' overlapping removes unsettled at once than the 63 overlap slots (paged tiers:
 # overflow sets)
 WIDE_FIXTURES = ["ref_wide400", "ref_wide_long"]

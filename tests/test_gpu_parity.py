@@ -802,7 +802,7 @@ def test_gpu_default_handle_is_unbounded(name):
 # (each capacity set once per fixture length: the 100k document at the 200k class's
 # capacities and through growth from 12 pages, the 60k one at the uniform C3 and 100k class's)
 XL_CASES = [("ref_c3_xl", "class_200k"), ("ref_c3_xl", "grow"), ("ref_c3_60k", "c3_bench"),
-            ("ref_c3_60k", "class_100k")]
+            ("ref_c3_60k", "class_100k"), ("ref_c3_200k", "class_200k")]
 
 
 @pytest.mark.parametrize("name,caps", XL_CASES)
@@ -845,6 +845,10 @@ HM_CASES = {
     # the skewed bench's long classes: 1.6k / 3.2k pages from the start
     "class_100k": ("ref_c3_60k", lambda b, bs, cfg: bs.class_caps(b, cfg, 100000)),
     "class_200k": ("ref_c3_xl", lambda b, bs, cfg: bs.class_caps(b, cfg, 200000)),
+    # the c3skew cap itself: a 200k-message document (~3k pages) at its class's capacities, and
+    # grown from 12 pages round after round
+    "class_200k_cap": ("ref_c3_200k", lambda b, bs, cfg: bs.class_caps(b, cfg, 200000)),
+    "grow_200k": ("ref_c3_200k", lambda b, bs, cfg: TIERS["grow"]),
     # 12 pages at first: growth rounds until the big region passes 512 pages (P_BIG_HM)
     "grow_60k": ("ref_c3_60k", lambda b, bs, cfg: TIERS["grow"]),
     # more concurrent overlapping removers than the 63 slots: overflow sets on the kHM tier
@@ -882,7 +886,7 @@ def test_gpu_hbm_page_metadata_matches_reference(case):
         if errs:
             bad.append((doc["doc"], errs))
     assert not bad, bad
-    if case == "grow_60k":
+    if case in ("grow_60k", "grow_200k"):
         assert mt.last_grown()["grown"] >= 1
 
 
