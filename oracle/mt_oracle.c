@@ -81,6 +81,14 @@ typedef struct Block {
     int count;
     Node *ch[MAXN + 1];
     int needs_scour;       /* -1 undefined, 0 false, 1 true */
+    /* cached aggregates of the subtree (the restatement's stand-in for the reference's
+       cachedLength + PartialSequenceLengths, MT/mergeTree.ts:1692-1732, partialLengths.ts):
+       c_obs = its length in the local client's view (sum of localNetLength), c_chg = the
+       largest seq / removedSeq in it (INT32_MAX for an unacked one), so every view with
+       refSeq >= c_chg sees exactly c_obs; valid while c_ok (cleared up the parent chain by
+       every change below, blk_dirty) */
+    int32_t c_obs, c_chg;
+    int c_ok;
 } Block;
 
 typedef struct HeapEnt {
@@ -112,6 +120,8 @@ struct orc_doc {
     int32_t local_seq;     /* collabWindow.localSeq */
     Group *pend_head, *pend_tail;   /* pendingSegments */
     int32_t n_pend;
+    Seg **segv;            /* the segments in document order (read-outs by index), valid while */
+    int32_t segv_n, segv_cap, segv_ok;   /* segv_ok: cleared by every mutating entry point */
 };
 
 typedef void (*seg_fn)(Seg *, void *);
@@ -235,7 +245,14 @@ static Seg *make_text_seg(orc_doc *d, const uint16_t *text, int32_t len) {
     if (len) memcpy(s->text, text, sizeof(uint16_t) * len);
     return s;
 }
+/* a block's children or a leaf below it changed: its cached aggregates and its ancestors'
+   are stale (a stale block's ancestors are always stale, so the walk stops at the first one) */
+static void blk_dirty(Block *b) {
+    for (; b && b->c_ok; b = b->n.parent) b->c_ok = 0;
+}
+static inline void seg_dirty(Seg *s) { blk_dirty(s->n.parent); }
 static void assign_child(Block *b, Node *child, int index) {  /* assignChild :374-381 */
+    blk_dirty(b);
     child->parent = b;
     child->index = index;
     b->ch[index] = child;
@@ -316,7 +333,41 @@ static int32_t seg_partial(const Seg *s, int32_t ref_seq, int32_t client) {
                                              (s->rseq != UNASSIGNED && s->rseq <= ref_seq));
     return s->len * (ins - rem);
 }
+static inline int32_t seg_chg(const Seg *s) {
+    int32_t c = s->seq == UNASSIGNED ? INT32_MAX : s->seq;
+    if (s->rseq != RSEQ_NONE) {
+        const int32_t r = s->rseq == UNASSIGNED ? INT32_MAX : s->rseq;
+        if (r > c) c = r;
+    }
+    return c;
+}
+static void blk_refresh(Block *b) {
+    if (b->c_ok) return;
+    int32_t obs = 0, chg = INT32_MIN;
+    for (int i = 0; i < b->count; i++) {
+        const Node *c = b->ch[i];
+        if (c->leaf) {
+            const Seg *s = (const Seg *)c;
+            obs += local_net_length(s);
+            const int32_t x = seg_chg(s);
+            if (x > chg) chg = x;
+        } else {
+            Block *cb = (Block *)c;
+            blk_refresh(cb);
+            obs += cb->c_obs;
+            if (cb->c_chg > chg) chg = cb->c_chg;
+        }
+    }
+    b->c_obs = obs;
+    b->c_chg = chg;
+    b->c_ok = 1;
+}
+/* A block's partial length for a remote view: the sum of its leaves' terms -- equal to its
+   local length when every segment below was inserted (and removed, if it is) at or below
+   refSeq: then each term is len * (1 - removed) = localNetLength. */
 static int32_t block_partial(const Block *b, int32_t ref_seq, int32_t client) {
+    blk_refresh((Block *)b);
+    if (b->c_chg <= ref_seq) return b->c_obs;
     int32_t sum = 0;
     for (int i = 0; i < b->count; i++)
         sum += b->ch[i]->leaf ? seg_partial((const Seg *)b->ch[i], ref_seq, client)
@@ -324,16 +375,36 @@ static int32_t block_partial(const Block *b, int32_t ref_seq, int32_t client) {
     return sum;
 }
 
+#ifdef ORC_CACHE_CHECK
+/* the aggregates recomputed from the leaves (cache check builds: tests of the caching) */
+static int32_t node_len_slow(const Node *n, int32_t ref_seq, int32_t client) {
+    if (n->leaf) {
+        const Seg *s = (const Seg *)n;
+        return client == OBSERVER ? local_net_length(s) : seg_partial(s, ref_seq, client);
+    }
+    const Block *b = (const Block *)n;
+    int32_t sum = 0;
+    for (int i = 0; i < b->count; i++) sum += node_len_slow(b->ch[i], ref_seq, client);
+    return sum;
+}
+#endif
 /* nodeLength :1692-1732.  Interior nodes read PartialSequenceLengths.getPartialLength
    (blockLength :1664-1670): the sum of their leaves' partial terms (seg_partial); leaves
    their visibility in the view. */
 static int32_t node_len(const Node *n, int32_t ref_seq, int32_t client) {
     if (!n->leaf) {
         const Block *b = (const Block *)n;
-        int32_t sum = 0;
-        if (client != OBSERVER) return block_partial(b, ref_seq, client);
-        for (int i = 0; i < b->count; i++) sum += node_len(b->ch[i], ref_seq, client);
-        return sum;
+        int32_t r;
+        if (client != OBSERVER) {
+            r = block_partial(b, ref_seq, client);
+        } else {
+            blk_refresh((Block *)b);
+            r = b->c_obs;
+        }
+#ifdef ORC_CACHE_CHECK
+        if (r != node_len_slow(n, ref_seq, client)) abort();
+#endif
+        return r;
     }
     const Seg *s = (const Seg *)n;
     if (client == OBSERVER) return local_net_length(s);
@@ -426,6 +497,7 @@ static void seg_append(orc_doc *d, Seg *prev, const Seg *s) {
     }
     memcpy(prev->text + prev->len, s->text, sizeof(uint16_t) * s->len);
     prev->len += s->len;
+    seg_dirty(prev);
 }
 
 /* scourNode :1322-1398 */
@@ -442,6 +514,7 @@ static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
                 if (s->rseq > d->min_seq) {
                     hold[(*nhold)++] = child;
                 } else {
+                    blk_dirty(s->n.parent);
                     s->n.parent = NULL;            /* unlink */
                     d->maint[2]++;                 /* UNLINK :1343-1348 */
                 }
@@ -451,6 +524,7 @@ static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
                          local_net_length(s) > 0;
                 if (ok) {
                     seg_append(d, prev, s);
+                    blk_dirty(s->n.parent);
                     s->n.parent = NULL;
                     d->maint[1]++;                 /* APPEND :1368-1373 */
                 } else {
@@ -476,6 +550,7 @@ static void pack(orc_doc *d, Block *block) {
     for (int ci = 0; ci < parent->count; ci++) {
         Block *cb = (Block *)parent->ch[ci];
         scour_node(d, cb, hold, &nhold);
+        blk_dirty(parent);
         cb->n.parent = NULL;
     }
     int total = nhold;
@@ -498,6 +573,7 @@ static void pack(orc_doc *d, Block *block) {
         assign_child(parent, &pb->n, ni);
     }
     parent->count = child_count;
+    blk_dirty(parent);
     if (parent->count < MAXN / 2 && parent->n.parent) pack(d, parent);
 }
 
@@ -513,6 +589,7 @@ static void zamboni(orc_doc *d) {
             scour_node(d, block, hold, &nhold);
             block->needs_scour = 0;
             if (nhold < block->count) {
+                blk_dirty(block);
                 block->count = nhold;
                 for (int j = 0; j < nhold; j++) assign_child(block, hold[j], j);
                 if (block->count < MAXN / 2 && block->n.parent) pack(d, block);
@@ -528,6 +605,7 @@ static Block theUnfinishedNode;   /* MergeTree.theUnfinishedNode */
 static Block *split_block(orc_doc *d, Block *node) {
     int half = MAXN / 2;
     Block *nb = make_block(d, half);
+    blk_dirty(node);
     node->count = half;
     for (int i = 0; i < half; i++) {
         assign_child(nb, node->ch[half + i], i);
@@ -552,6 +630,7 @@ static Seg *split_at(orc_doc *d, Seg *s, int32_t pos) {
     if (!(pos > 0) || s->marker >= 0) return NULL;
     Seg *r = make_text_seg(d, s->text + pos, s->len - pos);
     s->len = pos;
+    seg_dirty(s);
     r->props = props_clone(d, s->props);
     if (s->props) {                                  /* copyTo: the pending counts too */
         r->pk = props_clone(d, s->pk);
@@ -669,6 +748,7 @@ static Block *inserting_walk(orc_doc *d, Block *block, int32_t pos, int32_t ref_
         new_node = &cand->n;
     }
     if (new_node) {
+        blk_dirty(block);
         for (int i = block->count; i > ci; i--) {
             block->ch[i] = block->ch[i - 1];
             block->ch[i]->index = i;
@@ -875,6 +955,7 @@ static void ack_pending_properties(Seg *s, const uint32_t *rec) {
 static void map_leaf(MapCtx *m, Seg *s) {
     orc_doc *d = m->d;
     if (m->kind == MT_OP_REMOVE) {
+        seg_dirty(s);
         if (s->rseq == UNASSIGNED) {          /* a pending local removal: replaced :2657-2662 */
             s->rclient = m->client;
             s->rseq = m->seq;
@@ -972,6 +1053,7 @@ static void ack_pending(orc_doc *d, const mt_op_rec *op, const uint32_t *props_a
             }
             s->ghead++;
             s->gn--;
+            seg_dirty(s);
             if (op->kind == MT_OP_ANNOTATE) {
                 static const uint32_t empty_rec[1] = {0};
                 ack_pending_properties(s, op->props != MT_NO_PROPS ? props_arena + op->props : empty_rec);
@@ -1020,6 +1102,7 @@ static int local_range_ok(orc_doc *d, const mt_op_rec *op) {
 
 int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
                   const uint32_t *props_arena) {
+    d->segv_ok = 0;
     if (d->status) return d->status;
     int32_t r = op->ref_seq, c = op->client, seq = op->seq;
     if (op->flags & MT_F_ACK) {             /* applyMsg of our own op's echo :805-813 */
@@ -1236,6 +1319,7 @@ void orc_free(orc_doc *d) {
     for (int i = 0; i < d->allocs.n; i++) free(d->allocs.p[i]);
     free(d->allocs.p);
     free(d->heap);
+    free(d->segv);
     free(d->dlog.p);
     free(d);
 }
@@ -1248,6 +1332,7 @@ int32_t orc_status(const orc_doc *d) { return d->status; }
    group, -2 when an output buffer is too small (the document is then left unusable). */
 int32_t orc_regenerate(orc_doc *d, int32_t kind, orc_regen_rec *out, int32_t cap, uint16_t *text,
                        int32_t text_cap, uint32_t *props, int32_t props_cap) {
+    d->segv_ok = 0;
     Group *g = d->pend_head;
     if (!g) return -1;
     d->pend_head = g->next;
@@ -1385,19 +1470,11 @@ void orc_containing(orc_doc *d, int32_t pos, int32_t ref_seq, int32_t client, in
         return;
     }
 }
-typedef struct NthAcc {
-    int32_t want, idx;
-    Seg *hit;
-} NthAcc;
-static void nth_fn(Seg *s, void *arg) {
-    NthAcc *a = (NthAcc *)arg;
-    if (a->idx++ == a->want) a->hit = s;
-}
 /* getPosition of the seg_index-th segment (document order) in view (client, refSeq); -1: none */
+static Seg *seg_at(orc_doc *d, int32_t seg_index);
 int32_t orc_position(orc_doc *d, int32_t seg_index, int32_t ref_seq, int32_t client) {
-    NthAcc a = {seg_index, 0, NULL};
-    walk_segs(&d->root->n, nth_fn, &a);
-    return a.hit ? get_position_view(&a.hit->n, ref_seq, client) : -1;
+    const Seg *hit = seg_at(d, seg_index);
+    return hit ? get_position_view(&hit->n, ref_seq, client) : -1;
 }
 
 typedef void (*seg_fn)(Seg *, void *);
@@ -1452,23 +1529,31 @@ int32_t orc_segments(orc_doc *d, int32_t *out, int32_t cap_rows) {
     walk_segs(&d->root->n, seg_fn_dump, &a);
     return a.n;
 }
-typedef struct PropAcc {
-    int32_t want, idx;
-    Seg *hit;
-} PropAcc;
-static void prop_fn(Seg *s, void *arg) {
-    PropAcc *a = (PropAcc *)arg;
-    if (a->idx++ == a->want) a->hit = s;
+static void segv_fn(Seg *s, void *arg) {
+    orc_doc *d = (orc_doc *)arg;
+    if (d->segv_n == d->segv_cap) {
+        d->segv_cap = d->segv_cap ? 2 * d->segv_cap : 1024;
+        d->segv = (Seg **)realloc(d->segv, sizeof(Seg *) * d->segv_cap);
+    }
+    d->segv[d->segv_n++] = s;
+}
+/* segment seg_index in document order (NULL: none) */
+static Seg *seg_at(orc_doc *d, int32_t seg_index) {
+    if (!d->segv_ok) {
+        d->segv_n = 0;
+        walk_segs(&d->root->n, segv_fn, d);
+        d->segv_ok = 1;
+    }
+    return seg_index >= 0 && seg_index < d->segv_n ? d->segv[seg_index] : NULL;
 }
 int32_t orc_segment_props(orc_doc *d, int32_t seg_index, uint32_t *out, int32_t cap_pairs) {
-    PropAcc a = {seg_index, 0, NULL};
-    walk_segs(&d->root->n, prop_fn, &a);
-    if (!a.hit || !a.hit->props) return -1;
-    for (int i = 0; i < a.hit->props->n && i < cap_pairs; i++) {
-        out[2 * i] = a.hit->props->key[i];
-        out[2 * i + 1] = a.hit->props->val[i];
+    const Seg *hit = seg_at(d, seg_index);
+    if (!hit || !hit->props) return -1;
+    for (int i = 0; i < hit->props->n && i < cap_pairs; i++) {
+        out[2 * i] = hit->props->key[i];
+        out[2 * i + 1] = hit->props->val[i];
     }
-    return a.hit->props->n;
+    return hit->props->n;
 }
 
 static void leaves_rec(Block *b, int32_t *out, int32_t cap, int32_t *n) {

@@ -1,8 +1,6 @@
 """Pins the CPU restatement oracle (oracle/mt_oracle.c) to the reference itself: every
 golden fixture under tests/golden/ was produced by the reference's own MergeTree/Client
 (transpiled by oracle/build_ref.py, driven by oracle/ref_harness.mjs)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -11,8 +9,6 @@ import golden_util as gu
 
 @pytest.mark.parametrize("name", gu.ALL_FIXTURES + gu.LONG_FIXTURES + gu.WIDE_FIXTURES + gu.XL_FIXTURES)
 def test_oracle_matches_reference(oracle_lib, name):
-    if name == "ref_c3_200k" and not os.environ.get("MT_SLOW_ORACLE"):
-        pytest.skip("200k messages: minutes on the C restatement (MT_SLOW_ORACLE=1 runs it)")
     fx = gu.load(name)
     interner = gu.interner_for(fx)
     for doc in fx["docs"]:
