@@ -372,9 +372,10 @@ class MergeTreeBatch:
 
     def get_overlap_arena(self, doc):
         """A paged document's overflow overlap arena (mt_get_overlap_arena)."""
-        out = np.zeros(6, dtype=np.int32)
+        out = np.zeros(7, dtype=np.int32)
         self._check(self.lib.mt_get_overlap_arena(self.h, doc, _native.ptr(out)), "mt_get_overlap_arena")
-        return dict(zip(["capacity", "fill", "half", "largest_set", "live_units", "made"], (int(x) for x in out)))
+        return dict(zip(["capacity", "fill", "half", "largest_set", "live_units", "made", "peak_fill"],
+                        (int(x) for x in out)))
 
     def get_segment_props(self, doc, i):
         pairs = np.zeros(64, dtype=np.uint32)

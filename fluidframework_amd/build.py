@@ -22,6 +22,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno
          "-Wno-unused-value", "-mllvm", "-amdgpu-use-amdgpu-trackers=1"] + os.environ.get("MT_EXTRA_FLAGS", "").split()
 
 
+# Per-instantiation compile options (the generated translation unit's first lines, e.g.
+# {"P_C3": "#define MT_PAGED_WAVES 4\n"}); none in the product build -- round 6 A/B'd the C3 tier
+# at 4 waves per SIMD and found it slower (profiles/README.md).  MT_NO_VARIANT_DEFINES=1 drops
+# them; MT_SINGLE_TU=1 builds ignore them.
+VARIANT_DEFINES = {}
+
 # what the kernel instantiations (mtk_*.o) compile from: not mt_replay.hip's host code
 KERNEL_DEPS = [p for p in DEPS if not p.endswith("mt_replay.hip")]
 
@@ -81,7 +87,9 @@ def build(force=False, verbose=False):
         link_only.append(jobs.pop()[1])
     for name, expr in variants():
         src = os.path.join(obj_dir, f"mtk_{name}.hip")
-        body = (f'#include "{os.path.join(HERE, "csrc", "mt_kernels.h")}"\n'
+        body = (("" if os.environ.get("MT_NO_VARIANT_DEFINES") else VARIANT_DEFINES.get(name, "")) +
+                f'#include "{os.path.join(HERE, "csrc", "mt_kernels.h")}"\n'
+                f'#include "{os.path.join(HERE, "csrc", "mt_variants.h")}"\n'
                 f"const void *mtk_{name}() {{ return (const void *)({expr}); }}\n")
         if not os.path.exists(src) or open(src).read() != body:
             with open(src, "w") as fh:

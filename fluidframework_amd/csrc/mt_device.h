@@ -71,8 +71,12 @@ static __host__ __device__ inline int8_t pm_flg(const PageMeta &m, int q) { retu
 #define MT_OSLOT_USE 63
 #define MT_OVF_BIT (1ull << 63)
 // overflow arena header (u16 units): u32 {top, last message that made a set, largest set
-// made, current half (0: [MT_OVF_HDR, OA/2), 1: [OA/2, OA)), units of every set made}
-#define MT_OVF_HDR 10
+// made, current half (0: [MT_OVF_HDR, mid), 1: [mid, MT_OVF_HDR + 2 (mid - MT_OVF_HDR))), units of
+// every set made, high-water mark of the half in use (units)}
+#define MT_OVF_HDR 12
+// the overflow arena's two halves are the same size, so the live sets of either always fit the
+// other (pg_ovf_compact)
+static __host__ __device__ inline int mt_ovf_mid(int OA) { return MT_OVF_HDR + (((OA - MT_OVF_HDR) / 2) & ~7); }
 #define MT_OVF_ARENA 8192      // overflow-arena units per document in the main arrays (the growth step raises it)
 #define MT_OSLOT_FREE 0x7FFFFFFF
 #define MT_PG_SLOTS 64

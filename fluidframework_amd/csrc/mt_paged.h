@@ -87,6 +87,7 @@ template <class T> struct PagedDoc {
     int ovf_maxn, ovf_half;      // the largest set made; the half sets are appended in (the
                                  // other one receives the live sets at a compaction)
     uint32_t ovf_made;           // units of every set made (diagnostic: reclamation)
+    int ovf_peak;                // the most units the half in use has held (diagnostic)
     int press;                // a compaction left the text (4) / record (5) arena more than 7/8
                               // full: a tight launch hands the document on (pg_arena_room)
     int wgrow, opbound;       // tight tier: bound on the table's growth not yet in ut_n (the
@@ -2022,12 +2023,16 @@ TD bool ovf_member(DocT<T> &d, u64 o, int c) {
     for (int k = 1; k <= n; k++) in = in || s[k] == (uint16_t)c;
     return in;
 }
-// The arena is used in two halves, [MT_OVF_HDR, OA/2) and [OA/2, OA): sets are appended in
+// The arena is used in two halves of one size, [MT_OVF_HDR, mid) and [mid, 2 mid - MT_OVF_HDR)
+// (mt_ovf_mid): sets are appended in
 // one, and a compaction (pg_ovf_compact) copies the live ones -- those a segment row still
 // names -- into the other, as the text arena's halves are compacted.  Masks hold offsets from
 // the arena's start, so a set is read the same wherever it lies.
-TD int ovf_half_lo(const PagedDoc<T> &pd, int half) { return half ? (pd.OA / 2) & ~7 : MT_OVF_HDR; }
-TD int ovf_half_end(const PagedDoc<T> &pd) { return pd.ovf_half ? pd.OA : (pd.OA / 2) & ~7; }
+TD int ovf_half_lo(const PagedDoc<T> &pd, int half) { return half ? mt_ovf_mid(pd.OA) : MT_OVF_HDR; }
+TD int ovf_half_hi(const PagedDoc<T> &pd, int half) {
+    return half ? 2 * mt_ovf_mid(pd.OA) - MT_OVF_HDR : mt_ovf_mid(pd.OA);
+}
+TD int ovf_half_end(const PagedDoc<T> &pd) { return ovf_half_hi(pd, pd.ovf_half); }
 // Adds client c to the overlap list of the window's segment i (lanes with need; wave-uniform
 // call): its overflow set, or the clients of its slot bits, copied with c into a new set.
 // false: the arena is full (the caller fails the document, diagnostic 11).
@@ -2059,6 +2064,7 @@ TD bool ovf_mark(DocT<T> &d, bool need, int i, u64 o, int c, int seq) {
         d.O[i] = (typename T::O_v)(MT_OVF_BIT | (u64)(uint32_t)off);
     }
     pd.ovf_top = top + tot;
+    pd.ovf_peak = max(pd.ovf_peak, pd.ovf_top - ovf_half_lo(pd, pd.ovf_half));
     pd.ovf_made = (uint32_t)min((u64)pd.ovf_made + (u64)tot, (u64)0xFFFFFFFFu);
     pd.ovf_last = seq;
     d.wide = 1;
@@ -2079,7 +2085,7 @@ TD void pg_ovf_compact(PagedDoc<T> &pd) {
     if (w.status) return;
     gsync_rd();
     const int nh = 1 - pd.ovf_half;
-    const int lo = ovf_half_lo(pd, nh), hi = nh ? pd.OA : (pd.OA / 2) & ~7;
+    const int lo = ovf_half_lo(pd, nh), hi = ovf_half_hi(pd, nh);
     int top = lo;
     const int np = nbr(pd.up, 1);
     for (int q = 0; q < np; q++) {
@@ -2092,7 +2098,7 @@ TD void pg_ovf_compact(PagedDoc<T> &pd) {
         const int inc = wave_scan_incl(sz);
         const int tot = bcast(inc, MT_WAVE - 1);
         if (!ballot(isset)) continue;
-        if (top + tot > hi) {   // (cannot happen: the live sets fit the half they came from)
+        if (top + tot > hi) {   // (cannot happen: the live sets fit the half they came from, of the same size)
             FAIL_INTERNAL(w);
             return;
         }
@@ -2114,6 +2120,7 @@ TD void pg_ovf_compact(PagedDoc<T> &pd) {
     gsync_rd();
     pd.ovf_half = nh;
     pd.ovf_top = top;
+    pd.ovf_peak = max(pd.ovf_peak, top - lo);
     pd.cur = -1;
     if (keep >= 0) {
         pg_win_load(pd, keep);
@@ -2420,6 +2427,7 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
     pd.ovf_maxn = 0;
     pd.ovf_half = 0;
     pd.ovf_made = 0;
+    pd.ovf_peak = 0;
     if constexpr (T::kOvf) {
         if (pd.govf) {
             const GLB_AS uint32_t *hw = (const GLB_AS uint32_t *)pd.govf;
@@ -2427,10 +2435,11 @@ TD void pg_setup(PagedDoc<T> &pd, const DevState &st, int doc, LDS_AS uint8_t *s
             pd.ovf_last = (int)hw[1];
             pd.ovf_maxn = (int)hw[2];
             pd.ovf_made = hw[4];
+            pd.ovf_peak = (int)hw[5];
             // the upper half only while the fill is above the midpoint: after a growth step
             // (the arena doubled, its contents copied at the same offsets) the sets lie in the
             // new lower half
-            pd.ovf_half = ((int)hw[3] & 1) && pd.ovf_top > ((pd.OA / 2) & ~7) ? 1 : 0;
+            pd.ovf_half = ((int)hw[3] & 1) && pd.ovf_top > mt_ovf_mid(pd.OA) ? 1 : 0;
         }
     }
 }
@@ -2566,7 +2575,9 @@ TD void pg_store(PagedDoc<T> &pd, const DevState &st) {
                 lane() == 0 ? (uint32_t)pd.ovf_top
                             : (lane() == 1 ? (uint32_t)pd.ovf_last
                                            : (lane() == 2 ? (uint32_t)pd.ovf_maxn
-                                                          : (lane() == 3 ? (uint32_t)pd.ovf_half : pd.ovf_made)));
+                                                          : (lane() == 3 ? (uint32_t)pd.ovf_half
+                                                                         : (lane() == 4 ? pd.ovf_made
+                                                                                        : (uint32_t)pd.ovf_peak))));
     }
     wsync<T>();
     const int np = nbr(up, 1);

@@ -2729,11 +2729,11 @@ int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out) {
     HostDoc hd;
     int rc = fetch_doc(h, doc, hd, false, false);
     if (rc) return rc;
-    for (int k = 0; k < 6; k++) out[k] = 0;
+    for (int k = 0; k < 7; k++) out[k] = 0;
     if (hd.ovf.size() < MT_OVF_HDR) return 0;
     uint32_t w[MT_OVF_HDR / 2];
     memcpy(w, hd.ovf.data(), sizeof(w));
-    const int OA = (int)hd.ovf.size(), mid = (OA / 2) & ~7;
+    const int OA = (int)hd.ovf.size(), mid = mt_ovf_mid(OA);
     const int half = (w[3] & 1) && (int)w[0] > mid ? 1 : 0;
     out[0] = OA;
     out[1] = (int)w[0] - (half ? mid : MT_OVF_HDR);
@@ -2746,6 +2746,7 @@ int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out) {
     offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
     for (uint32_t off : offs) out[4] += off < hd.ovf.size() ? (int)hd.ovf[off] + 1 : 0;
     out[5] = (int)std::min<uint32_t>(w[4], INT32_MAX);
+    out[6] = (int)w[5];
     return 0;
 }
 

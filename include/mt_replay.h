@@ -279,9 +279,9 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
 /* Diagnostic: a paged document's overflow overlap arena (MT_OVF_BIT sets) as
    {capacity in u16 units, fill of the current half, current half, largest set made,
    units the live sets take (the sets segment rows name, each counted once), units of every
-   set made}; zeros for a document without one.  Compaction keeps the fill bounded by the live
+   set made, the most units the half in use ever held}; zeros for a document without one.  Compaction keeps the fill bounded by the live
    sets, not by every set ever made (MT/mergeTree.ts:1322-1398 drops a list with its segment). */
-int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out /* [6] */);
+int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out /* [7] */);
 int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_t *pairs,
                          uint32_t cap_pairs, int32_t *n_pairs);
 /* ---- segment read-outs of the Client / MergeTree surface SharedSegmentSequence calls

@@ -27,8 +27,10 @@ import pyoracle  # noqa: E402
 from fluidframework_amd.wire import Batch, Interner, compact_msgs_to_dicts  # noqa: E402
 
 HARNESS = os.path.join(REPO, "oracle", "ref_harness.mjs")
-# (config, documents, ops per document): full-length documents of each bench workload
-CASES = [("c2", 64, 2000), ("c3", 24, 10000)]
+# (config, documents, ops per document): full-length documents of each bench workload, and
+# (r6) the long documents of the c3skew classes (the reference pays O(log n) per message
+# through its partial lengths, the restatement O(depth) through cached subtree aggregates)
+CASES = [("c2", 64, 2000), ("c3", 24, 10000), ("c3", 4, 40000), ("c3", 2, 100000), ("c3", 1, 200000)]
 
 
 def calibrate(name, ndocs, nops, configs):
@@ -64,15 +66,17 @@ def calibrate(name, ndocs, nops, configs):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r3", "cpu_calibration.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r6", "cpu_calibration.json")
     configs = json.load(open(os.path.join(REPO, "bench", "configs.json")))
     res = {"note": "one thread each, same op streams: the transpiled reference MergeTree (Client.applyMsg, "
                    "observer with the position-recording delta callback / with no callback) under Node vs "
                    "oracle/mt_oracle.c as bench.py times it; measured in the build container by "
                    "oracle/calibrate.py"}
     for name, nd, no in CASES:
-        res[name] = calibrate(name, nd, no, configs)
-        print(name, res[name])
+        key = name if no <= 10000 else f"{name}_{no // 1000}k"
+        res[key] = calibrate(name, nd, no, configs)
+        print(key, res[key], flush=True)
+        json.dump(res, open(out, "w"), indent=1)
     json.dump(res, open(out, "w"), indent=1)
 
 

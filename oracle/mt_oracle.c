@@ -120,6 +120,9 @@ struct orc_doc {
     int32_t local_seq;     /* collabWindow.localSeq */
     Group *pend_head, *pend_tail;   /* pendingSegments */
     int32_t n_pend;
+    int64_t ovl_units, ovl_peak;   /* sum over segments in the tree of removedClientOverlap
+                                      lists as [n, ids...] (n + 1 units each) and its maximum
+                                      after a message (tests: the device's overflow arena) */
     Seg **segv;            /* the segments in document order (read-outs by index), valid while */
     int32_t segv_n, segv_cap, segv_ok;   /* segv_ok: cleared by every mutating entry point */
 };
@@ -271,6 +274,7 @@ static void ovl_push(orc_doc *d, Seg *s, int32_t c) {   /* addOverlappingClient 
         s->ovlcap = nc;
     }
     s->ovl[s->novl++] = c;
+    if (s->n.parent) d->ovl_units += s->novl == 1 ? 2 : 1;   /* (a split's right half: parent set first) */
 }
 
 /* SegmentGroupCollection.enqueue MT/segmentGroupCollection.ts:26-29: the group joins the
@@ -515,6 +519,7 @@ static void scour_node(orc_doc *d, Block *node, Node **hold, int *nhold) {
                     hold[(*nhold)++] = child;
                 } else {
                     blk_dirty(s->n.parent);
+                    if (s->novl) d->ovl_units -= s->novl + 1;
                     s->n.parent = NULL;            /* unlink */
                     d->maint[2]++;                 /* UNLINK :1343-1348 */
                 }
@@ -1100,8 +1105,20 @@ static int local_range_ok(orc_doc *d, const mt_op_rec *op) {
     return 1;
 }
 
+static int32_t orc_apply_impl(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
+                              const uint32_t *props_arena);
 int32_t orc_apply(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
                   const uint32_t *props_arena) {
+    const int32_t r = orc_apply_impl(d, op, text_arena, props_arena);
+    if (d->ovl_units > d->ovl_peak) d->ovl_peak = d->ovl_units;
+    return r;
+}
+void orc_overlap_units(const orc_doc *d, int64_t *out) {
+    out[0] = d->ovl_units;
+    out[1] = d->ovl_peak;
+}
+static int32_t orc_apply_impl(orc_doc *d, const mt_op_rec *op, const uint16_t *text_arena,
+                              const uint32_t *props_arena) {
     d->segv_ok = 0;
     if (d->status) return d->status;
     int32_t r = op->ref_seq, c = op->client, seq = op->seq;

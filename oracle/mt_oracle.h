@@ -61,6 +61,10 @@ void orc_checksum(orc_doc *d, mt_checksum *out);
 /* mergeTreeMaintenanceCallback event counts since creation: [SPLIT, APPEND, UNLINK]
    (MT/mergeTree.ts:2264-2269, :1368-1373, :1343-1348) */
 void orc_maintenance(orc_doc *d, uint32_t *out);
+/* removedClientOverlap lists of the segments in the tree (MT/mergeTree.ts:2577-2585), counted
+   as [n, ids...] (n + 1 u16 units each, the device's overflow-set form): {now, maximum after
+   any message so far} -- the bound the device's overflow arena is tested against */
+void orc_overlap_units(const orc_doc *d, int64_t *out);
 uint64_t orc_text_hash(const uint16_t *t, int32_t n);
 /* delta log: flattened records  [seq, kind, nsegs, (pos, len, ndeltas, (key, oldval)*)*]* */
 int32_t orc_deltas(orc_doc *d, int32_t *out, int32_t cap);

@@ -64,6 +64,7 @@ def lib():
         L.orc_leaves.restype = i32
         L.orc_checksum.argtypes = [P, P]
         L.orc_maintenance.argtypes = [P, P]
+        L.orc_overlap_units.argtypes = [P, P]
         L.orc_deltas.argtypes = [P, P, i32]
         L.orc_deltas.restype = i32
         L.orc_set_record_deltas.argtypes = [P, i32]
@@ -152,6 +153,12 @@ class OracleDoc:
         m = np.zeros(3, dtype=np.uint32)
         lib().orc_maintenance(self.h, _p(m))
         return m.tolist()
+
+    def overlap_units(self):
+        """removedClientOverlap lists as overflow-set units: (now, peak after any message)."""
+        m = np.zeros(2, dtype=np.int64)
+        lib().orc_overlap_units(self.h, _p(m))
+        return int(m[0]), int(m[1])
 
     def view_length(self, ref_seq, client):
         """MergeTree.getLength(refSeq, clientId) (partial lengths: stale views included)."""

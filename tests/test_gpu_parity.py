@@ -486,16 +486,21 @@ def test_gpu_overlap_beyond_the_slots_matches_reference(tier):
 
 
 @pytest.mark.parametrize("tier", ["paged", "tight", "grow"])
-def test_gpu_overflow_sets_are_reclaimed(tier):
+def test_gpu_overflow_sets_are_reclaimed(oracle_lib, tier):
     """removedClientOverlap lists leave with their segments (zamboni unlinks or merges them,
     MT/mergeTree.ts:1322-1398).  Over a 60k-message document with 200 writers at lag 400
     (tests/golden/ref_wide_long, made by the reference) overflow sets are made all along, few
-    live at once: the arena's halves are compacted (pg_ovf_compact), so it ends far smaller than
-    the sets made over the document's life -- its fill bounded by the live sets -- and the
-    document equals the reference's."""
+    live at once: the arena's halves are compacted (pg_ovf_compact), so from a 512-unit start
+    the most units the half in use ever holds stays within twice the peak of the reference's
+    live lists (the C restatement's count of every removedClientOverlap list in the tree after
+    each message, as [n, ids...] units), the arena within four times it -- far below the units
+    made over the document's life -- and the document equals the reference's."""
     fx = gu.load("ref_wide_long")
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
+    od = oracle_lib.OracleDoc.new(a["seed"][: a["seed_off"][1]])
+    od.apply_all(a["ops"], a["text"], a["props"])
+    peak_live = od.overlap_units()[1]
     mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 21, overlap_arena_capacity=512,
                     **OVF_TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
@@ -508,6 +513,8 @@ def test_gpu_overflow_sets_are_reclaimed(tier):
         assert ar["largest_set"] >= 2                 # sets were made (clients beyond the 63 slots)
         assert ar["made"] > 2 * ar["capacity"], ar    # far more than the arena ever held: reclaimed
         assert ar["live_units"] <= ar["fill"]
+        assert ar["peak_fill"] <= 2 * peak_live, (ar, peak_live)
+        assert ar["capacity"] <= max(512, 4 * peak_live), (ar, peak_live)
 
 
 # ---------------------------------------------------------------- error model
@@ -579,6 +586,39 @@ def test_gpu_full_streams_fast_path(oracle_lib, name):
                    seg_props=[mt.get_segment_props(i, j) for j in range(len(rows))], deltas=None,
                    status=int(mt.status()[i]))
         assert not gu.compare_oracle(got, exp), i
+
+
+@pytest.mark.parametrize("name", gu.ALL_FIXTURES + ["ref_c3_long", "ref_c3_60k", "ref_wide400"])
+def test_gpu_c3_tight_tier_matches_reference(oracle_lib, name):
+    """The bench's C3 tight tier (mt_replay.hip launch_paged: P_C3, capacities fixed at compile
+    time, 32-bit overlap masks) behind a 16-segment LDS tier, so every document of every
+    fixture passes through it -- converted from the flat tier, handed over when it outgrows 192
+    pages / 220 entries or its clients above 32 overlap -- with no delta log: text, segments,
+    leaf partition and property sets equal the reference's and every checksum (delta hash
+    included) the C restatement's."""
+    import json
+    import os
+    import bench
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    a = gu.encode_docs(fx, interner)
+    cfg = dict(json.load(open(os.path.join(bench.REPO, "bench", "configs.json")))["c3"], ops=10000)
+    caps = dict(bench.capacities(cfg), lds_seg_capacity=16)
+    assert (caps["lds_page_capacity"], caps["lds_unsettled_capacity"], caps["lds_page_heap_capacity"]) == (192, 220, 192)
+    mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=0, **caps)
+    mt.load_initial_text(a["seed_off"], a["seed"])
+    mt.apply_arrays(a)
+    osums, ost = oracle_lib.replay_batch(a, threads=2)
+    assert np.array_equal(mt.status(), ost)
+    assert np.array_equal(mt.checksums(), osums)
+    bad = []
+    for i, doc in enumerate(fx["docs"]):
+        exp = dict(gu.expected(doc, interner), deltas=None)
+        got = dict(_gpu_outputs_nolog(mt, i), deltas=None)
+        errs = gu.compare_oracle(got, exp, status=int(ost[i]))
+        if errs:
+            bad.append((doc["doc"], errs))
+    assert not bad, bad[:4]
 
 
 @pytest.mark.parametrize("name", gu.FULL_FIXTURES)

@@ -285,3 +285,19 @@ def test_oracle_readouts_match_reference_in_every_view(oracle_lib, name):
             assert got is not None and got[1:] == (offset, vpos, lpos), (where, got, exp)
             assert rows[got[0]][0] == clen, where
     assert n_stale > 200000 and n_stale_cont > 1000
+
+
+@pytest.mark.parametrize("name", gu.WIDE_FIXTURES)
+def test_oracle_overlap_unit_count(oracle_lib, name):
+    """The restatement's running count of removedClientOverlap units (the bound the device's
+    overflow arena is tested against) equals a recount of the final tree's lists."""
+    fx = gu.load(name)
+    interner = gu.interner_for(fx)
+    for doc in fx["docs"]:
+        a = gu.encode_docs(fx, interner, [doc])
+        od = oracle_lib.OracleDoc.new(a["seed"][: a["seed_off"][1]])
+        od.apply_all(a["ops"], a["text"], a["props"])
+        segs = od.outputs()["segs"]
+        novl = segs[:, 5]
+        now, peak = od.overlap_units()
+        assert now == int((novl[novl > 0] + 1).sum()) and peak >= now > 0
