@@ -47,6 +47,24 @@ def class_caps(bench, cfg, max_ops):
     return caps
 
 
+def _calibration_for(bench, max_ops):
+    """(case name, port-over-reference ratio without a callback) of the calibration case whose
+    document length matches a size class (oracle/calibrate.py; the reference cannot travel)."""
+    import json
+    try:
+        cal = json.load(open(bench.CALIBRATION))
+    except (OSError, ValueError):
+        return None
+    best = None
+    for name, c in cal.items():
+        if not (isinstance(c, dict) and name.startswith("c3")):
+            continue
+        d = abs(np.log(c["ops_per_doc"] / max_ops))
+        if best is None or d < best[0]:
+            best = (d, name, c["ratio_port_over_reference_nocb"])
+    return None if best is None else (best[1], best[2])
+
+
 def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     from fluidframework_amd import MergeTreeBatch
     from fluidframework_amd.skew import shard_range_ops, size_classes, zipf_lengths
@@ -133,72 +151,96 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
                 "frac": achieved / bench.HBM_PEAK, "traffic": None,
                 "kernel": f"k_replay_paged (class <= {dom['max_ops']} messages, its own stream)",
                 "kernel_ms": dom["kernel_ms"], "alg_bytes_per_launch": dom["alg_bytes"]}
-    # oracle sample and CPU baseline: the longest and a middle document of every class (rank 0),
-    # generated by the CPU restatement on parallel host threads (its generator replays them:
-    # their checksums are the check), then replayed again from their op records, timed
+    # oracle sample and CPU baseline (rank 0): per size class, a sample of >= 4 x threads
+    # documents spread over the class's length distribution (its longest included), generated
+    # by the CPU restatement on parallel host threads (its generator replays them: their
+    # checksums are the check against the GPU's), then replayed again from their op records,
+    # timed class by class with every thread busy (documents taken longest first as threads
+    # free up).  The job's CPU time is each class's messages at its own rate, summed.
     mism, sampled, cpu = 0, 0, None
     if rank == 0 and not args.no_cpu:
         from concurrent.futures import ThreadPoolExecutor
         sys.path.insert(0, os.path.join(bench.REPO, "oracle"))
         import pyoracle
-        picks = []
-        for ri, r in enumerate(runs):
-            order = np.argsort(-lens[r["idx"]], kind="stable")
-            for j in sorted({int(order[0]), int(order[len(order) // 2])}):
-                picks.append((ri, j, int(r["idx"][j])))
         threads = args.cpu_threads or bench.host_cores()
-
+        per = max(4 * threads, 8)
+        picks = []   # (class, position in the class, document)
+        for ri, r in enumerate(runs):
+            srt = np.argsort(lens[r["idx"]], kind="stable")
+            m = min(len(srt), per)
+            sel = sorted({int(srt[q]) for q in np.linspace(0, len(srt) - 1, m).round().astype(int)})
+            picks += [(ri, j, int(r["idx"][j])) for j in sel]
         t_o = time.time()
 
         def gen(pk):
             _, _, d = pk
             g = pyoracle.generate(dict(cfg, ops=int(lens[d])), int(ids[d]), keep=True)
             g["sum"] = g.pop("doc").outputs()["checksum"]
-            print(f"c3skew: oracle document {int(ids[d])} ({int(lens[d])} messages) done ({time.time() - t_o:.1f} s)",
-                  file=sys.stderr, flush=True)
             return g
 
-        # longest first, so the 200k documents do not start last
-        order = sorted(range(len(picks)), key=lambda k: -int(lens[picks[k][2]]))
+        order = sorted(range(len(picks)), key=lambda k: -int(lens[picks[k][2]]))   # longest first
         with ThreadPoolExecutor(max(1, threads)) as ex:
             gens = dict(zip(order, ex.map(gen, [picks[k] for k in order])))
+        print(f"c3skew: oracle generated {len(picks)} sample documents ({time.time() - t_o:.1f} s)",
+              file=sys.stderr, flush=True)
         for k, (ri, j, d) in enumerate(picks):
             got = runs[ri]["mt"].checksums()[j]
             osum = gens[k]["sum"]
             sampled += 1
             mism += int(any(got[f] != osum[f] for f in ("length", "text_hash", "props_hash", "delta_hash")))
-        # the CPU baseline: the same documents' streams replayed by the restatement
-        ops, text, props, seed, doc_off, seed_off = [], [], [], [], [0], [0]
-        tb = pb = 0
-        for k in order:
-            g = gens[k]
-            o = g["ops"].copy()
-            ins = o["kind"] == 0
-            o["payload"][ins] += tb
-            hp = o["props"] != 0xFFFFFFFF
-            o["props"][hp] += pb
-            ops.append(o)
-            text.append(g["text"])
-            props.append(g["props"])
-            seed.append(g["seed"])
-            tb += len(g["text"])
-            pb += len(g["props"])
-            doc_off.append(doc_off[-1] + len(o))
-            seed_off.append(seed_off[-1] + len(g["seed"]))
-        arrays = dict(ops=np.concatenate(ops), text=np.concatenate(text), props=np.concatenate(props),
-                      seed=np.concatenate(seed), doc_off=np.asarray(doc_off, dtype=np.int64),
-                      seed_off=np.asarray(seed_off, dtype=np.int64))
-        used = min(threads, len(picks))
-        print(f"c3skew: CPU baseline replay of {len(picks)} documents on {used} threads", file=sys.stderr, flush=True)
-        t_c = time.perf_counter()
-        osums, ost = pyoracle.replay_batch(arrays, threads=used)
-        t_c = time.perf_counter() - t_c
-        n_c = int(doc_off[-1])
-        cpu = dict(value=round(n_c / t_c, 1), unit="ops/s", cores=used, kind="port", host_cpus=os.cpu_count(),
-                   sample=f"oracle/mt_oracle.c replay of {len(picks)} documents (the longest and a middle one of "
-                          f"every size class, {n_c} messages; the 200k-message ones bound the wall time) on "
-                          f"{used} host threads, {t_c:.2f} s")
-        mism += int(sum(osums[q] != gens[k]["sum"] for q, k in enumerate(order)) + (ost != 0).sum())
+        classes_cpu = []
+        t_job = 0.0
+        for ri, r in enumerate(runs):
+            ks = sorted((k for k in range(len(picks)) if picks[k][0] == ri), key=lambda k: -int(lens[picks[k][2]]))
+            ops, text, props, seed, doc_off, seed_off = [], [], [], [], [0], [0]
+            tb = pb = 0
+            for k in ks:
+                g = gens[k]
+                o = g["ops"].copy()
+                ins = o["kind"] == 0
+                o["payload"][ins] += tb
+                hp = o["props"] != 0xFFFFFFFF
+                o["props"][hp] += pb
+                ops.append(o)
+                text.append(g["text"])
+                props.append(g["props"])
+                seed.append(g["seed"])
+                tb += len(g["text"])
+                pb += len(g["props"])
+                doc_off.append(doc_off[-1] + len(o))
+                seed_off.append(seed_off[-1] + len(g["seed"]))
+            arrays = dict(ops=np.concatenate(ops), text=np.concatenate(text), props=np.concatenate(props),
+                          seed=np.concatenate(seed), doc_off=np.asarray(doc_off, dtype=np.int64),
+                          seed_off=np.asarray(seed_off, dtype=np.int64))
+            t_c = time.perf_counter()
+            osums, ost = pyoracle.replay_batch(arrays, threads=threads)
+            t_c = time.perf_counter() - t_c
+            mism += int(sum(osums[q] != gens[k]["sum"] for q, k in enumerate(ks)) + (ost != 0).sum())
+            n_c = int(doc_off[-1])
+            rate = n_c / t_c
+            t_job += r["ops"] / rate
+            cal = _calibration_for(bench, r["max_ops"])
+            classes_cpu.append(dict(max_ops=r["max_ops"], docs=len(ks), messages=n_c, seconds=round(t_c, 3),
+                                    ops_per_s=round(rate, 1),
+                                    reference_estimate=(round(rate / cal[1], 1) if cal else None),
+                                    calibration=(cal[0] if cal else None)))
+            print(f"c3skew: CPU class <= {r['max_ops']}: {len(ks)} documents, {n_c} messages, {t_c:.2f} s "
+                  f"({rate / 1e6:.2f} M ops/s)", file=sys.stderr, flush=True)
+        total_job = int(sum(r["ops"] for r in runs))
+        value_cpu = total_job / t_job
+        t_ref = sum(r["ops"] / c["reference_estimate"] for r, c in zip(runs, classes_cpu) if c["reference_estimate"])
+        ref_ok = all(c["reference_estimate"] for c in classes_cpu)
+        cpu = dict(value=round(value_cpu, 1), unit="ops/s", cores=threads, kind="port", host_cpus=os.cpu_count(),
+                   sample=f"oracle/mt_oracle.c replay, class by class, of {sampled} documents (>= {per} per class "
+                          f"or the whole class, spread over its lengths, longest included) on {threads} host "
+                          f"threads; the job's CPU time = each class's messages at its measured rate",
+                   per_class=classes_cpu,
+                   reference_estimate=(dict(value=round(total_job / t_ref, 1), unit="ops/s", cores=threads,
+                                            how="each class's port rate / the port-over-reference ratio measured "
+                                                "at its length (profiles/r6/cpu_calibration.json: transpiled "
+                                                "reference MergeTree, observer without a delta callback, under "
+                                                "Node, one thread each), combined like the port's")
+                                       if ref_ok else None))
     if dist is not None:
         import torch
         t = torch.tensor([1 if ok else 0], device="cuda")

@@ -233,6 +233,104 @@ class MergeTreeBatch:
                     s_.free()
         return catchup_all, clients_all
 
+    def ingest_logs(self, slices, interner=None, threads=8):
+        """Sequenced message logs in, replayed documents out, as a pipeline (SEQ/sequence.ts:579-616
+        feeds SharedSegmentSequence JSON messages): ``slices`` yields (d0, blobs) -- the JSON
+        message arrays of documents [d0, d0 + len(blobs)), in document order.  A host thread
+        encodes slice k + 1 (the native encoder, mt_opdec, its own threads inside) while this
+        thread uploads slice k (mt_batch_upload) and enqueues its replay on the handle's
+        stream, behind slice k - 1's (mt_batch_apply_async).  Arenas are reused from slice to
+        slice.  Returns the seconds each stage was busy: {"encode", "upload", "apply_wait",
+        "wall"} (apply_wait: time the caller's thread waited for the previous slice's replay)."""
+        import queue
+        import threading
+        import time as _time
+        from .opdec import MessageDecoder
+        dec = MessageDecoder(interner or Interner(synthetic=True), threads=threads)
+        q = queue.Queue(maxsize=1)                     # one encoded slice waiting for its upload
+        free_sets = queue.Queue()
+        for ps in getattr(self, "_ingest_arenas", None) or [{}, {}]:
+            free_sets.put(ps)
+        stop = threading.Event()
+        busy = {"encode": 0.0, "upload": 0.0, "apply_wait": 0.0}
+
+        def produce():
+            try:
+                for d0, blobs in slices:
+                    if stop.is_set():
+                        return
+                    pset = free_sets.get()
+                    if stop.is_set():
+                        return
+
+                    def alloc(m, dt, pset=pset):
+                        key = np.dtype(dt).str
+                        a = pset.get(key)
+                        if a is None or len(a) < m:
+                            a = np.empty(int(m * 1.25) + 64, dtype=dt)
+                            pset[key] = a
+                        return a[:m]
+                    t = _time.perf_counter()
+                    off = pset.setdefault("off", np.zeros(self.n_docs + 1, dtype=np.int64))
+                    n = len(blobs)
+                    sub = np.zeros(n + 1, dtype=np.int64)
+                    out = dec.decode_packed(blobs, alloc=alloc, doc_off_out=sub)
+                    dec.remap(out)
+                    off[: d0 + 1] = 0
+                    off[d0 + 1: d0 + n + 1] = sub[1:]
+                    off[d0 + n + 1:] = sub[-1]
+                    out["doc_off"] = off
+                    busy["encode"] += _time.perf_counter() - t
+                    q.put((out, pset))
+                q.put(None)
+            except BaseException as e:   # surfaces in the consumer
+                q.put(e)
+
+        t_wall = _time.perf_counter()
+        th = threading.Thread(target=produce, daemon=True)
+        th.start()
+        prev = None
+        try:
+            while True:
+                item = q.get()
+                if item is None:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                out, pset = item
+                t = _time.perf_counter()
+                b = self.upload(out)   # (validation + copies: the arena set is free again after)
+                busy["upload"] += _time.perf_counter() - t
+                free_sets.put(pset)
+                t = _time.perf_counter()
+                b.apply_async()        # (waits for the previous slice's replay and growth step)
+                busy["apply_wait"] += _time.perf_counter() - t
+                if prev is not None:
+                    prev.free()
+                prev = b
+            self.sync()
+        finally:
+            stop.set()
+            while th.is_alive():
+                try:
+                    item = q.get(timeout=0.05)
+                    if isinstance(item, tuple):
+                        free_sets.put(item[1])
+                except queue.Empty:
+                    pass
+                free_sets.put({})
+            th.join()
+            if prev is not None:
+                self.sync()
+                prev.free()
+            self._ingest_arenas = []
+            while not free_sets.empty():
+                ps = free_sets.get()
+                if ps:
+                    self._ingest_arenas.append(ps)
+        busy["wall"] = _time.perf_counter() - t_wall
+        return busy
+
     def extract_snapshots_raw(self):
         """mt_extract_snapshots as concatenated arrays: (counts[n_docs, 3], records, text,
         props, min_seq, cur_seq); record offsets are relative to their document's arenas."""

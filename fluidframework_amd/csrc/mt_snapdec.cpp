@@ -1261,14 +1261,27 @@ int mt_opdec_decode(mt_snapdec *s, uint32_t n_docs, const char *const *json, con
         work(0);
         for (auto &t : pool) t.join();
     }
+    // a failed document fails the call before anything is interned: the decoder's key / value
+    // tables (which later calls continue) hold only ids of documents that were returned
+    {
+        size_t tx = 0, pr = 0;
+        for (uint32_t d = 0; d < n_docs; d++) {
+            if (!s->opdocs[d].err.empty()) {
+                s->err = "document " + std::to_string(d) + ": " + s->opdocs[d].err;
+                return -1;
+            }
+            tx += s->opdocs[d].text.size();
+            pr += s->opdocs[d].props.size();
+        }
+        if (tx > 0xFFFFFFFFull || pr > 0xFFFFFFFFull) {   // mt_op_rec offsets are 32-bit
+            s->err = "encoded text / property arena exceeds 2^32 entries: decode fewer documents per call";
+            return -1;
+        }
+    }
     // phase 2: places and the batch's key / value ids, first seen in document order
     size_t no = 0, ntx = 0, npr = 0;
     for (uint32_t d = 0; d < n_docs; d++) {
         OpDocOut &o = s->opdocs[d];
-        if (!o.err.empty()) {
-            s->err = "document " + std::to_string(d) + ": " + o.err;
-            return -1;
-        }
         o.oi = no;
         o.ti = ntx;
         o.pi = npr;

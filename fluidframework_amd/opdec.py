@@ -57,9 +57,11 @@ class MessageDecoder:
                 out.append(json.dumps(m, separators=(",", ":")).encode("ascii"))   # (as JSON.stringify)
         return out
 
-    def decode_packed(self, blobs):
+    def decode_packed(self, blobs, alloc=None, doc_off_out=None):
         """mt_opdec_decode + fetch over already serialised documents: the arrays with the
-        decoder's own property ids (remap() numbers them in the interner)."""
+        decoder's own property ids (remap() numbers them in the interner).  alloc(n, dtype):
+        where the op / text / property arrays go (reused buffers: no page faults on fresh
+        memory); doc_off_out: the (n + 1) offsets' array."""
         n = len(blobs)
         jp = (ctypes.c_char_p * max(n, 1))(*blobs)
         jl = np.asarray([len(x) for x in blobs] or [0], dtype=np.uint64)
@@ -67,9 +69,11 @@ class MessageDecoder:
             raise EncodeError(self.lib.mt_snapdec_error(self.h).decode())
         no, nt, npr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self.lib.mt_opdec_sizes(self.h, ctypes.byref(no), ctypes.byref(nt), ctypes.byref(npr))
-        out = dict(ops=np.empty(no.value, dtype=OP_DTYPE), doc_off=np.zeros(n + 1, dtype=np.int64),
-                   text=np.empty(nt.value, dtype=np.uint16) if nt.value else np.zeros(1, dtype=np.uint16),
-                   props=np.empty(npr.value, dtype=np.uint32) if npr.value else np.zeros(1, dtype=np.uint32))
+        alloc = alloc or (lambda m, dt: np.empty(m, dtype=dt))
+        out = dict(ops=alloc(no.value, OP_DTYPE),
+                   doc_off=doc_off_out if doc_off_out is not None else np.zeros(n + 1, dtype=np.int64),
+                   text=alloc(nt.value, np.uint16) if nt.value else np.zeros(1, dtype=np.uint16),
+                   props=alloc(npr.value, np.uint32) if npr.value else np.zeros(1, dtype=np.uint32))
         self.lib.mt_opdec_fetch(self.h, _p(out["doc_off"]), _p(out["ops"]), _p(out["text"]), _p(out["props"]))
         return out
 

@@ -1822,6 +1822,7 @@ fail:
 /* ------------------------------------------------------------------ batch replay */
 typedef struct BatchArg {
     int32_t d0, d1;
+    int32_t *next;   /* shared: the next document to take (dynamic: documents differ in length) */
     const int64_t *doc_op_off;
     const mt_op_rec *ops;
     const uint16_t *text;
@@ -1834,7 +1835,9 @@ typedef struct BatchArg {
 
 static void *batch_worker(void *p) {
     BatchArg *a = (BatchArg *)p;
-    for (int32_t doc = a->d0; doc < a->d1; doc++) {
+    for (;;) {
+        const int32_t doc = __atomic_fetch_add(a->next, 1, __ATOMIC_RELAXED);
+        if (doc >= a->d1) break;
         orc_doc *d = orc_new(a->seed + a->seed_off[doc], (int32_t)(a->seed_off[doc + 1] - a->seed_off[doc]));
         for (int64_t i = a->doc_op_off[doc]; i < a->doc_op_off[doc + 1]; i++)
             if (orc_apply(d, &a->ops[i], a->text, a->props)) break;
@@ -1853,10 +1856,12 @@ int32_t orc_replay_batch(int32_t n_docs, const int64_t *doc_op_off, const mt_op_
     if (threads > n_docs) threads = n_docs > 0 ? n_docs : 1;
     pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
     BatchArg *args = (BatchArg *)calloc(threads, sizeof(BatchArg));
+    int32_t next = 0;   /* documents are taken in index order as threads free up */
     for (int t = 0; t < threads; t++) {
         BatchArg *a = &args[t];
-        a->d0 = (int32_t)((int64_t)n_docs * t / threads);
-        a->d1 = (int32_t)((int64_t)n_docs * (t + 1) / threads);
+        a->d0 = 0;
+        a->d1 = n_docs;
+        a->next = &next;
         a->doc_op_off = doc_op_off;
         a->ops = ops;
         a->text = text_arena;

@@ -263,6 +263,30 @@ def test_native_message_encode_refuses_combining_tables():
         MessageDecoder(Interner()).decode(["[{]"])
 
 
+def test_native_message_encode_failed_call_interns_nothing():
+    """A call that fails on one document (here the second) leaves the decoder's key / value
+    tables as they were: the next successful call numbers its properties exactly as wire.Batch
+    does on the same messages (no orphan ids of the failed call's first document)."""
+    from fluidframework_amd.opdec import EncodeError, MessageDecoder
+    from fluidframework_amd.wire import Batch
+    m = lambda seq, op: dict(clientId="a", sequenceNumber=seq, referenceSequenceNumber=seq - 1,
+                             minimumSequenceNumber=0, type="op", contents=op)
+    first = [m(1, {"type": 0, "pos1": 0, "seg": {"text": "x", "props": {"orphan": "v0"}}})]
+    good = [[m(1, {"type": 0, "pos1": 0, "seg": {"text": "y", "props": {"kept": "v1"}}}),
+             m(2, {"type": 2, "pos1": 0, "pos2": 1, "props": {"other": 7}})]]
+    ni = Interner()
+    dec = MessageDecoder(ni)
+    with pytest.raises(EncodeError, match="document 1"):
+        dec.decode([first, "[{]"])
+    na, _ = dec.decode(good)
+    pi = Interner()
+    b = Batch(pi)
+    b.add_doc("", good[0])
+    pa = b.arrays()
+    assert np.array_equal(pa["props"], na["props"]) and pa["ops"].tobytes() == na["ops"].tobytes()
+    assert pi.keys == ni.keys and pi.val_ids == ni.val_ids
+
+
 def test_native_message_encode_matches_wire_batch_on_random_streams():
     """Seeded random message streams over the encoder's whole input space -- unicode text
     (astral planes, lone surrogates), markers, GROUPs (empty too), property values of every
