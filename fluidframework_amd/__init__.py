@@ -484,6 +484,24 @@ class MergeTreeBatch:
             return None
         return [(int(pairs[2 * j]), int(pairs[2 * j + 1])) for j in range(n.value)]
 
+    def get_all_segment_props(self, doc):
+        """get_segment_props of every segment, from one copy of the document."""
+        n = ctypes.c_uint64()
+        self._check(self.lib.mt_get_all_segment_props(self.h, doc, None, 0, ctypes.byref(n)), "mt_get_all_segment_props")
+        buf = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._check(self.lib.mt_get_all_segment_props(self.h, doc, _native.ptr(buf), n.value, ctypes.byref(n)),
+                    "mt_get_all_segment_props")
+        out, w, b = [], 0, buf.tolist()
+        while w < n.value:
+            k = b[w]
+            w += 1
+            if k < 0:
+                out.append(None)
+                continue
+            out.append([(b[w + 2 * j] & 0xFFFFFFFF, b[w + 2 * j + 1] & 0xFFFFFFFF) for j in range(k)])
+            w += 2 * k
+        return out
+
     # -------------------------------------------------------------- segment read-outs
     @staticmethod
     def _seg_info(info, text):

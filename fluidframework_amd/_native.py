@@ -93,6 +93,7 @@ SIGNATURES = [
     ("mt_get_prop_runs", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
     ("mt_get_segments", _I, [_P, _U32, _P, _U32, _P, _P, _U32, _P]),
     ("mt_get_segment_props", _I, [_P, _U32, _U32, _P, _U32, _P]),
+    ("mt_get_all_segment_props", _I, [_P, _U32, _P, ctypes.c_uint64, _P]),
     ("mt_get_overlap_arena", _I, [_P, _U32, _P]),
     ("mt_get_delta_log", _I, [_P, _U32, _P, _U32, _P]),
     ("mt_delta_log_reset", _I, [_P]),

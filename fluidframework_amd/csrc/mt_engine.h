@@ -2225,6 +2225,37 @@ TD bool lds_room(DocT<T> &d, const mt_op_rec &op) {
     return ok;
 }
 
+// Live documents on the flat HBM tier (TierLiveT with TierCaps.grow): can this message be
+// applied within the handle's capacities?  0: yes; else the capacity the growth step must raise
+// (1 segments, 2 blocks, 3 heap, 4 text, 5 property records, 12 segment groups) -- checked,
+// with the text / property arenas compacted first, before the message, so that a message never
+// fails half applied (segmentGroups and the pending queue are unbounded in the reference,
+// MT/mergeTree.ts:1955-1962, MT/segmentGroupCollection.ts).  The bounds are lds_room's for the
+// tree (a message adds <= 2 segments); an insert's text plus the slack a zamboni merge may copy
+// (1/8 of the arena, >= 4096 units); a range op's records (one per segment it reaches: <= its
+// span, <= the segments) plus an insert's one; one group for a local op.
+TD int live_room(DocT<T> &d, const mt_op_rec &op) {
+    if (d.n + 3 > d.S_cap) return 1;
+    for (int l = 0; l < d.depth; l++)
+        if (nbr(d, l) + 3 + 24 > bcap(d, l)) return 2;
+    const int nb0 = nbr(d, 0);
+    if (d.heap_n + (op.kind == MT_OP_INSERT ? 1 : nb0 + 3) > d.H_cap) return 3;
+    const int nt = op.kind == MT_OP_INSERT && !(op.flags & MT_F_MARKER) ? max(op.pos2, 0) : 0;
+    const int tslack = max(d.T_cap / 8, 4096);
+    if (d.text_top + nt + tslack > d.T_cap) {
+        text_gc(d);
+        if (d.text_top + nt + tslack > d.T_cap) return 4;
+    }
+    const int span = op.kind == MT_OP_ANNOTATE ? min(max(op.pos2 - op.pos1, 0), d.n) + 2 : 0;
+    const int np = span + (op.props != MT_NO_PROPS ? 1 : 0) + MT_WAVE;
+    if (d.props_top + np > d.P_cap) {
+        props_gc(d);
+        if (d.props_top + np > d.P_cap) return 5;
+    }
+    if ((op.flags & MT_F_LOCAL) && d.g_n + 1 > d.LG) return 12;
+    return 0;
+}
+
 // One sequenced message as the engine consumes it: the record plus (prefetched) the first
 // 8 UTF-16 units of an insert's payload and whether the payload ends with '\n'.
 struct OpIn {

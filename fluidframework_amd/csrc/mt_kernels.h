@@ -62,6 +62,10 @@ struct LoadScratch {
 struct TierCaps {
     int S, B, H;
     int resume;   // TierGlb: start from resume[doc] (documents handed over by the LDS tier)
+    int grow;     // TierLiveT: a document whose next message could outgrow the handle's
+                  // capacities (live_room) stops before it and is handed to the live growth
+                  // step (retry[doc] = 1, resume[doc] = that message; stats[13] counts them,
+                  // stats[14] ORs 1 << the capacity that ran out)
 };
 
 // Client.applyMsg for every record of this document (one wavefront per document).  The
@@ -111,8 +115,9 @@ __global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_
     const GLB_AS v4i *o4 = (const GLB_AS v4i *)ops;
     const GLB_AS uint16_t *gt = (const GLB_AS uint16_t *)tin;
     const GLB_AS uint32_t *gp = (const GLB_AS uint32_t *)pin;
-    int64_t spill_at = -1;
-    for (int64_t kb = k0; kb < k1 && d.status == 0 && spill_at < 0; kb += MT_WAVE) {
+    int64_t spill_at = -1, grow_at = -1;
+    int grow_cause = 0;
+    for (int64_t kb = k0; kb < k1 && d.status == 0 && spill_at < 0 && grow_at < 0; kb += MT_WAVE) {
         const int64_t k = kb + lane();
         v4i r0 = v4i{0, 0, 0, 0}, r1 = v4i{0, 0, 0, 0};
         uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
@@ -155,6 +160,15 @@ __global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_
                 spill_at = kb + j;
                 break;
             }
+            if constexpr (T::kLive && !T::kLds) {
+                if (caps.grow) {
+                    grow_cause = live_room(d, in.op);
+                    if (grow_cause) {
+                        grow_at = kb + j;
+                        break;
+                    }
+                }
+            }
             in.pay_lo = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w0, j) |
                         ((u64)(uint32_t)__builtin_amdgcn_readlane((int)w1, j) << 32);
             in.pay_hi = (u64)(uint32_t)__builtin_amdgcn_readlane((int)w2, j) |
@@ -178,7 +192,16 @@ __global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_
             atomicAdd(st.stats + 1, 1u);
         }
     }
-    if (!T::kLds && lane() == 0) st.retry[doc] = 0;
+    if (!T::kLds && lane() == 0) {
+        if (grow_at >= 0 && d.status == 0) {   // to the live growth step, from this message
+            st.retry[doc] = 1;
+            st.resume[doc] = grow_at;
+            atomicAdd(st.stats + 13, 1u);
+            atomicOr(st.stats + 14, 1u << grow_cause);
+        } else {
+            st.retry[doc] = 0;
+        }
+    }
 #ifdef MT_PROF
     if (st.prof) {
         atomicAdd(&st.prof[lane()], d.prof[lane()]);

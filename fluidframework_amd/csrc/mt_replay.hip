@@ -701,6 +701,12 @@ static int mt_settle(mt_handle *h);
     } while (0)
 
 static TierCaps glb_caps(const mt_handle *h) { return TierCaps{0, h->st.B, 0, h->lds.S > 0 ? 1 : 0}; }
+// the live handle's HBM tier: documents that could outgrow it go to the live growth step
+static TierCaps live_caps(const mt_handle *h) {
+    TierCaps c = glb_caps(h);
+    c.grow = 1;
+    return c;
+}
 
 // A props record [count | combine << 16, (key, value) x count] lies inside the arena.
 static bool props_rec_ok(const uint32_t *props, uint64_t props_len, uint32_t off) {
@@ -1241,11 +1247,11 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
             }
         }
     } else if (h->live && h->st.DL)
-        launch_replay(MTK(R_LIVE_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
-                           h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
+        launch_replay(MTK(R_LIVE_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, live_caps(h), 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, live_caps(h));
     else if (h->live)
-        launch_replay(MTK(R_LIVE), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
-                           h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
+        launch_replay(MTK(R_LIVE), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, live_caps(h), 0),
+                           h->stream, h->st, b->ops, b->off, b->text, b->props, live_caps(h));
     else if (h->st.DL)
         launch_replay(MTK(R_GLB_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0),
                            h->stream, h->st, b->ops, b->off, b->text, b->props, glb_caps(h));
@@ -1255,7 +1261,7 @@ int mt_batch_apply_async(mt_handle *h, const mt_batch *b) {
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
-    if (h->st.PP > 0) {   // its last paged tier may hand documents to the growth step
+    if (h->st.PP > 0 || h->live) {   // its last paged / live tier may hand documents to a growth step
         h->pending = const_cast<mt_batch *>(b);
         h->pending->owner = h;
     }
@@ -1547,6 +1553,191 @@ static int grow_loop(mt_handle *h, const mt_batch *b) {
     return MT_E_HIP;
 }
 
+// ---------------------------------------------------------------- live growth step
+// Live (participant) documents replay on the flat HBM tier, whose per-document capacities
+// (segments, blocks, heap, text and property arenas, segment groups) are the handle's.  They
+// are a starting point, not a limit: a document whose next message could outgrow them
+// (live_room) stops before it and is handed here; the step doubles what ran out for the whole
+// handle -- every document's arrays are copied to the new strides (k_live_regrow) -- and
+// replays the rest of the handed-over documents' messages, round after round.  Group ids are
+// a ring of st.LG: growing it renumbers each document's outstanding groups from 1 (the
+// segments' pending-group FIFOs with them).
+struct LiveArrays {
+    int32_t S, B, H, T, P, LG;
+    int4 *segA;
+    u64 *segO;
+    uint4 *segB;
+    uint8_t *cnt;
+    int8_t *flg;
+    int2 *heap;
+    uint16_t *text;
+    uint32_t *props;
+    PendQ *segP;
+    int32_t *grp;
+    uint16_t *ordS, *ordB;
+};
+__global__ void __launch_bounds__(MT_WAVE) k_live_regrow(const DocHdr *hdr, int32_t *live, LiveArrays a, LiveArrays b) {
+    const size_t doc = blockIdx.x;
+    const DocHdr h = hdr[doc];
+    const int n = h.n_seg;
+    for (int i = lane(); i < n; i += MT_WAVE) {
+        b.segA[doc * b.S + i] = a.segA[doc * a.S + i];
+        b.segO[doc * b.S + i] = a.segO[doc * a.S + i];
+        b.segB[doc * b.S + i] = a.segB[doc * a.S + i];
+        if (a.ordS) b.ordS[doc * b.S + i] = a.ordS[doc * a.S + i];
+    }
+    for (int l = 0; l < MT_LV; l++)
+        for (int q = lane(); q < h.n_blk[l]; q += MT_WAVE) {
+            b.cnt[doc * MT_LV * b.B + (size_t)l * b.B + q] = a.cnt[doc * MT_LV * a.B + (size_t)l * a.B + q];
+            if (a.ordB) b.ordB[doc * MT_LV * b.B + (size_t)l * b.B + q] = a.ordB[doc * MT_LV * a.B + (size_t)l * a.B + q];
+        }
+    for (int q = lane(); q < h.n_blk[0]; q += MT_WAVE) b.flg[doc * b.B + q] = a.flg[doc * a.B + q];
+    for (int i = 1 + lane(); i <= h.heap_n; i += MT_WAVE) b.heap[doc * (b.H + 1) + i] = a.heap[doc * (a.H + 1) + i];
+    {   // the live half of the arenas, same offsets
+        const uint16_t *ts = a.text + doc * 2 * a.T + (size_t)h.text_half * a.T;
+        uint16_t *td = b.text + doc * 2 * b.T + (size_t)h.text_half * b.T;
+        for (int i = lane(); i < h.text_top; i += MT_WAVE) td[i] = ts[i];
+        const uint32_t *ps = a.props + doc * 2 * a.P * MT_PREC + (size_t)h.props_half * a.P * MT_PREC;
+        uint32_t *pd = b.props + doc * 2 * b.P * MT_PREC + (size_t)h.props_half * b.P * MT_PREC;
+        for (size_t i = lane(); i < (size_t)h.props_top * MT_PREC; i += MT_WAVE) pd[i] = ps[i];
+    }
+    // segment groups: outstanding ids g_head .. (ring of a.LG) -> 1 .. g_n
+    const int g_head = live[4 * doc + 1], g_n = live[4 * doc + 2];
+    const bool renum = b.LG != a.LG;
+    auto nid = [&](int x) { return x == 0 ? 0 : (renum ? (x - g_head + a.LG) % a.LG + 1 : x); };
+    for (int i = lane(); i < n; i += MT_WAVE) {
+        PendQ q = a.segP[doc * a.S + i];
+        if (renum)
+            for (int k = 0; k < 4; k++) {
+                u64 w = 0;
+                for (int j = 0; j < 4; j++) w |= (u64)(uint32_t)nid((int)((q.w[k] >> (16 * j)) & 0xFFFFull)) << (16 * j);
+                q.w[k] = w;
+            }
+        b.segP[doc * b.S + i] = q;
+    }
+    const size_t ga = doc * (size_t)(a.LG + 1) * MT_GRP_WORDS, gb = doc * (size_t)(b.LG + 1) * MT_GRP_WORDS;
+    if (!renum) {
+        for (int i = lane(); i < (a.LG + 1) * MT_GRP_WORDS; i += MT_WAVE) b.grp[gb + i] = a.grp[ga + i];
+    } else {
+        for (int k = 0; k < g_n; k++) {
+            const int x = (g_head - 1 + k) % a.LG + 1;
+            if (lane() < MT_GRP_WORDS)
+                b.grp[gb + (size_t)(k + 1) * MT_GRP_WORDS + lane()] = a.grp[ga + (size_t)x * MT_GRP_WORDS + lane()];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane() == 0) live[4 * doc + 1] = 1;
+    }
+}
+static LiveArrays live_arrays(const DevState &st) {
+    return LiveArrays{st.S, st.B, st.H, st.T, st.P, st.LG, (int4 *)st.segA, (u64 *)st.segO, (uint4 *)st.segB,
+                      (uint8_t *)st.cnt, (int8_t *)st.flg, (int2 *)st.heap, (uint16_t *)st.text, (uint32_t *)st.props,
+                      (PendQ *)st.segP, (int32_t *)st.grp, (uint16_t *)st.ordS, (uint16_t *)st.ordB};
+}
+// every document's flat arrays at the new capacities
+static int live_regrow(mt_handle *h, int S2, int B2, int H2, int T2, int P2, int LG2) {
+    DevState &st = h->st;
+    const size_t N = h->n_docs;
+    LiveArrays a = live_arrays(st), b = a;
+    b.S = S2, b.B = B2, b.H = H2, b.T = T2, b.P = P2, b.LG = LG2;
+    bool ok = true;
+    auto alloc = [&](auto **p, size_t bytes) {
+        *p = nullptr;
+        if (ok && hipMalloc((void **)p, bytes ? bytes : 16) != hipSuccess) ok = false;
+    };
+    alloc(&b.segA, N * S2 * sizeof(int4));
+    alloc(&b.segO, N * S2 * sizeof(u64));
+    alloc(&b.segB, N * S2 * sizeof(uint4));
+    alloc(&b.cnt, N * MT_LV * (size_t)B2);
+    alloc(&b.flg, N * (size_t)B2);
+    alloc(&b.heap, N * (size_t)(H2 + 1) * sizeof(int2));
+    alloc(&b.text, N * 2 * (size_t)T2 * sizeof(uint16_t));
+    alloc(&b.props, N * 2 * (size_t)P2 * MT_PREC * sizeof(uint32_t));
+    alloc(&b.segP, N * (size_t)S2 * sizeof(PendQ));
+    alloc(&b.grp, N * (size_t)(LG2 + 1) * MT_GRP_WORDS * sizeof(int32_t));
+    if (a.ordS) {
+        alloc(&b.ordS, N * (size_t)S2 * sizeof(uint16_t));
+        alloc(&b.ordB, N * (size_t)MT_LV * B2 * sizeof(uint16_t));
+    }
+    void *nb[] = {b.segA, b.segO, b.segB, b.cnt, b.flg, b.heap, b.text, b.props, b.segP, b.grp, b.ordS, b.ordB};
+    if (!ok) {
+        for (void *p : nb)
+            if (p) hipFree(p);
+        h->err = "live growth step: device allocation failed (HBM exhausted)";
+        return MT_E_HIP;
+    }
+    hipLaunchKernelGGL(k_live_regrow, dim3((unsigned)N), dim3(MT_WAVE), 0, h->stream, st.hdr, st.live, a, b);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    void *old[] = {a.segA, a.segO, a.segB, a.cnt, a.flg, a.heap, a.text, a.props, a.segP, a.grp, a.ordS, a.ordB};
+    for (void *p : old)
+        if (p) hipFree(p);
+    st.S = S2, st.B = B2, st.H = H2, st.T = T2, st.P = P2, st.LG = LG2;
+    st.segA = (decltype(st.segA))b.segA;
+    st.segO = (decltype(st.segO))b.segO;
+    st.segB = (decltype(st.segB))b.segB;
+    st.cnt = (decltype(st.cnt))b.cnt;
+    st.flg = (decltype(st.flg))b.flg;
+    st.heap = (decltype(st.heap))b.heap;
+    st.text = (decltype(st.text))b.text;
+    st.props = (decltype(st.props))b.props;
+    st.segP = (decltype(st.segP))b.segP;
+    st.grp = (decltype(st.grp))b.grp;
+    st.ordS = (decltype(st.ordS))b.ordS;
+    st.ordB = (decltype(st.ordB))b.ordB;
+    return 0;
+}
+__global__ void k_live_fail_flagged(DevState st, int cause) {
+    const int doc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (doc >= st.n_docs || !st.retry[doc]) return;
+    st.retry[doc] = 0;
+    st.hdr[doc].status = MT_DOC_CAPACITY;
+    st.hdr[doc].pad[HDR_DIAG] = cause;
+}
+static int live_grow_loop(mt_handle *h, const mt_batch *b) {
+    DevState &st = h->st;
+    st.order = b->order;
+    h->grown_last = 0;
+    h->grow_rounds_last = 0;
+    for (int round = 0; round < 40; round++) {
+        uint32_t s[2];
+        HIPCHK(h, hipMemcpy(s, st.stats + 13, sizeof(s), hipMemcpyDeviceToHost));
+        if (s[0] == 0) return 0;
+        HIPCHK(h, hipMemset(st.stats + 13, 0, sizeof(s)));
+        const uint32_t c = s[1];
+        int S2 = st.S, B2 = st.B, H2 = st.H, T2 = st.T, P2 = st.P, LG2 = st.LG;
+        if (c & (1u << 1)) S2 = 2 * st.S;
+        B2 = std::max(st.B * ((c & (1u << 2)) ? 2 : 1), (std::max(64, S2 / 2) + 63) / 64 * 64);
+        H2 = std::max(st.H * ((c & (1u << 3)) ? 2 : 1), (int)((int64_t)st.H * S2 / st.S));
+        if (c & (1u << 4)) T2 = 2 * st.T;
+        P2 = std::max(st.P * ((c & (1u << 5)) ? 2 : 1), st.P + (S2 - st.S));
+        if (c & (1u << 12)) LG2 = std::min(2 * st.LG, 65535);
+        if (S2 == st.S && B2 == st.B && H2 == st.H && T2 == st.T && P2 == st.P && LG2 == st.LG) {
+            // nothing left to grow (group ids are 16 bits): the documents fail as before
+            hipLaunchKernelGGL(k_live_fail_flagged, dim3((h->n_docs + 255) / 256), dim3(256), 0, h->stream, st, 12);
+            HIPCHK(h, hipGetLastError());
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            return 0;
+        }
+        const int rc = live_regrow(h, S2, B2, H2, T2, P2, LG2);
+        if (rc) return rc;
+        h->grown_last += s[0];
+        h->grow_rounds_last++;
+        TierCaps caps = glb_caps(h);
+        caps.resume = 1;
+        caps.grow = 1;
+        if (st.DL)
+            launch_replay(MTK(R_LIVE_LOG), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, caps, 0), h->stream,
+                          st, b->ops, b->off, b->text, b->props, caps);
+        else
+            launch_replay(MTK(R_LIVE), dim3(h->n_docs), dim3(MT_WAVE), tier_lds_bytes(false, caps, 0), h->stream, st,
+                          b->ops, b->off, b->text, b->props, caps);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    h->err = "live growth step: no progress after 40 rounds";
+    return MT_E_HIP;
+}
+
 // Waits for the stream, then runs the growth step of the last applied batch.
 static int mt_settle(mt_handle *h) {
     HIPCHK(h, hipSetDevice(h->device));
@@ -1554,7 +1745,7 @@ static int mt_settle(mt_handle *h) {
     if (!h->pending) return 0;
     mt_batch *b = h->pending;
     h->pending = nullptr;
-    const int rc = grow_loop(h, b);
+    const int rc = h->live ? live_grow_loop(h, b) : grow_loop(h, b);
     b->owner = nullptr;
     // the growth step's launches belong to the batch: the batch's timing (mt_last_kernel_ms)
     // ends after them
@@ -2767,6 +2958,27 @@ int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_
         pairs[2 * k + 1] = x[2 + 2 * k];
     }
     *n_pairs = (int32_t)x[0];
+    return 0;
+}
+
+int mt_get_all_segment_props(mt_handle *h, uint32_t doc, int32_t *out, uint64_t cap_words, uint64_t *n_words) {
+    HostDoc hd;
+    int rc = fetch_doc(h, doc, hd, false, true);
+    if (rc) return rc;
+    uint64_t w = 0;
+    for (int i = 0; i < hd.hdr.n_seg; i++) {
+        const uint32_t ph = hd.B[i].y;
+        const uint32_t *x = ph ? &hd.props[(size_t)ph * MT_PREC] : nullptr;
+        const int np = x ? (int)x[0] : -1;
+        if (out && w < cap_words) out[w] = np;
+        w++;
+        for (int k = 0; k < np; k++, w += 2)
+            if (out && w + 1 < cap_words) {
+                out[w] = (int32_t)x[1 + 2 * k];
+                out[w + 1] = (int32_t)x[2 + 2 * k];
+            }
+    }
+    if (n_words) *n_words = w;
     return 0;
 }
 

@@ -53,12 +53,13 @@ class LiveClient:
     """One GPU document replica owned by a participant client (short id 0)."""
 
     def __init__(self, seed_text="", device=0, seg_capacity=4096, text_capacity=1 << 16, delta_log_capacity=0,
-                 interner=None, lds_seg_capacity=-1):
+                 interner=None, lds_seg_capacity=-1, live_group_capacity=0):
         # lds_seg_capacity > 0: each flush stages the document in LDS (TierLiveLdsT) while it
-        # fits, continuing in the HBM tier when it outgrows it
+        # fits, continuing in the HBM tier when it outgrows it.  The capacities are where the
+        # document starts: the live growth step raises what it outgrows (mt_replay.hip)
         self.mt = MergeTreeBatch(1, device=device, seg_capacity=seg_capacity, text_capacity=text_capacity,
                                  lds_seg_capacity=lds_seg_capacity, delta_log_capacity=delta_log_capacity,
-                                 live_client=1)
+                                 live_client=1, live_group_capacity=live_group_capacity)
         units = np.frombuffer(seed_text.encode("utf-16-le"), dtype="<u2")
         self.mt.load_initial_text(np.array([0, len(units)], dtype=np.int64),
                                   units if len(units) else np.zeros(1, dtype=np.uint16))

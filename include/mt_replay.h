@@ -282,6 +282,11 @@ int mt_get_segments(mt_handle *h, uint32_t doc, int32_t *rows, uint32_t cap_rows
    set made, the most units the half in use ever held}; zeros for a document without one.  Compaction keeps the fill bounded by the live
    sets, not by every set ever made (MT/mergeTree.ts:1322-1398 drops a list with its segment). */
 int mt_get_overlap_arena(mt_handle *h, uint32_t doc, int32_t *out /* [7] */);
+/* Every segment's property set in document order, from one copy of the document: per segment
+   [n, (key, value) x n] (n = -1: properties undefined); *n_words = the words written or, with
+   out = NULL / a short buffer, needed.  (mt_get_segment_props one segment at a time copies the
+   document each call.) */
+int mt_get_all_segment_props(mt_handle *h, uint32_t doc, int32_t *out, uint64_t cap_words, uint64_t *n_words);
 int mt_get_segment_props(mt_handle *h, uint32_t doc, uint32_t seg_index, uint32_t *pairs,
                          uint32_t cap_pairs, int32_t *n_pairs);
 /* ---- segment read-outs of the Client / MergeTree surface SharedSegmentSequence calls

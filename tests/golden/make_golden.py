@@ -7,7 +7,8 @@ fixture holds, per document, the input op log (compact messages) and the referen
 outputs (text, length, property runs, leaf-block partition, segment table, every delta
 callback).  The fixtures are data, not reference source.
 
-    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --events | --live | --only name,name]
+    python3 tests/golden/make_golden.py [--snapshots | --farm | --errors | --rich | --events | --live |
+                                         --readouts-xl | --only name,name]
 """
 import gzip
 import json
@@ -252,6 +253,11 @@ def make_events_fixture(name="ref_events", sources=EVENTS_FROM):
     print(name, len(out), "docs", sum(len(d["events"]) for d in out), "events")
 
 
+# long documents grown through page splits and repacks (>= 1k pages): read-outs on the paged
+# and HBM-page-metadata (kHM) tiers
+READOUTS_XL_FROM = [("ref_c3_60k", 1), ("ref_wide_long", 1)]
+
+
 # Read-outs of the final replicas (harness "readouts"): MergeTree.getLength(refSeq, clientId),
 # getContainingSegment(pos, refSeq, clientId) and getPosition in the observer's and the
 # writers' views, on the events fixture's streams.
@@ -287,6 +293,10 @@ LIVE_FIXTURES = {
     # a long-lived participant: 20k events, thousands of live segments, reconnects
     "ref_live_xl": (dict(LIVE_BASE, seed=4747, steps=20000, writers=8, lag=48, p_local=0.3, p_reconnect=0.001,
                          p_ack=0.6, n_keys=8, n_values=16), 3),
+    # a participant over 60k events (~18k live segments, thousands of pending groups over its
+    # life): the default live handle grows its capacities round after round (live growth step)
+    "ref_live_60k": (dict(LIVE_BASE, seed=4848, steps=60000, writers=8, lag=48, p_local=0.3, p_reconnect=0.0005,
+                          p_ack=0.6, n_keys=8, n_values=16), 1),
     # bench.py --config live: long streams without reconnects, replicated across documents
     "ref_live_bench": (dict(LIVE_BASE, seed=4545, steps=4000, writers=8, lag=48, p_local=0.3, p_reconnect=0.0,
                             p_ack=0.6, n_keys=8, n_values=16), 8),
@@ -300,8 +310,10 @@ LIVE_FIXTURES = {
 }
 
 
-def make_live_fixtures():
+def make_live_fixtures(only=None):
     for name, (cfg, ndocs) in LIVE_FIXTURES.items():
+        if only and name not in only:
+            continue
         with tempfile.TemporaryDirectory() as td:
             cp, op = os.path.join(td, "cfg.json"), os.path.join(td, "out.json")
             json.dump(cfg, open(cp, "w"))
@@ -317,7 +329,8 @@ def make_live_fixtures():
 def main():
     subprocess.check_call([sys.executable, os.path.join(REPO, "oracle", "build_ref.py")])
     if "--live" in sys.argv[1:]:
-        make_live_fixtures()
+        only = sys.argv[sys.argv.index("--live") + 1].split(",") if len(sys.argv) > sys.argv.index("--live") + 1 else None
+        make_live_fixtures(only)
         return
     if "--snapshots" in sys.argv[1:]:
         make_snapshot_fixtures()
@@ -337,6 +350,9 @@ def main():
         make_events_fixture("ref_events_wide", EVENTS_WIDE_FROM)
         make_readouts_fixture()
         make_readouts_fixture("ref_readouts_wide", EVENTS_WIDE_FROM)
+        return
+    if "--readouts-xl" in sys.argv[1:]:
+        make_readouts_fixture("ref_readouts_xl", READOUTS_XL_FROM)
         return
     if "--wide" in sys.argv[1:]:   # (only the overflow-set fixtures)
         make_events_fixture("ref_events_wide", EVENTS_WIDE_FROM)
@@ -375,6 +391,7 @@ def main():
     make_events_fixture("ref_events_wide", EVENTS_WIDE_FROM)
     make_readouts_fixture()
     make_readouts_fixture("ref_readouts_wide", EVENTS_WIDE_FROM)
+    make_readouts_fixture("ref_readouts_xl", READOUTS_XL_FROM)
     make_live_fixtures()
 
 

@@ -71,9 +71,12 @@ if (mode === "encode") {
     // live-client streams (ref_live*): one liveClient batch, one GpuClient per document; local
     // ops through insertSegmentLocal / removeRangeLocal / annotateRangeLocal, sequenced messages
     // (acks included) through applyMsg, reconnects through regeneratePendingOp
+    // (extra[0] "default": the drop-in default -- no capacity options; the live growth step
+    // raises whatever the documents outgrow; no delta log)
     const { GpuMergeTreeBatch } = require(path.join(repo, "fluidframework_amd", "js", "index.js"));
-    const b = new GpuMergeTreeBatch(fx.docs.length, { segCapacity: 16384, textCapacity: 1 << 17, liveClient: 1,
-        deltaLogCapacity: 1 << 16 });
+    const dflt = extra[0] === "default";
+    const b = new GpuMergeTreeBatch(fx.docs.length, dflt ? { liveClient: 1 }
+        : { segCapacity: 16384, textCapacity: 1 << 17, liveClient: 1, deltaLogCapacity: 1 << 16 });
     b.loadInitialText(fx.docs.map((d) => d.seed_text));
     const docs = [];
     const deltas = fx.docs.map(() => []);
@@ -81,7 +84,7 @@ if (mode === "encode") {
         const c = b.client(i);
         c.startOrUpdateCollaboration("local-0");
         // the reference harness's record: [seq or -1, operation, n, [[position, length(, propertyDeltas)]...]]
-        c.mergeTreeDeltaCallback = (opArgs, dargs) => {
+        if (!dflt) c.mergeTreeDeltaCallback = (opArgs, dargs) => {
             deltas[i].push([opArgs.sequencedMessage ? opArgs.sequencedMessage.sequenceNumber : -1, dargs.operation,
                 dargs.deltaSegments.length, dargs.deltaSegments.map((x) => (x.propertyDeltas !== undefined
                     ? [x.position, x.segment.cachedLength, x.propertyDeltas] : [x.position, x.segment.cachedLength]))]);

@@ -106,7 +106,9 @@ def test_gpu_segment_ordinals_need_the_rich_log():
 
 
 # ---------------------------------------------------------------- read-outs
-READ_TIERS = dict(ORD_TIERS, paged_noord=ORD_TIERS["paged"])
+READ_TIERS = dict(ORD_TIERS, paged_noord=ORD_TIERS["paged"],
+                  # >= 512 pages and no delta log: the page metadata in HBM (mt_replay.hip use_hm)
+                  hm=dict(lds_seg_capacity=-1, page_capacity=1600, unsettled_capacity=2048, page_heap_capacity=2048))
 
 
 def test_reference_readouts_differ_from_leaves_only_in_stale_views():
@@ -128,7 +130,7 @@ def test_reference_readouts_differ_from_leaves_only_in_stale_views():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tier", list(READ_TIERS))
-@pytest.mark.parametrize("name", ["ref_readouts", "ref_readouts_wide"])
+@pytest.mark.parametrize("name", ["ref_readouts", "ref_readouts_wide", "ref_readouts_xl"])
 def test_gpu_readouts_match_reference(tier, name):
     """MergeTree.getLength(refSeq, clientId), getContainingSegment(pos, refSeq, clientId) and
     getPosition (MT/mergeTree.ts:1610-1667, Client.getPosition / getContainingSegment) of the
@@ -139,10 +141,16 @@ def test_gpu_readouts_match_reference(tier, name):
     need not add up to their leaves (51 239 of 211 951 differ; 1 079 containing queries find
     no segment); ordinals too on every tier that keeps them.  ref_readouts_wide: the same on
     the paged tiers for the 200-writer / lag-400 streams (views through overflow overlap
-    sets)."""
+    sets).  ref_readouts_xl: a 60k-message C3 document and the 60k-message 200-writer one, grown
+    through page splits and repacks to ~1k pages -- on the growing paged tiers and with the page
+    metadata in HBM (kHM), stale views included."""
     from fluidframework_amd import MergeTreeBatch
-    if name == "ref_readouts_wide" and tier not in PAGED_TIERS + ("paged_noord",):
+    if name == "ref_readouts_wide" and tier not in PAGED_TIERS + ("paged_noord", "hm"):
         pytest.skip("more than 63 concurrent overlapping removers: paged layout only")
+    if name == "ref_readouts_xl" and tier not in ("paged", "grow", "paged_noord", "hm"):
+        pytest.skip("60k-message documents: the growing paged tiers and the kHM tier")
+    if tier == "hm" and name == "ref_readouts":
+        pytest.skip("short documents: the kHM tier is the long documents' (its 1600 pages suffice for all)")
     fx = gu.load(name)
     interner = gu.Interner()
     a = gu.encode_docs(fx, interner)

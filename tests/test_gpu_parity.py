@@ -23,7 +23,7 @@ def _gpu_batch(n_docs, **kw):
 def _gpu_outputs(mt, doc):
     rows, leaves = mt.get_segments(doc)
     return dict(text=mt.get_text(doc), length=mt.get_length(doc), leaves=leaves, segs=rows,
-                seg_props=[mt.get_segment_props(doc, i) for i in range(len(rows))],
+                seg_props=mt.get_all_segment_props(doc),
                 deltas=mt.get_delta_log(doc), status=int(mt.status()[doc]))
 
 
@@ -583,7 +583,7 @@ def test_gpu_full_streams_fast_path(oracle_lib, name):
         exp = dict(gu.expected(doc, interner), deltas=None)   # no delta log: its hash is checked above
         rows, leaves = mt.get_segments(i)
         got = dict(text=mt.get_text(i), length=mt.get_length(i), leaves=leaves, segs=rows,
-                   seg_props=[mt.get_segment_props(i, j) for j in range(len(rows))], deltas=None,
+                   seg_props=mt.get_all_segment_props(i), deltas=None,
                    status=int(mt.status()[i]))
         assert not gu.compare_oracle(got, exp), i
 
@@ -933,4 +933,4 @@ def test_gpu_hbm_page_metadata_matches_reference(case):
 def _gpu_outputs_nolog(mt, doc):
     rows, leaves = mt.get_segments(doc)
     return dict(text=mt.get_text(doc), length=mt.get_length(doc), leaves=leaves, segs=rows,
-                seg_props=[mt.get_segment_props(doc, i) for i in range(len(rows))], status=int(mt.status()[doc]))
+                seg_props=mt.get_all_segment_props(doc), status=int(mt.status()[doc]))

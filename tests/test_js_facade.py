@@ -290,6 +290,25 @@ def test_js_facade_live_client_matches_reference():
         assert g["deltas"] == d["out"]["deltas"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_live_xl", "ref_live_60k"])
+def test_js_facade_default_live_batch_is_unbounded(name):
+    """`new GpuMergeTreeBatch(n, {liveClient: 1})` with no capacity options (2048 segments,
+    32k text units, 1024 segment groups to start) replays participant streams far beyond them
+    -- 20k- and 60k-event live documents made by the reference, thousands of live segments and
+    pending groups -- equal to the reference: every local op, every regenerated op, the final
+    text and length.  The live growth step doubles what a document would outgrow, for the whole
+    batch, before the message that would (segmentGroups and the pending queue are unbounded in
+    the reference, MT/mergeTree.ts:1955-1962)."""
+    _addon()
+    fx = gu.load(name)
+    got = _node("live", os.path.join(gu.GOLDEN, name + ".json.gz"), "default", timeout=900)
+    for d, g in zip(fx["docs"], got["docs"]):
+        assert g["errs"] == [], g["errs"][:3]
+        assert g["text"] == d["out"]["text"]
+        assert g["length"] == d["out"]["length"]
+
+
 # ---------------------------------------------------------------- SharedSegmentSequence events
 def test_js_sequence_event_restatement_matches_reference_events():
     """tests/js/sequence_event.js (SequenceEvent.ranges over SortedSegmentSet, restated for the

@@ -55,11 +55,12 @@ def test_live_fixtures_are_reference_made():
 
 
 # ---------------------------------------------------------------- GPU
-def _run_doc(doc, log=True, lds=-1):
+def _run_doc(doc, log=True, lds=-1, caps=None):
     from fluidframework_amd.live import LiveClient
     interner = Interner(synthetic=True)
-    lc = LiveClient(doc["seed_text"], seg_capacity=16384, text_capacity=1 << 17,
-                    delta_log_capacity=(1 << 20) if log else 0, interner=interner, lds_seg_capacity=lds)
+    caps = caps or dict(seg_capacity=16384, text_capacity=1 << 17)
+    lc = LiveClient(doc["seed_text"], delta_log_capacity=(1 << 20) if log else 0, interner=interner,
+                    lds_seg_capacity=lds, **caps)
     lc.startOrUpdateCollaboration("local-0")
     unseq = []
     errs = []
@@ -92,20 +93,27 @@ def _run_doc(doc, log=True, lds=-1):
     return lc, interner, errs
 
 
+# grow: starting capacities far below the documents' (64 segments, 1024 text units, 16 segment
+# groups): the live growth step doubles them, round after round, mid-stream
+GROW_CAPS = dict(seg_capacity=64, text_capacity=1024, live_group_capacity=16)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds", [-1, 64, 192], ids=["hbm", "lds64", "lds192"])
-@pytest.mark.parametrize("name", LIVE_FIXTURES)
+@pytest.mark.parametrize("lds", [-1, 64, 192, "grow"], ids=["hbm", "lds64", "lds192", "grow"])
+@pytest.mark.parametrize("name", LIVE_FIXTURES + ["ref_live_60k"])
 def test_live_client_matches_reference(name, lds):
     """hbm: the flat HBM tier only; lds64 / lds192: each flush staged in LDS (TierLiveLdsT)
-    while the document fits 64 / 192 segments, continuing in the HBM tier beyond."""
+    while the document fits 64 / 192 segments, continuing in the HBM tier beyond; grow: the HBM
+    tier from capacities far below the documents' (the live growth step raises them: equal to
+    the reference all the same, every delta record included)."""
     fx = gu.load(name)
     bad = []
     for doc in fx["docs"]:
-        lc, interner, errs = _run_doc(doc, lds=lds)
+        lc, interner, errs = _run_doc(doc, lds=-1 if lds == "grow" else lds, caps=GROW_CAPS if lds == "grow" else None)
         mt = lc.mt
         rows, leaves = mt.get_segments(0)
         o = dict(text=mt.get_text(0), length=mt.get_length(0), leaves=leaves, segs=rows,
-                 seg_props=[mt.get_segment_props(0, i) for i in range(len(rows))],
+                 seg_props=mt.get_all_segment_props(0),
                  deltas=mt.get_delta_log(0), status=int(mt.status()[0]))
         errs += gu.compare_oracle(o, gu.expected_live(doc, interner))
         ls, ng = lc.pendingCounts()
@@ -138,7 +146,7 @@ def test_live_client_drained_matches_reference_and_observer():
         assert lc.getText() == exp["text"]
         assert list(leaves) == exp["leaves"]
         assert rows.tolist() == exp["segs"]
-        assert [lc.mt.get_segment_props(0, i) for i in range(len(rows))] == exp["seg_props"]
+        assert lc.mt.get_all_segment_props(0) == exp["seg_props"]
         obs = MergeTreeBatch(1, seg_capacity=16384, text_capacity=1 << 17, lds_seg_capacity=-1)
         b = Batch(Interner(synthetic=True))
         b.add_doc(doc["seed_text"], [_msg(e) for e in doc["events"] + doc["drain"] if e[0] == "M"])

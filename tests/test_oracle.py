@@ -232,7 +232,8 @@ def _replay_live_with_reconnects(oracle_lib, doc, interner):
     yield d, errs
 
 
-@pytest.mark.parametrize("name", ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep", "ref_live_xl"])
+@pytest.mark.parametrize("name", ["ref_live", "ref_live_long", "ref_live_markers", "ref_live_deep", "ref_live_xl",
+                                  "ref_live_60k"])
 def test_oracle_live_reconnects_match_reference(oracle_lib, name):
     """Every live fixture document, reconnects included: each regenerated op list equals the
     reference's, and the final state (text, length, leaves, segment table, property sets,
@@ -255,7 +256,7 @@ def test_oracle_live_reconnects_match_reference(oracle_lib, name):
             (exp["text"], exp["leaves"], exp["segs"], exp["seg_props"]), (name, doc["doc"])
 
 
-@pytest.mark.parametrize("name", ["ref_readouts", "ref_readouts_wide"])
+@pytest.mark.parametrize("name", ["ref_readouts", "ref_readouts_wide", "ref_readouts_xl"])
 def test_oracle_readouts_match_reference_in_every_view(oracle_lib, name):
     """MergeTree.getLength(refSeq, clientId), getContainingSegment and getPosition in every
     writer view of the collab window -- including the views below the writer's latest refSeq,
