@@ -147,8 +147,18 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     # the dominant class (longest kernel time) bounds the step: its roofline
     dom = max(per_class, key=lambda c: c["kernel_ms"])
     achieved = dom["alg_bytes"] / (dom["kernel_ms"] / 1000.0) if dom["kernel_ms"] > 0 else 0.0
+    # measured HBM traffic of the dominant class's replay (profiles/tools/collect_skew.sh: rocprofv3
+    # FETCH_SIZE / WRITE_SIZE passes over that class alone, 2 x FETCH_SIZE + WRITE_SIZE per step)
+    traffic = traffic_raw = None
+    try:
+        import json
+        pm = json.load(open(bench.PROFILE_PMC)).get("c3skew", {})
+        if pm.get("class") == dom["max_ops"] and pm.get("docs") == dom["docs"] and pm.get("ops") == dom["ops"]:
+            traffic, traffic_raw = pm.get("hbm_bytes_per_launch"), pm.get("hbm_bytes_per_launch_raw")
+    except (OSError, ValueError):
+        pass
     roofline = {"bound": "hbm", "achieved": round(achieved / 1e9, 3), "peak": bench.HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / bench.HBM_PEAK, "traffic": None,
+                "frac": achieved / bench.HBM_PEAK, "traffic": traffic, "traffic_raw": traffic_raw,
                 "kernel": f"k_replay_paged (class <= {dom['max_ops']} messages, its own stream)",
                 "kernel_ms": dom["kernel_ms"], "alg_bytes_per_launch": dom["alg_bytes"]}
     # oracle sample and CPU baseline (rank 0): per size class, a sample of >= 4 x threads

@@ -508,6 +508,13 @@ __global__ void __launch_bounds__(MT_WAVE) k_regen(DevState st, int doc, mt_rege
             }
             return;
         }
+        if (d.g_n - 1 + need_n > d.LG) {   // the new groups need more ids: the live growth step first
+            if (lane() == 0) {
+                io[0] = -5;
+                io[1] = d.g_n - 1 + need_n;
+            }
+            return;
+        }
     }
     d.g_head = g % d.LG + 1;   // dequeue first: the new groups may reuse its table slot
     d.g_n--;
@@ -3089,12 +3096,21 @@ int mt_regenerate_pending(mt_handle *h, uint32_t doc, mt_regen_rec *out, uint32_
               hipMalloc(&d_props, std::max<size_t>(props_cap, 1) * 4) == hipSuccess &&
               hipMalloc(&d_io, 16) == hipSuccess;
     int32_t io[4] = {0, 0, 0, 0};
-    if (ok) {
+    for (int round = 0; ok && round < 8; round++) {
         hipLaunchKernelGGL(k_regen, dim3(1), dim3(MT_WAVE), tier_lds_bytes(false, glb_caps(h), 0), h->stream, h->st,
                            (int)doc, d_out, (int)cap, d_text, (int)text_cap, d_props, (int)props_cap, d_io);
         ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(h->stream) == hipSuccess &&
              hipMemcpy(io, d_io, 16, hipMemcpyDeviceToHost) == hipSuccess;
-        if (ok && io[0] > 0)
+        if (!ok || io[0] != -5) break;
+        // more segment groups than the handle's ring holds (nothing changed yet): grow it
+        const int lg2 = std::min(65535, std::max(2 * h->st.LG, io[1]));
+        if (lg2 <= h->st.LG || live_regrow(h, h->st.S, h->st.B, h->st.H, h->st.T, h->st.P, lg2) != 0) {
+            io[0] = -2;
+            break;
+        }
+    }
+    if (ok) {
+        if (io[0] > 0)
             ok = hipMemcpy(out, d_out, (size_t)io[0] * sizeof(mt_regen_rec), hipMemcpyDeviceToHost) == hipSuccess &&
                  (io[1] == 0 || hipMemcpy(out_text, d_text, (size_t)io[1] * 2, hipMemcpyDeviceToHost) == hipSuccess) &&
                  (io[2] == 0 || hipMemcpy(out_props, d_props, (size_t)io[2] * 4, hipMemcpyDeviceToHost) == hipSuccess);

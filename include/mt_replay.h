@@ -43,7 +43,10 @@ typedef struct mt_batch mt_batch;
    text / property arenas, the uid map and the overflow overlap arena are starting points that
    the growth step raises per document (mt_last_grown), as the reference's documents grow
    without bound (MT/mergeTree.ts:2577-2585, MT/textSegment.ts:74-85).  page_capacity < 0
-   opts into a flat-only handle, whose capacities are hard (MT_DOC_CAPACITY beyond them). */
+   opts into a flat-only handle, whose capacities are hard (MT_DOC_CAPACITY beyond them) --
+   except on a live_client handle, where the live growth step (run by mt_sync) doubles the
+   flat capacities a document would outgrow (segments, blocks, heap, text, property records,
+   live_group_capacity) for the whole handle before that message. */
 typedef struct mt_options {
     int32_t device;          /* HIP device ordinal (one process per GPU) */
     int32_t seg_capacity;    /* leaf segments per document in the flat tiers (default 2048;
@@ -71,7 +74,10 @@ typedef struct mt_options {
     int32_t uid_capacity;       /* entries of a paged document's segment-id -> page map
                                    (default 65536; 8192 with the default page_capacity): ids
                                    are renumbered when they run out, and the growth step
-                                   raises it when live segments fill it */
+                                   raises it when live segments fill it.  (The renumbering
+                                   borrows the idle half of the text arena as 2 x pages int32
+                                   scratch: a text_capacity below twice the page count is
+                                   raised by the growth step first, cause 4.) */
     /* Tight paged tier (0 = off): LDS capacities below the three above.  Documents are
        replayed at these first (a smaller LDS footprint: more documents per CU); one that
        does not fit, or whose next message could outgrow them, continues -- from that
