@@ -705,7 +705,7 @@ def ingest_rates(mt, host, step_s, caps, device):
             "value_with_upload": round(n_ops / (step_s + t_up), 1)}
 
 
-def ingest_pipeline(caps, device, fx, blobs, threads, slice_docs=4096, n_slices=6):
+def ingest_pipeline(caps, device, fx, blobs, threads, slice_docs=3072, n_slices=8):
     """The C3 job from JSON message logs, overlapped (MergeTreeBatch.ingest_logs): the native
     encoder turns slice k + 1's logs into op records on the host's cores while slice k is
     uploaded and slice k - 1 replays on the GPU.  Slices of `slice_docs` C3 documents (the
