@@ -240,19 +240,25 @@ class MergeTreeBatch:
         encodes slice k + 1 (the native encoder, mt_opdec, its own threads inside) while this
         thread uploads slice k (mt_batch_upload) and enqueues its replay on the handle's
         stream, behind slice k - 1's (mt_batch_apply_async).  Arenas are reused from slice to
-        slice.  Returns the seconds each stage was busy: {"encode", "upload", "apply_wait",
-        "wall"} (apply_wait: time the caller's thread waited for the previous slice's replay)."""
+        slice, and so is the encoder (its buffers stay warm from call to call for the same
+        interner and thread count).  Returns the seconds each stage was busy: {"encode",
+        "upload", "apply_wait", "wall"} (apply_wait: time the caller's thread waited for the
+        previous slice's replay) and "encode_slices", each slice's encode seconds."""
         import queue
         import threading
         import time as _time
         from .opdec import MessageDecoder
-        dec = MessageDecoder(interner or Interner(synthetic=True), threads=threads)
+        interner = interner or getattr(self, "_ingest_interner", None) or Interner(synthetic=True)
+        self._ingest_interner = interner
+        dec = getattr(self, "_ingest_dec", None)
+        if dec is None or dec.interner is not interner or dec.threads != threads:
+            dec = self._ingest_dec = MessageDecoder(interner, threads=threads)
         q = queue.Queue(maxsize=1)                     # one encoded slice waiting for its upload
         free_sets = queue.Queue()
         for ps in getattr(self, "_ingest_arenas", None) or [{}, {}]:
             free_sets.put(ps)
         stop = threading.Event()
-        busy = {"encode": 0.0, "upload": 0.0, "apply_wait": 0.0}
+        busy = {"encode": 0.0, "upload": 0.0, "apply_wait": 0.0, "encode_slices": []}
 
         def produce():
             try:
@@ -280,7 +286,8 @@ class MergeTreeBatch:
                     off[d0 + 1: d0 + n + 1] = sub[1:]
                     off[d0 + n + 1:] = sub[-1]
                     out["doc_off"] = off
-                    busy["encode"] += _time.perf_counter() - t
+                    busy["encode_slices"].append(_time.perf_counter() - t)
+                    busy["encode"] += busy["encode_slices"][-1]
                     q.put((out, pset))
                 q.put(None)
             except BaseException as e:   # surfaces in the consumer
@@ -302,11 +309,17 @@ class MergeTreeBatch:
                 b = self.upload(out)   # (validation + copies: the arena set is free again after)
                 busy["upload"] += _time.perf_counter() - t
                 free_sets.put(pset)
+                if prev is not None:
+                    # before this slice's replay is queued: hipFree waits for the device to go
+                    # idle, and slice k - 1's replay has ended while slice k was encoded, so
+                    # nothing waits here (after the enqueue it would wait -- spinning a host
+                    # core the encoder needs -- for slice k's whole replay)
+                    t = _time.perf_counter()
+                    prev.free()
+                    busy["apply_wait"] += _time.perf_counter() - t
                 t = _time.perf_counter()
                 b.apply_async()        # (waits for the previous slice's replay and growth step)
                 busy["apply_wait"] += _time.perf_counter() - t
-                if prev is not None:
-                    prev.free()
                 prev = b
             self.sync()
         finally:

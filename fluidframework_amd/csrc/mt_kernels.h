@@ -481,8 +481,23 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 #ifndef MT_PAGED_WAVES
 #define MT_PAGED_WAVES 3
 #endif
+// The kHM tier (page metadata in HBM) is held to 7-10 documents per CU by its LDS footprint,
+// so at most 2-3 waves per SIMD run it anyway: compiled for 2 it keeps every value in its 256
+// VGPRs, where the 168 of 3 waves spill 120 of them to scratch (tools/regs.sh P_HM)
+// The last tiers at run-time capacities (full masks and table entries, kMayGrow: the hand-over
+// and growth launches) take 18-27 KB of LDS per document at their usual capacities, 8 or
+// fewer per CU, too: the same 2 waves (P_FULL spills 83 VGPRs at 3, P_BIG 177, none at 2)
+#ifndef MT_HM_WAVES
+#define MT_HM_WAVES 2
+#endif
+#ifndef MT_FULL_WAVES
+#define MT_FULL_WAVES 2
+#endif
+template <class T> constexpr int paged_waves() {
+    return T::kHM ? MT_HM_WAVES : (T::kMayGrow ? MT_FULL_WAVES : MT_PAGED_WAVES);
+}
 #if MT_PAGED_WAVES > 0
-#define MT_PAGED_WPE __attribute__((amdgpu_waves_per_eu(MT_PAGED_WAVES)))
+#define MT_PAGED_WPE __attribute__((amdgpu_waves_per_eu(paged_waves<T>())))
 #else
 #define MT_PAGED_WPE
 #endif
