@@ -649,7 +649,16 @@ def dispatch(args):
     raise SystemExit(f"bench.py: unknown --config {args.config}")
 
 
-def ingest_rates(mt, host, step_s, caps, device):
+def c3_logs():
+    """The reference's own C3 message logs (tests/golden/ref_c3_full): (fixture, JSON blobs)."""
+    import gzip
+    from fluidframework_amd.opdec import MessageDecoder
+    from fluidframework_amd.wire import compact_msgs_to_dicts
+    fx = json.load(gzip.open(os.path.join(REPO, "tests", "golden", "ref_c3_full.json.gz"), "rt"))
+    return fx, MessageDecoder.pack([compact_msgs_to_dicts(d["msgs"]) for d in fx["docs"]])
+
+
+def ingest_rates(mt, host, step_s, caps, device, pipeline=None):
     """What the timed region leaves out, reported beside it: the host encode of
     sequenced messages into op records (the reference's own C3 message logs, ref_c3_full,
     through wire.Batch -- the encoder encode.js mirrors) and the H2D upload of this step's op
@@ -698,7 +707,7 @@ def ingest_rates(mt, host, step_s, caps, device):
                                         f"-> op records + arenas by mt_opdec_decode + fetch (libmtsnapdec.so, equal to "
                                         f"wire.Batch: tests/test_snapdec.py), {t_nat:.2f} s"},
             "value_with_native_encode_and_upload_serial": round(n_ops / (step_s + t_up + n_ops / nat_rate), 1),
-            "pipeline": ingest_pipeline(caps, device, fx, blobs, threads),
+            "pipeline": pipeline or ingest_pipeline(caps, device, fx, blobs, threads),
             "h2d_upload": {"bytes": int(nbytes), "s": round(t_up, 3), "GB_per_s": round(nbytes / t_up / 1e9, 2),
                            "how": "mt_batch_upload of this step's op records, text and property arenas from pageable "
                                   "host memory (validation + hipMemcpy)"},
@@ -805,6 +814,15 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
         caps.update(lds_page_capacity=pp, lds_unsettled_capacity=ut, lds_page_heap_capacity=ph)
     if args.paged_slices and caps.get("page_capacity", 0) > 0:
         caps["paged_slices"] = args.paged_slices
+    # the overlapped ingest first, while the process holds nothing else: after the step it ran
+    # 7-10 % slower in its host encode (the line vs tools/ingest_probe.py, profiles/r6); rank 0
+    # only, like the CPU baseline (the host's cores are shared by the ranks)
+    pipeline = None
+    with_ingest = not args.no_ingest and rank == 0
+    if with_ingest:
+        fx, blobs = c3_logs()
+        pipeline = ingest_pipeline(caps, local_rank, fx, blobs, host_cores())
+        del fx, blobs
     t_gen = time.time()
     mt = MergeTreeBatch(docs, device=local_rank, **caps)
     batch = mt.generate(cfg, doc_base)          # untimed: inputs resident in HBM
@@ -887,7 +905,8 @@ def run_replay(args, cfg, rank, world, local_rank, dist):
     alg_bytes = n_ops * (OP_BYTES + RESULT_BYTES) + 2 * payload_chars + final_bytes
     k_ms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (k_ms / 1000.0)
-    ingest = None if args.no_ingest else ingest_rates(mt, host, ms_per_step / 1000.0, caps, local_rank)
+    ingest = None if not with_ingest else ingest_rates(mt, host, ms_per_step / 1000.0, caps, local_rank,
+                                                             pipeline)
     traffic = traffic_raw = None
     if os.path.exists(PROFILE_PMC):
         try:
