@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--seg-cap", type=int, default=0, help="flat HBM segments per document (0 = default; sweeps)")
     ap.add_argument("--skew-classes", default="",
                     help="c3skew: replay only these size classes (comma-separated bounds; diagnostics)")
+    ap.add_argument("--skew-priority", type=int, default=0,
+                    help="c3skew: the longest class's stream at the device's highest priority (1), the "
+                         "shortest classes' at its lowest (2: both), 0 none")
     ap.add_argument("--skew-serial", action="store_true",
                     help="c3skew: run the size classes one after another instead of concurrently")
     ap.add_argument("--heap-cap", type=int, default=0, help="zamboni heap entries per document (0 = default)")

@@ -81,6 +81,11 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
     runs = []
     for max_ops, idx in classes:        # longest class first
         mt = MergeTreeBatch(len(idx), device=local_rank, **class_caps(bench, cfg, max_ops))
+        prio = getattr(args, "skew_priority", 0)
+        if prio and not runs:
+            mt.set_stream_priority(1)       # the longest class: its waiting documents go first
+        elif prio >= 2 and max_ops <= 10000:
+            mt.set_stream_priority(-1)
         ccfg = dict(cfg, ops=int(max_ops))
         batch = mt.generate(ccfg, ops_per_doc=lens[idx], doc_ids=ids[idx])
         gsum = mt.checksums()

@@ -447,6 +447,10 @@ class MergeTreeBatch:
     def last_kernel_ms(self):
         return float(self.lib.mt_last_kernel_ms(self.h))
 
+    def set_stream_priority(self, priority):
+        """mt_set_stream_priority: > 0 the device's highest stream priority, < 0 its lowest."""
+        self._check(self.lib.mt_set_stream_priority(self.h, int(priority)), "mt_set_stream_priority")
+
     def last_load_ms(self):
         """Device time of the most recent snapshot load's kernels (mt_last_load_ms)."""
         return float(self.lib.mt_last_load_ms(self.h))

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("mt_batch_free", None, [_P]),
     ("mt_sync", _I, [_P]),
     ("mt_last_kernel_ms", ctypes.c_float, [_P]),
+    ("mt_set_stream_priority", ctypes.c_int, [_P, ctypes.c_int]),
     ("mt_last_load_ms", ctypes.c_float, [_P]),
     ("mt_last_hbm_docs", _I, [_P, _P]),
     ("mt_last_paged_peaks", _I, [_P, _P]),

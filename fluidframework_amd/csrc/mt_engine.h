@@ -106,12 +106,12 @@ template <bool kLogT> struct TierLiveLdsT {
 // kernel keeps none of them in registers (the bench's C3 tight tier, mt_replay.hip launch_paged).
 // kHMT: the page metadata (observer length, leaf-block counts, needsScour flags) stays in HBM
 // (mt_paged.h "page metadata accessors"): no LDS per page instead of 12 bytes, for documents
-// of thousands of pages (the skewed bench's long classes); replay only (no
-// delta log, no ordinals).
+// of thousands of pages (the skewed bench's long classes); with or without the delta log
+// (kLogT: P_HM_LOG, round 6), not with segment ordinals (their per-page characters follow the
+// LDS page metadata: mt_replay.hip use_hm).
 template <bool kLogT, bool kNarrowT = false, bool kBigT = false, bool kPackedT = false, int kPPT = 0, int kPHT = 0,
           int kUTT = 0, bool kHMT = false>
 struct TierPagedT {
-    static_assert(!(kHMT && kLogT), "HBM page metadata: replay tiers only");
     static constexpr int kPP = kPPT, kPH = kPHT, kUT = kUTT;
     static constexpr bool kHM = kHMT;
     static constexpr bool kBig = kBigT;

@@ -842,7 +842,7 @@ mt_handle *mt_create(uint32_t n_docs, const mt_options *opt) {
             return nullptr;
         }
         if (lb > 64 * 1024) {
-            const void *ks[] = {MTK(P_LOG), MTK(P_FULL), MTK(P_HM),
+            const void *ks[] = {MTK(P_LOG), MTK(P_FULL), MTK(P_HM), MTK(P_HM_LOG),
                                 MTK(GP_FULL),
                                 MTK(P_NARROW_LOG),
                                 MTK(P_NARROW),
@@ -1116,12 +1116,13 @@ __global__ void k_mark_big(DevState st, const int64_t *off, int resume_set) {
 // documents of the big region (the growth step's launches).
 // Documents of many pages replay with their page metadata in HBM (TierPagedT kHM: no LDS per
 // page instead of 12 bytes, so more of them share a CU); the bench's C3 / C4 documents (< 300
-// pages) keep it in LDS (no global load on their page searches).
+// pages) keep it in LDS (no global load on their page searches).  Delta-logging handles take
+// the kHM tier too (P_HM_LOG, P_BIG_HM_LOG); segment-ordinal handles keep the LDS metadata.
 #ifndef MT_HM_PAGES
 #define MT_HM_PAGES 512
 #endif
 static bool use_hm(const mt_handle *h, const PagedCaps &pc) {
-    return !pc.packed && !pc.narrow && !h->st.DL && pc.PP >= MT_HM_PAGES;
+    return !pc.packed && !pc.narrow && !h->ordinals && pc.PP >= MT_HM_PAGES;
 }
 static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, int res, const PagedSlice &sl,
                         bool big = false) {
@@ -1142,6 +1143,9 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     else if (pc.packed)
         launch_replay_paged(MTK(P_PACKED), g, blk, lb, h->stream, h->st,
                            b->ops, b->off, b->text, b->props, res, pc, sl);
+    else if (big && h->st.DL && hm)
+        launch_replay_paged(MTK(P_BIG_HM_LOG), g, blk, lb, h->stream, h->st, b->ops,
+                           b->off, b->text, b->props, res, pc, sl);
     else if (big && h->st.DL)
         launch_replay_paged(MTK(P_BIG_LOG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
@@ -1151,6 +1155,9 @@ static int launch_paged(mt_handle *h, const mt_batch *b, const PagedCaps &pc, in
     else if (big)
         launch_replay_paged(MTK(P_BIG), g, blk, lb, h->stream, h->st, b->ops,
                            b->off, b->text, b->props, res, pc, sl);
+    else if (h->st.DL && hm)
+        launch_replay_paged(MTK(P_HM_LOG), g, blk, lb, h->stream, h->st, b->ops, b->off, b->text,
+                           b->props, res, pc, sl);
     else if (h->st.DL && pc.narrow)
         launch_replay_paged(MTK(P_NARROW_LOG), g, blk, lb, h->stream, h->st, b->ops, b->off,
                            b->text, b->props, res, pc, sl);
@@ -1432,7 +1439,7 @@ static int regrow(mt_handle *h, const std::vector<uint32_t> &moving, const Paged
     h->big_caps = PagedCaps{c.PP, c.PH, c.UT, 0, 3, 0, 1};
     const size_t lb = paged_layout(c.PP, c.PH, c.UT, 0, 8).total;
     if (lb > 64 * 1024) {
-        const void *ks[] = {MTK(P_BIG_LOG),
+        const void *ks[] = {MTK(P_BIG_LOG), MTK(P_BIG_HM_LOG),
                             MTK(P_BIG), MTK(P_BIG_HM)};
         for (const void *k : ks) HIPCHK(h, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb));
     }
@@ -1789,6 +1796,25 @@ int mt_sync(mt_handle *h) {
 }
 
 float mt_last_kernel_ms(const mt_handle *h) { return h ? h->last_ms : 0.f; }
+
+// The handle's stream again, at a scheduling priority: > 0 the device's highest, < 0 its
+// lowest, 0 the default.  Handles sharing the GPU (the skewed bench's size classes, each on its
+// own stream) dispatch the high-priority stream's waiting workgroups first as CUs free up.
+int mt_set_stream_priority(mt_handle *h, int priority) {
+    if (!h) return MT_E_INVALID;
+    const int rc = mt_sync(h);
+    if (rc) return rc;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    int least = 0, greatest = 0;
+    HIPCHK(h, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s = nullptr;
+    HIPCHK(h, hipStreamCreateWithPriority(&s, hipStreamNonBlocking,
+                                          priority > 0 ? greatest : (priority < 0 ? least : 0)));
+    hipStreamDestroy(h->stream);
+    h->stream = s;
+    return 0;
+}
 
 int mt_last_hbm_docs(mt_handle *h, uint32_t *out) {
     if (!h || !out) return MT_E_INVALID;

@@ -27,6 +27,8 @@
     X(P_FULL, (k_replay_paged<TierPagedT<false>>))                                   \
     X(P_HM, (k_replay_paged<TierPagedT<false, false, false, false, 0, 0, 0, true>>)) \
     X(P_BIG_HM, (k_replay_paged<TierPagedT<false, false, true, false, 0, 0, 0, true>>)) \
+    X(P_HM_LOG, (k_replay_paged<TierPagedT<true, false, false, false, 0, 0, 0, true>>)) \
+    X(P_BIG_HM_LOG, (k_replay_paged<TierPagedT<true, false, true, false, 0, 0, 0, true>>)) \
     X(G_LDS, (k_generate<TierLdsT<false>>))                                          \
     X(G_GLB, (k_generate<TierGlbT<false>>))                                          \
     X(GP_NARROW, (k_generate_paged<TierPagedT<false, true>>))                        \

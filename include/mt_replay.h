@@ -223,6 +223,10 @@ void mt_batch_free(mt_batch *b);
 int mt_sync(mt_handle *h);
 /* Device time of the most recent replay kernel (HIP events on the handle's stream). */
 float mt_last_kernel_ms(const mt_handle *h);
+/* Recreates the handle's stream (after a sync) at a scheduling priority: > 0 the device's
+   highest, < 0 its lowest, 0 the default.  For handles that share one GPU (bench_skew.py's size
+   classes): the high-priority stream's waiting workgroups dispatch first as CUs free up. */
+int mt_set_stream_priority(mt_handle *h, int priority);
 /* Documents of the most recent batch that outgrew the LDS tier and were replayed from HBM:
    out[8] = {total, spilled before a message, segments, blocks, heap, text, property
    records, at load} (the causes count LDS capacities hit inside a message). */

@@ -788,7 +788,11 @@ def test_gpu_long_documents_match_reference(uid_capacity):
 
 
 # ---------------------------------------------------------------- rich callback stream
-@pytest.mark.parametrize("tier", list(TIERS))
+# (+ "hm": >= 512 pages, so the delta log runs on the kHM tier, P_HM_LOG)
+RICH_TIERS = dict(TIERS, hm=dict(TIERS["paged"], page_capacity=600))
+
+
+@pytest.mark.parametrize("tier", list(RICH_TIERS))
 def test_gpu_rich_callback_stream_matches_reference(tier):
     """delta_log_mode 1: every mergeTreeDeltaCallback with its segments' state (text or marker,
     properties after the op) and every mergeTreeMaintenanceCallback (SPLIT / APPEND / UNLINK
@@ -797,7 +801,7 @@ def test_gpu_rich_callback_stream_matches_reference(tier):
     fx = gu.load("ref_rich")
     interner = gu.Interner()
     a = gu.encode_docs(fx, interner)
-    mt = _gpu_batch(len(fx["docs"]), delta_log_mode=1, delta_log_capacity=1 << 20, **TIERS[tier])
+    mt = _gpu_batch(len(fx["docs"]), delta_log_mode=1, delta_log_capacity=1 << 20, **RICH_TIERS[tier])
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
     assert (mt.status() == 0).all()
@@ -808,7 +812,7 @@ def test_gpu_rich_callback_stream_matches_reference(tier):
                                                        got[bad] if bad is not None else None,
                                                        want[bad] if bad is not None else None)
     # the maintenance records are not part of the delta hash
-    plain = _gpu_batch(len(fx["docs"]), **TIERS[tier])
+    plain = _gpu_batch(len(fx["docs"]), **RICH_TIERS[tier])
     plain.load_initial_text(a["seed_off"], a["seed"])
     plain.apply_arrays(a)
     assert np.array_equal(plain.checksums(), mt.checksums())
@@ -853,7 +857,9 @@ def test_gpu_xl_documents_match_reference(name, caps):
     (bench_skew.class_caps: 1.6k / 3.2k pages, the two-level page search), at the uniform C3
     bench's (the tight tier hands them to the full tier, which hands them to the growth step
     as they pass 275 pages) and at the grow tier's (12 pages: growth round after round) --
-    text, leaf partition, segment table, property sets and every delta record equal."""
+    text, leaf partition, segment table, property sets and every delta record equal.  (At the
+    class capacities, >= 512 pages, the delta log runs on the kHM tier: P_HM_LOG, and
+    P_BIG_HM_LOG once growth passes 512 pages.)"""
     import json
     import os
     import bench
@@ -901,7 +907,8 @@ HM_CASES = {
 def test_gpu_hbm_page_metadata_matches_reference(case):
     """Documents of >= 512 pages without a delta log replay on the kHM tiers (mt_replay.hip
     use_hm: P_HM, P_BIG_HM), whose page metadata stays in HBM (LDS keeps one byte per page):
-    text, leaf partition, segment table and property sets equal the reference's."""
+    text, leaf partition, segment table and property sets equal the reference's.  (With a
+    delta log: test_gpu_xl_documents_match_reference, P_HM_LOG.)"""
     import json
     import os
     import bench
