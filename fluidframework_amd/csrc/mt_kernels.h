@@ -493,8 +493,15 @@ __device__ __forceinline__ void pg_peaks(const DevState &st, PagedDoc<T> &pd, in
 #ifndef MT_FULL_WAVES
 #define MT_FULL_WAVES 2
 #endif
+// The packed tiers (12-byte table entries) exist for tables that dominate a document's LDS:
+// C4's 39.7 KB runs 4 documents per CU, one wave per SIMD -- compiled for 3 it spilled 64
+// VGPRs (tools/regs.sh P_C4)
+#ifndef MT_PACKED_WAVES
+#define MT_PACKED_WAVES 2
+#endif
 template <class T> constexpr int paged_waves() {
-    return T::kHM ? MT_HM_WAVES : (T::kMayGrow ? MT_FULL_WAVES : MT_PAGED_WAVES);
+    return T::kHM ? MT_HM_WAVES
+                  : (T::kMayGrow ? MT_FULL_WAVES : (T::kPacked ? MT_PACKED_WAVES : MT_PAGED_WAVES));
 }
 #if MT_PAGED_WAVES > 0
 #define MT_PAGED_WPE __attribute__((amdgpu_waves_per_eu(paged_waves<T>())))
