@@ -79,10 +79,16 @@ struct TierCaps {
 //
 // WPG documents per workgroup, one per wave, each with its own LDS slice; the waves never
 // synchronise (more documents per CU than its workgroup limit of 16 would allow).
+// waves per SIMD the flat live tier (TierLiveT: its state in HBM, little LDS) is compiled for;
+// 1 = no constraint (the compiler's choice: 192 VGPRs, 2 waves)
+#ifndef MT_LIVE_WAVES
+#define MT_LIVE_WAVES 1
+#endif
+template <class T> constexpr int replay_waves() { return T::kLive && !T::kLds ? MT_LIVE_WAVES : 1; }
 template <class T, int WPG>
-__global__ void __launch_bounds__(MT_WAVE * WPG) k_replay(DevState st, const mt_op_rec *ops,
-                                                          const int64_t *off, const uint16_t *tin,
-                                                          const uint32_t *pin, TierCaps caps) {
+__global__ void __launch_bounds__(MT_WAVE * WPG) __attribute__((amdgpu_waves_per_eu(replay_waves<T>())))
+k_replay(DevState st, const mt_op_rec *ops, const int64_t *off, const uint16_t *tin, const uint32_t *pin,
+         TierCaps caps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     const LdsLayout L = lds_layout(T::kLds, caps.S, caps.B, caps.H, 0);
     // wave-uniform (SGPR) document index and LDS slice
