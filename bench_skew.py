@@ -168,7 +168,7 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
                 "frac": achieved / bench.HBM_PEAK, "traffic": traffic, "traffic_raw": traffic_raw,
                 "kernel": f"k_replay_paged (class <= {dom['max_ops']} messages, its own stream)",
                 "kernel_ms": dom["kernel_ms"], "alg_bytes_per_launch": dom["alg_bytes"]}
-    # oracle sample and CPU baseline (rank 0): per size class, a sample of >= 4 x threads
+    # oracle sample and CPU baseline (rank 0): per size class, a sample of >= 16 x threads
     # documents spread over the class's length distribution (its longest included), generated
     # by the CPU restatement on parallel host threads (its generator replays them: their
     # checksums are the check against the GPU's), then replayed again from their op records,
@@ -180,7 +180,7 @@ def run_skew(args, cfg, rank, world, local_rank, dist, bench):
         sys.path.insert(0, os.path.join(bench.REPO, "oracle"))
         import pyoracle
         threads = args.cpu_threads or bench.host_cores()
-        per = max(4 * threads, 8)
+        per = max(16 * threads, 32)
         picks = []   # (class, position in the class, document)
         for ri, r in enumerate(runs):
             srt = np.argsort(lens[r["idx"]], kind="stable")
