@@ -23,6 +23,28 @@ class DeltaLogOverflow(RuntimeError):
         self.records = records
 
 
+class PinnedArray:
+    """A page-locked host buffer (mt_host_alloc) and its numpy view (`a`); the buffer is freed
+    with this object, so keep it alive while the view is in use."""
+
+    def __init__(self, lib, n, dtype):
+        dt = np.dtype(dtype)
+        nbytes = max(int(n), 1) * dt.itemsize
+        self.lib = lib
+        self.p = lib.mt_host_alloc(nbytes)
+        if not self.p:
+            raise MemoryError(f"mt_host_alloc({nbytes}) failed")
+        self.a = np.frombuffer((ctypes.c_uint8 * nbytes).from_address(self.p), dtype=dt)
+
+    def __del__(self):
+        p, self.p = getattr(self, "p", None), None
+        if p:
+            try:
+                self.lib.mt_host_free(p)
+            except Exception:
+                pass
+
+
 class MergeTreeBatch:
     """N observer replicas (one per document) resident on one GPU.
 
@@ -233,7 +255,7 @@ class MergeTreeBatch:
                     s_.free()
         return catchup_all, clients_all
 
-    def ingest_logs(self, slices, interner=None, threads=8):
+    def ingest_logs(self, slices, interner=None, threads=8, pinned=True):
         """Sequenced message logs in, replayed documents out, as a pipeline (SEQ/sequence.ts:579-616
         feeds SharedSegmentSequence JSON messages): ``slices`` yields (d0, blobs) -- the JSON
         message arrays of documents [d0, d0 + len(blobs)), in document order.  A host thread
@@ -241,7 +263,8 @@ class MergeTreeBatch:
         thread uploads slice k (mt_batch_upload) and enqueues its replay on the handle's
         stream, behind slice k - 1's (mt_batch_apply_async).  Arenas are reused from slice to
         slice, and so is the encoder (its buffers stay warm from call to call for the same
-        interner and thread count).  Returns the seconds each stage was busy: {"encode",
+        interner and thread count); with `pinned` the arenas are page-locked (mt_host_alloc),
+        so the upload is a DMA that takes no host core from the encoder.  Returns the seconds each stage was busy: {"encode",
         "upload", "apply_wait", "wall"} (apply_wait: time the caller's thread waited for the
         previous slice's replay) and "encode_slices", each slice's encode seconds."""
         import queue
@@ -273,7 +296,12 @@ class MergeTreeBatch:
                         key = np.dtype(dt).str
                         a = pset.get(key)
                         if a is None or len(a) < m:
-                            a = np.empty(int(m * 1.25) + 64, dtype=dt)
+                            n = int(m * 1.25) + 64
+                            if pinned:
+                                pset["pin" + key] = PinnedArray(self.lib, n, dt)
+                                a = pset["pin" + key].a
+                            else:
+                                a = np.empty(n, dtype=dt)
                             pset[key] = a
                         return a[:m]
                     t = _time.perf_counter()

@@ -75,6 +75,8 @@ SIGNATURES = [
     ("mt_batch_apply_async", _I, [_P, _P]),
     ("mt_batch_num_ops", _U64, [_P]),
     ("mt_batch_free", None, [_P]),
+    ("mt_host_alloc", ctypes.c_void_p, [ctypes.c_uint64]),
+    ("mt_host_free", None, [ctypes.c_void_p]),
     ("mt_sync", _I, [_P]),
     ("mt_last_kernel_ms", ctypes.c_float, [_P]),
     ("mt_set_stream_priority", ctypes.c_int, [_P, ctypes.c_int]),

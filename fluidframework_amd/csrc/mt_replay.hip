@@ -1782,6 +1782,15 @@ void mt_batch_free(mt_batch *b) {
     delete b;
 }
 
+void *mt_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+void mt_host_free(void *p) {
+    if (p) hipHostFree(p);
+}
+
 int mt_sync(mt_handle *h) {
     if (!h) return MT_E_INVALID;
     const int rc = mt_settle(h);

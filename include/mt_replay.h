@@ -220,6 +220,11 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
 int mt_batch_apply_async(mt_handle *h, const mt_batch *b);   /* enqueue on the handle's stream */
 uint64_t mt_batch_num_ops(const mt_batch *b);
 void mt_batch_free(mt_batch *b);
+/* Page-locked host memory (hipHostMalloc) for the arenas a host encoder writes and
+   mt_batch_upload copies from: the copy is then a DMA, with no host-side staging copy on the
+   cores the encoder runs on.  NULL on failure; mt_host_free(NULL) is a no-op. */
+void *mt_host_alloc(uint64_t bytes);
+void mt_host_free(void *p);
 int mt_sync(mt_handle *h);
 /* Device time of the most recent replay kernel (HIP events on the handle's stream). */
 float mt_last_kernel_ms(const mt_handle *h);
