@@ -730,14 +730,18 @@ static bool props_rec_ok(const uint32_t *props, uint64_t props_len, uint32_t off
 // Host-side bounds check of a batch (MT_E_INVALID instead of a device fault): per-document
 // offsets monotonic inside [0, n_ops], every insert payload inside the text arena, every
 // props record inside the props arena, known op kinds.
+// (one pass over the records: also the largest |short client id| they name, for max_cli)
 static std::string validate_batch(uint32_t n_docs, const int64_t *off, const mt_op_rec *ops, uint64_t n_ops,
-                                  uint64_t text_len, const uint32_t *props, uint64_t props_len, bool live) {
+                                  uint64_t text_len, const uint32_t *props, uint64_t props_len, bool live,
+                                  int &max_cli) {
     if (off[0] < 0) return "doc_op_off[0] < 0";
     for (uint32_t d = 0; d < n_docs; d++)
         if (off[d + 1] < off[d]) return "doc_op_off not monotonic at document " + std::to_string(d);
     if ((uint64_t)off[n_docs] > n_ops) return "doc_op_off exceeds n_ops";
+    int mc = max_cli;
     for (uint64_t k = (uint64_t)off[0]; k < (uint64_t)off[n_docs]; k++) {
         const mt_op_rec &o = ops[k];
+        mc = std::max(mc, std::abs((int)(int16_t)o.client));
         if (o.kind > MT_OP_LOAD_ALIASED) return "op " + std::to_string(k) + ": unknown kind";
         if (o.kind >= MT_OP_LOAD_REMOVED && !(o.flags & MT_F_LOAD))
             return "op " + std::to_string(k) + ": summary-load record without MT_F_LOAD";
@@ -754,6 +758,7 @@ static std::string validate_batch(uint32_t n_docs, const int64_t *off, const mt_
         if ((o.kind == MT_OP_INSERT || o.kind == MT_OP_ANNOTATE) && !props_rec_ok(props, props_len, o.props))
             return "op " + std::to_string(k) + ": props record outside the props arena";
     }
+    max_cli = mc;
     return std::string();
 }
 static size_t tier_lds_bytes(bool seg_in_lds, const TierCaps &c, int gen_words) {
@@ -1071,12 +1076,13 @@ mt_batch *mt_batch_upload(mt_handle *h, const int64_t *doc_op_off, const mt_op_r
     // the kernels index ops, text and props straight from these values: reject anything
     // that would read outside the arrays (remote ops are trusted for their semantics, not
     // for memory safety)
-    std::string bad = validate_batch(h->n_docs, doc_op_off, ops, n_ops, text_len, props, props_len, h->live);
+    int max_cli = h->max_cli;
+    std::string bad = validate_batch(h->n_docs, doc_op_off, ops, n_ops, text_len, props, props_len, h->live, max_cli);
     if (!bad.empty()) {
         h->err = "mt_batch_upload: " + bad;
         return nullptr;
     }
-    for (uint64_t i = 0; i < n_ops; i++) h->max_cli = std::max(h->max_cli, std::abs((int)(int16_t)ops[i].client));
+    h->max_cli = max_cli;   // (over the records the documents replay)
     if (hipSetDevice(h->device) != hipSuccess) return nullptr;
     auto *b = new mt_batch();
     b->device = h->device;
