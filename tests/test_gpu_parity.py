@@ -770,16 +770,18 @@ def test_gpu_sliced_paged_schedule_matches_reference(lds_tier):
     assert all(sums[8][i].tobytes() == sums[8][i % 4].tobytes() for i in range(nd))
 
 
-@pytest.mark.parametrize("uid_capacity", [65536, 16384])
-def test_gpu_long_documents_match_reference(uid_capacity):
+@pytest.mark.parametrize("uid_capacity,text_capacity", [(65536, 1 << 17), (16384, 1 << 17), (16384, 4096)])
+def test_gpu_long_documents_match_reference(uid_capacity, text_capacity):
     """30k-message documents (~45k segment ids created, ~10.5k live segments at the end):
     segment ids are renumbered when the uid -> page map runs out (uid_capacity 16384 forces
-    it several times), and every output still equals the reference's."""
+    it several times), and every output still equals the reference's.  With a 4096-unit text
+    arena the renumbering's scratch (the arena's idle half, 2 x pages int32) and the text
+    itself both come from the growth step raising the arena (cause 4) as the document grows."""
     import bench
     fx = gu.load("ref_c3_long")
     interner = gu.interner_for(fx)
     a = gu.encode_docs(fx, interner)
-    caps = dict(bench.capacities(dict(fx["config"])), uid_capacity=uid_capacity, text_capacity=1 << 17)
+    caps = dict(bench.capacities(dict(fx["config"])), uid_capacity=uid_capacity, text_capacity=text_capacity)
     mt = _gpu_batch(len(fx["docs"]), delta_log_capacity=1 << 20, **caps)
     mt.load_initial_text(a["seed_off"], a["seed"])
     mt.apply_arrays(a)
